@@ -1,0 +1,288 @@
+#!/usr/bin/env python3
+"""bench.py -- rendered rays/s on KITTI-360-shaped frustums (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): one 192x640 frame per GPU,
+64 samples/ray (7,864,320 points), ViT-S/16-shaped 256x192x640 feature grid,
+ResnetFC 295->128->65 (random kaiming init), lindisp stratified sampling, bf16.
+A "step" = ImageRaySampler.sample (sd_gen_rays) -> sample_coarse (sd_sample_z) ->
+NCHW->NHWC grid pack (sd_pack_grid) -> fused field+composite (sd_render_fused) for
+one frame per GPU; for N>1 every rank renders its own frame (C3: frames sharded
+1-per-GPU) and the rendered maps (depth, DINO, RGB) are all-gathered over RCCL.
+The ViT/DPT encoder is not part of the timed step (separate scope row).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--precision bf16|fp32]
+N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+H, W, K_SAMPLES = 192, 640, 64
+C_GRID, HF, WF = 256, 192, 640
+KITTI_K = [[0.7849, 0.0, -0.0312], [0.0, 2.9391, 0.2701], [0.0, 0.0, 1.0]]
+PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}   # MI355X dense MFMA (MI355X_MICROARCH.md)
+D_HIDDEN, D_DINO = 128, 64
+D_IN = C_GRID + 39
+
+
+def mlp_flops_per_point(D=D_DINO):
+    return 2 * (D_IN * D_HIDDEN + D_HIDDEN * (1 + D))
+
+
+class FixedGridEncoder(torch.nn.Module):
+    def __init__(self, grid):
+        super().__init__()
+        self.register_buffer("grid", grid)
+        self.latent_size = grid.shape[1]
+        self.extra_outs = 0
+
+    def forward(self, x, ground_truth=False):
+        return [self.grid]
+
+
+def make_scene(frame_seed: int, device, precision="bf16", offset_pose=False):
+    """Synthetic inputs of SURVEY.md §8(d): image U[-1,1) (seed frame), grid N(0,1)
+    (seed 1+frame), MLP kaiming (seed 2)."""
+    from scenedino_amd.models import BTSNet
+    from scenedino_amd.models.prediction_heads import ResnetFC
+    from scenedino_amd.common.positional_encoding import PositionalEncoding
+    from scenedino_amd.renderer import NeRFRenderer
+    from scenedino_amd.common.ray_sampler import ImageRaySampler
+
+    g = torch.Generator().manual_seed(frame_seed)
+    images = (torch.rand(1, 1, 3, H, W, generator=g) * 2 - 1).to(device)
+    grid = torch.randn(1, C_GRID, HF, WF, generator=torch.Generator().manual_seed(1 + frame_seed))
+    torch.manual_seed(2)
+    head = ResnetFC(d_in=D_IN, d_out=1 + D_DINO, n_blocks=0, d_hidden=D_HIDDEN)
+    conf = {"predict_dino": True, "dino_dims": D_DINO, "learn_empty": False, "code_mode": "z",
+            "inv_z": True, "z_near": 3, "z_far": 80, "sample_color": True, "precision": precision}
+    net = BTSNet(conf, FixedGridEncoder(grid), PositionalEncoding(6, 3, 1.5, True),
+                 {"normal_head": head}, final_pred_head="normal_head").to(device).eval()
+    Ks = torch.tensor(KITTI_K, device=device).view(1, 1, 3, 3)
+    poses = torch.eye(4, device=device).view(1, 1, 4, 4)
+    net.encode(images, Ks, poses, ids_encoder=[0], ids_render=[0])
+    render_pose = poses.clone()
+    if offset_pose:  # 0.5 m lateral / 2 deg yaw render pose (SURVEY §8(d) second run)
+        import math
+        a = math.radians(2.0)
+        render_pose[0, 0, 0, 0] = math.cos(a); render_pose[0, 0, 0, 2] = math.sin(a)
+        render_pose[0, 0, 2, 0] = -math.sin(a); render_pose[0, 0, 2, 2] = math.cos(a)
+        render_pose[0, 0, 0, 3] = 0.5
+    renderer = NeRFRenderer(n_coarse=K_SAMPLES, lindisp=True, hard_alpha_cap=False,
+                            eval_batch_size=65536)
+    wrapper = renderer.bind_parallel(net, gpus=None).eval()
+    sampler = ImageRaySampler(z_near=3, z_far=80, height=H, width=W)
+    return net, renderer, wrapper, sampler, render_pose, Ks
+
+
+def render_step(net, wrapper, sampler, pose, Ks, timer=None):
+    net._grid_cache = None  # re-pack the (freshly encoded) feature grid every frame
+    rays, _ = sampler.sample(None, pose, Ks)
+    if timer is not None:
+        timer.start()
+    out = wrapper(rays, want_weights=False, want_alphas=False)
+    if timer is not None:
+        timer.stop()
+    return out
+
+
+class KernelTimer:
+    """HIP events around the fused render on the stream it is launched on."""
+
+    def __init__(self):
+        self.pairs = []
+        self.on = False
+
+    def start(self):
+        if self.on:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(torch.cuda.current_stream())
+            self.pairs.append([e, None])
+
+    def stop(self):
+        if self.on:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(torch.cuda.current_stream())
+            self.pairs[-1][1] = e
+
+    def mean_ms(self):
+        ts = [a.elapsed_time(b) for a, b in self.pairs]
+        return sum(ts) / max(len(ts), 1)
+
+
+def cpu_baseline(budget_s: float = 20.0):
+    """Oracle (pure-PyTorch CPU restatement of the reference, fp32) on the host cores:
+    renders whole image rows of the same C2 frame until ~budget_s of CPU work."""
+    from oracle import render_oracle as O
+
+    threads = int(os.environ.get("SD_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    torch.set_num_threads(threads)
+    g = torch.Generator().manual_seed(0)
+    images = torch.rand(1, 1, 3, H, W, generator=g) * 2 - 1
+    grid = torch.randn(1, C_GRID, HF, WF, generator=torch.Generator().manual_seed(1))
+    torch.manual_seed(2)
+    from scenedino_amd.models.prediction_heads import ResnetFC
+    head = ResnetFC(d_in=D_IN, d_out=1 + D_DINO, n_blocks=0, d_hidden=D_HIDDEN)
+    Kn = torch.tensor(KITTI_K)
+    pose = torch.eye(4)
+    rays = O.gen_rays(pose.view(1, 4, 4), Kn.view(1, 3, 3), H, W)
+    w2c = torch.inverse(pose).view(1, 4, 4)
+    imgs = (images * 0.5 + 0.5)
+    args = (grid, w2c, Kn.view(1, 3, 3), imgs, w2c.view(1, 1, 4, 4), Kn.view(1, 1, 3, 3),
+            head.lin_in.weight.detach(), head.lin_in.bias.detach(), head.lin_out.weight.detach(),
+            head.lin_out.bias.detach())
+    rows_per_chunk = 4
+    done_rays = 0
+    # warm-up on one chunk
+    u = torch.rand(rows_per_chunk * W, K_SAMPLES, generator=torch.Generator().manual_seed(3))
+    with torch.no_grad():
+        O.render(rays[: rows_per_chunk * W], u, *args, sb=1)
+        t0 = time.perf_counter()
+        row = 0
+        while row < H and time.perf_counter() - t0 < budget_s:
+            sl = slice(row * W, (row + rows_per_chunk) * W)
+            O.render(rays[sl], u, *args, sb=1)
+            done_rays += rows_per_chunk * W
+            row += rows_per_chunk
+        dt = time.perf_counter() - t0
+    cpu = platform.processor() or platform.machine()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": done_rays / dt, "unit": "rays/s", "cores": threads, "kind": "port",
+            "sample": f"{done_rays} rays ({row} of {H} rows) of the same 192x640x64 frame, "
+                      f"fp32 torch-CPU oracle restatement, {dt:.1f} s on {threads} threads "
+                      f"({cpu}); encoder excluded"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--offset-pose", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+        torch.cuda.set_device(local_rank)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    device = torch.device("cuda", local_rank)
+
+    from scenedino_amd import _lib
+    _lib.load()
+    net, renderer, wrapper, sampler, pose, Ks = make_scene(rank, device, args.precision,
+                                                          args.offset_pose)
+    R = H * W
+    gather_bufs = None
+    if dist:
+        import torch.distributed as tdist
+        maps = torch.empty(R, 1 + D_DINO + 3, device=device)
+        gather_bufs = [torch.empty_like(maps) for _ in range(world)]
+
+    timer = KernelTimer()
+
+    def step():
+        out = render_step(net, wrapper, sampler, pose, Ks, timer)
+        if dist:
+            c = out["coarse"]
+            maps = torch.cat((c["depth"].reshape(R, 1), c["dino_features"].reshape(R, D_DINO),
+                              c["rgb"].reshape(R, 3)), 1)
+            tdist.all_gather(gather_bufs, maps)
+        return out
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    timer.on = True
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = timer.mean_ms()
+    if dist:
+        t = torch.tensor([elapsed, kern_ms], device=device, dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+
+    if rank == 0:
+        total_rays = world * R * args.steps
+        ms_per_step = 1e3 * elapsed / args.steps
+        flops = R * K_SAMPLES * mlp_flops_per_point()
+        achieved = flops / (kern_ms * 1e-3) / 1e12
+        peak = PEAK_TFLOPS[args.precision]
+        line = {
+            "metric": "rendered rays/sec, KITTI-360 192x640x64-sample frustum",
+            "value": total_rays / elapsed,
+            "unit": "rays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "ms_per_frame": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.precision,
+            "data": "synthetic (seeded U[-1,1) image, N(0,1) 256x192x640 feature grid, "
+                    "kaiming-init ResnetFC; no dataset/checkpoint offline)",
+            "config": {
+                "workload": "C2: KITTI-360 192x640 frustum, 64 samples/ray, ViT-S/16-shaped "
+                            "256x192x640 DPT feature grid, ResnetFC 295-128-65, lindisp"
+                            + (", offset render pose" if args.offset_pose else ""),
+                "frames_per_gpu": 1, "rays_per_frame": R, "samples_per_ray": K_SAMPLES,
+                "grid": [C_GRID, HF, WF], "parallelism": f"frames{world}" +
+                ("+rccl_allgather" if world > 1 else ""),
+            },
+            "roofline": {
+                "kernel": "k_render (sd_render_fused)",
+                "bound": "mfma",
+                "achieved": achieved,
+                "peak": peak,
+                "unit": "TFLOP/s",
+                "frac": achieved / peak,
+                "traffic": None,
+                "kernel_ms": kern_ms,
+                "algorithmic_flops_per_launch": flops,
+            },
+        }
+        if not args.no_cpu_baseline and world == 1:
+            line["cpu_baseline"] = cpu_baseline(args.cpu_budget)
+        print(json.dumps(line), flush=True)
+    if dist:
+        tdist.barrier()
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,141 @@
+/*
+ * sdhip.h -- C ABI of the MI355X (gfx950) SceneDINO render hot path.
+ *
+ * libsdhip.so is a plain C-ABI shared library: raw device pointers, sizes and a
+ * hipStream_t (passed as void*), int status returns (0 = ok, <0 = error; text via
+ * sd_last_error()).  No torch types cross the boundary.  The caller owns and
+ * allocates every buffer; launches are asynchronous on the given stream; the
+ * library keeps no mutable global state beyond the per-thread error string.
+ *
+ * The reference (tum-vision/scenedino) is pure Python/PyTorch: its boundary for
+ * this path is the Python plugin API (scenedino.renderer.NeRFRenderer,
+ * scenedino.models.BTSNet, scenedino.common.ray_sampler.ImageRaySampler).  Each
+ * entry point below replaces the reference computation cited next to it; the
+ * Python mirror in scenedino_amd/ binds them with ctypes.
+ *
+ * Layouts (all row-major, float32 unless stated):
+ *   rays        (R, ray_dim>=8)  [o(3), d(3), near, far, (frame_id, x, y)]
+ *   z           (R, K)
+ *   camera rec  21 floats: w2c rows 0..2 (12 floats, 3x4) then K (9 floats, 3x3)
+ *   grid        (B, Hf, Wf, C) NHWC, element type bf16 (dtype=SD_BF16) or f32
+ *   colour img  (B, nv, Hc, Wc, 4) NHWC4 float32 (rgb + pad)
+ */
+#ifndef SDHIP_H
+#define SDHIP_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum sd_dtype { SD_F32 = 0, SD_BF16 = 1 };
+
+/* Last error text of the calling thread ("" if none). */
+const char *sd_last_error(void);
+
+/* Library / ABI version (bumped on any signature change). */
+int sd_abi_version(void);
+
+/* Frustum ray generation, bit-exact with the reference's fp32 arithmetic.
+ * Replaces util.unproj_map + util.gen_rays + ImageRaySampler.sample
+ *   (scenedino/common/util.py:113-158, util.py:253-285,
+ *    scenedino/common/ray_sampler.py:439-513).
+ * poses_c2w (n_views,4,4), Ks (n_views,3,3) normalised intrinsics,
+ * frame_ids (n_views); rays_out (n_views, H, W, 11). */
+int sd_gen_rays(const float *poses_c2w, const float *Ks, const float *frame_ids,
+                int64_t n_views, int64_t H, int64_t W, float z_near, float z_far,
+                float *rays_out, void *stream);
+
+/* Stratified inverse-depth (lindisp) or linear z sampling.
+ * Replaces NeRFRenderer.sample_coarse (scenedino/renderer/nerf.py:121-141).
+ * u == NULL: jitter drawn from a counter-based RNG keyed by (seed, offset);
+ * u != NULL: jitter read from u (R, K) -> bit-exact with the reference. */
+int sd_sample_z(const float *rays, int64_t R, int64_t ray_dim, int64_t K, int lindisp,
+                const float *u, uint64_t seed, uint64_t offset, float *z_out, void *stream);
+
+/* NCHW float32 feature grid (B,C,H,W) -> NHWC (B,H,W,C) in dtype.
+ * Layout step for F.grid_sample over BTSNet.grid_f_features (bts.py:299-309). */
+int sd_pack_grid(const float *grid_nchw, int64_t B, int64_t C, int64_t H, int64_t W,
+                 int dtype, void *out_nhwc, void *stream);
+
+/* NCHW colour images (B*nv, 3, H, W) -> NHWC4 float32 (B*nv, H, W, 4).
+ * Layout step for BTSNet.sample_colors' F.grid_sample (bts.py:348-358). */
+int sd_pack_image(const float *img_nchw, int64_t N, int64_t H, int64_t W, float *out_nhwc4,
+                  void *stream);
+
+/* Per-point MLP parameters, pre-packed (by the host) into MFMA fragment order.
+ * ResnetFC(n_blocks=0): out = W_out relu(W_in x + b_in) + b_out
+ *   (scenedino/models/prediction_heads/resnetfc.py:135-203). */
+typedef struct sd_mlp {
+    const void *w_in;      /* [C/16+3][4][64][8] of dtype (layer-1 A fragments)          */
+    const float *b_in_h;   /* [4][2][16] hidden bias, accumulator-row order                */
+    const float *w_sig_h;  /* [4][2][16] W_out row 0 (sigma), accumulator-row order        */
+    float b_sigma;         /* b_out[0]                                                     */
+    const void *w_out;     /* layer-2 A fragments for the D dino rows (dtype-specific)     */
+    const float *b_dino;   /* b_out[1:1+D]                                                 */
+    int32_t C;             /* grid channels (multiple of 16)                               */
+    int32_t D;             /* dino dims (multiple of 32)                                   */
+    int32_t dtype;         /* SD_BF16: bf16 MFMA + bf16 grid; SD_F32: f32 MFMA + f32 grid  */
+    int32_t d_hidden;      /* must be 128                                                  */
+} sd_mlp;
+
+/* Fused coarse render of R rays x K samples: point generation, projection into the
+ * encoder view, positional code, bilinear feature gather, MFMA MLP, softplus,
+ * colour sampling in nv render views, alpha compositing (sequential
+ * transmittance per ray) of depth / DINO features / colour.
+ * Replaces NeRFRenderer.composite + BTSNet.forward + sample_features + sample_colors
+ *   (nerf.py:230-449, bts.py:271-441, bts.py:476-595).
+ * Optional per-sample outputs may be NULL. */
+typedef struct sd_render_args {
+    const float *rays; int64_t ray_dim; int64_t R; int64_t rays_per_sb; int32_t K;
+    const float *z;                       /* (R, K)                                */
+    const void *grid; int32_t Hf, Wf;     /* (B, Hf, Wf, C) NHWC                   */
+    const float *cam_f;                   /* (B, 21)                               */
+    const float *img; int32_t nv, Hc, Wc; /* (B, nv, Hc, Wc, 4) or NULL if nv==0   */
+    const float *cam_c;                   /* (B, nv, 21)                           */
+    int32_t hard_alpha_cap;
+    /* required outputs */
+    float *depth;      /* (R)        */
+    float *dino;       /* (R, D)     */
+    float *rgb;        /* (R, 3 nv)  */
+    /* optional outputs (NULL = not wanted) */
+    float *weights;    /* (R, K)         */
+    float *alphas;     /* (R, K)         */
+    float *invalid;    /* (R, K, nv)     */
+    uint8_t *invalid_f;/* (R, K)         */
+    float *rgb_samps;  /* (R, K, 3 nv)   */
+} sd_render_args;
+
+int sd_render_fused(const sd_render_args *args, const sd_mlp *mlp, void *stream);
+
+/* Per-point field query without compositing (BTSNet.forward on raw points,
+ * bts.py:476-595; SSCBench predict_grid / demo inference_3d).  Points are
+ * (B, P, 3); outputs sigma (B,P), dino (B,P,D); colour outputs optional. */
+typedef struct sd_field_args {
+    const float *xyz; int64_t B; int64_t P;
+    const void *grid; int32_t Hf, Wf;
+    const float *cam_f;                   /* (B, 21)            */
+    const float *img; int32_t nv, Hc, Wc; /* may be NULL / nv=0 */
+    const float *cam_c;                   /* (B, nv, 21)        */
+    float *sigma;      /* (B, P)             */
+    float *dino;       /* (B, P, D)          */
+    float *rgb;        /* (B, P, 3 nv) or NULL */
+    float *invalid;    /* (B, P, nv) or NULL   */
+    uint8_t *invalid_f;/* (B, P) or NULL       */
+} sd_field_args;
+
+int sd_field_query(const sd_field_args *args, const sd_mlp *mlp, void *stream);
+
+/* Standalone alpha compositing for an arbitrary (non-fused) field model.
+ * Replaces nerf.py:343-405.  sigma,z (R,K); feat (R,K,F) optional, rgb (R,K,Cc). */
+int sd_composite(const float *z, const float *sigma, const float *feat, int64_t F,
+                 const float *rgb, int64_t Cc, int64_t R, int32_t K, int32_t hard_alpha_cap,
+                 float *weights, float *alphas, float *depth, float *feat_out, float *rgb_out,
+                 void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SDHIP_H */

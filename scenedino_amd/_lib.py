@@ -1,0 +1,200 @@
+"""ctypes binding of libsdhip.so (the C ABI declared in include/sdhip.h).
+
+The product path has no fallback: if the shared library is missing or a call
+fails, this module raises.  Only raw device pointers, sizes and the current HIP
+stream cross the boundary.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsdhip.so")
+ABI_VERSION = 1
+
+SD_F32 = 0
+SD_BF16 = 1
+
+_vp = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_i32 = ctypes.c_int32
+
+
+class SdMlp(ctypes.Structure):
+    _fields_ = [
+        ("w_in", _vp), ("b_in_h", _vp), ("w_sig_h", _vp), ("b_sigma", ctypes.c_float),
+        ("w_out", _vp), ("b_dino", _vp),
+        ("C", _i32), ("D", _i32), ("dtype", _i32), ("d_hidden", _i32),
+    ]
+
+
+class SdRenderArgs(ctypes.Structure):
+    _fields_ = [
+        ("rays", _vp), ("ray_dim", _i64), ("R", _i64), ("rays_per_sb", _i64), ("K", _i32),
+        ("z", _vp),
+        ("grid", _vp), ("Hf", _i32), ("Wf", _i32),
+        ("cam_f", _vp),
+        ("img", _vp), ("nv", _i32), ("Hc", _i32), ("Wc", _i32),
+        ("cam_c", _vp),
+        ("hard_alpha_cap", _i32),
+        ("depth", _vp), ("dino", _vp), ("rgb", _vp),
+        ("weights", _vp), ("alphas", _vp), ("invalid", _vp), ("invalid_f", _vp),
+        ("rgb_samps", _vp),
+    ]
+
+
+class SdFieldArgs(ctypes.Structure):
+    _fields_ = [
+        ("xyz", _vp), ("B", _i64), ("P", _i64),
+        ("grid", _vp), ("Hf", _i32), ("Wf", _i32),
+        ("cam_f", _vp),
+        ("img", _vp), ("nv", _i32), ("Hc", _i32), ("Wc", _i32),
+        ("cam_c", _vp),
+        ("sigma", _vp), ("dino", _vp), ("rgb", _vp), ("invalid", _vp), ("invalid_f", _vp),
+    ]
+
+
+# (name, argtypes) of every exported entry point; tests check the .so exports all.
+SIGNATURES = {
+    "sd_last_error": [],
+    "sd_abi_version": [],
+    "sd_gen_rays": [_vp, _vp, _vp, _i64, _i64, _i64, ctypes.c_float, ctypes.c_float, _vp, _vp],
+    "sd_sample_z": [_vp, _i64, _i64, _i64, ctypes.c_int, _vp, ctypes.c_uint64, ctypes.c_uint64,
+                    _vp, _vp],
+    "sd_pack_grid": [_vp, _i64, _i64, _i64, _i64, ctypes.c_int, _vp, _vp],
+    "sd_pack_image": [_vp, _i64, _i64, _i64, _vp, _vp],
+    "sd_render_fused": [ctypes.POINTER(SdRenderArgs), ctypes.POINTER(SdMlp), _vp],
+    "sd_field_query": [ctypes.POINTER(SdFieldArgs), ctypes.POINTER(SdMlp), _vp],
+    "sd_composite": [_vp, _vp, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp,
+                     _vp],
+}
+
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    """Load libsdhip.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"scenedino_amd: HIP library {path} is missing. Build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950).")
+    lib = ctypes.CDLL(path)
+    for name, argt in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argt
+        fn.restype = ctypes.c_int
+    lib.sd_last_error.restype = ctypes.c_char_p
+    if lib.sd_abi_version() != ABI_VERSION:
+        raise RuntimeError("scenedino_amd: libsdhip.so ABI version mismatch; rebuild it")
+    _lib = lib
+    return lib
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        msg = _lib.sd_last_error().decode(errors="replace") if _lib else ""
+        raise RuntimeError(f"scenedino_amd: {what} failed (rc={rc}): {msg}")
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_of(t: torch.Tensor):
+    if t.device.type != "cuda":
+        raise RuntimeError("scenedino_amd: HIP kernels need tensors on a ROCm (cuda) device; "
+                           f"got {t.device}")
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _req(t: torch.Tensor, name: str, dtype=torch.float32):
+    if t.dtype != dtype:
+        raise TypeError(f"scenedino_amd: {name} must be {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"scenedino_amd: {name} must be contiguous")
+    return t
+
+
+# ---------------------------------------------------------------------------
+# thin wrappers (torch tensors in, torch tensors out; all on the same device)
+# ---------------------------------------------------------------------------
+def gen_rays(poses_c2w, Ks, frame_ids, H, W, z_near, z_far):
+    lib = load()
+    v = poses_c2w.shape[0]
+    out = torch.empty(v, H, W, 11, device=poses_c2w.device, dtype=torch.float32)
+    _check(lib.sd_gen_rays(ptr(_req(poses_c2w, "poses")), ptr(_req(Ks, "Ks")),
+                           ptr(_req(frame_ids, "frame_ids")), v, H, W, float(z_near),
+                           float(z_far), ptr(out), stream_of(out)), "sd_gen_rays")
+    return out
+
+
+def sample_z(rays, K, lindisp, u=None, seed=0, offset=0, out=None):
+    lib = load()
+    R, rd = rays.shape
+    z = out if out is not None else torch.empty(R, K, device=rays.device, dtype=torch.float32)
+    if u is not None:
+        _req(u, "u")
+        if tuple(u.shape) != (R, K):
+            raise ValueError(f"jitter u must be ({R},{K}), got {tuple(u.shape)}")
+    _check(lib.sd_sample_z(ptr(_req(rays, "rays")), R, rd, K, int(bool(lindisp)), ptr(u),
+                           ctypes.c_uint64(seed & (2**64 - 1)),
+                           ctypes.c_uint64(offset & (2**64 - 1)), ptr(z), stream_of(z)),
+           "sd_sample_z")
+    return z
+
+
+def pack_grid(grid_nchw, dtype):
+    lib = load()
+    B, C, H, W = grid_nchw.shape
+    tdt = torch.bfloat16 if dtype == SD_BF16 else torch.float32
+    out = torch.empty(B, H, W, C, device=grid_nchw.device, dtype=tdt)
+    _check(lib.sd_pack_grid(ptr(_req(grid_nchw, "grid")), B, C, H, W, dtype, ptr(out),
+                            stream_of(out)), "sd_pack_grid")
+    return out
+
+
+def pack_image(img_nchw):
+    lib = load()
+    N, c3, H, W = img_nchw.shape
+    assert c3 == 3, "colour images must have 3 channels"
+    out = torch.empty(N, H, W, 4, device=img_nchw.device, dtype=torch.float32)
+    _check(lib.sd_pack_image(ptr(_req(img_nchw, "images")), N, H, W, ptr(out), stream_of(out)),
+           "sd_pack_image")
+    return out
+
+
+def render_fused(args: SdRenderArgs, mlp: SdMlp, ref_tensor):
+    lib = load()
+    _check(lib.sd_render_fused(ctypes.byref(args), ctypes.byref(mlp), stream_of(ref_tensor)),
+           "sd_render_fused")
+
+
+def field_query(args: SdFieldArgs, mlp: SdMlp, ref_tensor):
+    lib = load()
+    _check(lib.sd_field_query(ctypes.byref(args), ctypes.byref(mlp), stream_of(ref_tensor)),
+           "sd_field_query")
+
+
+def composite(z, sigma, feat, rgb, hard_alpha_cap, want_weights=True):
+    lib = load()
+    R, K = z.shape
+    dev = z.device
+    F = feat.shape[-1] if feat is not None else 0
+    Cc = rgb.shape[-1] if rgb is not None else 0
+    weights = torch.empty(R, K, device=dev)
+    alphas = torch.empty(R, K, device=dev)
+    depth = torch.empty(R, device=dev)
+    feat_out = torch.empty(R, F, device=dev) if feat is not None else None
+    rgb_out = torch.empty(R, Cc, device=dev) if rgb is not None else None
+    _check(lib.sd_composite(ptr(_req(z, "z")), ptr(_req(sigma, "sigma")),
+                            ptr(feat if feat is None else _req(feat, "feat")), F,
+                            ptr(rgb if rgb is None else _req(rgb, "rgb")), Cc, R, K,
+                            int(bool(hard_alpha_cap)), ptr(weights), ptr(alphas), ptr(depth),
+                            ptr(feat_out), ptr(rgb_out), stream_of(depth)), "sd_composite")
+    return weights, alphas, depth, feat_out, rgb_out

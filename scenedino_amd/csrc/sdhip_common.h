@@ -1,0 +1,88 @@
+// sdhip_common.h -- shared device helpers for the gfx950 SceneDINO kernels.
+// Compiled with -ffp-contract=off: every fused multiply-add is an explicit fmaf()
+// so that the bit-exact kernels (ray generation, z sampling) reproduce the
+// reference's separately rounded fp32 arithmetic.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/sdhip.h"
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+#define SD_WAVE 64
+#define SD_DH 128          // ResnetFC d_hidden (configs/model/dino_downsampler.yaml:39)
+#define SD_PE_CHUNKS 3     // 39 positional-code features padded to 48 = 3 x 16
+#define SD_EPS 1e-3f       // scenedino/common/cameras/pinhole.py:3
+#define SD_MAX_NV 4        // colour (render) views handled by the fused kernels
+
+// torch.linspace(start, end, n)[i] in fp32 (identical on CPU and CUDA builds of
+// torch; verified against the reference's rays bit for bit, tests/golden).
+__device__ __forceinline__ float sd_linspace_at(float start, float end, int64_t n, int64_t i) {
+    if (n == 1) return start;
+    float step = (end - start) / (float)(n - 1);
+    int64_t half = n / 2;
+    if (i < half) return fmaf(step, (float)i, start);
+    return fmaf(-step, (float)(n - 1 - i), end);
+}
+
+__device__ __forceinline__ float bf16lo(uint32_t d) { return __uint_as_float(d << 16); }
+__device__ __forceinline__ float bf16hi(uint32_t d) { return __uint_as_float(d & 0xffff0000u); }
+
+// Camera record: w2c rows 0..2 (3x4) then normalised K (3x3).
+// pts_into_camera (pinhole.py:40-59) followed by project_to_image (pinhole.py:62-84).
+__device__ __forceinline__ void sd_project(const float *__restrict__ cam, float px, float py,
+                                           float pz, float &x, float &y, float &zc) {
+    float c0 = ((cam[0] * px + cam[1] * py) + cam[2] * pz) + cam[3];
+    float c1 = ((cam[4] * px + cam[5] * py) + cam[6] * pz) + cam[7];
+    float c2 = ((cam[8] * px + cam[9] * py) + cam[10] * pz) + cam[11];
+    const float *K = cam + 12;
+    float i0 = (K[0] * c0 + K[1] * c1) + K[2] * c2;
+    float i1 = (K[3] * c0 + K[4] * c1) + K[5] * c2;
+    float i2 = (K[6] * c0 + K[7] * c1) + K[8] * c2;
+    float zd = fmaxf(i2, SD_EPS);
+    x = i0 / zd;
+    y = i1 / zd;
+    zc = i2;
+}
+
+// outside_frustum (pinhole.py:87-112)
+__device__ __forceinline__ bool sd_outside(float x, float y, float zc) {
+    return (zc <= SD_EPS) | (x < -1.f) | (x > 1.f) | (y < -1.f) | (y > 1.f);
+}
+
+// Bilinear tap setup of F.grid_sample(mode=bilinear, padding_mode=border,
+// align_corners=False) for normalised coords (x, y) on an (h, w) image.
+struct Taps {
+    int i00, i01, i10, i11;   // pixel indices (row-major y*w + x) of nw, ne, sw, se
+    float w00, w01, w10, w11; // bilinear weights
+};
+
+__device__ __forceinline__ Taps sd_taps(float x, float y, int w, int h) {
+    float ix = ((x + 1.f) * (float)w - 1.f) / 2.f;
+    float iy = ((y + 1.f) * (float)h - 1.f) / 2.f;
+    ix = fminf((float)(w - 1), fmaxf(ix, 0.f));
+    iy = fminf((float)(h - 1), fmaxf(iy, 0.f));
+    float fx0 = floorf(ix), fy0 = floorf(iy);
+    int x0 = (int)fx0, y0 = (int)fy0;
+    x0 = min(max(x0, 0), w - 1);
+    y0 = min(max(y0, 0), h - 1);
+    int x1 = min(x0 + 1, w - 1), y1 = min(y0 + 1, h - 1);
+    float ex = (fx0 + 1.f) - ix, wx = ix - fx0;  // weight of x0 / x1 column
+    float ey = (fy0 + 1.f) - iy, wy = iy - fy0;
+    Taps t;
+    t.i00 = y0 * w + x0; t.i01 = y0 * w + x1; t.i10 = y1 * w + x0; t.i11 = y1 * w + x1;
+    t.w00 = ex * ey; t.w01 = wx * ey; t.w10 = ex * wy; t.w11 = wx * wy;
+    return t;
+}
+
+// Counter-based uniform [0,1) (24-bit mantissa) for perf-mode jitter.
+__device__ __forceinline__ float sd_uniform(uint64_t seed, uint64_t ctr) {
+    uint64_t z = seed + 0x9E3779B97F4A7C15ull * (ctr + 1);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z = z ^ (z >> 31);
+    return (float)(uint32_t)(z >> 40) * (1.0f / 16777216.0f);
+}

@@ -1,0 +1,183 @@
+// sdhip_rays.hip -- bit-exact frustum ray generation, z sampling and layout packs.
+//
+// sd_gen_rays : util.unproj_map (scenedino/common/util.py:113-158), util.gen_rays
+//               (util.py:253-285), ImageRaySampler.sample (ray_sampler.py:439-513)
+// sd_sample_z : NeRFRenderer.sample_coarse (scenedino/renderer/nerf.py:121-141)
+// sd_pack_*   : NCHW -> NHWC layout steps feeding the fused gather kernels.
+#include "sdhip_common.h"
+
+// One thread per (view, pixel).  Output row = 11 floats.
+__global__ void __launch_bounds__(256) k_gen_rays(const float *__restrict__ poses,
+                                                  const float *__restrict__ Ks,
+                                                  const float *__restrict__ frame_ids,
+                                                  int64_t n_views, int64_t H, int64_t W,
+                                                  float xs, float xe, float ys, float ye,
+                                                  float z_near, float z_far,
+                                                  float *__restrict__ rays) {
+    int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int64_t npix = H * W;
+    if (gid >= n_views * npix) return;
+    int64_t v = gid / npix, p = gid - v * npix;
+    int64_t y = p / W, x = p - y * W;
+    const float *P = poses + v * 16;
+    const float *K = Ks + v * 9;
+    float xi = sd_linspace_at(xs, xe, W, x);
+    float yi = sd_linspace_at(ys, ye, H, y);
+    float ux = (xi - K[2]) / K[0];
+    float uy = (yi - K[5]) / K[4];
+    float uz = 1.0f;
+    // torch.norm over the last dim of 3: fma chain, then IEEE sqrt (verified bit-exact).
+    float nrm = sqrtf(fmaf(uz, uz, fmaf(uy, uy, ux * ux)));
+    ux = ux / nrm; uy = uy / nrm; uz = uz / nrm;
+    float *r = rays + gid * 11;
+    r[0] = P[3]; r[1] = P[7]; r[2] = P[11];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        float a = P[i * 4 + 0] * ux;
+        float b = P[i * 4 + 1] * uy;
+        float c = P[i * 4 + 2] * uz;
+        r[3 + i] = (a + b) + c;  // 3x3 matmul: separately rounded, left to right
+    }
+    r[6] = z_near; r[7] = z_far; r[8] = frame_ids[v];
+    r[9] = xi; r[10] = yi;
+}
+
+__global__ void __launch_bounds__(256) k_sample_z(const float *__restrict__ rays, int64_t R,
+                                                  int64_t ray_dim, int64_t K, int lindisp,
+                                                  const float *__restrict__ u, uint64_t seed,
+                                                  uint64_t offset, float step, float t_end,
+                                                  float *__restrict__ z) {
+    int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= R * K) return;
+    int64_t r = gid / K, k = gid - r * K;
+    float near = rays[r * ray_dim + 6], far = rays[r * ray_dim + 7];
+    float uu = u ? u[gid] : sd_uniform(seed, offset + (uint64_t)gid);
+    float t = sd_linspace_at(0.0f, t_end, K, k) + uu * step;
+    float zz;
+    if (lindisp) {
+        float a = (1.0f / near) * (1.0f - t);
+        float b = (1.0f / far) * t;
+        zz = 1.0f / (a + b);
+    } else {
+        zz = near * (1.0f - t) + far * t;
+    }
+    z[gid] = zz;
+}
+
+// NCHW f32 -> NHWC (f32 or bf16) through a 32x33 LDS tile; grid (W/32, C/32, B*H).
+template <int DT>
+__global__ void __launch_bounds__(256) k_pack_grid(const float *__restrict__ in, int64_t C,
+                                                   int64_t H, int64_t W, void *__restrict__ out) {
+    __shared__ float tile[32][33];
+    int64_t bh = blockIdx.z;
+    int64_t b = bh / H, y = bh - b * H;
+    int64_t x0 = (int64_t)blockIdx.x * 32, c0 = (int64_t)blockIdx.y * 32;
+    int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+    for (int j = ty; j < 32; j += 8) {
+        int64_t c = c0 + j, x = x0 + tx;
+        tile[j][tx] = (c < C && x < W) ? in[((b * C + c) * H + y) * W + x] : 0.f;
+    }
+    __syncthreads();
+    for (int j = ty; j < 32; j += 8) {
+        int64_t x = x0 + j, c = c0 + tx;
+        if (x < W && c < C) {
+            int64_t o = ((b * H + y) * W + x) * C + c;
+            float v = tile[tx][j];
+            if (DT == SD_BF16)
+                ((__bf16 *)out)[o] = (__bf16)v;
+            else
+                ((float *)out)[o] = v;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_pack_image(const float *__restrict__ in, int64_t N,
+                                                    int64_t H, int64_t W,
+                                                    float *__restrict__ out) {
+    int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int64_t hw = H * W;
+    if (gid >= N * hw) return;
+    int64_t n = gid / hw, p = gid - n * hw;
+    const float *s = in + n * 3 * hw + p;
+    f32x4 v = {s[0], s[hw], s[2 * hw], 0.f};
+    *(f32x4 *)(out + gid * 4) = v;
+}
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+extern "C" void sd_set_error(const char *msg);
+#define SD_CHECK_LAUNCH(name)                                   \
+    do {                                                        \
+        hipError_t e_ = hipGetLastError();                      \
+        if (e_ != hipSuccess) {                                 \
+            sd_set_error(name ": launch failed");               \
+            return -2;                                          \
+        }                                                       \
+    } while (0)
+
+extern "C" int sd_gen_rays(const float *poses_c2w, const float *Ks, const float *frame_ids,
+                           int64_t n_views, int64_t H, int64_t W, float z_near, float z_far,
+                           float *rays_out, void *stream) {
+    if (!poses_c2w || !Ks || !frame_ids || !rays_out || n_views <= 0 || H <= 0 || W <= 0) {
+        sd_set_error("sd_gen_rays: invalid argument");
+        return -1;
+    }
+    double pw = 2.0 / (double)W, ph = 2.0 / (double)H;
+    float xs = (float)(-1.0 + 0.5 * pw), xe = (float)(1.0 - 0.5 * pw);
+    float ys = (float)(-1.0 + 0.5 * ph), ye = (float)(1.0 - 0.5 * ph);
+    int64_t n = n_views * H * W;
+    hipLaunchKernelGGL(k_gen_rays, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, poses_c2w, Ks, frame_ids, n_views, H, W, xs, xe, ys,
+                       ye, z_near, z_far, rays_out);
+    SD_CHECK_LAUNCH("sd_gen_rays");
+    return 0;
+}
+
+extern "C" int sd_sample_z(const float *rays, int64_t R, int64_t ray_dim, int64_t K, int lindisp,
+                           const float *u, uint64_t seed, uint64_t offset, float *z_out,
+                           void *stream) {
+    if (!rays || !z_out || R < 0 || K <= 0 || ray_dim < 8) {
+        sd_set_error("sd_sample_z: invalid argument");
+        return -1;
+    }
+    if (R == 0) return 0;
+    double step_d = 1.0 / (double)K;
+    int64_t n = R * K;
+    hipLaunchKernelGGL(k_sample_z, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, rays, R, ray_dim, K, lindisp, u, seed, offset,
+                       (float)step_d, (float)(1.0 - step_d), z_out);
+    SD_CHECK_LAUNCH("sd_sample_z");
+    return 0;
+}
+
+extern "C" int sd_pack_grid(const float *grid_nchw, int64_t B, int64_t C, int64_t H, int64_t W,
+                            int dtype, void *out_nhwc, void *stream) {
+    if (!grid_nchw || !out_nhwc || B <= 0 || C <= 0 || H <= 0 || W <= 0 ||
+        (dtype != SD_F32 && dtype != SD_BF16) || B * H > 2147483647LL) {
+        sd_set_error("sd_pack_grid: invalid argument");
+        return -1;
+    }
+    dim3 g((unsigned)((W + 31) / 32), (unsigned)((C + 31) / 32), (unsigned)(B * H));
+    if (dtype == SD_BF16)
+        hipLaunchKernelGGL(k_pack_grid<SD_BF16>, g, dim3(256), 0, (hipStream_t)stream, grid_nchw,
+                           C, H, W, out_nhwc);
+    else
+        hipLaunchKernelGGL(k_pack_grid<SD_F32>, g, dim3(256), 0, (hipStream_t)stream, grid_nchw,
+                           C, H, W, out_nhwc);
+    SD_CHECK_LAUNCH("sd_pack_grid");
+    return 0;
+}
+
+extern "C" int sd_pack_image(const float *img_nchw, int64_t N, int64_t H, int64_t W,
+                             float *out_nhwc4, void *stream) {
+    if (!img_nchw || !out_nhwc4 || N <= 0 || H <= 0 || W <= 0) {
+        sd_set_error("sd_pack_image: invalid argument");
+        return -1;
+    }
+    int64_t n = N * H * W;
+    hipLaunchKernelGGL(k_pack_image, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, img_nchw, N, H, W, out_nhwc4);
+    SD_CHECK_LAUNCH("sd_pack_image");
+    return 0;
+}

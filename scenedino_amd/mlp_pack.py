@@ -1,0 +1,136 @@
+"""Pack ResnetFC(n_blocks=0) parameters into the MFMA fragment order the gfx950
+kernels read (see scenedino_amd/csrc/sdhip_field.hip).
+
+ResnetFC (scenedino/models/prediction_heads/resnetfc.py:135-203) with
+n_blocks=0 computes  out = lin_out(relu(lin_in(x)))  for x = [grid features (C),
+positional code (39)] (bts.py:321-328).  out[0] -> sigma (softplus), out[1:] -> DINO.
+
+Fragment maps (32x32 MFMA, lane l, half h = l >> 5; accumulator row of register r
+is (r & 3) + 8 (r >> 2) + 4 h, column l & 31):
+  layer 1 A   : wpk[q][ht][l][j] = W_in'[32 ht + (l & 31)][16 q + 8 h + j]
+                where W_in' holds the C grid columns, then the 39 code columns
+                permuted into the kernel's slot order (3 chunks of 16, padded).
+  bias/sigma  : [t][h][r] = vec[32 t + (r & 3) + 8 (r >> 2) + 4 h]
+  layer 2 A   : bf16 [dt][t][s][l][j] = W_out[1 + 32 dt + (l & 31)][32 t + 16 s + 8 (j >> 2) + 4 h + (j & 3)]
+                f32  [dt][t][l][r]    = W_out[1 + 32 dt + (l & 31)][32 t + (r & 3) + 8 (r >> 2) + 4 h]
+"""
+from __future__ import annotations
+
+import functools
+
+import numpy as np
+import torch
+
+from . import _lib
+
+N_PE = 39
+PE_CHUNKS = 3
+D_HIDDEN = 128
+
+
+def pe_slot_to_ref_col(pc: int, h: int, j: int) -> int:
+    """Column (within the 39 code columns) feeding fragment element j of PE chunk pc,
+    lane half h; -1 = zero padding.  Reference code order (positional_encoding.py:75-79):
+    [x, y, z~] then for j' = 2 i + phase (i = freq, phase 0 sin / 1 cos), dims 0..2."""
+    s = 8 * pc + j
+    if s < 18:
+        i, d = divmod(s, 3)
+        return 3 + 3 * (2 * i + h) + d
+    if s < 21 and h == 0:
+        return s - 18
+    return -1
+
+
+@functools.lru_cache(maxsize=8)
+def _index_tables(C: int, D: int):
+    nq = C // 16 + PE_CHUNKS
+    lanes = np.arange(64)
+    lo, hh = lanes & 31, lanes >> 5
+    # layer-1 columns of W_in' -> original W_in column (or -1)
+    kk_src = np.full(C + 16 * PE_CHUNKS, -1, dtype=np.int64)
+    kk_src[:C] = np.arange(C)
+    for pc in range(PE_CHUNKS):
+        for h in range(2):
+            for j in range(8):
+                c = pe_slot_to_ref_col(pc, h, j)
+                if c >= 0:
+                    kk_src[C + 16 * pc + 8 * h + j] = C + c
+    q = np.arange(nq)[:, None, None, None]
+    ht = np.arange(4)[None, :, None, None]
+    l_lo = lo[None, None, :, None]
+    l_h = hh[None, None, :, None]
+    j = np.arange(8)[None, None, None, :]
+    rows1 = np.broadcast_to(32 * ht + l_lo, (nq, 4, 64, 8))
+    cols1 = kk_src[16 * q + 8 * l_h + j]
+    cols1 = np.broadcast_to(cols1, (nq, 4, 64, 8))
+    # accumulator-row order for bias / sigma rows
+    t = np.arange(4)[:, None, None]
+    h2 = np.arange(2)[None, :, None]
+    r = np.arange(16)[None, None, :]
+    accrow = 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h2  # (4,2,16)
+    ndt = D // 32
+    dt = np.arange(ndt)[:, None, None, None, None]
+    tt = np.arange(4)[None, :, None, None, None]
+    s = np.arange(2)[None, None, :, None, None]
+    l5_lo = lo[None, None, None, :, None]
+    l5_h = hh[None, None, None, :, None]
+    j5 = np.arange(8)[None, None, None, None, :]
+    rows2b = np.broadcast_to(1 + 32 * dt + l5_lo, (ndt, 4, 2, 64, 8))
+    cols2b = np.broadcast_to(32 * tt + 16 * s + 8 * (j5 >> 2) + 4 * l5_h + (j5 & 3),
+                             (ndt, 4, 2, 64, 8))
+    dt4 = np.arange(ndt)[:, None, None, None]
+    t4 = np.arange(4)[None, :, None, None]
+    l4_lo = lo[None, None, :, None]
+    l4_h = hh[None, None, :, None]
+    r4 = np.arange(16)[None, None, None, :]
+    rows2f = np.broadcast_to(1 + 32 * dt4 + l4_lo, (ndt, 4, 64, 16))
+    cols2f = np.broadcast_to(32 * t4 + (r4 & 3) + 8 * (r4 >> 2) + 4 * l4_h, (ndt, 4, 64, 16))
+    to_t = lambda a: torch.from_numpy(np.ascontiguousarray(a))
+    return {
+        "rows1": to_t(rows1), "cols1": to_t(cols1), "accrow": to_t(accrow),
+        "rows2b": to_t(rows2b), "cols2b": to_t(cols2b),
+        "rows2f": to_t(rows2f), "cols2f": to_t(cols2f),
+    }
+
+
+class PackedMLP:
+    """Device buffers + the ctypes ``sd_mlp`` record.  Keep the object alive while
+    kernels that use it may run."""
+
+    def __init__(self, W_in, b_in, W_out, b_out, dtype: int):
+        W_in = W_in.detach().float()
+        b_in = b_in.detach().float()
+        W_out = W_out.detach().float()
+        b_out = b_out.detach().float()
+        dh, din = W_in.shape
+        C = din - N_PE
+        D = W_out.shape[0] - 1
+        if dh != D_HIDDEN or C <= 0 or C % 16 or D % 32 or W_out.shape[1] != dh:
+            raise NotImplementedError(
+                f"fused field kernel needs d_hidden=128, C%16==0, D%32==0 (got W_in {tuple(W_in.shape)}, "
+                f"W_out {tuple(W_out.shape)})")
+        dev = W_in.device
+        ix = {k: v.to(dev) for k, v in _index_tables(C, D).items()}
+        Wz = torch.cat((W_in, torch.zeros(dh, 1, device=dev)), 1)  # column din = zero pad
+        cols1 = torch.where(ix["cols1"] < 0, torch.full_like(ix["cols1"], din), ix["cols1"])
+        w1 = Wz[ix["rows1"], cols1]
+        tdt = torch.bfloat16 if dtype == _lib.SD_BF16 else torch.float32
+        self.w_in = w1.to(tdt).contiguous()
+        self.b_in_h = b_in[ix["accrow"]].contiguous()
+        self.w_sig_h = W_out[0][ix["accrow"]].contiguous()
+        if dtype == _lib.SD_BF16:
+            self.w_out = W_out[ix["rows2b"], ix["cols2b"]].to(torch.bfloat16).contiguous()
+        else:
+            self.w_out = W_out[ix["rows2f"], ix["cols2f"]].contiguous()
+        self.b_dino = b_out[1:].contiguous()
+        self.b_sigma = float(b_out[0].item())
+        self.C, self.D, self.dtype = C, D, dtype
+        self.rec = _lib.SdMlp(
+            w_in=self.w_in.data_ptr(), b_in_h=self.b_in_h.data_ptr(),
+            w_sig_h=self.w_sig_h.data_ptr(), b_sigma=self.b_sigma,
+            w_out=self.w_out.data_ptr(), b_dino=self.b_dino.data_ptr(),
+            C=C, D=D, dtype=dtype, d_hidden=dh)
+
+
+def param_key(*ts):
+    return tuple((t.data_ptr(), t._version, tuple(t.shape), str(t.device)) for t in ts)

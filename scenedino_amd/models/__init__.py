@@ -1,0 +1,40 @@
+"""Model factory (mirror of scenedino/models/__init__.py:9-63)."""
+from ..common.positional_encoding import PositionalEncoding
+from .bts import BTSNet
+from .prediction_heads import make_head
+
+
+def make_model(config, downstream_config=None, encoder=None, downstream_head=None):
+    """Build BTSNet from the reference's model config.
+
+    The image encoder (DINO/DINOv2 ViT + DPT decoder) is passed in as ``encoder``
+    (any module exposing ``latent_size``, ``extra_outs``, ``forward(x,
+    ground_truth=False) -> [grid]`` and ``expand_dim``); building the ViT from
+    ``config['encoder']`` is a later row of the scope table.
+    """
+    arch = config.get("arch", "BTSNet")
+    if arch != "BTSNet":
+        raise NotImplementedError("Model architecture was not implemented yet")
+    sample_color = config.get("sample_color", True)
+    predict_dino = config.get("predict_dino", False)
+    dino_dims = config.get("dino_dims", 16)
+    if sample_color and predict_dino:
+        d_out = 1 + dino_dims
+    elif sample_color:
+        d_out = 1
+    else:
+        d_out = 4
+    if encoder is None:
+        raise NotImplementedError(
+            "scenedino_amd.make_model: pass encoder=<module>; the ViT/DPT encoder builder "
+            f"for {config.get('encoder', {}).get('type')!r} is not part of this build yet")
+    code_xyz = PositionalEncoding.from_conf(config["code"], d_in=3)
+    d_in = encoder.latent_size + code_xyz.d_out
+    if config.get("split_dino_heads", False):
+        raise NotImplementedError("split_dino_heads is not used by any shipped config")
+    heads = {hc["name"]: make_head(hc, d_in, d_out) for hc in config["decoder_heads"]}
+    return BTSNet(config, encoder, code_xyz, heads, config.get("final_pred_head", None),
+                  downstream_head=downstream_head)
+
+
+__all__ = ["BTSNet", "make_model", "make_head"]

@@ -1,0 +1,301 @@
+"""BTSNet -- the feature-field model, MI355X-native.
+
+Mirror of scenedino.models.bts.BTSNet (/root/reference/scenedino/models/bts.py:22-595):
+same constructor, attributes, ``encode`` semantics and ``forward`` return contract,
+same state_dict keys (``encoder.*``, ``code_xyz._freqs/_phases``,
+``heads.<name>.lin_in/lin_out.*``).  The per-point work (projection, positional
+code, bilinear feature gather, ResnetFC MLP, softplus, colour sampling) runs in the
+hand-written gfx950 kernels of libsdhip.so (``sd_field_query``; and, through
+``render_fused``, the fused render+composite kernel ``sd_render_fused``).
+
+Precision: ``precision="bf16"`` (default; bf16 grid + bf16 MFMA, fp32 accumulate
+and fp32 geometry / compositing) or ``"fp32"`` (f32 grid + exact-f32 MFMA) for
+fp32-tolerance parity with the reference.  Set via ``conf["precision"]`` or
+``net.set_precision``.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import _lib
+from ..mlp_pack import PackedMLP, param_key
+
+EPS = 1e-3  # scenedino/common/cameras/pinhole.py:3
+
+
+def _cam_records(poses_w2c, Ks):
+    """(..., 4, 4) w2c and (..., 3, 3) K -> (..., 21) camera records (C ABI layout)."""
+    lead = poses_w2c.shape[:-2]
+    return torch.cat((poses_w2c[..., :3, :].reshape(*lead, 12).float(),
+                      Ks.reshape(*lead, 9).float()), -1).contiguous()
+
+
+class BTSNet(nn.Module):
+    def __init__(self, conf, encoder: nn.Module, code_xyz, heads: dict,
+                 final_pred_head: str | None = None, uncertainty_predictor: nn.Module | None = None,
+                 ren_nc=None, downstream_head: nn.Module | None = None):
+        super().__init__()
+        self.encoder = encoder
+        self.code_xyz = code_xyz
+        self.heads = nn.ModuleDict(heads)
+        self.uncertainty_predictor = uncertainty_predictor
+        self.extra_outs = self.encoder.extra_outs
+        self.final_pred_head = final_pred_head if final_pred_head else list(self.heads.keys())[0]
+        self.requires_bottleneck_feats = False
+        self.use_viewdirs = conf.get("use_viewdirs", False)
+        self.d_min, self.d_max = conf.get("z_near", 3), conf.get("z_far", 80)
+        self.learn_empty = conf.get("learn_empty", True)
+        self.empty_empty = conf.get("empty_empty", False)
+        self.inv_z = conf.get("inv_z", True)
+        self.color_interpolation = conf.get("color_interpolation", "bilinear")
+        self.code_mode = conf.get("code_mode", "z")
+        self.flip_augmentation = conf.get("flip_augmentation", False)
+        self.return_sample_depth = conf.get("return_sample_depth", False)
+        self.sample_color = conf.get("sample_color", True)
+        self.predict_dino = conf.get("predict_dino", False)
+        d_in = self.encoder.latent_size + self.code_xyz.d_out
+        if self.sample_color and self.predict_dino:
+            d_out = 1 + conf.get("dino_dims", 16)
+        elif self.sample_color:
+            d_out = 1
+        else:
+            d_out = 4
+        self._d_in, self._d_out = d_in, d_out
+        if self.learn_empty:
+            self.empty_feature = nn.Parameter(torch.randn((self.encoder.latent_size,)))
+        self._scale = 0
+        self.downstream_head = downstream_head
+        self.gt_classes = downstream_head.gt_classes if downstream_head is not None else None
+        self.precision = conf.get("precision", "bf16")
+        self._packed = None
+        self._packed_key = None
+        self._grid_cache = None
+        self._grid_key = None
+        self.grid_c_combine = None
+        self.color_frame_filter = None
+        self.grid_f_extra = None
+
+    # -- reference API --------------------------------------------------------
+    def set_scale(self, scale):
+        self._scale = scale
+
+    def get_scale(self):
+        return self._scale
+
+    def compute_grid_transforms(self, *args, **kwargs):
+        pass
+
+    def set_precision(self, precision: str):
+        if precision not in ("bf16", "fp32"):
+            raise ValueError("precision must be 'bf16' or 'fp32'")
+        self.precision = precision
+        self._packed = None
+        self._grid_cache = None
+
+    def encode(self, images, Ks, poses_c2w, ids_encoder=None, ids_render=None, ids_loss=None,
+               images_alt=None, combine_ids=None, color_frame_filter=None,
+               loss_feature_grid_shift=None):
+        """Same semantics as bts.py:112-259 (encoder call, pose inversion, stored grids)."""
+        if combine_ids is not None or loss_feature_grid_shift not in (None, (0, 0)):
+            raise NotImplementedError("combine_ids / loss_feature_grid_shift are training-only "
+                                      "options outside the MI355X hot path")
+        with torch.autocast(device_type=images.device.type, enabled=False):
+            poses_w2c = torch.inverse(poses_c2w.float())
+        if ids_encoder is None:
+            images_encoder, Ks_encoder, poses_w2c_encoder = images, Ks, poses_w2c
+        else:
+            images_encoder = images[:, ids_encoder]
+            Ks_encoder = Ks[:, ids_encoder]
+            poses_w2c_encoder = poses_w2c[:, ids_encoder]
+        images_loss = images if ids_loss is None else images[:, ids_loss]
+        images = images_alt if images_alt is not None else images * 0.5 + 0.5
+        if ids_render is None:
+            images_render, Ks_render, poses_w2c_render = images, Ks, poses_w2c
+        else:
+            images_render = images[:, ids_render]
+            Ks_render = Ks[:, ids_render]
+            poses_w2c_render = poses_w2c[:, ids_render]
+        n_, nv_, c_, h_, w_ = images_encoder.shape
+        n_l, nv_l = images_loss.shape[:2]
+        do_flip = self.flip_augmentation and self.training and bool(torch.rand(1) > 0.5)
+        if do_flip:
+            images_encoder = torch.flip(images_encoder, dims=(-1,))
+        lat = self.encoder(images_encoder.reshape(n_ * nv_, c_, h_, w_))
+        lat_loss = self.encoder(images_loss.reshape(n_l * nv_l, c_, h_, w_), ground_truth=True)
+        if do_flip:
+            lat = [torch.flip(x, dims=(-1,)) for x in lat]
+        _, _, hh, ww = lat[0].shape
+        lat = [F.interpolate(x, size=(hh, ww)).view(n_, nv_, -1, hh, ww) for x in lat]
+        _, _, hl, wl = lat_loss[0].shape
+        lat_loss = [x.view(n_l, nv_l, -1, hl, wl) for x in lat_loss]
+        if self.extra_outs > 0:
+            self.grid_f_extra = [x[:, :, -self.extra_outs:] for x in lat]
+            lat = [x[:, :, :-self.extra_outs] for x in lat]
+        else:
+            self.grid_f_extra = None
+        self.grid_f_features = lat
+        self.grid_f_Ks = Ks_encoder
+        self.grid_f_poses_w2c = poses_w2c_encoder
+        self.grid_f_combine = None
+        self.grid_c_imgs = images_render.detach()
+        self.grid_c_Ks = Ks_render
+        self.grid_c_poses_w2c = poses_w2c_render
+        self.grid_c_combine = None
+        self.grid_l_loss_features = lat_loss
+        self.color_frame_filter = color_frame_filter
+        self._grid_cache = None
+
+    # -- device-side state for the kernels ------------------------------------
+    def _dtype(self):
+        return _lib.SD_BF16 if self.precision == "bf16" else _lib.SD_F32
+
+    def _mlp(self):
+        head = self.heads[self.final_pred_head]
+        if getattr(head, "n_blocks", 0) != 0 or getattr(head, "d_latent", 0) != 0:
+            raise NotImplementedError("fused field kernel supports ResnetFC(n_blocks=0) heads "
+                                      "(every shipped config)")
+        if len(self.heads) != 1:
+            raise NotImplementedError("fused field kernel supports a single prediction head")
+        ps = (head.lin_in.weight, head.lin_in.bias, head.lin_out.weight, head.lin_out.bias)
+        key = param_key(*ps) + (self.precision,)
+        if self._packed is None or self._packed_key != key:
+            self._packed = PackedMLP(*ps, dtype=self._dtype())
+            self._packed_key = key
+        return self._packed
+
+    def _grids(self):
+        g = self.grid_f_features[self._scale]
+        key = (id(g), g._version, id(self.grid_c_imgs), self.grid_c_imgs._version,
+               id(self.grid_f_poses_w2c), id(self.grid_c_poses_w2c), self.precision)
+        if self._grid_cache is not None and self._grid_key == key:
+            return self._grid_cache
+        B, nvf, C, Hf, Wf = g.shape
+        if nvf != 1:
+            raise NotImplementedError("the field kernels take exactly one encoder view "
+                                      "(ids_encoder=[0], as every shipped config)")
+        if self.learn_empty:
+            raise NotImplementedError("learn_empty=True is not used by any shipped config")
+        grid = _lib.pack_grid(g.reshape(B, C, Hf, Wf).float().contiguous(), self._dtype())
+        imgs = self.grid_c_imgs
+        n, nv, c3, H, W = imgs.shape
+        img = _lib.pack_image(imgs.reshape(n * nv, c3, H, W).float().contiguous())
+        cache = {
+            "grid": grid, "C": C, "Hf": Hf, "Wf": Wf, "B": B,
+            "cam_f": _cam_records(self.grid_f_poses_w2c[:, 0], self.grid_f_Ks[:, 0]),
+            "img": img, "nv": nv, "Hc": H, "Wc": W,
+            "cam_c": _cam_records(self.grid_c_poses_w2c, self.grid_c_Ks),
+        }
+        self._grid_cache, self._grid_key = cache, key
+        return cache
+
+    def _check_supported(self):
+        if self.training and torch.is_grad_enabled():
+            raise NotImplementedError(
+                "scenedino_amd: backward kernels for the fused field are not implemented yet; "
+                "use eval() / torch.no_grad() (inference) with this build")
+        if self.grid_c_combine is not None or self.color_frame_filter is not None:
+            raise NotImplementedError("grid_c_combine / color_frame_filter (training) unsupported")
+        if self.grid_f_extra is not None:
+            raise NotImplementedError("extra encoder outputs unsupported")
+        if not (self.sample_color and self.predict_dino) or self.code_mode != "z" or not self.inv_z:
+            raise NotImplementedError("field kernels implement predict_dino + sample_color, "
+                                      "code_mode=z, inv_z (every shipped config)")
+        if (self.d_min, self.d_max) != (3, 80):
+            raise NotImplementedError("field kernels bake z_near=3, z_far=80 into the code")
+
+    # -- hot path -------------------------------------------------------------
+    def render_fused(self, rays, z, sb, hard_alpha_cap, want_weights=True, want_alphas=True,
+                     want_rgb_samps=False):
+        """Fused field query + alpha compositing for all rays (used by NeRFRenderer).
+        rays (R, ray_dim) fp32, z (R, K) fp32 on the GPU; R = sb * rays_per_sb."""
+        self._check_supported()
+        m = self._mlp()
+        gc = self._grids()
+        R, K = z.shape
+        if R % sb or gc["B"] != sb:
+            raise ValueError(f"rays ({R}) must split into {sb} super-batches matching the "
+                             f"encoded batch ({gc['B']})")
+        dev = z.device
+        nv = gc["nv"]
+        out = {
+            "depth": torch.empty(R, device=dev),
+            "dino": torch.empty(R, m.D, device=dev),
+            "rgb": torch.empty(R, 3 * nv, device=dev),
+            "invalid": torch.empty(R, K, nv, device=dev),
+            "invalid_f": torch.empty(R, K, device=dev, dtype=torch.uint8),
+            "weights": torch.empty(R, K, device=dev) if want_weights else None,
+            "alphas": torch.empty(R, K, device=dev) if want_alphas else None,
+            "rgb_samps": torch.empty(R, K, 3 * nv, device=dev) if want_rgb_samps else None,
+        }
+        rays = rays.float().contiguous()
+        z = z.contiguous()
+        args = _lib.SdRenderArgs(
+            rays=rays.data_ptr(), ray_dim=rays.shape[1], R=R, rays_per_sb=R // sb, K=K,
+            z=z.data_ptr(), grid=gc["grid"].data_ptr(), Hf=gc["Hf"], Wf=gc["Wf"],
+            cam_f=gc["cam_f"].data_ptr(), img=gc["img"].data_ptr(), nv=nv, Hc=gc["Hc"],
+            Wc=gc["Wc"], cam_c=gc["cam_c"].data_ptr(), hard_alpha_cap=int(bool(hard_alpha_cap)),
+            depth=out["depth"].data_ptr(), dino=out["dino"].data_ptr(),
+            rgb=out["rgb"].data_ptr(),
+            weights=out["weights"].data_ptr() if want_weights else None,
+            alphas=out["alphas"].data_ptr() if want_alphas else None,
+            invalid=out["invalid"].data_ptr(), invalid_f=out["invalid_f"].data_ptr(),
+            rgb_samps=out["rgb_samps"].data_ptr() if want_rgb_samps else None)
+        _lib.render_fused(args, m.rec, z)
+        return out
+
+    def query(self, xyz):
+        """Raw per-point field: sigma (n,P), dino (n,P,D), rgb (n,P,3nv), invalid (n,P,nv),
+        invalid_features (n,P) -- all from sd_field_query."""
+        self._check_supported()
+        m = self._mlp()
+        gc = self._grids()
+        n, P, _ = xyz.shape
+        if n != gc["B"]:
+            raise ValueError(f"xyz batch {n} != encoded batch {gc['B']}")
+        dev = xyz.device
+        nv = gc["nv"]
+        xyz = xyz.float().contiguous()
+        sigma = torch.empty(n, P, device=dev)
+        dino = torch.empty(n, P, m.D, device=dev)
+        rgb = torch.empty(n, P, 3 * nv, device=dev)
+        inv = torch.empty(n, P, nv, device=dev)
+        invf = torch.empty(n, P, device=dev, dtype=torch.uint8)
+        args = _lib.SdFieldArgs(
+            xyz=xyz.data_ptr(), B=n, P=P, grid=gc["grid"].data_ptr(), Hf=gc["Hf"], Wf=gc["Wf"],
+            cam_f=gc["cam_f"].data_ptr(), img=gc["img"].data_ptr(), nv=nv, Hc=gc["Hc"],
+            Wc=gc["Wc"], cam_c=gc["cam_c"].data_ptr(), sigma=sigma.data_ptr(),
+            dino=dino.data_ptr(), rgb=rgb.data_ptr(), invalid=inv.data_ptr(),
+            invalid_f=invf.data_ptr())
+        _lib.field_query(args, m.rec, xyz)
+        return sigma, dino, rgb, inv, invf.bool()
+
+    def forward(self, xyz: torch.Tensor, **kwargs):
+        """Same return contract as bts.py:476-595."""
+        only_density = kwargs.get("only_density", False)
+        render_flow = kwargs.get("render_flow", False)
+        predict_segmentation = kwargs.get("predict_segmentation", False)
+        prediction_mode = kwargs.get("prediction_mode", "stego_kmeans")
+        if render_flow:
+            raise NotImplementedError("render_flow is a training-only option")
+        with torch.profiler.record_function("model_inference"):
+            n_, n_pts, _ = xyz.shape
+            sigma, dino, rgb, inv, invf = self.query(xyz)
+            sigma = sigma.unsqueeze(-1)
+            if predict_segmentation:
+                dino_full = self.encoder.expand_dim(dino)
+                if self.downstream_head is not None:
+                    seg = self.downstream_head(dino_full, mode=prediction_mode)
+                    seg = F.one_hot(seg, self.gt_classes)
+                else:
+                    seg = None
+                return dino_full, None, sigma, seg
+            if only_density:
+                rgb = torch.zeros((n_, n_pts, rgb.shape[-1]), device=sigma.device)
+                invalid = invf.unsqueeze(-1).to(sigma.dtype)
+            else:
+                invalid = inv
+            state_dict = {"invalid_features": invf.reshape(1, n_ * n_pts, 1),
+                          "dino_features": dino}
+            return rgb, invalid, sigma, None, state_dict

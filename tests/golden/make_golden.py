@@ -1,0 +1,367 @@
+"""Generate golden input/output vectors from the reference (tum-vision/scenedino).
+
+Run ONLY in the build container, where the read-only reference lives at
+/root/reference:
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+It imports the reference's own Python modules (renderer, BTSNet, ray sampler,
+pinhole camera, positional encoding, ResnetFC) with a handful of tiny stub
+modules for third-party packages that are absent here and irrelevant to the
+hot path (dotmap, cv2, torchvision, omegaconf), runs them on CPU in fp32 on
+seeded inputs, and writes the inputs and outputs as ``.npz`` fixtures next to
+this script.  Nothing from the reference is copied: the fixtures are data
+(arrays), and this script only *calls* the reference.
+
+Fixtures written (all float32 unless noted):
+  gen_rays_small.npz      ImageRaySampler.sample at 24x80, two poses, 2 frames
+  gen_rays_full.json      sha256 of the raw bytes of the 192x640 rays (bit-exact)
+  sample_z.npz            NeRFRenderer.sample_coarse with injected jitter u
+  field_query.npz         BTSNet.forward on raw points (sigma, dino, rgb, invalid)
+  render_*.npz            NeRFRenderer(...).forward through BTSNet, 24x80 frames
+  render_full_digest.json summary statistics of a 192x640x64 reference render
+"""
+from __future__ import annotations
+
+import contextlib
+import hashlib
+import json
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+REF = os.environ.get("SCENEDINO_REF", "/root/reference")
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+KITTI_K = [[0.7849, 0.0, -0.0312], [0.0, 2.9391, 0.2701], [0.0, 0.0, 1.0]]
+
+
+# ----------------------------------------------------------------------------
+# reference import harness
+# ----------------------------------------------------------------------------
+def _install_stubs():
+    class DotMap(dict):
+        def __getattr__(self, k):
+            if k.startswith("__"):
+                raise AttributeError(k)
+            if k not in self:
+                self[k] = DotMap()
+            return self[k]
+
+        def __setattr__(self, k, v):
+            self[k] = v
+
+        def toDict(self):
+            out = {}
+            for k, v in self.items():
+                out[k] = v.toDict() if isinstance(v, DotMap) else v
+            return out
+
+    dm = types.ModuleType("dotmap")
+    dm.DotMap = DotMap
+    sys.modules["dotmap"] = dm
+
+    cv2 = types.ModuleType("cv2")
+    cv2.COLORMAP_HOT = 11
+    sys.modules["cv2"] = cv2
+
+    tv = types.ModuleType("torchvision")
+    tvt = types.ModuleType("torchvision.transforms")
+    tv.transforms = tvt
+    sys.modules["torchvision"] = tv
+    sys.modules["torchvision.transforms"] = tvt
+
+    oc = types.ModuleType("omegaconf")
+    oc.ListConfig = list
+    sys.modules["omegaconf"] = oc
+
+    sys.path.insert(0, REF)
+    import scenedino  # noqa: F401  (real package, light __init__)
+
+    for sub in ("scenedino.models", "scenedino.models.prediction_heads"):
+        m = types.ModuleType(sub)
+        m.__path__ = [os.path.join(REF, *sub.split("."))]
+        sys.modules[sub] = m
+
+
+@contextlib.contextmanager
+def _no_cuda_ones():
+    orig = torch.ones
+
+    def ones(*a, **kw):
+        kw.pop("device", None)
+        return orig(*a, **kw)
+
+    torch.ones = ones
+    try:
+        yield
+    finally:
+        torch.ones = orig
+
+
+def load_reference():
+    _install_stubs()
+    from scenedino.renderer.nerf import NeRFRenderer
+    from scenedino.common.ray_sampler import ImageRaySampler
+    from scenedino.common import util
+    from scenedino.common.positional_encoding import PositionalEncoding
+    from scenedino.models.prediction_heads.resnetfc import ResnetFC
+
+    with _no_cuda_ones():
+        from scenedino.models.bts import BTSNet
+    return types.SimpleNamespace(
+        NeRFRenderer=NeRFRenderer,
+        ImageRaySampler=ImageRaySampler,
+        util=util,
+        PositionalEncoding=PositionalEncoding,
+        ResnetFC=ResnetFC,
+        BTSNet=BTSNet,
+    )
+
+
+class FakeEncoder(torch.nn.Module):
+    """Stands in for DINOv2Module: returns a fixed feature grid (the ViT/DPT
+    encoder is a separate row of the scope table)."""
+
+    def __init__(self, grid):
+        super().__init__()
+        self.grid = grid  # (n*nv, C, h, w)
+        self.latent_size = grid.shape[1]
+        self.extra_outs = 0
+
+    def forward(self, x, ground_truth=False):
+        return [self.grid]
+
+
+def make_pose(yaw_deg, tx, ty=0.0, tz=0.0):
+    a = np.deg2rad(yaw_deg)
+    p = np.eye(4, dtype=np.float32)
+    p[0, 0], p[0, 2], p[2, 0], p[2, 2] = np.cos(a), np.sin(a), -np.sin(a), np.cos(a)
+    p[:3, 3] = [tx, ty, tz]
+    return torch.from_numpy(p)
+
+
+def build_net(ref, grid, n_views_enc=1, dino_dims=64, d_hidden=128, seed=2):
+    conf = {
+        "predict_dino": True,
+        "dino_dims": dino_dims,
+        "learn_empty": False,
+        "code_mode": "z",
+        "inv_z": True,
+        "z_near": 3,
+        "z_far": 80,
+        "sample_color": True,
+    }
+    torch.manual_seed(seed)
+    code = ref.PositionalEncoding(num_freqs=6, d_in=3, freq_factor=1.5, include_input=True)
+    enc = FakeEncoder(grid)
+    d_in = enc.latent_size + code.d_out
+    head = ref.ResnetFC(d_in=d_in, d_out=1 + dino_dims, n_blocks=0, d_hidden=d_hidden)
+    # ResnetFC initialises biases to zero; perturb them so parity covers the bias path.
+    with torch.no_grad():
+        g = torch.Generator().manual_seed(seed + 100)
+        head.lin_in.bias.copy_(0.1 * torch.randn(d_hidden, generator=g))
+        head.lin_out.bias.copy_(0.1 * torch.randn(1 + dino_dims, generator=g))
+    net = ref.BTSNet(conf, enc, code, {"normal_head": head}, final_pred_head="normal_head")
+    return net.eval()
+
+
+def np32(t):
+    return t.detach().cpu().numpy()
+
+
+# ----------------------------------------------------------------------------
+# fixtures
+# ----------------------------------------------------------------------------
+def fx_gen_rays(ref):
+    out = {}
+    K = torch.tensor(KITTI_K)
+    poses = torch.stack([torch.eye(4), make_pose(2.0, 0.5, 0.1, 0.3)])  # (2,4,4)
+    projs = torch.stack([K, K * torch.tensor([[1.05, 1, 1], [1, 0.97, 1], [1, 1, 1]])])
+    sampler = ref.ImageRaySampler(z_near=3, z_far=80, height=24, width=80)
+    rays, _ = sampler.sample(None, poses.view(1, 2, 4, 4), projs.view(1, 2, 3, 3))
+    out["poses"] = np32(poses)
+    out["projs"] = np32(projs)
+    out["rays"] = np32(rays)  # (1, 2*24*80, 11)
+    np.savez_compressed(os.path.join(HERE, "gen_rays_small.npz"), **out)
+
+    digests = {}
+    for name, P in (("identity", torch.eye(4)), ("offset", make_pose(2.0, 0.5, 0.1, 0.3))):
+        s = ref.ImageRaySampler(z_near=3, z_far=80, height=192, width=640)
+        r, _ = s.sample(None, P.view(1, 1, 4, 4), K.view(1, 1, 3, 3))
+        digests[name] = {
+            "pose": np32(P).tolist(),
+            "shape": list(r.shape),
+            "sha256": hashlib.sha256(np.ascontiguousarray(np32(r)).tobytes()).hexdigest(),
+        }
+    with open(os.path.join(HERE, "gen_rays_full.json"), "w") as f:
+        json.dump({"K": KITTI_K, "near": 3, "far": 80, "H": 192, "W": 640, "cases": digests}, f, indent=1)
+
+
+@contextlib.contextmanager
+def injected_rand(u):
+    orig = torch.rand_like
+
+    def rl(x, *a, **kw):
+        assert x.shape == u.shape, (x.shape, u.shape)
+        return u.clone()
+
+    torch.rand_like = rl
+    try:
+        yield
+    finally:
+        torch.rand_like = orig
+
+
+def fx_sample_z(ref):
+    g = torch.Generator().manual_seed(3)
+    rays = np.load(os.path.join(HERE, "gen_rays_small.npz"))["rays"][0][:512]
+    rays = torch.from_numpy(rays)
+    out = {"rays": np32(rays)}
+    for K in (8, 32, 64, 128):
+        u = torch.rand(rays.shape[0], K, generator=g)
+        for lindisp in (True, False):
+            r = ref.NeRFRenderer(n_coarse=K, lindisp=lindisp)
+            with injected_rand(u):
+                z = r.sample_coarse(rays)
+            out[f"u_{K}"] = np32(u)
+            out[f"z_{K}_{int(lindisp)}"] = np32(z)
+    np.savez_compressed(os.path.join(HERE, "sample_z.npz"), **out)
+
+    # full-size bit-exact digest at 192x640x64 with seeded u
+    K = torch.tensor(KITTI_K)
+    s = ref.ImageRaySampler(z_near=3, z_far=80, height=192, width=640)
+    full, _ = s.sample(None, torch.eye(4).view(1, 1, 4, 4), K.view(1, 1, 3, 3))
+    full = full[0]
+    u = torch.rand(full.shape[0], 64, generator=torch.Generator().manual_seed(7))
+    r = ref.NeRFRenderer(n_coarse=64, lindisp=True)
+    with injected_rand(u):
+        z = r.sample_coarse(full)
+    with open(os.path.join(HERE, "sample_z_full.json"), "w") as f:
+        json.dump({"seed": 7, "K": 64, "lindisp": True,
+                   "u_sha256": hashlib.sha256(np32(u).tobytes()).hexdigest(),
+                   "z_sha256": hashlib.sha256(np32(z).tobytes()).hexdigest()}, f, indent=1)
+
+
+def make_scene(n, nv_render, C, gh, gw, H, W, seed, offset_render=True):
+    """Inputs for encode(): images (n, nv, 3, H, W) in [-1,1], Ks, c2w poses.
+    view 0 = encoder view; views 0..nv_render-1 are render (colour) views."""
+    g = torch.Generator().manual_seed(seed)
+    images = torch.rand(n, nv_render, 3, H, W, generator=g) * 2 - 1
+    K = torch.tensor(KITTI_K)
+    Ks = K.view(1, 1, 3, 3).repeat(n, nv_render, 1, 1)
+    poses = torch.eye(4).view(1, 1, 4, 4).repeat(n, nv_render, 1, 1)
+    for b in range(n):
+        for v in range(nv_render):
+            if v > 0 or (b > 0 and offset_render):
+                poses[b, v] = make_pose(1.5 * v + 0.7 * b, 0.4 * v + 0.2 * b, 0.05 * v, 0.3 * v)
+    grid = torch.randn(n, C, gh, gw, generator=g)
+    return images, Ks, poses, grid
+
+
+def fx_field_query(ref):
+    """BTSNet.forward on raw world points (the SSCBench / inference_3d call)."""
+    n, C, gh, gw, H, W = 1, 256, 12, 40, 24, 80
+    images, Ks, poses, grid = make_scene(n, 1, C, gh, gw, H, W, seed=11)
+    net = build_net(ref, grid)
+    net.encode(images, Ks, poses, ids_encoder=[0], ids_render=[0])
+    g = torch.Generator().manual_seed(12)
+    P = 4096
+    xyz = torch.empty(1, P, 3)
+    xyz[..., 0] = (torch.rand(P, generator=g) * 2 - 1) * 25.0
+    xyz[..., 1] = (torch.rand(P, generator=g) * 2 - 1) * 4.0
+    xyz[..., 2] = torch.rand(P, generator=g) * 90.0 - 5.0  # includes z<=eps and far points
+    with torch.no_grad():
+        rgb, invalid, sigma, extras, sd = net(xyz)
+    head = net.heads["normal_head"]
+    np.savez_compressed(
+        os.path.join(HERE, "field_query.npz"),
+        images=np32(images), Ks=np32(Ks), poses=np32(poses), grid=np32(grid),
+        W_in=np32(head.lin_in.weight), b_in=np32(head.lin_in.bias),
+        W_out=np32(head.lin_out.weight), b_out=np32(head.lin_out.bias),
+        xyz=np32(xyz), rgb=np32(rgb), invalid=np32(invalid), sigma=np32(sigma),
+        dino=np32(sd["dino_features"]), invalid_features=np32(sd["invalid_features"]),
+    )
+
+
+def fx_render(ref, name, n, nv_render, K, hard_cap, H=24, W=80, gh=12, gw=40, seed=21):
+    C = 256
+    images, Ks, poses, grid = make_scene(n, nv_render, C, gh, gw, H, W, seed=seed)
+    net = build_net(ref, grid.view(n, C, gh, gw))
+    net.encode(images, Ks, poses, ids_encoder=[0], ids_render=list(range(nv_render)))
+    renderer = ref.NeRFRenderer(n_coarse=K, lindisp=True, hard_alpha_cap=hard_cap,
+                                eval_batch_size=65536)
+    wrapper = renderer.bind_parallel(net, gpus=None).eval()
+    sampler = ref.ImageRaySampler(z_near=3, z_far=80, height=H, width=W)
+    # render view: view 0 of each batch element (the encoder view), as the demo does
+    rays, _ = sampler.sample(None, poses[:, :1], Ks[:, :1])
+    g = torch.Generator().manual_seed(seed + 1)
+    u = torch.rand(rays.shape[0] * rays.shape[1], K, generator=g)
+    with torch.no_grad(), injected_rand(u):
+        out = wrapper(rays, want_weights=True, want_alphas=True, want_z_samps=True,
+                      want_rgb_samps=True)
+    c = out["coarse"]
+    head = net.heads["normal_head"]
+    np.savez_compressed(
+        os.path.join(HERE, f"render_{name}.npz"),
+        images=np32(images), Ks=np32(Ks), poses=np32(poses), grid=np32(grid),
+        W_in=np32(head.lin_in.weight), b_in=np32(head.lin_in.bias),
+        W_out=np32(head.lin_out.weight), b_out=np32(head.lin_out.bias),
+        rays=np32(rays), u=np32(u), K=np.int64(K), hard_cap=np.int64(hard_cap),
+        nv_render=np.int64(nv_render),
+        rgb=np32(c["rgb"]), depth=np32(c["depth"]), invalid=np32(c["invalid"]),
+        ray_info=np32(c["ray_info"]), weights=np32(c["weights"]), alphas=np32(c["alphas"]),
+        z_samps=np32(c["z_samps"]), rgb_samps=np32(c["rgb_samps"]),
+        dino_features=np32(c["dino_features"]),
+        invalid_features=np32(c["invalid_features"]),
+        sd_dino=np32(out["state_dict"]["dino_features"]),
+    )
+
+
+def fx_render_full_digest(ref):
+    """One 192x640x64 render (the BASELINE C2 shape, fp32 reference) at a small
+    grid; store summary statistics + a strided subsample of the outputs."""
+    H, W, K = 192, 640, 64
+    n, C, gh, gw = 1, 256, 48, 160
+    images, Ks, poses, grid = make_scene(n, 1, C, gh, gw, H, W, seed=31)
+    net = build_net(ref, grid)
+    net.encode(images, Ks, poses, ids_encoder=[0], ids_render=[0])
+    renderer = ref.NeRFRenderer(n_coarse=K, lindisp=True, hard_alpha_cap=False,
+                                eval_batch_size=65536)
+    wrapper = renderer.bind_parallel(net, gpus=None).eval()
+    sampler = ref.ImageRaySampler(z_near=3, z_far=80, height=H, width=W)
+    rays, _ = sampler.sample(None, poses[:, :1], Ks[:, :1])
+    u = torch.rand(rays.shape[1], K, generator=torch.Generator().manual_seed(32))
+    with torch.no_grad(), injected_rand(u):
+        out = wrapper(rays, want_weights=True, want_alphas=True)
+    c = out["coarse"]
+    idx = np.arange(0, H * W, 97)
+    np.savez_compressed(
+        os.path.join(HERE, "render_full_subsample.npz"),
+        grid_seed=np.int64(31), u_seed=np.int64(32), idx=idx,
+        depth=np32(c["depth"])[0, idx], dino=np32(c["dino_features"])[0, idx],
+        rgb=np32(c["rgb"])[0, idx], weights=np32(c["weights"])[0, idx],
+        depth_mean=np.float64(c["depth"].double().mean()),
+        dino_abs_mean=np.float64(c["dino_features"].double().abs().mean()),
+    )
+
+
+def main():
+    torch.set_num_threads(8)
+    ref = load_reference()
+    fx_gen_rays(ref)
+    fx_sample_z(ref)
+    fx_field_query(ref)
+    fx_render(ref, "k32_cap0", n=1, nv_render=1, K=32, hard_cap=False)
+    fx_render(ref, "k64_cap1", n=1, nv_render=1, K=64, hard_cap=True, H=16, W=48, seed=41)
+    fx_render(ref, "sb2_nv2_k16", n=2, nv_render=2, K=16, hard_cap=False, H=16, W=48, seed=51)
+    if os.environ.get("GOLDEN_FULL", "1") == "1":
+        fx_render_full_digest(ref)
+    print("golden fixtures written to", HERE)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,184 @@
+"""CPU checks of the MFMA fragment packing (scenedino_amd/mlp_pack.py).
+
+Emulates the lane-level semantics of v_mfma_f32_32x32x16_bf16 / v_mfma_f32_32x32x2_f32
+exactly as sdhip_field.hip feeds them (lane l, half h = l >> 5, accumulator row of
+register r = (r & 3) + 8 (r >> 2) + 4 h, column l & 31) and checks that the packed
+weights reproduce the dense ResnetFC math.  No GPU needed.
+"""
+import numpy as np
+import pytest
+import torch
+
+from scenedino_amd import _lib
+from scenedino_amd.mlp_pack import PackedMLP, pe_slot_to_ref_col
+from oracle import render_oracle as O
+
+LANES = np.arange(64)
+LO, HH = LANES & 31, LANES >> 5
+
+
+def accrow(r, h):
+    return (r & 3) + 8 * (r >> 2) + 4 * h
+
+
+def mfma_32x32x16(a_frag, b_frag, acc):
+    """a_frag, b_frag: (64, 8); acc: (64, 16) in accumulator layout."""
+    A = np.zeros((32, 16)); Bm = np.zeros((16, 32))
+    for l in range(64):
+        for j in range(8):
+            A[LO[l], 8 * HH[l] + j] = a_frag[l, j]
+            Bm[8 * HH[l] + j, LO[l]] = b_frag[l, j]
+    Dm = A @ Bm
+    out = acc.copy()
+    for l in range(64):
+        for r in range(16):
+            out[l, r] += Dm[accrow(r, HH[l]), LO[l]]
+    return out
+
+
+def mfma_32x32x2(a_val, b_val, acc):
+    A = np.zeros((32, 2)); Bm = np.zeros((2, 32))
+    for l in range(64):
+        A[LO[l], HH[l]] = a_val[l]
+        Bm[HH[l], LO[l]] = b_val[l]
+    Dm = A @ Bm
+    out = acc.copy()
+    for l in range(64):
+        for r in range(16):
+            out[l, r] += Dm[accrow(r, HH[l]), LO[l]]
+    return out
+
+
+def pe_chunk(v, pc, h):
+    """Kernel's sd_pe_chunk for one point (v = [x, y, z~])."""
+    out = np.zeros(8)
+    phase = np.float32(np.pi / 2) if h else 0.0
+    for j in range(8):
+        s = 8 * pc + j
+        if s < 18:
+            f = 1.5 * (1 << (s // 3))
+            out[j] = np.sin(phase + v[s % 3] * f)
+        elif s < 21:
+            out[j] = 0.0 if h else v[s - 18]
+    return out
+
+
+@pytest.fixture(scope="module")
+def mlp_params():
+    g = torch.Generator().manual_seed(5)
+    C, D = 32, 64
+    W_in = torch.randn(128, C + 39, generator=g) * 0.1
+    b_in = torch.randn(128, generator=g) * 0.1
+    W_out = torch.randn(1 + D, 128, generator=g) * 0.1
+    b_out = torch.randn(1 + D, generator=g) * 0.1
+    X = torch.randn(32, C, generator=g)                      # 32 points' grid features
+    V = torch.rand(32, 3, generator=g) * 2 - 1               # [x, y, z~]
+    return C, D, W_in, b_in, W_out, b_out, X, V
+
+
+def test_pe_slot_map_matches_reference_code(mlp_params):
+    """Slot order of the kernel's positional code vs the reference's 39-d code."""
+    *_, V = mlp_params
+    code = O.positional_code(V[:, :2], torch.zeros(32, 1)).numpy()  # shape check only
+    assert code.shape == (32, 39)
+    v = np.array([0.3, -0.7, 0.45], np.float32)
+    ref = O.positional_code(torch.tensor(v[None, :2]), torch.tensor([[1.0]])).numpy()[0]
+    # rebuild ref code from v directly (positional_code takes z, not z~): emulate directly
+    freqs = 1.5 * 2.0 ** np.arange(6)
+    refcode = [v[0], v[1], v[2]]
+    for i in range(6):
+        for p in range(2):
+            for d in range(3):
+                refcode.append(np.sin(p * np.float32(np.pi / 2) + v[d] * freqs[i]))
+    refcode = np.array(refcode)
+    seen = set()
+    for pc in range(3):
+        for h in range(2):
+            vals = pe_chunk(v, pc, h)
+            for j in range(8):
+                c = pe_slot_to_ref_col(pc, h, j)
+                if c < 0:
+                    assert vals[j] == 0
+                else:
+                    assert abs(vals[j] - refcode[c]) < 1e-5, (pc, h, j, c)
+                    seen.add(c)
+    assert seen == set(range(39))
+    assert ref.shape == (39,)
+
+
+@pytest.mark.parametrize("dtype", [_lib.SD_BF16, _lib.SD_F32])
+def test_layer1_and_layer2_fragments(mlp_params, dtype):
+    C, D, W_in, b_in, W_out, b_out, X, V = mlp_params
+    pk = PackedMLP(W_in, b_in, W_out, b_out, dtype)
+    w1 = pk.w_in.float().numpy()                       # (nq, 4, 64, 8)
+    nq = C // 16 + 3
+    # per-lane B fragments as the kernel builds them
+    feats = np.zeros((nq, 64, 8))
+    for l in range(64):
+        p, h = LO[l], HH[l]
+        for q in range(C // 16):
+            feats[q, l] = X[p, 16 * q + 8 * h: 16 * q + 8 * h + 8].numpy()
+        for pc in range(3):
+            feats[C // 16 + pc, l] = pe_chunk(V[p].numpy(), pc, h)
+    if dtype == _lib.SD_BF16:
+        feats = torch.tensor(feats).to(torch.bfloat16).double().numpy()
+    acc = [np.zeros((64, 16)) for _ in range(4)]
+    for q in range(nq):
+        for ht in range(4):
+            if dtype == _lib.SD_BF16:
+                acc[ht] = mfma_32x32x16(w1[q, ht], feats[q], acc[ht])
+            else:
+                for i in range(8):
+                    acc[ht] = mfma_32x32x2(w1[q, ht, :, i], feats[q, :, i], acc[ht])
+    # dense reference: h = W_in [X, code]^T
+    code = []
+    freqs = 1.5 * 2.0 ** np.arange(6)
+    for p in range(32):
+        v = V[p].numpy()
+        c = [v[0], v[1], v[2]]
+        for i in range(6):
+            for ph in range(2):
+                for d in range(3):
+                    c.append(np.sin(ph * np.float32(np.pi / 2) + v[d] * freqs[i]))
+        code.append(c)
+    xin = np.concatenate([X.numpy(), np.array(code)], 1)
+    Wd = W_in.double().numpy()
+    if dtype == _lib.SD_BF16:
+        Wd = W_in.to(torch.bfloat16).double().numpy()
+        xin = torch.tensor(xin).to(torch.bfloat16).double().numpy()
+    hdense = Wd @ xin.T  # (128, 32)
+    tol = 2e-2 if dtype == _lib.SD_BF16 else 1e-5
+    for ht in range(4):
+        for l in range(64):
+            for r in range(16):
+                assert abs(acc[ht][l, r] - hdense[32 * ht + accrow(r, HH[l]), LO[l]]) < tol
+    # bias / sigma row tables
+    bih = pk.b_in_h.numpy(); wsh = pk.w_sig_h.numpy()
+    for t in range(4):
+        for h in range(2):
+            for r in range(16):
+                assert bih[t, h, r] == b_in[32 * t + accrow(r, h)]
+                assert wsh[t, h, r] == W_out[0, 32 * t + accrow(r, h)]
+    # layer 2 on the accumulator-layout operand: out^T = W_out[1:] X
+    Hh = np.maximum(hdense + b_in.double().numpy()[:, None], 0)      # (128, 32)
+    Xacc = [np.zeros((64, 16)) for _ in range(4)]
+    for t in range(4):
+        for l in range(64):
+            for r in range(16):
+                Xacc[t][l, r] = Hh[32 * t + accrow(r, HH[l]), LO[l]]
+    w2 = pk.w_out.float().numpy()
+    dense2 = W_out[1:].double().numpy() @ Hh  # (D, 32)
+    for dt in range(D // 32):
+        o = np.zeros((64, 16))
+        for t in range(4):
+            if dtype == _lib.SD_BF16:
+                for s in range(2):
+                    b = Xacc[t][:, 8 * s: 8 * s + 8]
+                    o = mfma_32x32x16(w2[dt, t, s], b, o)
+            else:
+                for r in range(16):
+                    o = mfma_32x32x2(w2[dt, t, :, r], Xacc[t][:, r], o)
+        for l in range(64):
+            for r in range(16):
+                ref = dense2[32 * dt + accrow(r, HH[l]), LO[l]]
+                assert abs(o[l, r] - ref) < (5e-2 if dtype == _lib.SD_BF16 else 1e-5)
