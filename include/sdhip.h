@@ -17,7 +17,7 @@
  *   rays        (R, ray_dim>=8)  [o(3), d(3), near, far, (frame_id, x, y)]
  *   z           (R, K)
  *   camera rec  21 floats: w2c rows 0..2 (12 floats, 3x4) then K (9 floats, 3x3)
- *   grid        (B, Hf, Wf, C) NHWC, element type bf16 (dtype=SD_BF16) or f32
+ *   grid        (B, Hf, Wf, C) NHWC, element type f32 / bf16 / f16 (= the MLP dtype)
  *   colour img  (B, nv, Hc, Wc, 4) NHWC4 float32 (rgb + pad)
  */
 #ifndef SDHIP_H
@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-enum sd_dtype { SD_F32 = 0, SD_BF16 = 1 };
+enum sd_dtype { SD_F32 = 0, SD_BF16 = 1, SD_F16 = 2 };
 
 /* Last error text of the calling thread ("" if none). */
 const char *sd_last_error(void);
@@ -69,15 +69,16 @@ int sd_pack_image(const float *img_nchw, int64_t N, int64_t H, int64_t W, float 
  * ResnetFC(n_blocks=0): out = W_out relu(W_in x + b_in) + b_out
  *   (scenedino/models/prediction_heads/resnetfc.py:135-203). */
 typedef struct sd_mlp {
-    const void *w_in;      /* [C/16+3][4][64][8] of dtype (layer-1 A fragments)          */
+    const void *w_in;      /* [C/16+3][4][64][8] of dtype (layer-1 A fragments)            */
     const float *b_in_h;   /* [4][2][16] hidden bias, accumulator-row order                */
     const float *w_sig_h;  /* [4][2][16] W_out row 0 (sigma), accumulator-row order        */
     float b_sigma;         /* b_out[0]                                                     */
     const void *w_out;     /* layer-2 A fragments for the D dino rows (dtype-specific)     */
     const float *b_dino;   /* b_out[1:1+D]                                                 */
-    int32_t C;             /* grid channels (multiple of 16)                               */
+    int32_t C;             /* grid channels (multiple of 32)                               */
     int32_t D;             /* dino dims (multiple of 32)                                   */
-    int32_t dtype;         /* SD_BF16: bf16 MFMA + bf16 grid; SD_F32: f32 MFMA + f32 grid  */
+    int32_t dtype;         /* SD_F32 (exact-f32 MFMA), SD_BF16 or SD_F16 (16-bit MFMA,   */
+                           /* f32 accumulate); the grid must be packed in the same dtype  */
     int32_t d_hidden;      /* must be 128                                                  */
 } sd_mlp;
 

@@ -95,7 +95,8 @@ def positional_code(xy, z, d_min=3.0, d_max=80.0, num_freqs=6, freq_factor=1.5):
     phases = torch.zeros(2 * num_freqs)
     phases[1::2] = math.pi * 0.5
     phases = phases.view(-1, 1)
-    emb = torch.sin(phases + v.unsqueeze(-2) * freqs)  # (..., 12, 3)
+    # addcmul (positional_encoding.py:76): one fused multiply-add on CPU and GPU builds
+    emb = torch.sin(torch.addcmul(phases, v.unsqueeze(-2).expand(*v.shape[:-1], 12, 3), freqs))
     return torch.cat((v, emb.flatten(-2)), -1)  # (..., 39)
 
 

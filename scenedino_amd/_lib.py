@@ -17,6 +17,8 @@ ABI_VERSION = 1
 
 SD_F32 = 0
 SD_BF16 = 1
+SD_F16 = 2
+TORCH_DTYPE = {SD_F32: torch.float32, SD_BF16: torch.bfloat16, SD_F16: torch.float16}
 
 _vp = ctypes.c_void_p
 _i64 = ctypes.c_int64
@@ -152,8 +154,7 @@ def sample_z(rays, K, lindisp, u=None, seed=0, offset=0, out=None):
 def pack_grid(grid_nchw, dtype):
     lib = load()
     B, C, H, W = grid_nchw.shape
-    tdt = torch.bfloat16 if dtype == SD_BF16 else torch.float32
-    out = torch.empty(B, H, W, C, device=grid_nchw.device, dtype=tdt)
+    out = torch.empty(B, H, W, C, device=grid_nchw.device, dtype=TORCH_DTYPE[dtype])
     _check(lib.sd_pack_grid(ptr(_req(grid_nchw, "grid")), B, C, H, W, dtype, ptr(out),
                             stream_of(out)), "sd_pack_grid")
     return out

@@ -1,21 +1,30 @@
-// sdhip_field.hip -- fused feature-field render (gfx950 / CDNA4).
+// sdhip_field.hip -- fused feature-field render and field query (gfx950 / CDNA4).
 //
-// One wave owns a tile of 32 rays and walks their K samples in order
-// (sample-major).  Per sample the 32 points form the N=32 side of 32x32 MFMA
-// tiles of the first ResnetFC layer, computed transposed (H^T = W_in X^T) so that
-// every lane's accumulator column is "its" ray:
-//   * lane l (ray l&31, half h=l>>5) gathers 8 consecutive channels of its point
-//     from the NHWC grid for each 16-channel chunk -> B fragment, bilinear blend
-//     in fp32 registers (F.grid_sample bilinear/border/align_corners=False);
-//   * W_in fragments live in LDS (staged once per workgroup);
-//   * the 39-d positional code is computed in registers (3 more K chunks);
-//   * epilogue: +b_in, ReLU, sigma = w_sigma . h (fp32 dot + one cross-half add),
-//     softplus, alpha, sequential transmittance (exactly torch.cumprod's order),
-//     and the weighted sum  Hacc += w_k * relu(h_k)  in fp32 registers.
-// The DINO head is linear in h, so  sum_k w_k (W_out h_k + b) = W_out Hacc + (sum w) b:
-// the second layer runs ONCE per ray tile on the accumulated Hacc (16 MFMAs per 64
-// dims) instead of once per sample.  Colours are sampled per sample in the render
-// views (NHWC4 fp32) and composited in registers.
+// Work unit: one wave = 32 consecutive points (lanes l and l+32 share point l&31;
+// lane half h = l>>5 supplies the other 8 channels of every 16-channel K chunk).
+//   * render kernel: the 32 points are 32 consecutive samples of ONE ray (ray-major),
+//     so the bilinear taps of a sub-tile are spatially coherent (identical for the
+//     render-from-encoder-view case of the demo / SSCBench) and every per-sample
+//     store is coalesced;
+//   * field kernel: 32 consecutive query points.
+// First ResnetFC layer, transposed:  H^T (128 hidden x 32 points) = W_in . X^T as
+// 4 tiles of 32x32 MFMA; W_in fragments staged once per workgroup in LDS; the lane's
+// B fragment = bilinear blend of 8 NHWC channels from the 4 taps (F.grid_sample
+// bilinear/border/align_corners=False) or 8 values of the 39-d positional code.
+// Epilogue (accumulator layout: lane = point): +b_in via the initial accumulator,
+// ReLU, sigma = w_sigma . h (fp32 dot + one cross-half add), softplus.
+// Render kernel compositing: alpha, wave-level prefix product of (1-alpha+1e-10)
+// across the 32 lanes (+ carry across sub-tiles) = transmittance, weights, and the
+// DINO head folded into the compositing sum:
+//     sum_k w_k (W_out h_k + b) = sum_k (w_k h_k) W_out^T + (sum_k w_k) b
+// i.e. the second-layer MFMA consumes w-scaled hidden states and ACCUMULATES over
+// all samples of the ray in its accumulator (O layout: points summed in registers,
+// dims on lanes).  Colours: bilinear NHWC4 fp32 in each render view.
+//
+// Precision modes (template P): SD_F32 (f32 grid, exact-f32 MFMA 32x32x2, accurate
+// sinf), SD_BF16 (bf16 grid, fp32 blend, bf16 MFMA), SD_F16 (f16 grid, packed-f16
+// blend, f16 MFMA).  All modes accumulate in fp32 and keep geometry, alpha and
+// transmittance in fp32.
 //
 // Reference: NeRFRenderer.composite (scenedino/renderer/nerf.py:230-449),
 // BTSNet.forward / sample_features / sample_colors (scenedino/models/bts.py:271-595),
@@ -25,7 +34,9 @@
 #include "sdhip_common.h"
 
 #include <string.h>
-#include <type_traits>
+
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+typedef __attribute__((ext_vector_type(2))) _Float16 f16x2;
 
 static thread_local char g_err[512] = "";
 extern "C" void sd_set_error(const char *msg) {
@@ -35,12 +46,11 @@ extern "C" void sd_set_error(const char *msg) {
 extern "C" const char *sd_last_error(void) { return g_err; }
 extern "C" int sd_abi_version(void) { return 1; }
 
-template <int DT> struct GridT;
-template <> struct GridT<SD_BF16> { typedef uint16_t T; };
-template <> struct GridT<SD_F32> { typedef float T; };
+#define SD_WG 512            // threads per workgroup (8 waves, one workgroup per CU)
+#define SD_WAVES (SD_WG / 64)
 
 // ---------------------------------------------------------------------------
-// per-point geometry: projection into the encoder view, taps, positional code
+// per-point geometry
 // ---------------------------------------------------------------------------
 struct PointGeo {
     Taps t;
@@ -56,29 +66,29 @@ __device__ __forceinline__ PointGeo sd_point_geo(const float *__restrict__ cam, 
     g.inv_f = sd_outside(x, y, zc);
     x = fminf(fmaxf(x, -2.f), 2.f);
     y = fminf(fmaxf(y, -2.f), 2.f);
-    // encoding_mode._z with inv_z, d_min=3, d_max=80 (positional_encoding.py:13-21)
-    float zt = (1.f / fmaxf(zc, SD_EPS) - 1.f / 80.f) / (1.f / 3.f - 1.f / 80.f);
+    // encoding_mode._z, inv_z, d_min=3, d_max=80 (positional_encoding.py:13-21).
+    // (1/d_min - 1/d_max) is a Python double rounded once to fp32, as in the reference.
+    float zt = (1.f / fmaxf(zc, SD_EPS) - (float)(1.0 / 80.0)) / (float)(1.0 / 3.0 - 1.0 / 80.0);
     zt = 2.f * zt - 1.f;
     g.v[0] = x; g.v[1] = y; g.v[2] = zt;
     g.t = sd_taps(x, y, Wf, Hf);
     return g;
 }
 
-// Positional-code chunk pc (0..2) for lane half h: element j of the fragment is
-// slot s = 8*pc + j.  s < 18: freq index s/3 (f = 1.5 * 2^(s/3)), input dim s%3,
-// phase h*pi/2 (h=0 -> sin, h=1 -> cos as sin(x + pi/2), as the reference).  s in
-// 18..20 (h == 0): the raw inputs.  Everything else: 0.  The host packs W_in's 39
-// code columns in this order (scenedino_amd/mlp_pack.py).
+// Positional-code chunk pc (0..2) for lane half h: fragment element j = slot s = 8pc+j.
+// s < 18: sin(phase_h + v[s%3] * 1.5*2^(s/3)) with phase_h = h*float32(pi/2) (cos as
+// sin(x+pi/2), as the reference); s = 18..20 (h == 0): the raw inputs; else 0.
+// The host packs W_in's 39 code columns in this order (scenedino_amd/mlp_pack.py).
 template <bool FAST>
 __device__ __forceinline__ void sd_pe_chunk(const float v[3], int pc, int h, float out[8]) {
-    const float phase = h ? 1.5707963705062866f : 0.f;  // float32(pi/2), positional_encoding.py:65
+    const float phase = h ? 1.5707963705062866f : 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         int s = 8 * pc + j;
         float r = 0.f;
         if (s < 18) {
             float f = 1.5f * (float)(1 << (s / 3));
-            float a = phase + v[s % 3] * f;
+            float a = fmaf(v[s % 3], f, phase);  // torch.addcmul is a fused multiply-add
             r = FAST ? __sinf(a) : sinf(a);
         } else if (s < 21) {
             r = h ? 0.f : v[s - 18];
@@ -88,87 +98,138 @@ __device__ __forceinline__ void sd_pe_chunk(const float v[3], int pc, int h, flo
 }
 
 // ---------------------------------------------------------------------------
-// first layer: acc[ht] (32 hidden x 32 points) += W_in[ht] . X^T over C + 48 k
+// precision traits: grid storage, tap loads, blend, layer-1 / layer-2 MFMA
 // ---------------------------------------------------------------------------
-template <int DT> struct Layer1;
+template <int P> struct Prec;
 
-template <> struct Layer1<SD_BF16> {
-    struct TapRaw { uint4 a, b, c, d; };
-    static __device__ __forceinline__ TapRaw load(const uint16_t *__restrict__ g, const Taps &t,
-                                                  int C, int coff) {
-        TapRaw r;
-        r.a = *(const uint4 *)(g + (int64_t)t.i00 * C + coff);
-        r.b = *(const uint4 *)(g + (int64_t)t.i01 * C + coff);
-        r.c = *(const uint4 *)(g + (int64_t)t.i10 * C + coff);
-        r.d = *(const uint4 *)(g + (int64_t)t.i11 * C + coff);
-        return r;
+struct Raw16 { uint4 a, b, c, d; };  // 4 taps x 8 x 16-bit channels
+
+__device__ __forceinline__ Raw16 sd_load16(const uint16_t *__restrict__ g, const Taps &t, int C,
+                                           int coff) {
+    Raw16 r;
+    r.a = *(const uint4 *)(g + (int64_t)t.i00 * C + coff);
+    r.b = *(const uint4 *)(g + (int64_t)t.i01 * C + coff);
+    r.c = *(const uint4 *)(g + (int64_t)t.i10 * C + coff);
+    r.d = *(const uint4 *)(g + (int64_t)t.i11 * C + coff);
+    return r;
+}
+
+template <> struct Prec<SD_BF16> {
+    typedef uint16_t G;
+    typedef Raw16 Raw;
+    typedef bf16x8 Frag;
+    static constexpr bool FAST_PE = true;
+    static __device__ __forceinline__ Raw load(const G *__restrict__ g, const Taps &t, int C, int coff) {
+        return sd_load16(g, t, C, coff);
     }
-    static __device__ __forceinline__ float blend1(uint32_t a, uint32_t b, uint32_t c, uint32_t d,
-                                                   bool hi, const Taps &t) {
+    static __device__ __forceinline__ float b1(uint32_t a, uint32_t b, uint32_t c, uint32_t d,
+                                               bool hi, const Taps &t) {
         float va = hi ? bf16hi(a) : bf16lo(a), vb = hi ? bf16hi(b) : bf16lo(b);
         float vc = hi ? bf16hi(c) : bf16lo(c), vd = hi ? bf16hi(d) : bf16lo(d);
         return fmaf(vd, t.w11, fmaf(vc, t.w10, fmaf(vb, t.w01, va * t.w00)));
     }
-    static __device__ __forceinline__ bf16x8 blend(const TapRaw &r, const Taps &t) {
-        float f[8];
+    static __device__ __forceinline__ Frag blend(const Raw &r, const Taps &t) {
         uint32_t A[4] = {r.a.x, r.a.y, r.a.z, r.a.w}, B[4] = {r.b.x, r.b.y, r.b.z, r.b.w};
         uint32_t Cc[4] = {r.c.x, r.c.y, r.c.z, r.c.w}, D[4] = {r.d.x, r.d.y, r.d.z, r.d.w};
+        Frag o;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            f[2 * i] = blend1(A[i], B[i], Cc[i], D[i], false, t);
-            f[2 * i + 1] = blend1(A[i], B[i], Cc[i], D[i], true, t);
+            o[2 * i] = (__bf16)b1(A[i], B[i], Cc[i], D[i], false, t);
+            o[2 * i + 1] = (__bf16)b1(A[i], B[i], Cc[i], D[i], true, t);
         }
-        bf16x8 o;
+        return o;
+    }
+    static __device__ __forceinline__ Frag from_f(const float f[8]) {
+        Frag o;
 #pragma unroll
         for (int i = 0; i < 8; ++i) o[i] = (__bf16)f[i];
         return o;
     }
-    // acc[ht] += A(q, ht) . B
-    static __device__ __forceinline__ void mma(const uint8_t *lds_w, int q, int lane,
-                                               const bf16x8 &b, f32x16 acc[4]) {
-        const bf16x8 *w = (const bf16x8 *)lds_w + (q * 4) * SD_WAVE + lane;
+    // acc[ht] += W_in(q, ht) . X^T  (A fragments from LDS: [q][ht][lane] x 16 B)
+    static __device__ __forceinline__ void mma1(const uint8_t *lw, int q, int lane, const Frag &b,
+                                                f32x16 acc[4]) {
+        const Frag *w = (const Frag *)lw + (q * 4) * SD_WAVE + lane;
 #pragma unroll
         for (int ht = 0; ht < 4; ++ht)
             acc[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[ht * SD_WAVE], b, acc[ht], 0, 0, 0);
     }
-    static __device__ __forceinline__ void mma_f(const uint8_t *lds_w, int q, int lane,
-                                                 const float f[8], f32x16 acc[4]) {
-        bf16x8 b;
+    // out (32 points x 32 dims, O layout) += X^T . W_out^T[dt]; X in accumulator layout.
+    // w_out: [dt][t][s][lane] x 16 B
+    static __device__ __forceinline__ void mma2(const uint8_t *w_out, int dt, const f32x16 X[4],
+                                                int lane, f32x16 &out) {
+        const Frag *w = (const Frag *)w_out + (dt * 8) * SD_WAVE + lane;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) b[i] = (__bf16)f[i];
-        mma(lds_w, q, lane, b, acc);
-    }
-
-    template <bool FAST_PE>
-    static __device__ __forceinline__ void run(const uint16_t *__restrict__ g, int C,
-                                               const PointGeo &geo, const uint8_t *lds_w,
-                                               int lane, f32x16 acc[4]) {
-        const int h = lane >> 5;
-        const int nq = C >> 4;
-        int coff = 8 * h;
-        TapRaw cur = load(g, geo.t, C, coff);
-        for (int q = 0; q < nq; ++q) {
-            TapRaw nxt = cur;
-            if (q + 1 < nq) nxt = load(g, geo.t, C, coff + 16);
-            bf16x8 b = blend(cur, geo.t);
-            mma(lds_w, q, lane, b, acc);
-            cur = nxt;
-            coff += 16;
-        }
+        for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int pc = 0; pc < SD_PE_CHUNKS; ++pc) {
-            float f[8];
-            sd_pe_chunk<FAST_PE>(geo.v, pc, h, f);
-            mma_f(lds_w, nq + pc, lane, f, acc);
-        }
+            for (int s = 0; s < 2; ++s) {
+                Frag a;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) a[j] = (__bf16)X[t][8 * s + j];
+                out = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, w[(t * 2 + s) * SD_WAVE], out, 0, 0, 0);
+            }
     }
 };
 
-template <> struct Layer1<SD_F32> {
-    struct TapRaw { f32x4 a0, a1, b0, b1, c0, c1, d0, d1; };
-    static __device__ __forceinline__ TapRaw load(const float *__restrict__ g, const Taps &t, int C,
-                                                  int coff) {
-        TapRaw r;
+template <> struct Prec<SD_F16> {
+    typedef uint16_t G;
+    typedef Raw16 Raw;
+    typedef f16x8 Frag;
+    static constexpr bool FAST_PE = true;
+    static __device__ __forceinline__ Raw load(const G *__restrict__ g, const Taps &t, int C, int coff) {
+        return sd_load16(g, t, C, coff);
+    }
+    static __device__ __forceinline__ Frag blend(const Raw &r, const Taps &t) {
+        const f16x2 w0 = {(_Float16)t.w00, (_Float16)t.w00}, w1 = {(_Float16)t.w01, (_Float16)t.w01};
+        const f16x2 w2 = {(_Float16)t.w10, (_Float16)t.w10}, w3 = {(_Float16)t.w11, (_Float16)t.w11};
+        uint32_t A[4] = {r.a.x, r.a.y, r.a.z, r.a.w}, B[4] = {r.b.x, r.b.y, r.b.z, r.b.w};
+        uint32_t Cc[4] = {r.c.x, r.c.y, r.c.z, r.c.w}, D[4] = {r.d.x, r.d.y, r.d.z, r.d.w};
+        Frag o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            f16x2 v = __builtin_bit_cast(f16x2, A[i]) * w0;
+            v = __builtin_elementwise_fma(__builtin_bit_cast(f16x2, B[i]), w1, v);
+            v = __builtin_elementwise_fma(__builtin_bit_cast(f16x2, Cc[i]), w2, v);
+            v = __builtin_elementwise_fma(__builtin_bit_cast(f16x2, D[i]), w3, v);
+            o[2 * i] = v[0];
+            o[2 * i + 1] = v[1];
+        }
+        return o;
+    }
+    static __device__ __forceinline__ Frag from_f(const float f[8]) {
+        Frag o;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = (_Float16)f[i];
+        return o;
+    }
+    static __device__ __forceinline__ void mma1(const uint8_t *lw, int q, int lane, const Frag &b,
+                                                f32x16 acc[4]) {
+        const Frag *w = (const Frag *)lw + (q * 4) * SD_WAVE + lane;
+#pragma unroll
+        for (int ht = 0; ht < 4; ++ht)
+            acc[ht] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w[ht * SD_WAVE], b, acc[ht], 0, 0, 0);
+    }
+    static __device__ __forceinline__ void mma2(const uint8_t *w_out, int dt, const f32x16 X[4],
+                                                int lane, f32x16 &out) {
+        const Frag *w = (const Frag *)w_out + (dt * 8) * SD_WAVE + lane;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                Frag a;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) a[j] = (_Float16)X[t][8 * s + j];
+                out = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, w[(t * 2 + s) * SD_WAVE], out, 0, 0, 0);
+            }
+    }
+};
+
+template <> struct Prec<SD_F32> {
+    typedef float G;
+    struct Raw { f32x4 a0, a1, b0, b1, c0, c1, d0, d1; };
+    struct Frag { float f[8]; };
+    static constexpr bool FAST_PE = false;
+    static __device__ __forceinline__ Raw load(const G *__restrict__ g, const Taps &t, int C, int coff) {
+        Raw r;
         const float *pa = g + (int64_t)t.i00 * C + coff, *pb = g + (int64_t)t.i01 * C + coff;
         const float *pc = g + (int64_t)t.i10 * C + coff, *pd = g + (int64_t)t.i11 * C + coff;
         r.a0 = *(const f32x4 *)pa; r.a1 = *(const f32x4 *)(pa + 4);
@@ -177,109 +238,116 @@ template <> struct Layer1<SD_F32> {
         r.d0 = *(const f32x4 *)pd; r.d1 = *(const f32x4 *)(pd + 4);
         return r;
     }
-    // grid_sample order: nw, ne, sw, se accumulated left to right.
-    static __device__ __forceinline__ void blend(const TapRaw &r, const Taps &t, float f[8]) {
+    // grid_sample order: nw, ne, sw, se accumulated left to right, separately rounded.
+    static __device__ __forceinline__ Frag blend(const Raw &r, const Taps &t) {
+        Frag o;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            f[i] = ((r.a0[i] * t.w00 + r.b0[i] * t.w01) + r.c0[i] * t.w10) + r.d0[i] * t.w11;
-            f[4 + i] = ((r.a1[i] * t.w00 + r.b1[i] * t.w01) + r.c1[i] * t.w10) + r.d1[i] * t.w11;
+            o.f[i] = ((r.a0[i] * t.w00 + r.b0[i] * t.w01) + r.c0[i] * t.w10) + r.d0[i] * t.w11;
+            o.f[4 + i] = ((r.a1[i] * t.w00 + r.b1[i] * t.w01) + r.c1[i] * t.w10) + r.d1[i] * t.w11;
         }
+        return o;
     }
-    static __device__ __forceinline__ void mma_f(const uint8_t *lds_w, int q, int lane,
-                                                 const float f[8], f32x16 acc[4]) {
-        const f32x4 *w = (const f32x4 *)lds_w + ((q * 4) * SD_WAVE + lane) * 2;
+    static __device__ __forceinline__ Frag from_f(const float f[8]) {
+        Frag o;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o.f[i] = f[i];
+        return o;
+    }
+    // f32 A values: [q][ht][lane][8]; 8 exact-f32 32x32x2 MFMAs per (chunk, ht)
+    static __device__ __forceinline__ void mma1(const uint8_t *lw, int q, int lane, const Frag &b,
+                                                f32x16 acc[4]) {
+        const f32x4 *w = (const f32x4 *)lw + ((q * 4) * SD_WAVE + lane) * 2;
 #pragma unroll
         for (int ht = 0; ht < 4; ++ht) {
             f32x4 w0 = w[ht * SD_WAVE * 2], w1 = w[ht * SD_WAVE * 2 + 1];
 #pragma unroll
             for (int i = 0; i < 4; ++i)
-                acc[ht] = __builtin_amdgcn_mfma_f32_32x32x2f32(w0[i], f[i], acc[ht], 0, 0, 0);
+                acc[ht] = __builtin_amdgcn_mfma_f32_32x32x2f32(w0[i], b.f[i], acc[ht], 0, 0, 0);
 #pragma unroll
             for (int i = 0; i < 4; ++i)
-                acc[ht] = __builtin_amdgcn_mfma_f32_32x32x2f32(w1[i], f[4 + i], acc[ht], 0, 0, 0);
+                acc[ht] = __builtin_amdgcn_mfma_f32_32x32x2f32(w1[i], b.f[4 + i], acc[ht], 0, 0, 0);
         }
     }
-    template <bool FAST_PE>
-    static __device__ __forceinline__ void run(const float *__restrict__ g, int C,
-                                               const PointGeo &geo, const uint8_t *lds_w,
-                                               int lane, f32x16 acc[4]) {
-        const int h = lane >> 5;
-        const int nq = C >> 4;
-        int coff = 8 * h;
-        for (int q = 0; q < nq; ++q) {
-            TapRaw r = load(g, geo.t, C, coff);
-            float f[8];
-            blend(r, geo.t, f);
-            mma_f(lds_w, q, lane, f, acc);
-            coff += 16;
-        }
-#pragma unroll
-        for (int pc = 0; pc < SD_PE_CHUNKS; ++pc) {
-            float f[8];
-            sd_pe_chunk<FAST_PE>(geo.v, pc, h, f);
-            mma_f(lds_w, nq + pc, lane, f, acc);
-        }
-    }
-};
-
-// ---------------------------------------------------------------------------
-// second layer on an accumulator-layout operand X (32 hidden rows per tile t in
-// registers, point/ray on the lane):  out^T (32 dims x 32 points) = W[dt] . X
-// ---------------------------------------------------------------------------
-template <int DT> struct Layer2;
-template <> struct Layer2<SD_BF16> {
-    // A fragments: [dt][t][s][lane][8] bf16
-    static __device__ __forceinline__ f32x16 run(const bf16x8 *__restrict__ w, int dt,
-                                                 const f32x16 X[4], int lane) {
-        f32x16 acc = {};
+    // w_out: [dt][t][lane][16] f32;  out += X^T . W_out^T[dt]
+    static __device__ __forceinline__ void mma2(const uint8_t *w_out, int dt, const f32x16 X[4],
+                                                int lane, f32x16 &out) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
+            const f32x4 *wp = (const f32x4 *)w_out + ((int64_t)(dt * 4 + t) * SD_WAVE + lane) * 4;
 #pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                bf16x8 b;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) b[j] = (__bf16)X[t][8 * s + j];
-                bf16x8 a = w[((dt * 4 + t) * 2 + s) * SD_WAVE + lane];
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
-            }
-        }
-        return acc;
-    }
-};
-template <> struct Layer2<SD_F32> {
-    // A values: [dt][t][lane][16] f32
-    static __device__ __forceinline__ f32x16 run(const float *__restrict__ w, int dt,
-                                                 const f32x16 X[4], int lane) {
-        f32x16 acc = {};
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const f32x4 *wp = (const f32x4 *)(w + ((int64_t)(dt * 4 + t) * SD_WAVE + lane) * 16);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                f32x4 a = wp[q];
+            for (int q4 = 0; q4 < 4; ++q4) {
+                f32x4 b = wp[q4];
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
-                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], X[t][4 * q + i], acc, 0, 0, 0);
+                    out = __builtin_amdgcn_mfma_f32_32x32x2f32(X[t][4 * q4 + i], b[i], out, 0, 0, 0);
             }
         }
-        return acc;
     }
 };
 
-// relu(acc + b_in) in place; returns this lane's half of w_sigma . h
-__device__ __forceinline__ float sd_bias_relu_sigma(f32x16 acc[4], const float *lds_b,
-                                                    const float *lds_ws, int h) {
-    float s = 0.f;
+// An opaque zero: indexing LDS with it stops LICM from hoisting the per-sub-tile
+// weight reads out of the loop (which would pin ~100 VGPRs and spill).
+__device__ __forceinline__ int sd_opaque0() {
+    int z = 0;
+    asm volatile("" : "+v"(z));
+    return z;
+}
+
+// First layer over all C/16 grid chunks + 3 code chunks, with a 2-deep tap-load
+// pipeline (C % 32 == 0).  acc must hold the initial accumulator (b_in).
+template <int P>
+__device__ __forceinline__ void sd_layer1(const typename Prec<P>::G *__restrict__ g, int C,
+                                          const PointGeo &geo, const uint8_t *lw, int lane,
+                                          f32x16 acc[4]) {
+    typedef Prec<P> Pr;
+    const int h = lane >> 5;
+    const int nq = C >> 4;
+    const int c0 = 8 * h;
+    typename Pr::Raw ra = Pr::load(g, geo.t, C, c0);
+    typename Pr::Raw rb = Pr::load(g, geo.t, C, c0 + 16);
+    for (int q = 0; q < nq; q += 2) {
+        typename Pr::Frag fa = Pr::blend(ra, geo.t);
+        ra = Pr::load(g, geo.t, C, c0 + 16 * min(q + 2, nq - 2));
+        Pr::mma1(lw, q, lane, fa, acc);
+        typename Pr::Frag fb = Pr::blend(rb, geo.t);
+        rb = Pr::load(g, geo.t, C, c0 + 16 * min(q + 3, nq - 1));
+        Pr::mma1(lw, q + 1, lane, fb, acc);
+    }
+#pragma unroll
+    for (int pc = 0; pc < SD_PE_CHUNKS; ++pc) {
+        float f[8];
+        sd_pe_chunk<Pr::FAST_PE>(geo.v, pc, h, f);
+        Pr::mma1(lw, nq + pc, lane, Pr::from_f(f), acc);
+    }
+}
+
+// acc <- b_in rows (initial accumulator), from LDS [t][h][16]
+__device__ __forceinline__ void sd_init_bias(f32x16 acc[4], const float *lds_b, int h) {
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
         const f32x4 *bb = (const f32x4 *)(lds_b + (t * 2 + h) * 16);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            f32x4 b = bb[q];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[t][4 * q + i] = b[i];
+        }
+    }
+}
+
+// ReLU in place; returns this lane half's part of w_sigma . h
+__device__ __forceinline__ float sd_relu_sigma(f32x16 acc[4], const float *lds_ws, int h) {
+    float s = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
         const f32x4 *ww = (const f32x4 *)(lds_ws + (t * 2 + h) * 16);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            f32x4 b = bb[q], w = ww[q];
+            f32x4 w = ww[q];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                float v = fmaxf(acc[t][4 * q + i] + b[i], 0.f);
+                float v = fmaxf(acc[t][4 * q + i], 0.f);
                 acc[t][4 * q + i] = v;
                 s = fmaf(v, w[i], s);
             }
@@ -291,7 +359,6 @@ __device__ __forceinline__ float sd_bias_relu_sigma(f32x16 acc[4], const float *
 // torch.nn.functional.softplus(beta=1, threshold=20)
 __device__ __forceinline__ float sd_softplus(float x) { return x > 20.f ? x : log1pf(expf(x)); }
 
-// bilinear sample of an NHWC4 colour image (grid_sample, border, align_corners=False)
 __device__ __forceinline__ void sd_sample_rgb(const float *__restrict__ img, const Taps &t,
                                               float out[3]) {
     f32x4 a = *(const f32x4 *)(img + (int64_t)t.i00 * 4);
@@ -303,20 +370,34 @@ __device__ __forceinline__ void sd_sample_rgb(const float *__restrict__ img, con
         out[i] = ((a[i] * t.w00 + b[i] * t.w01) + c[i] * t.w10) + d[i] * t.w11;
 }
 
-// Stage W_in fragments + bias / sigma rows into LDS (one pass per workgroup).
-// An opaque zero: indexing LDS with it stops LICM from hoisting the per-sample
-// weight reads out of the sample loop (which would pin ~100 VGPRs and spill).
-__device__ __forceinline__ int sd_opaque0() {
-    int z = 0;
-    asm volatile("" : "+v"(z));
-    return z;
+// colour sample + validity in a render view (bts.py:336-346; clamp before the frustum test)
+__device__ __forceinline__ bool sd_color_view(const float *cam, const float *img, int Wc, int Hc,
+                                              float px, float py, float pz, float col[3]) {
+    float x, y, zc;
+    sd_project(cam, px, py, pz, x, y, zc);
+    x = fminf(fmaxf(x, -2.f), 2.f);
+    y = fminf(fmaxf(y, -2.f), 2.f);
+    bool inv = sd_outside(x, y, zc);
+    Taps tc = sd_taps(x, y, Wc, Hc);
+    sd_sample_rgb(img, tc, col);
+    return inv;
 }
 
-__device__ __forceinline__ void sd_stage_weights(uint8_t *lds, const sd_mlp &m, int win_bytes) {
+// LDS image: [W_in fragments | W_out fragments (if they fit) | b_in rows | w_sigma rows]
+struct LdsPlan {
+    int win_bytes, wout_bytes, wout_in_lds, total;
+};
+
+__device__ __forceinline__ void sd_stage(uint8_t *lds, const sd_mlp &m, const LdsPlan &pl) {
     const uint4 *src = (const uint4 *)m.w_in;
     uint4 *dst = (uint4 *)lds;
-    for (int i = threadIdx.x; i < win_bytes / 16; i += blockDim.x) dst[i] = src[i];
-    float *fb = (float *)(lds + win_bytes);
+    for (int i = threadIdx.x; i < pl.win_bytes / 16; i += blockDim.x) dst[i] = src[i];
+    if (pl.wout_in_lds) {
+        const uint4 *s2 = (const uint4 *)m.w_out;
+        uint4 *d2 = (uint4 *)(lds + pl.win_bytes);
+        for (int i = threadIdx.x; i < pl.wout_bytes / 16; i += blockDim.x) d2[i] = s2[i];
+    }
+    float *fb = (float *)(lds + pl.win_bytes + (pl.wout_in_lds ? pl.wout_bytes : 0));
     for (int i = threadIdx.x; i < 128; i += blockDim.x) {
         fb[i] = m.b_in_h[i];
         fb[128 + i] = m.w_sig_h[i];
@@ -325,29 +406,27 @@ __device__ __forceinline__ void sd_stage_weights(uint8_t *lds, const sd_mlp &m, 
 }
 
 // ---------------------------------------------------------------------------
-// fused render kernel
+// fused render: one wave per ray at a time, K/32 sub-tiles of 32 samples
 // ---------------------------------------------------------------------------
-template <int DT, bool FAST_PE>
-__global__ void __launch_bounds__(256, DT == SD_BF16 ? 2 : 1)
-k_render(const sd_render_args a, const sd_mlp m, int win_bytes) {
+template <int P, int NV, int NDT>
+__global__ void __launch_bounds__(SD_WG, 1)
+k_render(const sd_render_args a, const sd_mlp m, const LdsPlan pl) {
+    typedef typename Prec<P>::G G;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    typedef typename GridT<DT>::T G;
-    sd_stage_weights(lds, m, win_bytes);
-    const float *lds_b = (const float *)(lds + win_bytes);
+    sd_stage(lds, m, pl);
+    const uint8_t *wout_base = pl.wout_in_lds ? lds + pl.win_bytes : (const uint8_t *)m.w_out;
+    const float *lds_b = (const float *)(lds + pl.win_bytes + (pl.wout_in_lds ? pl.wout_bytes : 0));
     const float *lds_ws = lds_b + 128;
 
-    const int lane = threadIdx.x & 63, h = lane >> 5;
+    const int lane = threadIdx.x & 63, h = lane >> 5, li = lane & 31;
     const int wave = threadIdx.x >> 6;
-    const int64_t ntiles = (a.R + 31) / 32;
-    const int K = a.K, C = m.C, nv = a.nv;
+    const int K = a.K, C = m.C, nv = NV > 0 ? NV : a.nv;
+    const int nsub = K >> 5;
     const int64_t plane = (int64_t)a.Hf * a.Wf * C;
     const int64_t cplane = (int64_t)a.Hc * a.Wc * 4;
+    const int64_t nwaves = (int64_t)gridDim.x * SD_WAVES;
 
-    for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile < ntiles;
-         tile += (int64_t)gridDim.x * 4) {
-        const int64_t ray_u = tile * 32 + (lane & 31);
-        const bool valid = ray_u < a.R;
-        const int64_t ray = valid ? ray_u : a.R - 1;
+    for (int64_t ray = (int64_t)blockIdx.x * SD_WAVES + wave; ray < a.R; ray += nwaves) {
         const int64_t sbi = ray / a.rays_per_sb;
         const float *rr = a.rays + ray * a.ray_dim;
         const float ox = rr[0], oy = rr[1], oz = rr[2], dx = rr[3], dy = rr[4], dz = rr[5];
@@ -355,114 +434,119 @@ k_render(const sd_render_args a, const sd_mlp m, int win_bytes) {
         const G *grid = (const G *)a.grid + sbi * plane;
         const float *camf = a.cam_f + sbi * 21;
 
-        f32x16 hacc[4];
+        // dacc[dt]: sum over samples of (w h)^T W_out^T in O layout (D = 32 NDT)
+        f32x16 dacc[NDT];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) hacc[t] = f32x16{};
-        float T = 1.f, wsum = 0.f, depth = 0.f;
-        float rgbacc[3 * SD_MAX_NV];
+        for (int i = 0; i < NDT; ++i) dacc[i] = f32x16{};
+        float Tc = 1.f, dpart = 0.f, wpart = 0.f;
+        float cpart[3 * SD_MAX_NV];
 #pragma unroll
-        for (int i = 0; i < 3 * SD_MAX_NV; ++i) rgbacc[i] = 0.f;
+        for (int i = 0; i < 3 * SD_MAX_NV; ++i) cpart[i] = 0.f;
 
-        float zk = zr[0];
-        for (int k = 0; k < K; ++k) {
-            const float zn = (k + 1 < K) ? zr[k + 1] : 0.f;
-            const float delta = (k + 1 < K) ? (zn - zk) : 1e10f;
-            // points = o + z*d (nerf.py:252)
-            const float px = ox + zk * dx, py = oy + zk * dy, pz = oz + zk * dz;
+        for (int sub = 0; sub < nsub; ++sub) {
+            const int k = sub * 32 + li;
+            const float zk = zr[k];
+            const float delta = (k + 1 < K) ? (zr[min(k + 1, K - 1)] - zk) : 1e10f;
+            const float px = ox + zk * dx, py = oy + zk * dy, pz = oz + zk * dz;  // nerf.py:252
             PointGeo geo = sd_point_geo(camf, px, py, pz, a.Wf, a.Hf);
 
-            f32x16 acc[4];
-#pragma unroll
-            for (int t = 0; t < 4; ++t) acc[t] = f32x16{};
             const int lo = sd_opaque0();
-            Layer1<DT>::template run<FAST_PE>(grid, C, geo, lds + lo, lane, acc);
-
-            float s = sd_bias_relu_sigma(acc, lds_b + lo, lds_ws + lo, h);
+            f32x16 acc[4];
+            sd_init_bias(acc, lds_b + lo, h);
+            sd_layer1<P>(grid, C, geo, lds + lo, lane, acc);
+            float s = sd_relu_sigma(acc, lds_ws + lo, h);
             s += __shfl_xor(s, 32);
             const float sigma = sd_softplus(s + m.b_sigma);
 
-            // alpha compositing (nerf.py:376-389)
+            // alpha compositing (nerf.py:376-389); transmittance = prefix product
             float alpha = 1.f - expf(-fabsf(delta) * fmaxf(sigma, 0.f));
             if (a.hard_alpha_cap && k == K - 1) alpha = 1.f;
-            const float w = alpha * T;
-            T = T * ((1.f - alpha) + 1e-10f);
-            wsum += w;
-            depth += w * zk;
+            const float tk = (1.f - alpha) + 1e-10f;
+            float incl = tk;
+#pragma unroll
+            for (int d = 1; d < 32; d <<= 1) {
+                float v = __shfl_up(incl, d, 32);
+                if (li >= d) incl *= v;
+            }
+            float excl = __shfl_up(incl, 1, 32);
+            if (li == 0) excl = 1.f;
+            const float w = alpha * (Tc * excl);
+            Tc *= __shfl(incl, 31, 32);
+            dpart += w * zk;
+            wpart += w;
+
+            // colours (bts.py:330-441)
+            float col[3 * SD_MAX_NV];
+            bool invc[SD_MAX_NV];
+#pragma unroll
+            for (int v = 0; v < SD_MAX_NV; ++v) {
+                invc[v] = false;
+                col[3 * v] = col[3 * v + 1] = col[3 * v + 2] = 0.f;
+                if (v < nv) {
+                    invc[v] = sd_color_view(a.cam_c + (sbi * nv + v) * 21, a.img + (sbi * nv + v) * cplane,
+                                            a.Wc, a.Hc, px, py, pz, col + 3 * v);
+                    cpart[3 * v] += w * col[3 * v];
+                    cpart[3 * v + 1] += w * col[3 * v + 1];
+                    cpart[3 * v + 2] += w * col[3 * v + 2];
+                }
+            }
+
+            // DINO head folded into the compositing sum: dacc += (w h)^T W_out^T
 #pragma unroll
             for (int t = 0; t < 4; ++t)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) hacc[t][r] = fmaf(w, acc[t][r], hacc[t][r]);
-
-            // colours in the render views (bts.py:330-441)
-            bool inv_any_c[SD_MAX_NV];
-            float col[3 * SD_MAX_NV];
+                for (int r = 0; r < 16; ++r) acc[t][r] *= w;
+            const uint8_t *wo = wout_base + (pl.wout_in_lds ? lo : 0);
 #pragma unroll
-            for (int v = 0; v < SD_MAX_NV; ++v) {
-                inv_any_c[v] = false;
-                col[3 * v] = col[3 * v + 1] = col[3 * v + 2] = 0.f;
-                if (v < nv) {
-                    float x, y, zc;
-                    sd_project(a.cam_c + (sbi * nv + v) * 21, px, py, pz, x, y, zc);
-                    x = fminf(fmaxf(x, -2.f), 2.f);
-                    y = fminf(fmaxf(y, -2.f), 2.f);
-                    inv_any_c[v] = sd_outside(x, y, zc);
-                    Taps tc = sd_taps(x, y, a.Wc, a.Hc);
-                    sd_sample_rgb(a.img + (sbi * nv + v) * cplane, tc, col + 3 * v);
-                    rgbacc[3 * v] += w * col[3 * v];
-                    rgbacc[3 * v + 1] += w * col[3 * v + 1];
-                    rgbacc[3 * v + 2] += w * col[3 * v + 2];
-                }
-            }
+            for (int dt = 0; dt < NDT; ++dt) Prec<P>::mma2(wo, dt, acc, lane, dacc[dt]);
 
-            if (valid) {
-                const int64_t o = ray * K + k;
-                if (h == 0) {
-                    if (a.weights) a.weights[o] = w;
-                    if (a.alphas) a.alphas[o] = alpha;
-                    if (a.invalid_f) a.invalid_f[o] = geo.inv_f ? 1 : 0;
-                } else {
+            // per-sample outputs, coalesced along the ray
+            const int64_t o = ray * K + k;
+            if (h == 0) {
+                if (a.weights) a.weights[o] = w;
+                if (a.alphas) a.alphas[o] = alpha;
+                if (a.invalid_f) a.invalid_f[o] = geo.inv_f ? 1 : 0;
+            } else {
 #pragma unroll
-                    for (int v = 0; v < SD_MAX_NV; ++v) {
-                        if (v < nv) {
-                            if (a.invalid) a.invalid[o * nv + v] = (inv_any_c[v] | geo.inv_f) ? 1.f : 0.f;
-                            if (a.rgb_samps) {
-                                a.rgb_samps[(o * nv + v) * 3] = col[3 * v];
-                                a.rgb_samps[(o * nv + v) * 3 + 1] = col[3 * v + 1];
-                                a.rgb_samps[(o * nv + v) * 3 + 2] = col[3 * v + 2];
-                            }
+                for (int v = 0; v < SD_MAX_NV; ++v)
+                    if (v < nv) {
+                        if (a.invalid) a.invalid[o * nv + v] = (invc[v] | geo.inv_f) ? 1.f : 0.f;
+                        if (a.rgb_samps) {
+                            float *rs = a.rgb_samps + (o * nv + v) * 3;
+                            rs[0] = col[3 * v]; rs[1] = col[3 * v + 1]; rs[2] = col[3 * v + 2];
                         }
                     }
-                }
             }
-            zk = zn;
         }
 
-        // DINO head on the accumulated hidden state: dino = W_out Hacc + wsum * b
-        const int ndt = m.D >> 5;
-        for (int dt = 0; dt < ndt; ++dt) {
-            f32x16 o = Layer2<DT>::run((const typename std::conditional<DT == SD_BF16, bf16x8, float>::type *)m.w_out,
-                                       dt, hacc, lane);
-            if (valid) {
+        // ray epilogue: reduce the per-lane partial sums over the 32 lanes of a half
 #pragma unroll
-                for (int g4 = 0; g4 < 4; ++g4) {
-                    int dim = dt * 32 + 8 * g4 + 4 * h;
-                    f32x4 bb = *(const f32x4 *)(m.b_dino + dim);
-                    f32x4 val;
+        for (int d = 1; d < 32; d <<= 1) {
+            dpart += __shfl_xor(dpart, d);
+            wpart += __shfl_xor(wpart, d);
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) val[i] = o[4 * g4 + i] + wsum * bb[i];
-                    *(f32x4 *)(a.dino + ray * m.D + dim) = val;
-                }
+            for (int i = 0; i < 3 * SD_MAX_NV; ++i)
+                if (i < 3 * nv) cpart[i] += __shfl_xor(cpart[i], d);
+        }
+        // dino[dim] = sum over rows of dacc (+ other half) + wsum * b
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+            float sacc = 0.f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sacc += dacc[dt][r];
+            sacc += __shfl_xor(sacc, 32);
+            if ((dt & 1) == h) {
+                const int dim = dt * 32 + li;
+                a.dino[ray * m.D + dim] = sacc + wpart * m.b_dino[dim];
             }
         }
-        if (valid && h == 0) {
-            a.depth[ray] = depth;
+        if (lane == 0) a.depth[ray] = dpart;
+        if (lane < 3 * nv) {
+            float cv = 0.f;
 #pragma unroll
-            for (int v = 0; v < SD_MAX_NV; ++v)
-                if (v < nv) {
-                    a.rgb[ray * 3 * nv + 3 * v] = rgbacc[3 * v];
-                    a.rgb[ray * 3 * nv + 3 * v + 1] = rgbacc[3 * v + 1];
-                    a.rgb[ray * 3 * nv + 3 * v + 2] = rgbacc[3 * v + 2];
-                }
+            for (int i = 0; i < 3 * SD_MAX_NV; ++i)
+                if (i == lane) cv = cpart[i];
+            a.rgb[ray * 3 * nv + lane] = cv;
         }
     }
 }
@@ -470,26 +554,28 @@ k_render(const sd_render_args a, const sd_mlp m, int win_bytes) {
 // ---------------------------------------------------------------------------
 // per-point field query (no compositing): 32 consecutive points per wave step
 // ---------------------------------------------------------------------------
-template <int DT, bool FAST_PE>
-__global__ void __launch_bounds__(256, DT == SD_BF16 ? 2 : 1)
-k_field(const sd_field_args a, const sd_mlp m, int win_bytes) {
+template <int P>
+__global__ void __launch_bounds__(SD_WG, 1)
+k_field(const sd_field_args a, const sd_mlp m, const LdsPlan pl) {
+    typedef typename Prec<P>::G G;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    typedef typename GridT<DT>::T G;
-    sd_stage_weights(lds, m, win_bytes);
-    const float *lds_b = (const float *)(lds + win_bytes);
+    sd_stage(lds, m, pl);
+    const uint8_t *wout_base = pl.wout_in_lds ? lds + pl.win_bytes : (const uint8_t *)m.w_out;
+    const float *lds_b = (const float *)(lds + pl.win_bytes + (pl.wout_in_lds ? pl.wout_bytes : 0));
     const float *lds_ws = lds_b + 128;
 
-    const int lane = threadIdx.x & 63, h = lane >> 5;
+    const int lane = threadIdx.x & 63, h = lane >> 5, li = lane & 31;
     const int wave = threadIdx.x >> 6;
     const int64_t NP = a.B * a.P;
     const int64_t ntiles = (NP + 31) / 32;
     const int C = m.C, nv = a.nv;
+    const int ndt = m.D >> 5;
     const int64_t plane = (int64_t)a.Hf * a.Wf * C;
     const int64_t cplane = (int64_t)a.Hc * a.Wc * 4;
 
-    for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile < ntiles;
-         tile += (int64_t)gridDim.x * 4) {
-        const int64_t pu = tile * 32 + (lane & 31);
+    for (int64_t tile = (int64_t)blockIdx.x * SD_WAVES + wave; tile < ntiles;
+         tile += (int64_t)gridDim.x * SD_WAVES) {
+        const int64_t pu = tile * 32 + li;
         const bool valid = pu < NP;
         const int64_t p = valid ? pu : NP - 1;
         const int64_t b = p / a.P;
@@ -497,29 +583,25 @@ k_field(const sd_field_args a, const sd_mlp m, int win_bytes) {
         const G *grid = (const G *)a.grid + b * plane;
         PointGeo geo = sd_point_geo(a.cam_f + b * 21, px, py, pz, a.Wf, a.Hf);
 
-        f32x16 acc[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) acc[t] = f32x16{};
         const int lo = sd_opaque0();
-        Layer1<DT>::template run<FAST_PE>(grid, C, geo, lds + lo, lane, acc);
-        float s = sd_bias_relu_sigma(acc, lds_b + lo, lds_ws + lo, h);
+        f32x16 acc[4];
+        sd_init_bias(acc, lds_b + lo, h);
+        sd_layer1<P>(grid, C, geo, lds + lo, lane, acc);
+        float s = sd_relu_sigma(acc, lds_ws + lo, h);
         s += __shfl_xor(s, 32);
         const float sigma = sd_softplus(s + m.b_sigma);
 
-        const int ndt = m.D >> 5;
+        const uint8_t *wo = wout_base + (pl.wout_in_lds ? lo : 0);
         for (int dt = 0; dt < ndt; ++dt) {
-            f32x16 o = Layer2<DT>::run((const typename std::conditional<DT == SD_BF16, bf16x8, float>::type *)m.w_out,
-                                       dt, acc, lane);
-            if (valid) {
+            f32x16 o = {};
+            Prec<P>::mma2(wo, dt, acc, lane, o);
+            // O layout: row = point (r&3)+8(r>>2)+4h of this tile, column = dim li
+            const int dim = dt * 32 + li;
+            const float bd = m.b_dino[dim];
 #pragma unroll
-                for (int g4 = 0; g4 < 4; ++g4) {
-                    int dim = dt * 32 + 8 * g4 + 4 * h;
-                    f32x4 bb = *(const f32x4 *)(m.b_dino + dim);
-                    f32x4 val;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) val[i] = o[4 * g4 + i] + bb[i];
-                    *(f32x4 *)(a.dino + p * m.D + dim) = val;
-                }
+            for (int r = 0; r < 16; ++r) {
+                const int64_t pr = tile * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (pr < NP) a.dino[pr * m.D + dim] = o[r] + bd;
             }
         }
         if (valid && h == 0) {
@@ -527,30 +609,23 @@ k_field(const sd_field_args a, const sd_mlp m, int win_bytes) {
             if (a.invalid_f) a.invalid_f[p] = geo.inv_f ? 1 : 0;
         }
         if (valid && h == 1 && nv > 0 && (a.rgb || a.invalid)) {
-#pragma unroll
-            for (int v = 0; v < SD_MAX_NV; ++v) {
-                if (v < nv) {
-                    float x, y, zc, col[3];
-                    sd_project(a.cam_c + (b * nv + v) * 21, px, py, pz, x, y, zc);
-                    x = fminf(fmaxf(x, -2.f), 2.f);
-                    y = fminf(fmaxf(y, -2.f), 2.f);
-                    bool ic = sd_outside(x, y, zc);
-                    Taps tc = sd_taps(x, y, a.Wc, a.Hc);
-                    sd_sample_rgb(a.img + (b * nv + v) * cplane, tc, col);
-                    if (a.rgb) {
-                        a.rgb[(p * nv + v) * 3] = col[0];
-                        a.rgb[(p * nv + v) * 3 + 1] = col[1];
-                        a.rgb[(p * nv + v) * 3 + 2] = col[2];
-                    }
-                    if (a.invalid) a.invalid[p * nv + v] = (ic | geo.inv_f) ? 1.f : 0.f;
+            for (int v = 0; v < nv; ++v) {
+                float col[3];
+                bool ic = sd_color_view(a.cam_c + (b * nv + v) * 21, a.img + (b * nv + v) * cplane,
+                                        a.Wc, a.Hc, px, py, pz, col);
+                if (a.rgb) {
+                    a.rgb[(p * nv + v) * 3] = col[0];
+                    a.rgb[(p * nv + v) * 3 + 1] = col[1];
+                    a.rgb[(p * nv + v) * 3 + 2] = col[2];
                 }
+                if (a.invalid) a.invalid[p * nv + v] = (ic | geo.inv_f) ? 1.f : 0.f;
             }
         }
     }
 }
 
 // ---------------------------------------------------------------------------
-// standalone compositor: one wave per ray, lane = feature column
+// standalone compositor: one wave per ray, lane = feature column (sequential in k)
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256)
 k_composite(const float *__restrict__ z, const float *__restrict__ sigma,
@@ -609,64 +684,36 @@ static int sd_num_cus() {
     return n;
 }
 
-static int sd_check_mlp(const sd_mlp *m, int *win_bytes, int *lds_bytes) {
+static int sd_plan(const sd_mlp *m, LdsPlan *pl) {
     if (!m || !m->w_in || !m->b_in_h || !m->w_sig_h || !m->w_out || !m->b_dino) {
         sd_set_error("sd_mlp: null parameter pointer");
         return -1;
     }
-    if (m->d_hidden != SD_DH || m->C <= 0 || (m->C % 16) || m->D <= 0 || (m->D % 32) ||
-        (m->dtype != SD_BF16 && m->dtype != SD_F32)) {
-        sd_set_error("sd_mlp: unsupported shape (need d_hidden=128, C%16==0, D%32==0)");
+    if (m->d_hidden != SD_DH || m->C <= 0 || (m->C % 32) || m->D <= 0 || (m->D % 32) ||
+        (m->dtype != SD_BF16 && m->dtype != SD_F32 && m->dtype != SD_F16)) {
+        sd_set_error("sd_mlp: unsupported shape (need d_hidden=128, C%32==0, D%32==0)");
         return -1;
     }
     int nq = m->C / 16 + SD_PE_CHUNKS;
-    int esz = m->dtype == SD_BF16 ? 2 : 4;
-    *win_bytes = nq * 4 * SD_WAVE * 8 * esz;
-    *lds_bytes = *win_bytes + 256 * 4;
-    if (*lds_bytes > 160 * 1024) {
-        sd_set_error("sd_mlp: W_in fragments exceed LDS (reduce C or use bf16)");
+    int esz = m->dtype == SD_F32 ? 4 : 2;
+    pl->win_bytes = nq * 4 * SD_WAVE * 8 * esz;
+    pl->wout_bytes = (m->D / 32) * 4 * SD_WAVE * (m->dtype == SD_F32 ? 64 : 32);
+    int rest = 256 * 4;
+    pl->wout_in_lds = (pl->win_bytes + pl->wout_bytes + rest) <= 160 * 1024;
+    pl->total = pl->win_bytes + (pl->wout_in_lds ? pl->wout_bytes : 0) + rest;
+    if (pl->total > 160 * 1024) {
+        sd_set_error("sd_mlp: W_in fragments exceed LDS (reduce C or use a 16-bit dtype)");
         return -1;
     }
     return 0;
 }
 
-#define SD_LAUNCH_FIELD(KERN, DT, GRID, LDS, STREAM, ...)                                    \
-    do {                                                                                     \
-        static bool attr_set_##KERN##DT = false;                                             \
-        if (!attr_set_##KERN##DT) {                                                          \
-            (void)hipFuncSetAttribute((const void *)KERN<DT, SD_FASTPE>,                               \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS > 65536 ? 163840 : 65536); \
-            attr_set_##KERN##DT = true;                                                      \
-        }                                                                                    \
-        hipLaunchKernelGGL((KERN<DT, SD_FASTPE>), GRID, dim3(256), LDS, STREAM, __VA_ARGS__);    \
-    } while (0)
-
-extern "C" int sd_render_fused(const sd_render_args *args, const sd_mlp *mlp, void *stream) {
-    int win = 0, lds = 0;
-    if (!args) {
-        sd_set_error("sd_render_fused: null args");
-        return -1;
-    }
-    if (sd_check_mlp(mlp, &win, &lds)) return -1;
-    const sd_render_args &a = *args;
-    if (a.R < 0 || a.K <= 0 || a.ray_dim < 6 || a.rays_per_sb <= 0 || !a.rays || !a.z ||
-        !a.grid || !a.cam_f || !a.depth || !a.dino || a.Hf <= 0 || a.Wf <= 0 || a.nv < 0 ||
-        a.nv > SD_MAX_NV || (a.nv > 0 && (!a.img || !a.cam_c || !a.rgb || a.Hc <= 0 || a.Wc <= 0))) {
-        sd_set_error("sd_render_fused: invalid argument (nv must be 0..4)");
-        return -1;
-    }
-    if (a.R == 0) return 0;
-    int64_t ntiles = (a.R + 31) / 32;
-    int per_cu = mlp->dtype == SD_BF16 ? 2 : 1;
-    int64_t nblk = (ntiles + 3) / 4;
-    int64_t cap = (int64_t)sd_num_cus() * per_cu;
-    if (nblk > cap) nblk = cap;
-    dim3 grid((unsigned)nblk);
-    hipStream_t s = (hipStream_t)stream;
-    if (mlp->dtype == SD_BF16)
-        SD_LAUNCH_FIELD(k_render, SD_BF16, grid, lds, s, a, *mlp, win);
-    else
-        SD_LAUNCH_FIELD(k_render, SD_F32, grid, lds, s, a, *mlp, win);
+template <typename KernT, typename ArgT>
+static int sd_launch(KernT kern, int nblk, const LdsPlan &pl, hipStream_t s, const ArgT &a,
+                     const sd_mlp &m) {
+    (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    hipLaunchKernelGGL(kern, dim3(nblk), dim3(SD_WG), pl.total, s, a, m, pl);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         sd_set_error(hipGetErrorString(e));
@@ -675,13 +722,61 @@ extern "C" int sd_render_fused(const sd_render_args *args, const sd_mlp *mlp, vo
     return 0;
 }
 
+template <int P, int NV>
+static int sd_render_ndt(const sd_render_args &a, const sd_mlp &m, const LdsPlan &pl, int nblk,
+                         hipStream_t s) {
+    switch (m.D / 32) {
+        case 1: return sd_launch(k_render<P, NV, 1>, nblk, pl, s, a, m);
+        case 2: return sd_launch(k_render<P, NV, 2>, nblk, pl, s, a, m);
+        case 4: return sd_launch(k_render<P, NV, 4>, nblk, pl, s, a, m);
+        default:
+            sd_set_error("sd_render_fused: D must be 32, 64 or 128 (use sd_field_query + sd_composite)");
+            return -1;
+    }
+}
+
+template <int P>
+static int sd_render_nv(const sd_render_args &a, const sd_mlp &m, const LdsPlan &pl, int nblk,
+                        hipStream_t s) {
+    return a.nv == 1 ? sd_render_ndt<P, 1>(a, m, pl, nblk, s) : sd_render_ndt<P, 0>(a, m, pl, nblk, s);
+}
+
+static int sd_render_dispatch(const sd_render_args &a, const sd_mlp &m, const LdsPlan &pl,
+                              int nblk, hipStream_t s) {
+    if (m.dtype == SD_F16) return sd_render_nv<SD_F16>(a, m, pl, nblk, s);
+    if (m.dtype == SD_BF16) return sd_render_nv<SD_BF16>(a, m, pl, nblk, s);
+    return sd_render_nv<SD_F32>(a, m, pl, nblk, s);
+}
+
+extern "C" int sd_render_fused(const sd_render_args *args, const sd_mlp *mlp, void *stream) {
+    LdsPlan pl;
+    if (!args) {
+        sd_set_error("sd_render_fused: null args");
+        return -1;
+    }
+    if (sd_plan(mlp, &pl)) return -1;
+    const sd_render_args &a = *args;
+    if (a.R < 0 || a.K <= 0 || (a.K % 32) || a.ray_dim < 6 || a.rays_per_sb <= 0 || !a.rays ||
+        !a.z || !a.grid || !a.cam_f || !a.depth || !a.dino || a.Hf <= 0 || a.Wf <= 0 ||
+        a.nv < 0 || a.nv > SD_MAX_NV || mlp->D > 128 ||
+        (a.nv > 0 && (!a.img || !a.cam_c || !a.rgb || a.Hc <= 0 || a.Wc <= 0))) {
+        sd_set_error("sd_render_fused: invalid argument (K % 32 == 0, nv <= 4, D <= 128)");
+        return -1;
+    }
+    if (a.R == 0) return 0;
+    int64_t nblk = (a.R + SD_WAVES - 1) / SD_WAVES;
+    if (nblk > sd_num_cus()) nblk = sd_num_cus();
+    hipStream_t s = (hipStream_t)stream;
+    return sd_render_dispatch(a, *mlp, pl, (int)nblk, s);
+}
+
 extern "C" int sd_field_query(const sd_field_args *args, const sd_mlp *mlp, void *stream) {
-    int win = 0, lds = 0;
+    LdsPlan pl;
     if (!args) {
         sd_set_error("sd_field_query: null args");
         return -1;
     }
-    if (sd_check_mlp(mlp, &win, &lds)) return -1;
+    if (sd_plan(mlp, &pl)) return -1;
     const sd_field_args &a = *args;
     if (a.B <= 0 || a.P < 0 || !a.xyz || !a.grid || !a.cam_f || !a.sigma || !a.dino ||
         a.Hf <= 0 || a.Wf <= 0 || a.nv < 0 || a.nv > SD_MAX_NV ||
@@ -691,22 +786,12 @@ extern "C" int sd_field_query(const sd_field_args *args, const sd_mlp *mlp, void
     }
     if (a.P == 0) return 0;
     int64_t ntiles = (a.B * a.P + 31) / 32;
-    int per_cu = mlp->dtype == SD_BF16 ? 2 : 1;
-    int64_t nblk = (ntiles + 3) / 4;
-    int64_t cap = (int64_t)sd_num_cus() * per_cu * 4;
-    if (nblk > cap) nblk = cap;
-    dim3 grid((unsigned)nblk);
+    int64_t nblk = (ntiles + SD_WAVES - 1) / SD_WAVES;
+    if (nblk > sd_num_cus()) nblk = sd_num_cus();
     hipStream_t s = (hipStream_t)stream;
-    if (mlp->dtype == SD_BF16)
-        SD_LAUNCH_FIELD(k_field, SD_BF16, grid, lds, s, a, *mlp, win);
-    else
-        SD_LAUNCH_FIELD(k_field, SD_F32, grid, lds, s, a, *mlp, win);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) {
-        sd_set_error(hipGetErrorString(e));
-        return -2;
-    }
-    return 0;
+    if (mlp->dtype == SD_F16) return sd_launch(k_field<SD_F16>, (int)nblk, pl, s, a, *mlp);
+    if (mlp->dtype == SD_BF16) return sd_launch(k_field<SD_BF16>, (int)nblk, pl, s, a, *mlp);
+    return sd_launch(k_field<SD_F32>, (int)nblk, pl, s, a, *mlp);
 }
 
 extern "C" int sd_composite(const float *z, const float *sigma, const float *feat, int64_t F,

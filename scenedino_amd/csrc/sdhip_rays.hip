@@ -85,6 +85,8 @@ __global__ void __launch_bounds__(256) k_pack_grid(const float *__restrict__ in,
             float v = tile[tx][j];
             if (DT == SD_BF16)
                 ((__bf16 *)out)[o] = (__bf16)v;
+            else if (DT == SD_F16)
+                ((_Float16 *)out)[o] = (_Float16)v;
             else
                 ((float *)out)[o] = v;
         }
@@ -154,13 +156,16 @@ extern "C" int sd_sample_z(const float *rays, int64_t R, int64_t ray_dim, int64_
 extern "C" int sd_pack_grid(const float *grid_nchw, int64_t B, int64_t C, int64_t H, int64_t W,
                             int dtype, void *out_nhwc, void *stream) {
     if (!grid_nchw || !out_nhwc || B <= 0 || C <= 0 || H <= 0 || W <= 0 ||
-        (dtype != SD_F32 && dtype != SD_BF16) || B * H > 2147483647LL) {
+        (dtype != SD_F32 && dtype != SD_BF16 && dtype != SD_F16) || B * H > 2147483647LL) {
         sd_set_error("sd_pack_grid: invalid argument");
         return -1;
     }
     dim3 g((unsigned)((W + 31) / 32), (unsigned)((C + 31) / 32), (unsigned)(B * H));
     if (dtype == SD_BF16)
         hipLaunchKernelGGL(k_pack_grid<SD_BF16>, g, dim3(256), 0, (hipStream_t)stream, grid_nchw,
+                           C, H, W, out_nhwc);
+    else if (dtype == SD_F16)
+        hipLaunchKernelGGL(k_pack_grid<SD_F16>, g, dim3(256), 0, (hipStream_t)stream, grid_nchw,
                            C, H, W, out_nhwc);
     else
         hipLaunchKernelGGL(k_pack_grid<SD_F32>, g, dim3(256), 0, (hipStream_t)stream, grid_nchw,

@@ -105,21 +105,21 @@ class PackedMLP:
         dh, din = W_in.shape
         C = din - N_PE
         D = W_out.shape[0] - 1
-        if dh != D_HIDDEN or C <= 0 or C % 16 or D % 32 or W_out.shape[1] != dh:
+        if dh != D_HIDDEN or C <= 0 or C % 32 or D % 32 or W_out.shape[1] != dh:
             raise NotImplementedError(
-                f"fused field kernel needs d_hidden=128, C%16==0, D%32==0 (got W_in {tuple(W_in.shape)}, "
+                f"fused field kernel needs d_hidden=128, C%32==0, D%32==0 (got W_in {tuple(W_in.shape)}, "
                 f"W_out {tuple(W_out.shape)})")
         dev = W_in.device
         ix = {k: v.to(dev) for k, v in _index_tables(C, D).items()}
         Wz = torch.cat((W_in, torch.zeros(dh, 1, device=dev)), 1)  # column din = zero pad
         cols1 = torch.where(ix["cols1"] < 0, torch.full_like(ix["cols1"], din), ix["cols1"])
         w1 = Wz[ix["rows1"], cols1]
-        tdt = torch.bfloat16 if dtype == _lib.SD_BF16 else torch.float32
+        tdt = _lib.TORCH_DTYPE[dtype]
         self.w_in = w1.to(tdt).contiguous()
         self.b_in_h = b_in[ix["accrow"]].contiguous()
         self.w_sig_h = W_out[0][ix["accrow"]].contiguous()
-        if dtype == _lib.SD_BF16:
-            self.w_out = W_out[ix["rows2b"], ix["cols2b"]].to(torch.bfloat16).contiguous()
+        if dtype != _lib.SD_F32:
+            self.w_out = W_out[ix["rows2b"], ix["cols2b"]].to(tdt).contiguous()
         else:
             self.w_out = W_out[ix["rows2f"], ix["cols2f"]].contiguous()
         self.b_dino = b_out[1:].contiguous()

@@ -9,8 +9,9 @@ hand-written gfx950 kernels of libsdhip.so (``sd_field_query``; and, through
 ``render_fused``, the fused render+composite kernel ``sd_render_fused``).
 
 Precision: ``precision="bf16"`` (default; bf16 grid + bf16 MFMA, fp32 accumulate
-and fp32 geometry / compositing) or ``"fp32"`` (f32 grid + exact-f32 MFMA) for
-fp32-tolerance parity with the reference.  Set via ``conf["precision"]`` or
+and fp32 geometry / compositing), ``"fp16"`` (f16 grid, packed-f16 bilinear blend,
+f16 MFMA, fp32 accumulate -- the reference's own AMP dtype) or ``"fp32"`` (f32 grid
++ exact-f32 MFMA) for fp32-tolerance parity with the reference.  Set via ``conf["precision"]`` or
 ``net.set_precision``.
 """
 from __future__ import annotations
@@ -23,6 +24,7 @@ from .. import _lib
 from ..mlp_pack import PackedMLP, param_key
 
 EPS = 1e-3  # scenedino/common/cameras/pinhole.py:3
+PRECISIONS = {"fp32": _lib.SD_F32, "bf16": _lib.SD_BF16, "fp16": _lib.SD_F16}
 
 
 def _cam_records(poses_w2c, Ks):
@@ -88,8 +90,8 @@ class BTSNet(nn.Module):
         pass
 
     def set_precision(self, precision: str):
-        if precision not in ("bf16", "fp32"):
-            raise ValueError("precision must be 'bf16' or 'fp32'")
+        if precision not in PRECISIONS:
+            raise ValueError(f"precision must be one of {sorted(PRECISIONS)}")
         self.precision = precision
         self._packed = None
         self._grid_cache = None
@@ -149,7 +151,15 @@ class BTSNet(nn.Module):
 
     # -- device-side state for the kernels ------------------------------------
     def _dtype(self):
-        return _lib.SD_BF16 if self.precision == "bf16" else _lib.SD_F32
+        if self.precision not in PRECISIONS:
+            raise ValueError(f"precision must be one of {sorted(PRECISIONS)}")
+        return PRECISIONS[self.precision]
+
+    def fused_supported(self, K: int) -> bool:
+        """The fused render kernel takes K % 32 == 0 and D in {32, 64, 128}; other
+        shapes go through sd_field_query + sd_composite (also native)."""
+        D = self._d_out - 1
+        return K % 32 == 0 and D in (32, 64, 128)
 
     def _mlp(self):
         head = self.heads[self.final_pred_head]
@@ -213,6 +223,8 @@ class BTSNet(nn.Module):
         self._check_supported()
         m = self._mlp()
         gc = self._grids()
+        if gc["C"] != m.C:
+            raise ValueError(f"feature grid has {gc['C']} channels, the MLP expects {m.C}")
         R, K = z.shape
         if R % sb or gc["B"] != sb:
             raise ValueError(f"rays ({R}) must split into {sb} super-batches matching the "
@@ -251,6 +263,8 @@ class BTSNet(nn.Module):
         self._check_supported()
         m = self._mlp()
         gc = self._grids()
+        if gc["C"] != m.C:
+            raise ValueError(f"feature grid has {gc['C']} channels, the MLP expects {m.C}")
         n, P, _ = xyz.shape
         if n != gc["B"]:
             raise ValueError(f"xyz batch {n} != encoded batch {gc['B']}")

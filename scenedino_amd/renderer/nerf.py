@@ -135,7 +135,8 @@ class NeRFRenderer(torch.nn.Module):
             B, K = z_samp.shape
             r_dim = rays.shape[-1]
             sbn = sb if sb > 0 else 1
-            if hasattr(model, "render_fused") and not getattr(model, "use_viewdirs", False):
+            if (hasattr(model, "render_fused") and not getattr(model, "use_viewdirs", False)
+                    and model.fused_supported(K)):
                 o = model.render_fused(rays, z_samp, sbn, self.hard_alpha_cap,
                                        want_weights=True, want_alphas=True,
                                        want_rgb_samps=self._want_rgb_samps)

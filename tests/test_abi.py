@@ -1,0 +1,74 @@
+"""CPU: the C-ABI library loads and exports every entry point include/sdhip.h declares
+(no compute calls: there is no GPU here)."""
+import ctypes
+import os
+import re
+
+from conftest import ROOT
+
+
+def declared_functions():
+    src = open(os.path.join(ROOT, "include", "sdhip.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(sd_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_header_declares_expected_entry_points():
+    names = declared_functions()
+    for n in ("sd_gen_rays", "sd_sample_z", "sd_render_fused", "sd_field_query", "sd_composite",
+              "sd_pack_grid", "sd_pack_image", "sd_last_error", "sd_abi_version"):
+        assert n in names
+
+
+def test_library_exports_every_declared_symbol():
+    from scenedino_amd import _lib
+    lib = _lib.load()
+    for name in declared_functions():
+        assert hasattr(lib, name), f"libsdhip.so does not export {name}"
+        assert name in _lib.SIGNATURES, f"{name} has no ctypes signature in _lib"
+
+
+def test_abi_version_and_error_string():
+    from scenedino_amd import _lib
+    lib = _lib.load()
+    assert lib.sd_abi_version() == _lib.ABI_VERSION
+    assert isinstance(lib.sd_last_error(), bytes)
+
+
+def test_invalid_arguments_return_error_without_gpu():
+    """Argument validation happens before any HIP call, so it is testable on CPU."""
+    from scenedino_amd import _lib
+    lib = _lib.load()
+    rc = lib.sd_gen_rays(None, None, None, 0, 0, 0, 3.0, 80.0, None, None)
+    assert rc == -1 and b"invalid" in lib.sd_last_error()
+    rc = lib.sd_render_fused(None, None, None)
+    assert rc == -1
+
+
+def test_struct_layouts_match_the_c_header(tmp_path):
+    """ctypes mirrors of the ABI structs have the C compiler's sizes and offsets."""
+    import subprocess
+    from scenedino_amd import _lib
+    structs = {"sd_mlp": _lib.SdMlp, "sd_render_args": _lib.SdRenderArgs,
+               "sd_field_args": _lib.SdFieldArgs}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "sdhip.h"', "int main(void){"]
+    for cname, py in structs.items():
+        lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
+        for fname, _ in py._fields_:
+            lines.append(f'printf("{cname} {fname} %zu\\n", offsetof({cname}, {fname}));')
+    lines.append("return 0;}")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)],
+                   check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    got = {}
+    for line in out:
+        if line:
+            c, f, v = line.split()
+            got[(c, f)] = int(v)
+    for cname, py in structs.items():
+        assert ctypes.sizeof(py) == got[(cname, "size")], cname
+        for fname, _ in py._fields_:
+            assert getattr(py, fname).offset == got[(cname, fname)], (cname, fname)
