@@ -104,14 +104,39 @@ template <int P> struct Prec;
 
 struct Raw16 { uint4 a, b, c, d; };  // 4 taps x 8 x 16-bit channels
 
-__device__ __forceinline__ Raw16 sd_load16(const uint16_t *__restrict__ g, const Taps &t, int C,
-                                           int coff) {
+// Byte offsets (within the grid plane of this ray's batch element) of the lane's
+// channel slice in the 4 taps at chunk 0; chunk q adds q * 16 * esz bytes, which is
+// wave-uniform and goes into the buffer load's scalar offset (no per-load VALU).
+struct TapOff { uint32_t o00, o01, o10, o11; };
+
+__device__ __forceinline__ TapOff sd_tapoff(const Taps &t, int C, int esz, int h,
+                                           uint32_t base = 0) {
+    const uint32_t row = (uint32_t)C * esz, lo = (uint32_t)(8 * esz * h) + base;
+    return {t.i00 * row + lo, t.i01 * row + lo, t.i10 * row + lo, t.i11 * row + lo};
+}
+
+__device__ __forceinline__ uint4 sd_ld128(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff) {
+    return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
+}
+
+__device__ __forceinline__ Raw16 sd_load16(__amdgpu_buffer_rsrc_t rs, const TapOff &o, int q) {
+    const uint32_t s = (uint32_t)q * 32u;
     Raw16 r;
-    r.a = *(const uint4 *)(g + (int64_t)t.i00 * C + coff);
-    r.b = *(const uint4 *)(g + (int64_t)t.i01 * C + coff);
-    r.c = *(const uint4 *)(g + (int64_t)t.i10 * C + coff);
-    r.d = *(const uint4 *)(g + (int64_t)t.i11 * C + coff);
+    r.a = sd_ld128(rs, o.o00, s);
+    r.b = sd_ld128(rs, o.o01, s);
+    r.c = sd_ld128(rs, o.o10, s);
+    r.d = sd_ld128(rs, o.o11, s);
     return r;
+}
+
+// Buffer descriptor over one batch element's grid plane (wave-uniform inputs).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sd_rsrc(const void *base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, bytes, 0x00020000);
+}
+
+// ReLU without the canonicalising v_max hipcc adds in front of fmaxf on MFMA results
+__device__ __forceinline__ float sd_relu(float x) {
+    return __builtin_amdgcn_fmed3f(x, 0.f, __builtin_inff());
 }
 
 template <> struct Prec<SD_BF16> {
@@ -119,8 +144,9 @@ template <> struct Prec<SD_BF16> {
     typedef Raw16 Raw;
     typedef bf16x8 Frag;
     static constexpr bool FAST_PE = true;
-    static __device__ __forceinline__ Raw load(const G *__restrict__ g, const Taps &t, int C, int coff) {
-        return sd_load16(g, t, C, coff);
+    static constexpr int ESZ = 2, DEPTH = 4;
+    static __device__ __forceinline__ Raw load(__amdgpu_buffer_rsrc_t rs, const TapOff &o, int q) {
+        return sd_load16(rs, o, q);
     }
     static __device__ __forceinline__ float b1(uint32_t a, uint32_t b, uint32_t c, uint32_t d,
                                                bool hi, const Taps &t) {
@@ -175,8 +201,9 @@ template <> struct Prec<SD_F16> {
     typedef Raw16 Raw;
     typedef f16x8 Frag;
     static constexpr bool FAST_PE = true;
-    static __device__ __forceinline__ Raw load(const G *__restrict__ g, const Taps &t, int C, int coff) {
-        return sd_load16(g, t, C, coff);
+    static constexpr int ESZ = 2, DEPTH = 4;
+    static __device__ __forceinline__ Raw load(__amdgpu_buffer_rsrc_t rs, const TapOff &o, int q) {
+        return sd_load16(rs, o, q);
     }
     static __device__ __forceinline__ Frag blend(const Raw &r, const Taps &t) {
         const f16x2 w0 = {(_Float16)t.w00, (_Float16)t.w00}, w1 = {(_Float16)t.w01, (_Float16)t.w01};
@@ -228,14 +255,17 @@ template <> struct Prec<SD_F32> {
     struct Raw { f32x4 a0, a1, b0, b1, c0, c1, d0, d1; };
     struct Frag { float f[8]; };
     static constexpr bool FAST_PE = false;
-    static __device__ __forceinline__ Raw load(const G *__restrict__ g, const Taps &t, int C, int coff) {
+    static constexpr int ESZ = 4, DEPTH = 2;
+    static __device__ __forceinline__ f32x4 ld(__amdgpu_buffer_rsrc_t rs, uint32_t v, uint32_t s) {
+        return __builtin_bit_cast(f32x4, sd_ld128(rs, v, s));
+    }
+    static __device__ __forceinline__ Raw load(__amdgpu_buffer_rsrc_t rs, const TapOff &o, int q) {
+        const uint32_t s = (uint32_t)q * 64u;
         Raw r;
-        const float *pa = g + (int64_t)t.i00 * C + coff, *pb = g + (int64_t)t.i01 * C + coff;
-        const float *pc = g + (int64_t)t.i10 * C + coff, *pd = g + (int64_t)t.i11 * C + coff;
-        r.a0 = *(const f32x4 *)pa; r.a1 = *(const f32x4 *)(pa + 4);
-        r.b0 = *(const f32x4 *)pb; r.b1 = *(const f32x4 *)(pb + 4);
-        r.c0 = *(const f32x4 *)pc; r.c1 = *(const f32x4 *)(pc + 4);
-        r.d0 = *(const f32x4 *)pd; r.d1 = *(const f32x4 *)(pd + 4);
+        r.a0 = ld(rs, o.o00, s); r.a1 = ld(rs, o.o00, s + 16);
+        r.b0 = ld(rs, o.o01, s); r.b1 = ld(rs, o.o01, s + 16);
+        r.c0 = ld(rs, o.o10, s); r.c1 = ld(rs, o.o10, s + 16);
+        r.d0 = ld(rs, o.o11, s); r.d1 = ld(rs, o.o11, s + 16);
         return r;
     }
     // grid_sample order: nw, ne, sw, se accumulated left to right, separately rounded.
@@ -294,25 +324,49 @@ __device__ __forceinline__ int sd_opaque0() {
     return z;
 }
 
-// First layer over all C/16 grid chunks + 3 code chunks, with a 2-deep tap-load
-// pipeline (C % 32 == 0).  acc must hold the initial accumulator (b_in).
+// One pipeline step: blend chunk q from r, refill r with chunk q + DEPTH (compile-time
+// LOAD: the tail steps issue no loads), then the 4 (or 32 f32) MFMAs of chunk q.
+#define SD_STEP(r, qq, LOAD)                                                  \
+    do {                                                                      \
+        typename Pr::Frag f_ = Pr::blend(r, geo.t);                           \
+        if (LOAD) r = Pr::load(rs, o, (qq) + Pr::DEPTH);                      \
+        Pr::mma1(lw, (qq), lane, f_, acc);                                    \
+    } while (0)
+
+// First layer over all C/16 grid chunks + 3 code chunks, with a DEPTH-deep tap-load
+// pipeline held in registers (C % (16 DEPTH) == 0).  acc holds the initial
+// accumulator (b_in).  rs: buffer descriptor over this batch element's grid plane.
 template <int P>
-__device__ __forceinline__ void sd_layer1(const typename Prec<P>::G *__restrict__ g, int C,
-                                          const PointGeo &geo, const uint8_t *lw, int lane,
-                                          f32x16 acc[4]) {
+__device__ __forceinline__ void sd_layer1(__amdgpu_buffer_rsrc_t rs, int C, const PointGeo &geo,
+                                          const uint8_t *lw, int lane, f32x16 acc[4],
+                                          uint32_t base = 0) {
     typedef Prec<P> Pr;
     const int h = lane >> 5;
     const int nq = C >> 4;
-    const int c0 = 8 * h;
-    typename Pr::Raw ra = Pr::load(g, geo.t, C, c0);
-    typename Pr::Raw rb = Pr::load(g, geo.t, C, c0 + 16);
-    for (int q = 0; q < nq; q += 2) {
-        typename Pr::Frag fa = Pr::blend(ra, geo.t);
-        ra = Pr::load(g, geo.t, C, c0 + 16 * min(q + 2, nq - 2));
-        Pr::mma1(lw, q, lane, fa, acc);
-        typename Pr::Frag fb = Pr::blend(rb, geo.t);
-        rb = Pr::load(g, geo.t, C, c0 + 16 * min(q + 3, nq - 1));
-        Pr::mma1(lw, q + 1, lane, fb, acc);
+    const TapOff o = sd_tapoff(geo.t, C, Pr::ESZ, h, base);
+    if constexpr (Pr::DEPTH == 4) {
+        typename Pr::Raw r0 = Pr::load(rs, o, 0), r1 = Pr::load(rs, o, 1);
+        typename Pr::Raw r2 = Pr::load(rs, o, 2), r3 = Pr::load(rs, o, 3);
+        int q = 0;
+        for (; q + 4 < nq; q += 4) {
+            SD_STEP(r0, q, true);
+            SD_STEP(r1, q + 1, true);
+            SD_STEP(r2, q + 2, true);
+            SD_STEP(r3, q + 3, true);
+        }
+        SD_STEP(r0, q, false);
+        SD_STEP(r1, q + 1, false);
+        SD_STEP(r2, q + 2, false);
+        SD_STEP(r3, q + 3, false);
+    } else {
+        typename Pr::Raw r0 = Pr::load(rs, o, 0), r1 = Pr::load(rs, o, 1);
+        int q = 0;
+        for (; q + 2 < nq; q += 2) {
+            SD_STEP(r0, q, true);
+            SD_STEP(r1, q + 1, true);
+        }
+        SD_STEP(r0, q, false);
+        SD_STEP(r1, q + 1, false);
     }
 #pragma unroll
     for (int pc = 0; pc < SD_PE_CHUNKS; ++pc) {
@@ -347,7 +401,7 @@ __device__ __forceinline__ float sd_relu_sigma(f32x16 acc[4], const float *lds_w
             f32x4 w = ww[q];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                float v = fmaxf(acc[t][4 * q + i], 0.f);
+                float v = sd_relu(acc[t][4 * q + i]);
                 acc[t][4 * q + i] = v;
                 s = fmaf(v, w[i], s);
             }
@@ -411,18 +465,18 @@ __device__ __forceinline__ void sd_stage(uint8_t *lds, const sd_mlp &m, const Ld
 template <int P, int NV, int NDT>
 __global__ void __launch_bounds__(SD_WG, 1)
 k_render(const sd_render_args a, const sd_mlp m, const LdsPlan pl) {
-    typedef typename Prec<P>::G G;
+    constexpr bool WL = P != SD_F32;  // 16-bit W_out fragments live in LDS, f32 in L2
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     sd_stage(lds, m, pl);
-    const uint8_t *wout_base = pl.wout_in_lds ? lds + pl.win_bytes : (const uint8_t *)m.w_out;
-    const float *lds_b = (const float *)(lds + pl.win_bytes + (pl.wout_in_lds ? pl.wout_bytes : 0));
+    const uint8_t *wout_base = WL ? lds + pl.win_bytes : (const uint8_t *)m.w_out;
+    const float *lds_b = (const float *)(lds + pl.win_bytes + (WL ? pl.wout_bytes : 0));
     const float *lds_ws = lds_b + 128;
 
     const int lane = threadIdx.x & 63, h = lane >> 5, li = lane & 31;
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int K = a.K, C = m.C, nv = NV > 0 ? NV : a.nv;
     const int nsub = K >> 5;
-    const int64_t plane = (int64_t)a.Hf * a.Wf * C;
+    const uint32_t plane_bytes = (uint32_t)a.Hf * a.Wf * C * Prec<P>::ESZ;
     const int64_t cplane = (int64_t)a.Hc * a.Wc * 4;
     const int64_t nwaves = (int64_t)gridDim.x * SD_WAVES;
 
@@ -431,7 +485,8 @@ k_render(const sd_render_args a, const sd_mlp m, const LdsPlan pl) {
         const float *rr = a.rays + ray * a.ray_dim;
         const float ox = rr[0], oy = rr[1], oz = rr[2], dx = rr[3], dy = rr[4], dz = rr[5];
         const float *zr = a.z + ray * K;
-        const G *grid = (const G *)a.grid + sbi * plane;
+        const __amdgpu_buffer_rsrc_t rs =
+            sd_rsrc((const uint8_t *)a.grid + sbi * (int64_t)plane_bytes, plane_bytes);
         const float *camf = a.cam_f + sbi * 21;
 
         // dacc[dt]: sum over samples of (w h)^T W_out^T in O layout (D = 32 NDT)
@@ -453,7 +508,7 @@ k_render(const sd_render_args a, const sd_mlp m, const LdsPlan pl) {
             const int lo = sd_opaque0();
             f32x16 acc[4];
             sd_init_bias(acc, lds_b + lo, h);
-            sd_layer1<P>(grid, C, geo, lds + lo, lane, acc);
+            sd_layer1<P>(rs, C, geo, lds + lo, lane, acc);
             float s = sd_relu_sigma(acc, lds_ws + lo, h);
             s += __shfl_xor(s, 32);
             const float sigma = sd_softplus(s + m.b_sigma);
@@ -496,7 +551,7 @@ k_render(const sd_render_args a, const sd_mlp m, const LdsPlan pl) {
             for (int t = 0; t < 4; ++t)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[t][r] *= w;
-            const uint8_t *wo = wout_base + (pl.wout_in_lds ? lo : 0);
+            const uint8_t *wo = wout_base + (WL ? lo : 0);
 #pragma unroll
             for (int dt = 0; dt < NDT; ++dt) Prec<P>::mma2(wo, dt, acc, lane, dacc[dt]);
 
@@ -557,21 +612,23 @@ k_render(const sd_render_args a, const sd_mlp m, const LdsPlan pl) {
 template <int P>
 __global__ void __launch_bounds__(SD_WG, 1)
 k_field(const sd_field_args a, const sd_mlp m, const LdsPlan pl) {
-    typedef typename Prec<P>::G G;
+    constexpr bool WL = P != SD_F32;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     sd_stage(lds, m, pl);
-    const uint8_t *wout_base = pl.wout_in_lds ? lds + pl.win_bytes : (const uint8_t *)m.w_out;
-    const float *lds_b = (const float *)(lds + pl.win_bytes + (pl.wout_in_lds ? pl.wout_bytes : 0));
+    const uint8_t *wout_base = WL ? lds + pl.win_bytes : (const uint8_t *)m.w_out;
+    const float *lds_b = (const float *)(lds + pl.win_bytes + (WL ? pl.wout_bytes : 0));
     const float *lds_ws = lds_b + 128;
 
     const int lane = threadIdx.x & 63, h = lane >> 5, li = lane & 31;
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t NP = a.B * a.P;
     const int64_t ntiles = (NP + 31) / 32;
     const int C = m.C, nv = a.nv;
     const int ndt = m.D >> 5;
-    const int64_t plane = (int64_t)a.Hf * a.Wf * C;
+    const uint32_t plane_bytes = (uint32_t)a.Hf * a.Wf * C * Prec<P>::ESZ;
     const int64_t cplane = (int64_t)a.Hc * a.Wc * 4;
+    // one descriptor over all batch planes (host checks B * plane < 4 GiB)
+    const __amdgpu_buffer_rsrc_t rs = sd_rsrc(a.grid, (uint32_t)(a.B * (int64_t)plane_bytes));
 
     for (int64_t tile = (int64_t)blockIdx.x * SD_WAVES + wave; tile < ntiles;
          tile += (int64_t)gridDim.x * SD_WAVES) {
@@ -580,18 +637,17 @@ k_field(const sd_field_args a, const sd_mlp m, const LdsPlan pl) {
         const int64_t p = valid ? pu : NP - 1;
         const int64_t b = p / a.P;
         const float px = a.xyz[p * 3], py = a.xyz[p * 3 + 1], pz = a.xyz[p * 3 + 2];
-        const G *grid = (const G *)a.grid + b * plane;
         PointGeo geo = sd_point_geo(a.cam_f + b * 21, px, py, pz, a.Wf, a.Hf);
 
         const int lo = sd_opaque0();
         f32x16 acc[4];
         sd_init_bias(acc, lds_b + lo, h);
-        sd_layer1<P>(grid, C, geo, lds + lo, lane, acc);
+        sd_layer1<P>(rs, C, geo, lds + lo, lane, acc, (uint32_t)(b * plane_bytes));
         float s = sd_relu_sigma(acc, lds_ws + lo, h);
         s += __shfl_xor(s, 32);
         const float sigma = sd_softplus(s + m.b_sigma);
 
-        const uint8_t *wo = wout_base + (pl.wout_in_lds ? lo : 0);
+        const uint8_t *wo = wout_base + (WL ? lo : 0);
         for (int dt = 0; dt < ndt; ++dt) {
             f32x16 o = {};
             Prec<P>::mma2(wo, dt, acc, lane, o);
@@ -689,9 +745,9 @@ static int sd_plan(const sd_mlp *m, LdsPlan *pl) {
         sd_set_error("sd_mlp: null parameter pointer");
         return -1;
     }
-    if (m->d_hidden != SD_DH || m->C <= 0 || (m->C % 32) || m->D <= 0 || (m->D % 32) ||
+    if (m->d_hidden != SD_DH || m->C <= 0 || (m->C % 64) || m->D <= 0 || (m->D % 32) ||
         (m->dtype != SD_BF16 && m->dtype != SD_F32 && m->dtype != SD_F16)) {
-        sd_set_error("sd_mlp: unsupported shape (need d_hidden=128, C%32==0, D%32==0)");
+        sd_set_error("sd_mlp: unsupported shape (need d_hidden=128, C%64==0, D%32==0)");
         return -1;
     }
     int nq = m->C / 16 + SD_PE_CHUNKS;
@@ -699,10 +755,10 @@ static int sd_plan(const sd_mlp *m, LdsPlan *pl) {
     pl->win_bytes = nq * 4 * SD_WAVE * 8 * esz;
     pl->wout_bytes = (m->D / 32) * 4 * SD_WAVE * (m->dtype == SD_F32 ? 64 : 32);
     int rest = 256 * 4;
-    pl->wout_in_lds = (pl->win_bytes + pl->wout_bytes + rest) <= 160 * 1024;
+    pl->wout_in_lds = m->dtype != SD_F32;
     pl->total = pl->win_bytes + (pl->wout_in_lds ? pl->wout_bytes : 0) + rest;
     if (pl->total > 160 * 1024) {
-        sd_set_error("sd_mlp: W_in fragments exceed LDS (reduce C or use a 16-bit dtype)");
+        sd_set_error("sd_mlp: MLP fragments exceed the 160 KiB LDS (C or D too large)");
         return -1;
     }
     return 0;

@@ -105,9 +105,9 @@ class PackedMLP:
         dh, din = W_in.shape
         C = din - N_PE
         D = W_out.shape[0] - 1
-        if dh != D_HIDDEN or C <= 0 or C % 32 or D % 32 or W_out.shape[1] != dh:
+        if dh != D_HIDDEN or C <= 0 or C % 64 or D % 32 or W_out.shape[1] != dh:
             raise NotImplementedError(
-                f"fused field kernel needs d_hidden=128, C%32==0, D%32==0 (got W_in {tuple(W_in.shape)}, "
+                f"fused field kernel needs d_hidden=128, C%64==0, D%32==0 (got W_in {tuple(W_in.shape)}, "
                 f"W_out {tuple(W_out.shape)})")
         dev = W_in.device
         ix = {k: v.to(dev) for k, v in _index_tables(C, D).items()}

@@ -66,7 +66,7 @@ def pe_chunk(v, pc, h):
 @pytest.fixture(scope="module")
 def mlp_params():
     g = torch.Generator().manual_seed(5)
-    C, D = 32, 64
+    C, D = 64, 64
     W_in = torch.randn(128, C + 39, generator=g) * 0.1
     b_in = torch.randn(128, generator=g) * 0.1
     W_out = torch.randn(1 + D, 128, generator=g) * 0.1
