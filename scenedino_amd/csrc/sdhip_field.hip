@@ -46,8 +46,12 @@ extern "C" void sd_set_error(const char *msg) {
 extern "C" const char *sd_last_error(void) { return g_err; }
 extern "C" int sd_abi_version(void) { return 1; }
 
-#define SD_WG 512            // threads per workgroup (8 waves, one workgroup per CU)
-#define SD_WAVES (SD_WG / 64)
+// Threads per workgroup, one workgroup per CU: 16-bit kernels run 8 waves (2 per SIMD,
+// <= 256 VGPRs each); the f32 parity kernels run 4 waves (1 per SIMD, 512 VGPRs).
+template <int P> struct WG {
+    static constexpr int T = P == SD_F32 ? 256 : 512;
+    static constexpr int W = T / 64;
+};
 
 // ---------------------------------------------------------------------------
 // per-point geometry
@@ -460,11 +464,26 @@ __device__ __forceinline__ void sd_stage(uint8_t *lds, const sd_mlp &m, const Ld
 }
 
 // ---------------------------------------------------------------------------
-// fused render: one wave per ray at a time, K/32 sub-tiles of 32 samples
+// fused render: one wave per ray at a time, K/32 sub-tiles ("items") of 32 samples,
+// software-pipelined across items: while item i runs its MLP, the z values of item
+// i+1 are in flight; after item i's grid chunks, item i+1's geometry is computed and
+// its first DEPTH tap loads + colour taps are issued, so the epilogue of item i (code
+// chunks, sigma, compositing, DINO head) hides their latency.
 // ---------------------------------------------------------------------------
+struct Item {
+    int64_t ray;
+    int sub;
+    float zk, delta, px, py, pz;
+    PointGeo geo;
+    TapOff o;
+    __amdgpu_buffer_rsrc_t rs;
+    int64_t sbi;
+};
+
 template <int P, int NV, int NDT>
-__global__ void __launch_bounds__(SD_WG, 1)
+__global__ void __launch_bounds__(WG<P>::T, 1)
 k_render(const sd_render_args a, const sd_mlp m, const LdsPlan pl) {
+    typedef Prec<P> Pr;
     constexpr bool WL = P != SD_F32;  // 16-bit W_out fragments live in LDS, f32 in L2
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     sd_stage(lds, m, pl);
@@ -475,134 +494,224 @@ k_render(const sd_render_args a, const sd_mlp m, const LdsPlan pl) {
     const int lane = threadIdx.x & 63, h = lane >> 5, li = lane & 31;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int K = a.K, C = m.C, nv = NV > 0 ? NV : a.nv;
-    const int nsub = K >> 5;
-    const uint32_t plane_bytes = (uint32_t)a.Hf * a.Wf * C * Prec<P>::ESZ;
+    const int nsub = K >> 5, nq = C >> 4;
+    const uint32_t plane_bytes = (uint32_t)a.Hf * a.Wf * C * Pr::ESZ;
     const int64_t cplane = (int64_t)a.Hc * a.Wc * 4;
-    const int64_t nwaves = (int64_t)gridDim.x * SD_WAVES;
+    const int64_t nwaves = (int64_t)gridDim.x * WG<P>::W;
+    const int64_t ray0 = (int64_t)blockIdx.x * WG<P>::W + wave;
+    if (ray0 >= a.R) return;
+    const int64_t nitems = ((a.R - ray0 + nwaves - 1) / nwaves) * nsub;
 
-    for (int64_t ray = (int64_t)blockIdx.x * SD_WAVES + wave; ray < a.R; ray += nwaves) {
-        const int64_t sbi = ray / a.rays_per_sb;
-        const float *rr = a.rays + ray * a.ray_dim;
-        const float ox = rr[0], oy = rr[1], oz = rr[2], dx = rr[3], dy = rr[4], dz = rr[5];
+    auto item_ray = [&](int64_t i) { return ray0 + (i / nsub) * nwaves; };
+    // z and z_next of item i for this lane
+    auto load_z = [&](int64_t i, float &z0, float &z1) {
+        const int64_t ray = item_ray(i);
+        const int k = (int)(i % nsub) * 32 + li;
         const float *zr = a.z + ray * K;
-        const __amdgpu_buffer_rsrc_t rs =
-            sd_rsrc((const uint8_t *)a.grid + sbi * (int64_t)plane_bytes, plane_bytes);
-        const float *camf = a.cam_f + sbi * 21;
-
-        // dacc[dt]: sum over samples of (w h)^T W_out^T in O layout (D = 32 NDT)
-        f32x16 dacc[NDT];
+        z0 = zr[k];
+        z1 = zr[min(k + 1, K - 1)];
+    };
+    // geometry, buffer descriptor and tap offsets of item i (z already loaded)
+    auto open_item = [&](int64_t i, float z0, float z1, Item &it) {
+        it.ray = item_ray(i);
+        it.sub = (int)(i % nsub);
+        it.sbi = it.ray / a.rays_per_sb;
+        const int k = it.sub * 32 + li;
+        const float *rr = a.rays + it.ray * a.ray_dim;
+        it.zk = z0;
+        it.delta = (k + 1 < K) ? (z1 - z0) : 1e10f;
+        it.px = rr[0] + z0 * rr[3];  // points = o + z d (nerf.py:252)
+        it.py = rr[1] + z0 * rr[4];
+        it.pz = rr[2] + z0 * rr[5];
+        it.geo = sd_point_geo(a.cam_f + it.sbi * 21, it.px, it.py, it.pz, a.Wf, a.Hf);
+        it.rs = sd_rsrc((const uint8_t *)a.grid + it.sbi * (int64_t)plane_bytes, plane_bytes);
+        it.o = sd_tapoff(it.geo.t, C, Pr::ESZ, h);
+    };
+    auto colours = [&](const Item &it, float col[3 * SD_MAX_NV], bool invc[SD_MAX_NV]) {
 #pragma unroll
-        for (int i = 0; i < NDT; ++i) dacc[i] = f32x16{};
-        float Tc = 1.f, dpart = 0.f, wpart = 0.f;
-        float cpart[3 * SD_MAX_NV];
+        for (int v = 0; v < SD_MAX_NV; ++v) {
+            invc[v] = false;
+            col[3 * v] = col[3 * v + 1] = col[3 * v + 2] = 0.f;
+            if (v < nv)
+                invc[v] = sd_color_view(a.cam_c + (it.sbi * nv + v) * 21,
+                                        a.img + (it.sbi * nv + v) * cplane, a.Wc, a.Hc, it.px,
+                                        it.py, it.pz, col + 3 * v);
+        }
+    };
+
+    // prologue: item 0
+    Item cur;
+    float z0, z1;
+    load_z(0, z0, z1);
+    open_item(0, z0, z1, cur);
+    typename Pr::Raw r0 = Pr::load(cur.rs, cur.o, 0), r1 = Pr::load(cur.rs, cur.o, 1);
+    typename Pr::Raw r2, r3;
+    if constexpr (Pr::DEPTH == 4) {
+        r2 = Pr::load(cur.rs, cur.o, 2);
+        r3 = Pr::load(cur.rs, cur.o, 3);
+    }
+    float col[3 * SD_MAX_NV];
+    bool invc[SD_MAX_NV];
+    colours(cur, col, invc);
+
+    // per-ray compositing state
+    f32x16 dacc[NDT];
 #pragma unroll
-        for (int i = 0; i < 3 * SD_MAX_NV; ++i) cpart[i] = 0.f;
-
-        for (int sub = 0; sub < nsub; ++sub) {
-            const int k = sub * 32 + li;
-            const float zk = zr[k];
-            const float delta = (k + 1 < K) ? (zr[min(k + 1, K - 1)] - zk) : 1e10f;
-            const float px = ox + zk * dx, py = oy + zk * dy, pz = oz + zk * dz;  // nerf.py:252
-            PointGeo geo = sd_point_geo(camf, px, py, pz, a.Wf, a.Hf);
-
-            const int lo = sd_opaque0();
-            f32x16 acc[4];
-            sd_init_bias(acc, lds_b + lo, h);
-            sd_layer1<P>(rs, C, geo, lds + lo, lane, acc);
-            float s = sd_relu_sigma(acc, lds_ws + lo, h);
-            s += __shfl_xor(s, 32);
-            const float sigma = sd_softplus(s + m.b_sigma);
-
-            // alpha compositing (nerf.py:376-389); transmittance = prefix product
-            float alpha = 1.f - expf(-fabsf(delta) * fmaxf(sigma, 0.f));
-            if (a.hard_alpha_cap && k == K - 1) alpha = 1.f;
-            const float tk = (1.f - alpha) + 1e-10f;
-            float incl = tk;
+    for (int i = 0; i < NDT; ++i) dacc[i] = f32x16{};
+    float Tc = 1.f, dpart = 0.f, wpart = 0.f;
+    float cpart[3 * SD_MAX_NV];
 #pragma unroll
-            for (int d = 1; d < 32; d <<= 1) {
-                float v = __shfl_up(incl, d, 32);
-                if (li >= d) incl *= v;
-            }
-            float excl = __shfl_up(incl, 1, 32);
-            if (li == 0) excl = 1.f;
-            const float w = alpha * (Tc * excl);
-            Tc *= __shfl(incl, 31, 32);
-            dpart += w * zk;
-            wpart += w;
+    for (int i = 0; i < 3 * SD_MAX_NV; ++i) cpart[i] = 0.f;
 
-            // colours (bts.py:330-441)
-            float col[3 * SD_MAX_NV];
-            bool invc[SD_MAX_NV];
-#pragma unroll
-            for (int v = 0; v < SD_MAX_NV; ++v) {
-                invc[v] = false;
-                col[3 * v] = col[3 * v + 1] = col[3 * v + 2] = 0.f;
-                if (v < nv) {
-                    invc[v] = sd_color_view(a.cam_c + (sbi * nv + v) * 21, a.img + (sbi * nv + v) * cplane,
-                                            a.Wc, a.Hc, px, py, pz, col + 3 * v);
-                    cpart[3 * v] += w * col[3 * v];
-                    cpart[3 * v + 1] += w * col[3 * v + 1];
-                    cpart[3 * v + 2] += w * col[3 * v + 2];
+    for (int64_t i = 0; i < nitems; ++i) {
+        const int64_t inext = min(i + 1, nitems - 1);
+        float zn0, zn1;
+        load_z(inext, zn0, zn1);  // in flight during this item's MLP
+
+        const int lo = sd_opaque0();
+        const uint8_t *lw = lds + lo;
+        f32x16 acc[4];
+        sd_init_bias(acc, lds_b + lo, h);
+        {
+            const PointGeo &geo = cur.geo;
+            const __amdgpu_buffer_rsrc_t rs = cur.rs;
+            const TapOff o = cur.o;
+            if constexpr (Pr::DEPTH == 4) {
+                int q = 0;
+                for (; q + 4 < nq; q += 4) {
+                    SD_STEP(r0, q, true);
+                    SD_STEP(r1, q + 1, true);
+                    SD_STEP(r2, q + 2, true);
+                    SD_STEP(r3, q + 3, true);
                 }
-            }
-
-            // DINO head folded into the compositing sum: dacc += (w h)^T W_out^T
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) acc[t][r] *= w;
-            const uint8_t *wo = wout_base + (WL ? lo : 0);
-#pragma unroll
-            for (int dt = 0; dt < NDT; ++dt) Prec<P>::mma2(wo, dt, acc, lane, dacc[dt]);
-
-            // per-sample outputs, coalesced along the ray
-            const int64_t o = ray * K + k;
-            if (h == 0) {
-                if (a.weights) a.weights[o] = w;
-                if (a.alphas) a.alphas[o] = alpha;
-                if (a.invalid_f) a.invalid_f[o] = geo.inv_f ? 1 : 0;
+                SD_STEP(r0, q, false);
+                SD_STEP(r1, q + 1, false);
+                SD_STEP(r2, q + 2, false);
+                SD_STEP(r3, q + 3, false);
             } else {
-#pragma unroll
-                for (int v = 0; v < SD_MAX_NV; ++v)
-                    if (v < nv) {
-                        if (a.invalid) a.invalid[o * nv + v] = (invc[v] | geo.inv_f) ? 1.f : 0.f;
-                        if (a.rgb_samps) {
-                            float *rs = a.rgb_samps + (o * nv + v) * 3;
-                            rs[0] = col[3 * v]; rs[1] = col[3 * v + 1]; rs[2] = col[3 * v + 2];
-                        }
-                    }
+                int q = 0;
+                for (; q + 2 < nq; q += 2) {
+                    SD_STEP(r0, q, true);
+                    SD_STEP(r1, q + 1, true);
+                }
+                SD_STEP(r0, q, false);
+                SD_STEP(r1, q + 1, false);
             }
         }
 
-        // ray epilogue: reduce the per-lane partial sums over the 32 lanes of a half
+        // open the next item and put its first tap loads in flight
+        Item nxt;
+        open_item(inext, zn0, zn1, nxt);
+        r0 = Pr::load(nxt.rs, nxt.o, 0);
+        r1 = Pr::load(nxt.rs, nxt.o, 1);
+        if constexpr (Pr::DEPTH == 4) {
+            r2 = Pr::load(nxt.rs, nxt.o, 2);
+            r3 = Pr::load(nxt.rs, nxt.o, 3);
+        }
+
+        // positional-code chunks of this item
+#pragma unroll
+        for (int pc = 0; pc < SD_PE_CHUNKS; ++pc) {
+            float f[8];
+            sd_pe_chunk<Pr::FAST_PE>(cur.geo.v, pc, h, f);
+            Pr::mma1(lw, nq + pc, lane, Pr::from_f(f), acc);
+        }
+
+        float s = sd_relu_sigma(acc, lds_ws + lo, h);
+        s += __shfl_xor(s, 32);
+        const float sigma = sd_softplus(s + m.b_sigma);
+
+        // alpha compositing (nerf.py:376-389); transmittance = prefix product
+        const int k = cur.sub * 32 + li;
+        float alpha = 1.f - expf(-fabsf(cur.delta) * fmaxf(sigma, 0.f));
+        if (a.hard_alpha_cap && k == K - 1) alpha = 1.f;
+        const float tk = (1.f - alpha) + 1e-10f;
+        float incl = tk;
 #pragma unroll
         for (int d = 1; d < 32; d <<= 1) {
-            dpart += __shfl_xor(dpart, d);
-            wpart += __shfl_xor(wpart, d);
-#pragma unroll
-            for (int i = 0; i < 3 * SD_MAX_NV; ++i)
-                if (i < 3 * nv) cpart[i] += __shfl_xor(cpart[i], d);
+            float v = __shfl_up(incl, d, 32);
+            if (li >= d) incl *= v;
         }
-        // dino[dim] = sum over rows of dacc (+ other half) + wsum * b
+        float excl = __shfl_up(incl, 1, 32);
+        if (li == 0) excl = 1.f;
+        const float w = alpha * (Tc * excl);
+        Tc *= __shfl(incl, 31, 32);
+        dpart += w * cur.zk;
+        wpart += w;
 #pragma unroll
-        for (int dt = 0; dt < NDT; ++dt) {
-            float sacc = 0.f;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) sacc += dacc[dt][r];
-            sacc += __shfl_xor(sacc, 32);
-            if ((dt & 1) == h) {
-                const int dim = dt * 32 + li;
-                a.dino[ray * m.D + dim] = sacc + wpart * m.b_dino[dim];
+        for (int v = 0; v < SD_MAX_NV; ++v)
+            if (v < nv) {
+                cpart[3 * v] += w * col[3 * v];
+                cpart[3 * v + 1] += w * col[3 * v + 1];
+                cpart[3 * v + 2] += w * col[3 * v + 2];
             }
-        }
-        if (lane == 0) a.depth[ray] = dpart;
-        if (lane < 3 * nv) {
-            float cv = 0.f;
+
+        // DINO head folded into the compositing sum: dacc += (w h)^T W_out^T
 #pragma unroll
-            for (int i = 0; i < 3 * SD_MAX_NV; ++i)
-                if (i == lane) cv = cpart[i];
-            a.rgb[ray * 3 * nv + lane] = cv;
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[t][r] *= w;
+        const uint8_t *wo = wout_base + (WL ? lo : 0);
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) Pr::mma2(wo, dt, acc, lane, dacc[dt]);
+
+        // per-sample outputs, coalesced along the ray
+        const int64_t o = cur.ray * K + k;
+        if (h == 0) {
+            if (a.weights) a.weights[o] = w;
+            if (a.alphas) a.alphas[o] = alpha;
+            if (a.invalid_f) a.invalid_f[o] = cur.geo.inv_f ? 1 : 0;
+        } else {
+#pragma unroll
+            for (int v = 0; v < SD_MAX_NV; ++v)
+                if (v < nv) {
+                    if (a.invalid) a.invalid[o * nv + v] = (invc[v] | cur.geo.inv_f) ? 1.f : 0.f;
+                    if (a.rgb_samps) {
+                        float *rsp = a.rgb_samps + (o * nv + v) * 3;
+                        rsp[0] = col[3 * v]; rsp[1] = col[3 * v + 1]; rsp[2] = col[3 * v + 2];
+                    }
+                }
         }
+
+        if (cur.sub == nsub - 1) {
+            // ray epilogue: reduce the per-lane partial sums over the 32 lanes of a half
+#pragma unroll
+            for (int d = 1; d < 32; d <<= 1) {
+                dpart += __shfl_xor(dpart, d);
+                wpart += __shfl_xor(wpart, d);
+#pragma unroll
+                for (int c = 0; c < 3 * SD_MAX_NV; ++c)
+                    if (c < 3 * nv) cpart[c] += __shfl_xor(cpart[c], d);
+            }
+            // dino[dim] = sum over rows of dacc (+ other half) + wsum * b
+#pragma unroll
+            for (int dt = 0; dt < NDT; ++dt) {
+                float sacc = 0.f;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) sacc += dacc[dt][r];
+                sacc += __shfl_xor(sacc, 32);
+                if ((dt & 1) == h) {
+                    const int dim = dt * 32 + li;
+                    a.dino[cur.ray * m.D + dim] = sacc + wpart * m.b_dino[dim];
+                }
+                dacc[dt] = f32x16{};
+            }
+            if (lane == 0) a.depth[cur.ray] = dpart;
+            if (lane < 3 * nv) {
+                float cv = 0.f;
+#pragma unroll
+                for (int c = 0; c < 3 * SD_MAX_NV; ++c)
+                    if (c == lane) cv = cpart[c];
+                a.rgb[cur.ray * 3 * nv + lane] = cv;
+            }
+            Tc = 1.f; dpart = 0.f; wpart = 0.f;
+#pragma unroll
+            for (int c = 0; c < 3 * SD_MAX_NV; ++c) cpart[c] = 0.f;
+        }
+
+        // colours of the next item (its loads were issued with its taps above)
+        colours(nxt, col, invc);
+        cur = nxt;
     }
 }
 
@@ -610,7 +719,7 @@ k_render(const sd_render_args a, const sd_mlp m, const LdsPlan pl) {
 // per-point field query (no compositing): 32 consecutive points per wave step
 // ---------------------------------------------------------------------------
 template <int P>
-__global__ void __launch_bounds__(SD_WG, 1)
+__global__ void __launch_bounds__(WG<P>::T, 1)
 k_field(const sd_field_args a, const sd_mlp m, const LdsPlan pl) {
     constexpr bool WL = P != SD_F32;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -630,8 +739,8 @@ k_field(const sd_field_args a, const sd_mlp m, const LdsPlan pl) {
     // one descriptor over all batch planes (host checks B * plane < 4 GiB)
     const __amdgpu_buffer_rsrc_t rs = sd_rsrc(a.grid, (uint32_t)(a.B * (int64_t)plane_bytes));
 
-    for (int64_t tile = (int64_t)blockIdx.x * SD_WAVES + wave; tile < ntiles;
-         tile += (int64_t)gridDim.x * SD_WAVES) {
+    for (int64_t tile = (int64_t)blockIdx.x * WG<P>::W + wave; tile < ntiles;
+         tile += (int64_t)gridDim.x * WG<P>::W) {
         const int64_t pu = tile * 32 + li;
         const bool valid = pu < NP;
         const int64_t p = valid ? pu : NP - 1;
@@ -764,12 +873,16 @@ static int sd_plan(const sd_mlp *m, LdsPlan *pl) {
     return 0;
 }
 
-template <typename KernT, typename ArgT>
-static int sd_launch(KernT kern, int nblk, const LdsPlan &pl, hipStream_t s, const ArgT &a,
-                     const sd_mlp &m) {
+// Persistent grid: one workgroup per CU (fewer if there is less work); every wave
+// strides over its work units.
+template <int P, typename KernT, typename ArgT>
+static int sd_launch(KernT kern, int64_t work_waves, const LdsPlan &pl, hipStream_t s,
+                     const ArgT &a, const sd_mlp &m) {
+    int64_t nblk = (work_waves + WG<P>::W - 1) / WG<P>::W;
+    if (nblk > sd_num_cus()) nblk = sd_num_cus();
     (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
-    hipLaunchKernelGGL(kern, dim3(nblk), dim3(SD_WG), pl.total, s, a, m, pl);
+    hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(WG<P>::T), pl.total, s, a, m, pl);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         sd_set_error(hipGetErrorString(e));
@@ -779,12 +892,12 @@ static int sd_launch(KernT kern, int nblk, const LdsPlan &pl, hipStream_t s, con
 }
 
 template <int P, int NV>
-static int sd_render_ndt(const sd_render_args &a, const sd_mlp &m, const LdsPlan &pl, int nblk,
+static int sd_render_ndt(const sd_render_args &a, const sd_mlp &m, const LdsPlan &pl,
                          hipStream_t s) {
     switch (m.D / 32) {
-        case 1: return sd_launch(k_render<P, NV, 1>, nblk, pl, s, a, m);
-        case 2: return sd_launch(k_render<P, NV, 2>, nblk, pl, s, a, m);
-        case 4: return sd_launch(k_render<P, NV, 4>, nblk, pl, s, a, m);
+        case 1: return sd_launch<P>(k_render<P, NV, 1>, a.R, pl, s, a, m);
+        case 2: return sd_launch<P>(k_render<P, NV, 2>, a.R, pl, s, a, m);
+        case 4: return sd_launch<P>(k_render<P, NV, 4>, a.R, pl, s, a, m);
         default:
             sd_set_error("sd_render_fused: D must be 32, 64 or 128 (use sd_field_query + sd_composite)");
             return -1;
@@ -792,16 +905,9 @@ static int sd_render_ndt(const sd_render_args &a, const sd_mlp &m, const LdsPlan
 }
 
 template <int P>
-static int sd_render_nv(const sd_render_args &a, const sd_mlp &m, const LdsPlan &pl, int nblk,
+static int sd_render_nv(const sd_render_args &a, const sd_mlp &m, const LdsPlan &pl,
                         hipStream_t s) {
-    return a.nv == 1 ? sd_render_ndt<P, 1>(a, m, pl, nblk, s) : sd_render_ndt<P, 0>(a, m, pl, nblk, s);
-}
-
-static int sd_render_dispatch(const sd_render_args &a, const sd_mlp &m, const LdsPlan &pl,
-                              int nblk, hipStream_t s) {
-    if (m.dtype == SD_F16) return sd_render_nv<SD_F16>(a, m, pl, nblk, s);
-    if (m.dtype == SD_BF16) return sd_render_nv<SD_BF16>(a, m, pl, nblk, s);
-    return sd_render_nv<SD_F32>(a, m, pl, nblk, s);
+    return a.nv == 1 ? sd_render_ndt<P, 1>(a, m, pl, s) : sd_render_ndt<P, 0>(a, m, pl, s);
 }
 
 extern "C" int sd_render_fused(const sd_render_args *args, const sd_mlp *mlp, void *stream) {
@@ -815,15 +921,17 @@ extern "C" int sd_render_fused(const sd_render_args *args, const sd_mlp *mlp, vo
     if (a.R < 0 || a.K <= 0 || (a.K % 32) || a.ray_dim < 6 || a.rays_per_sb <= 0 || !a.rays ||
         !a.z || !a.grid || !a.cam_f || !a.depth || !a.dino || a.Hf <= 0 || a.Wf <= 0 ||
         a.nv < 0 || a.nv > SD_MAX_NV || mlp->D > 128 ||
+        (int64_t)a.Hf * a.Wf * mlp->C * (mlp->dtype == SD_F32 ? 4 : 2) >= (1LL << 32) ||
         (a.nv > 0 && (!a.img || !a.cam_c || !a.rgb || a.Hc <= 0 || a.Wc <= 0))) {
-        sd_set_error("sd_render_fused: invalid argument (K % 32 == 0, nv <= 4, D <= 128)");
+        sd_set_error("sd_render_fused: invalid argument (K % 32 == 0, nv <= 4, D <= 128, "
+                     "grid plane < 4 GiB)");
         return -1;
     }
     if (a.R == 0) return 0;
-    int64_t nblk = (a.R + SD_WAVES - 1) / SD_WAVES;
-    if (nblk > sd_num_cus()) nblk = sd_num_cus();
     hipStream_t s = (hipStream_t)stream;
-    return sd_render_dispatch(a, *mlp, pl, (int)nblk, s);
+    if (mlp->dtype == SD_F16) return sd_render_nv<SD_F16>(a, *mlp, pl, s);
+    if (mlp->dtype == SD_BF16) return sd_render_nv<SD_BF16>(a, *mlp, pl, s);
+    return sd_render_nv<SD_F32>(a, *mlp, pl, s);
 }
 
 extern "C" int sd_field_query(const sd_field_args *args, const sd_mlp *mlp, void *stream) {
@@ -836,18 +944,17 @@ extern "C" int sd_field_query(const sd_field_args *args, const sd_mlp *mlp, void
     const sd_field_args &a = *args;
     if (a.B <= 0 || a.P < 0 || !a.xyz || !a.grid || !a.cam_f || !a.sigma || !a.dino ||
         a.Hf <= 0 || a.Wf <= 0 || a.nv < 0 || a.nv > SD_MAX_NV ||
+        a.B * (int64_t)a.Hf * a.Wf * mlp->C * (mlp->dtype == SD_F32 ? 4 : 2) >= (1LL << 32) ||
         (a.nv > 0 && (a.rgb || a.invalid) && (!a.img || !a.cam_c || a.Hc <= 0 || a.Wc <= 0))) {
-        sd_set_error("sd_field_query: invalid argument");
+        sd_set_error("sd_field_query: invalid argument (all grid planes < 4 GiB)");
         return -1;
     }
     if (a.P == 0) return 0;
-    int64_t ntiles = (a.B * a.P + 31) / 32;
-    int64_t nblk = (ntiles + SD_WAVES - 1) / SD_WAVES;
-    if (nblk > sd_num_cus()) nblk = sd_num_cus();
+    const int64_t ntiles = (a.B * a.P + 31) / 32;
     hipStream_t s = (hipStream_t)stream;
-    if (mlp->dtype == SD_F16) return sd_launch(k_field<SD_F16>, (int)nblk, pl, s, a, *mlp);
-    if (mlp->dtype == SD_BF16) return sd_launch(k_field<SD_BF16>, (int)nblk, pl, s, a, *mlp);
-    return sd_launch(k_field<SD_F32>, (int)nblk, pl, s, a, *mlp);
+    if (mlp->dtype == SD_F16) return sd_launch<SD_F16>(k_field<SD_F16>, ntiles, pl, s, a, *mlp);
+    if (mlp->dtype == SD_BF16) return sd_launch<SD_BF16>(k_field<SD_BF16>, ntiles, pl, s, a, *mlp);
+    return sd_launch<SD_F32>(k_field<SD_F32>, ntiles, pl, s, a, *mlp);
 }
 
 extern "C" int sd_composite(const float *z, const float *sigma, const float *feat, int64_t F,
