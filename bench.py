@@ -86,39 +86,35 @@ def make_scene(frame_seed: int, device, precision="bf16", offset_pose=False):
     return net, renderer, wrapper, sampler, render_pose, Ks
 
 
-def render_step(net, wrapper, sampler, pose, Ks, timer=None):
-    net._grid_cache = None  # re-pack the (freshly encoded) feature grid every frame
+def render_step(net, wrapper, sampler, pose, Ks):
+    net._grid_cache = None  # re-pack / re-project the (freshly encoded) grid every frame
     rays, _ = sampler.sample(None, pose, Ks)
-    if timer is not None:
-        timer.start()
-    out = wrapper(rays, want_weights=False, want_alphas=False)
-    if timer is not None:
-        timer.stop()
-    return out
+    return wrapper(rays, want_weights=False, want_alphas=False)
 
 
 class KernelTimer:
-    """HIP events around the fused render on the stream it is launched on."""
+    """HIP events around named kernel launches (BTSNet.kernel_timer hook), recorded on
+    the stream the kernels are launched on (torch's current stream)."""
 
     def __init__(self):
-        self.pairs = []
+        self.pairs = {}
         self.on = False
 
-    def start(self):
+    def start(self, name):
         if self.on:
             e = torch.cuda.Event(enable_timing=True)
             e.record(torch.cuda.current_stream())
-            self.pairs.append([e, None])
+            self.pairs.setdefault(name, []).append([e, None])
 
-    def stop(self):
+    def stop(self, name):
         if self.on:
             e = torch.cuda.Event(enable_timing=True)
             e.record(torch.cuda.current_stream())
-            self.pairs[-1][1] = e
+            self.pairs[name][-1][1] = e
 
-    def mean_ms(self):
-        ts = [a.elapsed_time(b) for a, b in self.pairs]
-        return sum(ts) / max(len(ts), 1)
+    def mean_ms(self, name):
+        ts = [a.elapsed_time(b) for a, b in self.pairs.get(name, [])]
+        return sum(ts) / len(ts) if ts else 0.0
 
 
 def cpu_baseline(budget_s: float = 20.0):
@@ -178,6 +174,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp16", "fp32"])
     ap.add_argument("--offset-pose", action="store_true")
+    ap.add_argument("--mode", default="proj", choices=["proj", "grid"],
+                    help="16-bit render kernel: projected grid (default) or per-sample grid")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     args = ap.parse_args()
@@ -199,19 +197,17 @@ def main():
     R = H * W
     gather_bufs = None
     if dist:
-        import torch.distributed as tdist
-        maps = torch.empty(R, 1 + D_DINO + 3, device=device)
-        gather_bufs = [torch.empty_like(maps) for _ in range(world)]
+        from scenedino_amd import distributed as sdd
+        gather_bufs = [torch.empty(R, 1 + D_DINO + 3, device=device) for _ in range(world)]
 
+    net.fused_mode = args.mode
     timer = KernelTimer()
+    net.kernel_timer = timer
 
     def step():
-        out = render_step(net, wrapper, sampler, pose, Ks, timer)
-        if dist:
-            c = out["coarse"]
-            maps = torch.cat((c["depth"].reshape(R, 1), c["dino_features"].reshape(R, D_DINO),
-                              c["rgb"].reshape(R, 3)), 1)
-            tdist.all_gather(gather_bufs, maps)
+        out = render_step(net, wrapper, sampler, pose, Ks)
+        if dist:  # frame f on rank f; one RCCL all-gather of the packed rendered maps
+            sdd.gather_maps(sdd.pack_maps(out["coarse"]), out=gather_bufs)
         return out
 
     for _ in range(args.warmup):
@@ -229,18 +225,27 @@ def main():
         tdist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kern_ms = timer.mean_ms()
+    render_ms, proj_ms = timer.mean_ms("render"), timer.mean_ms("project")
     if dist:
-        t = torch.tensor([elapsed, kern_ms], device=device, dtype=torch.float64)
+        t = torch.tensor([elapsed, render_ms, proj_ms], device=device, dtype=torch.float64)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
+        elapsed, render_ms, proj_ms = float(t[0]), float(t[1]), float(t[2])
 
     if rank == 0:
         total_rays = world * R * args.steps
         ms_per_step = 1e3 * elapsed / args.steps
+        # SURVEY §8(d) algorithmic work: 92,160 FLOP per point (the reference MLP),
+        # over the kernels that turn the encoded grid into rendered maps
+        proj = net._use_proj()
+        kern_ms = render_ms + proj_ms
         flops = R * K_SAMPLES * mlp_flops_per_point()
         achieved = flops / (kern_ms * 1e-3) / 1e12
         peak = PEAK_TFLOPS[args.precision]
+        if proj:  # what the matrix cores actually execute (P = W G projection + code/head)
+            exec_flops = (HF * WF * 2 * C_GRID * D_HIDDEN
+                          + R * K_SAMPLES * 2 * (39 * D_HIDDEN + D_HIDDEN * (1 + D_DINO)))
+        else:
+            exec_flops = flops
         line = {
             "metric": "rendered rays/sec, KITTI-360 192x640x64-sample frustum",
             "value": total_rays / elapsed,
@@ -265,7 +270,8 @@ def main():
                 ("+rccl_allgather" if world > 1 else ""),
             },
             "roofline": {
-                "kernel": "k_render (sd_render_fused)",
+                "kernel": ("k_project + k_render_proj (sd_project_grid + sd_render_proj)"
+                           if proj else "k_render (sd_render_fused)"),
                 "bound": "mfma",
                 "achieved": achieved,
                 "peak": peak,
@@ -273,7 +279,11 @@ def main():
                 "frac": achieved / peak,
                 "traffic": None,
                 "kernel_ms": kern_ms,
+                "render_kernel_ms": render_ms,
+                "project_kernel_ms": proj_ms,
                 "algorithmic_flops_per_launch": flops,
+                "executed_mfma_flops_per_launch": exec_flops,
+                "executed_tflops": exec_flops / (kern_ms * 1e-3) / 1e12,
             },
         }
         if not args.no_cpu_baseline and world == 1:

@@ -111,6 +111,37 @@ typedef struct sd_render_args {
 
 int sd_render_fused(const sd_render_args *args, const sd_mlp *mlp, void *stream);
 
+/* ---- projected-grid render (16-bit modes) ----------------------------------
+ * F.grid_sample is linear in the grid and its bilinear weights sum to one, so the
+ * grid part of ResnetFC's first layer commutes with the feature gather
+ * (bts.py:299-328 then resnetfc.py:163):
+ *     W_in[:, :C] . sample(G, xy) + b_in  ==  sample(W_in[:, :C] . G + b_in, xy).
+ * sd_project_grid evaluates P = W_in[:, :C] . G + b_in once per grid PIXEL (an MFMA
+ * GEMM over C); sd_render_proj then gathers 128-channel P taps per sample and adds
+ * the positional-code columns by MFMA.  Same outputs as sd_render_fused up to
+ * rounding order (16-bit modes only; the f32 parity mode keeps sd_render_fused). */
+
+/* grid_nchw (B, C, Hf, Wf) float32 -> out (B, Hf, Wf, 128) in mlp->dtype (BF16/F16).
+ * Uses mlp->w_in chunks 0..C/16-1 and mlp->b_in_h. */
+int sd_project_grid(const float *grid_nchw, int64_t B, int64_t Hf, int64_t Wf,
+                    const sd_mlp *mlp, void *out, void *stream);
+
+/* Head of the projected render: code columns of W_in and the output layer, packed
+ * for 16x16x32 MFMA (scenedino_amd/mlp_pack.py documents the fragment maps). */
+typedef struct sd_head {
+    const void *w_pe;      /* [2][8][64][8] code-column A fragments, dtype           */
+    const void *w_sig;     /* [4][64][8]    W_out row 0 (sigma) A fragments, dtype    */
+    const void *w_out;     /* [D/16][4][64][8] W_out rows 1..D A fragments, dtype     */
+    const float *b_dino;   /* b_out[1:1+D]                                            */
+    float b_sigma;         /* b_out[0]                                                */
+    int32_t D;             /* 32, 64 or 128                                           */
+    int32_t dtype;         /* SD_BF16 or SD_F16                                       */
+} sd_head;
+
+/* args->grid = the projected grid (B, Hf, Wf, 128) from sd_project_grid; K % 16 == 0.
+ * Outputs as sd_render_fused. */
+int sd_render_proj(const sd_render_args *args, const sd_head *head, void *stream);
+
 /* Per-point field query without compositing (BTSNet.forward on raw points,
  * bts.py:476-595; SSCBench predict_grid / demo inference_3d).  Points are
  * (B, P, 3); outputs sigma (B,P), dino (B,P,D); colour outputs optional. */

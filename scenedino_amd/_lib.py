@@ -12,7 +12,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsdhip.so")
+# SDHIP_LIB: alternative build of the same library (diagnostic builds only)
+LIB_PATH = os.environ.get("SDHIP_LIB") or os.path.join(_HERE, "libsdhip.so")
 ABI_VERSION = 1
 
 SD_F32 = 0
@@ -30,6 +31,13 @@ class SdMlp(ctypes.Structure):
         ("w_in", _vp), ("b_in_h", _vp), ("w_sig_h", _vp), ("b_sigma", ctypes.c_float),
         ("w_out", _vp), ("b_dino", _vp),
         ("C", _i32), ("D", _i32), ("dtype", _i32), ("d_hidden", _i32),
+    ]
+
+
+class SdHead(ctypes.Structure):
+    _fields_ = [
+        ("w_pe", _vp), ("w_sig", _vp), ("w_out", _vp), ("b_dino", _vp),
+        ("b_sigma", ctypes.c_float), ("D", _i32), ("dtype", _i32),
     ]
 
 
@@ -70,6 +78,8 @@ SIGNATURES = {
     "sd_pack_image": [_vp, _i64, _i64, _i64, _vp, _vp],
     "sd_render_fused": [ctypes.POINTER(SdRenderArgs), ctypes.POINTER(SdMlp), _vp],
     "sd_field_query": [ctypes.POINTER(SdFieldArgs), ctypes.POINTER(SdMlp), _vp],
+    "sd_project_grid": [_vp, _i64, _i64, _i64, ctypes.POINTER(SdMlp), _vp, _vp],
+    "sd_render_proj": [ctypes.POINTER(SdRenderArgs), ctypes.POINTER(SdHead), _vp],
     "sd_composite": [_vp, _vp, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp,
                      _vp],
 }
@@ -174,6 +184,22 @@ def render_fused(args: SdRenderArgs, mlp: SdMlp, ref_tensor):
     lib = load()
     _check(lib.sd_render_fused(ctypes.byref(args), ctypes.byref(mlp), stream_of(ref_tensor)),
            "sd_render_fused")
+
+
+def project_grid(grid_nchw, mlp: SdMlp, dtype):
+    """P = W_in[:, :C] . grid + b_in per pixel: (B, Hf, Wf, 128) in dtype."""
+    lib = load()
+    B, C, H, W = grid_nchw.shape
+    out = torch.empty(B, H, W, 128, device=grid_nchw.device, dtype=TORCH_DTYPE[dtype])
+    _check(lib.sd_project_grid(ptr(_req(grid_nchw, "grid")), B, H, W, ctypes.byref(mlp),
+                               ptr(out), stream_of(out)), "sd_project_grid")
+    return out
+
+
+def render_proj(args: SdRenderArgs, head: SdHead, ref_tensor):
+    lib = load()
+    _check(lib.sd_render_proj(ctypes.byref(args), ctypes.byref(head), stream_of(ref_tensor)),
+           "sd_render_proj")
 
 
 def field_query(args: SdFieldArgs, mlp: SdMlp, ref_tensor):

@@ -33,12 +33,16 @@ __device__ __forceinline__ float bf16hi(uint32_t d) { return __uint_as_float(d &
 
 // Camera record: w2c rows 0..2 (3x4) then normalised K (3x3).
 // pts_into_camera (pinhole.py:40-59) followed by project_to_image (pinhole.py:62-84).
-__device__ __forceinline__ void sd_project(const float *__restrict__ cam, float px, float py,
+// CP: const float * or a constant-address-space pointer (scalar loads of a
+// wave-uniform record).
+typedef __attribute__((address_space(4))) const float sd_cfloat;
+template <typename CP>
+__device__ __forceinline__ void sd_project(CP cam, float px, float py,
                                            float pz, float &x, float &y, float &zc) {
     float c0 = ((cam[0] * px + cam[1] * py) + cam[2] * pz) + cam[3];
     float c1 = ((cam[4] * px + cam[5] * py) + cam[6] * pz) + cam[7];
     float c2 = ((cam[8] * px + cam[9] * py) + cam[10] * pz) + cam[11];
-    const float *K = cam + 12;
+    CP K = cam + 12;
     float i0 = (K[0] * c0 + K[1] * c1) + K[2] * c2;
     float i1 = (K[3] * c0 + K[4] * c1) + K[5] * c2;
     float i2 = (K[6] * c0 + K[7] * c1) + K[8] * c2;

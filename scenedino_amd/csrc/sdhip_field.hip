@@ -31,12 +31,9 @@
 // ResnetFC.forward (models/prediction_heads/resnetfc.py:135-203),
 // PositionalEncoding + encoding_mode._z (common/positional_encoding.py:13-80),
 // pinhole projection (common/cameras/pinhole.py:40-112).
-#include "sdhip_common.h"
+#include "sdhip_point.h"
 
 #include <string.h>
-
-typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
-typedef __attribute__((ext_vector_type(2))) _Float16 f16x2;
 
 static thread_local char g_err[512] = "";
 extern "C" void sd_set_error(const char *msg) {
@@ -52,32 +49,6 @@ template <int P> struct WG {
     static constexpr int T = P == SD_F32 ? 256 : 512;
     static constexpr int W = T / 64;
 };
-
-// ---------------------------------------------------------------------------
-// per-point geometry
-// ---------------------------------------------------------------------------
-struct PointGeo {
-    Taps t;
-    float v[3];   // [x, y, z~] inputs of the positional code (after clamp(-2,2))
-    bool inv_f;   // outside the encoder frustum
-};
-
-__device__ __forceinline__ PointGeo sd_point_geo(const float *__restrict__ cam, float px, float py,
-                                                 float pz, int Wf, int Hf) {
-    PointGeo g;
-    float x, y, zc;
-    sd_project(cam, px, py, pz, x, y, zc);
-    g.inv_f = sd_outside(x, y, zc);
-    x = fminf(fmaxf(x, -2.f), 2.f);
-    y = fminf(fmaxf(y, -2.f), 2.f);
-    // encoding_mode._z, inv_z, d_min=3, d_max=80 (positional_encoding.py:13-21).
-    // (1/d_min - 1/d_max) is a Python double rounded once to fp32, as in the reference.
-    float zt = (1.f / fmaxf(zc, SD_EPS) - (float)(1.0 / 80.0)) / (float)(1.0 / 3.0 - 1.0 / 80.0);
-    zt = 2.f * zt - 1.f;
-    g.v[0] = x; g.v[1] = y; g.v[2] = zt;
-    g.t = sd_taps(x, y, Wf, Hf);
-    return g;
-}
 
 // Positional-code chunk pc (0..2) for lane half h: fragment element j = slot s = 8pc+j.
 // s < 18: sin(phase_h + v[s%3] * 1.5*2^(s/3)) with phase_h = h*float32(pi/2) (cos as
@@ -119,10 +90,6 @@ __device__ __forceinline__ TapOff sd_tapoff(const Taps &t, int C, int esz, int h
     return {t.i00 * row + lo, t.i01 * row + lo, t.i10 * row + lo, t.i11 * row + lo};
 }
 
-__device__ __forceinline__ uint4 sd_ld128(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff) {
-    return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
-}
-
 __device__ __forceinline__ Raw16 sd_load16(__amdgpu_buffer_rsrc_t rs, const TapOff &o, int q) {
     const uint32_t s = (uint32_t)q * 32u;
     Raw16 r;
@@ -131,16 +98,6 @@ __device__ __forceinline__ Raw16 sd_load16(__amdgpu_buffer_rsrc_t rs, const TapO
     r.c = sd_ld128(rs, o.o10, s);
     r.d = sd_ld128(rs, o.o11, s);
     return r;
-}
-
-// Buffer descriptor over one batch element's grid plane (wave-uniform inputs).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t sd_rsrc(const void *base, uint32_t bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, bytes, 0x00020000);
-}
-
-// ReLU without the canonicalising v_max hipcc adds in front of fmaxf on MFMA results
-__device__ __forceinline__ float sd_relu(float x) {
-    return __builtin_amdgcn_fmed3f(x, 0.f, __builtin_inff());
 }
 
 template <> struct Prec<SD_BF16> {
@@ -320,14 +277,6 @@ template <> struct Prec<SD_F32> {
     }
 };
 
-// An opaque zero: indexing LDS with it stops LICM from hoisting the per-sub-tile
-// weight reads out of the loop (which would pin ~100 VGPRs and spill).
-__device__ __forceinline__ int sd_opaque0() {
-    int z = 0;
-    asm volatile("" : "+v"(z));
-    return z;
-}
-
 // One pipeline step: blend chunk q from r, refill r with chunk q + DEPTH (compile-time
 // LOAD: the tail steps issue no loads), then the 4 (or 32 f32) MFMAs of chunk q.
 #define SD_STEP(r, qq, LOAD)                                                  \
@@ -412,33 +361,6 @@ __device__ __forceinline__ float sd_relu_sigma(f32x16 acc[4], const float *lds_w
         }
     }
     return s;
-}
-
-// torch.nn.functional.softplus(beta=1, threshold=20)
-__device__ __forceinline__ float sd_softplus(float x) { return x > 20.f ? x : log1pf(expf(x)); }
-
-__device__ __forceinline__ void sd_sample_rgb(const float *__restrict__ img, const Taps &t,
-                                              float out[3]) {
-    f32x4 a = *(const f32x4 *)(img + (int64_t)t.i00 * 4);
-    f32x4 b = *(const f32x4 *)(img + (int64_t)t.i01 * 4);
-    f32x4 c = *(const f32x4 *)(img + (int64_t)t.i10 * 4);
-    f32x4 d = *(const f32x4 *)(img + (int64_t)t.i11 * 4);
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-        out[i] = ((a[i] * t.w00 + b[i] * t.w01) + c[i] * t.w10) + d[i] * t.w11;
-}
-
-// colour sample + validity in a render view (bts.py:336-346; clamp before the frustum test)
-__device__ __forceinline__ bool sd_color_view(const float *cam, const float *img, int Wc, int Hc,
-                                              float px, float py, float pz, float col[3]) {
-    float x, y, zc;
-    sd_project(cam, px, py, pz, x, y, zc);
-    x = fminf(fmaxf(x, -2.f), 2.f);
-    y = fminf(fmaxf(y, -2.f), 2.f);
-    bool inv = sd_outside(x, y, zc);
-    Taps tc = sd_taps(x, y, Wc, Hc);
-    sd_sample_rgb(img, tc, col);
-    return inv;
 }
 
 // LDS image: [W_in fragments | W_out fragments (if they fit) | b_in rows | w_sigma rows]
@@ -838,17 +760,6 @@ k_composite(const float *__restrict__ z, const float *__restrict__ sigma,
 // ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
-static int sd_num_cus() {
-    static int n = 0;
-    if (!n) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-            n = 256;
-    }
-    return n;
-}
-
 static int sd_plan(const sd_mlp *m, LdsPlan *pl) {
     if (!m || !m->w_in || !m->b_in_h || !m->w_sig_h || !m->w_out || !m->b_dino) {
         sd_set_error("sd_mlp: null parameter pointer");

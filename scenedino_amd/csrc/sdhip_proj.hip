@@ -1,0 +1,578 @@
+// sdhip_proj.hip -- projected-grid feature-field render (gfx950 / CDNA4, 16-bit modes).
+//
+// F.grid_sample (bilinear, border, align_corners=False; bts.py:299-309) is linear in
+// the grid and its four weights sum to one, so the grid columns of ResnetFC's first
+// layer (resnetfc.py:163) commute with the gather:
+//     W_in[:, :C] . sample(G, xy) + b_in  ==  sample(P, xy),   P = W_in[:, :C] . G + b_in.
+// k_project evaluates P once per grid pixel (B*Hf*Wf x 128 x C MFMA GEMM, HBM-bound on
+// reading G); k_render_proj gathers 4 taps x 128 P channels per sample (half of the
+// C = 256 grid channels) and needs only the 39 code columns per sample on the matrix
+// cores: the per-sample first-layer contraction drops from K = 295 to K = 39.
+//
+// Render work unit: one wave = one ray at a time, in items of 16 consecutive samples
+// (16x16x32 MFMA; lane l: sample j = l & 15, group g = l >> 4).  Per item:
+//   hidden (16 x 16 tile t = rows 16t..16t+15, 8 tiles) =
+//       I . blend(P taps)            one identity MFMA per tile (chunk q = t / 2)
+//     + W_code . code                2 code chunks x 8 tiles
+//   -> ReLU -> 16-bit X fragments (accumulator-as-operand: element e of fragment s of
+//      group g is hidden 32 s + 16 (e >> 2) + 4 g + (e & 3))
+//   sigma^T  = W_sigma . X^T         4 MFMAs, every row = sigma of sample j
+//   dino^T   = W_dino  . X^T         4 MFMAs per 16 dims, weighted by w_j and summed
+//                                    over the ray's samples in registers.
+// Compositing (nerf.py:376-405): alpha, DPP prefix product of (1-alpha+1e-10) over the
+// 16 samples of an item (+ carry across items), weights, depth, colour (group g
+// samples render view g), DINO; the ray epilogue reduces over the 16 sample lanes.
+// Pipelining: the z values of item i+2 and the P-tap loads of item i+1 are in flight
+// while item i computes.
+#include "sdhip_point.h"
+
+#define SD_PWG 256  // threads per workgroup (4 waves); several workgroups per CU
+
+// 16-bit element traits
+template <int P> struct T16;
+template <> struct T16<SD_F16> {
+    typedef f16x8 Frag;
+    typedef _Float16 E;
+    static __device__ __forceinline__ f32x4 mma(const Frag &a, const Frag &b, const f32x4 &c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ f32x16 mma32(const Frag &a, const Frag &b, const f32x16 &c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ uint16_t bits(float f) {
+        return __builtin_bit_cast(uint16_t, (_Float16)f);
+    }
+    // packed-f16 bilinear blend of 8 channels from the 4 taps
+    static __device__ __forceinline__ Frag blend(const uint4 &a, const uint4 &b, const uint4 &c,
+                                                 const uint4 &d, const float w[4]) {
+        const f16x2 w0 = {(_Float16)w[0], (_Float16)w[0]}, w1 = {(_Float16)w[1], (_Float16)w[1]};
+        const f16x2 w2 = {(_Float16)w[2], (_Float16)w[2]}, w3 = {(_Float16)w[3], (_Float16)w[3]};
+        const uint32_t A[4] = {a.x, a.y, a.z, a.w}, B[4] = {b.x, b.y, b.z, b.w};
+        const uint32_t C[4] = {c.x, c.y, c.z, c.w}, D[4] = {d.x, d.y, d.z, d.w};
+        Frag o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            f16x2 v = __builtin_bit_cast(f16x2, A[i]) * w0;
+            v = __builtin_elementwise_fma(__builtin_bit_cast(f16x2, B[i]), w1, v);
+            v = __builtin_elementwise_fma(__builtin_bit_cast(f16x2, C[i]), w2, v);
+            v = __builtin_elementwise_fma(__builtin_bit_cast(f16x2, D[i]), w3, v);
+            o[2 * i] = v[0];
+            o[2 * i + 1] = v[1];
+        }
+        return o;
+    }
+};
+template <> struct T16<SD_BF16> {
+    typedef bf16x8 Frag;
+    typedef __bf16 E;
+    static __device__ __forceinline__ f32x4 mma(const Frag &a, const Frag &b, const f32x4 &c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ f32x16 mma32(const Frag &a, const Frag &b, const f32x16 &c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ uint16_t bits(float f) {
+        return __builtin_bit_cast(uint16_t, (__bf16)f);
+    }
+    // fp32 blend of the bf16 taps, one rounding to bf16
+    static __device__ __forceinline__ Frag blend(const uint4 &a, const uint4 &b, const uint4 &c,
+                                                 const uint4 &d, const float w[4]) {
+        const uint32_t A[4] = {a.x, a.y, a.z, a.w}, B[4] = {b.x, b.y, b.z, b.w};
+        const uint32_t C[4] = {c.x, c.y, c.z, c.w}, D[4] = {d.x, d.y, d.z, d.w};
+        Frag o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float lo = fmaf(bf16lo(D[i]), w[3], fmaf(bf16lo(C[i]), w[2],
+                            fmaf(bf16lo(B[i]), w[1], bf16lo(A[i]) * w[0])));
+            float hi = fmaf(bf16hi(D[i]), w[3], fmaf(bf16hi(C[i]), w[2],
+                            fmaf(bf16hi(B[i]), w[1], bf16hi(A[i]) * w[0])));
+            o[2 * i] = (__bf16)lo;
+            o[2 * i + 1] = (__bf16)hi;
+        }
+        return o;
+    }
+};
+
+// ---------------------------------------------------------------------------
+// k_project: P[b][pix][n] = sum_c W_in[n][c] G[b][c][pix] + b_in[n]   (n < 128)
+// One wave = 32 pixels x 128 hidden = 4 tiles of 32x32x16; K = C in chunks of 16.
+// A = the sd_mlp layer-1 fragments of the grid columns (LDS); B = 8 channels of the
+// lane's pixel read from NCHW (32 consecutive floats per channel across a half).
+// ---------------------------------------------------------------------------
+template <int P>
+__global__ void __launch_bounds__(SD_PWG)
+k_project(const float *__restrict__ grid, int64_t B, int C, int64_t HW, const sd_mlp m,
+          uint16_t *__restrict__ out) {
+    typedef T16<P> Tr;
+    typedef typename Tr::Frag Frag;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int nq = C >> 4;
+    {
+        const uint4 *src = (const uint4 *)m.w_in;
+        uint4 *dst = (uint4 *)lds;
+        for (int i = threadIdx.x; i < nq * 4 * SD_WAVE; i += blockDim.x) dst[i] = src[i];
+        __syncthreads();
+    }
+    const Frag *lw = (const Frag *)lds;
+    const int lane = threadIdx.x & 63, h = lane >> 5, li = lane & 31;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t ntile = (HW + 31) / 32, total = B * ntile;
+    for (int64_t task = (int64_t)blockIdx.x * (SD_PWG / 64) + wave; task < total;
+         task += (int64_t)gridDim.x * (SD_PWG / 64)) {
+        const int64_t b = task / ntile;
+        const int64_t pix = (task - b * ntile) * 32 + li;
+        const bool valid = pix < HW;
+        const float *gp = grid + b * C * HW + (valid ? pix : HW - 1) + (int64_t)(8 * h) * HW;
+        f32x16 acc[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const f32x4 *bb = (const f32x4 *)(m.b_in_h + (t * 2 + h) * 16);
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+                f32x4 v = bb[q4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc[t][4 * q4 + i] = v[i];
+            }
+        }
+        float x[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] = gp[e * HW];
+        for (int q = 0; q < nq; ++q) {
+            Frag f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) f[e] = (typename Tr::E)x[e];
+            if (q + 1 < nq) {
+                const float *gn = gp + (int64_t)(16 * (q + 1)) * HW;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) x[e] = gn[e * HW];
+            }
+#pragma unroll
+            for (int t = 0; t < 4; ++t) acc[t] = Tr::mma32(lw[(q * 4 + t) * SD_WAVE + lane], f, acc[t]);
+        }
+        if (valid) {
+            uint16_t *op = out + (b * HW + pix) * SD_DH;
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int r4 = 0; r4 < 4; ++r4) {
+                    // accumulator rows 4 r4 .. 4 r4 + 3 = hidden 32 t + 8 r4 + 4 h + 0..3
+                    uint2 v;
+                    v.x = (uint32_t)Tr::bits(acc[t][4 * r4]) | ((uint32_t)Tr::bits(acc[t][4 * r4 + 1]) << 16);
+                    v.y = (uint32_t)Tr::bits(acc[t][4 * r4 + 2]) | ((uint32_t)Tr::bits(acc[t][4 * r4 + 3]) << 16);
+                    *(uint2 *)(op + 32 * t + 8 * r4 + 4 * h) = v;
+                }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// render helpers
+// ---------------------------------------------------------------------------
+// DPP with "old" = 1.0 for lanes whose source is outside the row (bound_ctrl off)
+#define SD_DPP1(x, ctrl) \
+    __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, 1.f), \
+                                                          __builtin_bit_cast(int, (x)), (ctrl), 0xf, 0xf, false))
+#define SD_DPP0(x, ctrl) \
+    __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, (x)), (ctrl), 0xf, 0xf, false))
+
+// inclusive product scan over the 16 lanes of every row (row_shr 1, 2, 4, 8)
+__device__ __forceinline__ float sd_scan_mul16(float x) {
+    x *= SD_DPP1(x, 0x111);
+    x *= SD_DPP1(x, 0x112);
+    x *= SD_DPP1(x, 0x114);
+    x *= SD_DPP1(x, 0x118);
+    return x;
+}
+// sum over the 16 lanes of every row, result in every lane (row_ror 8, 4, 2, 1)
+__device__ __forceinline__ float sd_rowsum16(float x) {
+    x += SD_DPP0(x, 0x128);
+    x += SD_DPP0(x, 0x124);
+    x += SD_DPP0(x, 0x122);
+    x += SD_DPP0(x, 0x121);
+    return x;
+}
+
+// sin for the 16-bit modes: one revolution-domain range reduction, then v_sin_f32
+__device__ __forceinline__ float sd_sin_fast(float x) {
+    return __builtin_amdgcn_sinf(__builtin_amdgcn_fractf(x * 0.15915494309189535f));
+}
+
+// Positional-code fragment of chunk pc for lane group g (element e):
+//   G = 2 pc + (g >> 1), phase = g & 1 (0: sin, 1: cos = sin(x + pi/2))
+//   G < 3, e < 6 : sin(fmaf(v[e % 3], 1.5 * 2^(2G + (e >= 3)), phase * pi/2))
+//   G = 0, e >= 6: raw inputs (g = 0: x, y; g = 1: z~, 0)
+//   otherwise 0.   (scenedino_amd/mlp_pack.py: proj_pe_col gives the W_in column.)
+template <typename Frag, typename E>
+__device__ __forceinline__ Frag sd_code_frag(const float v[3], int pc, int g) {
+    const float phase = (g & 1) ? 1.5707963705062866f : 0.f;
+    const float lscale = (g >> 1) ? 4.f : 1.f;
+    const bool on = 2 * pc + (g >> 1) < 3;
+    Frag o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        float r;
+        if (e < 6) {
+            const float f = 1.5f * (float)(1 << (4 * pc + (e >= 3 ? 1 : 0))) * lscale;
+            r = on ? sd_sin_fast(fmaf(v[e % 3], f, phase)) : 0.f;
+        } else if (pc == 0) {
+            r = (g >> 1) ? 0.f : (g == 0 ? v[e - 6] : (e == 6 ? v[2] : 0.f));
+        } else {
+            r = 0.f;
+        }
+        o[e] = (E)r;
+    }
+    return o;
+}
+
+struct PItem {
+    int64_t ray, sbi;
+    int sub;
+    float zk, delta, px, py, pz;
+    float v[3];
+    float w[4];
+    uint32_t o[4];  // tap byte offsets (+ 16 g) inside the batch element's P plane
+    bool inv_f;
+    __amdgpu_buffer_rsrc_t rs;
+};
+
+struct PRaw { uint4 a, b, c, d; };
+
+__device__ __forceinline__ PRaw sd_pload(const PItem &it, int q) {
+    const uint32_t s = (uint32_t)q * 64u;
+    PRaw r;
+    r.a = sd_ld128(it.rs, it.o[0], s);
+    r.b = sd_ld128(it.rs, it.o[1], s);
+    r.c = sd_ld128(it.rs, it.o[2], s);
+    r.d = sd_ld128(it.rs, it.o[3], s);
+    return r;
+}
+
+// LDS image of the render kernel: [identity 2][64] | [code 2][8][64] | [sigma 4][64] |
+// [dino D/16][4][64], 16 B per lane entry
+#define SD_LDS_ID 0
+#define SD_LDS_PE (2 * SD_WAVE)
+#define SD_LDS_SIG (SD_LDS_PE + 16 * SD_WAVE)
+#define SD_LDS_OUT (SD_LDS_SIG + 4 * SD_WAVE)
+
+template <int P, int NV, int NDT>
+__global__ void __launch_bounds__(SD_PWG)
+k_render_proj(const sd_render_args a, const sd_head m) {
+    typedef T16<P> Tr;
+    typedef typename Tr::Frag Frag;
+    typedef typename Tr::E E;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    {
+        uint4 *d = (uint4 *)lds;
+        for (int i = threadIdx.x; i < 2 * SD_WAVE; i += blockDim.x) {
+            // identity fragments: A[i][k] = 1 iff k == i (tile 2q) / k == 16 + i (tile 2q+1)
+            const int which = i / SD_WAVE, l = i % SD_WAVE, ii = l & 15, gg = l >> 4;
+            Frag f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) f[e] = (E)((8 * gg + e == ii + 16 * which) ? 1.f : 0.f);
+            d[SD_LDS_ID + i] = __builtin_bit_cast(uint4, f);
+        }
+        const uint4 *pe = (const uint4 *)m.w_pe, *sg = (const uint4 *)m.w_sig,
+                    *wo = (const uint4 *)m.w_out;
+        for (int i = threadIdx.x; i < 16 * SD_WAVE; i += blockDim.x) d[SD_LDS_PE + i] = pe[i];
+        for (int i = threadIdx.x; i < 4 * SD_WAVE; i += blockDim.x) d[SD_LDS_SIG + i] = sg[i];
+        for (int i = threadIdx.x; i < NDT * 4 * SD_WAVE; i += blockDim.x) d[SD_LDS_OUT + i] = wo[i];
+        __syncthreads();
+    }
+    const Frag *lf = (const Frag *)lds;
+
+    const int lane = threadIdx.x & 63, j = lane & 15, g = lane >> 4;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int K = a.K, nsub = K >> 4, nv = NV > 0 ? NV : a.nv;
+    const uint32_t plane_bytes = (uint32_t)a.Hf * a.Wf * SD_DH * 2;
+    const int64_t cplane = (int64_t)a.Hc * a.Wc * 4;
+    const int64_t nwaves = (int64_t)gridDim.x * (SD_PWG / 64);
+    const int64_t ray0 = (int64_t)blockIdx.x * (SD_PWG / 64) + wave;
+    if (ray0 >= a.R) return;
+    const int64_t nitems = ((a.R - ray0 + nwaves - 1) / nwaves) * nsub;
+
+    auto item_ray = [&](int64_t i) { return ray0 + (i / nsub) * nwaves; };
+    auto load_z = [&](int64_t i, float &z0, float &z1) {
+        const int64_t ray = item_ray(i);
+        const int k = (int)(i % nsub) * 16 + j;
+        const float *zr = a.z + ray * K;
+        z0 = zr[k];
+        z1 = zr[min(k + 1, K - 1)];
+    };
+    auto open_item = [&](int64_t i, float z0, float z1, PItem &it) {
+        it.ray = item_ray(i);
+        it.sub = (int)(i % nsub);
+        it.sbi = it.ray / a.rays_per_sb;
+        const int k = it.sub * 16 + j;
+        sd_cfloat *rr = (sd_cfloat *)(a.rays + it.ray * a.ray_dim);
+        it.zk = z0;
+        it.delta = (k + 1 < K) ? (z1 - z0) : 1e10f;
+        it.px = rr[0] + z0 * rr[3];  // points = o + z d (nerf.py:252)
+        it.py = rr[1] + z0 * rr[4];
+        it.pz = rr[2] + z0 * rr[5];
+        PointGeo geo = sd_point_geo((sd_cfloat *)(a.cam_f + it.sbi * 21), it.px, it.py, it.pz,
+                                    a.Wf, a.Hf);
+        it.v[0] = geo.v[0]; it.v[1] = geo.v[1]; it.v[2] = geo.v[2];
+        it.w[0] = geo.t.w00; it.w[1] = geo.t.w01; it.w[2] = geo.t.w10; it.w[3] = geo.t.w11;
+        const uint32_t lo = 16u * (uint32_t)g;
+        it.o[0] = (uint32_t)geo.t.i00 * 256u + lo;
+        it.o[1] = (uint32_t)geo.t.i01 * 256u + lo;
+        it.o[2] = (uint32_t)geo.t.i10 * 256u + lo;
+        it.o[3] = (uint32_t)geo.t.i11 * 256u + lo;
+        it.inv_f = geo.inv_f;
+        it.rs = sd_rsrc((const uint8_t *)a.grid + it.sbi * (int64_t)plane_bytes, plane_bytes);
+    };
+    // colour of the item's sample in render view g (NV == 1: every group samples view 0)
+    auto colours = [&](const PItem &it, float col[3], bool &invc) {
+        col[0] = col[1] = col[2] = 0.f;
+        invc = false;
+        if (NV == 1) {
+            invc = sd_color_view((sd_cfloat *)(a.cam_c + it.sbi * 21), a.img + it.sbi * cplane,
+                                 a.Wc, a.Hc, it.px, it.py, it.pz, col);
+        } else if (g < nv) {
+            invc = sd_color_view(a.cam_c + (it.sbi * nv + g) * 21, a.img + (it.sbi * nv + g) * cplane,
+                                 a.Wc, a.Hc, it.px, it.py, it.pz, col);
+        }
+    };
+
+    // prologue: item 0 open with its taps in flight, z of item 1 loaded
+    PItem cur;
+    {
+        float z0, z1;
+        load_z(0, z0, z1);
+        open_item(0, z0, z1, cur);
+    }
+    PRaw r0 = sd_pload(cur, 0), r1 = sd_pload(cur, 1), r2 = sd_pload(cur, 2), r3 = sd_pload(cur, 3);
+    float zq0, zq1;
+    load_z(min((int64_t)1, nitems - 1), zq0, zq1);
+    float col[3];
+    bool invc;
+    colours(cur, col, invc);
+
+    f32x4 dacc[NDT];
+#pragma unroll
+    for (int i = 0; i < NDT; ++i) dacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float Tc = 1.f, dpart = 0.f, wpart = 0.f, cpart[3] = {0.f, 0.f, 0.f};
+    const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+
+    for (int64_t i = 0; i < nitems; ++i) {
+        // open item i+1 (its z arrived during item i-1), put z of item i+2 in flight
+        PItem nxt;
+        open_item(min(i + 1, nitems - 1), zq0, zq1, nxt);
+        load_z(min(i + 2, nitems - 1), zq0, zq1);
+
+        const int lo = sd_opaque0();
+        const Frag *lw = lf + lo;
+        // grid part: identity MFMAs on the blended P chunks; refill with item i+1's taps
+        f32x4 acc[8];
+#define SD_PCHUNK(r, q)                                                        \
+        {                                                                      \
+            Frag f_ = Tr::blend(r.a, r.b, r.c, r.d, cur.w);                    \
+            r = sd_pload(nxt, q);                                              \
+            acc[2 * q] = Tr::mma(lw[SD_LDS_ID + lane], f_, zero4);             \
+            acc[2 * q + 1] = Tr::mma(lw[SD_LDS_ID + SD_WAVE + lane], f_, zero4); \
+        }
+        SD_PCHUNK(r0, 0)
+        SD_PCHUNK(r1, 1)
+        SD_PCHUNK(r2, 2)
+        SD_PCHUNK(r3, 3)
+#undef SD_PCHUNK
+        // positional-code columns
+#pragma unroll
+        for (int pc = 0; pc < 2; ++pc) {
+            const Frag f = sd_code_frag<Frag, E>(cur.v, pc, g);
+#pragma unroll
+            for (int t = 0; t < 8; ++t)
+                acc[t] = Tr::mma(lw[SD_LDS_PE + (pc * 8 + t) * SD_WAVE + lane], f, acc[t]);
+        }
+        // ReLU -> 16-bit operand fragments (accumulator-as-operand)
+        Frag X[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                X[s][e] = (E)sd_relu(acc[2 * s][e]);
+                X[s][4 + e] = (E)sd_relu(acc[2 * s + 1][e]);
+            }
+        // sigma (bts.py:516-541): every accumulator row holds w_sigma . h of sample j
+        f32x4 sg = zero4;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) sg = Tr::mma(lw[SD_LDS_SIG + s * SD_WAVE + lane], X[s], sg);
+        const float sv = sg[0] + m.b_sigma;
+        const float sigma = sv > 20.f ? sv : __logf(1.f + __expf(sv));
+
+        // alpha compositing (nerf.py:376-389)
+        const int k = cur.sub * 16 + j;
+        float alpha = 1.f - __expf(-fabsf(cur.delta) * fmaxf(sigma, 0.f));
+        if (a.hard_alpha_cap && k == K - 1) alpha = 1.f;
+        const float incl = sd_scan_mul16((1.f - alpha) + 1e-10f);
+        const float excl = SD_DPP1(incl, 0x111);
+        const float w = alpha * (Tc * excl);
+        Tc *= __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, incl), 15));
+        dpart += w * cur.zk;
+        wpart += w;
+        cpart[0] += w * col[0];
+        cpart[1] += w * col[1];
+        cpart[2] += w * col[2];
+        // DINO head folded into the compositing sum: dacc += w_j (W_dino h_j)
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+            f32x4 o = zero4;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) o = Tr::mma(lw[SD_LDS_OUT + (dt * 4 + s) * SD_WAVE + lane], X[s], o);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dacc[dt][r] = fmaf(w, o[r], dacc[dt][r]);
+        }
+
+        // per-sample outputs
+        const int64_t o = cur.ray * K + k;
+        if (g == 0) {
+            if (a.weights) a.weights[o] = w;
+            if (a.alphas) a.alphas[o] = alpha;
+            if (a.invalid_f) a.invalid_f[o] = cur.inv_f ? 1 : 0;
+        }
+        if (g < nv) {
+            if (a.invalid) a.invalid[o * nv + g] = (invc | cur.inv_f) ? 1.f : 0.f;
+            if (a.rgb_samps) {
+                float *rsp = a.rgb_samps + (o * nv + g) * 3;
+                rsp[0] = col[0]; rsp[1] = col[1]; rsp[2] = col[2];
+            }
+        }
+
+        if (cur.sub == nsub - 1) {
+            // ray epilogue: sums over the 16 sample lanes of every row
+            const float dsum = sd_rowsum16(dpart), wsum = sd_rowsum16(wpart);
+            const float c0 = sd_rowsum16(cpart[0]), c1 = sd_rowsum16(cpart[1]),
+                        c2 = sd_rowsum16(cpart[2]);
+#pragma unroll
+            for (int dt = 0; dt < NDT; ++dt) {
+                f32x4 v;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = sd_rowsum16(dacc[dt][r]);
+                if (j == 0) {
+                    // rows 4 g + r of dino tile dt = dims 16 dt + 4 g + r
+                    const int dim = 16 * dt + 4 * g;
+                    const f32x4 bd = *(const f32x4 *)(m.b_dino + dim);
+                    f32x4 res;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) res[r] = v[r] + wsum * bd[r];
+                    *(f32x4 *)(a.dino + cur.ray * m.D + dim) = res;
+                }
+                dacc[dt] = zero4;
+            }
+            if (lane == 0) a.depth[cur.ray] = dsum;
+            if (j == 0 && g < nv) {
+                float *rp = a.rgb + cur.ray * 3 * nv + 3 * g;
+                rp[0] = c0; rp[1] = c1; rp[2] = c2;
+            }
+            Tc = 1.f; dpart = 0.f; wpart = 0.f;
+            cpart[0] = cpart[1] = cpart[2] = 0.f;
+        }
+
+        colours(nxt, col, invc);
+        cur = nxt;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+template <typename KernT>
+static int sd_launch_proj(KernT kern, int64_t work_waves, int lds_bytes, hipStream_t s,
+                          int64_t &nblk) {
+    (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              lds_bytes);
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, SD_PWG, lds_bytes) !=
+            hipSuccess || per_cu <= 0)
+        per_cu = 1;
+    nblk = (work_waves + SD_PWG / 64 - 1) / (SD_PWG / 64);
+    const int64_t cap = (int64_t)sd_num_cus() * per_cu;
+    if (nblk > cap) nblk = cap;
+    return 0;
+}
+
+static int sd_check_err() {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        sd_set_error(hipGetErrorString(e));
+        return -2;
+    }
+    return 0;
+}
+
+extern "C" int sd_project_grid(const float *grid, int64_t B, int64_t Hf, int64_t Wf,
+                               const sd_mlp *m, void *out, void *stream) {
+    if (!grid || !m || !out || !m->w_in || !m->b_in_h || B <= 0 || Hf <= 0 || Wf <= 0 ||
+        m->d_hidden != SD_DH || m->C <= 0 || (m->C % 64) ||
+        (m->dtype != SD_BF16 && m->dtype != SD_F16)) {
+        sd_set_error("sd_project_grid: invalid argument (16-bit dtype, C % 64 == 0, d_hidden 128)");
+        return -1;
+    }
+    const int64_t HW = Hf * Wf;
+    const int lds_bytes = m->C / 16 * 4 * SD_WAVE * 16;
+    if (lds_bytes > 160 * 1024) {
+        sd_set_error("sd_project_grid: C too large for the LDS-staged weights");
+        return -1;
+    }
+    hipStream_t s = (hipStream_t)stream;
+    int64_t nblk;
+    const int64_t work = B * ((HW + 31) / 32);
+    if (m->dtype == SD_F16) {
+        sd_launch_proj(k_project<SD_F16>, work, lds_bytes, s, nblk);
+        hipLaunchKernelGGL(k_project<SD_F16>, dim3((unsigned)nblk), dim3(SD_PWG), lds_bytes, s,
+                           grid, B, m->C, HW, *m, (uint16_t *)out);
+    } else {
+        sd_launch_proj(k_project<SD_BF16>, work, lds_bytes, s, nblk);
+        hipLaunchKernelGGL(k_project<SD_BF16>, dim3((unsigned)nblk), dim3(SD_PWG), lds_bytes, s,
+                           grid, B, m->C, HW, *m, (uint16_t *)out);
+    }
+    return sd_check_err();
+}
+
+template <int P, int NV, int NDT>
+static int sd_rp_launch(const sd_render_args &a, const sd_head &m, hipStream_t s) {
+    const int lds_bytes = (SD_LDS_OUT + NDT * 4 * SD_WAVE) * 16;
+    int64_t nblk;
+    sd_launch_proj(k_render_proj<P, NV, NDT>, a.R, lds_bytes, s, nblk);
+    hipLaunchKernelGGL((k_render_proj<P, NV, NDT>), dim3((unsigned)nblk), dim3(SD_PWG), lds_bytes,
+                       s, a, m);
+    return sd_check_err();
+}
+
+template <int P, int NV>
+static int sd_rp_ndt(const sd_render_args &a, const sd_head &m, hipStream_t s) {
+    switch (m.D / 16) {
+        case 2: return sd_rp_launch<P, NV, 2>(a, m, s);
+        case 4: return sd_rp_launch<P, NV, 4>(a, m, s);
+        case 8: return sd_rp_launch<P, NV, 8>(a, m, s);
+        default:
+            sd_set_error("sd_render_proj: D must be 32, 64 or 128");
+            return -1;
+    }
+}
+
+template <int P>
+static int sd_rp_nv(const sd_render_args &a, const sd_head &m, hipStream_t s) {
+    return a.nv == 1 ? sd_rp_ndt<P, 1>(a, m, s) : sd_rp_ndt<P, 0>(a, m, s);
+}
+
+extern "C" int sd_render_proj(const sd_render_args *args, const sd_head *m, void *stream) {
+    if (!args || !m || !m->w_pe || !m->w_sig || !m->w_out || !m->b_dino ||
+        (m->dtype != SD_BF16 && m->dtype != SD_F16) ||
+        (m->D != 32 && m->D != 64 && m->D != 128)) {
+        sd_set_error("sd_render_proj: invalid head (16-bit dtype, D in {32, 64, 128})");
+        return -1;
+    }
+    const sd_render_args &a = *args;
+    if (a.R < 0 || a.K <= 0 || (a.K % 16) || a.ray_dim < 6 || a.rays_per_sb <= 0 || !a.rays ||
+        !a.z || !a.grid || !a.cam_f || !a.depth || !a.dino || a.Hf <= 0 || a.Wf <= 0 ||
+        a.nv < 0 || a.nv > SD_MAX_NV || (int64_t)a.Hf * a.Wf * SD_DH * 2 >= (1LL << 32) ||
+        (a.nv > 0 && (!a.img || !a.cam_c || !a.rgb || a.Hc <= 0 || a.Wc <= 0))) {
+        sd_set_error("sd_render_proj: invalid argument (K % 16 == 0, nv <= 4, P plane < 4 GiB)");
+        return -1;
+    }
+    if (a.R == 0) return 0;
+    hipStream_t s = (hipStream_t)stream;
+    if (m->dtype == SD_F16) return sd_rp_nv<SD_F16>(a, *m, s);
+    return sd_rp_nv<SD_BF16>(a, *m, s);
+}

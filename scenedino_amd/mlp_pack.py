@@ -13,6 +13,13 @@ is (r & 3) + 8 (r >> 2) + 4 h, column l & 31):
   bias/sigma  : [t][h][r] = vec[32 t + (r & 3) + 8 (r >> 2) + 4 h]
   layer 2 A   : bf16 [dt][t][s][l][j] = W_out[1 + 32 dt + (l & 31)][32 t + 16 s + 8 (j >> 2) + 4 h + (j & 3)]
                 f32  [dt][t][l][r]    = W_out[1 + 32 dt + (l & 31)][32 t + (r & 3) + 8 (r >> 2) + 4 h]
+
+Projected-grid head (16x16x32 MFMA, sdhip_proj.hip; lane l, sample/row i = l & 15,
+group g = l >> 4; hidden index of operand element e in k-step s:
+hid(s, g, e) = 32 s + 16 (e >> 2) + 4 g + (e & 3)):
+  code A      : w_pe[pc][t][l][e]  = W_in[16 t + (l & 15)][C + proj_pe_col(pc, g, e)]
+  sigma A     : w_sig[s][l][e]     = W_out[0][hid(s, g, e)]
+  dino A      : w_out16[dt][s][l][e] = W_out[1 + 16 dt + (l & 15)][hid(s, g, e)]
 """
 from __future__ import annotations
 
@@ -39,6 +46,45 @@ def pe_slot_to_ref_col(pc: int, h: int, j: int) -> int:
     if s < 21 and h == 0:
         return s - 18
     return -1
+
+
+def proj_pe_col(pc: int, g: int, e: int) -> int:
+    """Code column (0..38) feeding element e of code chunk pc for lane group g in the
+    projected-grid kernel (sd_code_frag in sdhip_proj.hip); -1 = zero."""
+    G = 2 * pc + (g >> 1)
+    ph = g & 1
+    if G < 3 and e < 6:
+        fi = 2 * G + (1 if e >= 3 else 0)
+        return 3 + 3 * (2 * fi + ph) + e % 3
+    if G == 0 and e >= 6:
+        return {(0, 6): 0, (0, 7): 1, (1, 6): 2}.get((g, e), -1)
+    return -1
+
+
+@functools.lru_cache(maxsize=8)
+def _proj_tables(C: int, D: int):
+    lanes = np.arange(64)
+    li, gg = lanes & 15, lanes >> 4
+    e = np.arange(8)
+    pe_rows = np.zeros((2, 8, 64, 8), np.int64)
+    pe_cols = np.zeros((2, 8, 64, 8), np.int64)
+    for pc in range(2):
+        for t in range(8):
+            for l in range(64):
+                for k in range(8):
+                    c = proj_pe_col(pc, l >> 4, k)
+                    pe_rows[pc, t, l, k] = 16 * t + (l & 15)
+                    pe_cols[pc, t, l, k] = C + c if c >= 0 else -1
+    s = np.arange(4)[:, None, None]
+    hid = 32 * s + 16 * (e[None, None, :] >> 2) + 4 * gg[None, :, None] + (e[None, None, :] & 3)
+    hid = np.broadcast_to(hid, (4, 64, 8))
+    nd = D // 16
+    out_rows = np.broadcast_to(1 + 16 * np.arange(nd)[:, None, None, None] + li[None, None, :, None],
+                               (nd, 4, 64, 8))
+    out_cols = np.broadcast_to(hid[None], (nd, 4, 64, 8))
+    to_t = lambda a: torch.from_numpy(np.array(a, copy=True))
+    return {"pe_rows": to_t(pe_rows), "pe_cols": to_t(pe_cols), "sig_cols": to_t(hid),
+            "out_rows": to_t(out_rows), "out_cols": to_t(out_cols)}
 
 
 @functools.lru_cache(maxsize=8)
@@ -85,7 +131,7 @@ def _index_tables(C: int, D: int):
     r4 = np.arange(16)[None, None, None, :]
     rows2f = np.broadcast_to(1 + 32 * dt4 + l4_lo, (ndt, 4, 64, 16))
     cols2f = np.broadcast_to(32 * t4 + (r4 & 3) + 8 * (r4 >> 2) + 4 * l4_h, (ndt, 4, 64, 16))
-    to_t = lambda a: torch.from_numpy(np.ascontiguousarray(a))
+    to_t = lambda a: torch.from_numpy(np.array(a, copy=True))
     return {
         "rows1": to_t(rows1), "cols1": to_t(cols1), "accrow": to_t(accrow),
         "rows2b": to_t(rows2b), "cols2b": to_t(cols2b),
@@ -125,6 +171,17 @@ class PackedMLP:
         self.b_dino = b_out[1:].contiguous()
         self.b_sigma = float(b_out[0].item())
         self.C, self.D, self.dtype = C, D, dtype
+        self.head_rec = None
+        if dtype != _lib.SD_F32 and D in (32, 64, 128):
+            px = {k: v.to(dev) for k, v in _proj_tables(C, D).items()}
+            pe_cols = torch.where(px["pe_cols"] < 0, torch.full_like(px["pe_cols"], din), px["pe_cols"])
+            self.w_pe16 = Wz[px["pe_rows"], pe_cols].to(tdt).contiguous()
+            self.w_sig16 = W_out[0][px["sig_cols"]].to(tdt).contiguous()
+            self.w_out16 = W_out[px["out_rows"], px["out_cols"]].to(tdt).contiguous()
+            self.head_rec = _lib.SdHead(
+                w_pe=self.w_pe16.data_ptr(), w_sig=self.w_sig16.data_ptr(),
+                w_out=self.w_out16.data_ptr(), b_dino=self.b_dino.data_ptr(),
+                b_sigma=self.b_sigma, D=D, dtype=dtype)
         self.rec = _lib.SdMlp(
             w_in=self.w_in.data_ptr(), b_in_h=self.b_in_h.data_ptr(),
             w_sig_h=self.w_sig_h.data_ptr(), b_sigma=self.b_sigma,

@@ -71,6 +71,11 @@ class BTSNet(nn.Module):
         self.downstream_head = downstream_head
         self.gt_classes = downstream_head.gt_classes if downstream_head is not None else None
         self.precision = conf.get("precision", "bf16")
+        # "proj": 16-bit modes render from the projected grid P = W_in[:, :C] G + b_in
+        # (sd_project_grid + sd_render_proj); "grid": per-sample C-channel gather
+        # (sd_render_fused, also the only fp32 path)
+        self.fused_mode = conf.get("fused_mode", "proj")
+        self.kernel_timer = None  # optional: .start(name) / .stop(name) around launches
         self._packed = None
         self._packed_key = None
         self._grid_cache = None
@@ -155,11 +160,26 @@ class BTSNet(nn.Module):
             raise ValueError(f"precision must be one of {sorted(PRECISIONS)}")
         return PRECISIONS[self.precision]
 
+    def _use_proj(self) -> bool:
+        if self.fused_mode not in ("proj", "grid"):
+            raise ValueError("fused_mode must be 'proj' or 'grid'")
+        return self.fused_mode == "proj" and self.precision != "fp32"
+
     def fused_supported(self, K: int) -> bool:
-        """The fused render kernel takes K % 32 == 0 and D in {32, 64, 128}; other
-        shapes go through sd_field_query + sd_composite (also native)."""
+        """The fused render kernels take D in {32, 64, 128} and K % 16 == 0 (projected,
+        16-bit) or K % 32 == 0 (grid kernel); other shapes go through sd_field_query +
+        sd_composite (also native)."""
         D = self._d_out - 1
-        return K % 32 == 0 and D in (32, 64, 128)
+        return K % (16 if self._use_proj() else 32) == 0 and D in (32, 64, 128)
+
+    def _timed(self, name, fn):
+        t = self.kernel_timer
+        if t is not None:
+            t.start(name)
+        r = fn()
+        if t is not None:
+            t.stop(name)
+        return r
 
     def _mlp(self):
         head = self.heads[self.final_pred_head]
@@ -187,18 +207,32 @@ class BTSNet(nn.Module):
                                       "(ids_encoder=[0], as every shipped config)")
         if self.learn_empty:
             raise NotImplementedError("learn_empty=True is not used by any shipped config")
-        grid = _lib.pack_grid(g.reshape(B, C, Hf, Wf).float().contiguous(), self._dtype())
         imgs = self.grid_c_imgs
         n, nv, c3, H, W = imgs.shape
         img = _lib.pack_image(imgs.reshape(n * nv, c3, H, W).float().contiguous())
         cache = {
-            "grid": grid, "C": C, "Hf": Hf, "Wf": Wf, "B": B,
+            "grid_nchw": g.reshape(B, C, Hf, Wf), "grid": None, "proj": None, "proj_key": None,
+            "C": C, "Hf": Hf, "Wf": Wf, "B": B,
             "cam_f": _cam_records(self.grid_f_poses_w2c[:, 0], self.grid_f_Ks[:, 0]),
             "img": img, "nv": nv, "Hc": H, "Wc": W,
             "cam_c": _cam_records(self.grid_c_poses_w2c, self.grid_c_Ks),
         }
         self._grid_cache, self._grid_key = cache, key
         return cache
+
+    def _grid_nhwc(self, gc):
+        """Encoder grid packed NHWC in the MLP dtype (sd_render_fused / sd_field_query)."""
+        if gc["grid"] is None:
+            gc["grid"] = _lib.pack_grid(gc["grid_nchw"].float().contiguous(), self._dtype())
+        return gc["grid"]
+
+    def _grid_proj(self, gc, m):
+        """Projected grid P = W_in[:, :C] G + b_in, (B, Hf, Wf, 128) (sd_render_proj)."""
+        if gc["proj"] is None or gc["proj_key"] != self._packed_key:
+            g = gc["grid_nchw"].float().contiguous()
+            gc["proj"] = self._timed("project", lambda: _lib.project_grid(g, m.rec, m.dtype))
+            gc["proj_key"] = self._packed_key
+        return gc["proj"]
 
     def _check_supported(self):
         if self.training and torch.is_grad_enabled():
@@ -243,9 +277,11 @@ class BTSNet(nn.Module):
         }
         rays = rays.float().contiguous()
         z = z.contiguous()
+        proj = self._use_proj()
+        grid = self._grid_proj(gc, m) if proj else self._grid_nhwc(gc)
         args = _lib.SdRenderArgs(
             rays=rays.data_ptr(), ray_dim=rays.shape[1], R=R, rays_per_sb=R // sb, K=K,
-            z=z.data_ptr(), grid=gc["grid"].data_ptr(), Hf=gc["Hf"], Wf=gc["Wf"],
+            z=z.data_ptr(), grid=grid.data_ptr(), Hf=gc["Hf"], Wf=gc["Wf"],
             cam_f=gc["cam_f"].data_ptr(), img=gc["img"].data_ptr(), nv=nv, Hc=gc["Hc"],
             Wc=gc["Wc"], cam_c=gc["cam_c"].data_ptr(), hard_alpha_cap=int(bool(hard_alpha_cap)),
             depth=out["depth"].data_ptr(), dino=out["dino"].data_ptr(),
@@ -254,7 +290,10 @@ class BTSNet(nn.Module):
             alphas=out["alphas"].data_ptr() if want_alphas else None,
             invalid=out["invalid"].data_ptr(), invalid_f=out["invalid_f"].data_ptr(),
             rgb_samps=out["rgb_samps"].data_ptr() if want_rgb_samps else None)
-        _lib.render_fused(args, m.rec, z)
+        if proj:
+            self._timed("render", lambda: _lib.render_proj(args, m.head_rec, z))
+        else:
+            self._timed("render", lambda: _lib.render_fused(args, m.rec, z))
         return out
 
     def query(self, xyz):
@@ -277,7 +316,8 @@ class BTSNet(nn.Module):
         inv = torch.empty(n, P, nv, device=dev)
         invf = torch.empty(n, P, device=dev, dtype=torch.uint8)
         args = _lib.SdFieldArgs(
-            xyz=xyz.data_ptr(), B=n, P=P, grid=gc["grid"].data_ptr(), Hf=gc["Hf"], Wf=gc["Wf"],
+            xyz=xyz.data_ptr(), B=n, P=P, grid=self._grid_nhwc(gc).data_ptr(), Hf=gc["Hf"],
+            Wf=gc["Wf"],
             cam_f=gc["cam_f"].data_ptr(), img=gc["img"].data_ptr(), nv=nv, Hc=gc["Hc"],
             Wc=gc["Wc"], cam_c=gc["cam_c"].data_ptr(), sigma=sigma.data_ptr(),
             dino=dino.data_ptr(), rgb=rgb.data_ptr(), invalid=inv.data_ptr(),

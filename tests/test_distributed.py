@@ -1,0 +1,84 @@
+"""CPU (gloo, world size 2) tests of the multi-GPU layout in scenedino_amd/distributed.py:
+frame / row-band sharding covers every unit exactly once and the all-gather of packed
+rendered maps returns every rank's frame in rank order."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from scenedino_amd import distributed as sdd
+
+
+def test_frames_and_row_bands_partition():
+    for world in (1, 2, 3, 8):
+        frames = sorted(f for r in range(world) for f in sdd.frames_of_rank(8, r, world))
+        assert frames == list(range(8))
+        rows = []
+        for r in range(world):
+            y0, y1 = sdd.row_band(192, r, world)
+            rows += list(range(y0, y1))
+        assert rows == list(range(192))
+    with pytest.raises(ValueError):
+        sdd.row_band(192, 2, 2)
+
+
+def test_pack_unpack_roundtrip():
+    R, D, nv = 50, 64, 1
+    c = {"depth": torch.rand(1, R), "dino_features": torch.rand(1, R, D),
+         "rgb": torch.rand(1, R, 3 * nv)}
+    m = sdd.pack_maps(c)
+    assert m.shape == (R, 1 + D + 3)
+    u = sdd.unpack_maps(m, D)
+    assert torch.equal(u["depth"], c["depth"].reshape(R))
+    assert torch.equal(u["dino_features"], c["dino_features"].reshape(R, D))
+    assert torch.equal(u["rgb"], c["rgb"].reshape(R, 3))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, R, D, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        frames = sdd.frames_of_rank(world, rank, world)
+        assert frames == [rank]
+        g = torch.Generator().manual_seed(100 + rank)
+        c = {"depth": torch.rand(1, R, generator=g), "dino_features": torch.rand(1, R, D, generator=g),
+             "rgb": torch.rand(1, R, 3, generator=g)}
+        got = sdd.gather_maps(sdd.pack_maps(c))
+        ok = True
+        for r in range(world):
+            g2 = torch.Generator().manual_seed(100 + r)
+            ref = {"depth": torch.rand(1, R, generator=g2),
+                   "dino_features": torch.rand(1, R, D, generator=g2),
+                   "rgb": torch.rand(1, R, 3, generator=g2)}
+            ok &= torch.equal(got[r], sdd.pack_maps(ref))
+        dist.barrier()
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_maps_gloo_world2():
+    world, R, D = 2, 300, 64
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, R, D, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    res = dict(q.get(timeout=10) for _ in range(world))
+    assert res == {0: True, 1: True}

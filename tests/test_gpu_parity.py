@@ -7,9 +7,10 @@ Tolerances (written here):
   * fp32 path (f32 grid + exact-f32 MFMA): |d| <= atol + rtol*|ref| with rtol 1e-4,
     atol 2e-5 (weights/alphas/rgb), 2e-4 (dino), 1e-3 m (depth);
     invalid masks: identical.
-  * bf16 path (bf16 grid + bf16 MFMA, fp32 accumulate): rel-L2 <= 1e-2 on dino
-    features and colour, depth rel-L2 <= 1e-2, weights max |d| <= 2e-2 and
-    rel-L2 <= 2e-2; invalid masks identical.
+  * bf16 / fp16 paths (16-bit grid or projected grid + 16-bit MFMA, fp32
+    accumulate), both kernels ("proj": sd_project_grid + sd_render_proj, "grid":
+    sd_render_fused): rel-L2 <= 1e-2 on dino features and colour, depth rel-L2 <=
+    1e-2, weights max |d| <= 2e-2 and rel-L2 <= 2e-2; invalid masks identical.
 """
 import hashlib
 import json
@@ -122,9 +123,9 @@ def test_field_query_vs_reference(precision):
 
 
 # --------------------------------------------------------------------------- full render
-def _render(d, precision, want_rgb_samps=True):
+def _render(d, precision, want_rgb_samps=True, mode="proj"):
     from scenedino_amd.renderer import NeRFRenderer
-    net = net_from_fixture(d, precision)
+    net = net_from_fixture(d, precision, mode=mode)
     K = int(d["K"])
     r = NeRFRenderer(n_coarse=K, lindisp=True, hard_alpha_cap=bool(d["hard_cap"]),
                      eval_batch_size=65536)
@@ -162,9 +163,10 @@ def test_render_fp32_vs_reference(fx):
 
 @pytest.mark.parametrize("fx", FIXTURES)
 @pytest.mark.parametrize("precision", ["bf16", "fp16"])
-def test_render_lowp_vs_reference(fx, precision):
+@pytest.mark.parametrize("mode", ["proj", "grid"])
+def test_render_lowp_vs_reference(fx, precision, mode):
     d = load(fx)
-    c = _render(d, precision)["coarse"]
+    c = _render(d, precision, mode=mode)["coarse"]
     assert torch.equal(c["invalid"].cpu(), torch.from_numpy(d["invalid"]))
     assert torch.equal(c["invalid_features"].cpu(), torch.from_numpy(d["invalid_features"]))
     assert rel_l2(c["dino_features"], d["dino_features"]) < 1e-2
@@ -172,6 +174,28 @@ def test_render_lowp_vs_reference(fx, precision):
     assert rel_l2(c["depth"], d["depth"]) < 1e-2
     assert rel_l2(c["weights"], d["weights"]) < 2e-2
     assert float((c["weights"].cpu() - torch.from_numpy(d["weights"])).abs().max()) < 2e-2
+    assert rel_l2(c["rgb_samps"], d["rgb_samps"]) < 1e-5
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp16"])
+def test_projected_grid_vs_dense_projection(precision):
+    """sd_project_grid against W_in[:, :C] . G + b_in computed in fp64 on the host."""
+    from scenedino_amd import _lib
+    from scenedino_amd.mlp_pack import PackedMLP
+    g = torch.Generator().manual_seed(11)
+    C, Hf, Wf = 256, 37, 53          # pixel count not a multiple of 32
+    grid = torch.randn(2, C, Hf, Wf, generator=g)
+    W_in = torch.randn(128, C + 39, generator=g) * 0.06
+    b_in = torch.randn(128, generator=g) * 0.1
+    W_out = torch.randn(65, 128, generator=g) * 0.1
+    b_out = torch.randn(65, generator=g) * 0.1
+    dt = _lib.SD_BF16 if precision == "bf16" else _lib.SD_F16
+    pk = PackedMLP(W_in.to(DEV), b_in.to(DEV), W_out.to(DEV), b_out.to(DEV), dt)
+    P = _lib.project_grid(grid.to(DEV), pk.rec, dt).double().cpu()   # (2, Hf, Wf, 128)
+    tdt = _lib.TORCH_DTYPE[dt]
+    ref = torch.einsum("nc,bchw->bhwn", W_in[:, :C].to(tdt).double(), grid.to(tdt).double()) \
+        + b_in.double()
+    assert rel_l2(P, ref) < (4e-3 if precision == "bf16" else 1e-3)
 
 
 def test_render_full_192x640x64_vs_reference_subsample():
@@ -258,9 +282,10 @@ def test_generic_composite_path_matches_fused():
     assert torch.equal(a["invalid"].cpu(), b["invalid"].cpu())
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16", "fp16"])
-def test_ragged_ray_count_and_offset_pose(precision):
-    """R not a multiple of the 32-ray tile; render pose offset from the encoder pose."""
+@pytest.mark.parametrize("precision,n_coarse", [("fp32", 24), ("bf16", 24), ("fp16", 24),
+                                                ("fp32", 32), ("bf16", 48), ("fp16", 48)])
+def test_ragged_ray_count_and_offset_pose(precision, n_coarse):
+    """R not a multiple of the ray tile; render pose offset from the encoder pose."""
     from scenedino_amd.renderer import NeRFRenderer
     from oracle import render_oracle as O
     d = load("render_sb2_nv2_k16.npz")
@@ -271,8 +296,8 @@ def test_ragged_ray_count_and_offset_pose(precision):
     # nv=2 render views needs an even ray count, nerf.py:596)
     rays = T(d["rays"])[:1, :762]
     g = torch.Generator().manual_seed(4)
-    u = torch.rand(rays.shape[1], 24, generator=g)
-    r = NeRFRenderer(n_coarse=24, lindisp=True)
+    u = torch.rand(rays.shape[1], n_coarse, generator=g)
+    r = NeRFRenderer(n_coarse=n_coarse, lindisp=True)
     r.z_jitter = u.to(DEV)
     with torch.no_grad():
         c = r(net, rays, want_weights=True)["coarse"]
@@ -291,3 +316,39 @@ def test_ragged_ray_count_and_offset_pose(precision):
         assert rel_l2(c["dino_features"], ref["dino_features"]) < 1e-2
         assert rel_l2(c["depth"], ref["depth"]) < 1e-2
     assert torch.equal(c["invalid"].cpu(), ref["invalid"])
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp16"])
+def test_render_full_192x640x64_projected_vs_reference_subsample(precision):
+    """BASELINE C2 shape through the projected 16-bit kernels against the reference
+    render's strided subsample (rel-L2 tolerances of the 16-bit modes)."""
+    from scenedino_amd.renderer import NeRFRenderer
+    from scenedino_amd.common.ray_sampler import ImageRaySampler
+    from scenedino_amd.models.prediction_heads import ResnetFC
+    d = load("render_full_subsample.npz")
+    g = torch.Generator().manual_seed(31)
+    images = torch.rand(1, 1, 3, 192, 640, generator=g) * 2 - 1
+    grid = torch.randn(1, 256, 48, 160, generator=g)
+    Kn = torch.tensor([[0.7849, 0.0, -0.0312], [0.0, 2.9391, 0.2701], [0.0, 0.0, 1.0]])
+    torch.manual_seed(2)
+    head = ResnetFC(d_in=295, d_out=65, n_blocks=0, d_hidden=128)
+    gb = torch.Generator().manual_seed(102)
+    with torch.no_grad():
+        head.lin_in.bias.copy_(0.1 * torch.randn(128, generator=gb))
+        head.lin_out.bias.copy_(0.1 * torch.randn(65, generator=gb))
+    net = build_net(grid, head.lin_in.weight, head.lin_in.bias, head.lin_out.weight,
+                    head.lin_out.bias, precision)
+    poses = torch.eye(4).view(1, 1, 4, 4)
+    net.encode(images.to(DEV), Kn.view(1, 1, 3, 3).to(DEV), poses.to(DEV), ids_encoder=[0],
+               ids_render=[0])
+    rays, _ = ImageRaySampler(3, 80, 192, 640).sample(None, poses.to(DEV), Kn.view(1, 1, 3, 3).to(DEV))
+    u = torch.rand(rays.shape[1], 64, generator=torch.Generator().manual_seed(32))
+    r = NeRFRenderer(n_coarse=64, lindisp=True, hard_alpha_cap=False, eval_batch_size=65536)
+    r.z_jitter = u.to(DEV)
+    with torch.no_grad():
+        c = r.bind_parallel(net).eval()(rays, want_weights=True, want_alphas=True)["coarse"]
+    idx = torch.from_numpy(d["idx"])
+    assert rel_l2(c["depth"][0].cpu()[idx], d["depth"]) < 1e-2
+    assert rel_l2(c["dino_features"][0].cpu()[idx], d["dino"]) < 1e-2
+    assert rel_l2(c["rgb"][0].cpu()[idx], d["rgb"]) < 1e-2
+    assert rel_l2(c["weights"][0].cpu()[idx], d["weights"]) < 2e-2
