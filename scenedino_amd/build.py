@@ -10,7 +10,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 SOURCES = ["csrc/sdhip_rays.hip", "csrc/sdhip_field.hip", "csrc/sdhip_proj.hip"]
 OUT = os.path.join(HERE, "libsdhip.so")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
-         "-DSD_FASTPE=0", "-Wno-unused-result"]
+         "-DSD_FASTPE=0", "-Wno-unused-result",
+         # MFMA accumulators in arch VGPRs (no v_accvgpr copies before VALU epilogues);
+         # no SLP packing of f32 math into v_pk_*_f32 (an issue-cost loss beside MFMAs)
+         "-mllvm", "-amdgpu-mfma-vgpr-form=1", "-fno-slp-vectorize"]
 
 
 def hipcc() -> str:

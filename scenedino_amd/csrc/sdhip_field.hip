@@ -393,13 +393,13 @@ __device__ __forceinline__ void sd_stage(uint8_t *lds, const sd_mlp &m, const Ld
 // chunks, sigma, compositing, DINO head) hides their latency.
 // ---------------------------------------------------------------------------
 struct Item {
-    int64_t ray;
+    int ray;
     int sub;
     float zk, delta, px, py, pz;
     PointGeo geo;
     TapOff o;
     __amdgpu_buffer_rsrc_t rs;
-    int64_t sbi;
+    int sbi;
 };
 
 template <int P, int NV, int NDT>
@@ -419,34 +419,33 @@ k_render(const sd_render_args a, const sd_mlp m, const LdsPlan pl) {
     const int nsub = K >> 5, nq = C >> 4;
     const uint32_t plane_bytes = (uint32_t)a.Hf * a.Wf * C * Pr::ESZ;
     const int64_t cplane = (int64_t)a.Hc * a.Wc * 4;
-    const int64_t nwaves = (int64_t)gridDim.x * WG<P>::W;
-    const int64_t ray0 = (int64_t)blockIdx.x * WG<P>::W + wave;
-    if (ray0 >= a.R) return;
-    const int64_t nitems = ((a.R - ray0 + nwaves - 1) / nwaves) * nsub;
+    const int nwaves = gridDim.x * WG<P>::W;
+    const int ray0 = blockIdx.x * WG<P>::W + wave;
+    const int R = (int)a.R, rps = (int)a.rays_per_sb;
+    if (ray0 >= R) return;
+    const int nitems = ((R - ray0 + nwaves - 1) / nwaves) * nsub;
 
-    auto item_ray = [&](int64_t i) { return ray0 + (i / nsub) * nwaves; };
-    // z and z_next of item i for this lane
-    auto load_z = [&](int64_t i, float &z0, float &z1) {
-        const int64_t ray = item_ray(i);
-        const int k = (int)(i % nsub) * 32 + li;
-        const float *zr = a.z + ray * K;
+    // z and z_next of item c for this lane
+    auto load_z = [&](const ItemCursor &c, float &z0, float &z1) {
+        const int k = c.sub * 32 + li;
+        const float *zr = a.z + (int64_t)c.ray * K;
         z0 = zr[k];
         z1 = zr[min(k + 1, K - 1)];
     };
-    // geometry, buffer descriptor and tap offsets of item i (z already loaded)
-    auto open_item = [&](int64_t i, float z0, float z1, Item &it) {
-        it.ray = item_ray(i);
-        it.sub = (int)(i % nsub);
-        it.sbi = it.ray / a.rays_per_sb;
+    // geometry, buffer descriptor and tap offsets of item c (z already loaded)
+    auto open_item = [&](const ItemCursor &c, float z0, float z1, Item &it) {
+        it.ray = c.ray;
+        it.sub = c.sub;
+        it.sbi = c.sbi;
         const int k = it.sub * 32 + li;
-        const float *rr = a.rays + it.ray * a.ray_dim;
+        sd_cfloat *rr = (sd_cfloat *)(a.rays + (int64_t)c.ray * a.ray_dim);
         it.zk = z0;
         it.delta = (k + 1 < K) ? (z1 - z0) : 1e10f;
         it.px = rr[0] + z0 * rr[3];  // points = o + z d (nerf.py:252)
         it.py = rr[1] + z0 * rr[4];
         it.pz = rr[2] + z0 * rr[5];
-        it.geo = sd_point_geo(a.cam_f + it.sbi * 21, it.px, it.py, it.pz, a.Wf, a.Hf);
-        it.rs = sd_rsrc((const uint8_t *)a.grid + it.sbi * (int64_t)plane_bytes, plane_bytes);
+        it.geo = sd_point_geo((sd_cfloat *)(a.cam_f + it.sbi * 21), it.px, it.py, it.pz, a.Wf, a.Hf);
+        it.rs = sd_rsrc((const uint8_t *)a.grid + (int64_t)it.sbi * plane_bytes, plane_bytes);
         it.o = sd_tapoff(it.geo.t, C, Pr::ESZ, h);
     };
     auto colours = [&](const Item &it, float col[3 * SD_MAX_NV], bool invc[SD_MAX_NV]) {
@@ -456,16 +455,18 @@ k_render(const sd_render_args a, const sd_mlp m, const LdsPlan pl) {
             col[3 * v] = col[3 * v + 1] = col[3 * v + 2] = 0.f;
             if (v < nv)
                 invc[v] = sd_color_view(a.cam_c + (it.sbi * nv + v) * 21,
-                                        a.img + (it.sbi * nv + v) * cplane, a.Wc, a.Hc, it.px,
+                                        a.img + (int64_t)(it.sbi * nv + v) * cplane, a.Wc, a.Hc, it.px,
                                         it.py, it.pz, col + 3 * v);
         }
     };
 
     // prologue: item 0
+    const ItemCursor c0 = sd_cursor0(ray0, rps);
+    ItemCursor c1 = sd_advance(c0, nsub, nwaves, R, rps);
     Item cur;
     float z0, z1;
-    load_z(0, z0, z1);
-    open_item(0, z0, z1, cur);
+    load_z(c0, z0, z1);
+    open_item(c0, z0, z1, cur);
     typename Pr::Raw r0 = Pr::load(cur.rs, cur.o, 0), r1 = Pr::load(cur.rs, cur.o, 1);
     typename Pr::Raw r2, r3;
     if constexpr (Pr::DEPTH == 4) {
@@ -485,10 +486,9 @@ k_render(const sd_render_args a, const sd_mlp m, const LdsPlan pl) {
 #pragma unroll
     for (int i = 0; i < 3 * SD_MAX_NV; ++i) cpart[i] = 0.f;
 
-    for (int64_t i = 0; i < nitems; ++i) {
-        const int64_t inext = min(i + 1, nitems - 1);
+    for (int i = 0; i < nitems; ++i) {
         float zn0, zn1;
-        load_z(inext, zn0, zn1);  // in flight during this item's MLP
+        load_z(c1, zn0, zn1);  // in flight during this item's MLP
 
         const int lo = sd_opaque0();
         const uint8_t *lw = lds + lo;
@@ -523,7 +523,8 @@ k_render(const sd_render_args a, const sd_mlp m, const LdsPlan pl) {
 
         // open the next item and put its first tap loads in flight
         Item nxt;
-        open_item(inext, zn0, zn1, nxt);
+        open_item(c1, zn0, zn1, nxt);
+        c1 = sd_advance(c1, nsub, nwaves, R, rps);
         r0 = Pr::load(nxt.rs, nxt.o, 0);
         r1 = Pr::load(nxt.rs, nxt.o, 1);
         if constexpr (Pr::DEPTH == 4) {
@@ -578,7 +579,7 @@ k_render(const sd_render_args a, const sd_mlp m, const LdsPlan pl) {
         for (int dt = 0; dt < NDT; ++dt) Pr::mma2(wo, dt, acc, lane, dacc[dt]);
 
         // per-sample outputs, coalesced along the ray
-        const int64_t o = cur.ray * K + k;
+        const int64_t o = (int64_t)cur.ray * K + k;
         if (h == 0) {
             if (a.weights) a.weights[o] = w;
             if (a.alphas) a.alphas[o] = alpha;
@@ -614,7 +615,7 @@ k_render(const sd_render_args a, const sd_mlp m, const LdsPlan pl) {
                 sacc += __shfl_xor(sacc, 32);
                 if ((dt & 1) == h) {
                     const int dim = dt * 32 + li;
-                    a.dino[cur.ray * m.D + dim] = sacc + wpart * m.b_dino[dim];
+                    a.dino[(int64_t)cur.ray * m.D + dim] = sacc + wpart * m.b_dino[dim];
                 }
                 dacc[dt] = f32x16{};
             }
@@ -624,7 +625,7 @@ k_render(const sd_render_args a, const sd_mlp m, const LdsPlan pl) {
 #pragma unroll
                 for (int c = 0; c < 3 * SD_MAX_NV; ++c)
                     if (c == lane) cv = cpart[c];
-                a.rgb[cur.ray * 3 * nv + lane] = cv;
+                a.rgb[(int64_t)cur.ray * 3 * nv + lane] = cv;
             }
             Tc = 1.f; dpart = 0.f; wpart = 0.f;
 #pragma unroll
@@ -829,7 +830,8 @@ extern "C" int sd_render_fused(const sd_render_args *args, const sd_mlp *mlp, vo
     }
     if (sd_plan(mlp, &pl)) return -1;
     const sd_render_args &a = *args;
-    if (a.R < 0 || a.K <= 0 || (a.K % 32) || a.ray_dim < 6 || a.rays_per_sb <= 0 || !a.rays ||
+    if (a.R < 0 || a.R >= (1LL << 31) || a.K <= 0 || (a.K % 32) || a.ray_dim < 6 ||
+        a.rays_per_sb <= 0 || !a.rays ||
         !a.z || !a.grid || !a.cam_f || !a.depth || !a.dino || a.Hf <= 0 || a.Wf <= 0 ||
         a.nv < 0 || a.nv > SD_MAX_NV || mlp->D > 128 ||
         (int64_t)a.Hf * a.Wf * mlp->C * (mlp->dtype == SD_F32 ? 4 : 2) >= (1LL << 32) ||

@@ -102,3 +102,27 @@ static int sd_num_cus() {
     return n;
 }
 
+
+// Wave-uniform position of a persistent wave's work item: ray (< 2^31), sub-tile of
+// the ray and the ray's super-batch (batch element) index.  Advanced without integer
+// division (a 64-bit divide is ~100 scalar instructions); clamps at the wave's last
+// item, which the software pipelines then only re-open for prefetch.
+struct ItemCursor {
+    int ray, sub, sbi;
+};
+
+__device__ __forceinline__ ItemCursor sd_cursor0(int ray0, int rays_per_sb) {
+    return {ray0, 0, (int)((unsigned)ray0 / (unsigned)rays_per_sb)};
+}
+
+__device__ __forceinline__ ItemCursor sd_advance(ItemCursor c, int nsub, int nwaves, int R,
+                                                 int rays_per_sb) {
+    if (c.sub + 1 < nsub) {
+        c.sub++;
+    } else if (c.ray + nwaves < R) {
+        c.ray += nwaves;
+        c.sub = 0;
+        c.sbi = (int)((unsigned)c.ray / (unsigned)rays_per_sb);
+    }
+    return c;
+}

@@ -224,14 +224,24 @@ __device__ __forceinline__ Frag sd_code_frag(const float v[3], int pc, int g) {
     return o;
 }
 
+// Per-sample record written by the ray pass into wave-private LDS, quad-major
+// ([q][k][4 words], q = 0 .. RS/4-1) so that both the ray pass (lane = sample) and the
+// item reads (lane j = sample) are conflict-free 16-byte accesses:
+//   q0: tap byte offsets pix * 256 of nw, ne, sw, se (bit 0 of o00: outside the encoder
+//       frustum; bits 0..3 of o01: outside render view 0..3)
+//   q1: bilinear weights w00, w01, w10, w11
+//   q2: x, y, z~ (positional-code inputs), z
+//   q3: delta, colour of render view 0 (r, g, b); then views 1..3 (3 words each)
+__host__ __device__ constexpr int sd_rec_words(int nv) { return (13 + 3 * nv + 3) & ~3; }
+
 struct PItem {
-    int64_t ray, sbi;
-    int sub;
-    float zk, delta, px, py, pz;
-    float v[3];
+    int ray, sub, sbi, n;
+    uint32_t o[4];  // tap byte offsets + 16 g inside the batch element's P plane
     float w[4];
-    uint32_t o[4];  // tap byte offsets (+ 16 g) inside the batch element's P plane
-    bool inv_f;
+    float v[3];
+    float zk, delta;
+    float col[3];   // colour of this lane's render view (group g; NV == 1: view 0)
+    bool inv_f, invc;
     __amdgpu_buffer_rsrc_t rs;
 };
 
@@ -247,12 +257,25 @@ __device__ __forceinline__ PRaw sd_pload(const PItem &it, int q) {
     return r;
 }
 
+// ReLU of two packed 16-bit values (bf16 or f16): a negative value has the sign bit
+// set, i.e. is a negative int16, so max_i16(x, 0) clamps it to +0.
+__device__ __forceinline__ uint32_t sd_relu2(uint32_t x) {
+    typedef __attribute__((ext_vector_type(2))) short s16x2;
+    const s16x2 v = __builtin_bit_cast(s16x2, x);
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(v, (s16x2){0, 0}));
+}
+
 // LDS image of the render kernel: [identity 2][64] | [code 2][8][64] | [sigma 4][64] |
-// [dino D/16][4][64], 16 B per lane entry
+// [dino D/16][4][64] (16 B per lane entry), then per wave 2 x K sample records.
 #define SD_LDS_ID 0
 #define SD_LDS_PE (2 * SD_WAVE)
 #define SD_LDS_SIG (SD_LDS_PE + 16 * SD_WAVE)
 #define SD_LDS_OUT (SD_LDS_SIG + 4 * SD_WAVE)
+
+// wave-uniform cursor with the wave's ray ordinal (selects the record buffer)
+struct RCursor {
+    int ray, sub, sbi, n;
+};
 
 template <int P, int NV, int NDT>
 __global__ void __launch_bounds__(SD_PWG)
@@ -283,70 +306,137 @@ k_render_proj(const sd_render_args a, const sd_head m) {
     const int lane = threadIdx.x & 63, j = lane & 15, g = lane >> 4;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int K = a.K, nsub = K >> 4, nv = NV > 0 ? NV : a.nv;
+    const int RQ = sd_rec_words(nv) / 4;  // 16-byte quads per record
+    uint4 *recs = (uint4 *)(lds + (SD_LDS_OUT + NDT * 4 * SD_WAVE) * 16) + wave * 2 * K * RQ;
     const uint32_t plane_bytes = (uint32_t)a.Hf * a.Wf * SD_DH * 2;
     const int64_t cplane = (int64_t)a.Hc * a.Wc * 4;
-    const int64_t nwaves = (int64_t)gridDim.x * (SD_PWG / 64);
-    const int64_t ray0 = (int64_t)blockIdx.x * (SD_PWG / 64) + wave;
-    if (ray0 >= a.R) return;
-    const int64_t nitems = ((a.R - ray0 + nwaves - 1) / nwaves) * nsub;
+    const int nwaves = gridDim.x * (SD_PWG / 64);
+    const int ray0 = blockIdx.x * (SD_PWG / 64) + wave;
+    const int R = (int)a.R, rps = (int)a.rays_per_sb;
+    if (ray0 >= R) return;
+    const int nitems = ((R - ray0 + nwaves - 1) / nwaves) * nsub;
 
-    auto item_ray = [&](int64_t i) { return ray0 + (i / nsub) * nwaves; };
-    auto load_z = [&](int64_t i, float &z0, float &z1) {
-        const int64_t ray = item_ray(i);
-        const int k = (int)(i % nsub) * 16 + j;
-        const float *zr = a.z + ray * K;
-        z0 = zr[k];
-        z1 = zr[min(k + 1, K - 1)];
+    auto advance = [&](RCursor c) {
+        if (c.sub + 1 < nsub) {
+            c.sub++;
+        } else if (c.ray + nwaves < R) {
+            c.ray += nwaves;
+            c.sub = 0;
+            c.n++;
+            c.sbi = (int)((unsigned)c.ray / (unsigned)rps);
+        }
+        return c;
     };
-    auto open_item = [&](int64_t i, float z0, float z1, PItem &it) {
-        it.ray = item_ray(i);
-        it.sub = (int)(i % nsub);
-        it.sbi = it.ray / a.rays_per_sb;
-        const int k = it.sub * 16 + j;
-        sd_cfloat *rr = (sd_cfloat *)(a.rays + it.ray * a.ray_dim);
-        it.zk = z0;
-        it.delta = (k + 1 < K) ? (z1 - z0) : 1e10f;
-        it.px = rr[0] + z0 * rr[3];  // points = o + z d (nerf.py:252)
-        it.py = rr[1] + z0 * rr[4];
-        it.pz = rr[2] + z0 * rr[5];
-        PointGeo geo = sd_point_geo((sd_cfloat *)(a.cam_f + it.sbi * 21), it.px, it.py, it.pz,
-                                    a.Wf, a.Hf);
-        it.v[0] = geo.v[0]; it.v[1] = geo.v[1]; it.v[2] = geo.v[2];
-        it.w[0] = geo.t.w00; it.w[1] = geo.t.w01; it.w[2] = geo.t.w10; it.w[3] = geo.t.w11;
-        const uint32_t lo = 16u * (uint32_t)g;
-        it.o[0] = (uint32_t)geo.t.i00 * 256u + lo;
-        it.o[1] = (uint32_t)geo.t.i01 * 256u + lo;
-        it.o[2] = (uint32_t)geo.t.i10 * 256u + lo;
-        it.o[3] = (uint32_t)geo.t.i11 * 256u + lo;
-        it.inv_f = geo.inv_f;
-        it.rs = sd_rsrc((const uint8_t *)a.grid + it.sbi * (int64_t)plane_bytes, plane_bytes);
-    };
-    // colour of the item's sample in render view g (NV == 1: every group samples view 0)
-    auto colours = [&](const PItem &it, float col[3], bool &invc) {
-        col[0] = col[1] = col[2] = 0.f;
-        invc = false;
-        if (NV == 1) {
-            invc = sd_color_view((sd_cfloat *)(a.cam_c + it.sbi * 21), a.img + it.sbi * cplane,
-                                 a.Wc, a.Hc, it.px, it.py, it.pz, col);
-        } else if (g < nv) {
-            invc = sd_color_view(a.cam_c + (it.sbi * nv + g) * 21, a.img + (it.sbi * nv + g) * cplane,
-                                 a.Wc, a.Hc, it.px, it.py, it.pz, col);
+
+    // ---- ray pass: per-sample geometry and colours of one ray, lane = sample ----------
+    // zq[2p], zq[2p+1]: z[k], z[k+1] of this lane's sample k = 64 p + lane (prefetched)
+    constexpr int MAXP = 2;  // K <= 128
+    auto load_ray_z = [&](int ray, float zq[2 * MAXP]) {
+        const float *zr = a.z + (int64_t)ray * K;
+#pragma unroll
+        for (int p = 0; p < MAXP; ++p) {
+            const int k = min(64 * p + lane, K - 1);
+            zq[2 * p] = zr[k];
+            zq[2 * p + 1] = zr[min(k + 1, K - 1)];
         }
     };
+    auto ray_pass = [&](int ray, int sbi, int buf, const float zq[2 * MAXP]) {
+        sd_cfloat *rr = (sd_cfloat *)(a.rays + (int64_t)ray * a.ray_dim);
+        const float ox = rr[0], oy = rr[1], oz = rr[2], dx = rr[3], dy = rr[4], dz = rr[5];
+        uint4 *rb = recs + buf * K * RQ;
+#pragma unroll
+        for (int p = 0; p < MAXP; ++p) {
+            const int k = 64 * p + lane;
+            if (64 * p < K && k < K) {
+                const float z0 = zq[2 * p], z1 = zq[2 * p + 1];
+                const float px = ox + z0 * dx, py = oy + z0 * dy, pz = oz + z0 * dz;  // nerf.py:252
+                PointGeo geo = sd_point_geo((sd_cfloat *)(a.cam_f + sbi * 21), px, py, pz, a.Wf, a.Hf);
+                float col[3 * SD_MAX_NV];
+                uint32_t invc = 0;
+#pragma unroll
+                for (int v = 0; v < SD_MAX_NV; ++v) {
+                    col[3 * v] = col[3 * v + 1] = col[3 * v + 2] = 0.f;
+                    if (v < nv) {
+                        const bool ic = NV == 1
+                            ? sd_color_view((sd_cfloat *)(a.cam_c + sbi * 21), a.img + (int64_t)sbi * cplane,
+                                            a.Wc, a.Hc, px, py, pz, col)
+                            : sd_color_view((sd_cfloat *)(a.cam_c + (sbi * nv + v) * 21),
+                                            a.img + (int64_t)(sbi * nv + v) * cplane, a.Wc, a.Hc,
+                                            px, py, pz, col + 3 * v);
+                        invc |= (ic ? 1u : 0u) << v;
+                    }
+                }
+                rb[0 * K + k] = uint4{(uint32_t)geo.t.i00 * 256u | (geo.inv_f ? 1u : 0u),
+                                      (uint32_t)geo.t.i01 * 256u | invc,
+                                      (uint32_t)geo.t.i10 * 256u, (uint32_t)geo.t.i11 * 256u};
+                rb[1 * K + k] = __builtin_bit_cast(uint4, f32x4{geo.t.w00, geo.t.w01, geo.t.w10, geo.t.w11});
+                rb[2 * K + k] = __builtin_bit_cast(uint4, f32x4{geo.v[0], geo.v[1], geo.v[2], z0});
+                const float delta = (k + 1 < K) ? (z1 - z0) : 1e10f;
+                rb[3 * K + k] = __builtin_bit_cast(uint4, f32x4{delta, col[0], col[1], col[2]});
+#pragma unroll
+                for (int q = 4; q < sd_rec_words(SD_MAX_NV) / 4; ++q)
+                    if (q < RQ) {
+                        float e[4];
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) {
+                            const int c = 4 * q + t - 16 + 3;  // colour word index
+                            e[t] = c < 3 * SD_MAX_NV ? col[c] : 0.f;
+                        }
+                        rb[q * K + k] = __builtin_bit_cast(uint4, f32x4{e[0], e[1], e[2], e[3]});
+                    }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    };
+    // ---- item open: this lane's sample record from LDS -------------------------------
+    auto open_item = [&](const RCursor &c, PItem &it) {
+        it.ray = c.ray;
+        it.sub = c.sub;
+        it.sbi = c.sbi;
+        it.n = c.n;
+        const uint4 *rb = recs + (c.n & 1) * K * RQ;
+        const int k = c.sub * 16 + j;
+        const uint4 q0 = rb[k];
+        const f32x4 q1 = __builtin_bit_cast(f32x4, rb[K + k]);
+        const f32x4 q2 = __builtin_bit_cast(f32x4, rb[2 * K + k]);
+        const f32x4 q3 = __builtin_bit_cast(f32x4, rb[3 * K + k]);
+        const uint32_t lo = 16u * (uint32_t)g;
+        it.o[0] = (q0.x & ~255u) + lo;
+        it.o[1] = (q0.y & ~255u) + lo;
+        it.o[2] = q0.z + lo;
+        it.o[3] = q0.w + lo;
+        it.inv_f = q0.x & 1u;
+        const int vv = NV == 1 ? 0 : g;
+        it.invc = (q0.y >> vv) & 1u;
+        it.w[0] = q1[0]; it.w[1] = q1[1]; it.w[2] = q1[2]; it.w[3] = q1[3];
+        it.v[0] = q2[0]; it.v[1] = q2[1]; it.v[2] = q2[2];
+        it.zk = q2[3];
+        it.delta = q3[0];
+        if (NV == 1 || g == 0) {
+            it.col[0] = q3[1]; it.col[1] = q3[2]; it.col[2] = q3[3];
+        } else {
+            // view g's colour: words 13 + 3 g .. 15 + 3 g of the record
+            const float *fb = (const float *)rb;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const int wd = 13 + 3 * g + c;
+                it.col[c] = g < nv ? fb[((wd >> 2) * K + k) * 4 + (wd & 3)] : 0.f;
+            }
+        }
+        it.rs = sd_rsrc((const uint8_t *)a.grid + (int64_t)it.sbi * plane_bytes, plane_bytes);
+    };
 
-    // prologue: item 0 open with its taps in flight, z of item 1 loaded
+    // prologue: records of the first ray, item 0 open with its taps in flight
+    RCursor c0 = {ray0, 0, (int)((unsigned)ray0 / (unsigned)rps), 0};
+    float zq[2 * MAXP];
+    load_ray_z(c0.ray, zq);
+    ray_pass(c0.ray, c0.sbi, 0, zq);
+    const bool more = ray0 + nwaves < R;
+    if (more) load_ray_z(ray0 + nwaves, zq);  // z of the wave's second ray in flight
     PItem cur;
-    {
-        float z0, z1;
-        load_z(0, z0, z1);
-        open_item(0, z0, z1, cur);
-    }
+    open_item(c0, cur);
+    RCursor c1 = advance(c0);
     PRaw r0 = sd_pload(cur, 0), r1 = sd_pload(cur, 1), r2 = sd_pload(cur, 2), r3 = sd_pload(cur, 3);
-    float zq0, zq1;
-    load_z(min((int64_t)1, nitems - 1), zq0, zq1);
-    float col[3];
-    bool invc;
-    colours(cur, col, invc);
 
     f32x4 dacc[NDT];
 #pragma unroll
@@ -354,11 +444,16 @@ k_render_proj(const sd_render_args a, const sd_head m) {
     float Tc = 1.f, dpart = 0.f, wpart = 0.f, cpart[3] = {0.f, 0.f, 0.f};
     const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
 
-    for (int64_t i = 0; i < nitems; ++i) {
-        // open item i+1 (its z arrived during item i-1), put z of item i+2 in flight
+    for (int i = 0; i < nitems; ++i) {
+        // first item of a ray: records of the wave's next ray into the other buffer
+        if (cur.sub == 0 && cur.ray + nwaves < R) {
+            const int nr = cur.ray + nwaves;
+            ray_pass(nr, (int)((unsigned)nr / (unsigned)rps), (cur.n + 1) & 1, zq);
+            if (nr + nwaves < R) load_ray_z(nr + nwaves, zq);
+        }
         PItem nxt;
-        open_item(min(i + 1, nitems - 1), zq0, zq1, nxt);
-        load_z(min(i + 2, nitems - 1), zq0, zq1);
+        open_item(c1, nxt);
+        c1 = advance(c1);
 
         const int lo = sd_opaque0();
         const Frag *lw = lf + lo;
@@ -384,15 +479,20 @@ k_render_proj(const sd_render_args a, const sd_head m) {
             for (int t = 0; t < 8; ++t)
                 acc[t] = Tr::mma(lw[SD_LDS_PE + (pc * 8 + t) * SD_WAVE + lane], f, acc[t]);
         }
-        // ReLU -> 16-bit operand fragments (accumulator-as-operand)
+        // 16-bit operand fragments (accumulator-as-operand), ReLU on the packed values
         Frag X[4];
 #pragma unroll
-        for (int s = 0; s < 4; ++s)
+        for (int s = 0; s < 4; ++s) {
+            Frag f;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                X[s][e] = (E)sd_relu(acc[2 * s][e]);
-                X[s][4 + e] = (E)sd_relu(acc[2 * s + 1][e]);
+                f[e] = (E)acc[2 * s][e];
+                f[4 + e] = (E)acc[2 * s + 1][e];
             }
+            uint4 u = __builtin_bit_cast(uint4, f);
+            u.x = sd_relu2(u.x); u.y = sd_relu2(u.y); u.z = sd_relu2(u.z); u.w = sd_relu2(u.w);
+            X[s] = __builtin_bit_cast(Frag, u);
+        }
         // sigma (bts.py:516-541): every accumulator row holds w_sigma . h of sample j
         f32x4 sg = zero4;
 #pragma unroll
@@ -410,9 +510,9 @@ k_render_proj(const sd_render_args a, const sd_head m) {
         Tc *= __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, incl), 15));
         dpart += w * cur.zk;
         wpart += w;
-        cpart[0] += w * col[0];
-        cpart[1] += w * col[1];
-        cpart[2] += w * col[2];
+        cpart[0] += w * cur.col[0];
+        cpart[1] += w * cur.col[1];
+        cpart[2] += w * cur.col[2];
         // DINO head folded into the compositing sum: dacc += w_j (W_dino h_j)
 #pragma unroll
         for (int dt = 0; dt < NDT; ++dt) {
@@ -424,25 +524,25 @@ k_render_proj(const sd_render_args a, const sd_head m) {
         }
 
         // per-sample outputs
-        const int64_t o = cur.ray * K + k;
+        const int64_t o = (int64_t)cur.ray * K + k;
         if (g == 0) {
             if (a.weights) a.weights[o] = w;
             if (a.alphas) a.alphas[o] = alpha;
             if (a.invalid_f) a.invalid_f[o] = cur.inv_f ? 1 : 0;
         }
         if (g < nv) {
-            if (a.invalid) a.invalid[o * nv + g] = (invc | cur.inv_f) ? 1.f : 0.f;
+            if (a.invalid) a.invalid[o * nv + g] = (cur.invc | cur.inv_f) ? 1.f : 0.f;
             if (a.rgb_samps) {
                 float *rsp = a.rgb_samps + (o * nv + g) * 3;
-                rsp[0] = col[0]; rsp[1] = col[1]; rsp[2] = col[2];
+                rsp[0] = cur.col[0]; rsp[1] = cur.col[1]; rsp[2] = cur.col[2];
             }
         }
 
         if (cur.sub == nsub - 1) {
             // ray epilogue: sums over the 16 sample lanes of every row
             const float dsum = sd_rowsum16(dpart), wsum = sd_rowsum16(wpart);
-            const float c0 = sd_rowsum16(cpart[0]), c1 = sd_rowsum16(cpart[1]),
-                        c2 = sd_rowsum16(cpart[2]);
+            const float c0s = sd_rowsum16(cpart[0]), c1s = sd_rowsum16(cpart[1]),
+                        c2s = sd_rowsum16(cpart[2]);
 #pragma unroll
             for (int dt = 0; dt < NDT; ++dt) {
                 f32x4 v;
@@ -455,20 +555,18 @@ k_render_proj(const sd_render_args a, const sd_head m) {
                     f32x4 res;
 #pragma unroll
                     for (int r = 0; r < 4; ++r) res[r] = v[r] + wsum * bd[r];
-                    *(f32x4 *)(a.dino + cur.ray * m.D + dim) = res;
+                    *(f32x4 *)(a.dino + (int64_t)cur.ray * m.D + dim) = res;
                 }
                 dacc[dt] = zero4;
             }
             if (lane == 0) a.depth[cur.ray] = dsum;
             if (j == 0 && g < nv) {
-                float *rp = a.rgb + cur.ray * 3 * nv + 3 * g;
-                rp[0] = c0; rp[1] = c1; rp[2] = c2;
+                float *rp = a.rgb + (int64_t)cur.ray * 3 * nv + 3 * g;
+                rp[0] = c0s; rp[1] = c1s; rp[2] = c2s;
             }
             Tc = 1.f; dpart = 0.f; wpart = 0.f;
             cpart[0] = cpart[1] = cpart[2] = 0.f;
         }
-
-        colours(nxt, col, invc);
         cur = nxt;
     }
 }
@@ -531,7 +629,8 @@ extern "C" int sd_project_grid(const float *grid, int64_t B, int64_t Hf, int64_t
 
 template <int P, int NV, int NDT>
 static int sd_rp_launch(const sd_render_args &a, const sd_head &m, hipStream_t s) {
-    const int lds_bytes = (SD_LDS_OUT + NDT * 4 * SD_WAVE) * 16;
+    const int lds_bytes = (SD_LDS_OUT + NDT * 4 * SD_WAVE) * 16 +
+                          (SD_PWG / 64) * 2 * a.K * sd_rec_words(a.nv) * 4;
     int64_t nblk;
     sd_launch_proj(k_render_proj<P, NV, NDT>, a.R, lds_bytes, s, nblk);
     hipLaunchKernelGGL((k_render_proj<P, NV, NDT>), dim3((unsigned)nblk), dim3(SD_PWG), lds_bytes,
@@ -564,11 +663,13 @@ extern "C" int sd_render_proj(const sd_render_args *args, const sd_head *m, void
         return -1;
     }
     const sd_render_args &a = *args;
-    if (a.R < 0 || a.K <= 0 || (a.K % 16) || a.ray_dim < 6 || a.rays_per_sb <= 0 || !a.rays ||
+    if (a.R < 0 || a.R >= (1LL << 31) || a.K <= 0 || (a.K % 16) || a.K > 128 || a.ray_dim < 6 ||
+        a.rays_per_sb <= 0 || !a.rays ||
         !a.z || !a.grid || !a.cam_f || !a.depth || !a.dino || a.Hf <= 0 || a.Wf <= 0 ||
         a.nv < 0 || a.nv > SD_MAX_NV || (int64_t)a.Hf * a.Wf * SD_DH * 2 >= (1LL << 32) ||
         (a.nv > 0 && (!a.img || !a.cam_c || !a.rgb || a.Hc <= 0 || a.Wc <= 0))) {
-        sd_set_error("sd_render_proj: invalid argument (K % 16 == 0, nv <= 4, P plane < 4 GiB)");
+        sd_set_error("sd_render_proj: invalid argument (K % 16 == 0, K <= 128, nv <= 4, "
+                     "P plane < 4 GiB)");
         return -1;
     }
     if (a.R == 0) return 0;

@@ -1,0 +1,58 @@
+"""Drop the MI355X render path into an unmodified reference checkout.
+
+The reference's callers (train.py, eval.py, demo_script.py, sscbench/
+evaluate_model_sscbench.py) import the hot path as
+
+    from scenedino.renderer import NeRFRenderer            # renderer/__init__.py:1
+    from scenedino.models import make_model                # models/__init__.py:9
+    from scenedino.common.ray_sampler import ImageRaySampler
+
+``install()`` registers this package's mirrors under those module names before the
+reference is imported, so those imports resolve here while every other reference
+module (encoders, data sets, trainer, losses, visualisation) stays the reference's.
+``make_model`` keeps the reference's signature (scenedino/models/__init__.py:9-63): the
+image encoder is still built by the reference's own ``make_backbone``
+(models/backbones/backbone_util.py) and the downstream head by
+``scenedino.downstream_head.make_downstream_head``, then handed to this package's BTSNet, whose parameter names equal the reference's, so
+``checkpoint.pt`` state dicts load unchanged (demo_utils/utils.py:52-55).
+"""
+from __future__ import annotations
+
+import importlib
+import sys
+import types
+
+
+def _ref_make_model(config, downstream_config=None):
+    from . import models as amd_models
+    backbones = importlib.import_module("scenedino.models.backbones")
+    encoder = backbones.make_backbone(config["encoder"])
+    downstream_head = None
+    if downstream_config is not None:
+        heads = importlib.import_module("scenedino.downstream_head")
+        downstream_head = heads.make_downstream_head(downstream_config)
+    return amd_models.make_model(config, downstream_config, encoder=encoder,
+                                 downstream_head=downstream_head)
+
+
+def install():
+    """Alias scenedino.renderer / scenedino.models.make_model / ImageRaySampler to the
+    MI355X build.  Call before the first ``import scenedino...``."""
+    from . import renderer as amd_renderer
+    from .common import ray_sampler as amd_rs
+    from .models import bts as amd_bts
+
+    ren = types.ModuleType("scenedino.renderer")
+    ren.NeRFRenderer = amd_renderer.NeRFRenderer
+    ren.__path__ = []  # package: scenedino.renderer.nerf resolves below
+    sys.modules["scenedino.renderer"] = ren
+    sys.modules["scenedino.renderer.nerf"] = importlib.import_module(
+        "scenedino_amd.renderer.nerf")
+
+    models = importlib.import_module("scenedino.models")
+    models.make_model = _ref_make_model
+    models.BTSNet = amd_bts.BTSNet
+    sys.modules["scenedino.models.bts"] = amd_bts
+
+    rs = importlib.import_module("scenedino.common.ray_sampler")
+    rs.ImageRaySampler = amd_rs.ImageRaySampler

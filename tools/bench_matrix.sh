@@ -3,8 +3,8 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-for cfg in ${CFGS:-"bf16 proj" "fp16 proj" "bf16 grid" "fp16 grid" "fp32 grid"}; do
-  set -- $cfg; prec=$1; mode=$2
+for cfg in ${CFGS:-bf16:proj fp16:proj bf16:grid fp16:grid fp32:grid}; do
+  prec=${cfg%%:*}; mode=${cfg##*:}
   for extra in "" "--offset-pose"; do
     log=gpurun_out/bm_${prec}_${mode}${extra}.log
     timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --precision $prec --mode $mode $extra > $log 2>&1 || { cat $log; exit 7; }
