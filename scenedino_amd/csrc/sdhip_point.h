@@ -18,7 +18,9 @@ struct PointGeo {
     bool inv_f;   // outside the encoder frustum
 };
 
-template <typename CP>
+// FASTZ (16-bit modes): z~ with a hardware reciprocal; it only feeds the positional
+// code, never the masks or taps.
+template <bool FASTZ = false, typename CP>
 __device__ __forceinline__ PointGeo sd_point_geo(CP cam, float px, float py,
                                                  float pz, int Wf, int Hf) {
     PointGeo g;
@@ -29,7 +31,9 @@ __device__ __forceinline__ PointGeo sd_point_geo(CP cam, float px, float py,
     y = fminf(fmaxf(y, -2.f), 2.f);
     // encoding_mode._z, inv_z, d_min=3, d_max=80 (positional_encoding.py:13-21).
     // (1/d_min - 1/d_max) is a Python double rounded once to fp32, as in the reference.
-    float zt = (1.f / fmaxf(zc, SD_EPS) - (float)(1.0 / 80.0)) / (float)(1.0 / 3.0 - 1.0 / 80.0);
+    float zt = FASTZ
+        ? (__builtin_amdgcn_rcpf(fmaxf(zc, SD_EPS)) - (float)(1.0 / 80.0)) * (float)(1.0 / (1.0 / 3.0 - 1.0 / 80.0))
+        : (1.f / fmaxf(zc, SD_EPS) - (float)(1.0 / 80.0)) / (float)(1.0 / 3.0 - 1.0 / 80.0);
     zt = 2.f * zt - 1.f;
     g.v[0] = x; g.v[1] = y; g.v[2] = zt;
     g.t = sd_taps(x, y, Wf, Hf);
@@ -38,7 +42,12 @@ __device__ __forceinline__ PointGeo sd_point_geo(CP cam, float px, float py,
 
 
 __device__ __forceinline__ uint4 sd_ld128(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff) {
+#if SD_ABL_NOLOAD  // diagnostic timing build only: the gather replaced by register values
+    (void)rs;
+    return uint4{voff & 0x3c003c00u, soff & 0x3c003c00u, (voff ^ soff) & 0x3c003c00u, 0x3c003c00u};
+#else
     return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
+#endif
 }
 
 

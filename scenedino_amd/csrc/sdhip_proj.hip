@@ -26,7 +26,22 @@
 // while item i computes.
 #include "sdhip_point.h"
 
+// diagnostic ablation switches (timing experiments only; outputs are wrong when set)
+#ifndef SD_ABL_NORAYPASS
+#define SD_ABL_NORAYPASS 0
+#endif
+#ifndef SD_ABL_NOBLEND
+#define SD_ABL_NOBLEND 0
+#endif
+#ifndef SD_ABL_NOPE
+#define SD_ABL_NOPE 0
+#endif
+#ifndef SD_ABL_NODINO
+#define SD_ABL_NODINO 0
+#endif
+#ifndef SD_PWG
 #define SD_PWG 256  // threads per workgroup (4 waves); several workgroups per CU
+#endif
 
 // 16-bit element traits
 template <int P> struct T16;
@@ -92,6 +107,14 @@ template <> struct T16<SD_BF16> {
         return o;
     }
 };
+
+// two floats -> one packed 16-bit pair (v_cvt_pk_f16_f32 / v_cvt_pk_bf16_f32, RNE)
+template <typename E>
+__device__ __forceinline__ uint32_t sd_pack2(float a, float b) {
+    typedef __attribute__((ext_vector_type(2))) float f32x2;
+    typedef __attribute__((ext_vector_type(2))) E e2;
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, e2));
+}
 
 // ---------------------------------------------------------------------------
 // k_project: P[b][pix][n] = sum_c W_in[n][c] G[b][c][pix] + b_in[n]   (n < 128)
@@ -173,7 +196,7 @@ k_project(const float *__restrict__ grid, int64_t B, int C, int64_t HW, const sd
     __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, 1.f), \
                                                           __builtin_bit_cast(int, (x)), (ctrl), 0xf, 0xf, false))
 #define SD_DPP0(x, ctrl) \
-    __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, (x)), (ctrl), 0xf, 0xf, false))
+    __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, (x)), (ctrl), 0xf, 0xf, true))
 
 // inclusive product scan over the 16 lanes of every row (row_shr 1, 2, 4, 8)
 __device__ __forceinline__ float sd_scan_mul16(float x) {
@@ -192,36 +215,38 @@ __device__ __forceinline__ float sd_rowsum16(float x) {
     return x;
 }
 
-// sin for the 16-bit modes: one revolution-domain range reduction, then v_sin_f32
-__device__ __forceinline__ float sd_sin_fast(float x) {
-    return __builtin_amdgcn_sinf(__builtin_amdgcn_fractf(x * 0.15915494309189535f));
+// sin of an angle given in revolutions (x / 2 pi): one range reduction + v_sin_f32
+__device__ __forceinline__ float sd_sin_rev(float r) {
+    return __builtin_amdgcn_sinf(__builtin_amdgcn_fractf(r));
 }
 
 // Positional-code fragment of chunk pc for lane group g (element e):
 //   G = 2 pc + (g >> 1), phase = g & 1 (0: sin, 1: cos = sin(x + pi/2))
-//   G < 3, e < 6 : sin(fmaf(v[e % 3], 1.5 * 2^(2G + (e >= 3)), phase * pi/2))
+//   G < 3, e < 6 : sin(v[e % 3] * 1.5 * 2^(2G + (e >= 3)) + phase * pi/2)
 //   G = 0, e >= 6: raw inputs (g = 0: x, y; g = 1: z~, 0)
-//   otherwise 0.   (scenedino_amd/mlp_pack.py: proj_pe_col gives the W_in column.)
+//   otherwise don't-care: the packed code weights of those slots are zero
+//   (scenedino_amd/mlp_pack.py: proj_pe_col gives the W_in column of every slot).
+// The angle is formed in revolutions, fmaf(v * 4^(g >> 1), 1.5 * 2^k / 2 pi, phase / 4).
 template <typename Frag, typename E>
 __device__ __forceinline__ Frag sd_code_frag(const float v[3], int pc, int g) {
-    const float phase = (g & 1) ? 1.5707963705062866f : 0.f;
-    const float lscale = (g >> 1) ? 4.f : 1.f;
-    const bool on = 2 * pc + (g >> 1) < 3;
-    Frag o;
+    const float ph = (g & 1) ? 0.25f : 0.f;
+    const float ls = (g >> 1) ? 4.f : 1.f;
+    const float u[3] = {v[0] * ls, v[1] * ls, v[2] * ls};
+    float r[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-        float r;
         if (e < 6) {
-            const float f = 1.5f * (float)(1 << (4 * pc + (e >= 3 ? 1 : 0))) * lscale;
-            r = on ? sd_sin_fast(fmaf(v[e % 3], f, phase)) : 0.f;
+            const float f = 1.5f * (float)(1 << (4 * pc + (e >= 3 ? 1 : 0))) * 0.15915494309189535f;
+            r[e] = sd_sin_rev(fmaf(u[e % 3], f, ph));
         } else if (pc == 0) {
-            r = (g >> 1) ? 0.f : (g == 0 ? v[e - 6] : (e == 6 ? v[2] : 0.f));
+            r[e] = (g >> 1) ? 0.f : (g == 0 ? v[e - 6] : (e == 6 ? v[2] : 0.f));
         } else {
-            r = 0.f;
+            r[e] = 0.f;
         }
-        o[e] = (E)r;
     }
-    return o;
+    const uint4 u4 = {sd_pack2<E>(r[0], r[1]), sd_pack2<E>(r[2], r[3]), sd_pack2<E>(r[4], r[5]),
+                      sd_pack2<E>(r[6], r[7])};
+    return __builtin_bit_cast(Frag, u4);
 }
 
 // Per-sample record written by the ray pass into wave-private LDS, quad-major
@@ -305,6 +330,13 @@ k_render_proj(const sd_render_args a, const sd_head m) {
 
     const int lane = threadIdx.x & 63, j = lane & 15, g = lane >> 4;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // identity fragments live in registers (8 VGPRs): A[i][k] = [k == i] / [k == 16 + i]
+    Frag id0, id1;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        id0[e] = (E)((8 * g + e == j) ? 1.f : 0.f);
+        id1[e] = (E)((8 * g + e == j + 16) ? 1.f : 0.f);
+    }
     const int K = a.K, nsub = K >> 4, nv = NV > 0 ? NV : a.nv;
     const int RQ = sd_rec_words(nv) / 4;  // 16-byte quads per record
     uint4 *recs = (uint4 *)(lds + (SD_LDS_OUT + NDT * 4 * SD_WAVE) * 16) + wave * 2 * K * RQ;
@@ -350,7 +382,7 @@ k_render_proj(const sd_render_args a, const sd_head m) {
             if (64 * p < K && k < K) {
                 const float z0 = zq[2 * p], z1 = zq[2 * p + 1];
                 const float px = ox + z0 * dx, py = oy + z0 * dy, pz = oz + z0 * dz;  // nerf.py:252
-                PointGeo geo = sd_point_geo((sd_cfloat *)(a.cam_f + sbi * 21), px, py, pz, a.Wf, a.Hf);
+                PointGeo geo = sd_point_geo<true>((sd_cfloat *)(a.cam_f + sbi * 21), px, py, pz, a.Wf, a.Hf);
                 float col[3 * SD_MAX_NV];
                 uint32_t invc = 0;
 #pragma unroll
@@ -444,14 +476,17 @@ k_render_proj(const sd_render_args a, const sd_head m) {
     float Tc = 1.f, dpart = 0.f, wpart = 0.f, cpart[3] = {0.f, 0.f, 0.f};
     const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
 
-    for (int i = 0; i < nitems; ++i) {
+    // one item: `cur` computes, `nxt` is opened (unrolled by two below so the item
+    // state ping-pongs between two register sets instead of being copied)
+    auto step = [&](PItem &cur, PItem &nxt) {
         // first item of a ray: records of the wave's next ray into the other buffer
         if (cur.sub == 0 && cur.ray + nwaves < R) {
             const int nr = cur.ray + nwaves;
+#if !SD_ABL_NORAYPASS
             ray_pass(nr, (int)((unsigned)nr / (unsigned)rps), (cur.n + 1) & 1, zq);
+#endif
             if (nr + nwaves < R) load_ray_z(nr + nwaves, zq);
         }
-        PItem nxt;
         open_item(c1, nxt);
         c1 = advance(c1);
 
@@ -461,10 +496,11 @@ k_render_proj(const sd_render_args a, const sd_head m) {
         f32x4 acc[8];
 #define SD_PCHUNK(r, q)                                                        \
         {                                                                      \
-            Frag f_ = Tr::blend(r.a, r.b, r.c, r.d, cur.w);                    \
+            Frag f_ = SD_ABL_NOBLEND ? __builtin_bit_cast(Frag, r.a ^ r.b ^ r.c ^ r.d) \
+                                     : Tr::blend(r.a, r.b, r.c, r.d, cur.w);   \
             r = sd_pload(nxt, q);                                              \
-            acc[2 * q] = Tr::mma(lw[SD_LDS_ID + lane], f_, zero4);             \
-            acc[2 * q + 1] = Tr::mma(lw[SD_LDS_ID + SD_WAVE + lane], f_, zero4); \
+            acc[2 * q] = Tr::mma(id0, f_, zero4);                              \
+            acc[2 * q + 1] = Tr::mma(id1, f_, zero4);                          \
         }
         SD_PCHUNK(r0, 0)
         SD_PCHUNK(r1, 1)
@@ -474,7 +510,12 @@ k_render_proj(const sd_render_args a, const sd_head m) {
         // positional-code columns
 #pragma unroll
         for (int pc = 0; pc < 2; ++pc) {
+#if SD_ABL_NOPE
+            Frag f;
+            for (int e = 0; e < 8; ++e) f[e] = (E)cur.v[e % 3];
+#else
             const Frag f = sd_code_frag<Frag, E>(cur.v, pc, g);
+#endif
 #pragma unroll
             for (int t = 0; t < 8; ++t)
                 acc[t] = Tr::mma(lw[SD_LDS_PE + (pc * 8 + t) * SD_WAVE + lane], f, acc[t]);
@@ -483,14 +524,10 @@ k_render_proj(const sd_render_args a, const sd_head m) {
         Frag X[4];
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-            Frag f;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                f[e] = (E)acc[2 * s][e];
-                f[4 + e] = (E)acc[2 * s + 1][e];
-            }
-            uint4 u = __builtin_bit_cast(uint4, f);
-            u.x = sd_relu2(u.x); u.y = sd_relu2(u.y); u.z = sd_relu2(u.z); u.w = sd_relu2(u.w);
+            const uint4 u = {sd_relu2(sd_pack2<E>(acc[2 * s][0], acc[2 * s][1])),
+                             sd_relu2(sd_pack2<E>(acc[2 * s][2], acc[2 * s][3])),
+                             sd_relu2(sd_pack2<E>(acc[2 * s + 1][0], acc[2 * s + 1][1])),
+                             sd_relu2(sd_pack2<E>(acc[2 * s + 1][2], acc[2 * s + 1][3]))};
             X[s] = __builtin_bit_cast(Frag, u);
         }
         // sigma (bts.py:516-541): every accumulator row holds w_sigma . h of sample j
@@ -518,7 +555,8 @@ k_render_proj(const sd_render_args a, const sd_head m) {
         for (int dt = 0; dt < NDT; ++dt) {
             f32x4 o = zero4;
 #pragma unroll
-            for (int s = 0; s < 4; ++s) o = Tr::mma(lw[SD_LDS_OUT + (dt * 4 + s) * SD_WAVE + lane], X[s], o);
+            for (int s = 0; s < 4; ++s)
+                if (!SD_ABL_NODINO || s == 0) o = Tr::mma(lw[SD_LDS_OUT + (dt * 4 + s) * SD_WAVE + lane], X[s], o);
 #pragma unroll
             for (int r = 0; r < 4; ++r) dacc[dt][r] = fmaf(w, o[r], dacc[dt][r]);
         }
@@ -567,7 +605,11 @@ k_render_proj(const sd_render_args a, const sd_head m) {
             Tc = 1.f; dpart = 0.f; wpart = 0.f;
             cpart[0] = cpart[1] = cpart[2] = 0.f;
         }
-        cur = nxt;
+    };
+    PItem alt;
+    for (int i = 0; i < nitems; i += 2) {
+        step(cur, alt);
+        if (i + 1 < nitems) step(alt, cur);
     }
 }
 

@@ -1,15 +1,14 @@
 #!/bin/bash
-# Build alternative sdhip_field.hip sources into scenedino_amd/variants/libsdhip_<name>.so
-# (diagnostic A/B builds, loaded via SDHIP_LIB).  usage: tools/variants.sh name=path.hip ...
+# Build diagnostic A/B variants of libsdhip.so with extra compiler flags into
+# scenedino_amd/variants/libsdhip_<name>.so (loaded via SDHIP_LIB by tools/ablate.sh).
+# usage: tools/variants.sh 'name=-DFOO=1 -DBAR=2' ...
 cd "$(dirname "$0")/.."
 mkdir -p scenedino_amd/variants
+FLAGS=$(python -c "import sys; sys.path.insert(0,'scenedino_amd'); import build; print(' '.join(build.FLAGS))")
+SRCS=$(python -c "import sys; sys.path.insert(0,'scenedino_amd'); import build; print(' '.join('scenedino_amd/'+s for s in build.SOURCES))")
 for spec in "$@"; do
-  name=${spec%%=*}; src=${spec#*=}
-  cp "$src" scenedino_amd/csrc/_variant_$name.hip
-  ( /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared \
-    -DSD_FASTPE=0 -Wno-unused-result -o scenedino_amd/variants/libsdhip_$name.so \
-    scenedino_amd/csrc/sdhip_rays.hip scenedino_amd/csrc/_variant_$name.hip;
-    rm -f scenedino_amd/csrc/_variant_$name.hip ) &
+  name=${spec%%=*}; extra=${spec#*=}
+  /opt/rocm/bin/hipcc $FLAGS $extra -o scenedino_amd/variants/libsdhip_$name.so $SRCS &
 done
 wait
 ls -la scenedino_amd/variants
