@@ -65,6 +65,13 @@ int sd_pack_grid(const float *grid_nchw, int64_t B, int64_t C, int64_t H, int64_
 int sd_pack_image(const float *img_nchw, int64_t N, int64_t H, int64_t W, float *out_nhwc4,
                   void *stream);
 
+/* Camera records of n views: out (n, 21) = [w2c rows 0..2 (3x4) | K (3x3)], the
+ * operands of pts_into_camera / project_to_image (pinhole.py:40-84) as the field
+ * kernels read them.  w2c: (n, 4, 4) with element stride s_w (>= 16) between views,
+ * inner 4x4 contiguous; Ks: (n, 3, 3), stride s_k (>= 9). */
+int sd_cam_records(const float *w2c, int64_t s_w, const float *Ks, int64_t s_k, int64_t n,
+                   float *out, void *stream);
+
 /* Per-point MLP parameters, pre-packed (by the host) into MFMA fragment order.
  * ResnetFC(n_blocks=0): out = W_out relu(W_in x + b_in) + b_out
  *   (scenedino/models/prediction_heads/resnetfc.py:135-203). */
@@ -107,6 +114,12 @@ typedef struct sd_render_args {
     float *invalid;    /* (R, K, nv)     */
     uint8_t *invalid_f;/* (R, K)         */
     float *rgb_samps;  /* (R, K, 3 nv)   */
+    /* In-kernel z sampling (sd_render_proj only): with z == NULL the kernel draws
+     * each ray's depths itself exactly as sd_sample_z(rays, R, ray_dim, K, z_lindisp,
+     * NULL, z_seed, z_offset) would (NeRFRenderer.sample_coarse, nerf.py:121-141),
+     * so the (R, K) depth array never goes through HBM.  Ignored when z != NULL. */
+    int32_t z_lindisp;
+    uint64_t z_seed, z_offset;
 } sd_render_args;
 
 int sd_render_fused(const sd_render_args *args, const sd_mlp *mlp, void *stream);
@@ -121,7 +134,9 @@ int sd_render_fused(const sd_render_args *args, const sd_mlp *mlp, void *stream)
  * the positional-code columns by MFMA.  Same outputs as sd_render_fused up to
  * rounding order (16-bit modes only; the f32 parity mode keeps sd_render_fused). */
 
-/* grid_nchw (B, C, Hf, Wf) float32 -> out (B, Hf, Wf, 128) in mlp->dtype (BF16/F16).
+/* grid_nchw (B, C, Hf, Wf) float32 -> out (B, Hf, Wf, 128, 2) in mlp->dtype (BF16/F16),
+ * pair-interleaved: out[b][y][x][n] = (P[y][x][n], P[y][min(x + 1, Wf - 1)][n]), i.e.
+ * both horizontal bilinear taps of a row (grid_sample border padding) in one dword.
  * Uses mlp->w_in chunks 0..C/16-1 and mlp->b_in_h. */
 int sd_project_grid(const float *grid_nchw, int64_t B, int64_t Hf, int64_t Wf,
                     const sd_mlp *mlp, void *out, void *stream);
@@ -138,8 +153,8 @@ typedef struct sd_head {
     int32_t dtype;         /* SD_BF16 or SD_F16                                       */
 } sd_head;
 
-/* args->grid = the projected grid (B, Hf, Wf, 128) from sd_project_grid; K % 16 == 0.
- * Outputs as sd_render_fused. */
+/* args->grid = the projected pair grid (B, Hf, Wf, 128, 2) from sd_project_grid; K % 16 == 0.
+ * Outputs as sd_render_fused; args->z may be NULL (in-kernel z sampling, see above). */
 int sd_render_proj(const sd_render_args *args, const sd_head *head, void *stream);
 
 /* Per-point field query without compositing (BTSNet.forward on raw points,

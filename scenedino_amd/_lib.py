@@ -14,7 +14,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # SDHIP_LIB: alternative build of the same library (diagnostic builds only)
 LIB_PATH = os.environ.get("SDHIP_LIB") or os.path.join(_HERE, "libsdhip.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 SD_F32 = 0
 SD_BF16 = 1
@@ -53,6 +53,7 @@ class SdRenderArgs(ctypes.Structure):
         ("depth", _vp), ("dino", _vp), ("rgb", _vp),
         ("weights", _vp), ("alphas", _vp), ("invalid", _vp), ("invalid_f", _vp),
         ("rgb_samps", _vp),
+        ("z_lindisp", _i32), ("z_seed", ctypes.c_uint64), ("z_offset", ctypes.c_uint64),
     ]
 
 
@@ -76,6 +77,7 @@ SIGNATURES = {
                     _vp, _vp],
     "sd_pack_grid": [_vp, _i64, _i64, _i64, _i64, ctypes.c_int, _vp, _vp],
     "sd_pack_image": [_vp, _i64, _i64, _i64, _vp, _vp],
+    "sd_cam_records": [_vp, _i64, _vp, _i64, _i64, _vp, _vp],
     "sd_render_fused": [ctypes.POINTER(SdRenderArgs), ctypes.POINTER(SdMlp), _vp],
     "sd_field_query": [ctypes.POINTER(SdFieldArgs), ctypes.POINTER(SdMlp), _vp],
     "sd_project_grid": [_vp, _i64, _i64, _i64, ctypes.POINTER(SdMlp), _vp, _vp],
@@ -180,6 +182,26 @@ def pack_image(img_nchw):
     return out
 
 
+def cam_records(poses_w2c, Ks):
+    """(..., 4, 4) w2c and (..., 3, 3) K -> (..., 21) camera records (one launch)."""
+    lib = load()
+    lead = poses_w2c.shape[:-2]
+    w = poses_w2c.float().reshape(-1, 4, 4)
+    k = Ks.float().reshape(-1, 3, 3)
+    if w.stride()[1:] != (4, 1):
+        w = w.contiguous()
+    if k.stride()[1:] != (3, 1):
+        k = k.contiguous()
+    n = w.shape[0]
+    if k.shape[0] != n:
+        raise ValueError("poses and intrinsics must have the same number of views")
+    out = torch.empty(*lead, 21, device=w.device, dtype=torch.float32)
+    _check(lib.sd_cam_records(ptr(w), w.stride(0) if n > 1 else 16, ptr(k),
+                              k.stride(0) if n > 1 else 9, n, ptr(out), stream_of(out)),
+           "sd_cam_records")
+    return out
+
+
 def render_fused(args: SdRenderArgs, mlp: SdMlp, ref_tensor):
     lib = load()
     _check(lib.sd_render_fused(ctypes.byref(args), ctypes.byref(mlp), stream_of(ref_tensor)),
@@ -187,10 +209,12 @@ def render_fused(args: SdRenderArgs, mlp: SdMlp, ref_tensor):
 
 
 def project_grid(grid_nchw, mlp: SdMlp, dtype):
-    """P = W_in[:, :C] . grid + b_in per pixel: (B, Hf, Wf, 128) in dtype."""
+    """P = W_in[:, :C] . grid + b_in per pixel, pair-interleaved with the right
+    neighbour's row: (B, Hf, Wf, 128, 2) in dtype, [..., 0] = P[x], [..., 1] =
+    P[min(x + 1, Wf - 1)]."""
     lib = load()
     B, C, H, W = grid_nchw.shape
-    out = torch.empty(B, H, W, 128, device=grid_nchw.device, dtype=TORCH_DTYPE[dtype])
+    out = torch.empty(B, H, W, 128, 2, device=grid_nchw.device, dtype=TORCH_DTYPE[dtype])
     _check(lib.sd_project_grid(ptr(_req(grid_nchw, "grid")), B, H, W, ctypes.byref(mlp),
                                ptr(out), stream_of(out)), "sd_project_grid")
     return out

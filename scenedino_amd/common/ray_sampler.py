@@ -36,6 +36,7 @@ class ImageRaySampler(RaySampler):
         self.channels = channels
         self.norm_dir = norm_dir
         self.dino_upscaled = dino_upscaled
+        self._ids_cache = {}
 
     def sample(self, images, poses, projs, image_ids=None, dino_features=None,
                dino_artifacts=None):
@@ -49,7 +50,10 @@ class ImageRaySampler(RaySampler):
             self.height, self.width = images.shape[-2:]
         h, w = self.height, self.width
         if image_ids is None:
-            ids = torch.arange(v, device=device, dtype=torch.float32)
+            key = (v, str(device))
+            ids = self._ids_cache.get(key)
+            if ids is None:
+                ids = self._ids_cache[key] = torch.arange(v, device=device, dtype=torch.float32)
         else:
             ids = torch.tensor(image_ids, device=device, dtype=torch.float32)
         all_rays, all_rgb, all_dino = [], [], []
@@ -65,8 +69,12 @@ class ImageRaySampler(RaySampler):
                 dc, ph, pw = dino_features.shape[-3:]
                 all_dino.append(dino_features[n_].view(-1, dc, ph, pw).permute(0, 2, 3, 1)
                                 .reshape(-1, dc))
-        all_rays = torch.stack(all_rays)
-        all_rgb = torch.stack(all_rgb) if images is not None else None
+        # a single frame is a view, not a copy (torch.stack would copy the rays)
+        all_rays = all_rays[0].unsqueeze(0) if n == 1 else torch.stack(all_rays)
+        if images is not None:
+            all_rgb = all_rgb[0].unsqueeze(0) if n == 1 else torch.stack(all_rgb)
+        else:
+            all_rgb = None
         if dino_features is not None:
             return all_rays, all_rgb, torch.stack(all_dino)
         return all_rays, all_rgb

@@ -82,6 +82,20 @@ __device__ __forceinline__ Taps sd_taps(float x, float y, int w, int h) {
     return t;
 }
 
+// NeRFRenderer.sample_coarse for sample k of a ray (nerf.py:121-141) given its jitter
+// uu: t = linspace(0, 1 - 1/K, K)[k] + uu / K, then lindisp / linear depth.  Every
+// operation separately rounded (bit-exact with the reference, tests/golden).
+__device__ __forceinline__ float sd_z_sample(float near, float far, int64_t K, int64_t k, float uu,
+                                             float step, float t_end, int lindisp) {
+    const float t = sd_linspace_at(0.0f, t_end, K, k) + uu * step;
+    if (lindisp) {
+        const float a = (1.0f / near) * (1.0f - t);
+        const float b = (1.0f / far) * t;
+        return 1.0f / (a + b);
+    }
+    return near * (1.0f - t) + far * t;
+}
+
 // Counter-based uniform [0,1) (24-bit mantissa) for perf-mode jitter.
 __device__ __forceinline__ float sd_uniform(uint64_t seed, uint64_t ctr) {
     uint64_t z = seed + 0x9E3779B97F4A7C15ull * (ctr + 1);

@@ -43,7 +43,10 @@
 #define SD_PWG 256  // threads per workgroup (4 waves); several workgroups per CU
 #endif
 
-// 16-bit element traits
+// 16-bit element traits.  Blend of the pair-interleaved projected grid (k_project):
+// every dword of a row holds (P[x0][c], P[x1][c]) of one channel c, so a bilinear
+// sample is two v_dot2 per channel, row y0 . (w00, w01) + row y1 . (w10, w11), in f32
+// with one rounding to the 16-bit operand type.
 template <int P> struct T16;
 template <> struct T16<SD_F16> {
     typedef f16x8 Frag;
@@ -57,29 +60,20 @@ template <> struct T16<SD_F16> {
     static __device__ __forceinline__ uint16_t bits(float f) {
         return __builtin_bit_cast(uint16_t, (_Float16)f);
     }
-    // packed-f16 bilinear blend of 8 channels from the 4 taps
-    static __device__ __forceinline__ Frag blend(const uint4 &a, const uint4 &b, const uint4 &c,
-                                                 const uint4 &d, const float w[4]) {
-        const f16x2 w0 = {(_Float16)w[0], (_Float16)w[0]}, w1 = {(_Float16)w[1], (_Float16)w[1]};
-        const f16x2 w2 = {(_Float16)w[2], (_Float16)w[2]}, w3 = {(_Float16)w[3], (_Float16)w[3]};
-        const uint32_t A[4] = {a.x, a.y, a.z, a.w}, B[4] = {b.x, b.y, b.z, b.w};
-        const uint32_t C[4] = {c.x, c.y, c.z, c.w}, D[4] = {d.x, d.y, d.z, d.w};
-        Frag o;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            f16x2 v = __builtin_bit_cast(f16x2, A[i]) * w0;
-            v = __builtin_elementwise_fma(__builtin_bit_cast(f16x2, B[i]), w1, v);
-            v = __builtin_elementwise_fma(__builtin_bit_cast(f16x2, C[i]), w2, v);
-            v = __builtin_elementwise_fma(__builtin_bit_cast(f16x2, D[i]), w3, v);
-            o[2 * i] = v[0];
-            o[2 * i + 1] = v[1];
-        }
-        return o;
+    // x . w with a zero accumulator (VOP3P form: no v_mov of the zero)
+    static __device__ __forceinline__ float dot2z(uint32_t x, uint32_t w) {
+        float r;
+        asm("v_dot2_f32_f16 %0, %1, %2, 0" : "=v"(r) : "v"(x), "v"(w));
+        return r;
+    }
+    static __device__ __forceinline__ float dot2(uint32_t x, uint32_t w, float c) {
+        return __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2, x), __builtin_bit_cast(f16x2, w), c, false);
     }
 };
 template <> struct T16<SD_BF16> {
     typedef bf16x8 Frag;
     typedef __bf16 E;
+    typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
     static __device__ __forceinline__ f32x4 mma(const Frag &a, const Frag &b, const f32x4 &c) {
         return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
     }
@@ -89,22 +83,13 @@ template <> struct T16<SD_BF16> {
     static __device__ __forceinline__ uint16_t bits(float f) {
         return __builtin_bit_cast(uint16_t, (__bf16)f);
     }
-    // fp32 blend of the bf16 taps, one rounding to bf16
-    static __device__ __forceinline__ Frag blend(const uint4 &a, const uint4 &b, const uint4 &c,
-                                                 const uint4 &d, const float w[4]) {
-        const uint32_t A[4] = {a.x, a.y, a.z, a.w}, B[4] = {b.x, b.y, b.z, b.w};
-        const uint32_t C[4] = {c.x, c.y, c.z, c.w}, D[4] = {d.x, d.y, d.z, d.w};
-        Frag o;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            float lo = fmaf(bf16lo(D[i]), w[3], fmaf(bf16lo(C[i]), w[2],
-                            fmaf(bf16lo(B[i]), w[1], bf16lo(A[i]) * w[0])));
-            float hi = fmaf(bf16hi(D[i]), w[3], fmaf(bf16hi(C[i]), w[2],
-                            fmaf(bf16hi(B[i]), w[1], bf16hi(A[i]) * w[0])));
-            o[2 * i] = (__bf16)lo;
-            o[2 * i + 1] = (__bf16)hi;
-        }
-        return o;
+    static __device__ __forceinline__ float dot2z(uint32_t x, uint32_t w) {
+        float r;
+        asm("v_dot2_f32_bf16 %0, %1, %2, 0" : "=v"(r) : "v"(x), "v"(w));
+        return r;
+    }
+    static __device__ __forceinline__ float dot2(uint32_t x, uint32_t w, float c) {
+        return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, x), __builtin_bit_cast(bf16x2, w), c, false);
     }
 };
 
@@ -116,16 +101,47 @@ __device__ __forceinline__ uint32_t sd_pack2(float a, float b) {
     return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, e2));
 }
 
+// blend weights as the ray pass stores them: (w00, w01), (w10, w11) packed in E
+template <int P>
+__device__ __forceinline__ uint4 sd_pack_w(float w00, float w01, float w10, float w11) {
+    typedef typename T16<P>::E E;
+    return uint4{sd_pack2<E>(w00, w01), sd_pack2<E>(w10, w11), 0u, 0u};
+}
+
+// 8 channels of one sample from its two pair rows: a, b = row y0 (channels 0-3, 4-7),
+// c, d = row y1
+template <int P>
+__device__ __forceinline__ typename T16<P>::Frag sd_blend_pair(const uint4 &a, const uint4 &b,
+                                                              const uint4 &c, const uint4 &d,
+                                                              const uint4 &wp) {
+    typedef T16<P> Tr;
+    const uint32_t R0[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    const uint32_t R1[8] = {c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float lo = Tr::dot2(R0[2 * i], wp.x, Tr::dot2z(R1[2 * i], wp.y));
+        const float hi = Tr::dot2(R0[2 * i + 1], wp.x, Tr::dot2z(R1[2 * i + 1], wp.y));
+        o[i] = sd_pack2<typename Tr::E>(lo, hi);
+    }
+    return __builtin_bit_cast(typename Tr::Frag, uint4{o[0], o[1], o[2], o[3]});
+}
+
 // ---------------------------------------------------------------------------
-// k_project: P[b][pix][n] = sum_c W_in[n][c] G[b][c][pix] + b_in[n]   (n < 128)
-// One wave = 32 pixels x 128 hidden = 4 tiles of 32x32x16; K = C in chunks of 16.
+// k_project: P[b][pix][n] = sum_c W_in[n][c] G[b][c][pix] + b_in[n]   (n < 128),
+// stored pair-interleaved: P2[b][pix][n] = (P[pix][n], P[right(pix)][n]) with
+// right(pix) = pix + 1, or pix itself in the last column (x1 = min(x0 + 1, W - 1) of
+// grid_sample's border padding), so one 16-byte load of a row gives both horizontal
+// taps of 4 channels.  One wave = 32 pixel columns x 128 hidden = 4 tiles of 32x32x16,
+// K = C in chunks of 16; waves step by 31 pixels so that column 31 (the next wave's
+// first pixel) supplies the right neighbour of column 30 (lane exchange, no reload).
 // A = the sd_mlp layer-1 fragments of the grid columns (LDS); B = 8 channels of the
 // lane's pixel read from NCHW (32 consecutive floats per channel across a half).
 // ---------------------------------------------------------------------------
 template <int P>
 __global__ void __launch_bounds__(SD_PWG)
-k_project(const float *__restrict__ grid, int64_t B, int C, int64_t HW, const sd_mlp m,
-          uint16_t *__restrict__ out) {
+k_project(const float *__restrict__ grid, int64_t B, int C, int64_t HW, int W, const sd_mlp m,
+          uint32_t *__restrict__ out) {
     typedef T16<P> Tr;
     typedef typename Tr::Frag Frag;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -139,13 +155,13 @@ k_project(const float *__restrict__ grid, int64_t B, int C, int64_t HW, const sd
     const Frag *lw = (const Frag *)lds;
     const int lane = threadIdx.x & 63, h = lane >> 5, li = lane & 31;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t ntile = (HW + 31) / 32, total = B * ntile;
+    const int64_t ntile = (HW + 30) / 31, total = B * ntile;
     for (int64_t task = (int64_t)blockIdx.x * (SD_PWG / 64) + wave; task < total;
          task += (int64_t)gridDim.x * (SD_PWG / 64)) {
         const int64_t b = task / ntile;
-        const int64_t pix = (task - b * ntile) * 32 + li;
-        const bool valid = pix < HW;
-        const float *gp = grid + b * C * HW + (valid ? pix : HW - 1) + (int64_t)(8 * h) * HW;
+        const int64_t pix = (task - b * ntile) * 31 + li;
+        const bool valid = li < 31 && pix < HW;
+        const float *gp = grid + b * C * HW + (pix < HW ? pix : HW - 1) + (int64_t)(8 * h) * HW;
         f32x16 acc[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
@@ -172,19 +188,27 @@ k_project(const float *__restrict__ grid, int64_t B, int C, int64_t HW, const sd
 #pragma unroll
             for (int t = 0; t < 4; ++t) acc[t] = Tr::mma32(lw[(q * 4 + t) * SD_WAVE + lane], f, acc[t]);
         }
-        if (valid) {
-            uint16_t *op = out + (b * HW + pix) * SD_DH;
+        // own values packed in hidden pairs; the right neighbour's from lane + 1
+        const bool last_col = (pix % W) == W - 1;
+        const int src = (lane + 1) << 2;
 #pragma unroll
-            for (int t = 0; t < 4; ++t)
+        for (int t = 0; t < 4; ++t)
 #pragma unroll
-                for (int r4 = 0; r4 < 4; ++r4) {
-                    // accumulator rows 4 r4 .. 4 r4 + 3 = hidden 32 t + 8 r4 + 4 h + 0..3
-                    uint2 v;
-                    v.x = (uint32_t)Tr::bits(acc[t][4 * r4]) | ((uint32_t)Tr::bits(acc[t][4 * r4 + 1]) << 16);
-                    v.y = (uint32_t)Tr::bits(acc[t][4 * r4 + 2]) | ((uint32_t)Tr::bits(acc[t][4 * r4 + 3]) << 16);
-                    *(uint2 *)(op + 32 * t + 8 * r4 + 4 * h) = v;
+            for (int r4 = 0; r4 < 4; ++r4) {
+                // accumulator rows 4 r4 .. 4 r4 + 3 = hidden 32 t + 8 r4 + 4 h + 0..3
+                const uint32_t o01 = sd_pack2<typename Tr::E>(acc[t][4 * r4], acc[t][4 * r4 + 1]);
+                const uint32_t o23 = sd_pack2<typename Tr::E>(acc[t][4 * r4 + 2], acc[t][4 * r4 + 3]);
+                uint32_t n01 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)o01);
+                uint32_t n23 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)o23);
+                if (last_col) { n01 = o01; n23 = o23; }
+                if (valid) {
+                    const uint4 v = {__builtin_amdgcn_perm(n01, o01, 0x05040100u),
+                                     __builtin_amdgcn_perm(n01, o01, 0x07060302u),
+                                     __builtin_amdgcn_perm(n23, o23, 0x05040100u),
+                                     __builtin_amdgcn_perm(n23, o23, 0x07060302u)};
+                    *(uint4 *)(out + (b * HW + pix) * SD_DH + 32 * t + 8 * r4 + 4 * h) = v;
                 }
-        }
+            }
     }
 }
 
@@ -252,17 +276,31 @@ __device__ __forceinline__ Frag sd_code_frag(const float v[3], int pc, int g) {
 // Per-sample record written by the ray pass into wave-private LDS, quad-major
 // ([q][k][4 words], q = 0 .. RS/4-1) so that both the ray pass (lane = sample) and the
 // item reads (lane j = sample) are conflict-free 16-byte accesses:
-//   q0: tap byte offsets pix * 256 of nw, ne, sw, se (bit 0 of o00: outside the encoder
-//       frustum; bits 0..3 of o01: outside render view 0..3)
-//   q1: bilinear weights w00, w01, w10, w11
+//   q0: byte offsets pix * 512 of the pair rows y0 and y1 at column x0 in the pair-
+//       interleaved P (bit 0 of the first: outside the encoder frustum; bits 0..3 of
+//       the second: outside render view 0..3), 2 spare words
+//   q1: bilinear weights pre-packed in the blend's operand format (T16<P>::pack_w)
 //   q2: x, y, z~ (positional-code inputs), z
 //   q3: delta, colour of render view 0 (r, g, b); then views 1..3 (3 words each)
+// SD_RECBUF = 1: one record buffer per wave, refilled for the wave's next ray just
+// before that ray's first item is opened (the current ray's records are dead by then);
+// 2: double-buffered, the next ray's pass one whole ray ahead (twice the LDS).
 __host__ __device__ constexpr int sd_rec_words(int nv) { return (13 + 3 * nv + 3) & ~3; }
+
+#ifndef SD_RECBUF
+#define SD_RECBUF 2
+#endif
+#ifndef SD_RWG
+#define SD_RWG 256  // render workgroup (4 waves; 2 waves per SIMD: VGPR-bound at ~215)
+#endif
+#ifndef SD_RWAVES
+#define SD_RWAVES 2  // waves per SIMD the register budget is cut for (2: <= 256 VGPRs)
+#endif
 
 struct PItem {
     int ray, sub, sbi, n;
-    uint32_t o[4];  // tap byte offsets + 16 g inside the batch element's P plane
-    float w[4];
+    uint32_t o[2];  // pair-row byte offsets (+ 32 g) inside the batch element's P plane
+    uint4 wp;       // packed blend weights
     float v[3];
     float zk, delta;
     float col[3];   // colour of this lane's render view (group g; NV == 1: view 0)
@@ -272,13 +310,14 @@ struct PItem {
 
 struct PRaw { uint4 a, b, c, d; };
 
+// chunk q (channels 32 q .. 32 q + 31; this lane's group: 8 of them = 32 bytes per row)
 __device__ __forceinline__ PRaw sd_pload(const PItem &it, int q) {
-    const uint32_t s = (uint32_t)q * 64u;
+    const uint32_t s = (uint32_t)q * 128u;
     PRaw r;
     r.a = sd_ld128(it.rs, it.o[0], s);
-    r.b = sd_ld128(it.rs, it.o[1], s);
-    r.c = sd_ld128(it.rs, it.o[2], s);
-    r.d = sd_ld128(it.rs, it.o[3], s);
+    r.b = sd_ld128(it.rs, it.o[0] + 16u, s);
+    r.c = sd_ld128(it.rs, it.o[1], s);
+    r.d = sd_ld128(it.rs, it.o[1] + 16u, s);
     return r;
 }
 
@@ -290,20 +329,19 @@ __device__ __forceinline__ uint32_t sd_relu2(uint32_t x) {
     return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(v, (s16x2){0, 0}));
 }
 
-// LDS image of the render kernel: [identity 2][64] | [code 2][8][64] | [sigma 4][64] |
-// [dino D/16][4][64] (16 B per lane entry), then per wave 2 x K sample records.
-#define SD_LDS_ID 0
-#define SD_LDS_PE (2 * SD_WAVE)
+// LDS image of the render kernel: [code 2][8][64] | [sigma 4][64] | [dino D/16][4][64]
+// (16 B per lane entry), then per wave SD_RECBUF x K sample records.
+#define SD_LDS_PE 0
 #define SD_LDS_SIG (SD_LDS_PE + 16 * SD_WAVE)
 #define SD_LDS_OUT (SD_LDS_SIG + 4 * SD_WAVE)
 
-// wave-uniform cursor with the wave's ray ordinal (selects the record buffer)
+// wave-uniform cursor with the wave's ray ordinal n (selects the record buffer)
 struct RCursor {
     int ray, sub, sbi, n;
 };
 
 template <int P, int NV, int NDT>
-__global__ void __launch_bounds__(SD_PWG)
+__global__ void __launch_bounds__(SD_RWG) __attribute__((amdgpu_waves_per_eu(SD_RWAVES)))
 k_render_proj(const sd_render_args a, const sd_head m) {
     typedef T16<P> Tr;
     typedef typename Tr::Frag Frag;
@@ -311,14 +349,6 @@ k_render_proj(const sd_render_args a, const sd_head m) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     {
         uint4 *d = (uint4 *)lds;
-        for (int i = threadIdx.x; i < 2 * SD_WAVE; i += blockDim.x) {
-            // identity fragments: A[i][k] = 1 iff k == i (tile 2q) / k == 16 + i (tile 2q+1)
-            const int which = i / SD_WAVE, l = i % SD_WAVE, ii = l & 15, gg = l >> 4;
-            Frag f;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) f[e] = (E)((8 * gg + e == ii + 16 * which) ? 1.f : 0.f);
-            d[SD_LDS_ID + i] = __builtin_bit_cast(uint4, f);
-        }
         const uint4 *pe = (const uint4 *)m.w_pe, *sg = (const uint4 *)m.w_sig,
                     *wo = (const uint4 *)m.w_out;
         for (int i = threadIdx.x; i < 16 * SD_WAVE; i += blockDim.x) d[SD_LDS_PE + i] = pe[i];
@@ -339,14 +369,16 @@ k_render_proj(const sd_render_args a, const sd_head m) {
     }
     const int K = a.K, nsub = K >> 4, nv = NV > 0 ? NV : a.nv;
     const int RQ = sd_rec_words(nv) / 4;  // 16-byte quads per record
-    uint4 *recs = (uint4 *)(lds + (SD_LDS_OUT + NDT * 4 * SD_WAVE) * 16) + wave * 2 * K * RQ;
-    const uint32_t plane_bytes = (uint32_t)a.Hf * a.Wf * SD_DH * 2;
+    uint4 *recs = (uint4 *)(lds + (SD_LDS_OUT + NDT * 4 * SD_WAVE) * 16) + wave * SD_RECBUF * K * RQ;
+    const uint32_t plane_bytes = (uint32_t)a.Hf * a.Wf * SD_DH * 4;
     const int64_t cplane = (int64_t)a.Hc * a.Wc * 4;
-    const int nwaves = gridDim.x * (SD_PWG / 64);
-    const int ray0 = blockIdx.x * (SD_PWG / 64) + wave;
+    const int nwaves = gridDim.x * (SD_RWG / 64);
+    const int ray0 = blockIdx.x * (SD_RWG / 64) + wave;
     const int R = (int)a.R, rps = (int)a.rays_per_sb;
     if (ray0 >= R) return;
     const int nitems = ((R - ray0 + nwaves - 1) / nwaves) * nsub;
+    // in-kernel z (a.z == NULL): sd_sample_z's arithmetic, jitter from the counter RNG
+    const float zstep = (float)(1.0 / (double)K), zend = (float)(1.0 - 1.0 / (double)K);
 
     auto advance = [&](RCursor c) {
         if (c.sub + 1 < nsub) {
@@ -364,12 +396,29 @@ k_render_proj(const sd_render_args a, const sd_head m) {
     // zq[2p], zq[2p+1]: z[k], z[k+1] of this lane's sample k = 64 p + lane (prefetched)
     constexpr int MAXP = 2;  // K <= 128
     auto load_ray_z = [&](int ray, float zq[2 * MAXP]) {
-        const float *zr = a.z + (int64_t)ray * K;
+        float zo[MAXP];
+        if (a.z) {
+            const float *zr = a.z + (int64_t)ray * K;
+#pragma unroll
+            for (int p = 0; p < MAXP; ++p) zo[p] = zr[min(64 * p + lane, K - 1)];
+        } else {
+            sd_cfloat *rr = (sd_cfloat *)(a.rays + (int64_t)ray * a.ray_dim);
+            const float near = rr[6], far = rr[7];
+            const uint64_t base = a.z_offset + (uint64_t)ray * (uint64_t)K;
+#pragma unroll
+            for (int p = 0; p < MAXP; ++p) {
+                const int k = min(64 * p + lane, K - 1);
+                zo[p] = sd_z_sample(near, far, K, k, sd_uniform(a.z_seed, base + k), zstep, zend,
+                                    a.z_lindisp);
+            }
+        }
+        // z[k + 1] from the next lane (lane 63: lane 0 of the next 64-sample block)
 #pragma unroll
         for (int p = 0; p < MAXP; ++p) {
-            const int k = min(64 * p + lane, K - 1);
-            zq[2 * p] = zr[k];
-            zq[2 * p + 1] = zr[min(k + 1, K - 1)];
+            float nx = __shfl_down(zo[p], 1, 64);
+            if (lane == 63) nx = (p + 1 < MAXP && 64 * (p + 1) < K) ? __shfl(zo[p + 1 < MAXP ? p + 1 : p], 0, 64) : zo[p];
+            zq[2 * p] = zo[p];
+            zq[2 * p + 1] = nx;
         }
     };
     auto ray_pass = [&](int ray, int sbi, int buf, const float zq[2 * MAXP]) {
@@ -398,10 +447,9 @@ k_render_proj(const sd_render_args a, const sd_head m) {
                         invc |= (ic ? 1u : 0u) << v;
                     }
                 }
-                rb[0 * K + k] = uint4{(uint32_t)geo.t.i00 * 256u | (geo.inv_f ? 1u : 0u),
-                                      (uint32_t)geo.t.i01 * 256u | invc,
-                                      (uint32_t)geo.t.i10 * 256u, (uint32_t)geo.t.i11 * 256u};
-                rb[1 * K + k] = __builtin_bit_cast(uint4, f32x4{geo.t.w00, geo.t.w01, geo.t.w10, geo.t.w11});
+                rb[0 * K + k] = uint4{(uint32_t)geo.t.i00 * 512u | (geo.inv_f ? 1u : 0u),
+                                      (uint32_t)geo.t.i10 * 512u | invc, 0u, 0u};
+                rb[1 * K + k] = sd_pack_w<P>(geo.t.w00, geo.t.w01, geo.t.w10, geo.t.w11);
                 rb[2 * K + k] = __builtin_bit_cast(uint4, f32x4{geo.v[0], geo.v[1], geo.v[2], z0});
                 const float delta = (k + 1 < K) ? (z1 - z0) : 1e10f;
                 rb[3 * K + k] = __builtin_bit_cast(uint4, f32x4{delta, col[0], col[1], col[2]});
@@ -426,21 +474,19 @@ k_render_proj(const sd_render_args a, const sd_head m) {
         it.sub = c.sub;
         it.sbi = c.sbi;
         it.n = c.n;
-        const uint4 *rb = recs + (c.n & 1) * K * RQ;
+        const uint4 *rb = recs + (SD_RECBUF == 2 ? (c.n & 1) : 0) * K * RQ;
         const int k = c.sub * 16 + j;
         const uint4 q0 = rb[k];
-        const f32x4 q1 = __builtin_bit_cast(f32x4, rb[K + k]);
+        const uint4 q1 = rb[K + k];
         const f32x4 q2 = __builtin_bit_cast(f32x4, rb[2 * K + k]);
         const f32x4 q3 = __builtin_bit_cast(f32x4, rb[3 * K + k]);
-        const uint32_t lo = 16u * (uint32_t)g;
-        it.o[0] = (q0.x & ~255u) + lo;
-        it.o[1] = (q0.y & ~255u) + lo;
-        it.o[2] = q0.z + lo;
-        it.o[3] = q0.w + lo;
+        const uint32_t lo = 32u * (uint32_t)g;
+        it.o[0] = (q0.x & ~511u) + lo;
+        it.o[1] = (q0.y & ~511u) + lo;
         it.inv_f = q0.x & 1u;
         const int vv = NV == 1 ? 0 : g;
         it.invc = (q0.y >> vv) & 1u;
-        it.w[0] = q1[0]; it.w[1] = q1[1]; it.w[2] = q1[2]; it.w[3] = q1[3];
+        it.wp = q1;
         it.v[0] = q2[0]; it.v[1] = q2[1]; it.v[2] = q2[2];
         it.zk = q2[3];
         it.delta = q3[0];
@@ -479,14 +525,21 @@ k_render_proj(const sd_render_args a, const sd_head m) {
     // one item: `cur` computes, `nxt` is opened (unrolled by two below so the item
     // state ping-pongs between two register sets instead of being copied)
     auto step = [&](PItem &cur, PItem &nxt) {
-        // first item of a ray: records of the wave's next ray into the other buffer
-        if (cur.sub == 0 && cur.ray + nwaves < R) {
-            const int nr = cur.ray + nwaves;
 #if !SD_ABL_NORAYPASS
-            ray_pass(nr, (int)((unsigned)nr / (unsigned)rps), (cur.n + 1) & 1, zq);
-#endif
-            if (nr + nwaves < R) load_ray_z(nr + nwaves, zq);
+        if (SD_RECBUF == 2) {
+            // first item of a ray: records of the wave's next ray into the other buffer
+            if (cur.sub == 0 && cur.ray + nwaves < R) {
+                const int nr = cur.ray + nwaves;
+                ray_pass(nr, (int)((unsigned)nr / (unsigned)rps), (cur.n + 1) & 1, zq);
+                if (nr + nwaves < R) load_ray_z(nr + nwaves, zq);
+            }
+        } else if (c1.n != cur.n) {
+            // the next item starts the wave's next ray: its records replace this ray's
+            // (every record of this ray was read when `cur` was opened)
+            ray_pass(c1.ray, c1.sbi, 0, zq);
+            if (c1.ray + nwaves < R) load_ray_z(c1.ray + nwaves, zq);
         }
+#endif
         open_item(c1, nxt);
         c1 = advance(c1);
 
@@ -497,7 +550,7 @@ k_render_proj(const sd_render_args a, const sd_head m) {
 #define SD_PCHUNK(r, q)                                                        \
         {                                                                      \
             Frag f_ = SD_ABL_NOBLEND ? __builtin_bit_cast(Frag, r.a ^ r.b ^ r.c ^ r.d) \
-                                     : Tr::blend(r.a, r.b, r.c, r.d, cur.w);   \
+                                     : sd_blend_pair<P>(r.a, r.b, r.c, r.d, cur.wp); \
             r = sd_pload(nxt, q);                                              \
             acc[2 * q] = Tr::mma(id0, f_, zero4);                              \
             acc[2 * q + 1] = Tr::mma(id1, f_, zero4);                          \
@@ -561,17 +614,17 @@ k_render_proj(const sd_render_args a, const sd_head m) {
             for (int r = 0; r < 4; ++r) dacc[dt][r] = fmaf(w, o[r], dacc[dt][r]);
         }
 
-        // per-sample outputs
-        const int64_t o = (int64_t)cur.ray * K + k;
+        // per-sample outputs: wave-uniform ray base + 32-bit lane offset
+        const int64_t rk = (int64_t)cur.ray * K;
         if (g == 0) {
-            if (a.weights) a.weights[o] = w;
-            if (a.alphas) a.alphas[o] = alpha;
-            if (a.invalid_f) a.invalid_f[o] = cur.inv_f ? 1 : 0;
+            if (a.weights) (a.weights + rk)[k] = w;
+            if (a.alphas) (a.alphas + rk)[k] = alpha;
+            if (a.invalid_f) (a.invalid_f + rk)[k] = cur.inv_f ? 1 : 0;
         }
         if (g < nv) {
-            if (a.invalid) a.invalid[o * nv + g] = (cur.invc | cur.inv_f) ? 1.f : 0.f;
+            if (a.invalid) (a.invalid + rk * nv)[k * nv + g] = (cur.invc | cur.inv_f) ? 1.f : 0.f;
             if (a.rgb_samps) {
-                float *rsp = a.rgb_samps + (o * nv + g) * 3;
+                float *rsp = a.rgb_samps + rk * nv * 3 + (k * nv + g) * 3;
                 rsp[0] = cur.col[0]; rsp[1] = cur.col[1]; rsp[2] = cur.col[2];
             }
         }
@@ -618,14 +671,14 @@ k_render_proj(const sd_render_args a, const sd_head m) {
 // ---------------------------------------------------------------------------
 template <typename KernT>
 static int sd_launch_proj(KernT kern, int64_t work_waves, int lds_bytes, hipStream_t s,
-                          int64_t &nblk) {
+                          int64_t &nblk, int wg = SD_PWG) {
     (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                               lds_bytes);
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, SD_PWG, lds_bytes) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, wg, lds_bytes) !=
             hipSuccess || per_cu <= 0)
         per_cu = 1;
-    nblk = (work_waves + SD_PWG / 64 - 1) / (SD_PWG / 64);
+    nblk = (work_waves + wg / 64 - 1) / (wg / 64);
     const int64_t cap = (int64_t)sd_num_cus() * per_cu;
     if (nblk > cap) nblk = cap;
     return 0;
@@ -656,15 +709,15 @@ extern "C" int sd_project_grid(const float *grid, int64_t B, int64_t Hf, int64_t
     }
     hipStream_t s = (hipStream_t)stream;
     int64_t nblk;
-    const int64_t work = B * ((HW + 31) / 32);
+    const int64_t work = B * ((HW + 30) / 31);
     if (m->dtype == SD_F16) {
         sd_launch_proj(k_project<SD_F16>, work, lds_bytes, s, nblk);
         hipLaunchKernelGGL(k_project<SD_F16>, dim3((unsigned)nblk), dim3(SD_PWG), lds_bytes, s,
-                           grid, B, m->C, HW, *m, (uint16_t *)out);
+                           grid, B, m->C, HW, (int)Wf, *m, (uint32_t *)out);
     } else {
         sd_launch_proj(k_project<SD_BF16>, work, lds_bytes, s, nblk);
         hipLaunchKernelGGL(k_project<SD_BF16>, dim3((unsigned)nblk), dim3(SD_PWG), lds_bytes, s,
-                           grid, B, m->C, HW, *m, (uint16_t *)out);
+                           grid, B, m->C, HW, (int)Wf, *m, (uint32_t *)out);
     }
     return sd_check_err();
 }
@@ -672,10 +725,14 @@ extern "C" int sd_project_grid(const float *grid, int64_t B, int64_t Hf, int64_t
 template <int P, int NV, int NDT>
 static int sd_rp_launch(const sd_render_args &a, const sd_head &m, hipStream_t s) {
     const int lds_bytes = (SD_LDS_OUT + NDT * 4 * SD_WAVE) * 16 +
-                          (SD_PWG / 64) * 2 * a.K * sd_rec_words(a.nv) * 4;
+                          (SD_RWG / 64) * SD_RECBUF * a.K * sd_rec_words(a.nv) * 4;
+    if (lds_bytes > 160 * 1024) {
+        sd_set_error("sd_render_proj: LDS image exceeds 160 KiB (K or D too large)");
+        return -1;
+    }
     int64_t nblk;
-    sd_launch_proj(k_render_proj<P, NV, NDT>, a.R, lds_bytes, s, nblk);
-    hipLaunchKernelGGL((k_render_proj<P, NV, NDT>), dim3((unsigned)nblk), dim3(SD_PWG), lds_bytes,
+    sd_launch_proj(k_render_proj<P, NV, NDT>, a.R, lds_bytes, s, nblk, SD_RWG);
+    hipLaunchKernelGGL((k_render_proj<P, NV, NDT>), dim3((unsigned)nblk), dim3(SD_RWG), lds_bytes,
                        s, a, m);
     return sd_check_err();
 }
@@ -706,9 +763,9 @@ extern "C" int sd_render_proj(const sd_render_args *args, const sd_head *m, void
     }
     const sd_render_args &a = *args;
     if (a.R < 0 || a.R >= (1LL << 31) || a.K <= 0 || (a.K % 16) || a.K > 128 || a.ray_dim < 6 ||
-        a.rays_per_sb <= 0 || !a.rays ||
-        !a.z || !a.grid || !a.cam_f || !a.depth || !a.dino || a.Hf <= 0 || a.Wf <= 0 ||
-        a.nv < 0 || a.nv > SD_MAX_NV || (int64_t)a.Hf * a.Wf * SD_DH * 2 >= (1LL << 32) ||
+        a.rays_per_sb <= 0 || !a.rays || (!a.z && a.ray_dim < 8) ||
+        !a.grid || !a.cam_f || !a.depth || !a.dino || a.Hf <= 0 || a.Wf <= 0 ||
+        a.nv < 0 || a.nv > SD_MAX_NV || (int64_t)a.Hf * a.Wf * SD_DH * 4 >= (1LL << 32) ||
         (a.nv > 0 && (!a.img || !a.cam_c || !a.rgb || a.Hc <= 0 || a.Wc <= 0))) {
         sd_set_error("sd_render_proj: invalid argument (K % 16 == 0, K <= 128, nv <= 4, "
                      "P plane < 4 GiB)");

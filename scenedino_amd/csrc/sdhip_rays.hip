@@ -52,15 +52,7 @@ __global__ void __launch_bounds__(256) k_sample_z(const float *__restrict__ rays
     int64_t r = gid / K, k = gid - r * K;
     float near = rays[r * ray_dim + 6], far = rays[r * ray_dim + 7];
     float uu = u ? u[gid] : sd_uniform(seed, offset + (uint64_t)gid);
-    float t = sd_linspace_at(0.0f, t_end, K, k) + uu * step;
-    float zz;
-    if (lindisp) {
-        float a = (1.0f / near) * (1.0f - t);
-        float b = (1.0f / far) * t;
-        zz = 1.0f / (a + b);
-    } else {
-        zz = near * (1.0f - t) + far * t;
-    }
+    float zz = sd_z_sample(near, far, K, k, uu, step, t_end, lindisp);
     z[gid] = zz;
 }
 
@@ -103,6 +95,17 @@ __global__ void __launch_bounds__(256) k_pack_image(const float *__restrict__ in
     const float *s = in + n * 3 * hw + p;
     f32x4 v = {s[0], s[hw], s[2 * hw], 0.f};
     *(f32x4 *)(out + gid * 4) = v;
+}
+
+// Camera records [w2c rows 0..2 | K] (21 floats) for n views; one thread per word.
+__global__ void __launch_bounds__(256) k_cam_records(const float *__restrict__ w2c, int64_t s_w,
+                                                     const float *__restrict__ Ks, int64_t s_k,
+                                                     int64_t n, float *__restrict__ out) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= n * 21) return;
+    const int64_t v = gid / 21;
+    const int e = (int)(gid - v * 21);
+    out[gid] = e < 12 ? w2c[v * s_w + e] : Ks[v * s_k + (e - 12)];
 }
 
 // ---------------------------------------------------------------------------
@@ -184,5 +187,18 @@ extern "C" int sd_pack_image(const float *img_nchw, int64_t N, int64_t H, int64_
     hipLaunchKernelGGL(k_pack_image, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                        (hipStream_t)stream, img_nchw, N, H, W, out_nhwc4);
     SD_CHECK_LAUNCH("sd_pack_image");
+    return 0;
+}
+
+extern "C" int sd_cam_records(const float *w2c, int64_t s_w, const float *Ks, int64_t s_k,
+                              int64_t n, float *out, void *stream) {
+    if (!w2c || !Ks || !out || n < 0 || s_w < 16 || s_k < 9) {
+        sd_set_error("sd_cam_records: invalid argument");
+        return -1;
+    }
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_cam_records, dim3((unsigned)((n * 21 + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, w2c, s_w, Ks, s_k, n, out);
+    SD_CHECK_LAUNCH("sd_cam_records");
     return 0;
 }

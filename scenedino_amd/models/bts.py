@@ -28,10 +28,9 @@ PRECISIONS = {"fp32": _lib.SD_F32, "bf16": _lib.SD_BF16, "fp16": _lib.SD_F16}
 
 
 def _cam_records(poses_w2c, Ks):
-    """(..., 4, 4) w2c and (..., 3, 3) K -> (..., 21) camera records (C ABI layout)."""
-    lead = poses_w2c.shape[:-2]
-    return torch.cat((poses_w2c[..., :3, :].reshape(*lead, 12).float(),
-                      Ks.reshape(*lead, 9).float()), -1).contiguous()
+    """(..., 4, 4) w2c and (..., 3, 3) K -> (..., 21) camera records (C ABI layout,
+    sd_cam_records)."""
+    return _lib.cam_records(poses_w2c, Ks)
 
 
 class BTSNet(nn.Module):
@@ -251,37 +250,48 @@ class BTSNet(nn.Module):
 
     # -- hot path -------------------------------------------------------------
     def render_fused(self, rays, z, sb, hard_alpha_cap, want_weights=True, want_alphas=True,
-                     want_rgb_samps=False):
+                     want_rgb_samps=False, K=None, z_seed=None, lindisp=True):
         """Fused field query + alpha compositing for all rays (used by NeRFRenderer).
-        rays (R, ray_dim) fp32, z (R, K) fp32 on the GPU; R = sb * rays_per_sb."""
+        rays (R, ray_dim) fp32, z (R, K) fp32 on the GPU; R = sb * rays_per_sb.
+        z None: K depths per ray drawn as sd_sample_z(seed=z_seed, lindisp) would -- inside
+        the projected render kernel (no (R, K) array), or by sd_sample_z for the grid
+        kernel."""
         self._check_supported()
         m = self._mlp()
         gc = self._grids()
         if gc["C"] != m.C:
             raise ValueError(f"feature grid has {gc['C']} channels, the MLP expects {m.C}")
-        R, K = z.shape
+        proj = self._use_proj()
+        rays = rays.float().contiguous()
+        if z is None:
+            if K is None or z_seed is None:
+                raise ValueError("render_fused: z=None needs K and z_seed")
+            if not proj:
+                z = _lib.sample_z(rays, K, lindisp, seed=z_seed)
+        R = rays.shape[0]
+        K = z.shape[1] if z is not None else K
         if R % sb or gc["B"] != sb:
             raise ValueError(f"rays ({R}) must split into {sb} super-batches matching the "
                              f"encoded batch ({gc['B']})")
-        dev = z.device
+        dev = rays.device
         nv = gc["nv"]
         out = {
             "depth": torch.empty(R, device=dev),
             "dino": torch.empty(R, m.D, device=dev),
             "rgb": torch.empty(R, 3 * nv, device=dev),
             "invalid": torch.empty(R, K, nv, device=dev),
-            "invalid_f": torch.empty(R, K, device=dev, dtype=torch.uint8),
+            "invalid_f": torch.empty(R, K, device=dev, dtype=torch.bool),  # bytes 0 / 1
             "weights": torch.empty(R, K, device=dev) if want_weights else None,
             "alphas": torch.empty(R, K, device=dev) if want_alphas else None,
             "rgb_samps": torch.empty(R, K, 3 * nv, device=dev) if want_rgb_samps else None,
         }
-        rays = rays.float().contiguous()
-        z = z.contiguous()
-        proj = self._use_proj()
+        if z is not None:
+            z = z.contiguous()
         grid = self._grid_proj(gc, m) if proj else self._grid_nhwc(gc)
         args = _lib.SdRenderArgs(
             rays=rays.data_ptr(), ray_dim=rays.shape[1], R=R, rays_per_sb=R // sb, K=K,
-            z=z.data_ptr(), grid=grid.data_ptr(), Hf=gc["Hf"], Wf=gc["Wf"],
+            z=z.data_ptr() if z is not None else None, grid=grid.data_ptr(), Hf=gc["Hf"],
+            Wf=gc["Wf"],
             cam_f=gc["cam_f"].data_ptr(), img=gc["img"].data_ptr(), nv=nv, Hc=gc["Hc"],
             Wc=gc["Wc"], cam_c=gc["cam_c"].data_ptr(), hard_alpha_cap=int(bool(hard_alpha_cap)),
             depth=out["depth"].data_ptr(), dino=out["dino"].data_ptr(),
@@ -289,11 +299,12 @@ class BTSNet(nn.Module):
             weights=out["weights"].data_ptr() if want_weights else None,
             alphas=out["alphas"].data_ptr() if want_alphas else None,
             invalid=out["invalid"].data_ptr(), invalid_f=out["invalid_f"].data_ptr(),
-            rgb_samps=out["rgb_samps"].data_ptr() if want_rgb_samps else None)
+            rgb_samps=out["rgb_samps"].data_ptr() if want_rgb_samps else None,
+            z_lindisp=int(bool(lindisp)), z_seed=(z_seed or 0) & (2**64 - 1), z_offset=0)
         if proj:
-            self._timed("render", lambda: _lib.render_proj(args, m.head_rec, z))
+            self._timed("render", lambda: _lib.render_proj(args, m.head_rec, rays))
         else:
-            self._timed("render", lambda: _lib.render_fused(args, m.rec, z))
+            self._timed("render", lambda: _lib.render_fused(args, m.rec, rays))
         return out
 
     def query(self, xyz):
@@ -314,7 +325,7 @@ class BTSNet(nn.Module):
         dino = torch.empty(n, P, m.D, device=dev)
         rgb = torch.empty(n, P, 3 * nv, device=dev)
         inv = torch.empty(n, P, nv, device=dev)
-        invf = torch.empty(n, P, device=dev, dtype=torch.uint8)
+        invf = torch.empty(n, P, device=dev, dtype=torch.bool)  # bytes 0 / 1
         args = _lib.SdFieldArgs(
             xyz=xyz.data_ptr(), B=n, P=P, grid=self._grid_nhwc(gc).data_ptr(), Hf=gc["Hf"],
             Wf=gc["Wf"],
@@ -323,7 +334,7 @@ class BTSNet(nn.Module):
             dino=dino.data_ptr(), rgb=rgb.data_ptr(), invalid=inv.data_ptr(),
             invalid_f=invf.data_ptr())
         _lib.field_query(args, m.rec, xyz)
-        return sigma, dino, rgb, inv, invf.bool()
+        return sigma, dino, rgb, inv, invf
 
     def forward(self, xyz: torch.Tensor, **kwargs):
         """Same return contract as bts.py:476-595."""

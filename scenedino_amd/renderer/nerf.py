@@ -73,6 +73,8 @@ class NeRFRenderer(torch.nn.Module):
         self.normalize_dino = normalize_dino
         self.z_jitter = None          # parity hook (see module docstring)
         self._rng_offset = 0
+        self._want = None             # per-forward: which per-sample outputs are written
+        self._z_seed = None           # per-forward: in-kernel z sampling seed
 
     # -- sampling -------------------------------------------------------------
     def _jitter_seed(self):
@@ -132,29 +134,39 @@ class NeRFRenderer(torch.nn.Module):
                 raise NotImplementedError("render_mode surface/neus is not used by shipped configs")
             if self.training and self.noise_std > 0.0:
                 raise NotImplementedError("sigma noise (training) is outside the inference hot path")
-            B, K = z_samp.shape
+            # z_samp None: the fused kernel draws the depths itself (forward() decided,
+            # seed in self._z_seed); the (B, K) depth array is never materialised
+            B = rays.shape[0]
+            K = z_samp.shape[1] if z_samp is not None else self.n_coarse
             r_dim = rays.shape[-1]
             sbn = sb if sb > 0 else 1
-            if (hasattr(model, "render_fused") and not getattr(model, "use_viewdirs", False)
-                    and model.fused_supported(K)):
+            want = getattr(self, "_want", None) or {}
+            if self._fused_ok(model, K):
                 o = model.render_fused(rays, z_samp, sbn, self.hard_alpha_cap,
-                                       want_weights=True, want_alphas=True,
-                                       want_rgb_samps=self._want_rgb_samps)
-                nv = o["invalid"].shape[-1]
+                                       want_weights=want.get("weights", True),
+                                       want_alphas=want.get("alphas", True),
+                                       want_rgb_samps=want.get("rgb_samps", False),
+                                       K=K, z_seed=self._z_seed, lindisp=self.lindisp)
                 weights, alphas = o["weights"], o["alphas"]
                 rgb_final, depth_final = o["rgb"], o["depth"]
                 invalid = o["invalid"]
                 rgbs = o["rgb_samps"]
-                state_dicts = {"invalid_features": o["invalid_f"].bool().view(B, K, 1),
+                state_dicts = {"invalid_features": o["invalid_f"].view(B, K, 1),
                                "dino_features": o["dino"]}
             else:
                 weights, alphas, rgb_final, depth_final, invalid, rgbs, state_dicts = \
                     self._composite_generic(model, rays, z_samp, coarse, sb)
             if self.white_bkgd:
+                if weights is None:
+                    raise RuntimeError("white_bkgd needs the per-sample weights")
                 rgb_final = rgb_final + 1 - weights.sum(dim=1).unsqueeze(-1)
             ray_info = rays[:, None, 8:] if r_dim > 8 else None
             return (weights, rgb_final, depth_final, alphas, invalid, z_samp, rgbs, ray_info,
                     None, state_dicts)
+
+    def _fused_ok(self, model, K):
+        return (hasattr(model, "render_fused") and not getattr(model, "use_viewdirs", False)
+                and model.fused_supported(K))
 
     def _composite_generic(self, model, rays, z_samp, coarse, sb):
         B, K = z_samp.shape
@@ -203,8 +215,17 @@ class NeRFRenderer(torch.nn.Module):
             sbs = rays.shape[0]
             r_dim = rays.shape[-1]
             rays = rays.reshape(-1, r_dim)
-            self._want_rgb_samps = want_rgb_samps
-            if sample_from_dist is None:
+            # per-sample outputs nobody asked for are not written by the fused kernel;
+            # the fine pass and white_bkgd need the weights
+            self._want = {"weights": want_weights or self.using_fine or self.white_bkgd,
+                          "alphas": want_alphas, "rgb_samps": want_rgb_samps}
+            self._z_seed = None
+            if (sample_from_dist is None and self.z_jitter is None and not want_z_samps
+                    and not self.using_fine and self._fused_ok(model, self.n_coarse)):
+                # z sampled inside the fused kernel (same RNG stream as sd_sample_z)
+                z_coarse = None
+                self._z_seed = self._jitter_seed()
+            elif sample_from_dist is None:
                 z_coarse = self.sample_coarse(rays)
             else:
                 pw, pz = sample_from_dist
@@ -225,13 +246,14 @@ class NeRFRenderer(torch.nn.Module):
                 fc = self.composite(model, rays, z_comb.contiguous(), coarse=False, sb=sbs)
                 outputs["fine"] = self._format_outputs(fc, sbs, want_weights, want_alphas,
                                                        want_z_samps, want_rgb_samps)
+            self._want, self._z_seed = None, None
             return outputs
 
     def _format_outputs(self, rendered, superbatch_size, want_weights=False, want_alphas=False,
                         want_z_samps=False, want_rgb_samps=False):
         (weights, rgb_final, depth, alphas, invalid, z_samps, rgb_samps, ray_info, extras,
          state_dict) = rendered
-        n_smps = weights.shape[-1]
+        n_smps = invalid.shape[1]
         out_d_rgb = rgb_final.shape[-1]
         out_d_i = invalid.shape[-1]
         if superbatch_size > 0:

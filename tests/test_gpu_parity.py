@@ -191,11 +191,17 @@ def test_projected_grid_vs_dense_projection(precision):
     b_out = torch.randn(65, generator=g) * 0.1
     dt = _lib.SD_BF16 if precision == "bf16" else _lib.SD_F16
     pk = PackedMLP(W_in.to(DEV), b_in.to(DEV), W_out.to(DEV), b_out.to(DEV), dt)
-    P = _lib.project_grid(grid.to(DEV), pk.rec, dt).double().cpu()   # (2, Hf, Wf, 128)
+    P2 = _lib.project_grid(grid.to(DEV), pk.rec, dt).double().cpu()   # (2, Hf, Wf, 128, 2)
+    assert P2.shape == (2, Hf, Wf, 128, 2)
+    P = P2[..., 0]
     tdt = _lib.TORCH_DTYPE[dt]
     ref = torch.einsum("nc,bchw->bhwn", W_in[:, :C].to(tdt).double(), grid.to(tdt).double()) \
         + b_in.double()
     assert rel_l2(P, ref) < (4e-3 if precision == "bf16" else 1e-3)
+    # pair slot: the right neighbour's row (border: the last column pairs with itself),
+    # bit-identical to that pixel's own slot (waves overlap by one column, 31-pixel steps)
+    right = torch.clamp(torch.arange(Wf) + 1, max=Wf - 1)
+    assert torch.equal(P2[..., 1], P[:, :, right])
 
 
 def test_render_full_192x640x64_vs_reference_subsample():
@@ -352,3 +358,35 @@ def test_render_full_192x640x64_projected_vs_reference_subsample(precision):
     assert rel_l2(c["dino_features"][0].cpu()[idx], d["dino"]) < 1e-2
     assert rel_l2(c["rgb"][0].cpu()[idx], d["rgb"]) < 1e-2
     assert rel_l2(c["weights"][0].cpu()[idx], d["weights"]) < 2e-2
+
+
+@pytest.mark.parametrize("fx", ["render_k64_cap1.npz", "render_sb2_nv2_k16.npz"])
+@pytest.mark.parametrize("precision", ["bf16", "fp16"])
+def test_in_kernel_z_matches_sample_z(fx, precision):
+    """With no jitter hook and want_z_samps=False the projected kernel draws the depths
+    itself (sd_render_args.z == NULL); with want_z_samps=True the same RNG stream goes
+    through sd_sample_z into an (R, K) array.  Same seed => bit-identical renders.
+    Also: per-sample outputs that were not asked for are absent (not written)."""
+    from scenedino_amd.renderer import NeRFRenderer
+    d = load(fx)
+    net = net_from_fixture(d, precision, mode="proj")
+    K = int(d["K"])
+    r = NeRFRenderer(n_coarse=K, lindisp=True, hard_alpha_cap=bool(d["hard_cap"]))
+    w = r.bind_parallel(net).eval()
+    outs = []
+    for want_z in (False, True):
+        torch.manual_seed(5)
+        with torch.no_grad():
+            outs.append(w(T(d["rays"]), want_weights=True, want_z_samps=want_z)["coarse"])
+    a, b = outs
+    assert "z_samps" not in a and "z_samps" in b and "alphas" not in a
+    for k in ("depth", "dino_features", "rgb", "weights", "invalid", "invalid_features"):
+        assert torch.equal(a[k], b[k]), k
+    # the in-kernel depths are sd_sample_z's: compare the composited depth with z_samps
+    zs = b["z_samps"]
+    assert bool((b["depth"] <= zs[..., -1] + 1e-3).all())
+    torch.manual_seed(5)
+    with torch.no_grad():
+        c = w(T(d["rays"]))["coarse"]
+    assert "weights" not in c
+    assert torch.equal(c["depth"], a["depth"]) and torch.equal(c["dino_features"], a["dino_features"])
