@@ -4,10 +4,12 @@
 Workload (BASELINE.json configs[1]): one 192x640 frame per GPU,
 64 samples/ray (7,864,320 points), ViT-S/16-shaped 256x192x640 feature grid,
 ResnetFC 295->128->65 (random kaiming init), lindisp stratified sampling, bf16.
-A "step" = ImageRaySampler.sample (sd_gen_rays) -> sample_coarse (sd_sample_z) ->
-NCHW->NHWC grid pack (sd_pack_grid) -> fused field+composite (sd_render_fused) for
-one frame per GPU; for N>1 every rank renders its own frame (C3: frames sharded
-1-per-GPU) and the rendered maps (depth, DINO, RGB) are all-gathered over RCCL.
+A "step" = ImageRaySampler.sample (sd_gen_rays) -> the frame's device-side state
+(sd_pack_image, sd_cam_records) -> projected grid P = W_in G + b_in (sd_project_grid) ->
+fused render (sd_render_proj: z sampling, points, projection, code, P gather, MFMA MLP,
+colours, alpha compositing) for one frame per GPU; for N>1 every rank renders its own
+frame (C3: frames sharded 1-per-GPU) and the rendered maps (depth, DINO, RGB) are
+all-gathered over RCCL.
 The ViT/DPT encoder is not part of the timed step (separate scope row).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--precision bf16|fp32]
@@ -167,6 +169,23 @@ def cpu_baseline(budget_s: float = 20.0):
                       f"({cpu}); encoder excluded"}
 
 
+def _traffic_from_profile(proj):
+    """HBM bytes per frame of the rendering kernels, from the committed rocprofv3 PMC
+    summary of this bench command (profiles/*_traffic.json, tools/traffic_json.py; PMC
+    counters cannot be read from inside the timed process)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")))
+    if not files:
+        return None
+    try:
+        d = json.load(open(files[-1]))
+        ks = ("k_project", "k_render_proj") if proj else ("k_render<",)
+        tot = sum(d["kernels"][k]["hbm_bytes"] for k in ks)
+    except (KeyError, TypeError, ValueError):
+        return None
+    return tot, os.path.relpath(files[-1], ROOT) + " (rocprofv3 PMC, per frame)"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -286,6 +305,10 @@ def main():
                 "executed_tflops": exec_flops / (kern_ms * 1e-3) / 1e12,
             },
         }
+        tr = _traffic_from_profile(proj)
+        if tr is not None:
+            line["roofline"]["traffic"] = tr[0]
+            line["roofline"]["traffic_source"] = tr[1]
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(args.cpu_budget)
         print(json.dumps(line), flush=True)

@@ -85,18 +85,50 @@ __device__ __forceinline__ void sd_sample_rgb(const float *__restrict__ img, con
         out[i] = ((a[i] * t.w00 + b[i] * t.w01) + c[i] * t.w10) + d[i] * t.w11;
 }
 
-// colour sample + validity in a render view (bts.py:336-346; clamp before the frustum test)
+// colour-sample taps + validity in a render view (bts.py:336-346; clamp before the
+// frustum test)
 template <typename CP>
-__device__ __forceinline__ bool sd_color_view(CP cam, const float *img, int Wc, int Hc,
-                                              float px, float py, float pz, float col[3]) {
+__device__ __forceinline__ Taps sd_color_taps(CP cam, int Wc, int Hc, float px, float py, float pz,
+                                              bool &inv) {
     float x, y, zc;
     sd_project(cam, px, py, pz, x, y, zc);
     x = fminf(fmaxf(x, -2.f), 2.f);
     y = fminf(fmaxf(y, -2.f), 2.f);
-    bool inv = sd_outside(x, y, zc);
-    Taps tc = sd_taps(x, y, Wc, Hc);
+    inv = sd_outside(x, y, zc);
+    return sd_taps(x, y, Wc, Hc);
+}
+
+template <typename CP>
+__device__ __forceinline__ bool sd_color_view(CP cam, const float *img, int Wc, int Hc,
+                                              float px, float py, float pz, float col[3]) {
+    bool inv;
+    const Taps tc = sd_color_taps(cam, Wc, Hc, px, py, pz, inv);
     sd_sample_rgb(img, tc, col);
     return inv;
+}
+
+// colour sample split in two: the four texel loads issued now, the blend later (after
+// other work has hidden their latency)
+struct ColPend {
+    f32x4 a, b, c, d;
+    float w00, w01, w10, w11;
+    float delta;
+};
+
+__device__ __forceinline__ void sd_color_issue(const float *__restrict__ img, const Taps &t,
+                                               ColPend &cp) {
+    cp.a = *(const f32x4 *)(img + (int64_t)t.i00 * 4);
+    cp.b = *(const f32x4 *)(img + (int64_t)t.i01 * 4);
+    cp.c = *(const f32x4 *)(img + (int64_t)t.i10 * 4);
+    cp.d = *(const f32x4 *)(img + (int64_t)t.i11 * 4);
+    cp.w00 = t.w00; cp.w01 = t.w01; cp.w10 = t.w10; cp.w11 = t.w11;
+}
+
+// same arithmetic and order as sd_sample_rgb
+__device__ __forceinline__ void sd_color_finish(const ColPend &cp, float out[3]) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+        out[i] = ((cp.a[i] * cp.w00 + cp.b[i] * cp.w01) + cp.c[i] * cp.w10) + cp.d[i] * cp.w11;
 }
 
 

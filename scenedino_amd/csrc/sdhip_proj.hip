@@ -421,6 +421,10 @@ k_render_proj(const sd_render_args a, const sd_head m) {
             zq[2 * p + 1] = nx;
         }
     };
+    // NV == 1: the colour texel loads of sample 64 p + lane, p = 0, are left in flight
+    // (ColPend) and the colour words written by ray_col at the end of the item
+    constexpr bool DEFER = NV == 1;
+    ColPend cpend;
     auto ray_pass = [&](int ray, int sbi, int buf, const float zq[2 * MAXP]) {
         sd_cfloat *rr = (sd_cfloat *)(a.rays + (int64_t)ray * a.ray_dim);
         const float ox = rr[0], oy = rr[1], oz = rr[2], dx = rr[3], dy = rr[4], dz = rr[5];
@@ -434,10 +438,19 @@ k_render_proj(const sd_render_args a, const sd_head m) {
                 PointGeo geo = sd_point_geo<true>((sd_cfloat *)(a.cam_f + sbi * 21), px, py, pz, a.Wf, a.Hf);
                 float col[3 * SD_MAX_NV];
                 uint32_t invc = 0;
+                const float delta = (k + 1 < K) ? (z1 - z0) : 1e10f;
+                if (DEFER && p == 0) {
+                    bool ic;
+                    const Taps tc = sd_color_taps((sd_cfloat *)(a.cam_c + sbi * 21), a.Wc, a.Hc,
+                                                  px, py, pz, ic);
+                    sd_color_issue(a.img + (int64_t)sbi * cplane, tc, cpend);
+                    cpend.delta = delta;
+                    invc = ic ? 1u : 0u;
+                }
 #pragma unroll
                 for (int v = 0; v < SD_MAX_NV; ++v) {
                     col[3 * v] = col[3 * v + 1] = col[3 * v + 2] = 0.f;
-                    if (v < nv) {
+                    if (v < nv && !(DEFER && p == 0)) {
                         const bool ic = NV == 1
                             ? sd_color_view((sd_cfloat *)(a.cam_c + sbi * 21), a.img + (int64_t)sbi * cplane,
                                             a.Wc, a.Hc, px, py, pz, col)
@@ -451,8 +464,8 @@ k_render_proj(const sd_render_args a, const sd_head m) {
                                       (uint32_t)geo.t.i10 * 512u | invc, 0u, 0u};
                 rb[1 * K + k] = sd_pack_w<P>(geo.t.w00, geo.t.w01, geo.t.w10, geo.t.w11);
                 rb[2 * K + k] = __builtin_bit_cast(uint4, f32x4{geo.v[0], geo.v[1], geo.v[2], z0});
-                const float delta = (k + 1 < K) ? (z1 - z0) : 1e10f;
-                rb[3 * K + k] = __builtin_bit_cast(uint4, f32x4{delta, col[0], col[1], col[2]});
+                if (!(DEFER && p == 0))
+                    rb[3 * K + k] = __builtin_bit_cast(uint4, f32x4{delta, col[0], col[1], col[2]});
 #pragma unroll
                 for (int q = 4; q < sd_rec_words(SD_MAX_NV) / 4; ++q)
                     if (q < RQ) {
@@ -465,6 +478,16 @@ k_render_proj(const sd_render_args a, const sd_head m) {
                         rb[q * K + k] = __builtin_bit_cast(uint4, f32x4{e[0], e[1], e[2], e[3]});
                     }
             }
+        }
+        __builtin_amdgcn_wave_barrier();
+    };
+    // deferred colour words of the last ray pass (sample k = lane)
+    auto ray_col = [&](int buf) {
+        if (DEFER && lane < K) {
+            float col[3];
+            sd_color_finish(cpend, col);
+            recs[buf * K * RQ + 3 * K + lane] =
+                __builtin_bit_cast(uint4, f32x4{cpend.delta, col[0], col[1], col[2]});
         }
         __builtin_amdgcn_wave_barrier();
     };
@@ -509,6 +532,7 @@ k_render_proj(const sd_render_args a, const sd_head m) {
     float zq[2 * MAXP];
     load_ray_z(c0.ray, zq);
     ray_pass(c0.ray, c0.sbi, 0, zq);
+    ray_col(0);
     const bool more = ray0 + nwaves < R;
     if (more) load_ray_z(ray0 + nwaves, zq);  // z of the wave's second ray in flight
     PItem cur;
@@ -525,18 +549,21 @@ k_render_proj(const sd_render_args a, const sd_head m) {
     // one item: `cur` computes, `nxt` is opened (unrolled by two below so the item
     // state ping-pongs between two register sets instead of being copied)
     auto step = [&](PItem &cur, PItem &nxt) {
+        bool passed = false;  // wave-uniform: a ray pass left colour loads in flight
 #if !SD_ABL_NORAYPASS
         if (SD_RECBUF == 2) {
             // first item of a ray: records of the wave's next ray into the other buffer
             if (cur.sub == 0 && cur.ray + nwaves < R) {
                 const int nr = cur.ray + nwaves;
                 ray_pass(nr, (int)((unsigned)nr / (unsigned)rps), (cur.n + 1) & 1, zq);
+                passed = true;
                 if (nr + nwaves < R) load_ray_z(nr + nwaves, zq);
             }
         } else if (c1.n != cur.n) {
             // the next item starts the wave's next ray: its records replace this ray's
             // (every record of this ray was read when `cur` was opened)
             ray_pass(c1.ray, c1.sbi, 0, zq);
+            ray_col(0);
             if (c1.ray + nwaves < R) load_ray_z(c1.ray + nwaves, zq);
         }
 #endif
@@ -658,6 +685,7 @@ k_render_proj(const sd_render_args a, const sd_head m) {
             Tc = 1.f; dpart = 0.f; wpart = 0.f;
             cpart[0] = cpart[1] = cpart[2] = 0.f;
         }
+        if (SD_RECBUF == 2 && passed) ray_col((cur.n + 1) & 1);
     };
     PItem alt;
     for (int i = 0; i < nitems; i += 2) {
