@@ -38,7 +38,8 @@ D_HIDDEN, D_DINO = 128, 64
 D_IN = C_GRID + 39
 
 
-def mlp_flops_per_point(D=D_DINO):
+def mlp_flops_per_point(D=None):
+    D = D_DINO if D is None else D
     return 2 * (D_IN * D_HIDDEN + D_HIDDEN * (1 + D))
 
 
@@ -196,8 +197,14 @@ def main():
     ap.add_argument("--mode", default="proj", choices=["proj", "grid"],
                     help="16-bit render kernel: projected grid (default) or per-sample grid")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--config", default="c2", choices=["c2", "c4"],
+                    help="c2: BASELINE configs[1] (K=64, D=64, the metric's config); c4: "
+                         "configs[3] render shape (K=128, 384-d feature field)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     args = ap.parse_args()
+    global K_SAMPLES, D_DINO
+    if args.config == "c4":
+        K_SAMPLES, D_DINO = 128, 384
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -261,12 +268,14 @@ def main():
         achieved = flops / (kern_ms * 1e-3) / 1e12
         peak = PEAK_TFLOPS[args.precision]
         if proj:  # what the matrix cores actually execute (P = W G projection + code/head)
+            hc = _lib.render_proj_work_bytes(R, D_DINO) > 0  # head applied per ray
             exec_flops = (HF * WF * 2 * C_GRID * D_HIDDEN
-                          + R * K_SAMPLES * 2 * (39 * D_HIDDEN + D_HIDDEN * (1 + D_DINO)))
+                          + R * K_SAMPLES * 2 * (39 * D_HIDDEN + D_HIDDEN * (1 + (0 if hc else D_DINO)))
+                          + (R * 2 * D_HIDDEN * D_DINO if hc else 0))
         else:
             exec_flops = flops
         line = {
-            "metric": "rendered rays/sec, KITTI-360 192x640x64-sample frustum",
+            "metric": f"rendered rays/sec, KITTI-360 192x640x{K_SAMPLES}-sample frustum",
             "value": total_rays / elapsed,
             "unit": "rays/s",
             "n_gpus": world,
@@ -281,9 +290,12 @@ def main():
             "data": "synthetic (seeded U[-1,1) image, N(0,1) 256x192x640 feature grid, "
                     "kaiming-init ResnetFC; no dataset/checkpoint offline)",
             "config": {
-                "workload": "C2: KITTI-360 192x640 frustum, 64 samples/ray, ViT-S/16-shaped "
-                            "256x192x640 DPT feature grid, ResnetFC 295-128-65, lindisp"
-                            + (", offset render pose" if args.offset_pose else ""),
+                "workload": ("C2: KITTI-360 192x640 frustum, 64 samples/ray, ViT-S/16-shaped "
+                             "256x192x640 DPT feature grid, ResnetFC 295-128-65, lindisp"
+                             if args.config == "c2" else
+                             "C4: KITTI-360 192x640 frustum, 128 samples/ray, DINOv2-B/14-shaped "
+                             "256x192x640 DPT feature grid, ResnetFC 295-128-385 (384-d field), "
+                             "lindisp") + (", offset render pose" if args.offset_pose else ""),
                 "frames_per_gpu": 1, "rays_per_frame": R, "samples_per_ray": K_SAMPLES,
                 "grid": [C_GRID, HF, WF], "parallelism": f"frames{world}" +
                 ("+rccl_allgather" if world > 1 else ""),

@@ -120,6 +120,12 @@ typedef struct sd_render_args {
      * so the (R, K) depth array never goes through HBM.  Ignored when z != NULL. */
     int32_t z_lindisp;
     uint64_t z_seed, z_offset;
+    /* Scratch of sd_render_proj_work_bytes(R, D) bytes (sd_render_proj only; NULL when
+     * that is 0): for wide DINO heads the kernel composites the 128-d hidden vectors,
+     * sum_k w_k relu(h_k), and applies W_dino once per ray afterwards (the output layer is
+     * linear: sum_k w_k (W h_k + b) = W sum_k w_k h_k + b sum_k w_k, nerf.py:394 over
+     * resnetfc.py:199). */
+    float *work;
 } sd_render_args;
 
 int sd_render_fused(const sd_render_args *args, const sd_mlp *mlp, void *stream);
@@ -149,13 +155,16 @@ typedef struct sd_head {
     const void *w_out;     /* [D/16][4][64][8] W_out rows 1..D A fragments, dtype     */
     const float *b_dino;   /* b_out[1:1+D]                                            */
     float b_sigma;         /* b_out[0]                                                */
-    int32_t D;             /* 32, 64 or 128                                           */
+    int32_t D;             /* multiple of 16, <= 512                                  */
     int32_t dtype;         /* SD_BF16 or SD_F16                                       */
 } sd_head;
 
 /* args->grid = the projected pair grid (B, Hf, Wf, 128, 2) from sd_project_grid; K % 16 == 0.
  * Outputs as sd_render_fused; args->z may be NULL (in-kernel z sampling, see above). */
 int sd_render_proj(const sd_render_args *args, const sd_head *head, void *stream);
+
+/* Bytes of args->work sd_render_proj needs for R rays and a D-dim DINO head (0: none). */
+int64_t sd_render_proj_work_bytes(int64_t R, int32_t D);
 
 /* Per-point field query without compositing (BTSNet.forward on raw points,
  * bts.py:476-595; SSCBench predict_grid / demo inference_3d).  Points are

@@ -54,6 +54,7 @@ class SdRenderArgs(ctypes.Structure):
         ("weights", _vp), ("alphas", _vp), ("invalid", _vp), ("invalid_f", _vp),
         ("rgb_samps", _vp),
         ("z_lindisp", _i32), ("z_seed", ctypes.c_uint64), ("z_offset", ctypes.c_uint64),
+        ("work", _vp),
     ]
 
 
@@ -82,6 +83,7 @@ SIGNATURES = {
     "sd_field_query": [ctypes.POINTER(SdFieldArgs), ctypes.POINTER(SdMlp), _vp],
     "sd_project_grid": [_vp, _i64, _i64, _i64, ctypes.POINTER(SdMlp), _vp, _vp],
     "sd_render_proj": [ctypes.POINTER(SdRenderArgs), ctypes.POINTER(SdHead), _vp],
+    "sd_render_proj_work_bytes": [_i64, _i32],
     "sd_composite": [_vp, _vp, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp,
                      _vp],
 }
@@ -104,6 +106,7 @@ def load(path: str = LIB_PATH):
         fn.argtypes = argt
         fn.restype = ctypes.c_int
     lib.sd_last_error.restype = ctypes.c_char_p
+    lib.sd_render_proj_work_bytes.restype = ctypes.c_int64
     if lib.sd_abi_version() != ABI_VERSION:
         raise RuntimeError("scenedino_amd: libsdhip.so ABI version mismatch; rebuild it")
     _lib = lib
@@ -218,6 +221,10 @@ def project_grid(grid_nchw, mlp: SdMlp, dtype):
     _check(lib.sd_project_grid(ptr(_req(grid_nchw, "grid")), B, H, W, ctypes.byref(mlp),
                                ptr(out), stream_of(out)), "sd_project_grid")
     return out
+
+
+def render_proj_work_bytes(R: int, D: int) -> int:
+    return int(load().sd_render_proj_work_bytes(R, D))
 
 
 def render_proj(args: SdRenderArgs, head: SdHead, ref_tensor):

@@ -101,6 +101,16 @@ __device__ __forceinline__ uint32_t sd_pack2(float a, float b) {
     return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, e2));
 }
 
+// 16-bit halves of a packed pair -> f32
+template <int P> __device__ __forceinline__ float sd_unpack_lo(uint32_t d) {
+    if (P == SD_BF16) return bf16lo(d);
+    return (float)__builtin_bit_cast(f16x2, d)[0];
+}
+template <int P> __device__ __forceinline__ float sd_unpack_hi(uint32_t d) {
+    if (P == SD_BF16) return bf16hi(d);
+    return (float)__builtin_bit_cast(f16x2, d)[1];
+}
+
 // blend weights as the ray pass stores them: (w00, w01), (w10, w11) packed in E
 template <int P>
 __device__ __forceinline__ uint4 sd_pack_w(float w00, float w01, float w10, float w11) {
@@ -293,6 +303,15 @@ __host__ __device__ constexpr int sd_rec_words(int nv) { return (13 + 3 * nv + 3
 #ifndef SD_RWG
 #define SD_RWG 256  // render workgroup (4 waves; 2 waves per SIMD: VGPR-bound at ~215)
 #endif
+#ifndef SD_HC_MIN_D
+#define SD_HC_MIN_D 16  // D >= this: hidden-space compositing + k_head_hc (measured faster
+                        // than the folded head already at D = 64: 0.685 vs 0.706 ms, C2)
+#endif
+#define SD_HC_STRIDE 132  // floats per ray of the hidden-composite scratch: hsum[128], wsum
+#define SD_MAX_D 512
+static inline bool sd_head_hc(int D) {
+    return D >= SD_HC_MIN_D || (D != 32 && D != 64 && D != 128);
+}
 #ifndef SD_RWAVES
 #define SD_RWAVES 2  // waves per SIMD the register budget is cut for (2: <= 256 VGPRs)
 #endif
@@ -415,8 +434,13 @@ k_render_proj(const sd_render_args a, const sd_head m) {
         // z[k + 1] from the next lane (lane 63: lane 0 of the next 64-sample block)
 #pragma unroll
         for (int p = 0; p < MAXP; ++p) {
+            // every lane takes part in the exchange (no shuffle under a lane condition)
             float nx = __shfl_down(zo[p], 1, 64);
-            if (lane == 63) nx = (p + 1 < MAXP && 64 * (p + 1) < K) ? __shfl(zo[p + 1 < MAXP ? p + 1 : p], 0, 64) : zo[p];
+            const float first_next = p + 1 < MAXP
+                ? __builtin_bit_cast(float, __builtin_amdgcn_readlane(
+                      __builtin_bit_cast(int, zo[p + 1 < MAXP ? p + 1 : p]), 0))
+                : zo[p];
+            if (lane == 63) nx = (p + 1 < MAXP && 64 * (p + 1) < K) ? first_next : zo[p];
             zq[2 * p] = zo[p];
             zq[2 * p + 1] = nx;
         }
@@ -540,9 +564,15 @@ k_render_proj(const sd_render_args a, const sd_head m) {
     RCursor c1 = advance(c0);
     PRaw r0 = sd_pload(cur, 0), r1 = sd_pload(cur, 1), r2 = sd_pload(cur, 2), r3 = sd_pload(cur, 3);
 
-    f32x4 dacc[NDT];
+    // NDT > 0: DINO head folded into the compositing sum (dacc, D = 16 NDT);
+    // NDT == 0: hidden-space compositing, hacc = sum_j w_j relu(h_j) (rows 16 t + 4 g + r),
+    // the head applied per ray afterwards (k_head_hc: W_dino . hsum + b_dino wsum)
+    constexpr bool HC = NDT == 0;
+    f32x4 dacc[HC ? 1 : NDT], hacc[HC ? 8 : 1];
 #pragma unroll
-    for (int i = 0; i < NDT; ++i) dacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < (HC ? 1 : NDT); ++i) dacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < (HC ? 8 : 1); ++i) hacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     float Tc = 1.f, dpart = 0.f, wpart = 0.f, cpart[3] = {0.f, 0.f, 0.f};
     const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
 
@@ -630,6 +660,20 @@ k_render_proj(const sd_render_args a, const sd_head m) {
         cpart[0] += w * cur.col[0];
         cpart[1] += w * cur.col[1];
         cpart[2] += w * cur.col[2];
+        if (HC) {
+            // from the ReLU'd 16-bit operands (the f32 accumulators are dead by now)
+#pragma unroll
+            for (int s2 = 0; s2 < 4; ++s2) {
+                const uint4 u = __builtin_bit_cast(uint4, X[s2]);
+                const uint32_t d4[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int t = 2 * s2 + (q >> 1), r = 2 * (q & 1);
+                    hacc[t][r] = fmaf(w, sd_unpack_lo<P>(d4[q]), hacc[t][r]);
+                    hacc[t][r + 1] = fmaf(w, sd_unpack_hi<P>(d4[q]), hacc[t][r + 1]);
+                }
+            }
+        }
         // DINO head folded into the compositing sum: dacc += w_j (W_dino h_j)
 #pragma unroll
         for (int dt = 0; dt < NDT; ++dt) {
@@ -677,6 +721,18 @@ k_render_proj(const sd_render_args a, const sd_head m) {
                 }
                 dacc[dt] = zero4;
             }
+            if (HC) {
+                float *hs = a.work + (int64_t)cur.ray * SD_HC_STRIDE;
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    f32x4 v;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = sd_rowsum16(hacc[t][r]);
+                    if (j == 0) *(f32x4 *)(hs + 16 * t + 4 * g) = v;
+                    hacc[t] = zero4;
+                }
+                if (lane == 0) hs[SD_DH] = wsum;
+            }
             if (lane == 0) a.depth[cur.ray] = dsum;
             if (j == 0 && g < nv) {
                 float *rp = a.rgb + (int64_t)cur.ray * 3 * nv + 3 * g;
@@ -691,6 +747,59 @@ k_render_proj(const sd_render_args a, const sd_head m) {
     for (int i = 0; i < nitems; i += 2) {
         step(cur, alt);
         if (i + 1 < nitems) step(alt, cur);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_head_hc: dino[r] = W_dino . hsum[r] + b_dino * wsum[r] for the hidden-space
+// composited rays (render kernel with NDT == 0).  One wave = 16 rays x all D dims:
+// A = the W_dino fragments of sd_head (LDS), B = hsum^T in the same hidden-index
+// permutation hid(s, g, e) = 32 s + 16 (e >> 2) + 4 g + (e & 3), 16x16x32 MFMA.
+// ---------------------------------------------------------------------------
+template <int P>
+__global__ void __launch_bounds__(SD_PWG)
+k_head_hc(const float *__restrict__ work, int64_t R, const sd_head m, float *__restrict__ dino) {
+    typedef T16<P> Tr;
+    typedef typename Tr::Frag Frag;
+    typedef typename Tr::E E;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int ndt = m.D >> 4;
+    {
+        const uint4 *src = (const uint4 *)m.w_out;
+        uint4 *dst = (uint4 *)lds;
+        for (int i = threadIdx.x; i < ndt * 4 * SD_WAVE; i += blockDim.x) dst[i] = src[i];
+        __syncthreads();
+    }
+    const Frag *lw = (const Frag *)lds;
+    const int lane = threadIdx.x & 63, j = lane & 15, g = lane >> 4;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t ntile = (R + 15) / 16;
+    for (int64_t tile = (int64_t)blockIdx.x * (SD_PWG / 64) + wave; tile < ntile;
+         tile += (int64_t)gridDim.x * (SD_PWG / 64)) {
+        const int64_t ray = tile * 16 + j;
+        const float *hs = work + (ray < R ? ray : R - 1) * SD_HC_STRIDE;
+        Frag B[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const f32x4 lo = *(const f32x4 *)(hs + 32 * s + 4 * g);
+            const f32x4 hi = *(const f32x4 *)(hs + 32 * s + 16 + 4 * g);
+            const uint4 u = {sd_pack2<E>(lo[0], lo[1]), sd_pack2<E>(lo[2], lo[3]),
+                             sd_pack2<E>(hi[0], hi[1]), sd_pack2<E>(hi[2], hi[3])};
+            B[s] = __builtin_bit_cast(Frag, u);
+        }
+        const float ws = hs[SD_DH];
+        for (int dt = 0; dt < ndt; ++dt) {
+            f32x4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < 4; ++s) o = Tr::mma(lw[(dt * 4 + s) * SD_WAVE + lane], B[s], o);
+            // rows 4 g + r of tile dt = dims 16 dt + 4 g + r, column j = ray
+            const int dim = 16 * dt + 4 * g;
+            const f32x4 bd = *(const f32x4 *)(m.b_dino + dim);
+            f32x4 res;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) res[r] = o[r] + ws * bd[r];
+            if (ray < R) *(f32x4 *)(dino + ray * m.D + dim) = res;
+        }
     }
 }
 
@@ -767,14 +876,21 @@ static int sd_rp_launch(const sd_render_args &a, const sd_head &m, hipStream_t s
 
 template <int P, int NV>
 static int sd_rp_ndt(const sd_render_args &a, const sd_head &m, hipStream_t s) {
-    switch (m.D / 16) {
-        case 2: return sd_rp_launch<P, NV, 2>(a, m, s);
-        case 4: return sd_rp_launch<P, NV, 4>(a, m, s);
-        case 8: return sd_rp_launch<P, NV, 8>(a, m, s);
-        default:
-            sd_set_error("sd_render_proj: D must be 32, 64 or 128");
-            return -1;
+    if (!sd_head_hc(m.D)) {
+        switch (m.D / 16) {
+            case 2: return sd_rp_launch<P, NV, 2>(a, m, s);
+            case 4: return sd_rp_launch<P, NV, 4>(a, m, s);
+            case 8: return sd_rp_launch<P, NV, 8>(a, m, s);
+        }
     }
+    int rc = sd_rp_launch<P, NV, 0>(a, m, s);
+    if (rc) return rc;
+    const int lds_bytes = (m.D >> 4) * 4 * SD_WAVE * 16;
+    int64_t nblk;
+    sd_launch_proj(k_head_hc<P>, (a.R + 15) / 16, lds_bytes, s, nblk);
+    hipLaunchKernelGGL(k_head_hc<P>, dim3((unsigned)nblk), dim3(SD_PWG), lds_bytes, s, a.work, a.R,
+                       m, a.dino);
+    return sd_check_err();
 }
 
 template <int P>
@@ -782,11 +898,19 @@ static int sd_rp_nv(const sd_render_args &a, const sd_head &m, hipStream_t s) {
     return a.nv == 1 ? sd_rp_ndt<P, 1>(a, m, s) : sd_rp_ndt<P, 0>(a, m, s);
 }
 
+extern "C" int64_t sd_render_proj_work_bytes(int64_t R, int32_t D) {
+    return sd_head_hc(D) ? R * SD_HC_STRIDE * (int64_t)sizeof(float) : 0;
+}
+
 extern "C" int sd_render_proj(const sd_render_args *args, const sd_head *m, void *stream) {
     if (!args || !m || !m->w_pe || !m->w_sig || !m->w_out || !m->b_dino ||
-        (m->dtype != SD_BF16 && m->dtype != SD_F16) ||
-        (m->D != 32 && m->D != 64 && m->D != 128)) {
-        sd_set_error("sd_render_proj: invalid head (16-bit dtype, D in {32, 64, 128})");
+        (m->dtype != SD_BF16 && m->dtype != SD_F16) || m->D <= 0 || (m->D % 16) ||
+        m->D > SD_MAX_D) {
+        sd_set_error("sd_render_proj: invalid head (16-bit dtype, D % 16 == 0, D <= 512)");
+        return -1;
+    }
+    if (sd_head_hc(m->D) && !args->work) {
+        sd_set_error("sd_render_proj: this D needs args->work (sd_render_proj_work_bytes)");
         return -1;
     }
     const sd_render_args &a = *args;

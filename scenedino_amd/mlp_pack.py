@@ -114,7 +114,7 @@ def _index_tables(C: int, D: int):
     h2 = np.arange(2)[None, :, None]
     r = np.arange(16)[None, None, :]
     accrow = 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h2  # (4,2,16)
-    ndt = D // 32
+    ndt = max(D // 32, 1)
     dt = np.arange(ndt)[:, None, None, None, None]
     tt = np.arange(4)[None, :, None, None, None]
     s = np.arange(2)[None, None, :, None, None]
@@ -151,9 +151,9 @@ class PackedMLP:
         dh, din = W_in.shape
         C = din - N_PE
         D = W_out.shape[0] - 1
-        if dh != D_HIDDEN or C <= 0 or C % 64 or D % 32 or W_out.shape[1] != dh:
+        if dh != D_HIDDEN or C <= 0 or C % 64 or D % 16 or W_out.shape[1] != dh:
             raise NotImplementedError(
-                f"fused field kernel needs d_hidden=128, C%64==0, D%32==0 (got W_in {tuple(W_in.shape)}, "
+                f"field kernels need d_hidden=128, C%64==0, D%16==0 (got W_in {tuple(W_in.shape)}, "
                 f"W_out {tuple(W_out.shape)})")
         dev = W_in.device
         ix = {k: v.to(dev) for k, v in _index_tables(C, D).items()}
@@ -164,7 +164,9 @@ class PackedMLP:
         self.w_in = w1.to(tdt).contiguous()
         self.b_in_h = b_in[ix["accrow"]].contiguous()
         self.w_sig_h = W_out[0][ix["accrow"]].contiguous()
-        if dtype != _lib.SD_F32:
+        if D % 32:  # the 32x32 grid / field kernels need D % 32 == 0 (they reject NULL)
+            self.w_out = None
+        elif dtype != _lib.SD_F32:
             self.w_out = W_out[ix["rows2b"], ix["cols2b"]].to(tdt).contiguous()
         else:
             self.w_out = W_out[ix["rows2f"], ix["cols2f"]].contiguous()
@@ -172,7 +174,7 @@ class PackedMLP:
         self.b_sigma = float(b_out[0].item())
         self.C, self.D, self.dtype = C, D, dtype
         self.head_rec = None
-        if dtype != _lib.SD_F32 and D in (32, 64, 128):
+        if dtype != _lib.SD_F32 and D % 16 == 0 and D <= 512:
             px = {k: v.to(dev) for k, v in _proj_tables(C, D).items()}
             pe_cols = torch.where(px["pe_cols"] < 0, torch.full_like(px["pe_cols"], din), px["pe_cols"])
             self.w_pe16 = Wz[px["pe_rows"], pe_cols].to(tdt).contiguous()
@@ -185,8 +187,8 @@ class PackedMLP:
         self.rec = _lib.SdMlp(
             w_in=self.w_in.data_ptr(), b_in_h=self.b_in_h.data_ptr(),
             w_sig_h=self.w_sig_h.data_ptr(), b_sigma=self.b_sigma,
-            w_out=self.w_out.data_ptr(), b_dino=self.b_dino.data_ptr(),
-            C=C, D=D, dtype=dtype, d_hidden=dh)
+            w_out=self.w_out.data_ptr() if self.w_out is not None else None,
+            b_dino=self.b_dino.data_ptr(), C=C, D=D, dtype=dtype, d_hidden=dh)
 
 
 def param_key(*ts):

@@ -165,11 +165,14 @@ class BTSNet(nn.Module):
         return self.fused_mode == "proj" and self.precision != "fp32"
 
     def fused_supported(self, K: int) -> bool:
-        """The fused render kernels take D in {32, 64, 128} and K % 16 == 0 (projected,
-        16-bit) or K % 32 == 0 (grid kernel); other shapes go through sd_field_query +
-        sd_composite (also native)."""
+        """The projected 16-bit render kernel takes K % 16 == 0, K <= 128 and D % 16 == 0,
+        D <= 512 (D >= 128 through hidden-space compositing + the per-ray head GEMM); the
+        grid kernel K % 32 == 0 and D in {32, 64, 128}; other shapes go through
+        sd_field_query + sd_composite (also native)."""
         D = self._d_out - 1
-        return K % (16 if self._use_proj() else 32) == 0 and D in (32, 64, 128)
+        if self._use_proj():
+            return K % 16 == 0 and K <= 128 and D % 16 == 0 and D <= 512
+        return K % 32 == 0 and K <= 128 and D in (32, 64, 128)
 
     def _timed(self, name, fn):
         t = self.kernel_timer
@@ -302,6 +305,9 @@ class BTSNet(nn.Module):
             rgb_samps=out["rgb_samps"].data_ptr() if want_rgb_samps else None,
             z_lindisp=int(bool(lindisp)), z_seed=(z_seed or 0) & (2**64 - 1), z_offset=0)
         if proj:
+            wb = _lib.render_proj_work_bytes(R, m.D)
+            work = torch.empty(wb // 4, device=dev) if wb > 0 else None
+            args.work = work.data_ptr() if work is not None else None
             self._timed("render", lambda: _lib.render_proj(args, m.head_rec, rays))
         else:
             self._timed("render", lambda: _lib.render_fused(args, m.rec, rays))
