@@ -191,6 +191,57 @@ int sd_composite(const float *z, const float *sigma, const float *feat, int64_t 
                  float *weights, float *alphas, float *depth, float *feat_out, float *rgb_out,
                  void *stream);
 
+/* ---- SSCBench voxel query (sdhip_seg.hip) ---------------------------------- */
+
+/* Voxel-centre grid of nx*ny*nz voxels, flat index (ix*ny + iy)*nz + iz (meshgrid ij),
+ * centre_j = f32(f64(f32 origin_j) + vox*coord_j + vox*0.5), moved by the rigid transform
+ * T (rows 0..2 of a 4x4, fp64) and stored as f32 (pts_out (n, 3), device).  Bit-exact with
+ * generate_point_grid -> TSDFVolume.vox2world -> rigid_transform -> .float()
+ *   (sscbench/point_utils.py:17-82, sscbench/fusion.py:203-219,407-411,
+ *    sscbench/evaluate_model_sscbench.py:270-278).
+ * origin (3) and T (12, row-major rows 0..2) are HOST pointers read during the call. */
+int sd_voxel_points(const double *origin, double vox, int64_t nx, int64_t ny, int64_t nz,
+                    const double *T, float *pts_out, void *stream);
+
+/* Folded MlpDimReduction.transform_expand + SemanticHead("stego_kmeans"), pre-packed by
+ * the host into 32x32x16 MFMA fragment order (scenedino_amd/seg_pack.py documents every
+ * map).  W1/W2: dim_reduction linear_in / linear_out; L = Wl W2, M = Wn1 W2 with Wl, Wn1,
+ * Wn2 the StegoClusterHead 1x1 convolutions; centres = normalised cluster centres. */
+typedef struct sd_seg_head {
+    const void *w1;        /* bf16 [d_latent/32][d_in/16][64][8]                      */
+    const float *b1;       /* [d_latent/32][2][16] accumulator-row order              */
+    const void *w2;        /* bf16 [d_full/32][d_latent/16][64][8]                    */
+    const float *b2;       /* [d_full/32][2][16]                                      */
+    const void *wl;        /* bf16 [d_code/32][d_latent/16][64][8]  L = Wl W2         */
+    const float *bl;       /* [d_code/32][2][16]  Wl b2                               */
+    const float *bo;       /* [d_code/32][2][16]  bl + bn2                            */
+    const void *wm;        /* bf16 [d_full/32][d_latent/16][64][8]  M = Wn1 W2        */
+    const float *bm;       /* [d_full/32][2][16]  Wn1 b2                              */
+    const float *bn1;      /* [d_full/32][2][16]                                      */
+    const void *wn2;       /* bf16 [d_code/32][d_full/16][64][8]                      */
+    const float *centres;  /* [n_clusters][d_code/32][2][16] normalised centres       */
+    const int32_t *assign; /* [n_clusters] pseudo_assignment                           */
+    int32_t n_clusters;    /* 1..256                                                   */
+    int32_t d_in;          /* 64  (reduced DINO dims)                                  */
+    int32_t d_latent;      /* 128                                                      */
+    int32_t d_full;        /* multiple of 32 (768)                                     */
+    int32_t d_code;        /* 64                                                       */
+} sd_seg_head;
+
+/* Per-point segmentation head on P DINO codes dino (P, d_in) f32.
+ * Replaces BTSNet.forward(predict_segmentation=True)'s encoder.expand_dim +
+ * downstream_head(..., "stego_kmeans") (bts.py:584-592, dim_reduction.py:22-25,
+ * semantic_head.py:107-111,285-373) and, with seg, the SSCBench alpha-weighted class pick
+ * (evaluate_model_sscbench.py:727-742, factor 1).  Outputs (device, NULL = not wanted):
+ *   labels    (P) int32  pseudo_assignment[argmax_k cos(stego, c_k)]
+ *   seg       (P) uint8  alpha > 0 ? label : 0, alpha = 1 - exp(-voxel_size * sigma)
+ *                        (needs sigma (P) f32)
+ *   dino_full (P, d_full) f32  transform_expand output (L2-normalised)
+ * At least one output; labels/seg need the stego fields of h. */
+int sd_seg_query(const float *dino, int64_t P, const sd_seg_head *h, const float *sigma,
+                float voxel_size, int32_t *labels, uint8_t *seg, float *dino_full,
+                void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -69,6 +69,16 @@ class SdFieldArgs(ctypes.Structure):
     ]
 
 
+class SdSegHead(ctypes.Structure):
+    _fields_ = [
+        ("w1", _vp), ("b1", _vp), ("w2", _vp), ("b2", _vp),
+        ("wl", _vp), ("bl", _vp), ("bo", _vp), ("wm", _vp), ("bm", _vp), ("bn1", _vp),
+        ("wn2", _vp), ("centres", _vp), ("assign", _vp),
+        ("n_clusters", _i32), ("d_in", _i32), ("d_latent", _i32), ("d_full", _i32),
+        ("d_code", _i32),
+    ]
+
+
 # (name, argtypes) of every exported entry point; tests check the .so exports all.
 SIGNATURES = {
     "sd_last_error": [],
@@ -85,6 +95,10 @@ SIGNATURES = {
     "sd_render_proj": [ctypes.POINTER(SdRenderArgs), ctypes.POINTER(SdHead), _vp],
     "sd_render_proj_work_bytes": [_i64, _i32],
     "sd_composite": [_vp, _vp, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp,
+                     _vp],
+    "sd_voxel_points": [ctypes.POINTER(ctypes.c_double), ctypes.c_double, _i64, _i64, _i64,
+                        ctypes.POINTER(ctypes.c_double), _vp, _vp],
+    "sd_seg_query": [_vp, _i64, ctypes.POINTER(SdSegHead), _vp, ctypes.c_float, _vp, _vp, _vp,
                      _vp],
 }
 
@@ -237,6 +251,40 @@ def field_query(args: SdFieldArgs, mlp: SdMlp, ref_tensor):
     lib = load()
     _check(lib.sd_field_query(ctypes.byref(args), ctypes.byref(mlp), stream_of(ref_tensor)),
            "sd_field_query")
+
+
+def voxel_points(origin, voxel_size, dims, T, device):
+    """SSCBench voxel-centre grid (sd_voxel_points): (nx*ny*nz, 3) float32 on device.
+    origin (3,), T (4, 4) or (3, 4): host numbers (float64)."""
+    lib = load()
+    nx, ny, nz = (int(d) for d in dims)
+    o = (ctypes.c_double * 3)(*[float(v) for v in origin])
+    Tm = torch.as_tensor(T, dtype=torch.float64).reshape(-1, 4)[:3].flatten().tolist()
+    t = (ctypes.c_double * 12)(*Tm)
+    out = torch.empty(nx * ny * nz, 3, device=device, dtype=torch.float32)
+    _check(lib.sd_voxel_points(o, float(voxel_size), nx, ny, nz, t, ptr(out), stream_of(out)),
+           "sd_voxel_points")
+    return out
+
+
+def seg_query(dino, rec: SdSegHead, sigma=None, voxel_size=0.2, want_labels=True,
+              want_seg=False, want_full=False):
+    """Folded transform_expand + stego k-means head (sd_seg_query) on dino (P, 64) f32.
+    Returns (labels int32 (P) | None, seg uint8 (P) | None, dino_full (P, d_full) | None)."""
+    lib = load()
+    _req(dino, "dino")
+    P = dino.shape[0]
+    dev = dino.device
+    labels = torch.empty(P, device=dev, dtype=torch.int32) if want_labels else None
+    seg = torch.empty(P, device=dev, dtype=torch.uint8) if want_seg else None
+    full = torch.empty(P, rec.d_full, device=dev) if want_full else None
+    if want_seg:
+        if sigma is None or sigma.numel() != P:
+            raise ValueError("seg_query: want_seg needs sigma (P,)")
+        _req(sigma, "sigma")
+    _check(lib.sd_seg_query(ptr(dino), P, ctypes.byref(rec), ptr(sigma), float(voxel_size),
+                            ptr(labels), ptr(seg), ptr(full), stream_of(dino)), "sd_seg_query")
+    return labels, seg, full
 
 
 def composite(z, sigma, feat, rgb, hard_alpha_cap, want_weights=True):

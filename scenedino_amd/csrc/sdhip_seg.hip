@@ -1,0 +1,417 @@
+// sdhip_seg.hip -- SSCBench voxel-query path on gfx950 (CDNA4).
+//
+//   k_voxel_points : voxel-centre grid in the velodyne frame, rigidly moved into the
+//                    camera frame.  fp64 arithmetic, one rounding to f32,
+//                    bit-exact with the reference's numba + numpy pipeline
+//                    (sscbench/point_utils.py:17-82, sscbench/fusion.py:203-219,407-411,
+//                    evaluate_model_sscbench.py:270-278).
+//   k_seg_head     : per-point DINO code (D_r = 64) -> MlpDimReduction.transform_expand
+//                    (64 -> 128 ReLU -> 768, L2 normalise; dim_reduction.py:22-25) ->
+//                    SemanticHead "stego_kmeans" (semantic_head.py:107-111: StegoClusterHead
+//                    768 -> 64 linear + 768 -> 768 ReLU -> 64, L2 normalise; cosine k-means
+//                    argmax over the cluster centres, pseudo_assignment lookup,
+//                    semantic_head.py:285-373) -> optionally the SSCBench alpha-weighted
+//                    class pick (evaluate_model_sscbench.py:727-742 at factor 1).
+//
+// Folding (all exact algebra; only the rounding order differs from the reference):
+//   f = e / n,  e = W2 h + b2,  n = max(|e|, 1e-12),  h = relu(W1 x + b1)   (transform_expand)
+//   SemanticHead re-normalises f (|f| = 1: the identity up to rounding).
+//   stego = Wl f + bl + Wn2 relu(Wn1 f + bn1) + bn2
+//         = (L h + Wl b2) / n + bl + bn2 + Wn2 relu((M h + Wn1 b2) / n + bn1)
+//   with L = Wl W2 (64 x 128) and M = Wn1 W2 (768 x 128) folded once on the host: the
+//   768 x 768 product of the reference becomes a 768 x 128 one.  The class is
+//   argmax_k <stego / |stego|, c_k / |c_k|> = argmax_k <stego, c_k / |c_k|> (a positive
+//   scale does not move an argmax), evaluated in fp32.
+//
+// Work unit: one wave = SG_NT x 32 points (lane = point, as the accumulator columns of
+// v_mfma_f32_32x32x16_bf16); weights are the MFMA A operands (rows = output features),
+// read straight from L2 as 1-KiB fragments (each feeds SG_NT MFMAs).  Hidden vectors
+// never leave the registers: an accumulator tile is converted in place into the B operand
+// of the next product (k order permuted; the host packs the A operands to match, see
+// scenedino_amd/seg_pack.py).
+#include "sdhip_common.h"
+
+extern "C" void sd_set_error(const char *msg);
+
+#define SG_NT 4        // 32-point column tiles per wave
+#define SG_WAVES 4     // waves per workgroup (one per SIMD)
+#define SG_DR 64       // reduced DINO dims (MlpDimReduction reduced_channels)
+#define SG_DL 128      // latent dims (MlpDimReduction latent_channels)
+#define SG_DC 64       // stego code dims
+
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+
+// ---------------------------------------------------------------------------
+// voxel-centre grid
+// ---------------------------------------------------------------------------
+struct VoxConst {
+    double o[3];   // origin, already rounded to f32 (vox2world casts vol_origin to float32)
+    double t[12];  // rows 0..2 of the 4x4 rigid transform
+};
+
+__global__ void __launch_bounds__(256) k_voxel_points(VoxConst c, double vox, int64_t nx,
+                                                      int64_t ny, int64_t nz,
+                                                      float *__restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= nx * ny * nz) return;
+    const int64_t iz = i % nz;
+    const int64_t q = i / nz;
+    const int64_t iy = q % ny;
+    const int64_t ix = q / ny;
+    // vox2world (numba, fusion.py:212-218): f32 coords, f64 arithmetic, f32 store
+    const double ci[3] = {(double)(float)ix, (double)(float)iy, (double)(float)iz};
+    double p[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        double v = c.o[j] + vox * ci[j];
+        v = v + vox * 0.5;
+        p[j] = (double)(float)v;
+    }
+    // rigid_transform (fusion.py:407-411) in f64, then .float() (evaluate_model_sscbench.py:278)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        double acc = c.t[4 * j] * p[0];
+        acc = acc + c.t[4 * j + 1] * p[1];
+        acc = acc + c.t[4 * j + 2] * p[2];
+        acc = acc + c.t[4 * j + 3];
+        out[i * 3 + j] = (float)acc;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// folded transform_expand + stego + k-means head
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ f32x16 sg_zero16() {
+    f32x16 z;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) z[i] = 0.f;
+    return z;
+}
+
+// 16 floats stored in accumulator-row order for lane half h: vec + (t * 2 + h) * 16
+__device__ __forceinline__ f32x16 sg_rows(const float *__restrict__ vec, int t, int h) {
+    const f32x4_t *p = (const f32x4_t *)(vec + (t * 2 + h) * 16);
+    f32x16 r;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        f32x4_t v = p[g];
+        r[4 * g] = v[0]; r[4 * g + 1] = v[1]; r[4 * g + 2] = v[2]; r[4 * g + 3] = v[3];
+    }
+    return r;
+}
+
+#define SG_MFMA(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_bf16((a), (b), (c), 0, 0, 0)
+
+// MODE bit 0: write dino_full (transform_expand output); bit 1: segmentation head.
+template <int MODE>
+__global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const float *__restrict__ dino,
+                                                            int64_t P, int32_t DF,
+                                                            const float *__restrict__ sigma,
+                                                            float neg_vox, sd_seg_head h,
+                                                            int32_t *__restrict__ labels,
+                                                            uint8_t *__restrict__ seg,
+                                                            float *__restrict__ full) {
+    constexpr bool FULL = MODE & 1;
+    constexpr bool SEG = MODE & 2;
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int r = lane & 31, hh = lane >> 5;
+    const int64_t base = ((int64_t)blockIdx.x * SG_WAVES + wave) * (32 * SG_NT);
+    if (base >= P) return;  // wave-uniform
+    const int T2 = DF / 32;
+
+    // ---- layer 1: h = relu(W1 x + b1) -> B operands hb[ct][k-step 0..7] ----
+    bf16x8 hb[SG_NT][SG_DL / 16];
+    {
+        bf16x8 xb[SG_NT][SG_DR / 16];
+#pragma unroll
+        for (int ct = 0; ct < SG_NT; ++ct) {
+            const int64_t p = base + 32 * ct + r;
+            if (p < P) {
+                const f32x4_t *src = (const f32x4_t *)(dino + p * SG_DR);
+#pragma unroll
+                for (int s = 0; s < SG_DR / 16; ++s) {
+                    f32x4_t a = src[4 * s + 2 * hh], b = src[4 * s + 2 * hh + 1];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        xb[ct][s][j] = (__bf16)a[j];
+                        xb[ct][s][4 + j] = (__bf16)b[j];
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int s = 0; s < SG_DR / 16; ++s)
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) xb[ct][s][j] = (__bf16)0.f;
+            }
+        }
+        const bf16x8 *w1 = (const bf16x8 *)h.w1;
+#pragma unroll
+        for (int t = 0; t < SG_DL / 32; ++t) {
+            f32x16 acc[SG_NT];
+#pragma unroll
+            for (int ct = 0; ct < SG_NT; ++ct) acc[ct] = sg_zero16();
+#pragma unroll
+            for (int s = 0; s < SG_DR / 16; ++s) {
+                const bf16x8 a = w1[(t * (SG_DR / 16) + s) * 64 + lane];
+#pragma unroll
+                for (int ct = 0; ct < SG_NT; ++ct) acc[ct] = SG_MFMA(a, xb[ct][s], acc[ct]);
+            }
+            const f32x16 bb = sg_rows(h.b1, t, hh);
+#pragma unroll
+            for (int ct = 0; ct < SG_NT; ++ct)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    hb[ct][2 * t][j] = (__bf16)fmaxf(acc[ct][j] + bb[j], 0.f);
+                    hb[ct][2 * t + 1][j] = (__bf16)fmaxf(acc[ct][8 + j] + bb[8 + j], 0.f);
+                }
+        }
+    }
+
+    // ---- n = max(|W2 h + b2|, 1e-12)  (F.normalize, dim_reduction.py:25) ----
+    float rinv[SG_NT], den[SG_NT];
+    {
+        float ss[SG_NT];
+#pragma unroll
+        for (int ct = 0; ct < SG_NT; ++ct) ss[ct] = 0.f;
+        const bf16x8 *w2 = (const bf16x8 *)h.w2;
+        for (int t = 0; t < T2; ++t) {
+            f32x16 acc[SG_NT];
+#pragma unroll
+            for (int ct = 0; ct < SG_NT; ++ct) acc[ct] = sg_zero16();
+#pragma unroll
+            for (int q = 0; q < SG_DL / 16; ++q) {
+                const bf16x8 a = w2[(t * (SG_DL / 16) + q) * 64 + lane];
+#pragma unroll
+                for (int ct = 0; ct < SG_NT; ++ct) acc[ct] = SG_MFMA(a, hb[ct][q], acc[ct]);
+            }
+            const f32x16 bb = sg_rows(h.b2, t, hh);
+#pragma unroll
+            for (int ct = 0; ct < SG_NT; ++ct)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const float e = acc[ct][i] + bb[i];
+                    ss[ct] = fmaf(e, e, ss[ct]);
+                }
+        }
+#pragma unroll
+        for (int ct = 0; ct < SG_NT; ++ct) {
+            const float tot = ss[ct] + __shfl_xor(ss[ct], 32);
+            den[ct] = fmaxf(sqrtf(tot), 1e-12f);
+            rinv[ct] = 1.f / den[ct];
+        }
+    }
+
+    if (FULL) {  // dino_full = e / n, recomputed with n known (one store per element)
+        const bf16x8 *w2 = (const bf16x8 *)h.w2;
+        for (int t = 0; t < T2; ++t) {
+            f32x16 acc[SG_NT];
+#pragma unroll
+            for (int ct = 0; ct < SG_NT; ++ct) acc[ct] = sg_zero16();
+#pragma unroll
+            for (int q = 0; q < SG_DL / 16; ++q) {
+                const bf16x8 a = w2[(t * (SG_DL / 16) + q) * 64 + lane];
+#pragma unroll
+                for (int ct = 0; ct < SG_NT; ++ct) acc[ct] = SG_MFMA(a, hb[ct][q], acc[ct]);
+            }
+            const f32x16 bb = sg_rows(h.b2, t, hh);
+#pragma unroll
+            for (int ct = 0; ct < SG_NT; ++ct) {
+                const int64_t p = base + 32 * ct + r;
+                if (p < P) {
+                    float *dst = full + p * DF + 32 * t + 4 * hh;
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        f32x4_t v;
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) v[e] = (acc[ct][4 * g + e] + bb[4 * g + e]) / den[ct];
+                        *(f32x4_t *)(dst + 8 * g) = v;
+                    }
+                }
+            }
+        }
+    }
+    if (!SEG) return;
+
+    // ---- stego: linear path folded to L (64 x 128) ----
+    f32x16 sacc[SG_NT][SG_DC / 32];
+    {
+        const bf16x8 *wl = (const bf16x8 *)h.wl;
+#pragma unroll
+        for (int rt = 0; rt < SG_DC / 32; ++rt) {
+#pragma unroll
+            for (int ct = 0; ct < SG_NT; ++ct) sacc[ct][rt] = sg_zero16();
+#pragma unroll
+            for (int q = 0; q < SG_DL / 16; ++q) {
+                const bf16x8 a = wl[(rt * (SG_DL / 16) + q) * 64 + lane];
+#pragma unroll
+                for (int ct = 0; ct < SG_NT; ++ct) sacc[ct][rt] = SG_MFMA(a, hb[ct][q], sacc[ct][rt]);
+            }
+            const f32x16 lb = sg_rows(h.bl, rt, hh);
+            const f32x16 ob = sg_rows(h.bo, rt, hh);
+#pragma unroll
+            for (int ct = 0; ct < SG_NT; ++ct)
+#pragma unroll
+                for (int i = 0; i < 16; ++i)
+                    sacc[ct][rt][i] = fmaf(sacc[ct][rt][i] + lb[i], rinv[ct], ob[i]);
+        }
+    }
+    // ---- stego: nonlinear path, u = relu((M h + Wn1 b2) / n + bn1) per 32-row tile,
+    //      consumed at once by Wn2 (64 x 768) ----
+    {
+        const bf16x8 *wm = (const bf16x8 *)h.wm;
+        const bf16x8 *wn2 = (const bf16x8 *)h.wn2;
+        const int KS = DF / 16;
+        for (int t = 0; t < T2; ++t) {
+            f32x16 acc[SG_NT];
+#pragma unroll
+            for (int ct = 0; ct < SG_NT; ++ct) acc[ct] = sg_zero16();
+#pragma unroll
+            for (int q = 0; q < SG_DL / 16; ++q) {
+                const bf16x8 a = wm[(t * (SG_DL / 16) + q) * 64 + lane];
+#pragma unroll
+                for (int ct = 0; ct < SG_NT; ++ct) acc[ct] = SG_MFMA(a, hb[ct][q], acc[ct]);
+            }
+            const f32x16 mb = sg_rows(h.bm, t, hh);
+            const f32x16 nb = sg_rows(h.bn1, t, hh);
+            bf16x8 ub[SG_NT][2];
+#pragma unroll
+            for (int ct = 0; ct < SG_NT; ++ct)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    ub[ct][0][j] = (__bf16)fmaxf(fmaf(acc[ct][j] + mb[j], rinv[ct], nb[j]), 0.f);
+                    ub[ct][1][j] =
+                        (__bf16)fmaxf(fmaf(acc[ct][8 + j] + mb[8 + j], rinv[ct], nb[8 + j]), 0.f);
+                }
+#pragma unroll
+            for (int rt = 0; rt < SG_DC / 32; ++rt)
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    const bf16x8 a = wn2[(rt * KS + 2 * t + s) * 64 + lane];
+#pragma unroll
+                    for (int ct = 0; ct < SG_NT; ++ct)
+                        sacc[ct][rt] = SG_MFMA(a, ub[ct][s], sacc[ct][rt]);
+                }
+        }
+    }
+
+    // ---- cosine k-means: argmax_k <stego, c_k/|c_k|> in fp32 (first maximum wins,
+    //      as torch.argmax) -> pseudo_assignment ----
+    float best[SG_NT];
+    int bi[SG_NT];
+#pragma unroll
+    for (int ct = 0; ct < SG_NT; ++ct) {
+        best[ct] = -INFINITY;
+        bi[ct] = 0;
+    }
+    for (int k = 0; k < h.n_clusters; ++k) {
+        const f32x16 c0 = sg_rows(h.centres, 2 * k + 0, hh);  // rows 0..31 (acc order)
+        const f32x16 c1 = sg_rows(h.centres, 2 * k + 1, hh);  // rows 32..63
+#pragma unroll
+        for (int ct = 0; ct < SG_NT; ++ct) {
+            float d = 0.f;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) d = fmaf(c0[i], sacc[ct][0][i], d);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) d = fmaf(c1[i], sacc[ct][1][i], d);
+            d += __shfl_xor(d, 32);
+            if (d > best[ct]) {
+                best[ct] = d;
+                bi[ct] = k;
+            }
+        }
+    }
+    if (hh == 0) {
+#pragma unroll
+        for (int ct = 0; ct < SG_NT; ++ct) {
+            const int64_t p = base + 32 * ct + r;
+            if (p >= P) continue;
+            const int lab = h.assign[bi[ct]];
+            if (labels) labels[p] = lab;
+            if (seg) {
+                // alphas = 1 - exp(-VOXEL_SIZE * sigma); argmax over the 19 classes of
+                // alpha * one_hot(label) = label if alpha > 0 else 0
+                const float alpha = 1.f - expf(neg_vox * sigma[p]);
+                seg[p] = (uint8_t)(alpha > 0.f ? lab : 0);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+extern "C" int sd_voxel_points(const double *origin, double vox, int64_t nx, int64_t ny,
+                               int64_t nz, const double *T, float *pts_out, void *stream) {
+    if (!origin || !T || !pts_out || nx <= 0 || ny <= 0 || nz <= 0 || !(vox > 0.0) ||
+        nx * ny * nz > ((int64_t)1 << 40)) {
+        sd_set_error("sd_voxel_points: invalid argument");
+        return -1;
+    }
+    VoxConst c;
+    for (int j = 0; j < 3; ++j) c.o[j] = (double)(float)origin[j];
+    for (int j = 0; j < 12; ++j) c.t[j] = T[j];
+    const int64_t n = nx * ny * nz;
+    hipLaunchKernelGGL(k_voxel_points, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, c, vox, nx, ny, nz, pts_out);
+    if (hipGetLastError() != hipSuccess) {
+        sd_set_error("sd_voxel_points: launch failed");
+        return -2;
+    }
+    return 0;
+}
+
+static int sg_valid(const sd_seg_head *h, int need_seg) {
+    if (!h || !h->w1 || !h->b1 || !h->w2 || !h->b2) return 0;
+    if (h->d_in != SG_DR || h->d_latent != SG_DL || h->d_full <= 0 || h->d_full % 32 ||
+        h->d_full > 4096)
+        return 0;
+    if (need_seg) {
+        if (!h->wl || !h->bl || !h->bo || !h->wm || !h->bm || !h->bn1 || !h->wn2 ||
+            !h->centres || !h->assign)
+            return 0;
+        if (h->d_code != SG_DC || h->n_clusters <= 0 || h->n_clusters > 256) return 0;
+    }
+    return 1;
+}
+
+extern "C" int sd_seg_query(const float *dino, int64_t P, const sd_seg_head *h,
+                            const float *sigma, float voxel_size, int32_t *labels, uint8_t *seg,
+                            float *dino_full, void *stream) {
+    const int want_seg = labels != nullptr || seg != nullptr;
+    if (!dino || P < 0 || !sg_valid(h, want_seg) || (seg && !sigma) ||
+        (!want_seg && !dino_full)) {
+        sd_set_error("sd_seg_query: invalid argument (d_in 64, d_latent 128, d_full % 32 == 0, "
+                     "d_code 64, 1..256 clusters; seg needs sigma; at least one output)");
+        return -1;
+    }
+    if (P == 0) return 0;
+    const int64_t per_wg = (int64_t)SG_WAVES * 32 * SG_NT;
+    const int64_t nblk = (P + per_wg - 1) / per_wg;
+    if (nblk > 0x7fffffffLL) {
+        sd_set_error("sd_seg_query: too many points");
+        return -1;
+    }
+    const float neg_vox = -voxel_size;
+    hipStream_t s = (hipStream_t)stream;
+    const int mode = (dino_full ? 1 : 0) | (want_seg ? 2 : 0);
+    switch (mode) {
+    case 1:
+        hipLaunchKernelGGL(k_seg_head<1>, dim3((unsigned)nblk), dim3(SG_WAVES * 64), 0, s, dino,
+                           P, h->d_full, sigma, neg_vox, *h, labels, seg, dino_full);
+        break;
+    case 2:
+        hipLaunchKernelGGL(k_seg_head<2>, dim3((unsigned)nblk), dim3(SG_WAVES * 64), 0, s, dino,
+                           P, h->d_full, sigma, neg_vox, *h, labels, seg, dino_full);
+        break;
+    default:
+        hipLaunchKernelGGL(k_seg_head<3>, dim3((unsigned)nblk), dim3(SG_WAVES * 64), 0, s, dino,
+                           P, h->d_full, sigma, neg_vox, *h, labels, seg, dino_full);
+        break;
+    }
+    if (hipGetLastError() != hipSuccess) {
+        sd_set_error("sd_seg_query: launch failed");
+        return -2;
+    }
+    return 0;
+}

@@ -313,9 +313,10 @@ class BTSNet(nn.Module):
             self._timed("render", lambda: _lib.render_fused(args, m.rec, rays))
         return out
 
-    def query(self, xyz):
+    def query(self, xyz, colors: bool = True):
         """Raw per-point field: sigma (n,P), dino (n,P,D), rgb (n,P,3nv), invalid (n,P,nv),
-        invalid_features (n,P) -- all from sd_field_query."""
+        invalid_features (n,P) -- all from sd_field_query.  colors=False skips the colour
+        sampling (the predict_segmentation path, bts.py:528-533): rgb / invalid are None."""
         self._check_supported()
         m = self._mlp()
         gc = self._grids()
@@ -325,22 +326,64 @@ class BTSNet(nn.Module):
         if n != gc["B"]:
             raise ValueError(f"xyz batch {n} != encoded batch {gc['B']}")
         dev = xyz.device
-        nv = gc["nv"]
+        nv = gc["nv"] if colors else 0
         xyz = xyz.float().contiguous()
         sigma = torch.empty(n, P, device=dev)
         dino = torch.empty(n, P, m.D, device=dev)
-        rgb = torch.empty(n, P, 3 * nv, device=dev)
-        inv = torch.empty(n, P, nv, device=dev)
+        rgb = torch.empty(n, P, 3 * nv, device=dev) if colors else None
+        inv = torch.empty(n, P, nv, device=dev) if colors else None
         invf = torch.empty(n, P, device=dev, dtype=torch.bool)  # bytes 0 / 1
         args = _lib.SdFieldArgs(
             xyz=xyz.data_ptr(), B=n, P=P, grid=self._grid_nhwc(gc).data_ptr(), Hf=gc["Hf"],
             Wf=gc["Wf"],
-            cam_f=gc["cam_f"].data_ptr(), img=gc["img"].data_ptr(), nv=nv, Hc=gc["Hc"],
-            Wc=gc["Wc"], cam_c=gc["cam_c"].data_ptr(), sigma=sigma.data_ptr(),
-            dino=dino.data_ptr(), rgb=rgb.data_ptr(), invalid=inv.data_ptr(),
-            invalid_f=invf.data_ptr())
-        _lib.field_query(args, m.rec, xyz)
+            cam_f=gc["cam_f"].data_ptr(), img=gc["img"].data_ptr() if colors else None, nv=nv,
+            Hc=gc["Hc"], Wc=gc["Wc"], cam_c=gc["cam_c"].data_ptr(), sigma=sigma.data_ptr(),
+            dino=dino.data_ptr(), rgb=rgb.data_ptr() if colors else None,
+            invalid=inv.data_ptr() if colors else None, invalid_f=invf.data_ptr())
+        self._timed("field", lambda: _lib.field_query(args, m.rec, xyz))
         return sigma, dino, rgb, inv, invf
+
+    # -- segmentation head (SSCBench / inference_3d) ----------------------------
+    def _dim_reduction(self):
+        dr = getattr(self.encoder, "dim_reduction", None)
+        if dr is None or not (hasattr(dr, "linear_in") and hasattr(dr, "linear_out")):
+            return None
+        return dr
+
+    def _seg_rec(self, with_head: bool):
+        """PackedSegHead for encoder.dim_reduction (+ downstream_head's stego path)."""
+        from ..seg_pack import PackedSegHead, seg_key
+        dr = self._dim_reduction()
+        if dr is None:
+            raise NotImplementedError("sd_seg_query needs encoder.dim_reduction = MlpDimReduction "
+                                      "(dim_reduction_arch: mlp, every shipped config)")
+        dh = self.downstream_head if with_head else None
+        stego = getattr(dh, "stego_head", None) if dh is not None else None
+        clus = getattr(dh, "stego_cluster_head", None) if dh is not None else None
+        key = seg_key(dr, stego, clus) + (with_head,)
+        cache = getattr(self, "_seg_cache", None)
+        if cache is None or cache[0] != key:
+            rec = PackedSegHead(dr, stego, clus, device=dr.linear_in.weight.device)
+            self._seg_cache = cache = (key, rec)
+        return cache[1]
+
+    def predict_voxels(self, xyz, voxel_size: float = 0.2, prediction_mode="stego_kmeans"):
+        """SSCBench per-chunk query, GPU-resident (evaluate_model_sscbench.py:717-742 at
+        factor 1 with USE_ALPHA_WEIGHTING): xyz (1, P, 3) -> sigma (P,) f32 and the
+        alpha-weighted class seg (P,) uint8 = label if 1 - exp(-voxel_size sigma) > 0 else 0.
+        sd_field_query (no colours) + sd_seg_query; the 768-d features never reach HBM."""
+        if prediction_mode != "stego_kmeans":
+            raise NotImplementedError("predict_voxels implements prediction_mode='stego_kmeans' "
+                                      "(the SSCBench 'scenedino' mode)")
+        if self.downstream_head is None:
+            raise ValueError("predict_voxels needs a downstream (segmentation) head")
+        sigma, dino, _, _, _ = self.query(xyz, colors=False)
+        rec = self._seg_rec(True)
+        P = sigma.numel()
+        _, seg, _ = self._timed("seg", lambda: _lib.seg_query(
+            dino.reshape(P, -1), rec.rec, sigma=sigma.reshape(P), voxel_size=voxel_size,
+            want_labels=False, want_seg=True))
+        return sigma.reshape(P), seg
 
     def forward(self, xyz: torch.Tensor, **kwargs):
         """Same return contract as bts.py:476-595."""
@@ -352,15 +395,26 @@ class BTSNet(nn.Module):
             raise NotImplementedError("render_flow is a training-only option")
         with torch.profiler.record_function("model_inference"):
             n_, n_pts, _ = xyz.shape
-            sigma, dino, rgb, inv, invf = self.query(xyz)
+            sigma, dino, rgb, inv, invf = self.query(xyz, colors=not predict_segmentation)
             sigma = sigma.unsqueeze(-1)
-            if predict_segmentation:
-                dino_full = self.encoder.expand_dim(dino)
-                if self.downstream_head is not None:
-                    seg = self.downstream_head(dino_full, mode=prediction_mode)
-                    seg = F.one_hot(seg, self.gt_classes)
+            if predict_segmentation:  # bts.py:584-592
+                D = dino.shape[-1]
+                fused = (self._dim_reduction() is not None and
+                         (self.downstream_head is None or prediction_mode == "stego_kmeans"))
+                if not fused:  # a foreign dim reduction / another head mode: their own forward
+                    dino_full = self.encoder.expand_dim(dino)
+                    seg = (self.downstream_head(dino_full, mode=prediction_mode)
+                           if self.downstream_head is not None else None)
                 else:
-                    seg = None
+                    with_head = self.downstream_head is not None
+                    rec = self._seg_rec(with_head)
+                    labels, _, full = self._timed("seg", lambda: _lib.seg_query(
+                        dino.reshape(-1, D).contiguous(), rec.rec, want_labels=with_head,
+                        want_full=True))
+                    dino_full = full.view(n_, n_pts, -1)
+                    seg = labels.view(n_, n_pts).long() if with_head else None
+                if seg is not None:
+                    seg = F.one_hot(seg, self.gt_classes)
                 return dino_full, None, sigma, seg
             if only_density:
                 rgb = torch.zeros((n_, n_pts, rgb.shape[-1]), device=sigma.device)

@@ -1,0 +1,152 @@
+"""Pack MlpDimReduction + SemanticHead("stego_kmeans") parameters into the folded,
+MFMA-fragment-ordered record ``sd_seg_head`` that k_seg_head (csrc/sdhip_seg.hip) reads.
+
+Reference modules: MlpDimReduction (scenedino/models/backbones/dino/dim_reduction.py:15-25),
+StegoClusterHead (scenedino/downstream_head/semantic_head.py:285-305), KMeansParamHead
+(semantic_head.py:308-373).
+
+Folding (exact algebra, done once here in fp64):
+    L  = Wl  @ W2   (d_code x d_latent)      bl_f = Wl  @ b2
+    M  = Wn1 @ W2   (d_full x d_latent)      bm   = Wn1 @ b2
+    bo = bl + bn2
+where W2, b2 = linear_out; Wl, bl = linear_path[0]; Wn1, bn1 = nonlinear_path[0];
+Wn2, bn2 = nonlinear_path[2] (1x1 convolutions viewed as matrices).
+
+Fragment maps (v_mfma_f32_32x32x16_bf16; lane l, r = l & 31, h = l >> 5, element j;
+accumulator register i of lane half h holds row (i & 3) + 8 (i >> 2) + 4 h):
+  natural k   : A[t][s][l][j]  = W[32 t + r][16 s + 8 h + j]                 (W1: input = x)
+  permuted k  : A[t][q][l][j]  = W[32 t + r][perm(q, h, j)],
+                perm(q, h, j)  = 32 (q >> 1) + 16 (q & 1) + 8 (j >> 2) + 4 h + (j & 3)
+                (inputs that are accumulator tiles converted in place: W2, L, M, Wn2)
+  row vectors : v[t][h][i]     = vec[32 t + (i & 3) + 8 (i >> 2) + 4 h]
+  centres     : c[k][rt][h][i] = C_norm[k][32 rt + (i & 3) + 8 (i >> 2) + 4 h]
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+
+
+def _accrow(n_tiles: int, device):
+    t = torch.arange(n_tiles, device=device).view(-1, 1, 1)
+    h = torch.arange(2, device=device).view(1, -1, 1)
+    i = torch.arange(16, device=device).view(1, 1, -1)
+    return 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h  # (n_tiles, 2, 16)
+
+
+def _frag_natural(W: torch.Tensor):
+    """(rows, cols) -> [rows/32][cols/16][64][8]"""
+    R, Ccols = W.shape
+    dev = W.device
+    t = torch.arange(R // 32, device=dev).view(-1, 1, 1, 1)
+    s = torch.arange(Ccols // 16, device=dev).view(1, -1, 1, 1)
+    l = torch.arange(64, device=dev).view(1, 1, -1, 1)
+    j = torch.arange(8, device=dev).view(1, 1, 1, -1)
+    rows = 32 * t + (l & 31)
+    cols = 16 * s + 8 * (l >> 5) + j
+    rows, cols = torch.broadcast_tensors(rows, cols)
+    return W[rows, cols]
+
+
+def _frag_permuted(W: torch.Tensor):
+    """(rows, cols) -> [rows/32][cols/16][64][8] with the accumulator-as-operand k order."""
+    R, Ccols = W.shape
+    dev = W.device
+    t = torch.arange(R // 32, device=dev).view(-1, 1, 1, 1)
+    q = torch.arange(Ccols // 16, device=dev).view(1, -1, 1, 1)
+    l = torch.arange(64, device=dev).view(1, 1, -1, 1)
+    j = torch.arange(8, device=dev).view(1, 1, 1, -1)
+    rows = 32 * t + (l & 31)
+    cols = 32 * (q >> 1) + 16 * (q & 1) + 8 * (j >> 2) + 4 * (l >> 5) + (j & 3)
+    rows, cols = torch.broadcast_tensors(rows, cols)
+    return W[rows, cols]
+
+
+def _mat(w: torch.Tensor) -> torch.Tensor:
+    """nn.Linear weight or 1x1 Conv2d weight -> (out, in) float64."""
+    return w.detach().reshape(w.shape[0], -1).double()
+
+
+class PackedSegHead:
+    """Device buffers + the ctypes ``sd_seg_head`` record.  Keep the object alive while
+    kernels that use it may run.
+
+    dim_reduction: module with ``linear_in`` / ``linear_out`` (MlpDimReduction).
+    stego_head / cluster_head: StegoClusterHead / KMeansParamHead, or None for an
+    expand-only record (transform_expand)."""
+
+    def __init__(self, dim_reduction, stego_head=None, cluster_head=None, device=None,
+                 frag_dtype=torch.bfloat16):
+        W1 = _mat(dim_reduction.linear_in.weight)
+        b1 = dim_reduction.linear_in.bias.detach().double()
+        W2 = _mat(dim_reduction.linear_out.weight)
+        b2 = dim_reduction.linear_out.bias.detach().double()
+        dev = device if device is not None else W1.device
+        W1, b1, W2, b2 = (x.to(dev) for x in (W1, b1, W2, b2))
+        d_latent, d_in = W1.shape
+        d_full = W2.shape[0]
+        if d_in != 64 or d_latent != 128 or d_full % 32 or W2.shape[1] != d_latent:
+            raise NotImplementedError(
+                f"sd_seg_query needs MlpDimReduction(64 -> 128 -> d_full % 32 == 0); got "
+                f"linear_in {tuple(W1.shape)}, linear_out {tuple(W2.shape)}")
+        bf = frag_dtype  # bf16 for the kernel; float64 lets tests emulate the MFMA chain
+        fdt = torch.float64 if frag_dtype == torch.float64 else torch.float32
+        self.w1 = _frag_natural(W1).to(bf).contiguous()
+        self.b1 = b1[_accrow(d_latent // 32, dev)].to(fdt).contiguous()
+        self.w2 = _frag_permuted(W2).to(bf).contiguous()
+        self.b2 = b2[_accrow(d_full // 32, dev)].to(fdt).contiguous()
+        self.d_in, self.d_latent, self.d_full = d_in, d_latent, d_full
+        self.seg = stego_head is not None and cluster_head is not None
+        null = None
+        fields = dict(w1=self.w1.data_ptr(), b1=self.b1.data_ptr(), w2=self.w2.data_ptr(),
+                      b2=self.b2.data_ptr(), wl=null, bl=null, bo=null, wm=null, bm=null,
+                      bn1=null, wn2=null, centres=null, assign=null, n_clusters=0,
+                      d_in=d_in, d_latent=d_latent, d_full=d_full, d_code=0)
+        if self.seg:
+            lin = stego_head.linear_path[0]
+            nl0, nl2 = stego_head.nonlinear_path[0], stego_head.nonlinear_path[2]
+            Wl, bl = _mat(lin.weight).to(dev), lin.bias.detach().double().to(dev)
+            Wn1, bn1 = _mat(nl0.weight).to(dev), nl0.bias.detach().double().to(dev)
+            Wn2, bn2 = _mat(nl2.weight).to(dev), nl2.bias.detach().double().to(dev)
+            d_code, d_mid = Wn2.shape
+            if (Wl.shape != (d_code, d_full) or Wn1.shape != (d_mid, d_full) or d_mid != d_full
+                    or d_code != 64):
+                raise NotImplementedError(
+                    "sd_seg_query needs StegoClusterHead(d_full -> 64, mid = d_full)")
+            L = Wl @ W2
+            M = Wn1 @ W2
+            self.wl = _frag_permuted(L).to(bf).contiguous()
+            self.bl = (Wl @ b2)[_accrow(d_code // 32, dev)].to(fdt).contiguous()
+            self.bo = (bl + bn2)[_accrow(d_code // 32, dev)].to(fdt).contiguous()
+            self.wm = _frag_permuted(M).to(bf).contiguous()
+            self.bm = (Wn1 @ b2)[_accrow(d_full // 32, dev)].to(fdt).contiguous()
+            self.bn1 = bn1[_accrow(d_full // 32, dev)].to(fdt).contiguous()
+            self.wn2 = _frag_permuted(Wn2).to(bf).contiguous()
+            # KMeansParamHead._kmeans_cosine: F.normalize(cluster_centers, dim=1) (fp32)
+            cn = F.normalize(cluster_head.cluster_centers.detach().to(fdt), dim=1).to(dev)
+            n_cl = cn.shape[0]
+            if cn.shape[1] != d_code or not 1 <= n_cl <= 256:
+                raise NotImplementedError("cluster centres must be (1..256, 64)")
+            self.centres = cn[:, _accrow(d_code // 32, dev)].contiguous()  # (k, rt, h, 16)
+            self.assign = cluster_head.pseudo_assignment.detach().to(dev, torch.int32).contiguous()
+            if self.assign.numel() != n_cl:
+                raise ValueError("pseudo_assignment must have one entry per cluster")
+            fields.update(wl=self.wl.data_ptr(), bl=self.bl.data_ptr(), bo=self.bo.data_ptr(),
+                          wm=self.wm.data_ptr(), bm=self.bm.data_ptr(), bn1=self.bn1.data_ptr(),
+                          wn2=self.wn2.data_ptr(), centres=self.centres.data_ptr(),
+                          assign=self.assign.data_ptr(), n_clusters=n_cl, d_code=d_code)
+            self.n_clusters, self.d_code = n_cl, d_code
+        self.rec = _lib.SdSegHead(**fields)
+
+
+def seg_key(*modules):
+    """Cache key over every parameter / buffer of the given modules."""
+    key = []
+    for m in modules:
+        if m is None:
+            continue
+        for t in list(m.parameters()) + list(m.buffers()):
+            key.append((t.data_ptr(), t._version, tuple(t.shape), str(t.device)))
+    return tuple(key)

@@ -349,8 +349,101 @@ def fx_render_full_digest(ref):
     )
 
 
+def load_reference_seg():
+    """The reference's MlpDimReduction and SemanticHead pieces (CPU).  semantic_head.py
+    imports the CRF helper (pydensecrf, torchvision.transforms.functional: absent here,
+    unused by the inference path) -> stub modules; SemanticHead.__init__ allocates its
+    training buffers on "cuda", so the head object is assembled with its reference
+    sub-modules and its own (unbound) forward is called."""
+    for name in ("pydensecrf", "pydensecrf.densecrf", "pydensecrf.utils",
+                 "torchvision.transforms.functional"):
+        sys.modules.setdefault(name, types.ModuleType(name))
+    sys.modules["pydensecrf"].densecrf = sys.modules["pydensecrf.densecrf"]
+    sys.modules["pydensecrf"].utils = sys.modules["pydensecrf.utils"]
+    for sub in ("scenedino.models.backbones", "scenedino.models.backbones.dino"):
+        m = types.ModuleType(sub)
+        m.__path__ = [os.path.join(REF, *sub.split("."))]
+        sys.modules[sub] = m
+    from scenedino.models.backbones.dino.dim_reduction import MlpDimReduction
+    from scenedino.downstream_head import semantic_head as sh
+    return MlpDimReduction, sh
+
+
+def fx_seg_head():
+    """transform_expand (dim_reduction.py:22-25) + SemanticHead.forward "stego_kmeans"
+    (semantic_head.py:107-111) on seeded 64-d DINO codes; d_full 768 (ViT-B) and 384
+    (ViT-S, configs/downstream/semantic.yaml input_dim)."""
+    MlpDimReduction, sh = load_reference_seg()
+    out = {}
+    for d_full in (768, 384):
+        torch.manual_seed(60 + d_full)
+        dr = MlpDimReduction(d_full, 64, latent_channels=128).eval()
+        stego = sh.StegoClusterHead(d_full, 64).eval()
+        clus = sh.KMeansParamHead(19, 19, 64).eval()
+        with torch.no_grad():
+            clus.pseudo_assignment.copy_((torch.arange(19) * 7 + 3) % 19)
+        head = torch.nn.Module()
+        head.stego_head, head.stego_cluster_head = stego, clus
+        g = torch.Generator().manual_seed(61)
+        P = 2048
+        x = torch.randn(P, 64, generator=g) * 0.5
+        x[:16] *= 40.0     # large codes
+        x[16:32] *= 1e-3   # tiny codes
+        x[32] = 0.0        # zero code -> relu(b1) path
+        with torch.no_grad():
+            full = dr.transform_expand(x.view(1, P, 64))
+            seg = sh.SemanticHead.forward(head, full, mode="stego_kmeans")
+        t = f"_{d_full}"
+        out.update({
+            "x" + t: np32(x), "full" + t: np32(full[0, :256]), "labels" + t: seg[0].numpy(),
+            "W1" + t: np32(dr.linear_in.weight), "b1" + t: np32(dr.linear_in.bias),
+            "W2" + t: np32(dr.linear_out.weight), "b2" + t: np32(dr.linear_out.bias),
+            "Wl" + t: np32(stego.linear_path[0].weight), "bl" + t: np32(stego.linear_path[0].bias),
+            "Wn1" + t: np32(stego.nonlinear_path[0].weight),
+            "bn1" + t: np32(stego.nonlinear_path[0].bias),
+            "Wn2" + t: np32(stego.nonlinear_path[2].weight),
+            "bn2" + t: np32(stego.nonlinear_path[2].bias),
+            "centres" + t: np32(clus.cluster_centers), "assign" + t: clus.pseudo_assignment.numpy(),
+        })
+    np.savez_compressed(os.path.join(HERE, "seg_head.npz"), **out)
+
+
+def fx_voxel_points():
+    """SSCBench voxel-centre grid (evaluate_model_sscbench.py:270-278 -> point_utils.py:17-82).
+    numba is absent here, so TSDFVolume.vox2world (fusion.py:203-219: float32 inputs, f64
+    arithmetic in a numba loop, float32 store) is restated in numpy with explicit f64
+    promotion; rigid_transform (fusion.py:407-411) is the reference's own numpy call
+    sequence (hstack + np.dot with the f64 transform, a BLAS dgemm); .float() rounds once.
+    T = read_calib()["Tr"] (point_utils.py:84-137), restated from its constants."""
+    cam2velo = np.array([0.04307104361, -0.08829286498, 0.995162929, 0.8043914418,
+                         -0.999004371, 0.007784614041, 0.04392796942, 0.2993489574,
+                         -0.01162548558, -0.9960641394, -0.08786966659, -0.1770225824]).reshape(3, 4)
+    C2V = np.concatenate([cam2velo, np.array([0, 0, 0, 1]).reshape(1, 4)], axis=0)
+    T = np.identity(4)
+    T[:3, :4] = np.linalg.inv(C2V)[:3, :]
+    origin = np.array([0, -25.6, -2])
+    dims = np.ceil(np.array([51.2, 51.2, 6.4]) / 0.2).astype(int)
+    xv, yv, zv = np.meshgrid(range(dims[0]), range(dims[1]), range(dims[2]), indexing="ij")
+    coords = np.stack([xv.reshape(-1), yv.reshape(-1), zv.reshape(-1)], 1).astype(np.float32)
+    o32 = origin.astype(np.float32).astype(np.float64)
+    cam = ((o32[None] + 0.2 * coords.astype(np.float64)) + 0.2 * 0.5).astype(np.float32)
+    xyz_h = np.hstack([cam, np.ones((len(cam), 1), dtype=np.float32)])
+    pts = torch.tensor(np.dot(T, xyz_h.T).T[:, :3]).float().numpy()
+    sel = np.arange(0, len(pts), 2049)
+    with open(os.path.join(HERE, "voxel_points.json"), "w") as f:
+        json.dump({"origin": origin.tolist(), "voxel_size": 0.2, "dims": dims.tolist(),
+                   "T": T.tolist(), "sha256": hashlib.sha256(pts.tobytes()).hexdigest(),
+                   "slice_stride": 2049, "slice": pts[sel].tolist()}, f)
+
+
 def main():
     torch.set_num_threads(8)
+    if os.environ.get("GOLDEN_ONLY") == "seg":
+        _install_stubs()
+        fx_seg_head()
+        fx_voxel_points()
+        print("seg / voxel fixtures written to", HERE)
+        return
     ref = load_reference()
     fx_gen_rays(ref)
     fx_sample_z(ref)

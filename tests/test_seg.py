@@ -1,0 +1,290 @@
+"""SSCBench voxel-query path: voxel-centre grid (a20), transform_expand (a18) and the
+stego / cosine k-means head (a22) with the alpha-weighted class pick (a21).
+
+CPU tests (no GPU): the oracle against the reference's golden vectors
+(tests/golden/seg_head.npz, voxel_points.json from tests/golden/make_golden.py), and the
+folded MFMA fragment packing (scenedino_amd/seg_pack.py) emulated lane by lane in fp64.
+
+GPU tests (through the C ABI): sd_voxel_points bit-exact (SHA-256 of the full 256x256x32
+grid), sd_seg_query against the fixtures and the oracle.  Tolerances (written here):
+  * voxel points: bit-exact.
+  * dino_full (transform_expand, bf16 MFMA, fp32 accumulate): rel-L2 <= 1e-2 per point set,
+    max |d| <= 1.5e-2 (unit vectors).
+  * labels: identical wherever the reference's top-2 cosine margin exceeds 2e-2 (a bf16
+    field can only flip near-ties), and >= 97 % agreement overall.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import GOLDEN
+from _helpers import load
+
+from oracle import seg_oracle as SO
+
+
+def seg_params(d, t, dtype=torch.float32):
+    g = lambda k: torch.as_tensor(d[k + t]).to(dtype)
+    p = {k: g(k) for k in ("W1", "b1", "W2", "b2", "bl", "bn1", "bn2", "centres")}
+    for k in ("Wl", "Wn1", "Wn2"):
+        w = g(k)
+        p[k] = w.reshape(w.shape[0], -1)
+    p["assign"] = torch.as_tensor(d["assign" + t]).long()
+    return p
+
+
+def modules_from(p):
+    """scenedino_amd mirror modules carrying the fixture's parameters."""
+    from scenedino_amd.models.backbones.dino import MlpDimReduction
+    from scenedino_amd.downstream_head import StegoClusterHead, KMeansParamHead
+    d_full = p["W2"].shape[0]
+    dr = MlpDimReduction(d_full, 64, 128)
+    st = StegoClusterHead(d_full, 64)
+    cl = KMeansParamHead(19, 19, 64)
+    with torch.no_grad():
+        dr.linear_in.weight.copy_(p["W1"]); dr.linear_in.bias.copy_(p["b1"])
+        dr.linear_out.weight.copy_(p["W2"]); dr.linear_out.bias.copy_(p["b2"])
+        st.linear_path[0].weight.copy_(p["Wl"].view(64, d_full, 1, 1))
+        st.linear_path[0].bias.copy_(p["bl"])
+        st.nonlinear_path[0].weight.copy_(p["Wn1"].view(d_full, d_full, 1, 1))
+        st.nonlinear_path[0].bias.copy_(p["bn1"])
+        st.nonlinear_path[2].weight.copy_(p["Wn2"].view(64, d_full, 1, 1))
+        st.nonlinear_path[2].bias.copy_(p["bn2"])
+        cl.cluster_centers.copy_(p["centres"])
+        cl.pseudo_assignment.copy_(p["assign"])
+    return dr.eval(), st.eval(), cl.eval()
+
+
+# ------------------------------------------------------------------ CPU: oracle pinning
+@pytest.mark.parametrize("d_full", [768, 384])
+def test_seg_oracle_matches_reference(d_full):
+    d = load("seg_head.npz")
+    t = f"_{d_full}"
+    p = seg_params(d, t)
+    x = torch.as_tensor(d["x" + t])
+    full, scores, labels = SO.seg_head(x, p)
+    np.testing.assert_allclose(full[:256].numpy(), d["full" + t], rtol=1e-5, atol=1e-6)
+    assert (labels.numpy() == d["labels" + t]).all()
+
+
+def test_voxel_oracle_matches_reference_sha():
+    from oracle import coracle
+    v = json.load(open(os.path.join(GOLDEN, "voxel_points.json")))
+    pts = coracle.voxel_points(v["origin"], v["voxel_size"], v["dims"], np.array(v["T"]))
+    assert hashlib.sha256(pts.tobytes()).hexdigest() == v["sha256"]
+    sl = np.array(v["slice"], np.float32)
+    assert (pts[:: v["slice_stride"]] == sl).all()
+
+
+def test_mirror_modules_state_dict_keys():
+    """Reference checkpoint keys of the head / dim-reduction modules are unchanged."""
+    from scenedino_amd.downstream_head import SemanticHead
+    from scenedino_amd.models.backbones.dino import MlpDimReduction
+    keys = set(SemanticHead(19, 19, 768, 64).state_dict())
+    for k in ("stego_head.linear_path.0.weight", "stego_head.nonlinear_path.0.weight",
+              "stego_head.nonlinear_path.2.bias", "stego_cluster_head.cluster_centers",
+              "stego_cluster_head.pseudo_assignment", "direct_cluster_head.cluster_centers",
+              "direct_linear_head.linear.weight", "stego_linear_head.linear.bias"):
+        assert k in keys, k
+    assert set(MlpDimReduction(768, 64, 128).state_dict()) == {
+        "linear_in.weight", "linear_in.bias", "linear_out.weight", "linear_out.bias"}
+
+
+# ----------------------------------------------- CPU: lane-level emulation of the kernel
+def _mfma(A, B):
+    """v_mfma_f32_32x32x16: A, B fragments (64, 8) -> acc (32 rows, 32 cols)."""
+    return A[:32] @ B[:32].t() + A[32:] @ B[32:].t()
+
+
+def _to_regs(acc):
+    """acc (32, 32) -> registers (64 lanes, 16): lane c + 32h, reg i = row (i&3)+8(i>>2)+4h."""
+    i = torch.arange(16)
+    regs = torch.empty(64, 16, dtype=acc.dtype)
+    for h in range(2):
+        rows = (i & 3) + 8 * (i >> 2) + 4 * h
+        regs[32 * h:32 * h + 32] = acc[rows].t()
+    return regs
+
+
+def _emulate(pk, x):
+    """The k_seg_head register program for 32 points, in fp64."""
+    B = lambda regs, s: regs[:, 8 * s:8 * s + 8]
+    xb = [torch.cat([x[:, 16 * s:16 * s + 8], x[:, 16 * s + 8:16 * s + 16]], 0) for s in range(4)]
+    hb = []
+    for t in range(4):
+        acc = sum(_mfma(pk.w1[t, s], xb[s]) for s in range(4))
+        regs = torch.relu(_to_regs(acc) + pk.b1[t].repeat_interleave(32, 0))
+        hb += [B(regs, 0), B(regs, 1)]
+    T2 = pk.d_full // 32
+    ss = torch.zeros(64, dtype=torch.float64)
+    for t in range(T2):
+        e = _to_regs(sum(_mfma(pk.w2[t, q], hb[q]) for q in range(8))) + pk.b2[t].repeat_interleave(32, 0)
+        ss += (e * e).sum(1)
+    n = (ss[:32] + ss[32:]).sqrt().clamp_min(1e-12).repeat(2).unsqueeze(1)
+    sacc = []
+    for rt in range(2):
+        a = _to_regs(sum(_mfma(pk.wl[rt, q], hb[q]) for q in range(8)))
+        sacc.append((a + pk.bl[rt].repeat_interleave(32, 0)) / n + pk.bo[rt].repeat_interleave(32, 0))
+    for t in range(T2):
+        v = _to_regs(sum(_mfma(pk.wm[t, q], hb[q]) for q in range(8)))
+        u = torch.relu((v + pk.bm[t].repeat_interleave(32, 0)) / n + pk.bn1[t].repeat_interleave(32, 0))
+        for rt in range(2):
+            sacc[rt] = sacc[rt] + _to_regs(sum(_mfma(pk.wn2[rt, 2 * t + s], B(u, s)) for s in range(2)))
+    scores = []
+    for k in range(pk.n_clusters):
+        d = sum((pk.centres[k, rt].repeat_interleave(32, 0) * sacc[rt]).sum(1) for rt in range(2))
+        scores.append(d[:32] + d[32:])
+    return torch.stack(scores, 1)
+
+
+def test_packed_fragments_emulate_reference_chain():
+    from scenedino_amd.seg_pack import PackedSegHead
+    d = load("seg_head.npz")
+    p = seg_params(d, "_384", torch.float64)
+    dr, st, cl = modules_from({k: v.float() if v.is_floating_point() else v for k, v in p.items()})
+    pk = PackedSegHead(dr, st, cl, frag_dtype=torch.float64)
+    x = torch.as_tensor(d["x_384"][:32]).double()
+    scores = _emulate(pk, x)
+    pd = {k: v.double() if v.is_floating_point() else v for k, v in p.items()}
+    pd["centres"] = torch.as_tensor(d["centres_384"]).double()
+    _, ref_scores, labels = SO.seg_head(x, pd)
+    # scores differ from the reference only by the positive |stego| scale
+    ref_dir = ref_scores / ref_scores.norm(dim=1, keepdim=True)
+    got_dir = scores / scores.norm(dim=1, keepdim=True)
+    assert torch.allclose(got_dir, ref_dir, atol=1e-9)
+    got_labels = pd["assign"][scores.argmax(1)]
+    assert (got_labels == labels).all()
+
+
+# ------------------------------------------------------------------------ GPU tests
+@pytest.fixture(scope="module")
+def gpu():
+    assert torch.cuda.is_available(), "GPU tests need a ROCm device"
+    from scenedino_amd import _lib
+    _lib.load()
+    return "cuda"
+
+
+@pytest.mark.gpu
+def test_voxel_points_bit_exact(gpu):
+    from scenedino_amd import _lib
+    v = json.load(open(os.path.join(GOLDEN, "voxel_points.json")))
+    pts = _lib.voxel_points(v["origin"], v["voxel_size"], v["dims"], v["T"], gpu).cpu().numpy()
+    assert pts.shape == (256 * 256 * 32, 3)
+    assert hashlib.sha256(pts.tobytes()).hexdigest() == v["sha256"]
+
+
+@pytest.mark.gpu
+def test_voxel_points_ragged_dims(gpu):
+    from scenedino_amd import _lib
+    from oracle import coracle
+    T = np.eye(4)
+    T[:3, :3] = [[0.0, -1.0, 0.0], [0.3, 0.0, -0.95], [0.95, 0.0, 0.3]]
+    T[:3, 3] = [0.5, -1.25, 2.0]
+    for dims in ((1, 1, 1), (7, 5, 3), (33, 17, 9)):
+        ref = coracle.voxel_points([0.1, -3.3, 1.7], 0.37, dims, T)
+        got = _lib.voxel_points([0.1, -3.3, 1.7], 0.37, dims, T, gpu).cpu().numpy()
+        assert (got == ref).all(), dims
+
+
+def _label_check(labels, ref_scores, ref_labels, what):
+    top2 = ref_scores.topk(2, dim=1).values
+    margin = (top2[:, 0] - top2[:, 1]).numpy()
+    labels = np.asarray(labels)
+    ref_labels = np.asarray(ref_labels)
+    sure = margin > 2e-2
+    assert (labels[sure] == ref_labels[sure]).all(), f"{what}: clear-margin label mismatch"
+    agree = (labels == ref_labels).mean()
+    assert agree >= 0.97, f"{what}: label agreement {agree:.4f}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d_full", [768, 384])
+def test_seg_query_vs_reference(gpu, d_full):
+    from scenedino_amd import _lib
+    from scenedino_amd.seg_pack import PackedSegHead
+    d = load("seg_head.npz")
+    t = f"_{d_full}"
+    p = seg_params(d, t)
+    dr, st, cl = (m.to(gpu) for m in modules_from(p))
+    pk = PackedSegHead(dr, st, cl)
+    x = torch.as_tensor(d["x" + t]).to(gpu)
+    labels, _, full = _lib.seg_query(x, pk.rec, want_labels=True, want_full=True)
+    f = full[:256].double().cpu()
+    ref = torch.as_tensor(d["full" + t]).double()
+    rel = ((f - ref).norm(dim=1) / ref.norm(dim=1)).max().item()
+    assert rel <= 1e-2, f"dino_full rel-L2 {rel:.3g}"
+    assert (f - ref).abs().max().item() <= 1.5e-2
+    _, ref_scores, ref_labels = SO.seg_head(torch.as_tensor(d["x" + t]), p)
+    _label_check(labels.cpu(), ref_scores, d["labels" + t], "labels")
+    # labels-only and full-only launches give the same results as the combined one
+    l2, _, _ = _lib.seg_query(x, pk.rec, want_labels=True)
+    assert torch.equal(l2, labels)
+    pk_e = PackedSegHead(dr)
+    _, _, f2 = _lib.seg_query(x, pk_e.rec, want_labels=False, want_full=True)
+    assert torch.equal(f2, full)
+
+
+@pytest.mark.gpu
+def test_seg_query_ragged_and_alpha_pick(gpu):
+    """P not a multiple of the 512-point workgroup tile; seg = alpha-weighted pick."""
+    from scenedino_amd import _lib
+    from scenedino_amd.seg_pack import PackedSegHead
+    d = load("seg_head.npz")
+    p = seg_params(d, "_768")
+    dr, st, cl = (m.to(gpu) for m in modules_from(p))
+    pk = PackedSegHead(dr, st, cl)
+    for P in (1, 31, 77, 545):
+        x = torch.as_tensor(d["x_768"][:P]).to(gpu)
+        g = torch.Generator().manual_seed(P)
+        sigma = torch.rand(P, generator=g) * 3
+        sigma[::5] = 0.0        # alpha == 0 -> class 0
+        sigma[1::7] = 1e-9      # alpha rounds to 0 as well
+        labels, seg, _ = _lib.seg_query(x, pk.rec, sigma=sigma.to(gpu), want_labels=True,
+                                        want_seg=True)
+        lab = labels.cpu().long()
+        ref_seg = SO.alpha_seg(sigma, lab)
+        assert torch.equal(seg.cpu().long(), ref_seg), P
+        full_labels, _, _ = _lib.seg_query(torch.as_tensor(d["x_768"]).to(gpu), pk.rec)
+        assert torch.equal(labels, full_labels[:P])
+
+
+@pytest.mark.gpu
+def test_btsnet_predict_segmentation_and_voxels(gpu):
+    """BTSNet.forward(predict_segmentation=True) (bts.py:584-592) and the SSCBench chunk
+    query predict_voxels against the field + head oracles."""
+    from _helpers import build_net
+    from oracle import render_oracle as O
+    fq = load("field_query.npz")
+    d = load("seg_head.npz")
+    p = seg_params(d, "_768")
+    net = build_net(fq["grid"], fq["W_in"], fq["b_in"], fq["W_out"], fq["b_out"], "fp32", gpu)
+    dr, st, cl = (m.to(gpu) for m in modules_from(p))
+    from scenedino_amd.downstream_head import SemanticHead
+    head = SemanticHead(19, 19, 768, 64).to(gpu).eval()
+    head.stego_head, head.stego_cluster_head = st, cl
+    net.encoder.dim_reduction = dr
+    net.downstream_head = head
+    net.gt_classes = 19
+    Tn = lambda k: torch.as_tensor(fq[k]).to(gpu)
+    net.encode(Tn("images"), Tn("Ks"), Tn("poses"), ids_encoder=[0], ids_render=[0])
+    xyz = Tn("xyz")
+    with torch.no_grad():
+        dino_full, invalid, sigma, seg = net(xyz, predict_segmentation=True)
+    assert invalid is None and seg.shape == (1, xyz.shape[1], 19)
+    np.testing.assert_allclose(sigma[0, :, 0].cpu().numpy(), fq["sigma"].reshape(-1), rtol=1e-4,
+                               atol=2e-5)
+    dino = torch.as_tensor(fq["dino"]).reshape(-1, 64)
+    ref_full, ref_scores, ref_labels = SO.seg_head(dino, p)
+    rel = (dino_full[0].double().cpu() - ref_full.double()).norm() / ref_full.double().norm()
+    assert rel.item() <= 1e-2
+    _label_check(seg[0].argmax(-1).cpu(), ref_scores, ref_labels, "forward labels")
+    sig2, segv = net.predict_voxels(xyz)
+    assert torch.allclose(sig2, sigma.view(-1))
+    ref_seg = SO.alpha_seg(sig2.cpu(), seg[0].argmax(-1).cpu())
+    assert torch.equal(segv.cpu().long(), ref_seg)
