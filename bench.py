@@ -187,6 +187,87 @@ def _traffic_from_profile(proj):
     return tot, os.path.relpath(files[-1], ROOT) + " (rocprofv3 PMC, per frame)"
 
 
+SEG_FLOPS_ALGO = 2 * (64 * 128 + 128 * 768) + 2 * (768 * 64 + 768 * 768 + 768 * 64) + 2 * 19 * 64
+SEG_FLOPS_EXEC = 2 * (64 * 128 + 2 * 768 * 128 + 64 * 128 + 64 * 768)
+
+
+def main_c5(args, world, rank, local_rank, dist, device):
+    """C5 (BASELINE configs[4]): SSCBench voxel query, 256x256x32 voxels per GPU frame:
+    voxel centres (sd_voxel_points, once per run as the reference does) -> per frame:
+    grid packing (sd_pack_grid) + field query without colours (sd_field_query) + folded
+    transform_expand / stego / k-means head with the alpha-weighted class pick
+    (sd_seg_query) + 3x3x3 density grow.  ViT-B/8-shaped 256x384x1280 grid, d_full 768."""
+    from scenedino_amd import _lib, sscbench
+    from scenedino_amd.models.backbones.dino import MlpDimReduction
+    from scenedino_amd.downstream_head import SemanticHead
+    global HF, WF
+    HF, WF = 384, 1280
+    net, _, _, _, _, _ = make_scene(rank, device, args.precision)
+    torch.manual_seed(5)
+    net.encoder.dim_reduction = MlpDimReduction(768, 64, 128).to(device).eval()
+    net.downstream_head = SemanticHead(19, 19, 768, 64).to(device).eval()
+    net.gt_classes = 19
+    dims = sscbench.grid_dims()
+    pts = sscbench.generate_point_grid(sscbench.read_calib()["Tr"], device=device)
+    n_vox = pts.shape[0]
+    timer = KernelTimer()
+    net.kernel_timer = timer
+
+    def step():
+        net._grid_cache = None
+        return sscbench.query_voxels(net, pts, dims)
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        if dist:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        timer.on = True
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        if dist:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+    seg_ms, field_ms = timer.mean_ms("seg"), timer.mean_ms("field")
+    if dist:
+        t = torch.tensor([elapsed, seg_ms, field_ms], device=device, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed, seg_ms, field_ms = (float(v) for v in t)
+    if rank == 0:
+        algo = n_vox * SEG_FLOPS_ALGO
+        exe = n_vox * SEG_FLOPS_EXEC
+        line = {
+            "metric": "SSCBench voxel-grid query, voxels/sec (256x256x32 grid per frame)",
+            "value": world * n_vox * args.steps / elapsed, "unit": "voxels/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
+            "data": "synthetic (seeded image, N(0,1) 256x384x1280 grid, random-init ResnetFC / "
+                    "MlpDimReduction / SemanticHead)",
+            "config": {"workload": "C5: SSCBench 256x256x32 voxel query, ViT-B/8-shaped "
+                                   "256x384x1280 grid, d_full 768, stego_kmeans, alpha-weighted "
+                                   "class pick + grow", "voxels_per_frame": n_vox,
+                       "parallelism": f"frames{world}"},
+            "roofline": {
+                "kernel": "k_seg_head (sd_seg_query)", "bound": "mfma",
+                "achieved": algo / (seg_ms * 1e-3) / 1e12, "peak": PEAK_TFLOPS["bf16"],
+                "unit": "TFLOP/s", "frac": algo / (seg_ms * 1e-3) / 1e12 / PEAK_TFLOPS["bf16"],
+                "traffic": None, "kernel_ms": seg_ms,
+                "algorithmic_flops_per_launch": algo, "executed_mfma_flops_per_launch": exe,
+                "executed_tflops": exe / (seg_ms * 1e-3) / 1e12,
+                "executed_frac": exe / (seg_ms * 1e-3) / 1e12 / PEAK_TFLOPS["bf16"],
+                "field_query_ms": field_ms,
+                "field_query_tflops": n_vox * mlp_flops_per_point() / (field_ms * 1e-3) / 1e12,
+            },
+        }
+        print(json.dumps(line), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -197,9 +278,10 @@ def main():
     ap.add_argument("--mode", default="proj", choices=["proj", "grid"],
                     help="16-bit render kernel: projected grid (default) or per-sample grid")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--config", default="c2", choices=["c2", "c4"],
+    ap.add_argument("--config", default="c2", choices=["c2", "c4", "c5"],
                     help="c2: BASELINE configs[1] (K=64, D=64, the metric's config); c4: "
-                         "configs[3] render shape (K=128, 384-d feature field)")
+                         "configs[3] render shape (K=128, 384-d feature field); c5: "
+                         "configs[4] SSCBench voxel query (voxels/s)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     args = ap.parse_args()
     global K_SAMPLES, D_DINO
@@ -218,6 +300,12 @@ def main():
 
     from scenedino_amd import _lib
     _lib.load()
+    if args.config == "c5":
+        main_c5(args, world, rank, local_rank, dist, device)
+        if dist:
+            tdist.barrier()
+            tdist.destroy_process_group()
+        return
     net, renderer, wrapper, sampler, pose, Ks = make_scene(rank, device, args.precision,
                                                           args.offset_pose)
     R = H * W
@@ -317,7 +405,7 @@ def main():
                 "executed_tflops": exec_flops / (kern_ms * 1e-3) / 1e12,
             },
         }
-        tr = _traffic_from_profile(proj)
+        tr = _traffic_from_profile(proj) if args.config == "c2" else None
         if tr is not None:
             line["roofline"]["traffic"] = tr[0]
             line["roofline"]["traffic_source"] = tr[1]

@@ -288,3 +288,37 @@ def test_btsnet_predict_segmentation_and_voxels(gpu):
     assert torch.allclose(sig2, sigma.view(-1))
     ref_seg = SO.alpha_seg(sig2.cpu(), seg[0].argmax(-1).cpu())
     assert torch.equal(segv.cpu().long(), ref_seg)
+
+
+@pytest.mark.gpu
+def test_sscbench_downsample_and_predict(gpu):
+    """sscbench.downsample_and_predict (evaluate_model_sscbench.py:660-758, factor 1) against
+    the reference-contract per-chunk path predict_grid -> alpha * one_hot -> argmax, grow."""
+    from _helpers import build_net
+    from scenedino_amd import sscbench
+    from scenedino_amd.downstream_head import SemanticHead
+    fq = load("field_query.npz")
+    p = seg_params(load("seg_head.npz"), "_768")
+    net = build_net(fq["grid"], fq["W_in"], fq["b_in"], fq["W_out"], fq["b_out"], "bf16", gpu)
+    dr, st, cl = (m.to(gpu) for m in modules_from(p))
+    head = SemanticHead(19, 19, 768, 64).to(gpu).eval()
+    head.stego_head, head.stego_cluster_head = st, cl
+    net.encoder.dim_reduction, net.downstream_head, net.gt_classes = dr, head, 19
+    img = torch.as_tensor(fq["images"])[0, 0]
+    data = {"imgs": [img], "poses": [np.eye(4, dtype=np.float32)],
+            "projs": [np.asarray(fq["Ks"])[0, 0]]}
+    pts = sscbench.generate_point_grid(sscbench.read_calib()["Tr"], device=gpu)
+    with torch.no_grad():
+        sig, segs, _ = sscbench.downsample_and_predict(data, net, pts, 1, "stego_kmeans")
+        assert sig.shape == (256, 256, 32) and segs.shape == (256, 256, 32)
+        # reference-contract path on the x-chunk i = 1, y-chunk j = 0
+        blk = pts.view(256, 256, 32, 3)[128:256, 0:128]
+        sg, seg1h, _ = sscbench.predict_grid(None, net, blk, "stego_kmeans")
+        alphas = 1 - torch.exp(-0.2 * sg.reshape(128, 128, 32))
+        ref_seg = (alphas.unsqueeze(-1) * seg1h.reshape(128, 128, 32, 19)).argmax(-1)
+    assert (segs[128:256, 0:128] == ref_seg.cpu().numpy()).all()
+    raw = torch.zeros(256, 256, 32)
+    raw[128:256, 0:128] = sg.reshape(128, 128, 32).cpu()
+    grown = F.max_pool3d(raw.unsqueeze(0), 3, 1, 1).squeeze(0)
+    inner = (slice(129, 255), slice(0, 127))
+    np.testing.assert_array_equal(sig[inner], grown[inner].numpy())
