@@ -242,6 +242,64 @@ int sd_seg_query(const float *dino, int64_t P, const sd_seg_head *h, const float
                 float voxel_size, int32_t *labels, uint8_t *seg, float *dino_full,
                 void *stream);
 
+/* ---- DINO / DINOv2 ViT encoder (sdhip_vit.hip) -------------------------------
+ * Replaces timm's VisionTransformer forward as the reference runs it
+ * (scenedino/models/backbones/dino/vit.py:48-62,112-189 via DINOv2Encoder.forward,
+ * dinov2_module.py:230-288): patch embedding, pre-LN blocks (qkv + softmax attention +
+ * proj, GELU MLP, optional DINOv2 layer scale), final norm.  Residual stream fp32,
+ * GEMM operands bf16, fp32 accumulation. */
+
+enum sd_epilogue {
+    SD_EPI_BF16 = 0,   /* out bf16 (M, ldo) = acc + bias                                  */
+    SD_EPI_GELU = 1,   /* out bf16 = gelu_erf(acc + bias)           (timm Mlp fc1 + act)   */
+    SD_EPI_F32 = 2,    /* out f32 = acc + bias                                             */
+    SD_EPI_RESID = 3,  /* out f32 += gamma * (acc + bias)  (residual add, ls1/ls2 gamma)   */
+    SD_EPI_QKV = 4,    /* scatter qkv columns into q (B,H,T,hd), k (B,H,Tp,hd),            */
+                       /* vt (B,H,hd,Tp) bf16 (timm Attention reshape/permute)             */
+    SD_EPI_PATCH = 5   /* out f32 (B, patches+1, N): row b*(patches+1)+1+p = acc+bias+pos  */
+};
+
+/* C = A (M, K) . W (N, K)^T (+ bias) with the epilogue above; A, W bf16 row-major
+ * (W = nn.Linear weight layout), K % 32 == 0, lda % 8 == 0. */
+typedef struct sd_gemm_args {
+    const void *a; int64_t lda;
+    const void *w;
+    const float *bias;          /* (N) or NULL                                           */
+    int64_t M, N, K;
+    int32_t epi;
+    void *out; int64_t ldo;     /* output / residual, element stride between rows        */
+    const float *gamma;         /* SD_EPI_RESID layer scale (N) or NULL (= 1)            */
+    void *q, *k, *vt;           /* SD_EPI_QKV destinations                               */
+    int32_t tokens, heads, head_dim, tokens_pad;
+    const float *pos;           /* SD_EPI_PATCH position embedding (patches+1, N)        */
+    int32_t patches;
+} sd_gemm_args;
+
+int sd_gemm(const sd_gemm_args *args, void *stream);
+
+/* softmax(q k^T * scale) v per (batch, head); q (B,H,T,64), k (B,H,Tp,64),
+ * vt (B,H,64,Tp) bf16 with rows/columns T..Tp-1 zero; out (B, T, H*64) bf16. */
+int sd_attention(const void *q, const void *k, const void *vt, int32_t B, int32_t heads,
+                 int32_t tokens, int32_t tokens_pad, int32_t head_dim, float scale, void *out,
+                 void *stream);
+
+/* nn.LayerNorm(C, eps) over rows of x (rows, C) f32 -> out (rows, C) bf16 (out_f32 = 0,
+ * the next GEMM's operand) or f32 (out_f32 = 1, the encoder's final norm). */
+int sd_layernorm(const float *x, int64_t rows, int32_t C, const float *w, const float *b,
+                 float eps, void *out, int32_t out_f32, void *stream);
+
+/* img (B,3,H,W) in [-1,1] -> normalised ((x/2+0.5 - mean)/std) im2col patches
+ * (B*Np, Kp) bf16 (zero-padded columns >= 3 p p), and class-token rows of x (B, Np+1, C):
+ * x[b,0,:] = cls + pos[0,:].  mean3/std3: HOST pointers (3). */
+int sd_patchify(const float *img, int32_t B, int32_t H, int32_t W, int32_t p, int32_t Kp,
+                const float *mean3, const float *std3, void *patches, const float *cls,
+                const float *pos, float *x, int32_t C, void *stream);
+
+/* x (B, T, C) f32 -> out (B, C, gh, gw): tokens n_prefix .. n_prefix+gh*gw-1 as a grid,
+ * optionally L2-normalised over C (F.normalize, eps 1e-12). */
+int sd_tokens_to_grid(const float *x, int32_t B, int32_t T, int32_t C, int32_t n_prefix,
+                      int32_t gh, int32_t gw, int32_t l2norm, float *out, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

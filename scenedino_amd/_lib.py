@@ -79,6 +79,18 @@ class SdSegHead(ctypes.Structure):
     ]
 
 
+class SdGemmArgs(ctypes.Structure):
+    _fields_ = [
+        ("a", _vp), ("lda", _i64), ("w", _vp), ("bias", _vp), ("M", _i64), ("N", _i64),
+        ("K", _i64), ("epi", _i32), ("out", _vp), ("ldo", _i64), ("gamma", _vp),
+        ("q", _vp), ("k", _vp), ("vt", _vp),
+        ("tokens", _i32), ("heads", _i32), ("head_dim", _i32), ("tokens_pad", _i32),
+        ("pos", _vp), ("patches", _i32),
+    ]
+
+
+SD_EPI_BF16, SD_EPI_GELU, SD_EPI_F32, SD_EPI_RESID, SD_EPI_QKV, SD_EPI_PATCH = range(6)
+
 # (name, argtypes) of every exported entry point; tests check the .so exports all.
 SIGNATURES = {
     "sd_last_error": [],
@@ -100,6 +112,12 @@ SIGNATURES = {
                         ctypes.POINTER(ctypes.c_double), _vp, _vp],
     "sd_seg_query": [_vp, _i64, ctypes.POINTER(SdSegHead), _vp, ctypes.c_float, _vp, _vp, _vp,
                      _vp],
+    "sd_gemm": [ctypes.POINTER(SdGemmArgs), _vp],
+    "sd_attention": [_vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, ctypes.c_float, _vp, _vp],
+    "sd_layernorm": [_vp, _i64, _i32, _vp, _vp, ctypes.c_float, _vp, _i32, _vp],
+    "sd_patchify": [_vp, _i32, _i32, _i32, _i32, _i32, ctypes.POINTER(ctypes.c_float),
+                    ctypes.POINTER(ctypes.c_float), _vp, _vp, _vp, _vp, _i32, _vp],
+    "sd_tokens_to_grid": [_vp, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp],
 }
 
 _lib = None
@@ -304,3 +322,60 @@ def composite(z, sigma, feat, rgb, hard_alpha_cap, want_weights=True):
                             int(bool(hard_alpha_cap)), ptr(weights), ptr(alphas), ptr(depth),
                             ptr(feat_out), ptr(rgb_out), stream_of(depth)), "sd_composite")
     return weights, alphas, depth, feat_out, rgb_out
+
+
+# ---------------------------------------------------------------------------
+# ViT encoder kernels (sdhip_vit.hip)
+# ---------------------------------------------------------------------------
+def gemm(a, w, bias, epi, out=None, gamma=None, qkv=None, tokens=0, heads=0, pos=None,
+         patches=0):
+    """sd_gemm: a (M, K) bf16 (row stride a.stride(0)), w (N, K) bf16 contiguous."""
+    lib = load()
+    M, K = a.shape
+    N = w.shape[0]
+    if a.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or a.stride(1) != 1:
+        raise TypeError("sd_gemm: a, w must be bf16 with unit inner stride")
+    _req(w, "w", torch.bfloat16)
+    g = SdGemmArgs(a=a.data_ptr(), lda=a.stride(0), w=w.data_ptr(),
+                   bias=bias.data_ptr() if bias is not None else None, M=M, N=N, K=K, epi=epi,
+                   out=out.data_ptr() if out is not None else None,
+                   ldo=out.stride(-2) if out is not None else 0,
+                   gamma=gamma.data_ptr() if gamma is not None else None)
+    if qkv is not None:
+        q, k, vt = qkv
+        g.q, g.k, g.vt = q.data_ptr(), k.data_ptr(), vt.data_ptr()
+        g.tokens, g.heads, g.head_dim, g.tokens_pad = tokens, heads, q.shape[-1], k.shape[-2]
+    if pos is not None:
+        g.pos, g.patches = pos.data_ptr(), patches
+    _check(lib.sd_gemm(ctypes.byref(g), stream_of(a)), "sd_gemm")
+
+
+def attention(q, k, vt, scale, out):
+    lib = load()
+    B, H, T, hd = q.shape
+    _check(lib.sd_attention(ptr(q), ptr(k), ptr(vt), B, H, T, k.shape[-2], hd, float(scale),
+                            ptr(out), stream_of(q)), "sd_attention")
+
+
+def layernorm(x, w, b, eps, out):
+    lib = load()
+    rows, C = x.shape
+    _check(lib.sd_layernorm(ptr(_req(x, "x")), rows, C, ptr(w), ptr(b), float(eps), ptr(out),
+                            int(out.dtype == torch.float32), stream_of(x)), "sd_layernorm")
+
+
+def patchify(img, p, Kp, mean, std, patches, cls, pos, x):
+    lib = load()
+    B, _, H, W = img.shape
+    m = (ctypes.c_float * 3)(*[float(v) for v in mean])
+    sd = (ctypes.c_float * 3)(*[float(v) for v in std])
+    _check(lib.sd_patchify(ptr(_req(img, "img")), B, H, W, p, Kp, m, sd, ptr(patches), ptr(cls),
+                           ptr(pos), ptr(x), x.shape[-1], stream_of(img)), "sd_patchify")
+
+
+def tokens_to_grid(x, B, T, C, n_prefix, gh, gw, l2norm):
+    lib = load()
+    out = torch.empty(B, C, gh, gw, device=x.device, dtype=torch.float32)
+    _check(lib.sd_tokens_to_grid(ptr(_req(x, "x")), B, T, C, n_prefix, gh, gw, int(bool(l2norm)),
+                                 ptr(out), stream_of(x)), "sd_tokens_to_grid")
+    return out

@@ -1,0 +1,554 @@
+// sdhip_vit.hip -- DINO / DINOv2 ViT encoder blocks on gfx950 (CDNA4) MFMA.
+//
+// The reference runs timm's VisionTransformer (scenedino/models/backbones/dino/vit.py:48-62,
+// 112-189, wrapped by DINOv2Encoder, dinov2_module.py:230-288): patch-embed convolution,
+// + class token + position embedding, depth x pre-LN Block
+//     x = x + ls1 * proj(attn(norm1(x)))        (qkv with bias, softmax(q k^T / sqrt(hd)) v)
+//     x = x + ls2 * fc2(gelu(fc1(norm2(x))))    (exact-erf GELU; LayerNorm eps 1e-6)
+// then the final norm.  Kernels here:
+//   k_gemm<BM,BN,EPI>  bf16 x bf16 -> fp32 MFMA (v_mfma_f32_32x32x16_bf16) "NT" GEMM
+//                      out = A (M,K) . W (N,K)^T + bias with fused epilogues: bf16 store,
+//                      GELU, fp32 residual update with layer scale, qkv scatter into the
+//                      attention layouts, patch-embed scatter (+ position embedding).
+//   k_attn             flash attention, head_dim 64, any token count: S^T = K Q^T per
+//                      64-key block with the query on the MFMA lane (softmax row reductions
+//                      stay in the lane), online softmax in fp32, O^T = V^T P with P taken
+//                      straight from the S^T accumulator as the B operand (no LDS trip).
+//   k_layernorm        one wave per token, fp32 in, bf16 out (the next GEMM's A operand).
+//   k_patchify         input normalisation ((x/2+0.5-mean)/std, dinov2_module.py:225-227)
+//                      + im2col of the patch-embed convolution, + class-token rows.
+//   k_tokens_to_grid   drop prefix tokens, (B,T,C) -> (B,C,h,w), optional L2 normalise
+//                      (vit.py:188, dinov2_module.py:270-287).
+// Residual stream x is fp32 (B*T, C); GEMM operands bf16; all accumulation fp32.
+#include "sdhip_common.h"
+
+extern "C" void sd_set_error(const char *msg);
+
+typedef __attribute__((ext_vector_type(4))) float vf4;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+
+#define VT_MFMA(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_bf16((a), (b), (c), 0, 0, 0)
+
+__device__ __forceinline__ f32x16 vt_zero16() {
+    f32x16 z;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) z[i] = 0.f;
+    return z;
+}
+
+// ---------------------------------------------------------------------------
+// GEMM
+// ---------------------------------------------------------------------------
+#define GK 32       // K per pipeline step
+#define GLDS 40     // bf16 per LDS row (32 + 8 pad: 80-B rows, conflict-free b128 reads)
+
+__device__ __forceinline__ float vt_gelu(float x) {
+    // nn.GELU() default (approximate='none'): 0.5 x (1 + erf(x / sqrt(2)))
+    return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+}
+
+template <int BM, int BN, int EPI>
+__global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
+    constexpr int WM = BM / 2, WN = BN / 2;   // per-wave tile (2 x 2 waves)
+    constexpr int TM = WM / 32, TN = WN / 32; // 32x32 MFMA tiles per wave
+    constexpr int CA = BM * 4 / 256;          // 16-B chunks of the A tile per thread
+    constexpr int CB = BN * 4 / 256;
+    __shared__ __attribute__((aligned(16))) __bf16 sA[2][BM * GLDS];
+    __shared__ __attribute__((aligned(16))) __bf16 sB[2][BN * GLDS];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int r = lane & 31, h = lane >> 5;
+    const int64_t m0 = (int64_t)blockIdx.y * BM, n0 = (int64_t)blockIdx.x * BN;
+    const __bf16 *A = (const __bf16 *)g.a;
+    const __bf16 *Wt = (const __bf16 *)g.w;
+    const int nk = (int)(g.K / GK);
+
+    bf16x8 ra[CA], rb[CB];
+    auto gload = [&](int kt) {
+#pragma unroll
+        for (int c = 0; c < CA; ++c) {
+            const int ch = tid + 256 * c, row = ch >> 2, col = (ch & 3) * 8;
+            const int64_t m = m0 + row;
+            if (m < g.M)
+                ra[c] = *(const bf16x8 *)(A + m * g.lda + (int64_t)kt * GK + col);
+            else
+#pragma unroll
+                for (int j = 0; j < 8; ++j) ra[c][j] = (__bf16)0.f;
+        }
+#pragma unroll
+        for (int c = 0; c < CB; ++c) {
+            const int ch = tid + 256 * c, row = ch >> 2, col = (ch & 3) * 8;
+            const int64_t n = n0 + row;
+            if (n < g.N)
+                rb[c] = *(const bf16x8 *)(Wt + n * g.K + (int64_t)kt * GK + col);
+            else
+#pragma unroll
+                for (int j = 0; j < 8; ++j) rb[c][j] = (__bf16)0.f;
+        }
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int c = 0; c < CA; ++c) {
+            const int ch = tid + 256 * c, row = ch >> 2, col = (ch & 3) * 8;
+            *(bf16x8 *)&sA[buf][row * GLDS + col] = ra[c];
+        }
+#pragma unroll
+        for (int c = 0; c < CB; ++c) {
+            const int ch = tid + 256 * c, row = ch >> 2, col = (ch & 3) * 8;
+            *(bf16x8 *)&sB[buf][row * GLDS + col] = rb[c];
+        }
+    };
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = vt_zero16();
+
+    gload(0);
+    lstore(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+        const int buf = kt & 1;
+        if (kt + 1 < nk) gload(kt + 1);
+#pragma unroll
+        for (int s = 0; s < GK / 16; ++s) {
+            bf16x8 af[TM], bfr[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+                af[i] = *(const bf16x8 *)&sA[buf][(wm * WM + i * 32 + r) * GLDS + 16 * s + 8 * h];
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+                bfr[j] = *(const bf16x8 *)&sB[buf][(wn * WN + j * 32 + r) * GLDS + 16 * s + 8 * h];
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) acc[i][j] = VT_MFMA(af[i], bfr[j], acc[i][j]);
+        }
+        if (kt + 1 < nk) lstore(buf ^ 1);
+        __syncthreads();
+    }
+
+    // epilogue: accumulator register q of tile (i, j): row (q&3)+8(q>>2)+4h, column r
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int64_t n = n0 + wn * WN + j * 32 + r;
+        if (n >= g.N) continue;
+        const float bias = g.bias ? g.bias[n] : 0.f;
+        float gam = 1.f;
+        if (EPI == SD_EPI_RESID && g.gamma) gam = g.gamma[n];
+        // qkv scatter coordinates of column n
+        int which = 0, head = 0, e = 0;
+        if (EPI == SD_EPI_QKV) {
+            const int C = g.heads * g.head_dim;
+            which = (int)(n / C);
+            const int rem = (int)(n - (int64_t)which * C);
+            head = rem / g.head_dim;
+            e = rem - head * g.head_dim;
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int64_t m = m0 + wm * WM + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+                if (m >= g.M) continue;
+                const float v = acc[i][j][q] + bias;
+                if (EPI == SD_EPI_BF16) {
+                    ((__bf16 *)g.out)[m * g.ldo + n] = (__bf16)v;
+                } else if (EPI == SD_EPI_GELU) {
+                    ((__bf16 *)g.out)[m * g.ldo + n] = (__bf16)vt_gelu(v);
+                } else if (EPI == SD_EPI_F32) {
+                    ((float *)g.out)[m * g.ldo + n] = v;
+                } else if (EPI == SD_EPI_RESID) {
+                    float *o = (float *)g.out + m * g.ldo + n;
+                    *o = *o + gam * v;
+                } else if (EPI == SD_EPI_QKV) {
+                    const int64_t b = m / g.tokens, t = m - b * g.tokens;
+                    const int64_t bh = b * g.heads + head;
+                    if (which == 0)
+                        ((__bf16 *)g.q)[(bh * g.tokens + t) * g.head_dim + e] = (__bf16)v;
+                    else if (which == 1)
+                        ((__bf16 *)g.k)[(bh * g.tokens_pad + t) * g.head_dim + e] = (__bf16)v;
+                    else
+                        ((__bf16 *)g.vt)[(bh * g.head_dim + e) * g.tokens_pad + t] = (__bf16)v;
+                } else {  // SD_EPI_PATCH: patch row m = b * patches + p -> token 1 + p
+                    const int64_t b = m / g.patches, p = m - b * g.patches;
+                    const int64_t tok = 1 + p;
+                    const int64_t T = g.patches + 1;
+                    ((float *)g.out)[(b * T + tok) * g.ldo + n] = v + g.pos[tok * g.N + n];
+                }
+            }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// flash attention (head_dim 64)
+// ---------------------------------------------------------------------------
+#define AT_HD 64
+
+__global__ void __launch_bounds__(256) k_attn(const __bf16 *__restrict__ Q,
+                                              const __bf16 *__restrict__ K,
+                                              const __bf16 *__restrict__ Vt, int T, int Tp,
+                                              int H, float sl2e, __bf16 *__restrict__ out) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int bh = blockIdx.y;
+    const int q0 = (blockIdx.x * 4 + wave) * 32;
+    if (q0 >= T) return;  // wave-uniform
+    const __bf16 *Qh = Q + (int64_t)bh * T * AT_HD;
+    const __bf16 *Kh = K + (int64_t)bh * Tp * AT_HD;
+    const __bf16 *Vh = Vt + (int64_t)bh * AT_HD * Tp;
+
+    // Q^T as B operand: lane (query r, half h), k-step s: Q[q][16 s + 8 h + j]
+    bf16x8 qb[AT_HD / 16];
+    {
+        const int q = q0 + r;
+#pragma unroll
+        for (int s = 0; s < AT_HD / 16; ++s) {
+            if (q < T)
+                qb[s] = *(const bf16x8 *)(Qh + (int64_t)q * AT_HD + 16 * s + 8 * h);
+            else
+#pragma unroll
+                for (int j = 0; j < 8; ++j) qb[s][j] = (__bf16)0.f;
+        }
+    }
+    f32x16 o[2];
+    o[0] = vt_zero16();
+    o[1] = vt_zero16();
+    float mrun = -INFINITY, lsum = 0.f;
+
+    for (int kb = 0; kb < Tp; kb += 64) {
+        // S^T tiles: keys kb + 32 t + row, queries on the lanes
+        f32x16 st[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            st[t] = vt_zero16();
+            const __bf16 *kr = Kh + (int64_t)(kb + 32 * t + r) * AT_HD + 8 * h;
+#pragma unroll
+            for (int s = 0; s < AT_HD / 16; ++s)
+                st[t] = VT_MFMA(*(const bf16x8 *)(kr + 16 * s), qb[s], st[t]);
+        }
+        // mask keys >= T (zero-padded rows of the last block)
+        if (kb + 64 > T) {
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int key = kb + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
+                    if (key >= T) st[t][i] = -INFINITY;
+                }
+        }
+        float mx = -INFINITY;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) mx = fmaxf(mx, st[t][i]);
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        const float mnew = fmaxf(mrun, mx * sl2e);
+        const float alpha = exp2f(mrun - mnew);
+        mrun = mnew;
+        bf16x8 pb[2][2];
+        float ps = 0.f;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const float p = exp2f(fmaf(st[t][i], sl2e, -mnew));
+                ps += p;
+                pb[t][i >> 3][i & 7] = (__bf16)p;
+            }
+        lsum = fmaf(lsum, alpha, ps);
+#pragma unroll
+        for (int ht = 0; ht < 2; ++ht)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) o[ht][i] *= alpha;
+        // O^T += V^T P: A = V^T rows (head dim), k = keys in the accumulator-operand order
+#pragma unroll
+        for (int ht = 0; ht < 2; ++ht) {
+            const __bf16 *vr = Vh + (int64_t)(32 * ht + r) * Tp + kb + 4 * h;
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    const bf16x4 lo = *(const bf16x4 *)(vr + 32 * t + 16 * s);
+                    const bf16x4 hi = *(const bf16x4 *)(vr + 32 * t + 16 * s + 8);
+                    bf16x8 a;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        a[j] = lo[j];
+                        a[4 + j] = hi[j];
+                    }
+                    o[ht] = VT_MFMA(a, pb[t][s], o[ht]);
+                }
+        }
+    }
+    const float ltot = lsum + __shfl_xor(lsum, 32);
+    const float inv = 1.f / ltot;
+    const int q = q0 + r;
+    if (q < T) {
+        const int b = bh / H, head = bh - b * H;
+        __bf16 *dst = out + ((int64_t)b * T + q) * (int64_t)(H * AT_HD) + head * AT_HD;
+#pragma unroll
+        for (int ht = 0; ht < 2; ++ht)
+#pragma unroll
+            for (int gq = 0; gq < 4; ++gq) {
+                bf16x4 v;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = (__bf16)(o[ht][4 * gq + e] * inv);
+                *(bf16x4 *)(dst + 32 * ht + 8 * gq + 4 * h) = v;
+            }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// LayerNorm (one wave per row), patchify, tokens -> grid
+// ---------------------------------------------------------------------------
+template <int PER, bool F32OUT>
+__global__ void __launch_bounds__(256) k_layernorm(const float *__restrict__ x, int64_t rows,
+                                                   int C, const float *__restrict__ w,
+                                                   const float *__restrict__ b, float eps,
+                                                   void *__restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const float *xr = x + row * C;
+    float v[PER];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int c = lane + 64 * i;
+        v[i] = c < C ? xr[c] : 0.f;
+        s += v[i];
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off);
+    const float mean = s / (float)C;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int c = lane + 64 * i;
+        const float d = c < C ? v[i] - mean : 0.f;
+        q = fmaf(d, d, q);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) q += __shfl_xor(q, off);
+    const float rstd = 1.f / sqrtf(q / (float)C + eps);
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int c = lane + 64 * i;
+        if (c < C) {
+            const float y = (v[i] - mean) * rstd * w[c] + b[c];
+            if (F32OUT)
+                ((float *)out)[row * C + c] = y;
+            else
+                ((__bf16 *)out)[row * C + c] = (__bf16)y;
+        }
+    }
+}
+
+// patches (B * Np, Kp) bf16, Kp >= 3 p p (zero-padded), column c * p * p + ky * p + kx;
+// class-token rows x[b, 0, :] = cls + pos[0].
+__global__ void __launch_bounds__(256) k_patchify(const float *__restrict__ img, int B, int Hh,
+                                                  int Ww, int p, int Kp, vf4 mean, vf4 stdv,
+                                                  __bf16 *__restrict__ patches,
+                                                  const float *__restrict__ cls,
+                                                  const float *__restrict__ pos,
+                                                  float *__restrict__ x, int C) {
+    const int gw = Ww / p, gh = Hh / p, Np = gw * gh;
+    const int64_t n_patch = (int64_t)B * Np * Kp;
+    const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (gid < n_patch) {
+        const int64_t row = gid / Kp;
+        const int col = (int)(gid - row * Kp);
+        float v = 0.f;
+        if (col < 3 * p * p) {
+            const int b = (int)(row / Np), pi = (int)(row - (int64_t)b * Np);
+            const int py = pi / gw, px = pi - py * gw;
+            const int c = col / (p * p), rem = col - c * p * p, ky = rem / p, kx = rem - ky * p;
+            const float raw = img[(((int64_t)b * 3 + c) * Hh + py * p + ky) * Ww + px * p + kx];
+            // torchvision Normalize(mean, std)(x / 2 + 0.5): (t - mean) / std
+            v = ((raw / 2.f + 0.5f) - mean[c]) / stdv[c];
+        }
+        patches[gid] = (__bf16)v;
+    } else if (gid < n_patch + (int64_t)B * C) {
+        const int64_t k = gid - n_patch;
+        const int b = (int)(k / C), c = (int)(k - (int64_t)b * C);
+        x[((int64_t)b * (Np + 1)) * C + c] = cls[c] + pos[c];
+    }
+}
+
+__global__ void __launch_bounds__(256) k_tokens_to_grid(const float *__restrict__ x, int B, int T,
+                                                        int C, int n_prefix, int gh, int gw,
+                                                        int l2, float *__restrict__ out) {
+    // one wave per output token: read C channels (coalesced), optional L2 norm, write planes
+    const int lane = threadIdx.x & 63;
+    const int64_t tok = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t n_tok = (int64_t)B * gh * gw;
+    if (tok >= n_tok) return;
+    const int b = (int)(tok / (gh * gw)), pi = (int)(tok - (int64_t)b * gh * gw);
+    const float *xr = x + ((int64_t)b * T + n_prefix + pi) * C;
+    float scale = 1.f;
+    if (l2) {
+        float s = 0.f;
+        for (int c = lane; c < C; c += 64) s = fmaf(xr[c], xr[c], s);
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off);
+        // F.normalize(p=2, eps=1e-12) applied twice (vit.py:188, dinov2_module.py:282):
+        // the second pass divides a unit vector by its own norm
+        const float n1 = fmaxf(sqrtf(s), 1e-12f);
+        scale = 1.f / n1;
+    }
+    for (int c = lane; c < C; c += 64)
+        out[(((int64_t)b * C + c) * gh) * gw + pi] = xr[c] * scale;
+}
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+template <int BM, int BN>
+static void vt_launch_gemm(const sd_gemm_args &g, hipStream_t s) {
+    dim3 grid((unsigned)((g.N + BN - 1) / BN), (unsigned)((g.M + BM - 1) / BM));
+    switch (g.epi) {
+    case SD_EPI_BF16: hipLaunchKernelGGL((k_gemm<BM, BN, SD_EPI_BF16>), grid, dim3(256), 0, s, g); break;
+    case SD_EPI_GELU: hipLaunchKernelGGL((k_gemm<BM, BN, SD_EPI_GELU>), grid, dim3(256), 0, s, g); break;
+    case SD_EPI_F32: hipLaunchKernelGGL((k_gemm<BM, BN, SD_EPI_F32>), grid, dim3(256), 0, s, g); break;
+    case SD_EPI_RESID: hipLaunchKernelGGL((k_gemm<BM, BN, SD_EPI_RESID>), grid, dim3(256), 0, s, g); break;
+    case SD_EPI_QKV: hipLaunchKernelGGL((k_gemm<BM, BN, SD_EPI_QKV>), grid, dim3(256), 0, s, g); break;
+    default: hipLaunchKernelGGL((k_gemm<BM, BN, SD_EPI_PATCH>), grid, dim3(256), 0, s, g); break;
+    }
+}
+
+extern "C" int sd_gemm(const sd_gemm_args *args, void *stream) {
+    if (!args) {
+        sd_set_error("sd_gemm: null args");
+        return -1;
+    }
+    const sd_gemm_args &g = *args;
+    bool ok = g.a && g.w && g.M >= 0 && g.N > 0 && g.K > 0 && g.K % GK == 0 && g.lda >= g.K &&
+              g.lda % 8 == 0 && g.epi >= SD_EPI_BF16 && g.epi <= SD_EPI_PATCH &&
+              g.M * (int64_t)g.lda < ((int64_t)1 << 40);
+    if (g.epi == SD_EPI_QKV)
+        ok = ok && g.q && g.k && g.vt && g.head_dim > 0 && g.heads > 0 && g.tokens > 0 &&
+             g.tokens_pad >= g.tokens && g.N == 3LL * g.heads * g.head_dim &&
+             g.M % g.tokens == 0;
+    else if (g.epi == SD_EPI_PATCH)
+        ok = ok && g.out && g.pos && g.patches > 0 && g.M % g.patches == 0 && g.ldo >= g.N;
+    else
+        ok = ok && g.out && g.ldo >= g.N;
+    if (!ok) {
+        sd_set_error("sd_gemm: invalid argument (K % 32 == 0, lda >= K and lda % 8 == 0, "
+                     "epilogue fields)");
+        return -1;
+    }
+    if (g.M == 0) return 0;
+    hipStream_t s = (hipStream_t)stream;
+    // 128x128 tiles once they fill the chip, else 64x64 (ViT-S-sized token counts)
+    const int64_t big = ((g.M + 127) / 128) * ((g.N + 127) / 128);
+    if (big >= 256)
+        vt_launch_gemm<128, 128>(g, s);
+    else
+        vt_launch_gemm<64, 64>(g, s);
+    if (hipGetLastError() != hipSuccess) {
+        sd_set_error("sd_gemm: launch failed");
+        return -2;
+    }
+    return 0;
+}
+
+extern "C" int sd_attention(const void *q, const void *k, const void *vt, int32_t B,
+                            int32_t heads, int32_t tokens, int32_t tokens_pad, int32_t head_dim,
+                            float scale, void *out, void *stream) {
+    if (!q || !k || !vt || !out || B <= 0 || heads <= 0 || tokens <= 0 || head_dim != AT_HD ||
+        tokens_pad < tokens || tokens_pad % 64 || (int64_t)B * heads > 65535) {
+        sd_set_error("sd_attention: invalid argument (head_dim 64, tokens_pad % 64 == 0)");
+        return -1;
+    }
+    dim3 grid((unsigned)((tokens + 127) / 128), (unsigned)(B * heads));
+    hipLaunchKernelGGL(k_attn, grid, dim3(256), 0, (hipStream_t)stream, (const __bf16 *)q,
+                       (const __bf16 *)k, (const __bf16 *)vt, tokens, tokens_pad, heads,
+                       scale * 1.4426950408889634f, (__bf16 *)out);
+    if (hipGetLastError() != hipSuccess) {
+        sd_set_error("sd_attention: launch failed");
+        return -2;
+    }
+    return 0;
+}
+
+extern "C" int sd_layernorm(const float *x, int64_t rows, int32_t C, const float *w,
+                            const float *b, float eps, void *out, int32_t out_f32,
+                            void *stream) {
+    if (!x || !w || !b || !out || rows < 0 || C <= 0 || C > 1024) {
+        sd_set_error("sd_layernorm: invalid argument (C <= 1024)");
+        return -1;
+    }
+    if (rows == 0) return 0;
+    dim3 grid((unsigned)((rows + 3) / 4));
+    hipStream_t s = (hipStream_t)stream;
+#define SD_LN(PER)                                                                          \
+    do {                                                                                    \
+        if (out_f32)                                                                        \
+            hipLaunchKernelGGL((k_layernorm<PER, true>), grid, dim3(256), 0, s, x, rows, C, w, \
+                               b, eps, out);                                                \
+        else                                                                                \
+            hipLaunchKernelGGL((k_layernorm<PER, false>), grid, dim3(256), 0, s, x, rows, C,   \
+                               w, b, eps, out);                                             \
+    } while (0)
+    if (C <= 384)
+        SD_LN(6);
+    else if (C <= 768)
+        SD_LN(12);
+    else
+        SD_LN(16);
+#undef SD_LN
+    if (hipGetLastError() != hipSuccess) {
+        sd_set_error("sd_layernorm: launch failed");
+        return -2;
+    }
+    return 0;
+}
+
+extern "C" int sd_patchify(const float *img, int32_t B, int32_t H, int32_t W, int32_t p,
+                           int32_t Kp, const float *mean3, const float *std3, void *patches,
+                           const float *cls, const float *pos, float *x, int32_t C, void *stream) {
+    if (!img || !mean3 || !std3 || !patches || !cls || !pos || !x || B <= 0 || p <= 0 ||
+        H % p || W % p || Kp < 3 * p * p || C <= 0) {
+        sd_set_error("sd_patchify: invalid argument (H, W multiples of the patch size)");
+        return -1;
+    }
+    vf4 mean, stdv;
+    for (int c = 0; c < 3; ++c) {
+        mean[c] = mean3[c];
+        stdv[c] = std3[c];
+    }
+    mean[3] = 0.f;
+    stdv[3] = 1.f;
+    const int64_t Np = (int64_t)(H / p) * (W / p);
+    const int64_t n = (int64_t)B * Np * Kp + (int64_t)B * C;
+    hipLaunchKernelGGL(k_patchify, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, img, B, H, W, p, Kp, mean, stdv, (__bf16 *)patches,
+                       cls, pos, x, C);
+    if (hipGetLastError() != hipSuccess) {
+        sd_set_error("sd_patchify: launch failed");
+        return -2;
+    }
+    return 0;
+}
+
+extern "C" int sd_tokens_to_grid(const float *x, int32_t B, int32_t T, int32_t C,
+                                 int32_t n_prefix, int32_t gh, int32_t gw, int32_t l2norm,
+                                 float *out, void *stream) {
+    if (!x || !out || B <= 0 || C <= 0 || n_prefix < 0 || gh <= 0 || gw <= 0 ||
+        (int64_t)n_prefix + (int64_t)gh * gw > T) {
+        sd_set_error("sd_tokens_to_grid: invalid argument");
+        return -1;
+    }
+    const int64_t n = (int64_t)B * gh * gw;
+    hipLaunchKernelGGL(k_tokens_to_grid, dim3((unsigned)((n + 3) / 4)), dim3(256), 0,
+                       (hipStream_t)stream, x, B, T, C, n_prefix, gh, gw, l2norm, out);
+    if (hipGetLastError() != hipSuccess) {
+        sd_set_error("sd_tokens_to_grid: launch failed");
+        return -2;
+    }
+    return 0;
+}

@@ -1,0 +1,204 @@
+"""ViT encoder: DINO / DINOv2 blocks on gfx950 MFMA.
+
+timm is absent here and unpinned by the reference, so parity is pinned to
+oracle/vit_oracle.py (PyTorch fp32 restatement of timm's VisionTransformer as the
+reference runs it) on random weights -- "parity unpinned" against reference fixtures.
+
+Tolerances (written here):
+  * sd_gemm (bf16 operands, fp32 accumulate): vs fp32 matmul of the same bf16 operands,
+    max |d| <= 1e-3 * sqrt(K) * max|ref| scale for f32 epilogues; bf16 outputs add one bf16
+    rounding (rel 2^-8).
+  * sd_attention: vs fp32 softmax attention of the same bf16 q, k, v: max |d| <= 2e-2.
+  * sd_layernorm: vs F.layer_norm, bf16 output: max |d| <= 2e-2 (|y| ~ 1).
+  * full encoder (12 blocks, bf16 activations, fp32 residual stream): per output grid
+    rel-L2 <= 3e-2 against the fp32 oracle.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import vit_oracle as VO
+
+
+def init_vit(vit, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for name, p in vit.named_parameters():
+            if name.endswith("gamma"):
+                p.copy_(0.5 + 0.2 * torch.rand(p.shape, generator=g))
+            elif "norm" in name and name.endswith("weight"):
+                p.copy_(1 + 0.1 * torch.randn(p.shape, generator=g))
+            elif name.endswith("bias"):
+                p.copy_(0.02 * torch.randn(p.shape, generator=g))
+            elif name in ("cls_token", "pos_embed"):
+                p.copy_(0.3 * torch.randn(p.shape, generator=g))
+            else:
+                fan_in = p[0].numel()
+                p.copy_(torch.randn(p.shape, generator=g) / math.sqrt(fan_in))
+    return vit
+
+
+def test_state_dict_keys_follow_timm_names():
+    from scenedino_amd.models.backbones.dino.vit import DINOv2Encoder
+    enc = DINOv2Encoder("vit-s", (192, 640), [3, 6, 9], False, "v2")
+    keys = set(enc.state_dict())
+    for k in ("model.vit.cls_token", "model.vit.pos_embed", "model.vit.patch_embed.proj.weight",
+              "model.vit.blocks.0.norm1.weight", "model.vit.blocks.0.attn.qkv.weight",
+              "model.vit.blocks.0.attn.qkv.bias", "model.vit.blocks.0.attn.proj.bias",
+              "model.vit.blocks.0.ls1.gamma", "model.vit.blocks.11.mlp.fc1.weight",
+              "model.vit.blocks.11.mlp.fc2.bias", "model.vit.blocks.11.ls2.gamma",
+              "model.vit.norm.weight"):
+        assert k in keys, k
+    assert enc.model.vit.pos_embed.shape == (1, 12 * 40 + 1, 384)  # 168x560 / 14
+    e1 = DINOv2Encoder("vit-b", (192, 640), [3, 6, 9], False, "v1")
+    assert e1.model.vit.pos_embed.shape == (1, 24 * 80 + 1, 768)
+    assert "model.vit.blocks.0.ls1.gamma" not in set(e1.state_dict())
+
+
+def test_oracle_shapes_and_normalisation():
+    from scenedino_amd.models.backbones.dino.vit import VisionTransformer
+    vit = init_vit(VisionTransformer((32, 64), 16, 384, 2, 6))
+    out = VO.encoder_forward(vit, torch.rand(2, 3, 32, 64) * 2 - 1, [0])
+    assert [tuple(o.shape) for o in out] == [(2, 384, 2, 4), (2, 384, 2, 4)]
+    assert torch.allclose(out[-1].norm(dim=1), torch.ones(2, 2, 4), atol=1e-5)
+
+
+# ------------------------------------------------------------------------ GPU
+@pytest.fixture(scope="module")
+def gpu():
+    assert torch.cuda.is_available(), "GPU tests need a ROCm device"
+    from scenedino_amd import _lib
+    _lib.load()
+    return "cuda"
+
+
+def _bf(t):
+    return t.to(torch.bfloat16)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(481, 1152, 384), (77, 96, 64), (1921, 768, 3072),
+                                   (4096, 1024, 256)])
+def test_gemm_epilogues(gpu, M, N, K):
+    from scenedino_amd import _lib
+    g = torch.Generator().manual_seed(M + N)
+    a = _bf(torch.randn(M, K, generator=g)).to(gpu)
+    w = _bf(torch.randn(N, K, generator=g) / math.sqrt(K)).to(gpu)
+    bias = (0.1 * torch.randn(N, generator=g)).to(gpu)
+    ref = a.float() @ w.float().t() + bias
+    scale = ref.abs().max().item()
+    out = torch.empty(M, N, device=gpu)
+    _lib.gemm(a, w, bias, _lib.SD_EPI_F32, out=out)
+    assert (out - ref).abs().max().item() <= 1e-4 * scale + 1e-5
+    ob = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    _lib.gemm(a, w, bias, _lib.SD_EPI_BF16, out=ob)
+    assert (ob.float() - ref).abs().max().item() <= 8e-3 * scale
+    _lib.gemm(a, w, bias, _lib.SD_EPI_GELU, out=ob)
+    assert (ob.float() - F.gelu(ref)).abs().max().item() <= 8e-3 * scale
+    res = torch.randn(M, N, generator=g).to(gpu)
+    gam = torch.rand(N, generator=g).to(gpu)
+    x = res.clone()
+    _lib.gemm(a, w, bias, _lib.SD_EPI_RESID, out=x, gamma=gam)
+    assert (x - (res + gam * ref)).abs().max().item() <= 1e-4 * scale + 1e-5
+    x = res.clone()
+    _lib.gemm(a, w, None, _lib.SD_EPI_RESID, out=x)
+    assert (x - (res + ref - bias)).abs().max().item() <= 1e-4 * scale + 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,H,T", [(1, 6, 481), (2, 12, 77), (1, 12, 1921), (1, 1, 1)])
+def test_qkv_scatter_and_attention(gpu, B, H, T):
+    from scenedino_amd import _lib
+    g = torch.Generator().manual_seed(T)
+    C = 64 * H
+    xn = _bf(torch.randn(B * T, C, generator=g)).to(gpu)
+    w = _bf(torch.randn(3 * C, C, generator=g) / math.sqrt(C)).to(gpu)
+    b = (0.1 * torch.randn(3 * C, generator=g)).to(gpu)
+    Tp = (T + 63) // 64 * 64
+    q = torch.empty(B, H, T, 64, device=gpu, dtype=torch.bfloat16)
+    k = torch.zeros(B, H, Tp, 64, device=gpu, dtype=torch.bfloat16)
+    vt = torch.zeros(B, H, 64, Tp, device=gpu, dtype=torch.bfloat16)
+    _lib.gemm(xn, w, b, _lib.SD_EPI_QKV, qkv=(q, k, vt), tokens=T, heads=H)
+    qkv = torch.empty(B * T, 3 * C, device=gpu, dtype=torch.bfloat16)
+    _lib.gemm(xn, w, b, _lib.SD_EPI_BF16, out=qkv)
+    r = qkv.view(B, T, 3, H, 64).permute(2, 0, 3, 1, 4)
+    assert torch.equal(q, r[0])
+    assert torch.equal(k[:, :, :T], r[1])
+    assert torch.equal(vt[..., :T], r[2].transpose(-1, -2))
+    assert not k[:, :, T:].any() and not vt[..., T:].any()
+    out = torch.empty(B * T, C, device=gpu, dtype=torch.bfloat16)
+    _lib.attention(q, k, vt, 64 ** -0.5, out)
+    att = ((r[0].float() * 64 ** -0.5) @ r[1].float().transpose(-1, -2)).softmax(-1)
+    ref = (att @ r[2].float()).transpose(1, 2).reshape(B * T, C)
+    assert (out.float() - ref).abs().max().item() <= 2e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C", [384, 768])
+def test_layernorm(gpu, C):
+    from scenedino_amd import _lib
+    g = torch.Generator().manual_seed(C)
+    x = (3 * torch.randn(333, C, generator=g) + 1).to(gpu)
+    w = (1 + 0.1 * torch.randn(C, generator=g)).to(gpu)
+    b = (0.1 * torch.randn(C, generator=g)).to(gpu)
+    ref = F.layer_norm(x, (C,), w, b, 1e-6)
+    ob = torch.empty(333, C, device=gpu, dtype=torch.bfloat16)
+    _lib.layernorm(x, w, b, 1e-6, ob)
+    assert (ob.float() - ref).abs().max().item() <= 2e-2
+    of = torch.empty(333, C, device=gpu)
+    _lib.layernorm(x, w, b, 1e-6, of)
+    assert (of - ref).abs().max().item() <= 1e-4
+
+
+def _encoder_check(enc, images, tol=3e-2):
+    dev = images.device
+    with torch.no_grad():
+        got = enc(images)
+    vit = enc.model.vit.cpu()
+    x = images.cpu()
+    if getattr(enc, "resize", None) is not None:
+        x = F.interpolate(x, size=enc.resize, mode="bilinear", align_corners=False, antialias=True)
+    ref = VO.encoder_forward(vit, x, enc.model.intermediate)
+    enc.to(dev)
+    assert len(got) == len(ref)
+    for i, (a, r) in enumerate(zip(got, ref)):
+        assert a.shape == r.shape, (i, a.shape, r.shape)
+        rel = ((a.double().cpu() - r.double()).norm() / r.double().norm()).item()
+        assert rel <= tol, f"output {i}: rel-L2 {rel:.3g}"
+
+
+@pytest.mark.gpu
+def test_encoder_vit_s16_192x640_vs_oracle(gpu):
+    from scenedino_amd.models.backbones.dino.vit import DINOv2Encoder
+    enc = DINOv2Encoder("vit-s", (192, 640), [3, 6, 9], False, "v1_16")
+    init_vit(enc.model.vit, 1)
+    enc = enc.to(gpu).eval()
+    img = (torch.rand(1, 3, 192, 640, generator=torch.Generator().manual_seed(2)) * 2 - 1).to(gpu)
+    _encoder_check(enc, img)
+
+
+@pytest.mark.gpu
+def test_encoder_dinov2_b14_layerscale_resize_vs_oracle(gpu):
+    from scenedino_amd.models.backbones.dino.vit import DINOv2Encoder
+    enc = DINOv2Encoder("vit-b", (64, 224), [3, 6, 9], False, "v2")
+    init_vit(enc.model.vit, 3)
+    enc = enc.to(gpu).eval()
+    img = (torch.rand(2, 3, 64, 224, generator=torch.Generator().manual_seed(4)) * 2 - 1).to(gpu)
+    _encoder_check(enc, img)
+
+
+@pytest.mark.gpu
+def test_encoder_vit_b8_1921_tokens_two_blocks(gpu):
+    from scenedino_amd.models.backbones.dino.vit import VisionTransformer, _ViT
+    vit = init_vit(VisionTransformer((192, 640), 8, 768, 2, 12), 5)
+    m = _ViT(vit, 8, intermediate_features=[0]).to(gpu).eval()
+    img = (torch.rand(1, 3, 192, 640, generator=torch.Generator().manual_seed(6)) * 2 - 1).to(gpu)
+    with torch.no_grad():
+        grids, final = m.forward_grids(img)
+    ref = VO.encoder_forward(vit.cpu(), img.cpu(), [0])
+    for a, r in zip(grids + [final], ref):
+        rel = ((a.double().cpu() - r.double()).norm() / r.double().norm()).item()
+        assert rel <= 3e-2, rel
