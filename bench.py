@@ -268,6 +268,53 @@ def main_c5(args, world, rank, local_rank, dist, device):
         print(json.dumps(line), flush=True)
 
 
+def vit_flops(T, C, L, p, Np, mlp=4):
+    """Algorithmic FLOPs of one ViT pass: per block qkv + proj + MLP GEMMs and the two
+    attention products (L T (24 C^2 + 4 T C) at mlp ratio 4), + patch embed."""
+    return L * T * (2 * C * 3 * C + 2 * C * C + 2 * 2 * C * mlp * C + 4 * T * C) + 2 * Np * 3 * p * p * C
+
+
+def main_vit(args, world, rank, device):
+    """a19: the DINO encoder's ViT forward (DINOv2Encoder -> _ViT) on one 192x640 frame:
+    ViT-S/16 (481 tokens, BASELINE configs[1]) and ViT-B/8 (1921 tokens, the released
+    SceneDINO checkpoints), random weights.  Timed: patchify + 12 blocks + final norm +
+    token grids, all libsdhip.so kernels."""
+    from scenedino_amd.models.backbones.dino.vit import DINOv2Encoder
+    results = {}
+    for name, (arch, ver) in {"vit-s16": ("vit-s", "v1_16"), "vit-b8": ("vit-b", "v1")}.items():
+        torch.manual_seed(0)
+        enc = DINOv2Encoder(arch, (H, W), [3, 6, 9], False, ver).to(device).eval()
+        img = (torch.rand(1, 3, H, W, generator=torch.Generator().manual_seed(rank)) * 2 - 1).to(device)
+        with torch.no_grad():
+            for _ in range(args.warmup):
+                enc(img)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                enc(img)
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / args.steps
+        vit = enc.model.vit
+        p, C = vit.patch_size, vit.embed_dim
+        Np = (H // p) * (W // p)
+        fl = vit_flops(Np + 1, C, len(vit.blocks), p, Np)
+        results[name] = {"ms_per_pass": dt * 1e3, "tokens": Np + 1, "dim": C,
+                         "gflop_per_pass": fl / 1e9, "tflops": fl / dt / 1e12,
+                         "frac_bf16_peak": fl / dt / 1e12 / PEAK_TFLOPS["bf16"]}
+    if rank == 0:
+        print(json.dumps({
+            "metric": "DINO ViT encoder passes/sec (192x640 frame, 12 blocks)",
+            "value": 1e3 / results["vit-s16"]["ms_per_pass"], "unit": "passes/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "higher_is_better": True, "dtype": "bf16", "data": "synthetic, random weights",
+            "config": {"workload": "a19 ViT encoder forward (DINOv2Encoder, no DPT decoder)"},
+            "models": results,
+            "roofline": {"kernel": "k_gemm + k_attn (ViT-B/8)", "bound": "mfma",
+                         "achieved": results["vit-b8"]["tflops"], "peak": PEAK_TFLOPS["bf16"],
+                         "unit": "TFLOP/s", "frac": results["vit-b8"]["frac_bf16_peak"]},
+        }), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -278,10 +325,11 @@ def main():
     ap.add_argument("--mode", default="proj", choices=["proj", "grid"],
                     help="16-bit render kernel: projected grid (default) or per-sample grid")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--config", default="c2", choices=["c2", "c4", "c5"],
+    ap.add_argument("--config", default="c2", choices=["c2", "c4", "c5", "vit"],
                     help="c2: BASELINE configs[1] (K=64, D=64, the metric's config); c4: "
                          "configs[3] render shape (K=128, 384-d feature field); c5: "
-                         "configs[4] SSCBench voxel query (voxels/s)")
+                         "configs[4] SSCBench voxel query (voxels/s); vit: the DINO ViT "
+                         "encoder forward (a19)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     args = ap.parse_args()
     global K_SAMPLES, D_DINO
@@ -300,8 +348,11 @@ def main():
 
     from scenedino_amd import _lib
     _lib.load()
-    if args.config == "c5":
-        main_c5(args, world, rank, local_rank, dist, device)
+    if args.config in ("c5", "vit"):
+        if args.config == "c5":
+            main_c5(args, world, rank, local_rank, dist, device)
+        else:
+            main_vit(args, world, rank, device)
         if dist:
             tdist.barrier()
             tdist.destroy_process_group()

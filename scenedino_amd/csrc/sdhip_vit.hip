@@ -191,11 +191,16 @@ __global__ void __launch_bounds__(256) k_attn(const __bf16 *__restrict__ Q,
                                               const __bf16 *__restrict__ K,
                                               const __bf16 *__restrict__ Vt, int T, int Tp,
                                               int H, float sl2e, __bf16 *__restrict__ out) {
+    // One workgroup = 32 queries of one (batch, head); its 4 waves split the 64-key blocks
+    // (wave w takes blocks w, w+4, ...), each keeping its own running (max, sum, O^T), and
+    // combine them through LDS at the end (a batch-1 ViT-B/8 has only 12 heads x 61 query
+    // tiles: without the split, fewer waves than SIMDs).
+    __shared__ float s_o[4][2][16][64];  // [wave][hd tile][acc register][lane]
+    __shared__ float s_m[4][64], s_l[4][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int r = lane & 31, h = lane >> 5;
     const int bh = blockIdx.y;
-    const int q0 = (blockIdx.x * 4 + wave) * 32;
-    if (q0 >= T) return;  // wave-uniform
+    const int q0 = blockIdx.x * 32;
     const __bf16 *Qh = Q + (int64_t)bh * T * AT_HD;
     const __bf16 *Kh = K + (int64_t)bh * Tp * AT_HD;
     const __bf16 *Vh = Vt + (int64_t)bh * AT_HD * Tp;
@@ -218,7 +223,7 @@ __global__ void __launch_bounds__(256) k_attn(const __bf16 *__restrict__ Q,
     o[1] = vt_zero16();
     float mrun = -INFINITY, lsum = 0.f;
 
-    for (int kb = 0; kb < Tp; kb += 64) {
+    for (int kb = 64 * wave; kb < Tp; kb += 256) {
         // S^T tiles: keys kb + 32 t + row, queries on the lanes
         f32x16 st[2];
 #pragma unroll
@@ -228,6 +233,24 @@ __global__ void __launch_bounds__(256) k_attn(const __bf16 *__restrict__ Q,
 #pragma unroll
             for (int s = 0; s < AT_HD / 16; ++s)
                 st[t] = VT_MFMA(*(const bf16x8 *)(kr + 16 * s), qb[s], st[t]);
+        }
+        // V^T fragments of this block, issued before the softmax so they land under it
+        bf16x8 va[2][2][2];
+#pragma unroll
+        for (int ht = 0; ht < 2; ++ht) {
+            const __bf16 *vr = Vh + (int64_t)(32 * ht + r) * Tp + kb + 4 * h;
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    const bf16x4 lo = *(const bf16x4 *)(vr + 32 * t + 16 * s);
+                    const bf16x4 hi = *(const bf16x4 *)(vr + 32 * t + 16 * s + 8);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        va[ht][t][s][j] = lo[j];
+                        va[ht][t][s][4 + j] = hi[j];
+                    }
+                }
         }
         // mask keys >= T (zero-padded rows of the last block)
         if (kb + 64 > T) {
@@ -265,39 +288,49 @@ __global__ void __launch_bounds__(256) k_attn(const __bf16 *__restrict__ Q,
             for (int i = 0; i < 16; ++i) o[ht][i] *= alpha;
         // O^T += V^T P: A = V^T rows (head dim), k = keys in the accumulator-operand order
 #pragma unroll
-        for (int ht = 0; ht < 2; ++ht) {
-            const __bf16 *vr = Vh + (int64_t)(32 * ht + r) * Tp + kb + 4 * h;
+        for (int ht = 0; ht < 2; ++ht)
 #pragma unroll
             for (int t = 0; t < 2; ++t)
 #pragma unroll
-                for (int s = 0; s < 2; ++s) {
-                    const bf16x4 lo = *(const bf16x4 *)(vr + 32 * t + 16 * s);
-                    const bf16x4 hi = *(const bf16x4 *)(vr + 32 * t + 16 * s + 8);
-                    bf16x8 a;
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        a[j] = lo[j];
-                        a[4 + j] = hi[j];
-                    }
-                    o[ht] = VT_MFMA(a, pb[t][s], o[ht]);
-                }
-        }
+                for (int s = 0; s < 2; ++s) o[ht] = VT_MFMA(va[ht][t][s], pb[t][s], o[ht]);
     }
-    const float ltot = lsum + __shfl_xor(lsum, 32);
-    const float inv = 1.f / ltot;
+    // combine the 4 waves' partial softmax states
+    s_m[wave][lane] = mrun;          // identical in both halves
+    s_l[wave][lane] = lsum;          // per-half partial sums
+#pragma unroll
+    for (int ht = 0; ht < 2; ++ht)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s_o[wave][ht][i][lane] = o[ht][i];
+    __syncthreads();
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) M = fmaxf(M, s_m[w][lane]);
+    float fw[4], L = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const float mw = s_m[w][lane];
+        fw[w] = mw == -INFINITY ? 0.f : exp2f(mw - M);  // a wave with no key block
+        L = fmaf(fw[w], s_l[w][r] + s_l[w][r + 32], L);
+    }
+    const float inv = 1.f / L;
     const int q = q0 + r;
     if (q < T) {
+        // wave w writes accumulator registers 4w..4w+3 of both head-dim tiles:
+        // rows 32 ht + 8 w + 4 h + e (4 contiguous head-dim values, one 8-B store)
         const int b = bh / H, head = bh - b * H;
         __bf16 *dst = out + ((int64_t)b * T + q) * (int64_t)(H * AT_HD) + head * AT_HD;
 #pragma unroll
-        for (int ht = 0; ht < 2; ++ht)
+        for (int ht = 0; ht < 2; ++ht) {
+            bf16x4 v;
 #pragma unroll
-            for (int gq = 0; gq < 4; ++gq) {
-                bf16x4 v;
+            for (int e = 0; e < 4; ++e) {
+                float acc = 0.f;
 #pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = (__bf16)(o[ht][4 * gq + e] * inv);
-                *(bf16x4 *)(dst + 32 * ht + 8 * gq + 4 * h) = v;
+                for (int w = 0; w < 4; ++w) acc = fmaf(fw[w], s_o[w][ht][4 * wave + e][lane], acc);
+                v[e] = (__bf16)(acc * inv);
             }
+            *(bf16x4 *)(dst + 32 * ht + 8 * wave + 4 * h) = v;
+        }
     }
 }
 
@@ -464,7 +497,7 @@ extern "C" int sd_attention(const void *q, const void *k, const void *vt, int32_
         sd_set_error("sd_attention: invalid argument (head_dim 64, tokens_pad % 64 == 0)");
         return -1;
     }
-    dim3 grid((unsigned)((tokens + 127) / 128), (unsigned)(B * heads));
+    dim3 grid((unsigned)((tokens + 31) / 32), (unsigned)(B * heads));
     hipLaunchKernelGGL(k_attn, grid, dim3(256), 0, (hipStream_t)stream, (const __bf16 *)q,
                        (const __bf16 *)k, (const __bf16 *)vt, tokens, tokens_pad, heads,
                        scale * 1.4426950408889634f, (__bf16 *)out);
