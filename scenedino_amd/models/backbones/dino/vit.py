@@ -127,7 +127,7 @@ def _param_key(m: nn.Module):
 
 
 def vit_forward(vit: VisionTransformer, images: torch.Tensor, packed: _Packed,
-                intermediate: List[int], kernel_timer=None):
+                intermediate: List[int]):
     """images (B, 3, H, W) in [-1, 1] (DINOv2Encoder input, before _normalize_input) ->
     (intermediate block outputs as (B, C, gh, gw) grids, final-norm tokens L2-normalised as
     a grid).  Every arithmetic step is a libsdhip.so kernel."""
@@ -197,7 +197,8 @@ class _ViT(nn.Module):
         self.intermediate = list(intermediate_features or [])
         self.vit = vit
         self._packed = None
-        self.kernel_timer = None
+        self._graph = None
+        self.use_graph = True
 
     def packed(self):
         key = _param_key(self.vit)
@@ -206,8 +207,30 @@ class _ViT(nn.Module):
         return self._packed[1]
 
     def forward_grids(self, images_pm1):
-        return vit_forward(self.vit, images_pm1, self.packed(), self.intermediate,
-                           self.kernel_timer)
+        """HIP-graph replay of the whole encoder (patchify, 12 x 7 kernels, final norm,
+        grids): captured once per (input shape, parameter version), then replayed -- the
+        ~90 launches of a pass cost one graph launch.  ``use_graph = False`` launches
+        eagerly."""
+        if not self.use_graph or not images_pm1.is_cuda:
+            return vit_forward(self.vit, images_pm1, self.packed(), self.intermediate)
+        key = (tuple(images_pm1.shape), str(images_pm1.device), _param_key(self.vit))
+        if self._graph is None or self._graph[0] != key:
+            self._graph = None
+            packed = self.packed()
+            static_in = images_pm1.detach().float().contiguous().clone()
+            side = torch.cuda.Stream(device=images_pm1.device)
+            side.wait_stream(torch.cuda.current_stream(images_pm1.device))
+            with torch.cuda.stream(side):  # warm-up outside the capture
+                vit_forward(self.vit, static_in, packed, self.intermediate)
+            torch.cuda.current_stream(images_pm1.device).wait_stream(side)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                outs = vit_forward(self.vit, static_in, packed, self.intermediate)
+            self._graph = (key, graph, static_in, outs)
+        _, graph, static_in, (grids, final) = self._graph
+        static_in.copy_(images_pm1)
+        graph.replay()
+        return [g.clone() for g in grids], final.clone()
 
     def forward(self, images_pm1) -> Dict[str, torch.Tensor]:
         grids, final = self.forward_grids(images_pm1)

@@ -202,3 +202,21 @@ def test_encoder_vit_b8_1921_tokens_two_blocks(gpu):
     for a, r in zip(grids + [final], ref):
         rel = ((a.double().cpu() - r.double()).norm() / r.double().norm()).item()
         assert rel <= 3e-2, rel
+
+
+@pytest.mark.gpu
+def test_graph_replay_matches_eager(gpu):
+    from scenedino_amd.models.backbones.dino.vit import DINOv2Encoder
+    enc = DINOv2Encoder("vit-s", (64, 160), [3, 6, 9], False, "v1_16")
+    init_vit(enc.model.vit, 7)
+    enc = enc.to(gpu).eval()
+    g = torch.Generator().manual_seed(8)
+    imgs = [(torch.rand(1, 3, 64, 160, generator=g) * 2 - 1).to(gpu) for _ in range(3)]
+    with torch.no_grad():
+        enc.model.use_graph = False
+        eager = [enc(x) for x in imgs]
+        enc.model.use_graph = True
+        graph = [enc(x) for x in imgs]  # capture on the first, replay on the others
+    for e, gr in zip(eager, graph):
+        for a, b in zip(e, gr):
+            assert torch.equal(a, b)
