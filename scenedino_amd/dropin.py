@@ -56,3 +56,16 @@ def install():
 
     rs = importlib.import_module("scenedino.common.ray_sampler")
     rs.ImageRaySampler = amd_rs.ImageRaySampler
+
+    # The DINO / DINOv2 ViT of the encoder (dinov2_module.py:19-28 build_encoder looks
+    # DINOv2Encoder up at call time): same parameter names (model.vit.*), gfx950 kernels,
+    # no hub download -- the weights come from checkpoint.pt.  The DPT decoder, the
+    # downsampler and the dimension reduction stay the reference's modules (BTSNet reads
+    # dim_reduction's parameters for the fused sd_seg_query head).
+    try:
+        dm = importlib.import_module("scenedino.models.backbones.dino.dinov2_module")
+    except ImportError:  # the reference's encoder dependencies (timm, torchvision) absent
+        dm = None
+    if dm is not None:
+        from .models.backbones.dino import vit as amd_vit
+        dm.DINOv2Encoder = amd_vit.DINOv2Encoder
