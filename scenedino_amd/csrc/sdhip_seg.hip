@@ -175,17 +175,25 @@ __global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const float *__restr
 #pragma unroll
         for (int ct = 0; ct < SG_NT; ++ct) ss[ct] = 0.f;
         const bf16x8 *w2 = (const bf16x8 *)h.w2;
+        // software pipeline: the fragments and bias rows of tile t + 1 are loaded while
+        // tile t runs on the matrix cores (one wave per SIMD: no other wave hides L2)
+        bf16x8 cur[SG_DL / 16];
+        f32x16 bb = sg_rows(h.b2, 0, hh);
+#pragma unroll
+        for (int q = 0; q < SG_DL / 16; ++q) cur[q] = w2[q * 64 + lane];
         for (int t = 0; t < T2; ++t) {
+            const int tn = t + 1 < T2 ? t + 1 : t;
+            bf16x8 nxt[SG_DL / 16];
+#pragma unroll
+            for (int q = 0; q < SG_DL / 16; ++q) nxt[q] = w2[(tn * (SG_DL / 16) + q) * 64 + lane];
+            const f32x16 bbn = sg_rows(h.b2, tn, hh);
             f32x16 acc[SG_NT];
 #pragma unroll
             for (int ct = 0; ct < SG_NT; ++ct) acc[ct] = sg_zero16();
 #pragma unroll
-            for (int q = 0; q < SG_DL / 16; ++q) {
-                const bf16x8 a = w2[(t * (SG_DL / 16) + q) * 64 + lane];
+            for (int q = 0; q < SG_DL / 16; ++q)
 #pragma unroll
-                for (int ct = 0; ct < SG_NT; ++ct) acc[ct] = SG_MFMA(a, hb[ct][q], acc[ct]);
-            }
-            const f32x16 bb = sg_rows(h.b2, t, hh);
+                for (int ct = 0; ct < SG_NT; ++ct) acc[ct] = SG_MFMA(cur[q], hb[ct][q], acc[ct]);
 #pragma unroll
             for (int ct = 0; ct < SG_NT; ++ct)
 #pragma unroll
@@ -193,6 +201,9 @@ __global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const float *__restr
                     const float e = acc[ct][i] + bb[i];
                     ss[ct] = fmaf(e, e, ss[ct]);
                 }
+#pragma unroll
+            for (int q = 0; q < SG_DL / 16; ++q) cur[q] = nxt[q];
+            bb = bbn;
         }
 #pragma unroll
         for (int ct = 0; ct < SG_NT; ++ct) {
@@ -262,18 +273,32 @@ __global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const float *__restr
         const bf16x8 *wm = (const bf16x8 *)h.wm;
         const bf16x8 *wn2 = (const bf16x8 *)h.wn2;
         const int KS = DF / 16;
+        bf16x8 cur[SG_DL / 16], cw[SG_DC / 32][2];
+        f32x16 mb = sg_rows(h.bm, 0, hh), nb = sg_rows(h.bn1, 0, hh);
+#pragma unroll
+        for (int q = 0; q < SG_DL / 16; ++q) cur[q] = wm[q * 64 + lane];
+#pragma unroll
+        for (int rt = 0; rt < SG_DC / 32; ++rt)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) cw[rt][s] = wn2[(rt * KS + s) * 64 + lane];
         for (int t = 0; t < T2; ++t) {
+            // tile t + 1's fragments and bias rows in flight under tile t's MFMAs
+            const int tn = t + 1 < T2 ? t + 1 : t;
+            bf16x8 nxt[SG_DL / 16], nw[SG_DC / 32][2];
+#pragma unroll
+            for (int q = 0; q < SG_DL / 16; ++q) nxt[q] = wm[(tn * (SG_DL / 16) + q) * 64 + lane];
+#pragma unroll
+            for (int rt = 0; rt < SG_DC / 32; ++rt)
+#pragma unroll
+                for (int s = 0; s < 2; ++s) nw[rt][s] = wn2[(rt * KS + 2 * tn + s) * 64 + lane];
+            const f32x16 mbn = sg_rows(h.bm, tn, hh), nbn = sg_rows(h.bn1, tn, hh);
             f32x16 acc[SG_NT];
 #pragma unroll
             for (int ct = 0; ct < SG_NT; ++ct) acc[ct] = sg_zero16();
 #pragma unroll
-            for (int q = 0; q < SG_DL / 16; ++q) {
-                const bf16x8 a = wm[(t * (SG_DL / 16) + q) * 64 + lane];
+            for (int q = 0; q < SG_DL / 16; ++q)
 #pragma unroll
-                for (int ct = 0; ct < SG_NT; ++ct) acc[ct] = SG_MFMA(a, hb[ct][q], acc[ct]);
-            }
-            const f32x16 mb = sg_rows(h.bm, t, hh);
-            const f32x16 nb = sg_rows(h.bn1, t, hh);
+                for (int ct = 0; ct < SG_NT; ++ct) acc[ct] = SG_MFMA(cur[q], hb[ct][q], acc[ct]);
             bf16x8 ub[SG_NT][2];
 #pragma unroll
             for (int ct = 0; ct < SG_NT; ++ct)
@@ -286,12 +311,18 @@ __global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const float *__restr
 #pragma unroll
             for (int rt = 0; rt < SG_DC / 32; ++rt)
 #pragma unroll
-                for (int s = 0; s < 2; ++s) {
-                    const bf16x8 a = wn2[(rt * KS + 2 * t + s) * 64 + lane];
+                for (int s = 0; s < 2; ++s)
 #pragma unroll
                     for (int ct = 0; ct < SG_NT; ++ct)
-                        sacc[ct][rt] = SG_MFMA(a, ub[ct][s], sacc[ct][rt]);
-                }
+                        sacc[ct][rt] = SG_MFMA(cw[rt][s], ub[ct][s], sacc[ct][rt]);
+#pragma unroll
+            for (int q = 0; q < SG_DL / 16; ++q) cur[q] = nxt[q];
+#pragma unroll
+            for (int rt = 0; rt < SG_DC / 32; ++rt)
+#pragma unroll
+                for (int s = 0; s < 2; ++s) cw[rt][s] = nw[rt][s];
+            mb = mbn;
+            nb = nbn;
         }
     }
 

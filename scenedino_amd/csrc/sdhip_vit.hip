@@ -39,20 +39,23 @@ __device__ __forceinline__ f32x16 vt_zero16() {
 // ---------------------------------------------------------------------------
 // GEMM
 // ---------------------------------------------------------------------------
-#define GK 32       // K per pipeline step
-#define GLDS 40     // bf16 per LDS row (32 + 8 pad: 80-B rows, conflict-free b128 reads)
+#define GK 32       // K granularity of sd_gemm (the K loop runs in steps of BK = 64 or 32)
 
 __device__ __forceinline__ float vt_gelu(float x) {
     // nn.GELU() default (approximate='none'): 0.5 x (1 + erf(x / sqrt(2)))
     return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
 }
 
-template <int BM, int BN, int EPI>
+template <int BM, int BN, int BK, int EPI>
 __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
     constexpr int WM = BM / 2, WN = BN / 2;   // per-wave tile (2 x 2 waves)
     constexpr int TM = WM / 32, TN = WN / 32; // 32x32 MFMA tiles per wave
-    constexpr int CA = BM * 4 / 256;          // 16-B chunks of the A tile per thread
-    constexpr int CB = BN * 4 / 256;
+    constexpr int CPR = BK / 8;               // 16-B chunks per tile row
+    constexpr int CA = BM * CPR / 256;        // 16-B chunks of the A tile per thread
+    constexpr int CB = BN * CPR / 256;
+    // LDS rows padded by 16 B: row stride (BK + 8) * 2 B puts the 16 rows a ds_read_b128
+    // lane group touches on 16 distinct 4-bank groups
+    constexpr int GLDS = BK + 8;
     __shared__ __attribute__((aligned(16))) __bf16 sA[2][BM * GLDS];
     __shared__ __attribute__((aligned(16))) __bf16 sB[2][BN * GLDS];
 
@@ -62,26 +65,26 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
     const int64_t m0 = (int64_t)blockIdx.y * BM, n0 = (int64_t)blockIdx.x * BN;
     const __bf16 *A = (const __bf16 *)g.a;
     const __bf16 *Wt = (const __bf16 *)g.w;
-    const int nk = (int)(g.K / GK);
+    const int nk = (int)(g.K / BK);
 
     bf16x8 ra[CA], rb[CB];
     auto gload = [&](int kt) {
 #pragma unroll
         for (int c = 0; c < CA; ++c) {
-            const int ch = tid + 256 * c, row = ch >> 2, col = (ch & 3) * 8;
+            const int ch = tid + 256 * c, row = ch / CPR, col = (ch % CPR) * 8;
             const int64_t m = m0 + row;
             if (m < g.M)
-                ra[c] = *(const bf16x8 *)(A + m * g.lda + (int64_t)kt * GK + col);
+                ra[c] = *(const bf16x8 *)(A + m * g.lda + (int64_t)kt * BK + col);
             else
 #pragma unroll
                 for (int j = 0; j < 8; ++j) ra[c][j] = (__bf16)0.f;
         }
 #pragma unroll
         for (int c = 0; c < CB; ++c) {
-            const int ch = tid + 256 * c, row = ch >> 2, col = (ch & 3) * 8;
+            const int ch = tid + 256 * c, row = ch / CPR, col = (ch % CPR) * 8;
             const int64_t n = n0 + row;
             if (n < g.N)
-                rb[c] = *(const bf16x8 *)(Wt + n * g.K + (int64_t)kt * GK + col);
+                rb[c] = *(const bf16x8 *)(Wt + n * g.K + (int64_t)kt * BK + col);
             else
 #pragma unroll
                 for (int j = 0; j < 8; ++j) rb[c][j] = (__bf16)0.f;
@@ -90,12 +93,12 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
     auto lstore = [&](int buf) {
 #pragma unroll
         for (int c = 0; c < CA; ++c) {
-            const int ch = tid + 256 * c, row = ch >> 2, col = (ch & 3) * 8;
+            const int ch = tid + 256 * c, row = ch / CPR, col = (ch % CPR) * 8;
             *(bf16x8 *)&sA[buf][row * GLDS + col] = ra[c];
         }
 #pragma unroll
         for (int c = 0; c < CB; ++c) {
-            const int ch = tid + 256 * c, row = ch >> 2, col = (ch & 3) * 8;
+            const int ch = tid + 256 * c, row = ch / CPR, col = (ch % CPR) * 8;
             *(bf16x8 *)&sB[buf][row * GLDS + col] = rb[c];
         }
     };
@@ -113,7 +116,7 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
         const int buf = kt & 1;
         if (kt + 1 < nk) gload(kt + 1);
 #pragma unroll
-        for (int s = 0; s < GK / 16; ++s) {
+        for (int s = 0; s < BK / 16; ++s) {
             bf16x8 af[TM], bfr[TN];
 #pragma unroll
             for (int i = 0; i < TM; ++i)
@@ -439,16 +442,16 @@ __global__ void __launch_bounds__(256) k_tokens_to_grid(const float *__restrict_
 // ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
-template <int BM, int BN>
+template <int BM, int BN, int BK>
 static void vt_launch_gemm(const sd_gemm_args &g, hipStream_t s) {
     dim3 grid((unsigned)((g.N + BN - 1) / BN), (unsigned)((g.M + BM - 1) / BM));
     switch (g.epi) {
-    case SD_EPI_BF16: hipLaunchKernelGGL((k_gemm<BM, BN, SD_EPI_BF16>), grid, dim3(256), 0, s, g); break;
-    case SD_EPI_GELU: hipLaunchKernelGGL((k_gemm<BM, BN, SD_EPI_GELU>), grid, dim3(256), 0, s, g); break;
-    case SD_EPI_F32: hipLaunchKernelGGL((k_gemm<BM, BN, SD_EPI_F32>), grid, dim3(256), 0, s, g); break;
-    case SD_EPI_RESID: hipLaunchKernelGGL((k_gemm<BM, BN, SD_EPI_RESID>), grid, dim3(256), 0, s, g); break;
-    case SD_EPI_QKV: hipLaunchKernelGGL((k_gemm<BM, BN, SD_EPI_QKV>), grid, dim3(256), 0, s, g); break;
-    default: hipLaunchKernelGGL((k_gemm<BM, BN, SD_EPI_PATCH>), grid, dim3(256), 0, s, g); break;
+    case SD_EPI_BF16: hipLaunchKernelGGL((k_gemm<BM, BN, BK, SD_EPI_BF16>), grid, dim3(256), 0, s, g); break;
+    case SD_EPI_GELU: hipLaunchKernelGGL((k_gemm<BM, BN, BK, SD_EPI_GELU>), grid, dim3(256), 0, s, g); break;
+    case SD_EPI_F32: hipLaunchKernelGGL((k_gemm<BM, BN, BK, SD_EPI_F32>), grid, dim3(256), 0, s, g); break;
+    case SD_EPI_RESID: hipLaunchKernelGGL((k_gemm<BM, BN, BK, SD_EPI_RESID>), grid, dim3(256), 0, s, g); break;
+    case SD_EPI_QKV: hipLaunchKernelGGL((k_gemm<BM, BN, BK, SD_EPI_QKV>), grid, dim3(256), 0, s, g); break;
+    default: hipLaunchKernelGGL((k_gemm<BM, BN, BK, SD_EPI_PATCH>), grid, dim3(256), 0, s, g); break;
     }
 }
 
@@ -478,10 +481,19 @@ extern "C" int sd_gemm(const sd_gemm_args *args, void *stream) {
     hipStream_t s = (hipStream_t)stream;
     // 128x128 tiles once they fill the chip, else 64x64 (ViT-S-sized token counts)
     const int64_t big = ((g.M + 127) / 128) * ((g.N + 127) / 128);
-    if (big >= 256)
-        vt_launch_gemm<128, 128>(g, s);
-    else
-        vt_launch_gemm<64, 64>(g, s);
+    // K steps of 64 whenever K allows (half the barriers, twice the work under each
+    // prefetch); 128x128 tiles once they fill the chip, else 64x64
+    if (g.K % 64 == 0) {
+        if (big >= 256)
+            vt_launch_gemm<128, 128, 64>(g, s);
+        else
+            vt_launch_gemm<64, 64, 64>(g, s);
+    } else {
+        if (big >= 256)
+            vt_launch_gemm<128, 128, 32>(g, s);
+        else
+            vt_launch_gemm<64, 64, 32>(g, s);
+    }
     if (hipGetLastError() != hipSuccess) {
         sd_set_error("sd_gemm: launch failed");
         return -2;
