@@ -190,6 +190,8 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
 // ---------------------------------------------------------------------------
 #define AT_HD 64
 
+#define AT_ROW 72  // bf16 per LDS tile row: 64 + 8 pad (144-B rows: conflict-free b128 reads)
+
 __global__ void __launch_bounds__(256) k_attn(const __bf16 *__restrict__ Q,
                                               const __bf16 *__restrict__ K,
                                               const __bf16 *__restrict__ Vt, int T, int Tp,
@@ -197,8 +199,11 @@ __global__ void __launch_bounds__(256) k_attn(const __bf16 *__restrict__ Q,
     // One workgroup = 32 queries of one (batch, head); its 4 waves split the 64-key blocks
     // (wave w takes blocks w, w+4, ...), each keeping its own running (max, sum, O^T), and
     // combine them through LDS at the end (a batch-1 ViT-B/8 has only 12 heads x 61 query
-    // tiles: without the split, fewer waves than SIMDs).
-    __shared__ float s_o[4][2][16][64];  // [wave][hd tile][acc register][lane]
+    // tiles: without the split, fewer waves than SIMDs).  A block's K (64 keys x 64) and V^T
+    // (64 x 64 keys) tiles are contiguous 128-B rows in HBM: each wave streams them with
+    // 16-B coalesced loads (prefetched one block ahead in registers) into its own LDS tiles,
+    // and the MFMA fragments are read from there.
+    __shared__ __attribute__((aligned(16))) __bf16 s_kv[4][2][64 * AT_ROW];  // [wave][K | V^T]
     __shared__ float s_m[4][64], s_l[4][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int r = lane & 31, h = lane >> 5;
@@ -207,6 +212,8 @@ __global__ void __launch_bounds__(256) k_attn(const __bf16 *__restrict__ Q,
     const __bf16 *Qh = Q + (int64_t)bh * T * AT_HD;
     const __bf16 *Kh = K + (int64_t)bh * Tp * AT_HD;
     const __bf16 *Vh = Vt + (int64_t)bh * AT_HD * Tp;
+    __bf16 *sK = s_kv[wave][0];
+    __bf16 *sV = s_kv[wave][1];
 
     // Q^T as B operand: lane (query r, half h), k-step s: Q[q][16 s + 8 h + j]
     bf16x8 qb[AT_HD / 16];
@@ -226,34 +233,35 @@ __global__ void __launch_bounds__(256) k_attn(const __bf16 *__restrict__ Q,
     o[1] = vt_zero16();
     float mrun = -INFINITY, lsum = 0.f;
 
+    // staging registers: chunk c = lane + 64 i (i < 8) of a 64 x 128-B tile, row c / 8,
+    // 16-B column c % 8
+    bf16x8 gk[8], gv[8];
+    auto gload = [&](int kb) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int c = lane + 64 * i, row = c >> 3, col = (c & 7) * 8;
+            gk[i] = *(const bf16x8 *)(Kh + (int64_t)(kb + row) * AT_HD + col);
+            gv[i] = *(const bf16x8 *)(Vh + (int64_t)row * Tp + kb + col);
+        }
+    };
+    if (64 * wave < Tp) gload(64 * wave);
     for (int kb = 64 * wave; kb < Tp; kb += 256) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int c = lane + 64 * i, row = c >> 3, col = (c & 7) * 8;
+            *(bf16x8 *)(sK + row * AT_ROW + col) = gk[i];
+            *(bf16x8 *)(sV + row * AT_ROW + col) = gv[i];
+        }
+        if (kb + 256 < Tp) gload(kb + 256);  // next block in flight under this one
         // S^T tiles: keys kb + 32 t + row, queries on the lanes
         f32x16 st[2];
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
             st[t] = vt_zero16();
-            const __bf16 *kr = Kh + (int64_t)(kb + 32 * t + r) * AT_HD + 8 * h;
 #pragma unroll
             for (int s = 0; s < AT_HD / 16; ++s)
-                st[t] = VT_MFMA(*(const bf16x8 *)(kr + 16 * s), qb[s], st[t]);
-        }
-        // V^T fragments of this block, issued before the softmax so they land under it
-        bf16x8 va[2][2][2];
-#pragma unroll
-        for (int ht = 0; ht < 2; ++ht) {
-            const __bf16 *vr = Vh + (int64_t)(32 * ht + r) * Tp + kb + 4 * h;
-#pragma unroll
-            for (int t = 0; t < 2; ++t)
-#pragma unroll
-                for (int s = 0; s < 2; ++s) {
-                    const bf16x4 lo = *(const bf16x4 *)(vr + 32 * t + 16 * s);
-                    const bf16x4 hi = *(const bf16x4 *)(vr + 32 * t + 16 * s + 8);
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        va[ht][t][s][j] = lo[j];
-                        va[ht][t][s][4 + j] = hi[j];
-                    }
-                }
+                st[t] = VT_MFMA(*(const bf16x8 *)(sK + (32 * t + r) * AT_ROW + 16 * s + 8 * h),
+                                qb[s], st[t]);
         }
         // mask keys >= T (zero-padded rows of the last block)
         if (kb + 64 > T) {
@@ -290,20 +298,35 @@ __global__ void __launch_bounds__(256) k_attn(const __bf16 *__restrict__ Q,
 #pragma unroll
             for (int i = 0; i < 16; ++i) o[ht][i] *= alpha;
         // O^T += V^T P: A = V^T rows (head dim), k = keys in the accumulator-operand order
+        // (element j of lane half h: key 32 t + 16 s + 8 (j >> 2) + 4 h + (j & 3))
 #pragma unroll
-        for (int ht = 0; ht < 2; ++ht)
+        for (int ht = 0; ht < 2; ++ht) {
+            const __bf16 *vr = sV + (32 * ht + r) * AT_ROW + 4 * h;
 #pragma unroll
             for (int t = 0; t < 2; ++t)
 #pragma unroll
-                for (int s = 0; s < 2; ++s) o[ht] = VT_MFMA(va[ht][t][s], pb[t][s], o[ht]);
+                for (int s = 0; s < 2; ++s) {
+                    const bf16x4 lo = *(const bf16x4 *)(vr + 32 * t + 16 * s);
+                    const bf16x4 hi = *(const bf16x4 *)(vr + 32 * t + 16 * s + 8);
+                    bf16x8 a;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        a[j] = lo[j];
+                        a[4 + j] = hi[j];
+                    }
+                    o[ht] = VT_MFMA(a, pb[t][s], o[ht]);
+                }
+        }
     }
-    // combine the 4 waves' partial softmax states
-    s_m[wave][lane] = mrun;          // identical in both halves
-    s_l[wave][lane] = lsum;          // per-half partial sums
+    // combine the 4 waves' partial softmax states (the K / V tiles are dead: reuse them)
+    __syncthreads();
+    float *s_o = (float *)&s_kv[0][0][0];  // [wave][hd tile][acc register][lane]
+    s_m[wave][lane] = mrun;                 // identical in both halves
+    s_l[wave][lane] = lsum;                 // per-half partial sums
 #pragma unroll
     for (int ht = 0; ht < 2; ++ht)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) s_o[wave][ht][i][lane] = o[ht][i];
+        for (int i = 0; i < 16; ++i) s_o[((wave * 2 + ht) * 16 + i) * 64 + lane] = o[ht][i];
     __syncthreads();
     float M = -INFINITY;
 #pragma unroll
@@ -329,7 +352,8 @@ __global__ void __launch_bounds__(256) k_attn(const __bf16 *__restrict__ Q,
             for (int e = 0; e < 4; ++e) {
                 float acc = 0.f;
 #pragma unroll
-                for (int w = 0; w < 4; ++w) acc = fmaf(fw[w], s_o[w][ht][4 * wave + e][lane], acc);
+                for (int w = 0; w < 4; ++w)
+                    acc = fmaf(fw[w], s_o[((w * 2 + ht) * 16 + 4 * wave + e) * 64 + lane], acc);
                 v[e] = (__bf16)(acc * inv);
             }
             *(bf16x4 *)(dst + 32 * ht + 8 * wave + 4 * h) = v;
