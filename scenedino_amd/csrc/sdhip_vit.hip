@@ -46,6 +46,11 @@ __device__ __forceinline__ float vt_gelu(float x) {
     return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
 }
 
+__device__ __forceinline__ uint32_t vt_bytes(int64_t elems) {
+    const int64_t b = elems * 2;
+    return b > 0xffffffffLL ? 0xffffffffu : (uint32_t)b;
+}
+
 template <int BM, int BN, int BK, int EPI>
 __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
     constexpr int WM = BM / 2, WN = BN / 2;   // per-wave tile (2 x 2 waves)
@@ -67,30 +72,41 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
     const __bf16 *Wt = (const __bf16 *)g.w;
     const int nk = (int)(g.K / BK);
 
-    bf16x8 ra[CA], rb[CB];
-    auto gload = [&](int kt) {
+    // Two register staging sets: the tile of step k + 2 is loaded while step k computes
+    // and step k + 1's tile (loaded one step earlier) goes to LDS after it -- global
+    // latency gets two steps of MFMA work to hide under, at one LDS double buffer.
+    bf16x8 ra0[CA], rb0[CB], ra1[CA], rb1[CB];
+    // Rows past M (N) are clamped to the last row instead of predicated: they only feed
+    // output rows (columns) that are never stored, and unpredicated loads keep the
+    // compiler's vmcnt accounting exact (a masked load forces vmcnt(0) waits).
+    // Buffer loads: the per-thread byte offset (voffset) is fixed for the whole K loop and
+    // the K step is the scalar offset, so no address VGPR is rewritten per step (a rewrite
+    // of a load's own destination/address registers costs a vmcnt drain).
+    const __amdgpu_buffer_rsrc_t rsA =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16 *>(A), 0, vt_bytes(g.M * g.lda), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsB =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16 *>(Wt), 0, vt_bytes(g.N * g.K), 0x00020000);
+    uint32_t voA[CA], voB[CB];
 #pragma unroll
-        for (int c = 0; c < CA; ++c) {
-            const int ch = tid + 256 * c, row = ch / CPR, col = (ch % CPR) * 8;
-            const int64_t m = m0 + row;
-            if (m < g.M)
-                ra[c] = *(const bf16x8 *)(A + m * g.lda + (int64_t)kt * BK + col);
-            else
+    for (int c = 0; c < CA; ++c) {
+        const int ch = tid + 256 * c, row = ch / CPR, col = (ch % CPR) * 8;
+        voA[c] = (uint32_t)((min(m0 + row, g.M - 1) * g.lda + col) * 2);
+    }
 #pragma unroll
-                for (int j = 0; j < 8; ++j) ra[c][j] = (__bf16)0.f;
-        }
+    for (int c = 0; c < CB; ++c) {
+        const int ch = tid + 256 * c, row = ch / CPR, col = (ch % CPR) * 8;
+        voB[c] = (uint32_t)((min(n0 + row, g.N - 1) * g.K + col) * 2);
+    }
+    auto gload = [&](int kt, bf16x8 (&ra)[CA], bf16x8 (&rb)[CB]) {
+        const uint32_t so = (uint32_t)kt * BK * 2;
 #pragma unroll
-        for (int c = 0; c < CB; ++c) {
-            const int ch = tid + 256 * c, row = ch / CPR, col = (ch % CPR) * 8;
-            const int64_t n = n0 + row;
-            if (n < g.N)
-                rb[c] = *(const bf16x8 *)(Wt + n * g.K + (int64_t)kt * BK + col);
-            else
+        for (int c = 0; c < CA; ++c)
+            ra[c] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsA, voA[c], so, 0));
 #pragma unroll
-                for (int j = 0; j < 8; ++j) rb[c][j] = (__bf16)0.f;
-        }
+        for (int c = 0; c < CB; ++c)
+            rb[c] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsB, voB[c], so, 0));
     };
-    auto lstore = [&](int buf) {
+    auto lstore = [&](int buf, bf16x8 (&ra)[CA], bf16x8 (&rb)[CB]) {
 #pragma unroll
         for (int c = 0; c < CA; ++c) {
             const int ch = tid + 256 * c, row = ch / CPR, col = (ch % CPR) * 8;
@@ -109,12 +125,12 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = vt_zero16();
 
-    gload(0);
-    lstore(0);
-    __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
+    auto step = [&](int kt, bf16x8 (&ca)[CA], bf16x8 (&cb)[CB], bf16x8 (&na)[CA],
+                    bf16x8 (&nb)[CB]) {
         const int buf = kt & 1;
-        if (kt + 1 < nk) gload(kt + 1);
+        // unconditional (the last steps re-load stage nk - 1): a load issued on one path
+        // only makes the compiler's vmcnt model wait for the newest loads as well
+        gload(min(kt + 2, nk - 1), na, nb);
 #pragma unroll
         for (int s = 0; s < BK / 16; ++s) {
             bf16x8 af[TM], bfr[TN];
@@ -129,8 +145,17 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
 #pragma unroll
                 for (int j = 0; j < TN; ++j) acc[i][j] = VT_MFMA(af[i], bfr[j], acc[i][j]);
         }
-        if (kt + 1 < nk) lstore(buf ^ 1);
+        if (kt + 1 < nk) lstore(buf ^ 1, ca, cb);
         __syncthreads();
+    };
+
+    gload(0, ra0, rb0);
+    lstore(0, ra0, rb0);
+    gload(min(1, nk - 1), ra0, rb0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; kt += 2) {
+        step(kt, ra0, rb0, ra1, rb1);          // set 0 holds step kt + 1, set 1 gets kt + 2
+        if (kt + 1 < nk) step(kt + 1, ra1, rb1, ra0, rb0);
     }
 
     // epilogue: accumulator register q of tile (i, j): row (q&3)+8(q>>2)+4h, column r
@@ -487,7 +512,7 @@ extern "C" int sd_gemm(const sd_gemm_args *args, void *stream) {
     const sd_gemm_args &g = *args;
     bool ok = g.a && g.w && g.M >= 0 && g.N > 0 && g.K > 0 && g.K % GK == 0 && g.lda >= g.K &&
               g.lda % 8 == 0 && g.epi >= SD_EPI_BF16 && g.epi <= SD_EPI_PATCH &&
-              g.M * (int64_t)g.lda < ((int64_t)1 << 40);
+              g.M * (int64_t)g.lda < ((int64_t)1 << 31) && g.N * g.K < ((int64_t)1 << 31);
     if (g.epi == SD_EPI_QKV)
         ok = ok && g.q && g.k && g.vt && g.head_dim > 0 && g.heads > 0 && g.tokens > 0 &&
              g.tokens_pad >= g.tokens && g.N == 3LL * g.heads * g.head_dim &&
@@ -498,7 +523,7 @@ extern "C" int sd_gemm(const sd_gemm_args *args, void *stream) {
         ok = ok && g.out && g.ldo >= g.N;
     if (!ok) {
         sd_set_error("sd_gemm: invalid argument (K % 32 == 0, lda >= K and lda % 8 == 0, "
-                     "epilogue fields)");
+                     "operands < 4 GiB, epilogue fields)");
         return -1;
     }
     if (g.M == 0) return 0;
