@@ -185,6 +185,37 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
             const int rem = (int)(n - (int64_t)which * C);
             head = rem / g.head_dim;
             e = rem - head * g.head_dim;
+            if (which == 2) {
+                // V^T: a lane's registers 4g..4g+3 are 4 consecutive tokens of its head-dim
+                // row -> one 8-B store instead of four 2-B stores into four cache lines
+                // (the 32-column tile lies inside the V third: `which` is wave-uniform)
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int gq = 0; gq < 4; ++gq) {
+                        const int64_t m = m0 + wm * WM + i * 32 + 8 * gq + 4 * h;
+                        if (m >= g.M) continue;
+                        const uint32_t b = (uint32_t)m / (uint32_t)g.tokens;
+                        const int64_t t = m - (int64_t)b * g.tokens;
+                        __bf16 *dst = (__bf16 *)g.vt +
+                                      (((int64_t)b * g.heads + head) * g.head_dim + e) * g.tokens_pad + t;
+                        if (m + 3 < g.M && t + 3 < g.tokens && (t & 3) == 0) {
+                            bf16x4 v4;
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) v4[u] = (__bf16)(acc[i][j][4 * gq + u] + bias);
+                            *(bf16x4 *)dst = v4;
+                        } else {
+                            for (int u = 0; u < 4 && m + u < g.M; ++u) {
+                                const uint32_t bu = (uint32_t)(m + u) / (uint32_t)g.tokens;
+                                const int64_t tu = m + u - (int64_t)bu * g.tokens;
+                                ((__bf16 *)g.vt)[(((int64_t)bu * g.heads + head) * g.head_dim + e) *
+                                                     g.tokens_pad + tu] =
+                                    (__bf16)(acc[i][j][4 * gq + u] + bias);
+                            }
+                        }
+                    }
+                continue;
+            }
         }
 #pragma unroll
         for (int i = 0; i < TM; ++i)
