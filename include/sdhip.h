@@ -256,7 +256,11 @@ enum sd_epilogue {
     SD_EPI_RESID = 3,  /* out f32 += gamma * (acc + bias)  (residual add, ls1/ls2 gamma)   */
     SD_EPI_QKV = 4,    /* scatter qkv columns into q (B,H,T,hd), k (B,H,Tp,hd),            */
                        /* vt (B,H,hd,Tp) bf16 (timm Attention reshape/permute)             */
-    SD_EPI_PATCH = 5   /* out f32 (B, patches+1, N): row b*(patches+1)+1+p = acc+bias+pos  */
+    SD_EPI_PATCH = 5,  /* out f32 (B, patches+1, N): row b*(patches+1)+1+p = acc+bias+pos  */
+    SD_EPI_SHUF = 6,   /* ConvTranspose2d(k, stride k): row m = input pixel (b, y, x),      */
+                       /* column n = (dy k + dx) Cout + co -> out bf16 NHWC                 */
+                       /* (B, in_h k, in_w k, Cout)[b, y k + dy, x k + dx, co] = acc + bias[n] */
+    SD_EPI_NCHW = 7    /* out f32 NCHW (B, N, plane): row m = b * plane + p (plane = tokens) */
 };
 
 /* C = A (M, K) . W (N, K)^T (+ bias) with the epilogue above; A, W bf16 row-major
@@ -273,6 +277,14 @@ typedef struct sd_gemm_args {
     int32_t tokens, heads, head_dim, tokens_pad;
     const float *pos;           /* SD_EPI_PATCH position embedding (patches+1, N)        */
     int32_t patches;
+    /* residuals added by the BF16 / F32 epilogues: bf16 (M, N) row stride ldo, or NULL     */
+    const void *res, *res2;
+    /* implicit 3x3 convolution, padding 1 (conv != 0): a = NHWC bf16 input (B, H, W, Cin),
+     * rows m = output pixels (B, OH, OW), k = (ky, kx, ci) (K = 9 Cin, Cin % 64 == 0),
+     * w = (Cout, 3, 3, Cin); relu_in applies ReLU to the input as it is loaded (the
+     * pre-activation of DPT's residual conv units) */
+    int32_t conv, H, W, Cin, stride, OH, OW, relu_in;
+    int32_t shuf_k, in_h, in_w; /* SD_EPI_SHUF geometry                                  */
 } sd_gemm_args;
 
 int sd_gemm(const sd_gemm_args *args, void *stream);
@@ -299,6 +311,21 @@ int sd_patchify(const float *img, int32_t B, int32_t H, int32_t W, int32_t p, in
  * optionally L2-normalised over C (F.normalize, eps 1e-12). */
 int sd_tokens_to_grid(const float *x, int32_t B, int32_t T, int32_t C, int32_t n_prefix,
                       int32_t gh, int32_t gw, int32_t l2norm, float *out, void *stream);
+
+/* ---- DPT decoder pieces (sdhip_vit.hip; dpt_head.py:23-236) -------------------
+ * The convolutions of the DPT head run through sd_gemm (1x1: plain GEMM; 3x3: conv = 1;
+ * ConvTranspose2d(k, stride k): SD_EPI_SHUF; the last one writes NCHW f32 for the field
+ * kernels: SD_EPI_NCHW).  Activations are NHWC bf16. */
+
+/* x (B, T, C) f32 -> out (B, npix, C) bf16: tokens n_prefix .. n_prefix+npix-1, optionally
+ * L2-normalised (the DPT inputs: ViT block outputs / normalised final tokens). */
+int sd_tokens_to_nhwc(const float *x, int32_t B, int32_t T, int32_t C, int32_t n_prefix,
+                      int32_t npix, int32_t l2norm, void *out, void *stream);
+
+/* F.interpolate(scale_factor=2, mode="bilinear", align_corners=True) on NHWC bf16
+ * (FeatureFusionBlock, dpt_head.py:157): in (B, H, W, C) -> out (B, 2H, 2W, C). */
+int sd_upsample2x(const void *in, int32_t B, int32_t H, int32_t W, int32_t C, void *out,
+                  void *stream);
 
 #ifdef __cplusplus
 }

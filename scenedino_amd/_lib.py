@@ -86,10 +86,15 @@ class SdGemmArgs(ctypes.Structure):
         ("q", _vp), ("k", _vp), ("vt", _vp),
         ("tokens", _i32), ("heads", _i32), ("head_dim", _i32), ("tokens_pad", _i32),
         ("pos", _vp), ("patches", _i32),
+        ("res", _vp), ("res2", _vp),
+        ("conv", _i32), ("H", _i32), ("W", _i32), ("Cin", _i32), ("stride", _i32), ("OH", _i32),
+        ("OW", _i32), ("relu_in", _i32),
+        ("shuf_k", _i32), ("in_h", _i32), ("in_w", _i32),
     ]
 
 
-SD_EPI_BF16, SD_EPI_GELU, SD_EPI_F32, SD_EPI_RESID, SD_EPI_QKV, SD_EPI_PATCH = range(6)
+(SD_EPI_BF16, SD_EPI_GELU, SD_EPI_F32, SD_EPI_RESID, SD_EPI_QKV, SD_EPI_PATCH, SD_EPI_SHUF,
+ SD_EPI_NCHW) = range(8)
 
 # (name, argtypes) of every exported entry point; tests check the .so exports all.
 SIGNATURES = {
@@ -118,6 +123,8 @@ SIGNATURES = {
     "sd_patchify": [_vp, _i32, _i32, _i32, _i32, _i32, ctypes.POINTER(ctypes.c_float),
                     ctypes.POINTER(ctypes.c_float), _vp, _vp, _vp, _vp, _i32, _vp],
     "sd_tokens_to_grid": [_vp, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp],
+    "sd_tokens_to_nhwc": [_vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp],
+    "sd_upsample2x": [_vp, _i32, _i32, _i32, _i32, _vp, _vp],
 }
 
 _lib = None
@@ -378,4 +385,74 @@ def tokens_to_grid(x, B, T, C, n_prefix, gh, gw, l2norm):
     out = torch.empty(B, C, gh, gw, device=x.device, dtype=torch.float32)
     _check(lib.sd_tokens_to_grid(ptr(_req(x, "x")), B, T, C, n_prefix, gh, gw, int(bool(l2norm)),
                                  ptr(out), stream_of(x)), "sd_tokens_to_grid")
+    return out
+
+
+# ---------------------------------------------------------------------------
+# DPT decoder helpers
+# ---------------------------------------------------------------------------
+def conv3x3(x, w, bias, stride=1, relu_in=False, epi=None, out=None, res=None, res2=None):
+    """Implicit-GEMM 3x3 convolution, padding 1: x (B, H, W, Cin) bf16 NHWC, w (Cout, 9 Cin)
+    bf16 (k order ky, kx, ci) -> (B, OH, OW, Cout) bf16 (or f32 NCHW with epi=SD_EPI_NCHW)."""
+    lib = load()
+    B, H, W, Cin = x.shape
+    _req(x, "x", torch.bfloat16)
+    _req(w, "w", torch.bfloat16)
+    Cout = w.shape[0]
+    OH, OW = (H - 1) // stride + 1, (W - 1) // stride + 1
+    epi = SD_EPI_BF16 if epi is None else epi
+    M = B * OH * OW
+    if out is None:
+        out = (torch.empty(B, Cout, OH, OW, device=x.device) if epi == SD_EPI_NCHW else
+               torch.empty(B, OH, OW, Cout, device=x.device,
+                           dtype=torch.float32 if epi == SD_EPI_F32 else torch.bfloat16))
+    g = SdGemmArgs(a=x.data_ptr(), lda=9 * Cin, w=w.data_ptr(),
+                   bias=bias.data_ptr() if bias is not None else None, M=M, N=Cout, K=9 * Cin,
+                   epi=epi, out=out.data_ptr(), ldo=Cout,
+                   res=res.data_ptr() if res is not None else None,
+                   res2=res2.data_ptr() if res2 is not None else None,
+                   conv=1, H=H, W=W, Cin=Cin, stride=stride, OH=OH, OW=OW,
+                   relu_in=int(bool(relu_in)), tokens=OH * OW)
+    _check(lib.sd_gemm(ctypes.byref(g), stream_of(x)), "sd_gemm(conv3x3)")
+    return out
+
+
+def linear_nhwc(x, w, bias, epi=None, out=None, shuf=None, res=None):
+    """1x1 convolution / ConvTranspose2d(k, stride k) on NHWC bf16 x (B, H, W, Cin):
+    w (N, Cin) bf16.  shuf=k: SD_EPI_SHUF into (B, H k, W k, N / k^2)."""
+    lib = load()
+    B, H, W, Cin = x.shape
+    _req(x, "x", torch.bfloat16)
+    _req(w, "w", torch.bfloat16)
+    N = w.shape[0]
+    M = B * H * W
+    if shuf is not None:
+        epi = SD_EPI_SHUF
+        out = torch.empty(B, H * shuf, W * shuf, N // (shuf * shuf), device=x.device,
+                          dtype=torch.bfloat16) if out is None else out
+    else:
+        epi = SD_EPI_BF16 if epi is None else epi
+        out = torch.empty(B, H, W, N, device=x.device, dtype=torch.bfloat16) if out is None else out
+    g = SdGemmArgs(a=x.data_ptr(), lda=Cin, w=w.data_ptr(),
+                   bias=bias.data_ptr() if bias is not None else None, M=M, N=N, K=Cin, epi=epi,
+                   out=out.data_ptr(), ldo=N, res=res.data_ptr() if res is not None else None,
+                   shuf_k=shuf or 0, in_h=H, in_w=W)
+    _check(lib.sd_gemm(ctypes.byref(g), stream_of(x)), "sd_gemm(1x1)")
+    return out
+
+
+def tokens_to_nhwc(x, B, T, C, n_prefix, gh, gw, l2norm):
+    lib = load()
+    out = torch.empty(B, gh, gw, C, device=x.device, dtype=torch.bfloat16)
+    _check(lib.sd_tokens_to_nhwc(ptr(_req(x, "x")), B, T, C, n_prefix, gh * gw, int(bool(l2norm)),
+                                 ptr(out), stream_of(x)), "sd_tokens_to_nhwc")
+    return out
+
+
+def upsample2x(x):
+    lib = load()
+    B, H, W, C = x.shape
+    out = torch.empty(B, 2 * H, 2 * W, C, device=x.device, dtype=torch.bfloat16)
+    _check(lib.sd_upsample2x(ptr(_req(x, "x", torch.bfloat16)), B, H, W, C, ptr(out),
+                             stream_of(x)), "sd_upsample2x")
     return out

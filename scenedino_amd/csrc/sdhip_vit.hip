@@ -62,7 +62,16 @@ __device__ __forceinline__ uint32_t vt_bytes(int64_t elems) {
     return b > 0xffffffffLL ? 0xffffffffu : (uint32_t)b;
 }
 
-template <int BM, int BN, int BK, int EPI>
+// bf16 ReLU on 8 packed values (sign bit set -> +0), integer ops only
+__device__ __forceinline__ bf16x8 vt_relu8(bf16x8 v) {
+    uint4 u = __builtin_bit_cast(uint4, v);
+    uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] &= ~(((w[i] >> 15) & 0x00010001u) * 0xffffu);
+    return __builtin_bit_cast(bf16x8, uint4{w[0], w[1], w[2], w[3]});
+}
+
+template <int BM, int BN, int BK, int EPI, bool CONV>
 __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
     constexpr int WM = BM / 2, WN = BN / 2;   // per-wave tile (2 x 2 waves)
     constexpr int TM = WM / 32, TN = WN / 32; // 32x32 MFMA tiles per wave
@@ -93,15 +102,32 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
     // Buffer loads: the per-thread byte offset (voffset) is fixed for the whole K loop and
     // the K step is the scalar offset, so no address VGPR is rewritten per step (a rewrite
     // of a load's own destination/address registers costs a vmcnt drain).
+    // conv: A = NHWC input of B = M / (OH OW) images; an out-of-image tap gets an offset
+    // past the buffer's end, which the buffer load returns as zeros (the padding)
+    const int64_t a_elems = CONV ? (g.M / ((int64_t)g.OH * g.OW)) * g.H * g.W * g.Cin
+                                 : g.M * g.lda;
     const __amdgpu_buffer_rsrc_t rsA =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16 *>(A), 0, vt_bytes(g.M * g.lda), 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16 *>(A), 0, vt_bytes(a_elems), 0x00020000);
     const __amdgpu_buffer_rsrc_t rsB =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16 *>(Wt), 0, vt_bytes(g.N * g.K), 0x00020000);
     uint32_t voA[CA], voB[CB];
+    int cpix[CA], ciy[CA], cix[CA];  // conv: image base pixel, top-left tap row / column
 #pragma unroll
     for (int c = 0; c < CA; ++c) {
         const int ch = tid + 256 * c, row = ch / CPR, col = (ch % CPR) * 8;
-        voA[c] = (uint32_t)((min(m0 + row, g.M - 1) * g.lda + col) * 2);
+        const int64_t m = min(m0 + row, g.M - 1);
+        if (CONV) {
+            const int ohw = g.OH * g.OW;
+            const int b = (int)((uint32_t)m / (uint32_t)ohw);
+            const int p = (int)(m - (int64_t)b * ohw);
+            const int oy = p / g.OW, ox = p - oy * g.OW;
+            cpix[c] = b * g.H * g.W;
+            ciy[c] = oy * g.stride - 1;
+            cix[c] = ox * g.stride - 1;
+            voA[c] = (uint32_t)col;
+        } else {
+            voA[c] = (uint32_t)((m * g.lda + col) * 2);
+        }
     }
 #pragma unroll
     for (int c = 0; c < CB; ++c) {
@@ -110,9 +136,24 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
     }
     auto gload = [&](int kt, bf16x8 (&ra)[CA], bf16x8 (&rb)[CB]) {
         const uint32_t so = (uint32_t)kt * BK * 2;
+        if (CONV) {
+            const int k0 = kt * BK;
+            const int tap = k0 / g.Cin, ci0 = k0 - tap * g.Cin;
+            const int ky = tap / 3, kx = tap - 3 * (tap / 3);
 #pragma unroll
-        for (int c = 0; c < CA; ++c)
-            ra[c] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsA, voA[c], so, 0));
+            for (int c = 0; c < CA; ++c) {
+                const int iy = ciy[c] + ky, ix = cix[c] + kx;
+                const bool ok = (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
+                const uint32_t off =
+                    ok ? (uint32_t)(((cpix[c] + iy * g.W + ix) * g.Cin + ci0) * 2) + voA[c] * 2
+                       : 0x80000000u;
+                ra[c] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsA, off, 0, 0));
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < CA; ++c)
+                ra[c] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsA, voA[c], so, 0));
+        }
 #pragma unroll
         for (int c = 0; c < CB; ++c)
             rb[c] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsB, voB[c], so, 0));
@@ -121,7 +162,7 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
 #pragma unroll
         for (int c = 0; c < CA; ++c) {
             const int ch = tid + 256 * c, row = ch / CPR, col = (ch % CPR) * 8;
-            *(bf16x8 *)&sA[buf][row * GLDS + col] = ra[c];
+            *(bf16x8 *)&sA[buf][row * GLDS + col] = (CONV && g.relu_in) ? vt_relu8(ra[c]) : ra[c];
         }
 #pragma unroll
         for (int c = 0; c < CB; ++c) {
@@ -223,9 +264,29 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
             for (int q = 0; q < 16; ++q) {
                 const int64_t m = m0 + wm * WM + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
                 if (m >= g.M) continue;
-                const float v = acc[i][j][q] + bias;
+                float v = acc[i][j][q] + bias;
+                if (EPI == SD_EPI_BF16 || EPI == SD_EPI_F32) {
+                    if (g.res) v += (float)((const __bf16 *)g.res)[m * g.ldo + n];
+                    if (g.res2) v += (float)((const __bf16 *)g.res2)[m * g.ldo + n];
+                }
                 if (EPI == SD_EPI_BF16) {
                     ((__bf16 *)g.out)[m * g.ldo + n] = (__bf16)v;
+                } else if (EPI == SD_EPI_SHUF) {
+                    const int kk = g.shuf_k, cout = (int)(g.N / (kk * kk));
+                    const int sub = (int)(n / cout), co = (int)(n - (int64_t)sub * cout);
+                    const int dy = sub / kk, dx = sub - dy * kk;
+                    const int hw = g.in_h * g.in_w;
+                    const int b = (int)((uint32_t)m / (uint32_t)hw);
+                    const int pix = (int)(m - (int64_t)b * hw);
+                    const int y = pix / g.in_w, x = pix - y * g.in_w;
+                    const int64_t orow = ((int64_t)b * g.in_h * kk + y * kk + dy) * (g.in_w * kk) +
+                                         x * kk + dx;
+                    ((__bf16 *)g.out)[orow * cout + co] = (__bf16)v;
+                } else if (EPI == SD_EPI_NCHW) {
+                    const int plane = g.tokens;
+                    const int b = (int)((uint32_t)m / (uint32_t)plane);
+                    const int64_t pix = m - (int64_t)b * plane;
+                    ((float *)g.out)[((int64_t)b * g.N + n) * plane + pix] = v;
                 } else if (EPI == SD_EPI_GELU) {
                     ((__bf16 *)g.out)[m * g.ldo + n] = (__bf16)vt_gelu(v);
                 } else if (EPI == SD_EPI_F32) {
@@ -533,19 +594,93 @@ __global__ void __launch_bounds__(256) k_tokens_to_grid(const float *__restrict_
         out[(((int64_t)b * C + c) * gh) * gw + pi] = xr[c] * scale;
 }
 
+// tokens (B, T, C) f32 -> NHWC bf16 (B, gh*gw, C) (prefix tokens dropped, optional L2
+// normalisation): the DPT decoder's inputs.  One wave per token.
+__global__ void __launch_bounds__(256) k_tokens_to_nhwc(const float *__restrict__ x, int B, int T,
+                                                        int C, int n_prefix, int npix, int l2,
+                                                        __bf16 *__restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t tok = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (tok >= (int64_t)B * npix) return;
+    const int b = (int)(tok / npix), pi = (int)(tok - (int64_t)b * npix);
+    const float *xr = x + ((int64_t)b * T + n_prefix + pi) * C;
+    float scale = 1.f;
+    if (l2) {
+        float s = 0.f;
+        for (int c = lane; c < C; c += 64) s = fmaf(xr[c], xr[c], s);
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off);
+        scale = 1.f / fmaxf(sqrtf(s), 1e-12f);
+    }
+    for (int c = lane; c < C; c += 64) out[tok * C + c] = (__bf16)(xr[c] * scale);
+}
+
+// F.interpolate(scale_factor=2, mode="bilinear", align_corners=True) on NHWC bf16, one
+// thread per (output pixel, 8 channels); source coordinate = dst * (in - 1) / (out - 1) in
+// f32, lambda weights as aten's upsample_bilinear2d.
+__global__ void __launch_bounds__(256) k_upsample2x(const __bf16 *__restrict__ in, int B, int H,
+                                                    int W, int C, __bf16 *__restrict__ out) {
+    const int OH = 2 * H, OW = 2 * W, C8 = C / 8;
+    const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (gid >= (int64_t)B * OH * OW * C8) return;
+    const int c8 = (int)(gid % C8);
+    const int64_t pix = gid / C8;
+    const int ox = (int)(pix % OW);
+    const int64_t t = pix / OW;
+    const int oy = (int)(t % OH), b = (int)(t / OH);
+    const float sh = OH > 1 ? (float)(H - 1) / (float)(OH - 1) : 0.f;
+    const float sw = OW > 1 ? (float)(W - 1) / (float)(OW - 1) : 0.f;
+    const float fy = sh * (float)oy, fx = sw * (float)ox;
+    const int y0 = (int)fy, x0 = (int)fx;
+    const int yp = y0 < H - 1 ? 1 : 0, xp = x0 < W - 1 ? 1 : 0;
+    const float ly = fy - (float)y0, lx = fx - (float)x0;
+    const float hy = 1.f - ly, hx = 1.f - lx;
+    const __bf16 *base = in + ((int64_t)b * H * W) * C + c8 * 8;
+    const bf16x8 v00 = *(const bf16x8 *)(base + ((int64_t)y0 * W + x0) * C);
+    const bf16x8 v01 = *(const bf16x8 *)(base + ((int64_t)y0 * W + x0 + xp) * C);
+    const bf16x8 v10 = *(const bf16x8 *)(base + ((int64_t)(y0 + yp) * W + x0) * C);
+    const bf16x8 v11 = *(const bf16x8 *)(base + ((int64_t)(y0 + yp) * W + x0 + xp) * C);
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        o[j] = (__bf16)(hy * (hx * (float)v00[j] + lx * (float)v01[j]) +
+                        ly * (hx * (float)v10[j] + lx * (float)v11[j]));
+    *(bf16x8 *)(out + pix * C + c8 * 8) = o;
+}
+
 // ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
-template <int BM, int BN, int BK>
+template <int BM, int BN, int BK, bool CONV>
 static void vt_launch_gemm(const sd_gemm_args &g, hipStream_t s) {
     dim3 grid((unsigned)((g.N + BN - 1) / BN), (unsigned)((g.M + BM - 1) / BM));
     switch (g.epi) {
-    case SD_EPI_BF16: hipLaunchKernelGGL((k_gemm<BM, BN, BK, SD_EPI_BF16>), grid, dim3(256), 0, s, g); break;
-    case SD_EPI_GELU: hipLaunchKernelGGL((k_gemm<BM, BN, BK, SD_EPI_GELU>), grid, dim3(256), 0, s, g); break;
-    case SD_EPI_F32: hipLaunchKernelGGL((k_gemm<BM, BN, BK, SD_EPI_F32>), grid, dim3(256), 0, s, g); break;
-    case SD_EPI_RESID: hipLaunchKernelGGL((k_gemm<BM, BN, BK, SD_EPI_RESID>), grid, dim3(256), 0, s, g); break;
-    case SD_EPI_QKV: hipLaunchKernelGGL((k_gemm<BM, BN, BK, SD_EPI_QKV>), grid, dim3(256), 0, s, g); break;
-    default: hipLaunchKernelGGL((k_gemm<BM, BN, BK, SD_EPI_PATCH>), grid, dim3(256), 0, s, g); break;
+    case SD_EPI_BF16: hipLaunchKernelGGL((k_gemm<BM, BN, BK, SD_EPI_BF16, CONV>), grid, dim3(256), 0, s, g); break;
+    case SD_EPI_GELU: hipLaunchKernelGGL((k_gemm<BM, BN, BK, SD_EPI_GELU, CONV>), grid, dim3(256), 0, s, g); break;
+    case SD_EPI_F32: hipLaunchKernelGGL((k_gemm<BM, BN, BK, SD_EPI_F32, CONV>), grid, dim3(256), 0, s, g); break;
+    case SD_EPI_RESID: hipLaunchKernelGGL((k_gemm<BM, BN, BK, SD_EPI_RESID, CONV>), grid, dim3(256), 0, s, g); break;
+    case SD_EPI_QKV: hipLaunchKernelGGL((k_gemm<BM, BN, BK, SD_EPI_QKV, CONV>), grid, dim3(256), 0, s, g); break;
+    case SD_EPI_SHUF: hipLaunchKernelGGL((k_gemm<BM, BN, BK, SD_EPI_SHUF, CONV>), grid, dim3(256), 0, s, g); break;
+    case SD_EPI_NCHW: hipLaunchKernelGGL((k_gemm<BM, BN, BK, SD_EPI_NCHW, CONV>), grid, dim3(256), 0, s, g); break;
+    default: hipLaunchKernelGGL((k_gemm<BM, BN, BK, SD_EPI_PATCH, CONV>), grid, dim3(256), 0, s, g); break;
+    }
+}
+
+template <bool CONV>
+static void vt_pick_gemm(const sd_gemm_args &g, hipStream_t s) {
+    // K steps of 64 whenever K allows (half the barriers, twice the work under each
+    // prefetch); 128x128 tiles once they fill the chip, else 64x64
+    const int64_t big = ((g.M + 127) / 128) * ((g.N + 127) / 128);
+    if (g.K % 64 == 0) {
+        if (big >= 256)
+            vt_launch_gemm<128, 128, 64, CONV>(g, s);
+        else
+            vt_launch_gemm<64, 64, 64, CONV>(g, s);
+    } else {
+        if (big >= 256)
+            vt_launch_gemm<128, 128, 32, CONV>(g, s);
+        else
+            vt_launch_gemm<64, 64, 32, CONV>(g, s);
     }
 }
 
@@ -556,9 +691,18 @@ extern "C" int sd_gemm(const sd_gemm_args *args, void *stream) {
     }
     const sd_gemm_args &g = *args;
     bool ok = g.a && g.w && g.M >= 0 && g.N > 0 && g.K > 0 && g.K % GK == 0 && g.lda >= g.K &&
-              g.lda % 8 == 0 && g.epi >= SD_EPI_BF16 && g.epi <= SD_EPI_PATCH &&
+              g.lda % 8 == 0 && g.epi >= SD_EPI_BF16 && g.epi <= SD_EPI_NCHW &&
               g.M * (int64_t)g.lda < ((int64_t)1 << 31) && g.N * g.K < ((int64_t)1 << 31);
-    if (g.epi == SD_EPI_QKV)
+    if (g.conv)
+        ok = ok && g.H > 0 && g.W > 0 && g.Cin > 0 && g.Cin % 64 == 0 && g.K == 9LL * g.Cin &&
+             g.stride >= 1 && g.OH > 0 && g.OW > 0 && g.M % ((int64_t)g.OH * g.OW) == 0 &&
+             (g.M / ((int64_t)g.OH * g.OW)) * g.H * g.W * g.Cin < ((int64_t)1 << 30);
+    if (g.epi == SD_EPI_SHUF)
+        ok = ok && g.out && g.shuf_k > 0 && g.N % (g.shuf_k * g.shuf_k) == 0 && g.in_h > 0 &&
+             g.in_w > 0 && g.M % ((int64_t)g.in_h * g.in_w) == 0;
+    else if (g.epi == SD_EPI_NCHW)
+        ok = ok && g.out && g.tokens > 0 && g.M % g.tokens == 0;
+    else if (g.epi == SD_EPI_QKV)
         ok = ok && g.q && g.k && g.vt && g.head_dim > 0 && g.heads > 0 && g.tokens > 0 &&
              g.tokens_pad >= g.tokens && g.N == 3LL * g.heads * g.head_dim &&
              g.M % g.tokens == 0;
@@ -573,21 +717,10 @@ extern "C" int sd_gemm(const sd_gemm_args *args, void *stream) {
     }
     if (g.M == 0) return 0;
     hipStream_t s = (hipStream_t)stream;
-    // 128x128 tiles once they fill the chip, else 64x64 (ViT-S-sized token counts)
-    const int64_t big = ((g.M + 127) / 128) * ((g.N + 127) / 128);
-    // K steps of 64 whenever K allows (half the barriers, twice the work under each
-    // prefetch); 128x128 tiles once they fill the chip, else 64x64
-    if (g.K % 64 == 0) {
-        if (big >= 256)
-            vt_launch_gemm<128, 128, 64>(g, s);
-        else
-            vt_launch_gemm<64, 64, 64>(g, s);
-    } else {
-        if (big >= 256)
-            vt_launch_gemm<128, 128, 32>(g, s);
-        else
-            vt_launch_gemm<64, 64, 32>(g, s);
-    }
+    if (g.conv)
+        vt_pick_gemm<true>(g, s);
+    else
+        vt_pick_gemm<false>(g, s);
     if (hipGetLastError() != hipSuccess) {
         sd_set_error("sd_gemm: launch failed");
         return -2;
@@ -687,6 +820,40 @@ extern "C" int sd_tokens_to_grid(const float *x, int32_t B, int32_t T, int32_t C
                        (hipStream_t)stream, x, B, T, C, n_prefix, gh, gw, l2norm, out);
     if (hipGetLastError() != hipSuccess) {
         sd_set_error("sd_tokens_to_grid: launch failed");
+        return -2;
+    }
+    return 0;
+}
+
+extern "C" int sd_tokens_to_nhwc(const float *x, int32_t B, int32_t T, int32_t C,
+                                 int32_t n_prefix, int32_t npix, int32_t l2norm, void *out,
+                                 void *stream) {
+    if (!x || !out || B <= 0 || C <= 0 || n_prefix < 0 || npix <= 0 ||
+        (int64_t)n_prefix + npix > T) {
+        sd_set_error("sd_tokens_to_nhwc: invalid argument");
+        return -1;
+    }
+    const int64_t n = (int64_t)B * npix;
+    hipLaunchKernelGGL(k_tokens_to_nhwc, dim3((unsigned)((n + 3) / 4)), dim3(256), 0,
+                       (hipStream_t)stream, x, B, T, C, n_prefix, npix, l2norm, (__bf16 *)out);
+    if (hipGetLastError() != hipSuccess) {
+        sd_set_error("sd_tokens_to_nhwc: launch failed");
+        return -2;
+    }
+    return 0;
+}
+
+extern "C" int sd_upsample2x(const void *in, int32_t B, int32_t H, int32_t W, int32_t C,
+                             void *out, void *stream) {
+    if (!in || !out || B <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 8) {
+        sd_set_error("sd_upsample2x: invalid argument (C % 8 == 0)");
+        return -1;
+    }
+    const int64_t n = (int64_t)B * 4 * H * W * (C / 8);
+    hipLaunchKernelGGL(k_upsample2x, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, (const __bf16 *)in, B, H, W, C, (__bf16 *)out);
+    if (hipGetLastError() != hipSuccess) {
+        sd_set_error("sd_upsample2x: launch failed");
         return -2;
     }
     return 0;

@@ -436,8 +436,48 @@ def fx_voxel_points():
                    "slice_stride": 2049, "slice": pts[sel].tolist()}, f)
 
 
+def det_fill(module, seed):
+    """Deterministic parameter fill by sorted state_dict name (shared with tests/test_dpt.py):
+    weights N(0, 1/fan) with fan = numel of one output slice, vectors N(0, 0.05^2)."""
+    g = torch.Generator().manual_seed(seed)
+    sd = module.state_dict()
+    with torch.no_grad():
+        for name in sorted(sd):
+            t = sd[name]
+            if t.dim() > 1:
+                t.copy_(torch.randn(t.shape, generator=g) / float(t[0].numel()) ** 0.5)
+            else:
+                t.copy_(0.05 * torch.randn(t.shape, generator=g))
+
+
+def fx_dpt():
+    """The reference's DPTHead (dpt_head.py:179-236, only torch imports) with the shipped
+    decoder shape (embed 384 = ViT-S, post_process_channels [64, 64, 128, 256], d_out 256,
+    configs/model/dino_downsampler.yaml:22-25) on a 2 x 4 token grid."""
+    sys.path.insert(0, REF)
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "ref_dpt_head", os.path.join(REF, "scenedino/models/backbones/dino/dpt_head.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    head = mod.DPTHead(embed_dims=384, post_process_channels=[64, 64, 128, 256],
+                       readout_type="ignore", patch_size=16, d_out=256, expand_channels=False).eval()
+    det_fill(head, 70)
+    g = torch.Generator().manual_seed(71)
+    inputs = [torch.randn(1, 384, 2, 4, generator=g) for _ in range(4)]
+    with torch.no_grad():
+        out = head(inputs)[0]
+    np.savez_compressed(os.path.join(HERE, "dpt_head.npz"),
+                        **{f"in{i}": np32(x) for i, x in enumerate(inputs)},
+                        out=np32(out).astype(np.float16), out_norm=np.float64(out.double().norm()))
+
+
 def main():
     torch.set_num_threads(8)
+    if os.environ.get("GOLDEN_ONLY") == "dpt":
+        fx_dpt()
+        print("dpt fixture written to", HERE)
+        return
     if os.environ.get("GOLDEN_ONLY") == "seg":
         _install_stubs()
         fx_seg_head()
