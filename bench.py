@@ -315,6 +315,83 @@ def main_vit(args, world, rank, device):
         }), flush=True)
 
 
+def dpt_flops(head, gh, gw):
+    """Algorithmic FLOPs of one DPTHead pass on a (gh, gw) token grid (2 MACs per
+    multiply-add; convolutions as their dense products, ConvTranspose(k, k) as k^2 C_in
+    C_out per input pixel, bilinear resizes not counted)."""
+    post, d = head.post_process_channels, head.d_out
+    C = head.reassemble_blocks.projects[0].in_channels
+    c3 = lambda h, w, ci, co: 2 * h * w * 9 * ci * co
+    fl = sum(2 * gh * gw * C * c for c in post)
+    fl += 2 * gh * gw * post[0] ** 2 * 16 + 2 * gh * gw * post[1] ** 2 * 4
+    h3, w3 = (gh + 1) // 2, (gw + 1) // 2
+    fl += c3(h3, w3, post[3], post[3])
+    sizes = [(4 * gh, 4 * gw), (2 * gh, 2 * gw), (gh, gw), (h3, w3)]
+    fl += sum(c3(h, w, c, d) for (h, w), c in zip(sizes, post))
+    h, w = h3, w3
+    for i in range(len(head.fusion_blocks)):
+        fl += (2 if i == 0 else 4) * c3(h, w, d, d)  # rcu2 (+ rcu1)
+        h, w = 2 * h, 2 * w
+        fl += 2 * h * w * d * d  # project 1x1
+    fl += 2 * c3(h, w, d, d)  # project + head0
+    fl += 2 * h * w * d * d * 4  # head1 ConvTranspose(2, 2)
+    return fl + c3(2 * h, 2 * w, d, d)  # head2
+
+
+def main_encode(args, world, rank, device):
+    """The SceneDINO image encoder's prediction pass (DINOv2Module.forward: ViT -> DPT ->
+    NCHW f32 feature grid) on one 192x640 frame, random weights, as configs/model/
+    dino_downsampler.yaml builds it (ViT-B/8, DPT num_ch_enc [64, 64, 128, 256], d_out 256)
+    and with the ViT-S/16 of BASELINE configs[1].  One HIP graph per pass, output cloned
+    (the reference's fresh tensor)."""
+    from scenedino_amd.models.backbones import make_backbone
+    results = {}
+    for name, (arch, ver) in {"vit-s16": ("vit-s", "v1_16"), "vit-b8": ("vit-b", "v1")}.items():
+        torch.manual_seed(0)
+        conf = dict(type="dinov2", mode="downsample-prediction", decoder_arch="dpt",
+                    downsampler_arch="featup", encoder_arch=arch, version=ver,
+                    separate_gt_version=None, encoder_freeze=True, flip_avg_gt=False,
+                    dim_reduction_arch="mlp", num_ch_enc=[64, 64, 128, 256],
+                    intermediate_features=[3, 6, 9], decoder_out_dim=256, dino_pca_dim=64,
+                    image_size=[H, W], key_features=False)
+        m = make_backbone(conf).to(device).eval()
+        img = (torch.rand(1, 3, H, W, generator=torch.Generator().manual_seed(rank)) * 2 - 1).to(device)
+        with torch.no_grad():
+            for _ in range(args.warmup):
+                m(img)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                m(img)
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / args.steps
+            out_shape = list(m(img)[0].shape)
+        vit = m.encoder.model.vit
+        p, C = vit.patch_size, vit.embed_dim
+        gh, gw = H // p, W // p
+        fv = vit_flops(gh * gw + 1, C, len(vit.blocks), p, gh * gw)
+        fd = dpt_flops(m.decoder, gh, gw)
+        results[name] = {"ms_per_pass": dt * 1e3, "out_shape": out_shape,
+                         "gflop_vit": fv / 1e9, "gflop_dpt": fd / 1e9,
+                         "tflops": (fv + fd) / dt / 1e12,
+                         "frac_bf16_peak": (fv + fd) / dt / 1e12 / PEAK_TFLOPS["bf16"]}
+        del m
+        torch.cuda.empty_cache()
+    if rank == 0:
+        print(json.dumps({
+            "metric": "SceneDINO encoder passes/sec (ViT + DPT, 192x640 frame)",
+            "value": 1e3 / results["vit-b8"]["ms_per_pass"], "unit": "passes/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "higher_is_better": True, "dtype": "bf16", "data": "synthetic, random weights",
+            "config": {"workload": "DINOv2Module prediction pass (ViT-B/8 + DPT, "
+                                   "configs/model/dino_downsampler.yaml)"},
+            "models": results,
+            "roofline": {"kernel": "k_gemm (+ k_attn), ViT-B/8 + DPT", "bound": "mfma",
+                         "achieved": results["vit-b8"]["tflops"], "peak": PEAK_TFLOPS["bf16"],
+                         "unit": "TFLOP/s", "frac": results["vit-b8"]["frac_bf16_peak"]},
+        }), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -325,11 +402,11 @@ def main():
     ap.add_argument("--mode", default="proj", choices=["proj", "grid"],
                     help="16-bit render kernel: projected grid (default) or per-sample grid")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--config", default="c2", choices=["c2", "c4", "c5", "vit"],
+    ap.add_argument("--config", default="c2", choices=["c2", "c4", "c5", "vit", "encode"],
                     help="c2: BASELINE configs[1] (K=64, D=64, the metric's config); c4: "
                          "configs[3] render shape (K=128, 384-d feature field); c5: "
                          "configs[4] SSCBench voxel query (voxels/s); vit: the DINO ViT "
-                         "encoder forward (a19)")
+                         "encoder forward (a19); encode: ViT + DPT decoder (DINOv2Module)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     args = ap.parse_args()
     global K_SAMPLES, D_DINO
@@ -348,11 +425,13 @@ def main():
 
     from scenedino_amd import _lib
     _lib.load()
-    if args.config in ("c5", "vit"):
+    if args.config in ("c5", "vit", "encode"):
         if args.config == "c5":
             main_c5(args, world, rank, local_rank, dist, device)
-        else:
+        elif args.config == "vit":
             main_vit(args, world, rank, device)
+        else:
+            main_encode(args, world, rank, device)
         if dist:
             tdist.barrier()
             tdist.destroy_process_group()

@@ -7,10 +7,11 @@ from .prediction_heads import make_head
 def make_model(config, downstream_config=None, encoder=None, downstream_head=None):
     """Build BTSNet from the reference's model config.
 
-    The image encoder (DINO/DINOv2 ViT + DPT decoder) is passed in as ``encoder``
-    (any module exposing ``latent_size``, ``extra_outs``, ``forward(x,
-    ground_truth=False) -> [grid]`` and ``expand_dim``); building the ViT from
-    ``config['encoder']`` is a later row of the scope table.
+    As the reference, the encoder is built from ``config['encoder']``
+    (backbones.make_backbone -> DINOv2Module: ViT + DPT on the gfx950 kernels) and the
+    downstream head from ``downstream_config``; ``encoder`` / ``downstream_head`` may be
+    passed in instead (any module exposing ``latent_size``, ``extra_outs``,
+    ``forward(x, ground_truth=False) -> [grid]`` and ``expand_dim``).
     """
     arch = config.get("arch", "BTSNet")
     if arch != "BTSNet":
@@ -25,9 +26,11 @@ def make_model(config, downstream_config=None, encoder=None, downstream_head=Non
     else:
         d_out = 4
     if encoder is None:
-        raise NotImplementedError(
-            "scenedino_amd.make_model: pass encoder=<module>; the ViT/DPT encoder builder "
-            f"for {config.get('encoder', {}).get('type')!r} is not part of this build yet")
+        from .backbones import make_backbone
+        encoder = make_backbone(config["encoder"])
+    if downstream_head is None and downstream_config is not None:
+        from ..downstream_head import make_downstream_head
+        downstream_head = make_downstream_head(downstream_config)
     code_xyz = PositionalEncoding.from_conf(config["code"], d_in=3)
     d_in = encoder.latent_size + code_xyz.d_out
     if config.get("split_dino_heads", False):

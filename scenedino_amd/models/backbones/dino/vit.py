@@ -127,10 +127,12 @@ def _param_key(m: nn.Module):
 
 
 def vit_forward(vit: VisionTransformer, images: torch.Tensor, packed: _Packed,
-                intermediate: List[int]):
+                intermediate: List[int], nhwc: bool = False):
     """images (B, 3, H, W) in [-1, 1] (DINOv2Encoder input, before _normalize_input) ->
-    (intermediate block outputs as (B, C, gh, gw) grids, final-norm tokens L2-normalised as
-    a grid).  Every arithmetic step is a libsdhip.so kernel."""
+    (intermediate block outputs as (B, C, gh, gw) f32 grids, final-norm tokens
+    L2-normalised as a grid).  ``nhwc=True`` returns (B, gh, gw, C) bf16 grids instead: the
+    DPT decoder's operand layout, written straight from the token rows.  Every arithmetic
+    step is a libsdhip.so kernel."""
     if torch.is_grad_enabled() and vit.training:
         raise NotImplementedError("scenedino_amd ViT: no backward kernels; use no_grad / eval")
     B, _, H, W = images.shape
@@ -160,6 +162,7 @@ def vit_forward(vit: VisionTransformer, images: torch.Tensor, packed: _Packed,
     ao = torch.empty(B * T, C, device=dev, dtype=bf)
     hid = torch.empty(B * T, packed.blocks[0]["fc1_w"].shape[0], device=dev, dtype=bf)
     grids = []
+    to_grid = _lib.tokens_to_nhwc if nhwc else _lib.tokens_to_grid
     scale = hd ** -0.5
     for i, blk in enumerate(packed.blocks):
         _lib.layernorm(x, blk["n1w"], blk["n1b"], 1e-6, xn)
@@ -171,10 +174,10 @@ def vit_forward(vit: VisionTransformer, images: torch.Tensor, packed: _Packed,
         _lib.gemm(xn, blk["fc1_w"], blk["fc1_b"], _lib.SD_EPI_GELU, out=hid)
         _lib.gemm(hid, blk["fc2_w"], blk["fc2_b"], _lib.SD_EPI_RESID, out=x, gamma=blk["ls2"])
         if i in intermediate:
-            grids.append(_lib.tokens_to_grid(x, B, T, C, 1, gh, gw, False))
+            grids.append(to_grid(x, B, T, C, 1, gh, gw, False))
     xf = torch.empty(B * T, C, device=dev)
     _lib.layernorm(x, packed.nw, packed.nb, 1e-6, xf)
-    final = _lib.tokens_to_grid(xf, B, T, C, 1, gh, gw, True)
+    final = to_grid(xf, B, T, C, 1, gh, gw, True)
     return grids, final
 
 
