@@ -81,8 +81,17 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
     // LDS rows padded by 16 B: row stride (BK + 8) * 2 B puts the 16 rows a ds_read_b128
     // lane group touches on 16 distinct 4-bank groups
     constexpr int GLDS = BK + 8;
-    __shared__ __attribute__((aligned(16))) __bf16 sA[2][BM * GLDS];
-    __shared__ __attribute__((aligned(16))) __bf16 sB[2][BN * GLDS];
+    // Output-staged epilogues: the fp32 tile goes through LDS (reusing the operand
+    // buffers) so that global stores are 16-B vectors along the output's contiguous axis
+    // (pixels for NCHW, channels otherwise) instead of 2-B lane scatters.
+    constexpr bool STAGED = EPI == SD_EPI_BF16 || EPI == SD_EPI_GELU || EPI == SD_EPI_SHUF ||
+                            EPI == SD_EPI_NCHW;
+    constexpr int OST = EPI == SD_EPI_NCHW ? BN + 1 : BN + 8;  // fp32 words per staged row
+    constexpr int KL_BYTES = 2 * (BM + BN) * GLDS * 2;
+    constexpr int EP_BYTES = STAGED ? BM * OST * 4 : 0;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[KL_BYTES > EP_BYTES ? KL_BYTES : EP_BYTES];
+#define SA(buf) ((__bf16 *)smem + (buf) * (BM * GLDS))
+#define SB(buf) ((__bf16 *)smem + 2 * BM * GLDS + (buf) * (BN * GLDS))
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
@@ -162,12 +171,12 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
 #pragma unroll
         for (int c = 0; c < CA; ++c) {
             const int ch = tid + 256 * c, row = ch / CPR, col = (ch % CPR) * 8;
-            *(bf16x8 *)&sA[buf][row * GLDS + col] = (CONV && g.relu_in) ? vt_relu8(ra[c]) : ra[c];
+            *(bf16x8 *)&SA(buf)[row * GLDS + col] = (CONV && g.relu_in) ? vt_relu8(ra[c]) : ra[c];
         }
 #pragma unroll
         for (int c = 0; c < CB; ++c) {
             const int ch = tid + 256 * c, row = ch / CPR, col = (ch % CPR) * 8;
-            *(bf16x8 *)&sB[buf][row * GLDS + col] = rb[c];
+            *(bf16x8 *)&SB(buf)[row * GLDS + col] = rb[c];
         }
     };
 
@@ -188,10 +197,10 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
             bf16x8 af[TM], bfr[TN];
 #pragma unroll
             for (int i = 0; i < TM; ++i)
-                af[i] = *(const bf16x8 *)&sA[buf][(wm * WM + i * 32 + r) * GLDS + 16 * s + 8 * h];
+                af[i] = *(const bf16x8 *)&SA(buf)[(wm * WM + i * 32 + r) * GLDS + 16 * s + 8 * h];
 #pragma unroll
             for (int j = 0; j < TN; ++j)
-                bfr[j] = *(const bf16x8 *)&sB[buf][(wn * WN + j * 32 + r) * GLDS + 16 * s + 8 * h];
+                bfr[j] = *(const bf16x8 *)&SB(buf)[(wn * WN + j * 32 + r) * GLDS + 16 * s + 8 * h];
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -211,6 +220,117 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
     }
 
     // epilogue: accumulator register q of tile (i, j): row (q&3)+8(q>>2)+4h, column r
+    if constexpr (STAGED) {
+        // phase 1: v = acc + bias (GELU) -> fp32 tile [m][n] in LDS (the K loop ended on a
+        // barrier, every wave is done with the operand tiles)
+        float *sT = (float *)smem;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int nl = wn * WN + j * 32 + r;
+            const float bias = (g.bias && n0 + nl < g.N) ? g.bias[n0 + nl] : 0.f;
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const int ml = wm * WM + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+                    float v = acc[i][j][q] + bias;
+                    if (EPI == SD_EPI_GELU) v = vt_gelu(v);
+                    sT[ml * OST + nl] = v;
+                }
+        }
+        __syncthreads();
+        if constexpr (EPI == SD_EPI_NCHW) {
+            // phase 2: thread = 4 consecutive pixels of one channel -> one 16-B store
+            const int plane = g.tokens;
+            const bool vec = (plane & 3) == 0;
+#pragma unroll 4
+            for (int t = tid; t < BN * (BM / 4); t += 256) {
+                const int nl = t / (BM / 4), ml = (t - nl * (BM / 4)) * 4;
+                const int64_t n = n0 + nl, m = m0 + ml;
+                if (n >= g.N || m >= g.M) continue;
+                float v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) v[u] = sT[(ml + u) * OST + nl];
+                const uint32_t b = (uint32_t)m / (uint32_t)plane;
+                const int64_t pix = m - (int64_t)b * plane;
+                float *dst = (float *)g.out + ((int64_t)b * g.N + n) * plane + pix;
+                if (vec && m + 3 < g.M) {
+                    *(vf4 *)dst = vf4{v[0], v[1], v[2], v[3]};
+                } else {
+                    for (int u = 0; u < 4 && m + u < g.M; ++u) {
+                        const uint32_t bu = (uint32_t)(m + u) / (uint32_t)plane;
+                        const int64_t pu = m + u - (int64_t)bu * plane;
+                        ((float *)g.out)[((int64_t)bu * g.N + n) * plane + pu] = v[u];
+                    }
+                }
+            }
+        } else {
+            // phase 2: thread = 8 consecutive columns of one row -> one 16-B bf16 store
+            const int cout = EPI == SD_EPI_SHUF ? (int)(g.N / (g.shuf_k * g.shuf_k)) : 0;
+            const bool vec = EPI == SD_EPI_SHUF ? (cout & 7) == 0 : (g.ldo & 7) == 0;
+#pragma unroll 4
+            for (int t = tid; t < BM * (BN / 8); t += 256) {
+                const int ml = t / (BN / 8), nl = (t - ml * (BN / 8)) * 8;
+                const int64_t m = m0 + ml, n = n0 + nl;
+                if (m >= g.M || n >= g.N) continue;
+                const vf4 lo = *(const vf4 *)&sT[ml * OST + nl];
+                const vf4 hi = *(const vf4 *)&sT[ml * OST + nl + 4];
+                float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                const bool full = vec && n + 8 <= g.N;
+                if (EPI == SD_EPI_BF16 && full) {
+                    if (g.res) {
+                        const bf16x8 a = *(const bf16x8 *)((const __bf16 *)g.res + m * g.ldo + n);
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) v[u] += (float)a[u];
+                    }
+                    if (g.res2) {
+                        const bf16x8 a = *(const bf16x8 *)((const __bf16 *)g.res2 + m * g.ldo + n);
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) v[u] += (float)a[u];
+                    }
+                } else if (EPI == SD_EPI_BF16 && (g.res || g.res2)) {
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        if (n + u >= g.N) break;
+                        if (g.res) v[u] += (float)((const __bf16 *)g.res)[m * g.ldo + n + u];
+                        if (g.res2) v[u] += (float)((const __bf16 *)g.res2)[m * g.ldo + n + u];
+                    }
+                }
+                int64_t base;  // element index of column n of row m
+                if (EPI == SD_EPI_SHUF) {
+                    const int kk = g.shuf_k, hw = g.in_h * g.in_w;
+                    const int b = (int)((uint32_t)m / (uint32_t)hw);
+                    const int pix = (int)(m - (int64_t)b * hw);
+                    const int y = pix / g.in_w, x = pix - y * g.in_w;
+                    if (full) {
+                        const int sub = (int)(n / cout), co = (int)(n - (int64_t)sub * cout);
+                        const int dy = sub / kk, dx = sub - dy * kk;
+                        base = (((int64_t)b * g.in_h * kk + y * kk + dy) * (g.in_w * kk) + x * kk + dx) *
+                                   cout + co;
+                    } else {
+                        for (int u = 0; u < 8 && n + u < g.N; ++u) {
+                            const int sub = (int)((n + u) / cout), co = (int)(n + u - (int64_t)sub * cout);
+                            const int dy = sub / kk, dx = sub - dy * kk;
+                            ((__bf16 *)g.out)[(((int64_t)b * g.in_h * kk + y * kk + dy) * (g.in_w * kk) +
+                                               x * kk + dx) * cout + co] = (__bf16)v[u];
+                        }
+                        continue;
+                    }
+                } else {
+                    base = m * g.ldo + n;
+                }
+                if (full) {
+                    bf16x8 o;
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) o[u] = (__bf16)v[u];
+                    *(bf16x8 *)((__bf16 *)g.out + base) = o;
+                } else {
+                    for (int u = 0; u < 8 && n + u < g.N; ++u) ((__bf16 *)g.out)[base + u] = (__bf16)v[u];
+                }
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         const int64_t n = n0 + wn * WN + j * 32 + r;
@@ -315,6 +435,9 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
             }
     }
 }
+
+#undef SA
+#undef SB
 
 // ---------------------------------------------------------------------------
 // flash attention (head_dim 64)
