@@ -8,7 +8,8 @@ Mirror of scenedino/models/backbones/dino/dinov2_module.py:19-222 (``build_*`` h
 DPT decoder (same kernels, NHWC bf16) -> NCHW f32 feature grid -- is one HIP graph per
 (input shape, parameter version): the intermediate token grids go to the decoder in its
 NHWC operand layout without a transposition, and the ~170 launches of a 192x640 frame are
-replayed by one graph launch.
+replayed by one graph launch (the DPT's last convolution is launched after the replay so
+that it writes the caller's fresh output tensor).
 
 Out of scope (training-loss machinery, SURVEY §8 "out"): the feature-upsampling GT
 wrappers of ``mode="upsample-gt"`` (upsampler.py, kornia) and the ``featup`` /
@@ -153,8 +154,9 @@ class DINOv2Module(nn.Module):
         self._graph = None
 
     # -- prediction pass --------------------------------------------------------
-    def _decode(self, x):
-        """ViT -> decoder, eager.  DPT: NHWC bf16 token grids straight into the decoder."""
+    def _decode(self, x, last: bool = True):
+        """ViT -> decoder, eager.  DPT: NHWC bf16 token grids straight into the decoder
+        (``last=False``: stop before the DPT's final convolution, see _predict)."""
         enc = self.encoder
         if enc.resize is not None:
             x = F.interpolate(x, size=enc.resize, mode="bilinear", align_corners=False,
@@ -162,13 +164,14 @@ class DINOv2Module(nn.Module):
         vit = enc.model
         if isinstance(self.decoder, DPTHead):
             grids, final = vit_forward(vit.vit, x, vit.packed(), vit.intermediate, nhwc=True)
-            return self.decoder.forward_nhwc(grids + [final])
+            return self.decoder.forward_nhwc(grids + [final], last=last)
         grids, final = vit_forward(vit.vit, x, vit.packed(), vit.intermediate)
         return self.decoder(grids + [final])
 
     def _predict(self, x):
         if not self.use_graph or not x.is_cuda:
             return self._decode(x)
+        dpt = isinstance(self.decoder, DPTHead)
         key = (tuple(x.shape), str(x.device), _param_key(self.encoder), _param_key(self.decoder))
         if self._graph is None or self._graph[0] != key:
             self._graph = None
@@ -176,15 +179,17 @@ class DINOv2Module(nn.Module):
             side = torch.cuda.Stream(device=x.device)
             side.wait_stream(torch.cuda.current_stream(x.device))
             with torch.cuda.stream(side):  # warm-up (packing, allocations) outside capture
-                self._decode(static_in)
+                self._decode(static_in, last=not dpt)
             torch.cuda.current_stream(x.device).wait_stream(side)
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
-                outs = self._decode(static_in)
+                outs = self._decode(static_in, last=not dpt)
             self._graph = (key, graph, static_in, outs)
         _, graph, static_in, outs = self._graph
         static_in.copy_(x)
         graph.replay()
+        if dpt:  # the final convolution writes a fresh output (no copy of a graph buffer)
+            return self.decoder.forward_last(outs)
         return [o.clone() for o in outs]
 
     def forward(self, x, ground_truth: bool = False):

@@ -147,8 +147,11 @@ class DPTHead(nn.Module):
         self._packed = (key, P)
         return P
 
-    def forward_nhwc(self, xs):
-        """xs: 4 NHWC bf16 tensors (B, h, w, embed) -> [NCHW f32 (B, d_out, H, W)]."""
+    def forward_nhwc(self, xs, last: bool = True):
+        """xs: 4 NHWC bf16 tensors (B, h, w, embed) -> [NCHW f32 (B, d_out, H, W)].
+        ``last=False`` stops before the final convolution and returns its NHWC bf16 input
+        (``forward_last`` applies it: the graph-captured pass leaves that one launch out,
+        so its output is a fresh tensor instead of a copy of a graph-owned buffer)."""
         if torch.is_grad_enabled() and self.training:
             raise NotImplementedError("scenedino_amd DPT: no backward kernels; use no_grad / eval")
         L = _lib
@@ -191,8 +194,12 @@ class DPTHead(nn.Module):
         out = L.conv3x3(out, *P["head0"])
         wt, bt, k = P["head1"]
         out = L.linear_nhwc(out, wt, bt, shuf=k)
-        w2, b2 = P["head2"]
-        return [L.conv3x3(out, w2, b2, epi=L.SD_EPI_NCHW)]
+        return self.forward_last(out) if last else out
+
+    def forward_last(self, x):
+        """output_head.head_modules[2] (3x3 conv) on NHWC bf16 -> [NCHW f32 grid]."""
+        w2, b2 = self._pack()["head2"]
+        return [_lib.conv3x3(x, w2, b2, epi=_lib.SD_EPI_NCHW)]
 
     def forward(self, inputs):
         """dpt_head.py:226-236: list of 4 NCHW grids -> [NCHW f32 grid]."""

@@ -79,6 +79,8 @@ class BTSNet(nn.Module):
         self._packed_key = None
         self._grid_cache = None
         self._grid_key = None
+        self._loss_features = None
+        self._loss_pending = None
         self.grid_c_combine = None
         self.color_frame_filter = None
         self.grid_f_extra = None
@@ -129,13 +131,10 @@ class BTSNet(nn.Module):
         if do_flip:
             images_encoder = torch.flip(images_encoder, dims=(-1,))
         lat = self.encoder(images_encoder.reshape(n_ * nv_, c_, h_, w_))
-        lat_loss = self.encoder(images_loss.reshape(n_l * nv_l, c_, h_, w_), ground_truth=True)
         if do_flip:
             lat = [torch.flip(x, dims=(-1,)) for x in lat]
         _, _, hh, ww = lat[0].shape
         lat = [F.interpolate(x, size=(hh, ww)).view(n_, nv_, -1, hh, ww) for x in lat]
-        _, _, hl, wl = lat_loss[0].shape
-        lat_loss = [x.view(n_l, nv_l, -1, hl, wl) for x in lat_loss]
         if self.extra_outs > 0:
             self.grid_f_extra = [x[:, :, -self.extra_outs:] for x in lat]
             lat = [x[:, :, :-self.extra_outs] for x in lat]
@@ -149,9 +148,29 @@ class BTSNet(nn.Module):
         self.grid_c_Ks = Ks_render
         self.grid_c_poses_w2c = poses_w2c_render
         self.grid_c_combine = None
-        self.grid_l_loss_features = lat_loss
+        # the ground-truth (loss) features: a second ViT pass (bts.py:207) that only the
+        # training loss reads -- run on first access of grid_l_loss_features (SURVEY
+        # §8(f) rank 3), so a pure render / voxel query never pays for it
+        gt_in = images_loss.reshape(n_l * nv_l, c_, h_, w_).detach().clone()
+        self._loss_pending = (gt_in, n_l, nv_l)
+        self._loss_features = None
         self.color_frame_filter = color_frame_filter
         self._grid_cache = None
+
+    @property
+    def grid_l_loss_features(self):
+        if self._loss_features is None and getattr(self, "_loss_pending", None) is not None:
+            gt_in, n_l, nv_l = self._loss_pending
+            lat_loss = self.encoder(gt_in, ground_truth=True)
+            _, _, hl, wl = lat_loss[0].shape
+            self._loss_features = [x.view(n_l, nv_l, -1, hl, wl) for x in lat_loss]
+            self._loss_pending = None
+        return self._loss_features
+
+    @grid_l_loss_features.setter
+    def grid_l_loss_features(self, value):
+        self._loss_features = value
+        self._loss_pending = None
 
     # -- device-side state for the kernels ------------------------------------
     def _dtype(self):

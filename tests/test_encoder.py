@@ -47,6 +47,34 @@ def test_from_conf_and_checkpoint_keys():
     assert shared.gt_encoder is shared.encoder and shared.encoder_frozen
 
 
+def test_encode_defers_the_ground_truth_pass():
+    """bts.py:207 runs the gt encoder inside encode(); the build runs it on the first read
+    of grid_l_loss_features (same value), so render-only callers skip it."""
+    import _helpers
+    calls = []
+
+    class Enc(_helpers.FixedGridEncoder):
+        def forward(self, x, ground_truth=False):
+            calls.append((ground_truth, tuple(x.shape)))
+            g = self.grid.expand(x.shape[0], -1, -1, -1)
+            return [g * (2.0 if ground_truth else 1.0)]
+
+    grid = torch.randn(1, 8, 6, 10)
+    net = _helpers.build_net(torch.zeros(1, 8, 6, 10), torch.zeros(128, 47), torch.zeros(128),
+                             torch.zeros(5, 128), torch.zeros(5), device="cpu")
+    net.encoder = Enc(grid)
+    imgs = torch.rand(1, 2, 3, 12, 20) * 2 - 1
+    Ks = torch.eye(3).expand(1, 2, 3, 3).contiguous()
+    poses = torch.eye(4).expand(1, 2, 4, 4).contiguous()
+    net.encode(imgs, Ks, poses, ids_encoder=[0], ids_render=[0, 1])
+    assert calls == [(False, (1, 3, 12, 20))]
+    loss = net.grid_l_loss_features
+    assert calls[1] == (True, (2, 3, 12, 20)) and len(calls) == 2
+    assert len(loss) == 1 and loss[0].shape == (1, 2, 8, 6, 10)
+    assert torch.equal(loss[0][0, 1], 2 * grid[0])
+    assert net.grid_l_loss_features is loss and len(calls) == 2  # computed once
+
+
 def test_unsupported_modes_fail_loudly():
     from scenedino_amd.models.backbones import make_backbone
     with pytest.raises(NotImplementedError):
@@ -108,3 +136,49 @@ def test_encoder_graph_replay_matches_eager(gpu):
         graph = [m(x)[0] for x in xs]
     for a, b in zip(eager, graph):
         assert torch.equal(a, b)
+
+
+MODEL_CONF = {"arch": "BTSNet", "predict_dino": True, "dino_dims": 64, "learn_empty": False,
+              "code_mode": "z", "inv_z": True, "z_near": 3, "z_far": 80, "sample_color": True,
+              "encoder": CONF, "code": {"num_freqs": 6, "freq_factor": 1.5, "include_input": True},
+              "decoder_heads": [{"type": "resnet", "name": "normal_head", "freeze": False,
+                                 "args": {"n_blocks": 0, "d_hidden": 128}}],
+              "final_prediction_head": "normal_head", "precision": "bf16"}
+
+
+@pytest.mark.gpu
+def test_make_model_encode_render_end_to_end(gpu):
+    """make_model builds the native encoder; encode() -> render reads the DPT grid exactly
+    as a fixed-grid net holding the same grid does."""
+    import _helpers
+    from scenedino_amd.models import make_model
+    from scenedino_amd.renderer import NeRFRenderer
+    from scenedino_amd.common.ray_sampler import ImageRaySampler
+    torch.manual_seed(31)
+    net = make_model(MODEL_CONF)
+    init_vit(net.encoder.encoder.model.vit, 32)
+    det_fill(net.encoder.decoder, 33)
+    net = net.to(gpu).eval()
+    g = torch.Generator().manual_seed(34)
+    imgs = (torch.rand(1, 1, 3, 64, 160, generator=g) * 2 - 1).to(gpu)
+    Ks = torch.tensor([[0.7849, 0, -0.0312], [0, 2.9391, 0.2701], [0, 0, 1]], device=gpu).view(1, 1, 3, 3)
+    poses = torch.eye(4, device=gpu).view(1, 1, 4, 4)
+    with torch.no_grad():
+        net.encode(imgs, Ks, poses, ids_encoder=[0], ids_render=[0])
+        grid = net.grid_f_features[0][:, 0]
+        assert grid.shape == (1, 256, 64, 160) and torch.isfinite(grid).all()
+        assert torch.equal(grid, net.encoder(imgs[:, 0])[0])
+        ref = _helpers.build_net(grid.cpu(), *(t.detach().cpu() for t in (
+            net.heads["normal_head"].lin_in.weight, net.heads["normal_head"].lin_in.bias,
+            net.heads["normal_head"].lin_out.weight, net.heads["normal_head"].lin_out.bias)),
+            precision="bf16", device=gpu)
+        ref.encode(imgs, Ks, poses, ids_encoder=[0], ids_render=[0])
+        rays, _ = ImageRaySampler(3, 80, 64, 160).sample(None, poses, Ks)
+        outs = []
+        for n in (net, ref):
+            r = NeRFRenderer(n_coarse=32, lindisp=True, hard_alpha_cap=False)
+            torch.manual_seed(35)
+            outs.append(r.bind_parallel(n, gpus=None).eval()(rays, want_weights=True)["coarse"])
+    for k in ("depth", "dino_features", "weights"):
+        assert torch.isfinite(outs[0][k]).all()
+        assert torch.equal(outs[0][k], outs[1][k]), k
