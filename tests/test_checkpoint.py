@@ -1,0 +1,76 @@
+"""Reference checkpoint loading (demo_utils/utils.py:52-55), on CPU.
+
+No released checkpoint travels here (remote download), so the file is synthesised in the
+reference's layout: the BTSWrapper state_dict keys (``renderer.net.*``,
+``renderer.renderer.*``) of a model built from the shipped model config, plus the keys of
+the training-only modules the build does not construct (the featup downsampler of the
+loss).  Loading must reproduce every parameter bit-for-bit in a freshly initialised model.
+"""
+import pytest
+import torch
+
+from test_encoder import MODEL_CONF
+
+DOWNSTREAM = {"type": "segmentation", "n_classes": 19, "gt_classes": 19, "input_dim": 384,
+              "code_dim": 64, "knn_neighbors": 4, "buffer_size": 256, "patch_sample_size": 576,
+              "mode": "3d", "apply_crf": False}
+
+
+def build(seed):
+    from scenedino_amd.models import make_model
+    from scenedino_amd.renderer import NeRFRenderer
+    torch.manual_seed(seed)
+    net = make_model(MODEL_CONF, DOWNSTREAM)
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for p in net.parameters():
+            p.copy_(torch.randn(p.shape, generator=g))
+    return NeRFRenderer(n_coarse=32, lindisp=True).bind_parallel(net, gpus=None)
+
+
+def reference_layout(wrapper):
+    sd = {"renderer." + k: v.clone() for k, v in wrapper.state_dict().items()}
+    sd["renderer.net.encoder.downsampler.conv.weight"] = torch.randn(8, 768, 1, 1)
+    sd["renderer.net.encoder.downsampler.conv.bias"] = torch.randn(8)
+    sd["renderer.renderer.iter_idx"] = torch.tensor(1234)
+    return sd
+
+
+def test_roundtrip_through_file(tmp_path):
+    from scenedino_amd.checkpoint import load_checkpoint
+    src = build(1)
+    sd = reference_layout(src)
+    assert any(k.startswith("renderer.net.encoder.encoder.model.vit.blocks.") for k in sd)
+    assert any(k.startswith("renderer.net.downstream_head.") for k in sd)
+    path = tmp_path / "checkpoint.pt"
+    torch.save(sd, path)
+    dst = build(2)
+    rep = load_checkpoint(dst, str(path))
+    assert not rep.missing and not rep.unexpected
+    assert sorted(rep.ignored) == ["encoder.downsampler.conv.bias", "encoder.downsampler.conv.weight"]
+    a, b = src.net.state_dict(), dst.net.state_dict()
+    assert a.keys() == b.keys()
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+    assert int(dst.renderer.iter_idx) == 1234
+    # the older {"model": ...} layout and a bare BTSNet target load the same way
+    dst2 = build(3)
+    rep2 = load_checkpoint(dst2.net, {"model": sd})
+    assert not rep2.missing
+    assert torch.equal(dst2.net.heads["normal_head"].lin_in.weight,
+                       src.net.heads["normal_head"].lin_in.weight)
+
+
+def test_missing_or_misshaped_hot_path_keys_fail_loudly():
+    from scenedino_amd.checkpoint import load_checkpoint
+    src = build(4)
+    sd = reference_layout(src)
+    del sd["renderer.net.heads.normal_head.lin_in.weight"]
+    with pytest.raises(KeyError):
+        load_checkpoint(build(5), sd)
+    rep = load_checkpoint(build(5), sd, strict=False)
+    assert rep.missing == ["heads.normal_head.lin_in.weight"]
+    sd = reference_layout(src)
+    sd["renderer.net.encoder.decoder.project.weight"] = torch.zeros(3, 3)
+    with pytest.raises(ValueError):
+        load_checkpoint(build(6), sd)
