@@ -182,6 +182,8 @@ def _traffic_from_profile(proj):
         d = json.load(open(files[-1]))
         ks = ("k_project", "k_render_proj") if proj else ("k_render<",)
         tot = sum(d["kernels"][k]["hbm_bytes"] for k in ks)
+        if proj and "k_head_hc" in d["kernels"]:  # launched inside sd_render_proj (timed with it)
+            tot += d["kernels"]["k_head_hc"]["hbm_bytes"]
     except (KeyError, TypeError, ValueError):
         return None
     return tot, os.path.relpath(files[-1], ROOT) + " (rocprofv3 PMC, per frame)"

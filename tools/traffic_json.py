@@ -16,7 +16,7 @@ vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in sorted(glob.glob(os.path.join(d, "pmc*", "*counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"]
-        for k in ("k_render_proj", "k_project", "k_render<", "k_field"):
+        for k in ("k_render_proj", "k_project", "k_head_hc", "k_render<", "k_field"):
             if k in name:
                 vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
 res = {"source": d, "note": "per-dispatch means; bytes = 2 x FETCH_SIZE(KB) x 1024 + "
