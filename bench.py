@@ -283,7 +283,10 @@ def main_vit(args, world, rank, device):
     token grids, all libsdhip.so kernels."""
     from scenedino_amd.models.backbones.dino.vit import DINOv2Encoder
     results = {}
-    for name, (arch, ver) in {"vit-s16": ("vit-s", "v1_16"), "vit-b8": ("vit-b", "v1")}.items():
+    models = {"vit-s16": ("vit-s", "v1_16"), "vit-b8": ("vit-b", "v1")}
+    if args.models:
+        models = {k: models[k] for k in args.models.split(",")}
+    for name, (arch, ver) in models.items():
         torch.manual_seed(0)
         enc = DINOv2Encoder(arch, (H, W), [3, 6, 9], False, ver).to(device).eval()
         img = (torch.rand(1, 3, H, W, generator=torch.Generator().manual_seed(rank)) * 2 - 1).to(device)
@@ -303,17 +306,19 @@ def main_vit(args, world, rank, device):
         results[name] = {"ms_per_pass": dt * 1e3, "tokens": Np + 1, "dim": C,
                          "gflop_per_pass": fl / 1e9, "tflops": fl / dt / 1e12,
                          "frac_bf16_peak": fl / dt / 1e12 / PEAK_TFLOPS["bf16"]}
+    first = next(iter(results))
+    roof = "vit-b8" if "vit-b8" in results else first
     if rank == 0:
         print(json.dumps({
             "metric": "DINO ViT encoder passes/sec (192x640 frame, 12 blocks)",
-            "value": 1e3 / results["vit-s16"]["ms_per_pass"], "unit": "passes/s",
+            "value": 1e3 / results[first]["ms_per_pass"], "unit": "passes/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "higher_is_better": True, "dtype": "bf16", "data": "synthetic, random weights",
             "config": {"workload": "a19 ViT encoder forward (DINOv2Encoder, no DPT decoder)"},
             "models": results,
-            "roofline": {"kernel": "k_gemm + k_attn (ViT-B/8)", "bound": "mfma",
-                         "achieved": results["vit-b8"]["tflops"], "peak": PEAK_TFLOPS["bf16"],
-                         "unit": "TFLOP/s", "frac": results["vit-b8"]["frac_bf16_peak"]},
+            "roofline": {"kernel": f"k_gemm + k_attn ({roof})", "bound": "mfma",
+                         "achieved": results[roof]["tflops"], "peak": PEAK_TFLOPS["bf16"],
+                         "unit": "TFLOP/s", "frac": results[roof]["frac_bf16_peak"]},
         }), flush=True)
 
 
@@ -348,7 +353,10 @@ def main_encode(args, world, rank, device):
     (the reference's fresh tensor)."""
     from scenedino_amd.models.backbones import make_backbone
     results = {}
-    for name, (arch, ver) in {"vit-s16": ("vit-s", "v1_16"), "vit-b8": ("vit-b", "v1")}.items():
+    models = {"vit-s16": ("vit-s", "v1_16"), "vit-b8": ("vit-b", "v1")}
+    if args.models:
+        models = {k: models[k] for k in args.models.split(",")}
+    for name, (arch, ver) in models.items():
         torch.manual_seed(0)
         conf = dict(type="dinov2", mode="downsample-prediction", decoder_arch="dpt",
                     downsampler_arch="featup", encoder_arch=arch, version=ver,
@@ -379,18 +387,19 @@ def main_encode(args, world, rank, device):
                          "frac_bf16_peak": (fv + fd) / dt / 1e12 / PEAK_TFLOPS["bf16"]}
         del m
         torch.cuda.empty_cache()
+    main = "vit-b8" if "vit-b8" in results else next(iter(results))
     if rank == 0:
         print(json.dumps({
             "metric": "SceneDINO encoder passes/sec (ViT + DPT, 192x640 frame)",
-            "value": 1e3 / results["vit-b8"]["ms_per_pass"], "unit": "passes/s",
+            "value": 1e3 / results[main]["ms_per_pass"], "unit": "passes/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "higher_is_better": True, "dtype": "bf16", "data": "synthetic, random weights",
-            "config": {"workload": "DINOv2Module prediction pass (ViT-B/8 + DPT, "
+            "config": {"workload": f"DINOv2Module prediction pass ({main} + DPT, "
                                    "configs/model/dino_downsampler.yaml)"},
             "models": results,
-            "roofline": {"kernel": "k_gemm (+ k_attn), ViT-B/8 + DPT", "bound": "mfma",
-                         "achieved": results["vit-b8"]["tflops"], "peak": PEAK_TFLOPS["bf16"],
-                         "unit": "TFLOP/s", "frac": results["vit-b8"]["frac_bf16_peak"]},
+            "roofline": {"kernel": f"k_gemm (+ k_attn), {main} + DPT", "bound": "mfma",
+                         "achieved": results[main]["tflops"], "peak": PEAK_TFLOPS["bf16"],
+                         "unit": "TFLOP/s", "frac": results[main]["frac_bf16_peak"]},
         }), flush=True)
 
 
@@ -410,6 +419,8 @@ def main():
                          "configs[4] SSCBench voxel query (voxels/s); vit: the DINO ViT "
                          "encoder forward (a19); encode: ViT + DPT decoder (DINOv2Module)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--models", default="", help="--config encode/vit: comma list of "
+                    "vit-s16, vit-b8 (default both)")
     args = ap.parse_args()
     global K_SAMPLES, D_DINO
     if args.config == "c4":

@@ -71,9 +71,17 @@ __device__ __forceinline__ bf16x8 vt_relu8(bf16x8 v) {
     return __builtin_bit_cast(bf16x8, uint4{w[0], w[1], w[2], w[3]});
 }
 
+// BM = BN = 32 is the split-K form for GEMMs too small to fill the chip with 64x64 tiles
+// (ViT-S/16: 481 tokens): the 4 waves share one 32x32 output tile and split every BK step
+// between them (wave w runs the 16-deep MFMA sub-steps w, w + 4, ...), then their
+// accumulators are summed through LDS in a fixed order (deterministic) and wave 0 runs the
+// epilogue.  Four times the workgroups of the 64x64 tiling, a quarter of the MFMA chain per
+// wave.
 template <int BM, int BN, int BK, int EPI, bool CONV>
 __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
-    constexpr int WM = BM / 2, WN = BN / 2;   // per-wave tile (2 x 2 waves)
+    constexpr bool SK = BM == 32;
+    static_assert(!SK || (BN == 32 && BK % 64 == 0), "split-K tile: 32x32, BK multiple of 64");
+    constexpr int WM = SK ? 32 : BM / 2, WN = SK ? 32 : BN / 2;  // per-wave tile (2 x 2 waves)
     constexpr int TM = WM / 32, TN = WN / 32; // 32x32 MFMA tiles per wave
     constexpr int CPR = BK / 8;               // 16-B chunks per tile row
     constexpr int CA = BM * CPR / 256;        // 16-B chunks of the A tile per thread
@@ -94,7 +102,7 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
 #define SB(buf) ((__bf16 *)smem + 2 * BM * GLDS + (buf) * (BN * GLDS))
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wm = wave >> 1, wn = wave & 1;
+    const int wm = SK ? 0 : wave >> 1, wn = SK ? 0 : wave & 1;
     const int r = lane & 31, h = lane >> 5;
     const int64_t m0 = (int64_t)blockIdx.y * BM, n0 = (int64_t)blockIdx.x * BN;
     const __bf16 *A = (const __bf16 *)g.a;
@@ -193,7 +201,8 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
         // only makes the compiler's vmcnt model wait for the newest loads as well
         gload(min(kt + 2, nk - 1), na, nb);
 #pragma unroll
-        for (int s = 0; s < BK / 16; ++s) {
+        for (int s0 = 0; s0 < (SK ? BK / 64 : BK / 16); ++s0) {
+            const int s = SK ? 4 * s0 + wave : s0;
             bf16x8 af[TM], bfr[TN];
 #pragma unroll
             for (int i = 0; i < TM; ++i)
@@ -219,6 +228,25 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
         if (kt + 1 < nk) step(kt + 1, ra1, rb1, ra0, rb0);
     }
 
+    if constexpr (SK) {
+        // split-K reduction: waves 1..3 park their partial tiles past the staging area,
+        // wave 0 adds them in wave order (the K loop ended on a barrier)
+        float *part = (float *)(smem + 16384);
+        if (wave > 0) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) part[((wave - 1) * 16 + q) * 64 + lane] = acc[0][0][q];
+        }
+        __syncthreads();
+        if (wave == 0) {
+#pragma unroll
+            for (int w = 0; w < 3; ++w)
+#pragma unroll
+                for (int q = 0; q < 16; ++q) acc[0][0][q] += part[(w * 16 + q) * 64 + lane];
+        }
+        if constexpr (!STAGED) {
+            if (wave != 0) return;
+        }
+    }
     // epilogue: accumulator register q of tile (i, j): row (q&3)+8(q>>2)+4h, column r
     if constexpr (STAGED) {
         // phase 1: v = acc + bias (GELU) -> fp32 tile [m][n] in LDS (the K loop ended on a
@@ -226,6 +254,7 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
         float *sT = (float *)smem;
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
+            if (SK && wave != 0) break;
             const int nl = wn * WN + j * 32 + r;
             const float bias = (g.bias && n0 + nl < g.N) ? g.bias[n0 + nl] : 0.f;
 #pragma unroll
@@ -794,6 +823,11 @@ static void vt_pick_gemm(const sd_gemm_args &g, hipStream_t s) {
     // K steps of 64 whenever K allows (half the barriers, twice the work under each
     // prefetch); 128x128 tiles once they fill the chip, else 64x64
     const int64_t big = ((g.M + 127) / 128) * ((g.N + 127) / 128);
+    const int64_t mid = ((g.M + 63) / 64) * ((g.N + 63) / 64);
+    if (!CONV && mid < 256 && g.K % 128 == 0 && g.K >= 256) {
+        vt_launch_gemm<32, 32, 128, CONV>(g, s);  // split-K over the 4 waves
+        return;
+    }
     if (g.K % 64 == 0) {
         if (big >= 256)
             vt_launch_gemm<128, 128, 64, CONV>(g, s);
