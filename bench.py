@@ -89,6 +89,56 @@ def make_scene(frame_seed: int, device, precision="bf16", offset_pose=False):
     return net, renderer, wrapper, sampler, render_pose, Ks
 
 
+def end_to_end(args, device, rank):
+    """Whole frame through make_model's native encoder (BASELINE configs[1]: DINO
+    ViT-S/16 -> DPT -> 256x192x640 grid, random weights) then the C2 render: BTSNet.encode
+    (the gt-encoder pass stays deferred, nothing reads grid_l_loss_features at inference)
+    + ImageRaySampler + NeRFRenderer.  Reported beside the render-only `value`; SURVEY
+    §8(d) prices the encoder separately."""
+    from scenedino_amd.models import make_model
+    from scenedino_amd.renderer import NeRFRenderer
+    from scenedino_amd.common.ray_sampler import ImageRaySampler
+    enc = dict(type="dinov2", mode="downsample-prediction", decoder_arch="dpt",
+               downsampler_arch="featup", encoder_arch="vit-s", version="v1_16",
+               separate_gt_version=None, encoder_freeze=True, flip_avg_gt=False,
+               dim_reduction_arch="mlp", num_ch_enc=[64, 64, 128, 256],
+               intermediate_features=[3, 6, 9], decoder_out_dim=256, dino_pca_dim=64,
+               image_size=[H, W], key_features=False)
+    conf = {"arch": "BTSNet", "predict_dino": True, "dino_dims": D_DINO, "learn_empty": False,
+            "code_mode": "z", "inv_z": True, "z_near": 3, "z_far": 80, "sample_color": True,
+            "encoder": enc, "code": {"num_freqs": 6, "freq_factor": 1.5, "include_input": True},
+            "decoder_heads": [{"type": "resnet", "name": "normal_head", "freeze": False,
+                               "args": {"n_blocks": 0, "d_hidden": D_HIDDEN}}],
+            "final_prediction_head": "normal_head", "precision": args.precision}
+    torch.manual_seed(2)
+    net = make_model(conf).to(device).eval()
+    g = torch.Generator().manual_seed(rank)
+    images = (torch.rand(1, 1, 3, H, W, generator=g) * 2 - 1).to(device)
+    Ks = torch.tensor(KITTI_K, device=device).view(1, 1, 3, 3)
+    poses = torch.eye(4, device=device).view(1, 1, 4, 4)
+    wrapper = NeRFRenderer(n_coarse=K_SAMPLES, lindisp=True, hard_alpha_cap=False,
+                           eval_batch_size=65536).bind_parallel(net, gpus=None).eval()
+    sampler = ImageRaySampler(z_near=3, z_far=80, height=H, width=W)
+
+    def frame():
+        net.encode(images, Ks, poses, ids_encoder=[0], ids_render=[0])
+        return render_step(net, wrapper, sampler, poses, Ks)
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            frame()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            frame()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / args.steps
+    del net
+    torch.cuda.empty_cache()
+    return {"encoder": "DINO ViT-S/16 + DPT (make_model native encoder, random weights)",
+            "ms_per_frame": dt * 1e3, "rays_per_s": H * W / dt}
+
+
 def render_step(net, wrapper, sampler, pose, Ks):
     net._grid_cache = None  # re-pack / re-project the (freshly encoded) grid every frame
     rays, _ = sampler.sample(None, pose, Ks)
@@ -419,6 +469,8 @@ def main():
                          "configs[4] SSCBench voxel query (voxels/s); vit: the DINO ViT "
                          "encoder forward (a19); encode: ViT + DPT decoder (DINOv2Module)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--no-end-to-end", action="store_true",
+                    help="c2: skip the encode + render frame timing reported beside value")
     ap.add_argument("--models", default="", help="--config encode/vit: comma list of "
                     "vit-s16, vit-b8 (default both)")
     args = ap.parse_args()
@@ -552,6 +604,8 @@ def main():
         if tr is not None:
             line["roofline"]["traffic"] = tr[0]
             line["roofline"]["traffic_source"] = tr[1]
+        if args.config == "c2" and not args.no_end_to_end and world == 1:
+            line["end_to_end"] = end_to_end(args, device, rank)
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(args.cpu_budget)
         print(json.dumps(line), flush=True)

@@ -11,9 +11,11 @@ evaluate_model_sscbench.py) import the hot path as
 reference is imported, so those imports resolve here while every other reference
 module (encoders, data sets, trainer, losses, visualisation) stays the reference's.
 ``make_model`` keeps the reference's signature (scenedino/models/__init__.py:9-63): the
-image encoder is still built by the reference's own ``make_backbone``
-(models/backbones/backbone_util.py) and the downstream head by
-``scenedino.downstream_head.make_downstream_head``, then handed to this package's BTSNet, whose parameter names equal the reference's, so
+image encoder is this package's ``DINOv2Module`` (ViT + DPT on gfx950, one HIP graph per
+pass) for every configuration it covers, else the reference's own ``make_backbone``
+(models/backbones/backbone_util.py) with its ViT and DPTHead aliased to the gfx950
+mirrors; the downstream head comes from ``scenedino.downstream_head.make_downstream_head``.
+Both go to this package's BTSNet, whose parameter names equal the reference's, so
 ``checkpoint.pt`` state dicts load unchanged (demo_utils/utils.py:52-55).
 """
 from __future__ import annotations
@@ -25,8 +27,16 @@ import types
 
 def _ref_make_model(config, downstream_config=None):
     from . import models as amd_models
-    backbones = importlib.import_module("scenedino.models.backbones")
-    encoder = backbones.make_backbone(config["encoder"])
+    from .models.backbones import make_backbone as amd_make_backbone
+    try:
+        # the native DINOv2Module (ViT + DPT as one HIP graph; same parameter names)
+        encoder = amd_make_backbone(config["encoder"])
+    except NotImplementedError:
+        # encoder variants this build does not cover (non-DPT decoders, register / FiT3D
+        # ViTs, separate gt versions, upsample-gt mode): the reference's own module, whose
+        # ViT and DPTHead still resolve to the gfx950 mirrors aliased by install()
+        backbones = importlib.import_module("scenedino.models.backbones")
+        encoder = backbones.make_backbone(config["encoder"])
     downstream_head = None
     if downstream_config is not None:
         heads = importlib.import_module("scenedino.downstream_head")
@@ -68,4 +78,7 @@ def install():
         dm = None
     if dm is not None:
         from .models.backbones.dino import vit as amd_vit
+        from .models.backbones.dino import dpt_head as amd_dpt
         dm.DINOv2Encoder = amd_vit.DINOv2Encoder
+        # build_decoder (dinov2_module.py:31-56) looks DPTHead up at call time too
+        dm.DPTHead = amd_dpt.DPTHead

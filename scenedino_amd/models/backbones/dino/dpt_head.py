@@ -26,6 +26,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from .... import _lib
+from .vit import _param_key
 
 
 class ReassembleBlocks(nn.Module):
@@ -124,7 +125,7 @@ class DPTHead(nn.Module):
         self._packed = None
 
     def _pack(self):
-        key = tuple((t.data_ptr(), t._version) for t in self.parameters())
+        key = _param_key(self)
         if self._packed is not None and self._packed[0] == key:
             return self._packed[1]
         rb = self.reassemble_blocks

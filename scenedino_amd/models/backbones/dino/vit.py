@@ -123,7 +123,17 @@ class _Packed:
 
 
 def _param_key(m: nn.Module):
-    return tuple((t.data_ptr(), t._version) for t in m.parameters())
+    """(storage, version) of every parameter: changes on load_state_dict, in-place edits,
+    .to() and Parameter replacement.  The module list is collected once (a recursive
+    m.parameters() walk costs ~0.3 ms of host time per encode for ViT + DPT, enough to
+    starve the launch queue); re-structuring a module after its first forward is not
+    tracked."""
+    mods = m.__dict__.get("_sd_modules")
+    if mods is None:
+        mods = list(m.modules())
+        m.__dict__["_sd_modules"] = mods
+    return tuple((t.data_ptr(), t._version) for x in mods for t in x._parameters.values()
+                 if t is not None)
 
 
 def vit_forward(vit: VisionTransformer, images: torch.Tensor, packed: _Packed,

@@ -33,6 +33,17 @@ def _cam_records(poses_w2c, Ks):
     return _lib.cam_records(poses_w2c, Ks)
 
 
+def _take(t, ids):
+    """t[:, ids] (bts.py:140-160).  A run of consecutive non-negative view ids is a slice
+    view instead of an index gather: the same values, one kernel launch less per tensor
+    per encode."""
+    if (isinstance(ids, (list, tuple)) and len(ids) > 0 and isinstance(ids[0], int)
+            and ids[0] >= 0 and ids[0] + len(ids) <= t.shape[1]
+            and list(ids) == list(range(ids[0], ids[0] + len(ids)))):
+        return t[:, ids[0]:ids[0] + len(ids)]
+    return t[:, ids]
+
+
 class BTSNet(nn.Module):
     def __init__(self, conf, encoder: nn.Module, code_xyz, heads: dict,
                  final_pred_head: str | None = None, uncertainty_predictor: nn.Module | None = None,
@@ -110,21 +121,23 @@ class BTSNet(nn.Module):
             raise NotImplementedError("combine_ids / loss_feature_grid_shift are training-only "
                                       "options outside the MI355X hot path")
         with torch.autocast(device_type=images.device.type, enabled=False):
-            poses_w2c = torch.inverse(poses_c2w.float())
+            # torch.inverse's LU (same kernels) without its device-to-host error check,
+            # which would stall the launch queue once per frame
+            poses_w2c = torch.linalg.inv_ex(poses_c2w.float())[0]
         if ids_encoder is None:
             images_encoder, Ks_encoder, poses_w2c_encoder = images, Ks, poses_w2c
         else:
-            images_encoder = images[:, ids_encoder]
-            Ks_encoder = Ks[:, ids_encoder]
-            poses_w2c_encoder = poses_w2c[:, ids_encoder]
-        images_loss = images if ids_loss is None else images[:, ids_loss]
+            images_encoder = _take(images, ids_encoder)
+            Ks_encoder = _take(Ks, ids_encoder)
+            poses_w2c_encoder = _take(poses_w2c, ids_encoder)
+        images_loss = images if ids_loss is None else _take(images, ids_loss)
         images = images_alt if images_alt is not None else images * 0.5 + 0.5
         if ids_render is None:
             images_render, Ks_render, poses_w2c_render = images, Ks, poses_w2c
         else:
-            images_render = images[:, ids_render]
-            Ks_render = Ks[:, ids_render]
-            poses_w2c_render = poses_w2c[:, ids_render]
+            images_render = _take(images, ids_render)
+            Ks_render = _take(Ks, ids_render)
+            poses_w2c_render = _take(poses_w2c, ids_render)
         n_, nv_, c_, h_, w_ = images_encoder.shape
         n_l, nv_l = images_loss.shape[:2]
         do_flip = self.flip_augmentation and self.training and bool(torch.rand(1) > 0.5)
@@ -134,7 +147,10 @@ class BTSNet(nn.Module):
         if do_flip:
             lat = [torch.flip(x, dims=(-1,)) for x in lat]
         _, _, hh, ww = lat[0].shape
-        lat = [F.interpolate(x, size=(hh, ww)).view(n_, nv_, -1, hh, ww) for x in lat]
+        # nearest resize to the first level's size (bts.py:197); at equal size it is the
+        # identity, so that level (the 126-503 MB f32 grid) is viewed, not copied
+        lat = [(x if tuple(x.shape[-2:]) == (hh, ww) else F.interpolate(x, size=(hh, ww)))
+               .view(n_, nv_, -1, hh, ww) for x in lat]
         if self.extra_outs > 0:
             self.grid_f_extra = [x[:, :, -self.extra_outs:] for x in lat]
             lat = [x[:, :, :-self.extra_outs] for x in lat]
