@@ -191,6 +191,37 @@ int sd_composite(const float *z, const float *sigma, const float *feat, int64_t 
                  float *weights, float *alphas, float *depth, float *feat_out, float *rgb_out,
                  void *stream);
 
+/* ---- Differentiable (training) field path (sdhip_train.hip) ----------------- */
+
+/* MLP input rows of the training path: per point the projection / frustum mask
+ * (pinhole.py:40-112), the bilinear border gather of the C grid channels
+ * (bts.py:299-309, F.grid_sample align_corners=False) and the 39-d positional code
+ * (positional_encoding.py:13-80), written as x_out (B*P, C+39) = [feat | code]
+ * (bts.py:321-328).  grid_nhwc (B, Hf, Wf, C) f32.  Colour samples / masks as
+ * sd_field_query (bts.py:330-441; rgb, invalid, img, cam_c may be NULL / nv = 0). */
+int sd_field_gather(const float *xyz, int64_t B, int64_t P, const float *grid_nhwc,
+                    int32_t C, int32_t Hf, int32_t Wf, const float *cam_f,
+                    const float *img, int32_t nv, int32_t Hc, int32_t Wc,
+                    const float *cam_c, float *x_out, uint8_t *invalid_f, float *rgb,
+                    float *invalid, void *stream);
+
+/* Backward of the feature gather (grid_sample input gradient, bts.py:299-309):
+ * dgrid_nhwc (B, Hf, Wf, C) += bilinear scatter of dx[:, :C] (row stride ldx).
+ * Accumulates with f32 atomics: the caller zeroes dgrid_nhwc. */
+int sd_field_gather_bwd(const float *xyz, int64_t B, int64_t P, const float *dx,
+                        int64_t ldx, int32_t C, int32_t Hf, int32_t Wf,
+                        const float *cam_f, float *dgrid_nhwc, void *stream);
+
+/* Backward of sd_composite (alpha compositing, nerf.py:376-405): upstream gradients
+ * of depth (R), feat_out (R,F), rgb_out (R,Cc), weights (R,K), alphas (R,K) (any may be
+ * NULL) -> d_sigma (R,K) and, when non-NULL, d_feat (R,K,F) / d_rgb (R,K,Cc).
+ * K <= 512.  Division-free reverse transmittance recurrence (sdhip_train.hip). */
+int sd_composite_bwd(const float *z, const float *sigma, const float *feat, int64_t F,
+                     const float *rgb, int64_t Cc, int64_t R, int32_t K,
+                     int32_t hard_alpha_cap, const float *g_depth, const float *g_feat,
+                     const float *g_rgb, const float *g_weights, const float *g_alphas,
+                     float *d_sigma, float *d_feat, float *d_rgb, void *stream);
+
 /* ---- SSCBench voxel query (sdhip_seg.hip) ---------------------------------- */
 
 /* Voxel-centre grid of nx*ny*nz voxels, flat index (ix*ny + iy)*nz + iz (meshgrid ij),

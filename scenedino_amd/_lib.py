@@ -108,6 +108,11 @@ SIGNATURES = {
     "sd_cam_records": [_vp, _i64, _vp, _i64, _i64, _vp, _vp],
     "sd_render_fused": [ctypes.POINTER(SdRenderArgs), ctypes.POINTER(SdMlp), _vp],
     "sd_field_query": [ctypes.POINTER(SdFieldArgs), ctypes.POINTER(SdMlp), _vp],
+    "sd_field_gather": [_vp, _i64, _i64, _vp, _i32, _i32, _i32, _vp, _vp, _i32, _i32, _i32, _vp,
+                        _vp, _vp, _vp, _vp, _vp],
+    "sd_field_gather_bwd": [_vp, _i64, _i64, _vp, _i64, _i32, _i32, _i32, _vp, _vp, _vp],
+    "sd_composite_bwd": [_vp, _vp, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp, _vp,
+                         _vp, _vp, _vp, _vp, _vp],
     "sd_project_grid": [_vp, _i64, _i64, _i64, ctypes.POINTER(SdMlp), _vp, _vp],
     "sd_render_proj": [ctypes.POINTER(SdRenderArgs), ctypes.POINTER(SdHead), _vp],
     "sd_render_proj_work_bytes": [_i64, _i32],
@@ -329,6 +334,66 @@ def composite(z, sigma, feat, rgb, hard_alpha_cap, want_weights=True):
                             int(bool(hard_alpha_cap)), ptr(weights), ptr(alphas), ptr(depth),
                             ptr(feat_out), ptr(rgb_out), stream_of(depth)), "sd_composite")
     return weights, alphas, depth, feat_out, rgb_out
+
+
+def field_gather(xyz, grid_nhwc, cam_f, img=None, cam_c=None, colors=True):
+    """sd_field_gather: xyz (B,P,3), grid_nhwc (B,Hf,Wf,C) f32 -> x (B,P,C+39),
+    invalid_f (B,P) bool, rgb (B,P,3nv) | None, invalid (B,P,nv) | None."""
+    lib = load()
+    B, P, _ = xyz.shape
+    _, Hf, Wf, C = grid_nhwc.shape
+    dev = xyz.device
+    x = torch.empty(B, P, C + 39, device=dev)
+    invf = torch.empty(B, P, device=dev, dtype=torch.bool)
+    nv, Hc, Wc = 0, 0, 0
+    if colors:  # img: pack_image output (B*nv, Hc, Wc, 4); cam_c (B, nv, 21)
+        nv, Hc, Wc = cam_c.shape[1], img.shape[1], img.shape[2]
+    rgb = torch.empty(B, P, 3 * nv, device=dev) if colors else None
+    inv = torch.empty(B, P, nv, device=dev) if colors else None
+    _check(lib.sd_field_gather(ptr(_req(xyz, "xyz")), B, P, ptr(_req(grid_nhwc, "grid")), C, Hf,
+                               Wf, ptr(_req(cam_f, "cam_f")), ptr(img), nv, Hc, Wc, ptr(cam_c),
+                               ptr(x), ptr(invf), ptr(rgb), ptr(inv), stream_of(x)),
+           "sd_field_gather")
+    return x, invf, rgb, inv
+
+
+def field_gather_bwd(xyz, dx, cam_f, Hf, Wf, C):
+    """sd_field_gather_bwd: dx (B,P,>=C) (unit inner stride) -> dgrid (B,Hf,Wf,C) f32."""
+    lib = load()
+    B, P, _ = xyz.shape
+    if dx.stride(-1) != 1 or dx.dtype != torch.float32 or dx.stride(1) != dx.shape[-1] \
+            or dx.stride(0) != P * dx.shape[-1]:
+        dx = dx.float().contiguous()
+    dgrid = torch.zeros(B, Hf, Wf, C, device=xyz.device)
+    _check(lib.sd_field_gather_bwd(ptr(_req(xyz, "xyz")), B, P, ptr(dx), dx.shape[-1], C, Hf, Wf,
+                                   ptr(_req(cam_f, "cam_f")), ptr(dgrid), stream_of(dgrid)),
+           "sd_field_gather_bwd")
+    return dgrid
+
+
+def composite_bwd(z, sigma, feat, rgb, hard_alpha_cap, g_depth, g_feat, g_rgb, g_weights,
+                  g_alphas, need_feat=True, need_rgb=False):
+    """sd_composite_bwd -> d_sigma (R,K), d_feat (R,K,F) | None, d_rgb (R,K,Cc) | None."""
+    lib = load()
+    R, K = z.shape
+    F = feat.shape[-1] if feat is not None else 0
+    Cc = rgb.shape[-1] if rgb is not None else 0
+    g = [None if t is None else _req(t.float().contiguous(), n) for t, n in
+         ((g_depth, "g_depth"), (g_feat, "g_feat"), (g_rgb, "g_rgb"), (g_weights, "g_weights"),
+          (g_alphas, "g_alphas"))]
+    if feat is None:
+        g[1] = None
+    if rgb is None:
+        g[2] = None
+    d_sigma = torch.empty(R, K, device=z.device)
+    d_feat = torch.empty(R, K, F, device=z.device) if (need_feat and g[1] is not None) else None
+    d_rgb = torch.empty(R, K, Cc, device=z.device) if (need_rgb and g[2] is not None) else None
+    _check(lib.sd_composite_bwd(ptr(_req(z, "z")), ptr(_req(sigma, "sigma")),
+                                ptr(feat if feat is None else _req(feat, "feat")), F,
+                                ptr(rgb if rgb is None else _req(rgb, "rgb")), Cc, R, K,
+                                int(bool(hard_alpha_cap)), *[ptr(t) for t in g], ptr(d_sigma),
+                                ptr(d_feat), ptr(d_rgb), stream_of(d_sigma)), "sd_composite_bwd")
+    return d_sigma, d_feat, d_rgb
 
 
 # ---------------------------------------------------------------------------

@@ -8,7 +8,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SOURCES = ["csrc/sdhip_rays.hip", "csrc/sdhip_field.hip", "csrc/sdhip_proj.hip",
-           "csrc/sdhip_seg.hip", "csrc/sdhip_vit.hip"]
+           "csrc/sdhip_seg.hip", "csrc/sdhip_vit.hip", "csrc/sdhip_train.hip"]
 OUT = os.path.join(HERE, "libsdhip.so")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
          "-DSD_FASTPE=0", "-Wno-unused-result",

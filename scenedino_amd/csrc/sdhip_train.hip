@@ -1,0 +1,305 @@
+// sdhip_train.hip -- gfx950 kernels of the differentiable (training) field path.
+//
+// The inference path fuses gather -> MLP -> compositing into one kernel and never
+// materialises per-sample activations.  Training (train.py through the renderer,
+// base_trainer.py:223,251) needs gradients w.r.t. the feature grid and the ResnetFC
+// parameters, so the training path splits at the two places where autograd needs
+// saved state:
+//
+//   k_field_gather      a8-a10 + a15: per point, projection, frustum mask, the bilinear
+//                       border gather of the C grid channels and the 39-d positional code,
+//                       written as the MLP input row X = [feat | code] (bts.py:321-328),
+//                       plus the colour samples / invalid masks (no gradient: images are
+//                       data).  The ResnetFC layers are plain library GEMMs (autograd).
+//   k_field_gather_bwd  grid_sample backward (bts.py:299-309): dX[:, :C] scattered into the
+//                       NHWC grid gradient with the forward's bilinear weights (hardware
+//                       f32 atomics; the border clamp duplicates a tap only with weight 0,
+//                       as torch's within-bounds test drops it).
+//   k_composite_bwd     alpha-compositing backward (nerf.py:376-405): reverse transmittance
+//                       recurrence, division-free (below), d sigma and d per-sample
+//                       features / colours.
+//
+// Composite backward.  w_k = a_k T_k, T_k = prod_{j<k} (1 - a_j + 1e-10).  With
+// g_k = dL/dw_k (direct + depth z_k + <dL/dfeat, f_k> + <dL/drgb, c_k>):
+//   dL/da_k = T_k (g_k - U_k) + dL/dalphas_k,
+//   U_{K-1} = 0,  U_{k-1} = g_k a_k + (1 - a_k + 1e-10) U_k,
+// which equals the textbook  T_k g_k - (sum_{m>k} g_m w_m) / (1 - a_k + 1e-10)  without
+// dividing by a factor that is 1e-10 once a sample saturates.
+// d sigma_k = dL/da_k * exp(-|delta_k| relu(sigma_k)) * |delta_k| * [sigma_k > 0]
+// (hard_alpha_cap: the last alpha is the constant 1, no gradient).
+#include "sdhip_point.h"
+
+#define TR_WAVES 4
+#define TR_MAXK 512
+
+// LDS written by some lanes of a wave, read by others: complete the wave's LDS traffic
+// and stop the compiler moving accesses across (waves of a block run different rays,
+// so no block barrier)
+__device__ __forceinline__ void sd_wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// ---------------------------------------------------------------------------
+// forward gather: one wave per point, lane = 4 channels (f32x4) of the NHWC grid
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(TR_WAVES * 64)
+k_field_gather(const float *__restrict__ xyz, int64_t B, int64_t P,
+               const float *__restrict__ grid, int C, int Hf, int Wf,
+               const float *__restrict__ cam_f, const float *__restrict__ img, int nv, int Hc,
+               int Wc, const float *__restrict__ cam_c, float *__restrict__ x_out,
+               uint8_t *__restrict__ invalid_f, float *__restrict__ rgb,
+               float *__restrict__ invalid) {
+    const int lane = threadIdx.x & 63;
+    const int64_t NP = B * P;
+    const int ld = C + 39;
+    const int64_t plane = (int64_t)Hf * Wf * C;
+    const int64_t cplane = (int64_t)Hc * Wc * 4;
+    for (int64_t p = (int64_t)blockIdx.x * TR_WAVES + (threadIdx.x >> 6); p < NP;
+         p += (int64_t)gridDim.x * TR_WAVES) {
+        const int64_t b = p / P;
+        const float px = xyz[p * 3], py = xyz[p * 3 + 1], pz = xyz[p * 3 + 2];
+        const PointGeo geo = sd_point_geo(cam_f + b * 21, px, py, pz, Wf, Hf);
+        const float *g = grid + b * plane;
+        float *xr = x_out + p * ld;
+        for (int c = lane * 4; c < C; c += 256) {
+            const f32x4 a = *(const f32x4 *)(g + (int64_t)geo.t.i00 * C + c);
+            const f32x4 bb = *(const f32x4 *)(g + (int64_t)geo.t.i01 * C + c);
+            const f32x4 cc = *(const f32x4 *)(g + (int64_t)geo.t.i10 * C + c);
+            const f32x4 d = *(const f32x4 *)(g + (int64_t)geo.t.i11 * C + c);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)  // grid_sampler_2d's nw, ne, sw, se order
+                xr[c + i] = ((a[i] * geo.t.w00 + bb[i] * geo.t.w01) + cc[i] * geo.t.w10) +
+                            d[i] * geo.t.w11;
+        }
+        // positional code (positional_encoding.py:68-80): [x, y, z~, sin(f_j v + phi)]
+        // with rows (freq j, phase) and the 3 coordinates innermost
+        if (lane < 39) {
+            float r;
+            if (lane < 3) {
+                r = geo.v[lane];
+            } else {
+                const int s = lane - 3, fi = s / 6, cs = (s % 6) / 3, co = s % 3;
+                const float f = 1.5f * (float)(1 << fi);
+                r = sinf(fmaf(geo.v[co], f, cs ? 1.5707963705062866f : 0.f));
+            }
+            xr[C + lane] = r;
+        }
+        if (lane == 0 && invalid_f) invalid_f[p] = geo.inv_f ? 1 : 0;
+        if (lane < nv && (rgb || invalid)) {
+            const int v = lane;
+            float col[3];
+            const bool ic = sd_color_view(cam_c + (b * nv + v) * 21, img + (b * nv + v) * cplane,
+                                          Wc, Hc, px, py, pz, col);
+            if (rgb) {
+                rgb[(p * nv + v) * 3] = col[0];
+                rgb[(p * nv + v) * 3 + 1] = col[1];
+                rgb[(p * nv + v) * 3 + 2] = col[2];
+            }
+            if (invalid) invalid[p * nv + v] = (ic | geo.inv_f) ? 1.f : 0.f;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// gather backward: dG (B, Hf, Wf, C) += bilinear scatter of dX[:, :C]
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(TR_WAVES * 64)
+k_field_gather_bwd(const float *__restrict__ xyz, int64_t B, int64_t P,
+                   const float *__restrict__ dx, int64_t ldx, int C, int Hf, int Wf,
+                   const float *__restrict__ cam_f, float *__restrict__ dgrid) {
+    const int lane = threadIdx.x & 63;
+    const int64_t NP = B * P;
+    const int64_t plane = (int64_t)Hf * Wf * C;
+    for (int64_t p = (int64_t)blockIdx.x * TR_WAVES + (threadIdx.x >> 6); p < NP;
+         p += (int64_t)gridDim.x * TR_WAVES) {
+        const int64_t b = p / P;
+        const PointGeo geo =
+            sd_point_geo(cam_f + b * 21, xyz[p * 3], xyz[p * 3 + 1], xyz[p * 3 + 2], Wf, Hf);
+        float *g = dgrid + b * plane;
+        const float *dr = dx + p * ldx;
+        for (int c = lane * 4; c < C; c += 256) {
+            f32x4 v;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = dr[c + i];
+            const int idx[4] = {geo.t.i00, geo.t.i01, geo.t.i10, geo.t.i11};
+            const float wt[4] = {geo.t.w00, geo.t.w01, geo.t.w10, geo.t.w11};
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                if (wt[t] == 0.f) continue;  // clamped duplicate taps carry weight 0
+                float *dst = g + (int64_t)idx[t] * C + c;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) unsafeAtomicAdd(dst + i, v[i] * wt[t]);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// composite backward: one wave per ray
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(TR_WAVES * 64)
+k_composite_bwd(const float *__restrict__ z, const float *__restrict__ sigma,
+                const float *__restrict__ feat, int F, const float *__restrict__ rgb, int Cc,
+                int64_t R, int K, int hard_cap, const float *__restrict__ g_depth,
+                const float *__restrict__ g_feat, const float *__restrict__ g_rgb,
+                const float *__restrict__ g_w, const float *__restrict__ g_a,
+                float *__restrict__ d_sigma, float *__restrict__ d_feat,
+                float *__restrict__ d_rgb) {
+    __shared__ float s_a[TR_WAVES][TR_MAXK], s_g[TR_WAVES][TR_MAXK], s_t[TR_WAVES][TR_MAXK];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    float *sa = s_a[wv], *sg = s_g[wv], *st = s_t[wv];
+    for (int64_t ray = (int64_t)blockIdx.x * TR_WAVES + wv; ray < R;
+         ray += (int64_t)gridDim.x * TR_WAVES) {
+        const float *zr = z + ray * K, *sr = sigma + ray * K;
+        const float gd = g_depth ? g_depth[ray] : 0.f;
+        // phase 1 (lane = sample): alpha and g_k = dL/dw_k
+        for (int k = lane; k < K; k += 64) {
+            const float zk = zr[k];
+            const float delta = (k + 1 < K) ? zr[k + 1] - zk : 1e10f;
+            float alpha = 1.f - expf(-fabsf(delta) * fmaxf(sr[k], 0.f));
+            if (hard_cap && k == K - 1) alpha = 1.f;
+            float g = gd * zk;
+            if (g_w) g += g_w[ray * K + k];
+            if (feat && g_feat) {
+                const float *fr = feat + (ray * K + k) * (int64_t)F;
+                const float *gf = g_feat + ray * F;
+                float s = 0.f;
+                for (int c = 0; c < F; ++c) s += gf[c] * fr[c];
+                g += s;
+            }
+            if (rgb && g_rgb) {
+                const float *cr = rgb + (ray * K + k) * (int64_t)Cc;
+                const float *gc = g_rgb + ray * Cc;
+                float s = 0.f;
+                for (int c = 0; c < Cc; ++c) s += gc[c] * cr[c];
+                g += s;
+            }
+            sa[k] = alpha;
+            sg[k] = g;
+        }
+        sd_wave_lds_sync();
+        // phase 2 (one lane): T_k forward, U_k backward; sa <- w_k, sg <- dL/da_k
+        if (lane == 0) {
+            float T = 1.f;
+            for (int k = 0; k < K; ++k) {
+                st[k] = T;
+                T = T * ((1.f - sa[k]) + 1e-10f);
+            }
+            float U = 0.f;
+            for (int k = K - 1; k >= 0; --k) {
+                const float a = sa[k], g = sg[k];
+                const float tk = st[k];
+                float da = tk * (g - U);
+                U = g * a + ((1.f - a) + 1e-10f) * U;
+                sg[k] = da;
+                sa[k] = a * tk;  // w_k
+            }
+        }
+        sd_wave_lds_sync();
+        // phase 3 (lane = sample): d sigma
+        for (int k = lane; k < K; k += 64) {
+            const float zk = zr[k];
+            const float delta = (k + 1 < K) ? zr[k + 1] - zk : 1e10f;
+            const float s = sr[k];
+            float da = sg[k];
+            if (g_a) da += g_a[ray * K + k];
+            float ds = 0.f;
+            if (!(hard_cap && k == K - 1) && s > 0.f) {
+                const float ad = fabsf(delta);
+                ds = da * expf(-ad * s) * ad;
+            }
+            d_sigma[ray * K + k] = ds;
+        }
+        // phase 4 (lane = channel): d feat_k = w_k dL/dfeat, d rgb_k = w_k dL/drgb
+        if (d_feat && g_feat) {
+            for (int k = 0; k < K; ++k) {
+                const float w = sa[k];
+                for (int c = lane; c < F; c += 64)
+                    d_feat[(ray * K + k) * (int64_t)F + c] = w * g_feat[ray * F + c];
+            }
+        }
+        if (d_rgb && g_rgb) {
+            for (int k = 0; k < K; ++k) {
+                const float w = sa[k];
+                for (int c = lane; c < Cc; c += 64)
+                    d_rgb[(ray * K + k) * (int64_t)Cc + c] = w * g_rgb[ray * Cc + c];
+            }
+        }
+        sd_wave_lds_sync();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+static int tr_blocks(int64_t units) {
+    const int64_t want = (units + TR_WAVES - 1) / TR_WAVES;
+    const int64_t cap = (int64_t)sd_num_cus() * 32;
+    return (int)(want < cap ? want : cap);
+}
+
+extern "C" int sd_field_gather(const float *xyz, int64_t B, int64_t P, const float *grid_nhwc,
+                               int32_t C, int32_t Hf, int32_t Wf, const float *cam_f,
+                               const float *img, int32_t nv, int32_t Hc, int32_t Wc,
+                               const float *cam_c, float *x_out, uint8_t *invalid_f, float *rgb,
+                               float *invalid, void *stream) {
+    if (B <= 0 || P < 0 || !xyz || !grid_nhwc || !cam_f || !x_out || C <= 0 || (C % 4) ||
+        Hf <= 0 || Wf <= 0 || nv < 0 || nv > 64 ||
+        (nv > 0 && (rgb || invalid) && (!img || !cam_c || Hc <= 0 || Wc <= 0))) {
+        sd_set_error("sd_field_gather: invalid argument (C % 4 == 0, nv <= 64)");
+        return -1;
+    }
+    if (P == 0) return 0;
+    hipLaunchKernelGGL(k_field_gather, dim3(tr_blocks(B * P)), dim3(TR_WAVES * 64), 0,
+                       (hipStream_t)stream, xyz, B, P, grid_nhwc, C, Hf, Wf, cam_f, img, nv, Hc,
+                       Wc, cam_c, x_out, invalid_f, rgb, invalid);
+    if (hipGetLastError() != hipSuccess) {
+        sd_set_error("sd_field_gather: launch failed");
+        return -2;
+    }
+    return 0;
+}
+
+extern "C" int sd_field_gather_bwd(const float *xyz, int64_t B, int64_t P, const float *dx,
+                                   int64_t ldx, int32_t C, int32_t Hf, int32_t Wf,
+                                   const float *cam_f, float *dgrid_nhwc, void *stream) {
+    if (B <= 0 || P < 0 || !xyz || !dx || !cam_f || !dgrid_nhwc || C <= 0 || (C % 4) ||
+        ldx < C || Hf <= 0 || Wf <= 0) {
+        sd_set_error("sd_field_gather_bwd: invalid argument (C % 4 == 0, ldx >= C)");
+        return -1;
+    }
+    if (P == 0) return 0;
+    hipLaunchKernelGGL(k_field_gather_bwd, dim3(tr_blocks(B * P)), dim3(TR_WAVES * 64), 0,
+                       (hipStream_t)stream, xyz, B, P, dx, ldx, C, Hf, Wf, cam_f, dgrid_nhwc);
+    if (hipGetLastError() != hipSuccess) {
+        sd_set_error("sd_field_gather_bwd: launch failed");
+        return -2;
+    }
+    return 0;
+}
+
+extern "C" int sd_composite_bwd(const float *z, const float *sigma, const float *feat, int64_t F,
+                                const float *rgb, int64_t Cc, int64_t R, int32_t K,
+                                int32_t hard_alpha_cap, const float *g_depth, const float *g_feat,
+                                const float *g_rgb, const float *g_weights, const float *g_alphas,
+                                float *d_sigma, float *d_feat, float *d_rgb, void *stream) {
+    if (R < 0 || K <= 0 || K > TR_MAXK || !z || !sigma || !d_sigma || F < 0 || Cc < 0 ||
+        (d_feat && (!feat || !g_feat)) || (d_rgb && (!rgb || !g_rgb)) ||
+        (g_feat && !feat) || (g_rgb && !rgb) || F >= (1 << 30) || Cc >= (1 << 30)) {
+        sd_set_error("sd_composite_bwd: invalid argument (0 < K <= 512; feature / colour "
+                     "gradients need their forward inputs)");
+        return -1;
+    }
+    if (R == 0) return 0;
+    hipLaunchKernelGGL(k_composite_bwd, dim3(tr_blocks(R)), dim3(TR_WAVES * 64), 0,
+                       (hipStream_t)stream, z, sigma, feat, (int)F, rgb, (int)Cc, R, K,
+                       hard_alpha_cap, g_depth, g_feat, g_rgb, g_weights, g_alphas, d_sigma,
+                       d_feat, d_rgb);
+    if (hipGetLastError() != hipSuccess) {
+        sd_set_error("sd_composite_bwd: launch failed");
+        return -2;
+    }
+    return 0;
+}

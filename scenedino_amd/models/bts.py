@@ -205,6 +205,8 @@ class BTSNet(nn.Module):
         grid kernel K % 32 == 0 and D in {32, 64, 128}; other shapes go through
         sd_field_query + sd_composite (also native)."""
         D = self._d_out - 1
+        if self._differentiable():
+            return False  # the renderer takes its generic (autograd) compositing path
         if self._use_proj():
             return K % 16 == 0 and K <= 128 and D % 16 == 0 and D <= 512
         return K % 32 == 0 and K <= 128 and D in (32, 64, 128)
@@ -271,11 +273,16 @@ class BTSNet(nn.Module):
             gc["proj_key"] = self._packed_key
         return gc["proj"]
 
+    def _differentiable(self) -> bool:
+        """Training path (autograd through sd_field_gather / ResnetFC / sd_composite) when
+        grad mode is on and the module trains or its feature grid carries a gradient;
+        otherwise the fused inference kernels."""
+        if not torch.is_grad_enabled():
+            return False
+        g = self.grid_f_features[self._scale] if self.grid_f_features else None
+        return self.training or (g is not None and g.requires_grad)
+
     def _check_supported(self):
-        if self.training and torch.is_grad_enabled():
-            raise NotImplementedError(
-                "scenedino_amd: backward kernels for the fused field are not implemented yet; "
-                "use eval() / torch.no_grad() (inference) with this build")
         if self.grid_c_combine is not None or self.color_frame_filter is not None:
             raise NotImplementedError("grid_c_combine / color_frame_filter (training) unsupported")
         if self.grid_f_extra is not None:
@@ -378,6 +385,28 @@ class BTSNet(nn.Module):
         self._timed("field", lambda: _lib.field_query(args, m.rec, xyz))
         return sigma, dino, rgb, inv, invf
 
+    def _query_diff(self, xyz):
+        """query() with autograd (training path, scenedino_amd/autograd.py): the grid is
+        gathered by sd_field_gather (backward sd_field_gather_bwd) and the prediction head
+        runs as its own nn.Linear layers, so gradients reach grid_f_features and the head
+        parameters as in bts.py:476-595."""
+        from ..autograd import FieldGather
+        self._check_supported()
+        head = self.heads[self.final_pred_head]
+        if len(self.heads) != 1:
+            raise NotImplementedError("the field path supports a single prediction head")
+        gc = self._grids()
+        g = self.grid_f_features[self._scale]
+        n, P, _ = xyz.shape
+        if n != gc["B"]:
+            raise ValueError(f"xyz batch {n} != encoded batch {gc['B']}")
+        grid_nhwc = g[:, 0].float().permute(0, 2, 3, 1).contiguous()  # differentiable
+        x, invf, rgb, inv = FieldGather.apply(grid_nhwc, xyz.float().contiguous(), gc["cam_f"],
+                                              gc["img"], gc["cam_c"], True)
+        out = head(x.reshape(n * P, 1, -1)).reshape(n, P, -1)  # bts.py:502-514
+        sigma = F.softplus(out[..., 0])
+        return sigma, out[..., 1:], rgb, inv, invf
+
     # -- segmentation head (SSCBench / inference_3d) ----------------------------
     def _dim_reduction(self):
         dr = getattr(self.encoder, "dim_reduction", None)
@@ -430,7 +459,10 @@ class BTSNet(nn.Module):
             raise NotImplementedError("render_flow is a training-only option")
         with torch.profiler.record_function("model_inference"):
             n_, n_pts, _ = xyz.shape
-            sigma, dino, rgb, inv, invf = self.query(xyz, colors=not predict_segmentation)
+            if not predict_segmentation and self._differentiable():
+                sigma, dino, rgb, inv, invf = self._query_diff(xyz)
+            else:
+                sigma, dino, rgb, inv, invf = self.query(xyz, colors=not predict_segmentation)
             sigma = sigma.unsqueeze(-1)
             if predict_segmentation:  # bts.py:584-592
                 D = dino.shape[-1]

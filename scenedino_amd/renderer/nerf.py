@@ -20,7 +20,7 @@ from __future__ import annotations
 
 import torch
 
-from .. import _lib
+from .. import _lib, autograd
 
 
 class _RenderWrapper(torch.nn.Module):
@@ -198,8 +198,9 @@ class NeRFRenderer(torch.nn.Module):
         if state_dicts is not None:
             state_dicts = {k: v.reshape(B, K, *v.shape[2:]) for k, v in state_dicts.items()}
         feat = state_dicts["dino_features"].float().contiguous() if state_dicts else None
-        weights, alphas, depth, feat_out, rgb_out = _lib.composite(
-            z_samp.float().contiguous(), sigmas, feat, rgbs, self.hard_alpha_cap)
+        # sd_composite; with autograd (sd_composite_bwd) when the field output carries grad
+        weights, alphas, depth, feat_out, rgb_out = autograd.composite(
+            z_samp, sigmas, feat, rgbs, self.hard_alpha_cap)
         if state_dicts is not None:
             state_dicts["dino_features"] = feat_out
         return weights, alphas, rgb_out, depth, invalid, rgbs, state_dicts

@@ -1,0 +1,193 @@
+"""Training path: backward of the field gather and the alpha
+compositing (sdhip_train.hip) against torch autograd of the reference op sequence
+(oracle/render_oracle.py, pinned by the golden renders), and gradients of a full
+train-mode render w.r.t. the feature grid and the ResnetFC parameters.
+
+Tolerances: composite backward rel-L2 <= 1e-4 vs float64 autograd; gather forward
+rtol 1e-5; gather backward and the end-to-end gradients rel-L2 <= 1e-3 vs float32 CPU
+autograd (atomic accumulation order and GEMM summation order differ)."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from _helpers import build_net, rel_l2
+from oracle import render_oracle as O
+from oracle import train_oracle as TO
+
+KN = torch.tensor([[0.7849, 0.0, -0.0312], [0.0, 2.9391, 0.2701], [0.0, 0.0, 1.0]])
+
+
+def _comp_inputs(R, K, F, Cc, seed):
+    g = torch.Generator().manual_seed(seed)
+    z = torch.sort(3 + 77 * torch.rand(R, K, generator=g, dtype=torch.float64), -1)[0]
+    sigma = torch.randn(R, K, generator=g, dtype=torch.float64) * 2
+    sigma[:, ::7] = 0.0  # relu kink
+    feat = torch.randn(R, K, F, generator=g, dtype=torch.float64)
+    rgb = torch.rand(R, K, Cc, generator=g, dtype=torch.float64)
+    grads = {"weights": torch.randn(R, K, generator=g, dtype=torch.float64),
+             "alphas": torch.randn(R, K, generator=g, dtype=torch.float64),
+             "depth": torch.randn(R, generator=g, dtype=torch.float64),
+             "dino": torch.randn(R, F, generator=g, dtype=torch.float64),
+             "rgb": torch.randn(R, Cc, generator=g, dtype=torch.float64)}
+    return z, sigma, feat, rgb, grads
+
+
+def _autograd_composite(z, sigma, feat, rgb, hard, grads):
+    s = sigma.clone().requires_grad_(True)
+    f = feat.clone().requires_grad_(True)
+    c = rgb.clone().requires_grad_(True)
+    out = O.composite(z, s, f, c, hard)
+    loss = sum((out[k] * grads[k]).sum() for k in grads)
+    loss.backward()
+    return s.grad, f.grad, c.grad
+
+
+@pytest.mark.parametrize("hard", [False, True])
+def test_composite_bwd_oracle_vs_autograd(hard):
+    """CPU: the division-free recurrence (what the kernel implements) equals autograd."""
+    z, sigma, feat, rgb, gr = _comp_inputs(40, 33, 8, 6, 1)
+    ds, df, dc = _autograd_composite(z, sigma, feat, rgb, hard, gr)
+    ds2, df2, dc2 = TO.composite_bwd(z.numpy(), sigma.numpy(), feat.numpy(), rgb.numpy(), hard,
+                                     gr["depth"].numpy(), gr["dino"].numpy(), gr["rgb"].numpy(),
+                                     gr["weights"].numpy(), gr["alphas"].numpy())
+    np.testing.assert_allclose(ds2, ds.numpy(), rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(df2, df.numpy(), rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(dc2, dc.numpy(), rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hard", [False, True])
+@pytest.mark.parametrize("K", [64, 100])
+def test_composite_bwd_gpu(hard, K):
+    from scenedino_amd import _lib
+    R, F, Cc = 300, 64, 6
+    z, sigma, feat, rgb, gr = _comp_inputs(R, K, F, Cc, 2 + K)
+    ds, df, dc = _autograd_composite(z, sigma, feat, rgb, hard, gr)
+    c = lambda t: t.float().cuda().contiguous()
+    d_sigma, d_feat, d_rgb = _lib.composite_bwd(
+        c(z), c(sigma), c(feat), c(rgb), hard, c(gr["depth"]), c(gr["dino"]), c(gr["rgb"]),
+        c(gr["weights"]), c(gr["alphas"]), need_feat=True, need_rgb=True)
+    assert rel_l2(d_sigma, ds) < 1e-4
+    assert rel_l2(d_feat, df) < 1e-5
+    assert rel_l2(d_rgb, dc) < 1e-5
+    # partial upstream gradients (only depth): other terms absent, not zero-filled garbage
+    d2, f2, _ = _lib.composite_bwd(c(z), c(sigma), c(feat), None, hard, c(gr["depth"]), None,
+                                   None, None, None, need_feat=True)
+    ds_d, _, _ = _autograd_composite(z, sigma, feat, rgb, hard, {"depth": gr["depth"]})
+    assert f2 is None
+    assert rel_l2(d2, ds_d) < 1e-4
+
+
+@pytest.mark.gpu
+def test_composite_autograd_function_gpu():
+    from scenedino_amd.autograd import Composite
+    z, sigma, feat, rgb, gr = _comp_inputs(128, 32, 64, 3, 7)
+    s = sigma.float().cuda().requires_grad_(True)
+    f = feat.float().cuda().requires_grad_(True)
+    w, a, d, fo, ro = Composite.apply(z.float().cuda(), s, f, rgb.float().cuda(), True)
+    (w * gr["weights"].float().cuda()).sum().add((fo * gr["dino"].float().cuda()).sum()) \
+        .add((d * gr["depth"].float().cuda()).sum()).backward()
+    ds, df, _ = _autograd_composite(z, sigma, feat, rgb, True,
+                                    {k: gr[k] for k in ("weights", "dino", "depth")})
+    assert rel_l2(s.grad, ds) < 1e-4
+    assert rel_l2(f.grad, df) < 1e-5
+
+
+def _gather_case(seed, B=2, P=3000, C=256, Hf=12, Wf=40):
+    g = torch.Generator().manual_seed(seed)
+    grid = torch.randn(B, C, Hf, Wf, generator=g)
+    # points spread over and beyond the frustum (border clamp, z <= eps, |xy| > 1)
+    xyz = torch.empty(B, P, 3)
+    xyz[..., 2] = torch.rand(B, P, generator=g) * 60 - 5
+    xyz[..., 0] = (torch.rand(B, P, generator=g) * 2.6 - 1.3) * xyz[..., 2].abs().clamp_min(1) / 0.78
+    xyz[..., 1] = (torch.rand(B, P, generator=g) * 2.6 - 1.3) * xyz[..., 2].abs().clamp_min(1) / 2.9
+    w2c = torch.eye(4).expand(B, 4, 4).clone()
+    w2c[1, 0, 3] = 0.4
+    Ks = KN.expand(B, 3, 3).clone()
+    return grid, xyz, w2c, Ks
+
+
+@pytest.mark.gpu
+def test_field_gather_fwd_bwd_gpu():
+    from scenedino_amd import _lib
+    from scenedino_amd.autograd import FieldGather
+    grid, xyz, w2c, Ks = _gather_case(3)
+    B, C, Hf, Wf = grid.shape
+    cam_f = _lib.cam_records(w2c.cuda(), Ks.cuda())
+    gn = grid.permute(0, 2, 3, 1).contiguous().cuda().requires_grad_(True)
+    x, invf, rgb, inv = FieldGather.apply(gn, xyz.cuda(), cam_f, None, None, False)
+    assert rgb is None and inv is None
+    # oracle: grid_sample (border, align_corners=False) + positional code
+    gl = grid.clone().requires_grad_(True)
+    xy, zz = O._project(xyz, w2c.unsqueeze(1), Ks.unsqueeze(1))
+    inv_ref = O._outside(xy, zz)[:, 0, :, 0]
+    xy = xy.clamp(-2, 2)
+    code = O.positional_code(xy[:, 0], zz[:, 0])
+    feat = torch.nn.functional.grid_sample(gl, xy.view(B, 1, -1, 2), mode="bilinear",
+                                           padding_mode="border", align_corners=False)
+    x_ref = torch.cat((feat.view(B, C, -1).permute(0, 2, 1), code), -1)
+    assert torch.equal(invf.cpu(), inv_ref)
+    np.testing.assert_allclose(x.detach().cpu().numpy(), x_ref.detach().numpy(), rtol=1e-5,
+                               atol=2e-5)
+    gx = torch.randn(x_ref.shape, generator=torch.Generator().manual_seed(4))
+    (x_ref * gx).sum().backward()
+    (x * gx.cuda()).sum().backward()
+    dg = gn.grad.permute(0, 3, 1, 2).cpu()
+    assert rel_l2(dg, gl.grad) < 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hard", [False, True])
+def test_train_mode_render_gradients_gpu(hard):
+    """train(): NeRFRenderer -> BTSNet.forward (sd_field_gather, ResnetFC, softplus) ->
+    sd_composite; loss.backward() reaches the feature grid and every head parameter
+    with the reference's gradients (oracle.render under CPU autograd)."""
+    from scenedino_amd.common.ray_sampler import ImageRaySampler
+    from scenedino_amd.renderer import NeRFRenderer
+    g = torch.Generator().manual_seed(5)
+    H, W, K, C, D = 12, 40, 32, 256, 64
+    images = torch.rand(1, 1, 3, H, W, generator=g) * 2 - 1
+    grid = torch.randn(1, C, 6, 20, generator=g)
+    W_in = torch.randn(128, C + 39, generator=g) * 0.08
+    b_in = torch.randn(128, generator=g) * 0.1
+    W_out = torch.randn(1 + D, 128, generator=g) * 0.1
+    b_out = torch.randn(1 + D, generator=g) * 0.1
+    pose = torch.eye(4).view(1, 1, 4, 4)
+    Kn = KN.view(1, 1, 3, 3)
+    u = torch.rand(H * W, K, generator=g)
+    dev = "cuda"
+    net = build_net(grid, W_in, b_in, W_out, b_out, "fp32", dev)
+    net.encode(images.to(dev), Kn.to(dev), pose.to(dev), ids_encoder=[0], ids_render=[0])
+    leaf = net.grid_f_features[0].detach().clone().requires_grad_(True)
+    net.grid_f_features[0] = leaf
+    net.train()
+    rays, _ = ImageRaySampler(3, 80, H, W).sample(None, pose.to(dev), Kn.to(dev))
+    r = NeRFRenderer(n_coarse=K, lindisp=True, hard_alpha_cap=hard, eval_batch_size=4096)
+    r.z_jitter = u.to(dev)
+    out = r.bind_parallel(net).train()(rays, want_weights=True)["coarse"]
+    gw = torch.randn(out["weights"].shape, generator=g)
+    gd = torch.randn(out["depth"].shape, generator=g)
+    gf = torch.randn(out["dino_features"].shape, generator=g)
+    gr = torch.randn(out["rgb"].shape, generator=g)
+    loss = ((out["weights"] * gw.to(dev)).sum() + (out["depth"] * gd.to(dev)).sum() +
+            (out["dino_features"] * gf.to(dev)).sum() + (out["rgb"] * gr.to(dev)).sum())
+    loss.backward()
+    head = net.heads["normal_head"]
+
+    lg = grid.clone().requires_grad_(True)
+    ps = [t.clone().requires_grad_(True) for t in (W_in, b_in, W_out, b_out)]
+    w2c = torch.inverse(pose)
+    ref = O.render(rays[0].cpu(), u, lg, w2c[:, 0], Kn[:, 0], images * 0.5 + 0.5, w2c, Kn,
+                   *ps, sb=1, hard_alpha_cap=hard)
+    for k in ("weights", "depth", "dino_features", "rgb"):
+        assert rel_l2(out[k].detach(), ref[k].detach()) < 1e-4, k
+    rl = ((ref["weights"] * gw).sum() + (ref["depth"] * gd).sum() +
+          (ref["dino_features"] * gf).sum() + (ref["rgb"] * gr).sum())
+    rl.backward()
+    assert leaf.grad is not None
+    assert rel_l2(leaf.grad.reshape(lg.shape), lg.grad) < 1e-3
+    for p, q, name in zip((head.lin_in.weight, head.lin_in.bias, head.lin_out.weight,
+                           head.lin_out.bias), ps, ("W_in", "b_in", "W_out", "b_out")):
+        assert rel_l2(p.grad, q.grad) < 1e-3, name
