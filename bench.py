@@ -453,6 +453,109 @@ def main_encode(args, world, rank, device):
         }), flush=True)
 
 
+def main_train(args, world, rank, device):
+    """Training step through the render path (train_scenedino_kitti_360
+    .yaml: batch_size 4, n_coarse 32, hard_alpha_cap, training/scenedino.yaml ray_batch_size
+    2048 in 8x8 patches): per step 4 frames x 2048 rays x 32 samples through BTSNet.forward
+    (sd_field_gather -> ResnetFC -> softplus) + sd_composite, an L2 loss on the rendered
+    DINO / colour maps, and loss.backward() (sd_composite_bwd, ResnetFC GEMM backward,
+    sd_field_gather_bwd into the 4 x 256 x 192 x 640 grid gradient).  The encoder backward is
+    not part of the step (the grid is the leaf)."""
+    from scenedino_amd import autograd as sda
+    from scenedino_amd.models import BTSNet
+    from scenedino_amd.models.prediction_heads import ResnetFC
+    from scenedino_amd.common.positional_encoding import PositionalEncoding
+    from scenedino_amd.renderer import NeRFRenderer
+    from scenedino_amd.common.ray_sampler import ImageRaySampler
+    NB, RB, KT, PS = 4, 2048, 32, 8
+    g = torch.Generator(device=device).manual_seed(rank)
+    grid = torch.randn(NB, C_GRID, HF, WF, device=device, generator=g)
+    torch.manual_seed(2)
+    head = ResnetFC(d_in=D_IN, d_out=1 + D_DINO, n_blocks=0, d_hidden=D_HIDDEN)
+    conf = {"predict_dino": True, "dino_dims": D_DINO, "learn_empty": False, "code_mode": "z",
+            "inv_z": True, "z_near": 3, "z_far": 80, "sample_color": True, "precision": "fp32"}
+    net = BTSNet(conf, FixedGridEncoder(grid), PositionalEncoding(6, 3, 1.5, True),
+                 {"normal_head": head}, final_pred_head="normal_head").to(device)
+    images = torch.rand(NB, 1, 3, H, W, device=device, generator=g) * 2 - 1
+    Ks = torch.tensor(KITTI_K, device=device).view(1, 1, 3, 3).expand(NB, 1, 3, 3).contiguous()
+    poses = torch.eye(4, device=device).view(1, 1, 4, 4).expand(NB, 1, 4, 4).contiguous()
+    with torch.no_grad():
+        net.encode(images, Ks, poses, ids_encoder=[0], ids_render=[0])
+    leaf = net.grid_f_features[0].detach().clone().requires_grad_(True)
+    net.grid_f_features[0] = leaf
+    net.train()
+    renderer = NeRFRenderer(n_coarse=KT, lindisp=True, hard_alpha_cap=True, eval_batch_size=65536)
+    wrapper = renderer.bind_parallel(net, gpus=None).train()
+    ray_poses = poses
+    if args.offset_pose:  # rays from a 0.5 m lateral / 2 deg yaw view: samples of a ray
+        import math        # project onto different texels of the encoder grid
+        a = math.radians(2.0)
+        ray_poses = poses.clone()
+        ray_poses[:, 0, 0, 0] = math.cos(a); ray_poses[:, 0, 0, 2] = math.sin(a)
+        ray_poses[:, 0, 2, 0] = -math.sin(a); ray_poses[:, 0, 2, 2] = math.cos(a)
+        ray_poses[:, 0, 0, 3] = 0.5
+    all_rays, _ = ImageRaySampler(3, 80, H, W).sample(None, ray_poses, Ks)  # (NB, H*W, 11)
+    opt = torch.optim.Adam(list(head.parameters()) + [leaf], lr=1e-4)
+    target_dino = torch.randn(NB, RB, D_DINO, device=device, generator=g)
+    target_rgb = torch.rand(NB, RB, 3, device=device, generator=g)
+    npatch = RB // (PS * PS)
+    oy, ox = torch.meshgrid(torch.arange(PS, device=device), torch.arange(PS, device=device),
+                            indexing="ij")
+
+    def step():
+        # PatchRaySampler-shaped batch: npatch random 8x8 patches per frame
+        py = torch.randint(0, H - PS + 1, (NB, npatch, 1, 1), device=device, generator=g)
+        px = torch.randint(0, W - PS + 1, (NB, npatch, 1, 1), device=device, generator=g)
+        idx = ((py + oy) * W + (px + ox)).reshape(NB, RB)
+        rays = torch.gather(all_rays, 1, idx.unsqueeze(-1).expand(NB, RB, all_rays.shape[-1]))
+        out = wrapper(rays, want_weights=True)["coarse"]
+        loss = ((out["dino_features"] - target_dino) ** 2).mean() + \
+            (out["rgb"] - target_rgb).abs().mean()
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+        return loss
+
+    timer = KernelTimer()
+    sda.kernel_timer = timer
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    timer.on = True
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    timer.on = False
+    sda.kernel_timer = None
+    ms = {k: timer.mean_ms(k) for k in ("gather", "gather_bwd", "composite_bwd")}
+    n_pts = NB * RB * KT
+    # compulsory HBM bytes of the scatter: dX rows read (4 C B / point) + the grid gradient
+    # written once (4 C B / grid pixel); taps re-hit L2 (atomics execute in L2)
+    bwd_bytes = n_pts * 4 * C_GRID + NB * HF * WF * C_GRID * 4
+    line = {
+        "metric": "training rays/sec (render forward + backward into grid and ResnetFC)",
+        "value": world * NB * RB * args.steps / elapsed, "unit": "rays/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (N(0,1) 4x256x192x640 grid, U[-1,1) images, random targets)",
+        "config": {"workload": "train: 4 frames x 2048 rays (8x8 patches) x 32 samples, "
+                               "hard_alpha_cap, ResnetFC 295-128-65, Adam step" +
+                               (", rays from an offset view" if args.offset_pose else
+                                ", rays from the encoder view"),
+                   "points_per_step": n_pts, "parallelism": f"frames{world}"},
+        "roofline": {"kernel": "k_field_gather_bwd (sd_field_gather_bwd)", "bound": "hbm",
+                     "achieved": bwd_bytes / (ms["gather_bwd"] * 1e-3) / 1e9, "peak": 8000.0,
+                     "unit": "GB/s",
+                     "frac": bwd_bytes / (ms["gather_bwd"] * 1e-3) / 1e9 / 8000.0,
+                     "traffic": None, "kernel_ms": ms["gather_bwd"],
+                     "gather_ms": ms["gather"], "composite_bwd_ms": ms["composite_bwd"]},
+    }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -463,11 +566,12 @@ def main():
     ap.add_argument("--mode", default="proj", choices=["proj", "grid"],
                     help="16-bit render kernel: projected grid (default) or per-sample grid")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--config", default="c2", choices=["c2", "c4", "c5", "vit", "encode"],
+    ap.add_argument("--config", default="c2", choices=["c2", "c4", "c5", "vit", "encode", "train"],
                     help="c2: BASELINE configs[1] (K=64, D=64, the metric's config); c4: "
                          "configs[3] render shape (K=128, 384-d feature field); c5: "
                          "configs[4] SSCBench voxel query (voxels/s); vit: the DINO ViT "
-                         "encoder forward (a19); encode: ViT + DPT decoder (DINOv2Module)")
+                         "encoder forward (a19); encode: ViT + DPT decoder (DINOv2Module); "
+                         "train: render forward + backward (training step)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-end-to-end", action="store_true",
                     help="c2: skip the encode + render frame timing reported beside value")
@@ -490,8 +594,10 @@ def main():
 
     from scenedino_amd import _lib
     _lib.load()
-    if args.config in ("c5", "vit", "encode"):
-        if args.config == "c5":
+    if args.config in ("c5", "vit", "encode", "train"):
+        if args.config == "train":
+            main_train(args, world, rank, device)
+        elif args.config == "c5":
             main_c5(args, world, rank, local_rank, dist, device)
         elif args.config == "vit":
             main_vit(args, world, rank, device)

@@ -196,8 +196,8 @@ int sd_composite(const float *z, const float *sigma, const float *feat, int64_t 
 /* MLP input rows of the training path: per point the projection / frustum mask
  * (pinhole.py:40-112), the bilinear border gather of the C grid channels
  * (bts.py:299-309, F.grid_sample align_corners=False) and the 39-d positional code
- * (positional_encoding.py:13-80), written as x_out (B*P, C+39) = [feat | code]
- * (bts.py:321-328).  grid_nhwc (B, Hf, Wf, C) f32.  Colour samples / masks as
+ * (positional_encoding.py:13-80), written as x_out (B*P, C+40) = [feat | code | 1]
+ * (bts.py:321-328; the constant 1 column carries the ResnetFC biases through its GEMMs).  grid_nhwc (B, Hf, Wf, C) f32.  Colour samples / masks as
  * sd_field_query (bts.py:330-441; rgb, invalid, img, cam_c may be NULL / nv = 0). */
 int sd_field_gather(const float *xyz, int64_t B, int64_t P, const float *grid_nhwc,
                     int32_t C, int32_t Hf, int32_t Wf, const float *cam_f,
@@ -211,6 +211,11 @@ int sd_field_gather(const float *xyz, int64_t B, int64_t P, const float *grid_nh
 int sd_field_gather_bwd(const float *xyz, int64_t B, int64_t P, const float *dx,
                         int64_t ldx, int32_t C, int32_t Hf, int32_t Wf,
                         const float *cam_f, float *dgrid_nhwc, void *stream);
+
+/* NHWC f32 (B, H, W, C) -> NCHW f32 (B, C, H, W): the grid gradient of the training path
+ * back in the encoder's layout (inverse of sd_pack_grid with dtype SD_F32). */
+int sd_unpack_grid(const float *grid_nhwc, int64_t B, int64_t C, int64_t H, int64_t W,
+                   float *grid_nchw, void *stream);
 
 /* Backward of sd_composite (alpha compositing, nerf.py:376-405): upstream gradients
  * of depth (R), feat_out (R,F), rgb_out (R,Cc), weights (R,K), alphas (R,K) (any may be

@@ -111,6 +111,7 @@ SIGNATURES = {
     "sd_field_gather": [_vp, _i64, _i64, _vp, _i32, _i32, _i32, _vp, _vp, _i32, _i32, _i32, _vp,
                         _vp, _vp, _vp, _vp, _vp],
     "sd_field_gather_bwd": [_vp, _i64, _i64, _vp, _i64, _i32, _i32, _i32, _vp, _vp, _vp],
+    "sd_unpack_grid": [_vp, _i64, _i64, _i64, _i64, _vp, _vp],
     "sd_composite_bwd": [_vp, _vp, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp, _vp,
                          _vp, _vp, _vp, _vp, _vp],
     "sd_project_grid": [_vp, _i64, _i64, _i64, ctypes.POINTER(SdMlp), _vp, _vp],
@@ -337,13 +338,13 @@ def composite(z, sigma, feat, rgb, hard_alpha_cap, want_weights=True):
 
 
 def field_gather(xyz, grid_nhwc, cam_f, img=None, cam_c=None, colors=True):
-    """sd_field_gather: xyz (B,P,3), grid_nhwc (B,Hf,Wf,C) f32 -> x (B,P,C+39),
+    """sd_field_gather: xyz (B,P,3), grid_nhwc (B,Hf,Wf,C) f32 -> x (B,P,C+40) = [feat|code|1],
     invalid_f (B,P) bool, rgb (B,P,3nv) | None, invalid (B,P,nv) | None."""
     lib = load()
     B, P, _ = xyz.shape
     _, Hf, Wf, C = grid_nhwc.shape
     dev = xyz.device
-    x = torch.empty(B, P, C + 39, device=dev)
+    x = torch.empty(B, P, C + 40, device=dev)
     invf = torch.empty(B, P, device=dev, dtype=torch.bool)
     nv, Hc, Wc = 0, 0, 0
     if colors:  # img: pack_image output (B*nv, Hc, Wc, 4); cam_c (B, nv, 21)
@@ -357,18 +358,29 @@ def field_gather(xyz, grid_nhwc, cam_f, img=None, cam_c=None, colors=True):
     return x, invf, rgb, inv
 
 
-def field_gather_bwd(xyz, dx, cam_f, Hf, Wf, C):
-    """sd_field_gather_bwd: dx (B,P,>=C) (unit inner stride) -> dgrid (B,Hf,Wf,C) f32."""
+def field_gather_bwd(xyz, dx, cam_f, Hf, Wf, C, dgrid=None):
+    """sd_field_gather_bwd: dx (B,P,>=C) -> dgrid (B,Hf,Wf,C) f32 (zeros, or accumulated
+    into the given dgrid)."""
     lib = load()
     B, P, _ = xyz.shape
-    if dx.stride(-1) != 1 or dx.dtype != torch.float32 or dx.stride(1) != dx.shape[-1] \
-            or dx.stride(0) != P * dx.shape[-1]:
-        dx = dx.float().contiguous()
-    dgrid = torch.zeros(B, Hf, Wf, C, device=xyz.device)
+    dx = dx.float().contiguous()
+    if dgrid is None:
+        dgrid = torch.zeros(B, Hf, Wf, C, device=xyz.device)
+    _req(dgrid, "dgrid")
     _check(lib.sd_field_gather_bwd(ptr(_req(xyz, "xyz")), B, P, ptr(dx), dx.shape[-1], C, Hf, Wf,
                                    ptr(_req(cam_f, "cam_f")), ptr(dgrid), stream_of(dgrid)),
            "sd_field_gather_bwd")
     return dgrid
+
+
+def unpack_grid(grid_nhwc):
+    """sd_unpack_grid: (B,H,W,C) f32 -> (B,C,H,W) f32."""
+    lib = load()
+    B, H, W, C = grid_nhwc.shape
+    out = torch.empty(B, C, H, W, device=grid_nhwc.device)
+    _check(lib.sd_unpack_grid(ptr(_req(grid_nhwc, "grid")), B, C, H, W, ptr(out),
+                              stream_of(out)), "sd_unpack_grid")
+    return out
 
 
 def composite_bwd(z, sigma, feat, rgb, hard_alpha_cap, g_depth, g_feat, g_rgb, g_weights,

@@ -20,17 +20,59 @@ import torch
 
 from . import _lib
 
+# bench hook: an object with start(name) / stop(name) (HIP events on the launch stream)
+kernel_timer = None
 
-class FieldGather(torch.autograd.Function):
-    """X = [grid_sample(grid, project(xyz)) | positional_code(xyz)], differentiable in the
-    grid (bts.py:271-328).  grid_nhwc (B, Hf, Wf, C) f32; xyz (B, P, 3) (no gradient: the
-    reference's sample points come from rays and depths without grad)."""
+
+def _timed(name, fn):
+    t = kernel_timer
+    if t is not None:
+        t.start(name)
+    r = fn()
+    if t is not None:
+        t.stop(name)
+    return r
+
+
+class GridNHWC(torch.autograd.Function):
+    """NCHW f32 grid (B, C, Hf, Wf) -> NHWC f32 (sd_pack_grid); backward sd_unpack_grid."""
 
     @staticmethod
-    def forward(ctx, grid_nhwc, xyz, cam_f, img, cam_c, colors):
-        x, invf, rgb, inv = _lib.field_gather(xyz, grid_nhwc, cam_f, img, cam_c, colors)
+    def forward(ctx, grid_nchw):
+        return _lib.pack_grid(grid_nchw.float().contiguous(), _lib.SD_F32)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _lib.unpack_grid(g.float().contiguous())
+
+
+class GatherAcc:
+    """Grid-gradient accumulator shared by the FieldGather calls of one compositing pass
+    (the renderer's chunks): every chunk's backward scatters into ONE zeroed NHWC buffer,
+    handed to autograd by the first chunk of the backward pass (the others return no
+    gradient), instead of one zeroed 4 x 126 MB buffer per chunk summed by autograd.
+    Autograd runs the grid's node only after every chunk's backward, so the buffer is
+    complete when it is read."""
+
+    def __init__(self):
+        self.n = 0        # FieldGather calls recorded in the forward pass
+        self.left = 0     # chunks still to run in the current backward pass
+        self.buf = None
+
+
+class FieldGather(torch.autograd.Function):
+    """X = [grid_sample(grid, project(xyz)) | positional_code(xyz) | 1], differentiable in
+    the grid (bts.py:271-328).  grid_nhwc (B, Hf, Wf, C) f32; xyz (B, P, 3) (no gradient:
+    the reference's sample points come from rays and depths without grad)."""
+
+    @staticmethod
+    def forward(ctx, grid_nhwc, xyz, cam_f, img, cam_c, colors, acc=None):
+        x, invf, rgb, inv = _timed("gather", lambda: _lib.field_gather(
+            xyz, grid_nhwc, cam_f, img, cam_c, colors))
         ctx.save_for_backward(xyz, cam_f)
         ctx.grid_shape = tuple(grid_nhwc.shape)
+        ctx.acc = acc if acc is not None else GatherAcc()
+        ctx.acc.n += 1
         outs = [t for t in (invf, rgb, inv) if t is not None]
         ctx.mark_non_differentiable(*outs)
         return x, invf, rgb, inv
@@ -38,11 +80,57 @@ class FieldGather(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gx, *_):
         xyz, cam_f = ctx.saved_tensors
-        dgrid = None
-        if ctx.needs_input_grad[0] and gx is not None:
-            _, Hf, Wf, C = ctx.grid_shape
-            dgrid = _lib.field_gather_bwd(xyz, gx, cam_f, Hf, Wf, C)
-        return dgrid, None, None, None, None, None
+        if not ctx.needs_input_grad[0] or gx is None:
+            return None, None, None, None, None, None, None
+        B, Hf, Wf, C = ctx.grid_shape
+        acc = ctx.acc
+        first = acc.left == 0
+        if first:
+            acc.left = acc.n
+            acc.buf = torch.zeros(B, Hf, Wf, C, device=xyz.device)
+        _timed("gather_bwd", lambda: _lib.field_gather_bwd(xyz, gx, cam_f, Hf, Wf, C,
+                                                           dgrid=acc.buf))
+        acc.left -= 1
+        out = acc.buf if first else None
+        if acc.left == 0:
+            acc.buf = None
+        return out, None, None, None, None, None, None
+
+
+class FieldMLP(torch.autograd.Function):
+    """ResnetFC with n_blocks = 0 (resnetfc.py:135-203): out = W_o relu(W_i x + b_i) + b_o
+    on the gather rows x_aug = [x | 1] (N, d_in + 1).  The biases ride in the GEMMs:
+    W2 = [[W_i, b_i], [0, 1]] (129 x (d_in+1)) gives h_aug = relu(x_aug W2^T) = [h | 1] and
+    Wo = [W_o, b_o] gives out = h_aug Wo^T, so the backward is three GEMMs whose extra
+    column / row are the bias gradients -- no column reductions (torch's are the slowest
+    op of the step at 65 536-point chunks)."""
+
+    @staticmethod
+    def forward(ctx, x_aug, w_in, b_in, w_out, b_out):
+        dh, d_in = w_in.shape
+        if x_aug.shape[1] != d_in + 1:
+            raise ValueError(f"FieldMLP: x_aug has {x_aug.shape[1]} columns, expected {d_in + 1}")
+        W2 = torch.zeros(dh + 1, d_in + 1, device=w_in.device, dtype=w_in.dtype)
+        W2[:dh, :d_in] = w_in
+        W2[:dh, d_in] = b_in
+        W2[dh, d_in] = 1.0
+        Wo = torch.cat((w_out, b_out[:, None]), 1)
+        h = torch.relu(x_aug @ W2.t())
+        out = h @ Wo.t()
+        ctx.save_for_backward(x_aug, h, W2, Wo)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x_aug, h, W2, Wo = ctx.saved_tensors
+        g = g.contiguous()
+        dh_, d_in = W2.shape[0] - 1, W2.shape[1] - 1
+        dWo = g.t() @ h
+        dh = (g @ Wo) * (h > 0)
+        dW2 = dh.t() @ x_aug
+        dx = dh @ W2 if ctx.needs_input_grad[0] else None
+        return (dx, dW2[:dh_, :d_in].contiguous(), dW2[:dh_, d_in].contiguous(),
+                dWo[:, :dh_].contiguous(), dWo[:, dh_].contiguous())
 
 
 class Composite(torch.autograd.Function):
@@ -65,9 +153,9 @@ class Composite(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_w, g_a, g_d, g_f, g_r):
         z, sigma, feat, rgb = ctx.saved_tensors
-        d_sigma, d_feat, d_rgb = _lib.composite_bwd(
+        d_sigma, d_feat, d_rgb = _timed("composite_bwd", lambda: _lib.composite_bwd(
             z, sigma, feat, rgb, ctx.hard, g_d, g_f, g_r, g_w, g_a,
-            need_feat=ctx.needs_input_grad[2], need_rgb=ctx.needs_input_grad[3])
+            need_feat=ctx.needs_input_grad[2], need_rgb=ctx.needs_input_grad[3]))
         return (None, d_sigma if ctx.needs_input_grad[1] else None, d_feat, d_rgb, None)
 
 

@@ -8,7 +8,8 @@
 //
 //   k_field_gather      a8-a10 + a15: per point, projection, frustum mask, the bilinear
 //                       border gather of the C grid channels and the 39-d positional code,
-//                       written as the MLP input row X = [feat | code] (bts.py:321-328),
+//                       written as the MLP input row X = [feat | code | 1] (bts.py:321-328;
+//                       the trailing 1 folds the ResnetFC biases into its GEMMs),
 //                       plus the colour samples / invalid masks (no gradient: images are
 //                       data).  The ResnetFC layers are plain library GEMMs (autograd).
 //   k_field_gather_bwd  grid_sample backward (bts.py:299-309): dX[:, :C] scattered into the
@@ -53,7 +54,7 @@ k_field_gather(const float *__restrict__ xyz, int64_t B, int64_t P,
                float *__restrict__ invalid) {
     const int lane = threadIdx.x & 63;
     const int64_t NP = B * P;
-    const int ld = C + 39;
+    const int ld = C + 40;  // [feat (C) | code (39) | 1]: the 1 carries the bias through the GEMM
     const int64_t plane = (int64_t)Hf * Wf * C;
     const int64_t cplane = (int64_t)Hc * Wc * 4;
     for (int64_t p = (int64_t)blockIdx.x * TR_WAVES + (threadIdx.x >> 6); p < NP;
@@ -85,6 +86,8 @@ k_field_gather(const float *__restrict__ xyz, int64_t B, int64_t P,
                 r = sinf(fmaf(geo.v[co], f, cs ? 1.5707963705062866f : 0.f));
             }
             xr[C + lane] = r;
+        } else if (lane == 39) {
+            xr[C + 39] = 1.f;
         }
         if (lane == 0 && invalid_f) invalid_f[p] = geo.inv_f ? 1 : 0;
         if (lane < nv && (rgb || invalid)) {
@@ -104,34 +107,63 @@ k_field_gather(const float *__restrict__ xyz, int64_t B, int64_t P,
 
 // ---------------------------------------------------------------------------
 // gather backward: dG (B, Hf, Wf, C) += bilinear scatter of dX[:, :C]
+// One wave per run of TR_RUN consecutive points (a ray's samples are consecutive, and
+// they often project onto the same 2x2 texels -- always when the render view is the
+// encoder view): contributions are summed in registers while a point's four tap indices
+// equal the previous point's, and only flushed to HBM (f32 atomics in L2) when they change.
 // ---------------------------------------------------------------------------
+#define TR_RUN 16
+
+__device__ __forceinline__ void tr_flush(float *g, const int idx[4], const f32x4 acc[4], int C,
+                                         int c) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        float *dst = g + (int64_t)idx[t] * C + c;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (acc[t][i] != 0.f) unsafeAtomicAdd(dst + i, acc[t][i]);
+    }
+}
+
 __global__ void __launch_bounds__(TR_WAVES * 64)
 k_field_gather_bwd(const float *__restrict__ xyz, int64_t B, int64_t P,
                    const float *__restrict__ dx, int64_t ldx, int C, int Hf, int Wf,
                    const float *__restrict__ cam_f, float *__restrict__ dgrid) {
     const int lane = threadIdx.x & 63;
     const int64_t NP = B * P;
+    const int64_t nruns = (NP + TR_RUN - 1) / TR_RUN;
     const int64_t plane = (int64_t)Hf * Wf * C;
-    for (int64_t p = (int64_t)blockIdx.x * TR_WAVES + (threadIdx.x >> 6); p < NP;
-         p += (int64_t)gridDim.x * TR_WAVES) {
-        const int64_t b = p / P;
-        const PointGeo geo =
-            sd_point_geo(cam_f + b * 21, xyz[p * 3], xyz[p * 3 + 1], xyz[p * 3 + 2], Wf, Hf);
-        float *g = dgrid + b * plane;
-        const float *dr = dx + p * ldx;
+    for (int64_t run = (int64_t)blockIdx.x * TR_WAVES + (threadIdx.x >> 6); run < nruns;
+         run += (int64_t)gridDim.x * TR_WAVES) {
+        const int64_t p0 = run * TR_RUN;
+        const int64_t p1 = p0 + TR_RUN < NP ? p0 + TR_RUN : NP;
         for (int c = lane * 4; c < C; c += 256) {
-            f32x4 v;
+            int idx[4] = {-1, -1, -1, -1};
+            int64_t bcur = -1;
+            f32x4 acc[4] = {};
+            for (int64_t p = p0; p < p1; ++p) {
+                const int64_t b = p / P;
+                const PointGeo geo = sd_point_geo(cam_f + b * 21, xyz[p * 3], xyz[p * 3 + 1],
+                                                  xyz[p * 3 + 2], Wf, Hf);
+                const int ni[4] = {geo.t.i00, geo.t.i01, geo.t.i10, geo.t.i11};
+                const float wt[4] = {geo.t.w00, geo.t.w01, geo.t.w10, geo.t.w11};
+                if (b != bcur || ni[0] != idx[0] || ni[1] != idx[1] || ni[2] != idx[2] ||
+                    ni[3] != idx[3]) {  // wave-uniform branch
+                    if (bcur >= 0) tr_flush(dgrid + bcur * plane, idx, acc, C, c);
+                    bcur = b;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) v[i] = dr[c + i];
-            const int idx[4] = {geo.t.i00, geo.t.i01, geo.t.i10, geo.t.i11};
-            const float wt[4] = {geo.t.w00, geo.t.w01, geo.t.w10, geo.t.w11};
+                    for (int t = 0; t < 4; ++t) {
+                        idx[t] = ni[t];
+                        acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    }
+                }
+                const f32x4 v = *(const f32x4 *)(dx + p * ldx + c);
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                if (wt[t] == 0.f) continue;  // clamped duplicate taps carry weight 0
-                float *dst = g + (int64_t)idx[t] * C + c;
+                for (int t = 0; t < 4; ++t)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) unsafeAtomicAdd(dst + i, v[i] * wt[t]);
+                    for (int i = 0; i < 4; ++i) acc[t][i] += v[i] * wt[t];
             }
+            if (bcur >= 0) tr_flush(dgrid + bcur * plane, idx, acc, C, c);
         }
     }
 }
@@ -232,6 +264,29 @@ k_composite_bwd(const float *__restrict__ z, const float *__restrict__ sigma,
 }
 
 // ---------------------------------------------------------------------------
+// NHWC f32 -> NCHW f32 (the grid gradient back in the encoder's layout) through a
+// 32x33 LDS tile; grid (W/32, C/32, B*H); inverse of sdhip_rays.hip's k_pack_grid
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_unpack_grid(const float *__restrict__ in, int64_t C,
+                                                     int64_t H, int64_t W,
+                                                     float *__restrict__ out) {
+    __shared__ float tile[32][33];
+    const int64_t bh = blockIdx.z;
+    const int64_t b = bh / H, y = bh - b * H;
+    const int64_t x0 = (int64_t)blockIdx.x * 32, c0 = (int64_t)blockIdx.y * 32;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+    for (int j = ty; j < 32; j += 8) {  // rows = pixels x, columns = channels c (contiguous)
+        const int64_t x = x0 + j, c = c0 + tx;
+        tile[j][tx] = (c < C && x < W) ? in[((b * H + y) * W + x) * C + c] : 0.f;
+    }
+    __syncthreads();
+    for (int j = ty; j < 32; j += 8) {
+        const int64_t c = c0 + j, x = x0 + tx;
+        if (c < C && x < W) out[((b * C + c) * H + y) * W + x] = tile[tx][j];
+    }
+}
+
+// ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
 static int tr_blocks(int64_t units) {
@@ -271,7 +326,11 @@ extern "C" int sd_field_gather_bwd(const float *xyz, int64_t B, int64_t P, const
         return -1;
     }
     if (P == 0) return 0;
-    hipLaunchKernelGGL(k_field_gather_bwd, dim3(tr_blocks(B * P)), dim3(TR_WAVES * 64), 0,
+    if (ldx % 4) {
+        sd_set_error("sd_field_gather_bwd: ldx must be a multiple of 4 (16-B row loads)");
+        return -1;
+    }
+    hipLaunchKernelGGL(k_field_gather_bwd, dim3(tr_blocks((B * P + TR_RUN - 1) / TR_RUN)), dim3(TR_WAVES * 64), 0,
                        (hipStream_t)stream, xyz, B, P, dx, ldx, C, Hf, Wf, cam_f, dgrid_nhwc);
     if (hipGetLastError() != hipSuccess) {
         sd_set_error("sd_field_gather_bwd: launch failed");
@@ -299,6 +358,24 @@ extern "C" int sd_composite_bwd(const float *z, const float *sigma, const float 
                        d_feat, d_rgb);
     if (hipGetLastError() != hipSuccess) {
         sd_set_error("sd_composite_bwd: launch failed");
+        return -2;
+    }
+    return 0;
+}
+
+extern "C" int sd_unpack_grid(const float *grid_nhwc, int64_t B, int64_t C, int64_t H, int64_t W,
+                              float *grid_nchw, void *stream) {
+    if (B < 0 || C <= 0 || H <= 0 || W <= 0 || !grid_nhwc || !grid_nchw ||
+        B * H >= (1LL << 31)) {
+        sd_set_error("sd_unpack_grid: invalid argument");
+        return -1;
+    }
+    if (B == 0) return 0;
+    dim3 g((unsigned)((W + 31) / 32), (unsigned)((C + 31) / 32), (unsigned)(B * H));
+    hipLaunchKernelGGL(k_unpack_grid, g, dim3(256), 0, (hipStream_t)stream, grid_nhwc, C, H, W,
+                       grid_nchw);
+    if (hipGetLastError() != hipSuccess) {
+        sd_set_error("sd_unpack_grid: launch failed");
         return -2;
     }
     return 0;

@@ -89,6 +89,7 @@ class BTSNet(nn.Module):
         self._packed = None
         self._packed_key = None
         self._grid_cache = None
+        self._in_pass, self._pass_nhwc = False, None  # training-path NHWC grid per pass
         self._grid_key = None
         self._loss_features = None
         self._loss_pending = None
@@ -282,6 +283,13 @@ class BTSNet(nn.Module):
         g = self.grid_f_features[self._scale] if self.grid_f_features else None
         return self.training or (g is not None and g.requires_grad)
 
+    def begin_pass(self):
+        """Renderer hook: the chunked model calls of one compositing pass follow."""
+        self._in_pass, self._pass_nhwc = True, None
+
+    def end_pass(self):
+        self._in_pass, self._pass_nhwc = False, None
+
     def _check_supported(self):
         if self.grid_c_combine is not None or self.color_frame_filter is not None:
             raise NotImplementedError("grid_c_combine / color_frame_filter (training) unsupported")
@@ -390,7 +398,7 @@ class BTSNet(nn.Module):
         gathered by sd_field_gather (backward sd_field_gather_bwd) and the prediction head
         runs as its own nn.Linear layers, so gradients reach grid_f_features and the head
         parameters as in bts.py:476-595."""
-        from ..autograd import FieldGather
+        from ..autograd import FieldGather, FieldMLP, GatherAcc, GridNHWC
         self._check_supported()
         head = self.heads[self.final_pred_head]
         if len(self.heads) != 1:
@@ -400,10 +408,24 @@ class BTSNet(nn.Module):
         n, P, _ = xyz.shape
         if n != gc["B"]:
             raise ValueError(f"xyz batch {n} != encoded batch {gc['B']}")
-        grid_nhwc = g[:, 0].float().permute(0, 2, 3, 1).contiguous()  # differentiable
-        x, invf, rgb, inv = FieldGather.apply(grid_nhwc, xyz.float().contiguous(), gc["cam_f"],
-                                              gc["img"], gc["cam_c"], True)
-        out = head(x.reshape(n * P, 1, -1)).reshape(n, P, -1)  # bts.py:502-514
+        # NHWC copy of the grid (differentiable); shared by the chunks of one compositing
+        # pass (begin_pass / end_pass from the renderer), else made per call
+        key = (id(g), g._version)
+        nh = self._pass_nhwc
+        if nh is None or nh[0] != key:
+            nh = (key, GridNHWC.apply(g[:, 0]), GatherAcc())
+            if self._in_pass:
+                self._pass_nhwc = nh
+        x, invf, rgb, inv = FieldGather.apply(nh[1], xyz.float().contiguous(), gc["cam_f"],
+                                              gc["img"], gc["cam_c"], True, nh[2])
+        x = x.reshape(n * P, -1)
+        if (type(head).__name__ == "ResnetFC" and getattr(head, "n_blocks", 1) == 0
+                and getattr(head, "d_latent", 1) == 0 and isinstance(head.activation, nn.ReLU)
+                and getattr(head, "view_number", None) in (None, 0)):
+            out = FieldMLP.apply(x, head.lin_in.weight, head.lin_in.bias,
+                                 head.lin_out.weight, head.lin_out.bias).reshape(n, P, -1)
+        else:  # any other head: its own forward on [feat | code] (bts.py:502-514)
+            out = head(x[:, :-1].reshape(n * P, 1, -1)).reshape(n, P, -1)
         sigma = F.softplus(out[..., 0])
         return sigma, out[..., 1:], rgb, inv, invf
 

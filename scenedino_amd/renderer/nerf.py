@@ -183,14 +183,22 @@ class NeRFRenderer(torch.nn.Module):
         chunks = torch.split(points, bs, dim=dim)
         infos = torch.split(ray_info, bs, dim=dim) if ray_info is not None else [None] * len(chunks)
         rgbs_all, inv_all, sig_all, sds = [], [], [], []
-        for pnts, info in zip(chunks, infos):
-            rgbs, invalid, sigmas, extras, sd = model(pnts, coarse=coarse, only_density=False,
-                                                      ray_info=info, render_flow=self.render_flow)
-            if extras is not None:
-                raise NotImplementedError("field extras are not used by shipped configs")
-            rgbs_all.append(rgbs); inv_all.append(invalid); sig_all.append(sigmas)
-            if sd is not None:
-                sds.append(sd)
+        hooks = hasattr(model, "begin_pass") and hasattr(model, "end_pass")
+        if hooks:
+            model.begin_pass()
+        try:
+            for pnts, info in zip(chunks, infos):
+                rgbs, invalid, sigmas, extras, sd = model(pnts, coarse=coarse, only_density=False,
+                                                          ray_info=info,
+                                                          render_flow=self.render_flow)
+                if extras is not None:
+                    raise NotImplementedError("field extras are not used by shipped configs")
+                rgbs_all.append(rgbs); inv_all.append(invalid); sig_all.append(sigmas)
+                if sd is not None:
+                    sds.append(sd)
+        finally:
+            if hooks:
+                model.end_pass()
         rgbs = torch.cat(rgbs_all, dim=dim).reshape(B, K, -1).float().contiguous()
         invalid = torch.cat(inv_all, dim=dim).reshape(B, K, -1)
         sigmas = torch.cat(sig_all, dim=dim).reshape(B, K).float().contiguous()

@@ -129,6 +129,8 @@ def test_field_gather_fwd_bwd_gpu():
                                            padding_mode="border", align_corners=False)
     x_ref = torch.cat((feat.view(B, C, -1).permute(0, 2, 1), code), -1)
     assert torch.equal(invf.cpu(), inv_ref)
+    assert bool((x[..., -1] == 1).all())  # the bias column
+    x = x[..., :-1]
     np.testing.assert_allclose(x.detach().cpu().numpy(), x_ref.detach().numpy(), rtol=1e-5,
                                atol=2e-5)
     gx = torch.randn(x_ref.shape, generator=torch.Generator().manual_seed(4))
@@ -136,6 +138,37 @@ def test_field_gather_fwd_bwd_gpu():
     (x * gx.cuda()).sum().backward()
     dg = gn.grad.permute(0, 3, 1, 2).cpu()
     assert rel_l2(dg, gl.grad) < 1e-5
+
+
+@pytest.mark.gpu
+def test_grid_layout_and_field_mlp_gpu():
+    """GridNHWC (sd_pack_grid / sd_unpack_grid) round trip and gradient; FieldMLP (biases
+    folded into the GEMMs) vs the nn.Linear pair under autograd."""
+    from scenedino_amd.autograd import FieldMLP, GridNHWC
+    g = torch.Generator().manual_seed(9)
+    grid = torch.randn(2, 64, 7, 45, generator=g).cuda().requires_grad_(True)
+    nh = GridNHWC.apply(grid)
+    assert torch.equal(nh, grid.detach().permute(0, 2, 3, 1))
+    w = torch.randn(nh.shape, generator=g).cuda()
+    (nh * w).sum().backward()
+    assert torch.equal(grid.grad, w.permute(0, 3, 1, 2))
+    N, d_in = 5000, 295
+    x = torch.randn(N, d_in, generator=g).cuda()
+    x_aug = torch.cat((x, torch.ones(N, 1, device="cuda")), 1).requires_grad_(True)
+    ps = [(torch.randn(s, generator=g) * 0.1).cuda().requires_grad_(True)
+          for s in ((128, d_in), (128,), (65, 128), (65,))]
+    qs = [p.detach().clone().requires_grad_(True) for p in ps]
+    xr = x.clone().requires_grad_(True)
+    out = FieldMLP.apply(x_aug, *ps)
+    ref = torch.nn.functional.linear(torch.relu(torch.nn.functional.linear(xr, qs[0], qs[1])),
+                                     qs[2], qs[3])
+    assert rel_l2(out.detach(), ref.detach()) < 1e-5
+    go = torch.randn(out.shape, generator=g).cuda()
+    (out * go).sum().backward()
+    (ref * go).sum().backward()
+    for p, q in zip(ps, qs):
+        assert rel_l2(p.grad, q.grad) < 1e-5
+    assert rel_l2(x_aug.grad[:, :d_in], xr.grad) < 1e-5
 
 
 @pytest.mark.gpu
