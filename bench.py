@@ -495,7 +495,10 @@ def main_train(args, world, rank, device):
         ray_poses[:, 0, 2, 0] = -math.sin(a); ray_poses[:, 0, 2, 2] = math.cos(a)
         ray_poses[:, 0, 0, 3] = 0.5
     all_rays, _ = ImageRaySampler(3, 80, H, W).sample(None, ray_poses, Ks)  # (NB, H*W, 11)
-    opt = torch.optim.Adam(list(head.parameters()) + [leaf], lr=1e-4)
+    # the grid is an activation (the encoder's output): its gradient is computed, the
+    # optimizer steps the head (a frozen-encoder config; encoder backward is not ours)
+    opt = torch.optim.Adam(head.parameters(), lr=1e-4)
+    amp = not args.no_amp  # train_scenedino_kitti_360.yaml: with_amp: true (fp16 autocast)
     target_dino = torch.randn(NB, RB, D_DINO, device=device, generator=g)
     target_rgb = torch.rand(NB, RB, 3, device=device, generator=g)
     npatch = RB // (PS * PS)
@@ -508,10 +511,12 @@ def main_train(args, world, rank, device):
         px = torch.randint(0, W - PS + 1, (NB, npatch, 1, 1), device=device, generator=g)
         idx = ((py + oy) * W + (px + ox)).reshape(NB, RB)
         rays = torch.gather(all_rays, 1, idx.unsqueeze(-1).expand(NB, RB, all_rays.shape[-1]))
-        out = wrapper(rays, want_weights=True)["coarse"]
-        loss = ((out["dino_features"] - target_dino) ** 2).mean() + \
-            (out["rgb"] - target_rgb).abs().mean()
+        with torch.autocast("cuda", dtype=torch.float16, enabled=amp):
+            out = wrapper(rays, want_weights=True)["coarse"]
+            loss = ((out["dino_features"].float() - target_dino) ** 2).mean() + \
+                (out["rgb"].float() - target_rgb).abs().mean()
         opt.zero_grad(set_to_none=True)
+        leaf.grad = None
         loss.backward()
         opt.step()
         return loss
@@ -538,10 +543,12 @@ def main_train(args, world, rank, device):
         "metric": "training rays/sec (render forward + backward into grid and ResnetFC)",
         "value": world * NB * RB * args.steps / elapsed, "unit": "rays/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "fp16 autocast MLP, fp32 gather / compositing" if amp else "fp32",
         "data": "synthetic (N(0,1) 4x256x192x640 grid, U[-1,1) images, random targets)",
         "config": {"workload": "train: 4 frames x 2048 rays (8x8 patches) x 32 samples, "
-                               "hard_alpha_cap, ResnetFC 295-128-65, Adam step" +
+                               "hard_alpha_cap, ResnetFC 295-128-65, Adam step on the head, "
+                               "grid gradient computed" +
                                (", rays from an offset view" if args.offset_pose else
                                 ", rays from the encoder view"),
                    "points_per_step": n_pts, "parallelism": f"frames{world}"},
@@ -573,6 +580,8 @@ def main():
                          "encoder forward (a19); encode: ViT + DPT decoder (DINOv2Module); "
                          "train: render forward + backward (training step)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--no-amp", action="store_true",
+                    help="--config train: fp32 MLP instead of the reference's fp16 autocast")
     ap.add_argument("--no-end-to-end", action="store_true",
                     help="c2: skip the encode + render frame timing reported beside value")
     ap.add_argument("--models", default="", help="--config encode/vit: comma list of "

@@ -97,6 +97,18 @@ class FieldGather(torch.autograd.Function):
         return out, None, None, None, None, None, None
 
 
+def _wgrad(a, b):
+    """a^T b for tall a (N, m), b (N, n) with small m, n (weight gradients over N = 65 536
+    points): as a batched GEMM over S slices of N + a sum, so the chip gets S times the
+    workgroups of a single (m x n) output (a plain GEMM launches ~15 tiles here)."""
+    N = a.shape[0]
+    S = next((s for s in (32, 16, 8, 4, 2) if N % s == 0 and N // s >= 256), 1)
+    if S == 1:
+        return (a.t() @ b).float()
+    part = torch.bmm(a.view(S, N // S, -1).transpose(1, 2), b.view(S, N // S, -1))
+    return part.float().sum(0)
+
+
 class FieldMLP(torch.autograd.Function):
     """ResnetFC with n_blocks = 0 (resnetfc.py:135-203): out = W_o relu(W_i x + b_i) + b_o
     on the gather rows x_aug = [x | 1] (N, d_in + 1).  The biases ride in the GEMMs:
@@ -110,25 +122,33 @@ class FieldMLP(torch.autograd.Function):
         dh, d_in = w_in.shape
         if x_aug.shape[1] != d_in + 1:
             raise ValueError(f"FieldMLP: x_aug has {x_aug.shape[1]} columns, expected {d_in + 1}")
-        W2 = torch.zeros(dh + 1, d_in + 1, device=w_in.device, dtype=w_in.dtype)
+        # torch.autocast (the reference trains with_amp: nn.Linear in fp16): the GEMMs run
+        # in the autocast dtype, parameter gradients come back in the parameters' dtype
+        dt = (torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda")
+              else w_in.dtype)
+        W2 = torch.zeros(dh + 1, d_in + 1, device=w_in.device, dtype=dt)
         W2[:dh, :d_in] = w_in
         W2[:dh, d_in] = b_in
         W2[dh, d_in] = 1.0
-        Wo = torch.cat((w_out, b_out[:, None]), 1)
-        h = torch.relu(x_aug @ W2.t())
-        out = h @ Wo.t()
-        ctx.save_for_backward(x_aug, h, W2, Wo)
+        Wo = torch.cat((w_out, b_out[:, None]), 1).to(dt)
+        xa = x_aug.to(dt)
+        with torch.autocast("cuda", enabled=False):
+            h = torch.relu(xa @ W2.t())
+            out = h @ Wo.t()
+        ctx.save_for_backward(xa, h, W2, Wo)
+        ctx.dtypes = (x_aug.dtype, w_in.dtype)
         return out
 
     @staticmethod
     def backward(ctx, g):
         x_aug, h, W2, Wo = ctx.saved_tensors
-        g = g.contiguous()
+        xdt, pdt = ctx.dtypes
+        g = g.to(h.dtype).contiguous()
         dh_, d_in = W2.shape[0] - 1, W2.shape[1] - 1
-        dWo = g.t() @ h
+        dWo = _wgrad(g, h).to(pdt)
         dh = (g @ Wo) * (h > 0)
-        dW2 = dh.t() @ x_aug
-        dx = dh @ W2 if ctx.needs_input_grad[0] else None
+        dW2 = _wgrad(dh, x_aug).to(pdt)
+        dx = (dh @ W2).to(xdt) if ctx.needs_input_grad[0] else None
         return (dx, dW2[:dh_, :d_in].contiguous(), dW2[:dh_, d_in].contiguous(),
                 dWo[:, :dh_].contiguous(), dWo[:, dh_].contiguous())
 

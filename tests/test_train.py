@@ -224,3 +224,29 @@ def test_train_mode_render_gradients_gpu(hard):
     for p, q, name in zip((head.lin_in.weight, head.lin_in.bias, head.lin_out.weight,
                            head.lin_out.bias), ps, ("W_in", "b_in", "W_out", "b_out")):
         assert rel_l2(p.grad, q.grad) < 1e-3, name
+
+
+@pytest.mark.gpu
+def test_field_mlp_autocast_gpu():
+    """Under torch.autocast (the reference's with_amp) FieldMLP runs fp16 GEMMs like the
+    reference's nn.Linear under autocast; parameter gradients stay fp32."""
+    from scenedino_amd.autograd import FieldMLP
+    g = torch.Generator().manual_seed(11)
+    N, d_in = 4096, 295
+    x = torch.randn(N, d_in, generator=g).cuda()
+    x_aug = torch.cat((x, torch.ones(N, 1, device="cuda")), 1)
+    ps = [(torch.randn(s, generator=g) * 0.1).cuda().requires_grad_(True)
+          for s in ((128, d_in), (128,), (65, 128), (65,))]
+    qs = [p.detach().clone().requires_grad_(True) for p in ps]
+    with torch.autocast("cuda", dtype=torch.float16):
+        out = FieldMLP.apply(x_aug, *ps)
+        ref = torch.nn.functional.linear(
+            torch.relu(torch.nn.functional.linear(x, qs[0], qs[1])), qs[2], qs[3])
+    assert out.dtype == torch.float16 and ref.dtype == torch.float16
+    assert rel_l2(out.float(), ref.float()) < 1e-2
+    go = torch.randn(out.shape, generator=g).cuda()
+    (out.float() * go).sum().backward()
+    (ref.float() * go).sum().backward()
+    for p, q in zip(ps, qs):
+        assert p.grad.dtype == torch.float32
+        assert rel_l2(p.grad, q.grad) < 2e-2
