@@ -536,9 +536,19 @@ def main_train(args, world, rank, device):
     sda.kernel_timer = None
     ms = {k: timer.mean_ms(k) for k in ("gather", "gather_bwd", "composite_bwd")}
     n_pts = NB * RB * KT
-    # compulsory HBM bytes of the scatter: dX rows read (4 C B / point) + the grid gradient
-    # written once (4 C B / grid pixel); taps re-hit L2 (atomics execute in L2)
-    bwd_bytes = n_pts * 4 * C_GRID + NB * HF * WF * C_GRID * 4
+    chunk = n_pts  # points per k_field_gather_bwd launch (training path: one per pass)
+    # compulsory HBM bytes of one scatter launch: the C feature columns of the dX rows
+    # (4 C B per point) + the touched grid-gradient pixels written once (4 taps x 4 C B per
+    # texel quad; depends on the geometry) -- counted as the dX reads only, the floor
+    bwd_bytes = chunk * 4 * C_GRID
+    traffic, tsrc = None, None
+    tf = os.path.join(ROOT, "profiles", "r1_train_pmc.json")
+    if os.path.exists(tf):
+        try:
+            traffic = json.load(open(tf))["kernels"]["k_field_gather_bwd"]["hbm_bytes"]
+            tsrc = "profiles/r1_train_pmc.json (rocprofv3 PMC, per launch)"
+        except (KeyError, TypeError, ValueError):
+            traffic = None
     line = {
         "metric": "training rays/sec (render forward + backward into grid and ResnetFC)",
         "value": world * NB * RB * args.steps / elapsed, "unit": "rays/s", "n_gpus": world,
@@ -553,10 +563,11 @@ def main_train(args, world, rank, device):
                                 ", rays from the encoder view"),
                    "points_per_step": n_pts, "parallelism": f"frames{world}"},
         "roofline": {"kernel": "k_field_gather_bwd (sd_field_gather_bwd)", "bound": "hbm",
+                     "algorithmic_bytes_per_launch": bwd_bytes,
                      "achieved": bwd_bytes / (ms["gather_bwd"] * 1e-3) / 1e9, "peak": 8000.0,
                      "unit": "GB/s",
                      "frac": bwd_bytes / (ms["gather_bwd"] * 1e-3) / 1e9 / 8000.0,
-                     "traffic": None, "kernel_ms": ms["gather_bwd"],
+                     "traffic": traffic, "traffic_source": tsrc, "kernel_ms": ms["gather_bwd"],
                      "gather_ms": ms["gather"], "composite_bwd_ms": ms["composite_bwd"]},
     }
     if rank == 0:

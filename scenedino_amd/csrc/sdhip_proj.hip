@@ -183,21 +183,33 @@ k_project(const float *__restrict__ grid, int64_t B, int C, int64_t HW, int W, c
                 for (int i = 0; i < 4; ++i) acc[t][4 * q4 + i] = v[i];
             }
         }
-        float x[8];
+        // two K steps of grid loads in flight (x0: step q, x1: step q + 1): the kernel
+        // is HBM-bound and one step per wave does not cover the latency
+        float x0[8], x1[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) x[e] = gp[e * HW];
-        for (int q = 0; q < nq; ++q) {
+        for (int e = 0; e < 8; ++e) x0[e] = gp[e * HW];
+        if (nq > 1) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) x1[e] = gp[(int64_t)16 * HW + e * HW];
+        }
+        auto kstep = [&](int q, float (&x)[8]) {
             Frag f;
 #pragma unroll
             for (int e = 0; e < 8; ++e) f[e] = (typename Tr::E)x[e];
-            if (q + 1 < nq) {
-                const float *gn = gp + (int64_t)(16 * (q + 1)) * HW;
+            if (q + 2 < nq) {
+                const float *gn = gp + (int64_t)(16 * (q + 2)) * HW;
 #pragma unroll
                 for (int e = 0; e < 8; ++e) x[e] = gn[e * HW];
             }
 #pragma unroll
             for (int t = 0; t < 4; ++t) acc[t] = Tr::mma32(lw[(q * 4 + t) * SD_WAVE + lane], f, acc[t]);
+        };
+        int q = 0;
+        for (; q + 1 < nq; q += 2) {
+            kstep(q, x0);
+            kstep(q + 1, x1);
         }
+        if (q < nq) kstep(q, x0);
         // own values packed in hidden pairs; the right neighbour's from lane + 1
         const bool last_col = (pix % W) == W - 1;
         const int src = (lane + 1) << 2;

@@ -114,6 +114,8 @@ k_field_gather(const float *__restrict__ xyz, int64_t B, int64_t P,
 // ---------------------------------------------------------------------------
 #define TR_RUN 16
 
+// lane's channels c + 64 i (i < 4): every atomic instruction covers 64 consecutive floats
+// (atomics are not merged across lanes; 16-B-strided lanes would move 4x the sectors)
 __device__ __forceinline__ void tr_flush(float *g, const int idx[4], const f32x4 acc[4], int C,
                                          int c) {
 #pragma unroll
@@ -121,7 +123,7 @@ __device__ __forceinline__ void tr_flush(float *g, const int idx[4], const f32x4
         float *dst = g + (int64_t)idx[t] * C + c;
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-            if (acc[t][i] != 0.f) unsafeAtomicAdd(dst + i, acc[t][i]);
+            if (c + 64 * i < C && acc[t][i] != 0.f) unsafeAtomicAdd(dst + 64 * i, acc[t][i]);
     }
 }
 
@@ -136,32 +138,56 @@ k_field_gather_bwd(const float *__restrict__ xyz, int64_t B, int64_t P,
     for (int64_t run = (int64_t)blockIdx.x * TR_WAVES + (threadIdx.x >> 6); run < nruns;
          run += (int64_t)gridDim.x * TR_WAVES) {
         const int64_t p0 = run * TR_RUN;
-        const int64_t p1 = p0 + TR_RUN < NP ? p0 + TR_RUN : NP;
-        for (int c = lane * 4; c < C; c += 256) {
-            int idx[4] = {-1, -1, -1, -1};
-            int64_t bcur = -1;
+        const int n = (int)(p0 + TR_RUN < NP ? TR_RUN : NP - p0);
+        // geometry of the run's points, lane j < n = point p0 + j (broadcast below)
+        int gi[4] = {0, 0, 0, 0}, gb = 0;
+        float gw[4] = {0.f, 0.f, 0.f, 0.f};
+        if (lane < n) {
+            const int64_t p = p0 + lane;
+            const int64_t b = p / P;
+            const PointGeo geo = sd_point_geo(cam_f + b * 21, xyz[p * 3], xyz[p * 3 + 1],
+                                              xyz[p * 3 + 2], Wf, Hf);
+            gi[0] = geo.t.i00; gi[1] = geo.t.i01; gi[2] = geo.t.i10; gi[3] = geo.t.i11;
+            gw[0] = geo.t.w00; gw[1] = geo.t.w01; gw[2] = geo.t.w10; gw[3] = geo.t.w11;
+            gb = (int)b;
+        }
+        for (int c = lane; c < C; c += 256) {
+            // all rows of the run in flight at once (16 x 4 coalesced words per lane)
+            f32x4 v[TR_RUN];
+#pragma unroll
+            for (int j = 0; j < TR_RUN; ++j)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    v[j][i] = (j < n && c + 64 * i < C) ? dx[(p0 + j) * ldx + c + 64 * i] : 0.f;
+            int idx[4] = {-1, -1, -1, -1}, bcur = -1;
             f32x4 acc[4] = {};
-            for (int64_t p = p0; p < p1; ++p) {
-                const int64_t b = p / P;
-                const PointGeo geo = sd_point_geo(cam_f + b * 21, xyz[p * 3], xyz[p * 3 + 1],
-                                                  xyz[p * 3 + 2], Wf, Hf);
-                const int ni[4] = {geo.t.i00, geo.t.i01, geo.t.i10, geo.t.i11};
-                const float wt[4] = {geo.t.w00, geo.t.w01, geo.t.w10, geo.t.w11};
-                if (b != bcur || ni[0] != idx[0] || ni[1] != idx[1] || ni[2] != idx[2] ||
-                    ni[3] != idx[3]) {  // wave-uniform branch
-                    if (bcur >= 0) tr_flush(dgrid + bcur * plane, idx, acc, C, c);
-                    bcur = b;
+#pragma unroll
+            for (int j = 0; j < TR_RUN; ++j) {
+                if (j < n) {
+                    int ni[4];
+                    float wt[4];
 #pragma unroll
                     for (int t = 0; t < 4; ++t) {
-                        idx[t] = ni[t];
-                        acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+                        ni[t] = __builtin_amdgcn_readlane(gi[t], j);
+                        wt[t] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(
+                                                              __builtin_bit_cast(int, gw[t]), j));
                     }
+                    const int b = __builtin_amdgcn_readlane(gb, j);
+                    if (b != bcur || ni[0] != idx[0] || ni[1] != idx[1] || ni[2] != idx[2] ||
+                        ni[3] != idx[3]) {  // wave-uniform branch
+                        if (bcur >= 0) tr_flush(dgrid + bcur * plane, idx, acc, C, c);
+                        bcur = b;
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) {
+                            idx[t] = ni[t];
+                            acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+                        }
+                    }
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) acc[t][i] += v[j][i] * wt[t];
                 }
-                const f32x4 v = *(const f32x4 *)(dx + p * ldx + c);
-#pragma unroll
-                for (int t = 0; t < 4; ++t)
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) acc[t][i] += v[i] * wt[t];
             }
             if (bcur >= 0) tr_flush(dgrid + bcur * plane, idx, acc, C, c);
         }
@@ -326,10 +352,6 @@ extern "C" int sd_field_gather_bwd(const float *xyz, int64_t B, int64_t P, const
         return -1;
     }
     if (P == 0) return 0;
-    if (ldx % 4) {
-        sd_set_error("sd_field_gather_bwd: ldx must be a multiple of 4 (16-B row loads)");
-        return -1;
-    }
     hipLaunchKernelGGL(k_field_gather_bwd, dim3(tr_blocks((B * P + TR_RUN - 1) / TR_RUN)), dim3(TR_WAVES * 64), 0,
                        (hipStream_t)stream, xyz, B, P, dx, ldx, C, Hf, Wf, cam_f, dgrid_nhwc);
     if (hipGetLastError() != hipSuccess) {

@@ -283,6 +283,12 @@ class BTSNet(nn.Module):
         g = self.grid_f_features[self._scale] if self.grid_f_features else None
         return self.training or (g is not None and g.requires_grad)
 
+    def wants_single_chunk(self) -> bool:
+        """Renderer hook: the training path takes all of a pass's points in one call (the
+        eval_batch_size chunking of nerf.py:268-326 only bounds memory; the results are the
+        same, and per-chunk launch + autograd overhead dominates a 262 144-point step)."""
+        return self._differentiable()
+
     def begin_pass(self):
         """Renderer hook: the chunked model calls of one compositing pass follow."""
         self._in_pass, self._pass_nhwc = True, None

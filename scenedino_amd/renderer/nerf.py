@@ -180,6 +180,8 @@ class NeRFRenderer(torch.nn.Module):
             dim, bs = 1, (self.eval_batch_size - 1) // sb + 1
         else:
             dim, bs = 0, self.eval_batch_size
+        if getattr(model, "wants_single_chunk", None) is not None and model.wants_single_chunk():
+            bs = points.shape[dim]  # the model's training path: one launch per kernel per pass
         chunks = torch.split(points, bs, dim=dim)
         infos = torch.split(ray_info, bs, dim=dim) if ray_info is not None else [None] * len(chunks)
         rgbs_all, inv_all, sig_all, sds = [], [], [], []

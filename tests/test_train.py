@@ -104,7 +104,7 @@ def _gather_case(seed, B=2, P=3000, C=256, Hf=12, Wf=40):
     xyz[..., 0] = (torch.rand(B, P, generator=g) * 2.6 - 1.3) * xyz[..., 2].abs().clamp_min(1) / 0.78
     xyz[..., 1] = (torch.rand(B, P, generator=g) * 2.6 - 1.3) * xyz[..., 2].abs().clamp_min(1) / 2.9
     w2c = torch.eye(4).expand(B, 4, 4).clone()
-    w2c[1, 0, 3] = 0.4
+    w2c[B - 1, 0, 3] = 0.4
     Ks = KN.expand(B, 3, 3).clone()
     return grid, xyz, w2c, Ks
 
@@ -250,3 +250,27 @@ def test_field_mlp_autocast_gpu():
     for p, q in zip(ps, qs):
         assert p.grad.dtype == torch.float32
         assert rel_l2(p.grad, q.grad) < 2e-2
+
+
+@pytest.mark.gpu
+def test_gather_shared_accumulator_gpu():
+    """Chunks of one pass share one grid-gradient buffer (GatherAcc): the gradient equals
+    the single-call gradient, and a second backward through a retained graph repeats it."""
+    from scenedino_amd import _lib
+    from scenedino_amd.autograd import FieldGather, GatherAcc, GridNHWC
+    grid, xyz, w2c, Ks = _gather_case(6, B=2, P=4000)
+    cam_f = _lib.cam_records(w2c.cuda(), Ks.cuda())
+    gx = torch.randn(2, 4000, grid.shape[1] + 40, generator=torch.Generator().manual_seed(8)).cuda()
+    g1 = grid.cuda().requires_grad_(True)
+    x, *_ = FieldGather.apply(GridNHWC.apply(g1), xyz.cuda(), cam_f, None, None, False)
+    (x * gx).sum().backward()
+    g2 = grid.cuda().requires_grad_(True)
+    nh, acc = GridNHWC.apply(g2), GatherAcc()
+    parts = [FieldGather.apply(nh, xyz[:, s].cuda().contiguous(), cam_f, None, None, False, acc)[0]
+             for s in (slice(0, 1500), slice(1500, 2600), slice(2600, 4000))]
+    loss = (torch.cat(parts, 1) * gx).sum()
+    loss.backward(retain_graph=True)
+    assert rel_l2(g2.grad, g1.grad) < 1e-6
+    g2.grad = None
+    loss.backward()
+    assert rel_l2(g2.grad, g1.grad) < 1e-6
