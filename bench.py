@@ -462,6 +462,7 @@ def main_train(args, world, rank, device):
     sd_field_gather_bwd into the 4 x 256 x 192 x 640 grid gradient).  The encoder backward is
     not part of the step (the grid is the leaf)."""
     from scenedino_amd import autograd as sda
+    from scenedino_amd import distributed as sdd
     from scenedino_amd.models import BTSNet
     from scenedino_amd.models.prediction_heads import ResnetFC
     from scenedino_amd.common.positional_encoding import PositionalEncoding
@@ -518,6 +519,8 @@ def main_train(args, world, rank, device):
         opt.zero_grad(set_to_none=True)
         leaf.grad = None
         loss.backward()
+        if world > 1:  # data-parallel head: one RCCL all-reduce of the gradient bucket
+            sdd.allreduce_grads(head.parameters())
         opt.step()
         return loss
 
@@ -526,15 +529,26 @@ def main_train(args, world, rank, device):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
     timer.on = True
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     timer.on = False
     sda.kernel_timer = None
     ms = {k: timer.mean_ms(k) for k in ("gather", "gather_bwd", "composite_bwd")}
+    if world > 1:
+        t = torch.tensor([elapsed] + [ms[k] for k in ms], device=device, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t[0])
+        ms = {k: float(v) for k, v in zip(ms, t[1:])}
     n_pts = NB * RB * KT
     chunk = n_pts  # points per k_field_gather_bwd launch (training path: one per pass)
     # compulsory HBM bytes of one scatter launch: the C feature columns of the dX rows
@@ -561,7 +575,8 @@ def main_train(args, world, rank, device):
                                "grid gradient computed" +
                                (", rays from an offset view" if args.offset_pose else
                                 ", rays from the encoder view"),
-                   "points_per_step": n_pts, "parallelism": f"frames{world}"},
+                   "points_per_step": n_pts,
+                   "parallelism": f"dp{world} (4 frames per GPU, head gradients all-reduced)"},
         "roofline": {"kernel": "k_field_gather_bwd (sd_field_gather_bwd)", "bound": "hbm",
                      "algorithmic_bytes_per_launch": bwd_bytes,
                      "achieved": bwd_bytes / (ms["gather_bwd"] * 1e-3) / 1e9, "peak": 8000.0,

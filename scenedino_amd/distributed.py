@@ -53,3 +53,24 @@ def gather_maps(maps: torch.Tensor, group=None, out: list | None = None) -> list
     bufs = out if out is not None else [torch.empty_like(maps) for _ in range(world)]
     dist.all_gather(bufs, maps, group=group)
     return bufs
+
+
+def allreduce_grads(params, group=None) -> None:
+    """Data-parallel training of the field head (frames sharded over ranks, the training
+    path of scenedino_amd/autograd.py on each): average the parameter gradients with ONE
+    all-reduce of a flat bucket (the ResnetFC's 46 k parameters are far below a ring's
+    per-link latency floor, so one collective beats one per tensor).  Replaces what
+    DistributedDataParallel does for the reference's trainer (base_trainer.py)."""
+    import torch.distributed as dist
+    ps = [p for p in params if p.grad is not None]
+    if not ps:
+        return
+    world = dist.get_world_size(group)
+    flat = torch.cat([p.grad.reshape(-1) for p in ps])
+    dist.all_reduce(flat, group=group)
+    flat /= world
+    o = 0
+    for p in ps:
+        n = p.grad.numel()
+        p.grad.copy_(flat[o:o + n].view_as(p.grad))
+        o += n

@@ -82,3 +82,42 @@ def test_gather_maps_gloo_world2():
         assert p.exitcode == 0
     res = dict(q.get(timeout=10) for _ in range(world))
     assert res == {0: True, 1: True}
+
+
+def _grad_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lin = torch.nn.Linear(5, 3)
+        g = torch.Generator().manual_seed(rank)
+        lin.weight.grad = torch.randn(3, 5, generator=g)
+        lin.bias.grad = torch.randn(3, generator=g)
+        sdd.allreduce_grads(lin.parameters())
+        ws, bs = [], []
+        for r in range(world):
+            g2 = torch.Generator().manual_seed(r)
+            ws.append(torch.randn(3, 5, generator=g2))
+            bs.append(torch.randn(3, generator=g2))
+        ok = torch.allclose(lin.weight.grad, sum(ws) / world, atol=1e-6) and \
+            torch.allclose(lin.bias.grad, sum(bs) / world, atol=1e-6)
+        dist.barrier()
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_allreduce_grads_gloo_world2():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_grad_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    res = dict(q.get(timeout=10) for _ in range(world))
+    assert res == {0: True, 1: True}
