@@ -85,6 +85,48 @@ __global__ void __launch_bounds__(256) k_pack_grid(const float *__restrict__ in,
     }
 }
 
+// Vector variant (C % 4 == 0, W % 4 == 0): 64 channels x 64 pixels per block, 16-byte
+// global loads along x and 16-byte (f32) / 8-byte (16-bit) stores along c, through a
+// 64 x 65 LDS tile; grid (W/64, C/64, B*H).
+template <int DT>
+__global__ void __launch_bounds__(256) k_pack_grid4(const float *__restrict__ in, int64_t C,
+                                                    int64_t H, int64_t W, void *__restrict__ out) {
+    __shared__ float tile[64][65];
+    const int64_t bh = blockIdx.z;
+    const int64_t b = bh / H, y = bh - b * H;
+    const int64_t x0 = (int64_t)blockIdx.x * 64, c0 = (int64_t)blockIdx.y * 64;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int i = threadIdx.x + 256 * k, ch = i >> 4, px = (i & 15) * 4;
+        const int64_t c = c0 + ch, x = x0 + px;
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (c < C && x < W) v = *(const f32x4 *)(in + ((b * C + c) * H + y) * W + x);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) tile[ch][px + j] = v[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int i = threadIdx.x + 256 * k, px = i >> 4, ch = (i & 15) * 4;
+        const int64_t x = x0 + px, c = c0 + ch;
+        if (x < W && c < C) {
+            const int64_t o = ((b * H + y) * W + x) * C + c;
+            const float v0 = tile[ch][px], v1 = tile[ch + 1][px], v2 = tile[ch + 2][px],
+                        v3 = tile[ch + 3][px];
+            if (DT == SD_BF16) {
+                typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+                *(bf16x4 *)((__bf16 *)out + o) = bf16x4{(__bf16)v0, (__bf16)v1, (__bf16)v2, (__bf16)v3};
+            } else if (DT == SD_F16) {
+                typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
+                *(f16x4 *)((_Float16 *)out + o) =
+                    f16x4{(_Float16)v0, (_Float16)v1, (_Float16)v2, (_Float16)v3};
+            } else {
+                *(f32x4 *)((float *)out + o) = f32x4{v0, v1, v2, v3};
+            }
+        }
+    }
+}
+
 __global__ void __launch_bounds__(256) k_pack_image(const float *__restrict__ in, int64_t N,
                                                     int64_t H, int64_t W,
                                                     float *__restrict__ out) {
@@ -162,6 +204,21 @@ extern "C" int sd_pack_grid(const float *grid_nchw, int64_t B, int64_t C, int64_
         (dtype != SD_F32 && dtype != SD_BF16 && dtype != SD_F16) || B * H > 2147483647LL) {
         sd_set_error("sd_pack_grid: invalid argument");
         return -1;
+    }
+    if (C % 4 == 0 && W % 4 == 0 && ((uintptr_t)grid_nchw & 15) == 0 &&
+        ((uintptr_t)out_nhwc & 15) == 0) {
+        dim3 g4((unsigned)((W + 63) / 64), (unsigned)((C + 63) / 64), (unsigned)(B * H));
+        if (dtype == SD_BF16)
+            hipLaunchKernelGGL(k_pack_grid4<SD_BF16>, g4, dim3(256), 0, (hipStream_t)stream,
+                               grid_nchw, C, H, W, out_nhwc);
+        else if (dtype == SD_F16)
+            hipLaunchKernelGGL(k_pack_grid4<SD_F16>, g4, dim3(256), 0, (hipStream_t)stream,
+                               grid_nchw, C, H, W, out_nhwc);
+        else
+            hipLaunchKernelGGL(k_pack_grid4<SD_F32>, g4, dim3(256), 0, (hipStream_t)stream,
+                               grid_nchw, C, H, W, out_nhwc);
+        SD_CHECK_LAUNCH("sd_pack_grid");
+        return 0;
     }
     dim3 g((unsigned)((W + 31) / 32), (unsigned)((C + 31) / 32), (unsigned)(B * H));
     if (dtype == SD_BF16)

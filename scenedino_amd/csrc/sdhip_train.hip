@@ -312,6 +312,35 @@ __global__ void __launch_bounds__(256) k_unpack_grid(const float *__restrict__ i
     }
 }
 
+// vector variant (C % 4 == 0, W % 4 == 0): 64 x 64 tile, 16-byte loads along c and
+// stores along x; grid (W/64, C/64, B*H)
+__global__ void __launch_bounds__(256) k_unpack_grid4(const float *__restrict__ in, int64_t C,
+                                                      int64_t H, int64_t W,
+                                                      float *__restrict__ out) {
+    __shared__ float tile[64][65];
+    const int64_t bh = blockIdx.z;
+    const int64_t b = bh / H, y = bh - b * H;
+    const int64_t x0 = (int64_t)blockIdx.x * 64, c0 = (int64_t)blockIdx.y * 64;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int i = threadIdx.x + 256 * k, px = i >> 4, ch = (i & 15) * 4;
+        const int64_t x = x0 + px, c = c0 + ch;
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (x < W && c < C) v = *(const f32x4 *)(in + ((b * H + y) * W + x) * C + c);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) tile[ch + j][px] = v[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int i = threadIdx.x + 256 * k, ch = i >> 4, px = (i & 15) * 4;
+        const int64_t c = c0 + ch, x = x0 + px;
+        if (c < C && x < W)
+            *(f32x4 *)(out + ((b * C + c) * H + y) * W + x) =
+                f32x4{tile[ch][px], tile[ch][px + 1], tile[ch][px + 2], tile[ch][px + 3]};
+    }
+}
+
 // ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
@@ -393,6 +422,17 @@ extern "C" int sd_unpack_grid(const float *grid_nhwc, int64_t B, int64_t C, int6
         return -1;
     }
     if (B == 0) return 0;
+    if (C % 4 == 0 && W % 4 == 0 && ((uintptr_t)grid_nhwc & 15) == 0 &&
+        ((uintptr_t)grid_nchw & 15) == 0) {
+        dim3 g4((unsigned)((W + 63) / 64), (unsigned)((C + 63) / 64), (unsigned)(B * H));
+        hipLaunchKernelGGL(k_unpack_grid4, g4, dim3(256), 0, (hipStream_t)stream, grid_nhwc, C, H,
+                           W, grid_nchw);
+        if (hipGetLastError() != hipSuccess) {
+            sd_set_error("sd_unpack_grid: launch failed");
+            return -2;
+        }
+        return 0;
+    }
     dim3 g((unsigned)((W + 31) / 32), (unsigned)((C + 31) / 32), (unsigned)(B * H));
     hipLaunchKernelGGL(k_unpack_grid, g, dim3(256), 0, (hipStream_t)stream, grid_nhwc, C, H, W,
                        grid_nchw);

@@ -274,3 +274,17 @@ def test_gather_shared_accumulator_gpu():
     g2.grad = None
     loss.backward()
     assert rel_l2(g2.grad, g1.grad) < 1e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(2, 64, 7, 45), (1, 256, 12, 40), (2, 100, 5, 132)])
+def test_pack_unpack_grid_gpu(shape):
+    """sd_pack_grid (f32 / bf16 / f16) and sd_unpack_grid equal torch's permutes exactly,
+    for the vector (C, W % 4 == 0, 64x64 tiles with ragged edges) and scalar kernels."""
+    from scenedino_amd import _lib
+    g = torch.randn(*shape, generator=torch.Generator().manual_seed(12)).cuda()
+    ref = g.permute(0, 2, 3, 1)
+    for dt, tdt in ((_lib.SD_F32, torch.float32), (_lib.SD_BF16, torch.bfloat16),
+                    (_lib.SD_F16, torch.float16)):
+        assert torch.equal(_lib.pack_grid(g, dt), ref.to(tdt))
+    assert torch.equal(_lib.unpack_grid(ref.contiguous()), g)
