@@ -824,7 +824,10 @@ static void vt_pick_gemm(const sd_gemm_args &g, hipStream_t s) {
     // prefetch); 128x128 tiles once they fill the chip, else 64x64
     const int64_t big = ((g.M + 127) / 128) * ((g.N + 127) / 128);
     const int64_t mid = ((g.M + 63) / 64) * ((g.N + 63) / 64);
-    if (!CONV && mid < 256 && g.K % 128 == 0 && g.K >= 256) {
+    // conv: a 128-deep K step must stay inside one 3x3 tap (Cin % 128 == 0); the DPT's
+    // low-resolution 256-channel convolutions (12x40, 24x80) are exactly these small-M,
+    // large-K GEMMs
+    if ((!CONV || g.Cin % 128 == 0) && mid < 256 && g.K % 128 == 0 && g.K >= 256) {
         vt_launch_gemm<32, 32, 128, CONV>(g, s);  // split-K over the 4 waves
         return;
     }
