@@ -818,6 +818,10 @@ static void vt_launch_gemm(const sd_gemm_args &g, hipStream_t s) {
     }
 }
 
+#ifndef SD_CONV_SK_MID
+#define SD_CONV_SK_MID 256  // conv: split-K tiles below this many 64x64 tiles (1024: no gain)
+#endif
+
 template <bool CONV>
 static void vt_pick_gemm(const sd_gemm_args &g, hipStream_t s) {
     // K steps of 64 whenever K allows (half the barriers, twice the work under each
@@ -827,7 +831,8 @@ static void vt_pick_gemm(const sd_gemm_args &g, hipStream_t s) {
     // conv: a 128-deep K step must stay inside one 3x3 tap (Cin % 128 == 0); the DPT's
     // low-resolution 256-channel convolutions (12x40, 24x80) are exactly these small-M,
     // large-K GEMMs
-    if ((!CONV || g.Cin % 128 == 0) && mid < 256 && g.K % 128 == 0 && g.K >= 256) {
+    if ((CONV ? g.Cin % 128 == 0 && mid < SD_CONV_SK_MID : mid < 256) && g.K % 128 == 0 &&
+        g.K >= 256) {
         vt_launch_gemm<32, 32, 128, CONV>(g, s);  // split-K over the 4 waves
         return;
     }
