@@ -43,8 +43,12 @@ __device__ __forceinline__ void sd_wave_lds_sync() {
 }
 
 // ---------------------------------------------------------------------------
-// forward gather: one wave per point, lane = 4 channels (f32x4) of the NHWC grid
+// forward gather: one wave per run of TR_FRUN consecutive points; lane j < n computes
+// point j's geometry (broadcast with readlane), then every lane gathers 4 channels
+// (f32x4 of the NHWC grid) of all the run's points with their tap loads issued together
 // ---------------------------------------------------------------------------
+#define TR_FRUN 4
+
 __global__ void __launch_bounds__(TR_WAVES * 64)
 k_field_gather(const float *__restrict__ xyz, int64_t B, int64_t P,
                const float *__restrict__ grid, int C, int Hf, int Wf,
@@ -57,41 +61,83 @@ k_field_gather(const float *__restrict__ xyz, int64_t B, int64_t P,
     const int ld = C + 40;  // [feat (C) | code (39) | 1]: the 1 carries the bias through the GEMM
     const int64_t plane = (int64_t)Hf * Wf * C;
     const int64_t cplane = (int64_t)Hc * Wc * 4;
-    for (int64_t p = (int64_t)blockIdx.x * TR_WAVES + (threadIdx.x >> 6); p < NP;
-         p += (int64_t)gridDim.x * TR_WAVES) {
-        const int64_t b = p / P;
-        const float px = xyz[p * 3], py = xyz[p * 3 + 1], pz = xyz[p * 3 + 2];
-        const PointGeo geo = sd_point_geo(cam_f + b * 21, px, py, pz, Wf, Hf);
-        const float *g = grid + b * plane;
-        float *xr = x_out + p * ld;
+    const int64_t nruns = (NP + TR_FRUN - 1) / TR_FRUN;
+    for (int64_t run = (int64_t)blockIdx.x * TR_WAVES + (threadIdx.x >> 6); run < nruns;
+         run += (int64_t)gridDim.x * TR_WAVES) {
+        const int64_t p0 = run * TR_FRUN;
+        const int n = (int)(p0 + TR_FRUN < NP ? TR_FRUN : NP - p0);
+        int gi[4] = {0, 0, 0, 0}, gb = 0;
+        float gw[4] = {0.f, 0.f, 0.f, 0.f}, gv[3] = {0.f, 0.f, 0.f};
+        if (lane < n) {
+            const int64_t p = p0 + lane;
+            const int64_t b = p / P;
+            const PointGeo geo = sd_point_geo(cam_f + b * 21, xyz[p * 3], xyz[p * 3 + 1],
+                                              xyz[p * 3 + 2], Wf, Hf);
+            gi[0] = geo.t.i00; gi[1] = geo.t.i01; gi[2] = geo.t.i10; gi[3] = geo.t.i11;
+            gw[0] = geo.t.w00; gw[1] = geo.t.w01; gw[2] = geo.t.w10; gw[3] = geo.t.w11;
+            gv[0] = geo.v[0]; gv[1] = geo.v[1]; gv[2] = geo.v[2];
+            gb = (int)b;
+            if (invalid_f) invalid_f[p] = geo.inv_f ? 1 : 0;
+        }
         for (int c = lane * 4; c < C; c += 256) {
-            const f32x4 a = *(const f32x4 *)(g + (int64_t)geo.t.i00 * C + c);
-            const f32x4 bb = *(const f32x4 *)(g + (int64_t)geo.t.i01 * C + c);
-            const f32x4 cc = *(const f32x4 *)(g + (int64_t)geo.t.i10 * C + c);
-            const f32x4 d = *(const f32x4 *)(g + (int64_t)geo.t.i11 * C + c);
+            f32x4 t[TR_FRUN][4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i)  // grid_sampler_2d's nw, ne, sw, se order
-                xr[c + i] = ((a[i] * geo.t.w00 + bb[i] * geo.t.w01) + cc[i] * geo.t.w10) +
-                            d[i] * geo.t.w11;
+            for (int j = 0; j < TR_FRUN; ++j) {
+                const int jj = j < n ? j : 0;
+                const float *g = grid + (int64_t)__builtin_amdgcn_readlane(gb, jj) * plane + c;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    t[j][q] = *(const f32x4 *)(g + (int64_t)__builtin_amdgcn_readlane(gi[q], jj) * C);
+            }
+#pragma unroll
+            for (int j = 0; j < TR_FRUN; ++j) {
+                if (j < n) {
+                    float w[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        w[q] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(
+                                                             __builtin_bit_cast(int, gw[q]), j));
+                    f32x4 o;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)  // grid_sampler_2d's nw, ne, sw, se order
+                        o[i] = ((t[j][0][i] * w[0] + t[j][1][i] * w[1]) + t[j][2][i] * w[2]) +
+                               t[j][3][i] * w[3];
+                    *(f32x4 *)(x_out + (p0 + j) * ld + c) = o;
+                }
+            }
         }
         // positional code (positional_encoding.py:68-80): [x, y, z~, sin(f_j v + phi)]
-        // with rows (freq j, phase) and the 3 coordinates innermost
-        if (lane < 39) {
-            float r;
-            if (lane < 3) {
-                r = geo.v[lane];
-            } else {
-                const int s = lane - 3, fi = s / 6, cs = (s % 6) / 3, co = s % 3;
-                const float f = 1.5f * (float)(1 << fi);
-                r = sinf(fmaf(geo.v[co], f, cs ? 1.5707963705062866f : 0.f));
+        // with rows (freq j, phase) and the 3 coordinates innermost; then the bias 1
+#pragma unroll
+        for (int j = 0; j < TR_FRUN; ++j) {
+            if (j < n) {
+                float v[3];
+#pragma unroll
+                for (int e = 0; e < 3; ++e)
+                    v[e] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(
+                                                         __builtin_bit_cast(int, gv[e]), j));
+                float *xr = x_out + (p0 + j) * ld;
+                if (lane < 39) {
+                    float r;
+                    if (lane < 3) {
+                        r = v[lane];
+                    } else {
+                        const int s = lane - 3, fi = s / 6, cs = (s % 6) / 3, co = s % 3;
+                        const float f = 1.5f * (float)(1 << fi);
+                        r = sinf(fmaf(v[co], f, cs ? 1.5707963705062866f : 0.f));
+                    }
+                    xr[C + lane] = r;
+                } else if (lane == 39) {
+                    xr[C + 39] = 1.f;
+                }
             }
-            xr[C + lane] = r;
-        } else if (lane == 39) {
-            xr[C + 39] = 1.f;
         }
-        if (lane == 0 && invalid_f) invalid_f[p] = geo.inv_f ? 1 : 0;
-        if (lane < nv && (rgb || invalid)) {
-            const int v = lane;
+        // colour samples / masks: lane = (point, view)
+        if (nv > 0 && (rgb || invalid) && lane < n * nv) {
+            const int j = lane / nv, v = lane - j * nv;
+            const int64_t p = p0 + j;
+            const int64_t b = p / P;
+            const float px = xyz[p * 3], py = xyz[p * 3 + 1], pz = xyz[p * 3 + 2];
             float col[3];
             const bool ic = sd_color_view(cam_c + (b * nv + v) * 21, img + (b * nv + v) * cplane,
                                           Wc, Hc, px, py, pz, col);
@@ -100,7 +146,11 @@ k_field_gather(const float *__restrict__ xyz, int64_t B, int64_t P,
                 rgb[(p * nv + v) * 3 + 1] = col[1];
                 rgb[(p * nv + v) * 3 + 2] = col[2];
             }
-            if (invalid) invalid[p * nv + v] = (ic | geo.inv_f) ? 1.f : 0.f;
+            if (invalid) {
+                float x, y, zc;  // the encoder-frustum test of sd_point_geo, same arithmetic
+                sd_project(cam_f + b * 21, px, py, pz, x, y, zc);
+                invalid[p * nv + v] = (ic | sd_outside(x, y, zc)) ? 1.f : 0.f;
+            }
         }
     }
 }
@@ -362,7 +412,11 @@ extern "C" int sd_field_gather(const float *xyz, int64_t B, int64_t P, const flo
         return -1;
     }
     if (P == 0) return 0;
-    hipLaunchKernelGGL(k_field_gather, dim3(tr_blocks(B * P)), dim3(TR_WAVES * 64), 0,
+    if (nv > 64 / TR_FRUN) {
+        sd_set_error("sd_field_gather: at most 16 colour views");
+        return -1;
+    }
+    hipLaunchKernelGGL(k_field_gather, dim3(tr_blocks((B * P + TR_FRUN - 1) / TR_FRUN)), dim3(TR_WAVES * 64), 0,
                        (hipStream_t)stream, xyz, B, P, grid_nhwc, C, Hf, Wf, cam_f, img, nv, Hc,
                        Wc, cam_c, x_out, invalid_f, rgb, invalid);
     if (hipGetLastError() != hipSuccess) {

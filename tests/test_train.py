@@ -288,3 +288,29 @@ def test_pack_unpack_grid_gpu(shape):
                     (_lib.SD_F16, torch.float16)):
         assert torch.equal(_lib.pack_grid(g, dt), ref.to(tdt))
     assert torch.equal(_lib.unpack_grid(ref.contiguous()), g)
+
+
+@pytest.mark.gpu
+def test_field_gather_colours_gpu():
+    """sd_field_gather's colour samples and invalid masks (2 render views) equal the
+    oracle's field query (bts.py:330-441)."""
+    from scenedino_amd import _lib
+    grid, xyz, w2c, Ks = _gather_case(13, B=2, P=1001)
+    B, C = grid.shape[:2]
+    nv, Hc, Wc = 2, 24, 80
+    g = torch.Generator().manual_seed(14)
+    imgs = torch.rand(B, nv, 3, Hc, Wc, generator=g)
+    w2c_c = w2c.unsqueeze(1).repeat(1, nv, 1, 1)
+    w2c_c[:, 1, 0, 3] -= 0.3
+    K_c = Ks.unsqueeze(1).repeat(1, nv, 1, 1)
+    cam_f = _lib.cam_records(w2c.cuda(), Ks.cuda())
+    cam_c = _lib.cam_records(w2c_c.cuda(), K_c.cuda())
+    img = _lib.pack_image(imgs.reshape(B * nv, 3, Hc, Wc).cuda().contiguous())
+    gn = grid.permute(0, 2, 3, 1).contiguous().cuda()
+    x, invf, rgb, inv = _lib.field_gather(xyz.cuda(), gn, cam_f, img, cam_c, True)
+    W_in, b_in = torch.zeros(128, C + 39), torch.zeros(128)
+    W_out, b_out = torch.zeros(65, 128), torch.zeros(65)
+    ref = O.field_query(xyz, grid, w2c, Ks, imgs, w2c_c, K_c, W_in, b_in, W_out, b_out)
+    assert torch.equal(invf.cpu(), ref["invalid_features"])
+    assert torch.equal(inv.cpu().bool(), ref["invalid"])
+    np.testing.assert_allclose(rgb.cpu().numpy(), ref["rgb"].numpy(), rtol=1e-5, atol=1e-6)
