@@ -262,6 +262,31 @@ k_composite_bwd(const float *__restrict__ z, const float *__restrict__ sigma,
          ray += (int64_t)gridDim.x * TR_WAVES) {
         const float *zr = z + ray * K, *sr = sigma + ray * K;
         const float gd = g_depth ? g_depth[ray] : 0.f;
+        // phase 0 (F % 4 == 0): <dL/dfeat, f_k> with coalesced 16-B row reads, 4 samples per
+        // instruction (16 lanes per row), reduced over the row's lanes -> st[k]
+        const bool vec = feat && g_feat && (F % 4) == 0;
+        if (vec) {
+            const int rr = lane >> 4, c4 = (lane & 15) * 4;
+            const float *gf = g_feat + ray * F;
+#pragma unroll 4
+            for (int k0 = 0; k0 < K; k0 += 4) {
+                const int k = k0 + rr;
+                float s = 0.f;
+                if (k < K) {
+                    const float *fr = feat + (ray * K + k) * (int64_t)F;
+                    for (int c = c4; c < F; c += 64) {
+                        const f32x4 a = *(const f32x4 *)(fr + c), b = *(const f32x4 *)(gf + c);
+                        s += ((a[0] * b[0] + a[1] * b[1]) + a[2] * b[2]) + a[3] * b[3];
+                    }
+                }
+                s += __shfl_xor(s, 8);
+                s += __shfl_xor(s, 4);
+                s += __shfl_xor(s, 2);
+                s += __shfl_xor(s, 1);
+                if ((lane & 15) == 0 && k < K) st[k] = s;
+            }
+            sd_wave_lds_sync();
+        }
         // phase 1 (lane = sample): alpha and g_k = dL/dw_k
         for (int k = lane; k < K; k += 64) {
             const float zk = zr[k];
@@ -270,7 +295,9 @@ k_composite_bwd(const float *__restrict__ z, const float *__restrict__ sigma,
             if (hard_cap && k == K - 1) alpha = 1.f;
             float g = gd * zk;
             if (g_w) g += g_w[ray * K + k];
-            if (feat && g_feat) {
+            if (vec) {
+                g += st[k];
+            } else if (feat && g_feat) {
                 const float *fr = feat + (ray * K + k) * (int64_t)F;
                 const float *gf = g_feat + ray * F;
                 float s = 0.f;

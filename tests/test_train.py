@@ -60,9 +60,10 @@ def test_composite_bwd_oracle_vs_autograd(hard):
 @pytest.mark.gpu
 @pytest.mark.parametrize("hard", [False, True])
 @pytest.mark.parametrize("K", [64, 100])
-def test_composite_bwd_gpu(hard, K):
+@pytest.mark.parametrize("F", [64, 30, 384])
+def test_composite_bwd_gpu(hard, K, F):
     from scenedino_amd import _lib
-    R, F, Cc = 300, 64, 6
+    R, Cc = 300, 6
     z, sigma, feat, rgb, gr = _comp_inputs(R, K, F, Cc, 2 + K)
     ds, df, dc = _autograd_composite(z, sigma, feat, rgb, hard, gr)
     c = lambda t: t.float().cuda().contiguous()
