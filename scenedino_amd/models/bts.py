@@ -419,7 +419,10 @@ class BTSNet(nn.Module):
         key = (id(g), g._version)
         nh = self._pass_nhwc
         if nh is None or nh[0] != key:
-            nh = (key, GridNHWC.apply(g[:, 0]), GatherAcc())
+            # (B, 1, C, Hf, Wf) -> (B, C, Hf, Wf) as a view: its backward is a view too,
+            # where g[:, 0]'s select backward zero-fills and copies the whole grid gradient
+            g0 = g.flatten(0, 1) if g.shape[1] == 1 else g[:, 0]
+            nh = (key, GridNHWC.apply(g0), GatherAcc())
             if self._in_pass:
                 self._pass_nhwc = nh
         x, invf, rgb, inv = FieldGather.apply(nh[1], xyz.float().contiguous(), gc["cam_f"],
