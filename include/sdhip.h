@@ -198,19 +198,20 @@ int sd_composite(const float *z, const float *sigma, const float *feat, int64_t 
  * (bts.py:299-309, F.grid_sample align_corners=False) and the 39-d positional code
  * (positional_encoding.py:13-80), written as x_out (B*P, C+40) = [feat | code | 1]
  * (bts.py:321-328; the constant 1 column carries the ResnetFC biases through its GEMMs).  grid_nhwc (B, Hf, Wf, C) f32.  Colour samples / masks as
- * sd_field_query (bts.py:330-441; rgb, invalid, img, cam_c may be NULL / nv = 0). */
+ * sd_field_query (bts.py:330-441; rgb, invalid, img, cam_c may be NULL / nv = 0).
+ * x_out element type x_dtype: SD_F32, or SD_F16 / SD_BF16 (the MLP's autocast dtype). */
 int sd_field_gather(const float *xyz, int64_t B, int64_t P, const float *grid_nhwc,
                     int32_t C, int32_t Hf, int32_t Wf, const float *cam_f,
                     const float *img, int32_t nv, int32_t Hc, int32_t Wc,
-                    const float *cam_c, float *x_out, uint8_t *invalid_f, float *rgb,
-                    float *invalid, void *stream);
+                    const float *cam_c, void *x_out, int32_t x_dtype /* sd_dtype */,
+                    uint8_t *invalid_f, float *rgb, float *invalid, void *stream);
 
 /* Backward of the feature gather (grid_sample input gradient, bts.py:299-309):
  * dgrid_nhwc (B, Hf, Wf, C) += bilinear scatter of dx[:, :C] (row stride ldx).
  * Accumulates with f32 atomics: the caller zeroes dgrid_nhwc. */
-int sd_field_gather_bwd(const float *xyz, int64_t B, int64_t P, const float *dx,
-                        int64_t ldx, int32_t C, int32_t Hf, int32_t Wf,
-                        const float *cam_f, float *dgrid_nhwc, void *stream);
+int sd_field_gather_bwd(const float *xyz, int64_t B, int64_t P, const void *dx,
+                        int32_t dx_dtype /* sd_dtype */, int64_t ldx, int32_t C, int32_t Hf,
+                        int32_t Wf, const float *cam_f, float *dgrid_nhwc, void *stream);
 
 /* NHWC f32 (B, H, W, C) -> NCHW f32 (B, C, H, W): the grid gradient of the training path
  * back in the encoder's layout (inverse of sd_pack_grid with dtype SD_F32). */

@@ -20,6 +20,7 @@ SD_F32 = 0
 SD_BF16 = 1
 SD_F16 = 2
 TORCH_DTYPE = {SD_F32: torch.float32, SD_BF16: torch.bfloat16, SD_F16: torch.float16}
+SD_OF_TORCH = {v: k for k, v in TORCH_DTYPE.items()}
 
 _vp = ctypes.c_void_p
 _i64 = ctypes.c_int64
@@ -109,8 +110,8 @@ SIGNATURES = {
     "sd_render_fused": [ctypes.POINTER(SdRenderArgs), ctypes.POINTER(SdMlp), _vp],
     "sd_field_query": [ctypes.POINTER(SdFieldArgs), ctypes.POINTER(SdMlp), _vp],
     "sd_field_gather": [_vp, _i64, _i64, _vp, _i32, _i32, _i32, _vp, _vp, _i32, _i32, _i32, _vp,
-                        _vp, _vp, _vp, _vp, _vp],
-    "sd_field_gather_bwd": [_vp, _i64, _i64, _vp, _i64, _i32, _i32, _i32, _vp, _vp, _vp],
+                        _vp, _i32, _vp, _vp, _vp, _vp],
+    "sd_field_gather_bwd": [_vp, _i64, _i64, _vp, _i32, _i64, _i32, _i32, _i32, _vp, _vp, _vp],
     "sd_unpack_grid": [_vp, _i64, _i64, _i64, _i64, _vp, _vp],
     "sd_composite_bwd": [_vp, _vp, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp, _vp,
                          _vp, _vp, _vp, _vp, _vp],
@@ -337,14 +338,15 @@ def composite(z, sigma, feat, rgb, hard_alpha_cap, want_weights=True):
     return weights, alphas, depth, feat_out, rgb_out
 
 
-def field_gather(xyz, grid_nhwc, cam_f, img=None, cam_c=None, colors=True):
+def field_gather(xyz, grid_nhwc, cam_f, img=None, cam_c=None, colors=True,
+                 dtype=torch.float32):
     """sd_field_gather: xyz (B,P,3), grid_nhwc (B,Hf,Wf,C) f32 -> x (B,P,C+40) = [feat|code|1],
     invalid_f (B,P) bool, rgb (B,P,3nv) | None, invalid (B,P,nv) | None."""
     lib = load()
     B, P, _ = xyz.shape
     _, Hf, Wf, C = grid_nhwc.shape
     dev = xyz.device
-    x = torch.empty(B, P, C + 40, device=dev)
+    x = torch.empty(B, P, C + 40, device=dev, dtype=dtype)
     invf = torch.empty(B, P, device=dev, dtype=torch.bool)
     nv, Hc, Wc = 0, 0, 0
     if colors:  # img: pack_image output (B*nv, Hc, Wc, 4); cam_c (B, nv, 21)
@@ -353,7 +355,8 @@ def field_gather(xyz, grid_nhwc, cam_f, img=None, cam_c=None, colors=True):
     inv = torch.empty(B, P, nv, device=dev) if colors else None
     _check(lib.sd_field_gather(ptr(_req(xyz, "xyz")), B, P, ptr(_req(grid_nhwc, "grid")), C, Hf,
                                Wf, ptr(_req(cam_f, "cam_f")), ptr(img), nv, Hc, Wc, ptr(cam_c),
-                               ptr(x), ptr(invf), ptr(rgb), ptr(inv), stream_of(x)),
+                               ptr(x), SD_OF_TORCH[dtype], ptr(invf), ptr(rgb), ptr(inv),
+                               stream_of(x)),
            "sd_field_gather")
     return x, invf, rgb, inv
 
@@ -363,11 +366,14 @@ def field_gather_bwd(xyz, dx, cam_f, Hf, Wf, C, dgrid=None):
     into the given dgrid)."""
     lib = load()
     B, P, _ = xyz.shape
+    # f32 rows: the kernel's 4-byte lane loads keep its atomics lane-contiguous; 16-bit rows
+    # (sd_field_gather_bwd accepts them) measured slower than one conversion pass
     dx = dx.float().contiguous()
     if dgrid is None:
         dgrid = torch.zeros(B, Hf, Wf, C, device=xyz.device)
     _req(dgrid, "dgrid")
-    _check(lib.sd_field_gather_bwd(ptr(_req(xyz, "xyz")), B, P, ptr(dx), dx.shape[-1], C, Hf, Wf,
+    _check(lib.sd_field_gather_bwd(ptr(_req(xyz, "xyz")), B, P, ptr(dx), SD_OF_TORCH[dx.dtype],
+                                   dx.shape[-1], C, Hf, Wf,
                                    ptr(_req(cam_f, "cam_f")), ptr(dgrid), stream_of(dgrid)),
            "sd_field_gather_bwd")
     return dgrid

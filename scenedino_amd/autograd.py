@@ -67,8 +67,12 @@ class FieldGather(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, grid_nhwc, xyz, cam_f, img, cam_c, colors, acc=None):
+        # under torch.autocast the rows are written in the autocast dtype the MLP GEMMs
+        # consume (no separate cast pass over the (N, C + 40) matrix)
+        dt = (torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda")
+              else torch.float32)
         x, invf, rgb, inv = _timed("gather", lambda: _lib.field_gather(
-            xyz, grid_nhwc, cam_f, img, cam_c, colors))
+            xyz, grid_nhwc, cam_f, img, cam_c, colors, dtype=dt))
         ctx.save_for_backward(xyz, cam_f)
         ctx.grid_shape = tuple(grid_nhwc.shape)
         ctx.acc = acc if acc is not None else GatherAcc()
@@ -88,6 +92,7 @@ class FieldGather(torch.autograd.Function):
         if first:
             acc.left = acc.n
             acc.buf = torch.zeros(B, Hf, Wf, C, device=xyz.device)
+        gx = gx.float().contiguous()  # f32 rows for the scatter (see _lib.field_gather_bwd)
         _timed("gather_bwd", lambda: _lib.field_gather_bwd(xyz, gx, cam_f, Hf, Wf, C,
                                                            dgrid=acc.buf))
         acc.left -= 1
@@ -148,7 +153,7 @@ class FieldMLP(torch.autograd.Function):
         dWo = _wgrad(g, h).to(pdt)
         dh = (g @ Wo) * (h > 0)
         dW2 = _wgrad(dh, x_aug).to(pdt)
-        dx = (dh @ W2).to(xdt) if ctx.needs_input_grad[0] else None
+        dx = (dh @ W2).to(xdt) if ctx.needs_input_grad[0] else None  # xdt: the rows' dtype
         return (dx, dW2[:dh_, :d_in].contiguous(), dW2[:dh_, d_in].contiguous(),
                 dWo[:, :dh_].contiguous(), dWo[:, dh_].contiguous())
 

@@ -49,13 +49,31 @@ __device__ __forceinline__ void sd_wave_lds_sync() {
 // ---------------------------------------------------------------------------
 #define TR_FRUN 4
 
+// row element types of X / dX: f32, or the autocast dtype (f16 / bf16) of the MLP GEMMs
+template <int DT> struct TrE { typedef float T; };
+template <> struct TrE<SD_F16> { typedef _Float16 T; };
+template <> struct TrE<SD_BF16> { typedef __bf16 T; };
+
+template <int DT>
+__device__ __forceinline__ void tr_store4(typename TrE<DT>::T *dst, const f32x4 &o) {
+    if constexpr (DT == SD_F32) {
+        *(f32x4 *)dst = o;
+    } else {
+        typedef typename TrE<DT>::T E;
+        typedef __attribute__((ext_vector_type(4))) E e4;
+        *(e4 *)dst = e4{(E)o[0], (E)o[1], (E)o[2], (E)o[3]};
+    }
+}
+
+template <int DT>
 __global__ void __launch_bounds__(TR_WAVES * 64)
 k_field_gather(const float *__restrict__ xyz, int64_t B, int64_t P,
                const float *__restrict__ grid, int C, int Hf, int Wf,
                const float *__restrict__ cam_f, const float *__restrict__ img, int nv, int Hc,
-               int Wc, const float *__restrict__ cam_c, float *__restrict__ x_out,
+               int Wc, const float *__restrict__ cam_c, typename TrE<DT>::T *__restrict__ x_out,
                uint8_t *__restrict__ invalid_f, float *__restrict__ rgb,
                float *__restrict__ invalid) {
+    typedef typename TrE<DT>::T E;
     const int lane = threadIdx.x & 63;
     const int64_t NP = B * P;
     const int ld = C + 40;  // [feat (C) | code (39) | 1]: the 1 carries the bias through the GEMM
@@ -102,7 +120,7 @@ k_field_gather(const float *__restrict__ xyz, int64_t B, int64_t P,
                     for (int i = 0; i < 4; ++i)  // grid_sampler_2d's nw, ne, sw, se order
                         o[i] = ((t[j][0][i] * w[0] + t[j][1][i] * w[1]) + t[j][2][i] * w[2]) +
                                t[j][3][i] * w[3];
-                    *(f32x4 *)(x_out + (p0 + j) * ld + c) = o;
+                    tr_store4<DT>(x_out + (p0 + j) * ld + c, o);
                 }
             }
         }
@@ -116,7 +134,7 @@ k_field_gather(const float *__restrict__ xyz, int64_t B, int64_t P,
                 for (int e = 0; e < 3; ++e)
                     v[e] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(
                                                          __builtin_bit_cast(int, gv[e]), j));
-                float *xr = x_out + (p0 + j) * ld;
+                E *xr = x_out + (p0 + j) * ld;
                 if (lane < 39) {
                     float r;
                     if (lane < 3) {
@@ -126,9 +144,9 @@ k_field_gather(const float *__restrict__ xyz, int64_t B, int64_t P,
                         const float f = 1.5f * (float)(1 << fi);
                         r = sinf(fmaf(v[co], f, cs ? 1.5707963705062866f : 0.f));
                     }
-                    xr[C + lane] = r;
+                    xr[C + lane] = (E)r;
                 } else if (lane == 39) {
-                    xr[C + 39] = 1.f;
+                    xr[C + 39] = (E)1.f;
                 }
             }
         }
@@ -177,9 +195,10 @@ __device__ __forceinline__ void tr_flush(float *g, const int idx[4], const f32x4
     }
 }
 
+template <int DT>
 __global__ void __launch_bounds__(TR_WAVES * 64)
 k_field_gather_bwd(const float *__restrict__ xyz, int64_t B, int64_t P,
-                   const float *__restrict__ dx, int64_t ldx, int C, int Hf, int Wf,
+                   const typename TrE<DT>::T *__restrict__ dx, int64_t ldx, int C, int Hf, int Wf,
                    const float *__restrict__ cam_f, float *__restrict__ dgrid) {
     const int lane = threadIdx.x & 63;
     const int64_t NP = B * P;
@@ -208,7 +227,7 @@ k_field_gather_bwd(const float *__restrict__ xyz, int64_t B, int64_t P,
             for (int j = 0; j < TR_RUN; ++j)
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
-                    v[j][i] = (j < n && c + 64 * i < C) ? dx[(p0 + j) * ldx + c + 64 * i] : 0.f;
+                    v[j][i] = (j < n && c + 64 * i < C) ? (float)dx[(p0 + j) * ldx + c + 64 * i] : 0.f;
             int idx[4] = {-1, -1, -1, -1}, bcur = -1;
             f32x4 acc[4] = {};
 #pragma unroll
@@ -430,9 +449,10 @@ static int tr_blocks(int64_t units) {
 extern "C" int sd_field_gather(const float *xyz, int64_t B, int64_t P, const float *grid_nhwc,
                                int32_t C, int32_t Hf, int32_t Wf, const float *cam_f,
                                const float *img, int32_t nv, int32_t Hc, int32_t Wc,
-                               const float *cam_c, float *x_out, uint8_t *invalid_f, float *rgb,
-                               float *invalid, void *stream) {
+                               const float *cam_c, void *x_out, int32_t x_dtype,
+                               uint8_t *invalid_f, float *rgb, float *invalid, void *stream) {
     if (B <= 0 || P < 0 || !xyz || !grid_nhwc || !cam_f || !x_out || C <= 0 || (C % 4) ||
+        (x_dtype != SD_F32 && x_dtype != SD_F16 && x_dtype != SD_BF16) ||
         Hf <= 0 || Wf <= 0 || nv < 0 || nv > 64 ||
         (nv > 0 && (rgb || invalid) && (!img || !cam_c || Hc <= 0 || Wc <= 0))) {
         sd_set_error("sd_field_gather: invalid argument (C % 4 == 0, nv <= 64)");
@@ -443,9 +463,20 @@ extern "C" int sd_field_gather(const float *xyz, int64_t B, int64_t P, const flo
         sd_set_error("sd_field_gather: at most 16 colour views");
         return -1;
     }
-    hipLaunchKernelGGL(k_field_gather, dim3(tr_blocks((B * P + TR_FRUN - 1) / TR_FRUN)), dim3(TR_WAVES * 64), 0,
-                       (hipStream_t)stream, xyz, B, P, grid_nhwc, C, Hf, Wf, cam_f, img, nv, Hc,
-                       Wc, cam_c, x_out, invalid_f, rgb, invalid);
+    const dim3 grid(tr_blocks((B * P + TR_FRUN - 1) / TR_FRUN)), blk(TR_WAVES * 64);
+    hipStream_t s = (hipStream_t)stream;
+    if (x_dtype == SD_F16)
+        hipLaunchKernelGGL(k_field_gather<SD_F16>, grid, blk, 0, s, xyz, B, P, grid_nhwc, C, Hf,
+                           Wf, cam_f, img, nv, Hc, Wc, cam_c, (_Float16 *)x_out, invalid_f, rgb,
+                           invalid);
+    else if (x_dtype == SD_BF16)
+        hipLaunchKernelGGL(k_field_gather<SD_BF16>, grid, blk, 0, s, xyz, B, P, grid_nhwc, C, Hf,
+                           Wf, cam_f, img, nv, Hc, Wc, cam_c, (__bf16 *)x_out, invalid_f, rgb,
+                           invalid);
+    else
+        hipLaunchKernelGGL(k_field_gather<SD_F32>, grid, blk, 0, s, xyz, B, P, grid_nhwc, C, Hf,
+                           Wf, cam_f, img, nv, Hc, Wc, cam_c, (float *)x_out, invalid_f, rgb,
+                           invalid);
     if (hipGetLastError() != hipSuccess) {
         sd_set_error("sd_field_gather: launch failed");
         return -2;
@@ -453,17 +484,28 @@ extern "C" int sd_field_gather(const float *xyz, int64_t B, int64_t P, const flo
     return 0;
 }
 
-extern "C" int sd_field_gather_bwd(const float *xyz, int64_t B, int64_t P, const float *dx,
-                                   int64_t ldx, int32_t C, int32_t Hf, int32_t Wf,
-                                   const float *cam_f, float *dgrid_nhwc, void *stream) {
+extern "C" int sd_field_gather_bwd(const float *xyz, int64_t B, int64_t P, const void *dx,
+                                   int32_t dx_dtype, int64_t ldx, int32_t C, int32_t Hf,
+                                   int32_t Wf, const float *cam_f, float *dgrid_nhwc,
+                                   void *stream) {
     if (B <= 0 || P < 0 || !xyz || !dx || !cam_f || !dgrid_nhwc || C <= 0 || (C % 4) ||
+        (dx_dtype != SD_F32 && dx_dtype != SD_F16 && dx_dtype != SD_BF16) ||
         ldx < C || Hf <= 0 || Wf <= 0) {
         sd_set_error("sd_field_gather_bwd: invalid argument (C % 4 == 0, ldx >= C)");
         return -1;
     }
     if (P == 0) return 0;
-    hipLaunchKernelGGL(k_field_gather_bwd, dim3(tr_blocks((B * P + TR_RUN - 1) / TR_RUN)), dim3(TR_WAVES * 64), 0,
-                       (hipStream_t)stream, xyz, B, P, dx, ldx, C, Hf, Wf, cam_f, dgrid_nhwc);
+    const dim3 grid(tr_blocks((B * P + TR_RUN - 1) / TR_RUN)), blk(TR_WAVES * 64);
+    hipStream_t s = (hipStream_t)stream;
+    if (dx_dtype == SD_F16)
+        hipLaunchKernelGGL(k_field_gather_bwd<SD_F16>, grid, blk, 0, s, xyz, B, P,
+                           (const _Float16 *)dx, ldx, C, Hf, Wf, cam_f, dgrid_nhwc);
+    else if (dx_dtype == SD_BF16)
+        hipLaunchKernelGGL(k_field_gather_bwd<SD_BF16>, grid, blk, 0, s, xyz, B, P,
+                           (const __bf16 *)dx, ldx, C, Hf, Wf, cam_f, dgrid_nhwc);
+    else
+        hipLaunchKernelGGL(k_field_gather_bwd<SD_F32>, grid, blk, 0, s, xyz, B, P,
+                           (const float *)dx, ldx, C, Hf, Wf, cam_f, dgrid_nhwc);
     if (hipGetLastError() != hipSuccess) {
         sd_set_error("sd_field_gather_bwd: launch failed");
         return -2;

@@ -315,3 +315,26 @@ def test_field_gather_colours_gpu():
     assert torch.equal(invf.cpu(), ref["invalid_features"])
     assert torch.equal(inv.cpu().bool(), ref["invalid"])
     np.testing.assert_allclose(rgb.cpu().numpy(), ref["rgb"].numpy(), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+def test_field_gather_autocast_rows_gpu(dt):
+    """Under torch.autocast the gather writes its rows in the autocast dtype (values = the
+    f32 rows rounded) and its backward reads 16-bit row gradients."""
+    from scenedino_amd import _lib
+    from scenedino_amd.autograd import FieldGather
+    grid, xyz, w2c, Ks = _gather_case(15, B=2, P=777)
+    cam_f = _lib.cam_records(w2c.cuda(), Ks.cuda())
+    gn = grid.permute(0, 2, 3, 1).contiguous().cuda()
+    x32, *_ = _lib.field_gather(xyz.cuda(), gn, cam_f, colors=False)
+    g1 = gn.clone().requires_grad_(True)
+    with torch.autocast("cuda", dtype=dt):
+        x, *_ = FieldGather.apply(g1, xyz.cuda(), cam_f, None, None, False)
+    assert x.dtype == dt
+    assert torch.equal(x, x32.to(dt))
+    gx = torch.randn(x.shape, generator=torch.Generator().manual_seed(16)).cuda().to(dt)
+    (x.float() * gx.float()).sum().backward()
+    ref = _lib.field_gather_bwd(xyz.cuda(), gx.float(), cam_f, gn.shape[1], gn.shape[2],
+                                gn.shape[3])
+    assert rel_l2(g1.grad, ref) < 1e-6
