@@ -124,7 +124,9 @@ class BTSNet(nn.Module):
         with torch.autocast(device_type=images.device.type, enabled=False):
             # torch.inverse's LU (same kernels) without its device-to-host error check,
             # which would stall the launch queue once per frame
-            poses_w2c = torch.linalg.inv_ex(poses_c2w.float())[0]
+            # (made row-major once here: the batched inverse comes back column-major, and
+            # every camera-record build would otherwise copy it)
+            poses_w2c = torch.linalg.inv_ex(poses_c2w.float())[0].contiguous()
         if ids_encoder is None:
             images_encoder, Ks_encoder, poses_w2c_encoder = images, Ks, poses_w2c
         else:
