@@ -126,6 +126,10 @@ typedef struct sd_render_args {
      * linear: sum_k w_k (W h_k + b) = W sum_k w_k h_k + b sum_k w_k, nerf.py:394 over
      * resnetfc.py:199). */
     float *work;
+    /* Row strides (in floats) of depth / dino / rgb; 0 = dense (1, D, 3 nv).  Lets the caller
+     * render straight into one packed [depth | dino | rgb] row per ray, e.g. the send buffer
+     * of the multi-GPU all-gather (sd_render_proj only; sd_render_fused requires 0). */
+    int64_t ld_depth, ld_dino, ld_rgb;
 } sd_render_args;
 
 int sd_render_fused(const sd_render_args *args, const sd_mlp *mlp, void *stream);
@@ -140,9 +144,8 @@ int sd_render_fused(const sd_render_args *args, const sd_mlp *mlp, void *stream)
  * the positional-code columns by MFMA.  Same outputs as sd_render_fused up to
  * rounding order (16-bit modes only; the f32 parity mode keeps sd_render_fused). */
 
-/* grid_nchw (B, C, Hf, Wf) float32 -> out (B, Hf, Wf, 128, 2) in mlp->dtype (BF16/F16),
- * pair-interleaved: out[b][y][x][n] = (P[y][x][n], P[y][min(x + 1, Wf - 1)][n]), i.e.
- * both horizontal bilinear taps of a row (grid_sample border padding) in one dword.
+/* grid_nchw (B, C, Hf, Wf) float32 -> out (B, Hf, Wf, 128) in mlp->dtype (BF16/F16),
+ * plain NHWC: out[b][y][x][n] = P[y][x][n], 256 B per grid pixel.
  * Uses mlp->w_in chunks 0..C/16-1 and mlp->b_in_h. */
 int sd_project_grid(const float *grid_nchw, int64_t B, int64_t Hf, int64_t Wf,
                     const sd_mlp *mlp, void *out, void *stream);
@@ -159,7 +162,7 @@ typedef struct sd_head {
     int32_t dtype;         /* SD_BF16 or SD_F16                                       */
 } sd_head;
 
-/* args->grid = the projected pair grid (B, Hf, Wf, 128, 2) from sd_project_grid; K % 16 == 0.
+/* args->grid = the projected grid (B, Hf, Wf, 128) from sd_project_grid; K % 16 == 0.
  * Outputs as sd_render_fused; args->z may be NULL (in-kernel z sampling, see above). */
 int sd_render_proj(const sd_render_args *args, const sd_head *head, void *stream);
 

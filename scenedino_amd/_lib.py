@@ -14,7 +14,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # SDHIP_LIB: alternative build of the same library (diagnostic builds only)
 LIB_PATH = os.environ.get("SDHIP_LIB") or os.path.join(_HERE, "libsdhip.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 SD_F32 = 0
 SD_BF16 = 1
@@ -56,6 +56,7 @@ class SdRenderArgs(ctypes.Structure):
         ("rgb_samps", _vp),
         ("z_lindisp", _i32), ("z_seed", ctypes.c_uint64), ("z_offset", ctypes.c_uint64),
         ("work", _vp),
+        ("ld_depth", _i64), ("ld_dino", _i64), ("ld_rgb", _i64),
     ]
 
 
@@ -258,12 +259,11 @@ def render_fused(args: SdRenderArgs, mlp: SdMlp, ref_tensor):
 
 
 def project_grid(grid_nchw, mlp: SdMlp, dtype):
-    """P = W_in[:, :C] . grid + b_in per pixel, pair-interleaved with the right
-    neighbour's row: (B, Hf, Wf, 128, 2) in dtype, [..., 0] = P[x], [..., 1] =
-    P[min(x + 1, Wf - 1)]."""
+    """P = W_in[:, :C] . grid + b_in per pixel: (B, Hf, Wf, 128) in dtype (plain NHWC,
+    256 B per pixel)."""
     lib = load()
     B, C, H, W = grid_nchw.shape
-    out = torch.empty(B, H, W, 128, 2, device=grid_nchw.device, dtype=TORCH_DTYPE[dtype])
+    out = torch.empty(B, H, W, 128, device=grid_nchw.device, dtype=TORCH_DTYPE[dtype])
     _check(lib.sd_project_grid(ptr(_req(grid_nchw, "grid")), B, H, W, ctypes.byref(mlp),
                                ptr(out), stream_of(out)), "sd_project_grid")
     return out

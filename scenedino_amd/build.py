@@ -7,7 +7,7 @@ import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SOURCES = ["csrc/sdhip_rays.hip", "csrc/sdhip_field.hip", "csrc/sdhip_proj.hip",
+SOURCES = ["csrc/sdhip_rays.hip", "csrc/sdhip_field.hip", "csrc/sdhip_proj.hip", "csrc/sdhip_tile.hip",
            "csrc/sdhip_seg.hip", "csrc/sdhip_vit.hip", "csrc/sdhip_train.hip"]
 OUT = os.path.join(HERE, "libsdhip.so")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
@@ -27,6 +27,7 @@ def hipcc() -> str:
 def build(force: bool = False, verbose: bool = False) -> str:
     srcs = [os.path.join(HERE, s) for s in SOURCES]
     deps = srcs + [os.path.join(HERE, "csrc", "sdhip_common.h"), os.path.join(HERE, "csrc", "sdhip_point.h"),
+            os.path.join(HERE, "csrc", "sdhip_render.h"),
                    os.path.join(HERE, "..", "include", "sdhip.h")]
     if not force and os.path.exists(OUT):
         t = os.path.getmtime(OUT)

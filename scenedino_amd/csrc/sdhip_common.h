@@ -62,6 +62,7 @@ __device__ __forceinline__ bool sd_outside(float x, float y, float zc) {
 struct Taps {
     int i00, i01, i10, i11;   // pixel indices (row-major y*w + x) of nw, ne, sw, se
     float w00, w01, w10, w11; // bilinear weights
+    int x0, y0;               // column / row of the nw tap
 };
 
 __device__ __forceinline__ Taps sd_taps(float x, float y, int w, int h) {
@@ -79,6 +80,7 @@ __device__ __forceinline__ Taps sd_taps(float x, float y, int w, int h) {
     Taps t;
     t.i00 = y0 * w + x0; t.i01 = y0 * w + x1; t.i10 = y1 * w + x0; t.i11 = y1 * w + x1;
     t.w00 = ex * ey; t.w01 = wx * ey; t.w10 = ex * wy; t.w11 = wx * wy;
+    t.x0 = x0; t.y0 = y0;
     return t;
 }
 
@@ -96,11 +98,16 @@ __device__ __forceinline__ float sd_z_sample(float near, float far, int64_t K, i
     return near * (1.0f - t) + far * t;
 }
 
-// Counter-based uniform [0,1) (24-bit mantissa) for perf-mode jitter.
+// Counter-based uniform [0,1) (24-bit mantissa) for perf-mode jitter: murmur3's 32-bit
+// finaliser over the counter, keyed by both halves of the 64-bit seed (the reference draws
+// torch.rand_like, nerf.py:134; any uniform stream is a valid stratified sample).
 __device__ __forceinline__ float sd_uniform(uint64_t seed, uint64_t ctr) {
-    uint64_t z = seed + 0x9E3779B97F4A7C15ull * (ctr + 1);
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    z = z ^ (z >> 31);
-    return (float)(uint32_t)(z >> 40) * (1.0f / 16777216.0f);
+    uint32_t x = (uint32_t)ctr ^ (uint32_t)seed;
+    x = (x ^ (uint32_t)(ctr >> 32)) * 0x9E3779B1u + (uint32_t)(seed >> 32);
+    x ^= x >> 16;
+    x *= 0x85EBCA6Bu;
+    x ^= x >> 13;
+    x *= 0xC2B2AE35u;
+    x ^= x >> 16;
+    return (float)(x >> 8) * (1.0f / 16777216.0f);
 }

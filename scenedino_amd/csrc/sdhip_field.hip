@@ -41,7 +41,7 @@ extern "C" void sd_set_error(const char *msg) {
     g_err[sizeof(g_err) - 1] = 0;
 }
 extern "C" const char *sd_last_error(void) { return g_err; }
-extern "C" int sd_abi_version(void) { return 2; }
+extern "C" int sd_abi_version(void) { return 3; }
 
 // Threads per workgroup, one workgroup per CU: 16-bit kernels run 8 waves (2 per SIMD,
 // <= 256 VGPRs each); the f32 parity kernels run 4 waves (1 per SIMD, 512 VGPRs).
@@ -830,6 +830,10 @@ extern "C" int sd_render_fused(const sd_render_args *args, const sd_mlp *mlp, vo
     }
     if (sd_plan(mlp, &pl)) return -1;
     const sd_render_args &a = *args;
+    if (a.ld_depth || a.ld_dino || a.ld_rgb) {
+        sd_set_error("sd_render_fused: output row strides are not supported (must be 0)");
+        return -1;
+    }
     if (a.R < 0 || a.R >= (1LL << 31) || a.K <= 0 || (a.K % 32) || a.ray_dim < 6 ||
         a.rays_per_sb <= 0 || !a.rays ||
         !a.z || !a.grid || !a.cam_f || !a.depth || !a.dino || a.Hf <= 0 || a.Wf <= 0 ||

@@ -24,7 +24,7 @@
 // samples render view g), DINO; the ray epilogue reduces over the 16 sample lanes.
 // Pipelining: the z values of item i+2 and the P-tap loads of item i+1 are in flight
 // while item i computes.
-#include "sdhip_point.h"
+#include "sdhip_render.h"
 
 // diagnostic ablation switches (timing experiments only; outputs are wrong when set)
 #ifndef SD_ABL_NORAYPASS
@@ -43,108 +43,12 @@
 #define SD_PWG 256  // threads per workgroup (4 waves); several workgroups per CU
 #endif
 
-// 16-bit element traits.  Blend of the pair-interleaved projected grid (k_project):
-// every dword of a row holds (P[x0][c], P[x1][c]) of one channel c, so a bilinear
-// sample is two v_dot2 per channel, row y0 . (w00, w01) + row y1 . (w10, w11), in f32
-// with one rounding to the 16-bit operand type.
-template <int P> struct T16;
-template <> struct T16<SD_F16> {
-    typedef f16x8 Frag;
-    typedef _Float16 E;
-    static __device__ __forceinline__ f32x4 mma(const Frag &a, const Frag &b, const f32x4 &c) {
-        return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
-    }
-    static __device__ __forceinline__ f32x16 mma32(const Frag &a, const Frag &b, const f32x16 &c) {
-        return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
-    }
-    static __device__ __forceinline__ uint16_t bits(float f) {
-        return __builtin_bit_cast(uint16_t, (_Float16)f);
-    }
-    // x . w with a zero accumulator (VOP3P form: no v_mov of the zero)
-    static __device__ __forceinline__ float dot2z(uint32_t x, uint32_t w) {
-        float r;
-        asm("v_dot2_f32_f16 %0, %1, %2, 0" : "=v"(r) : "v"(x), "v"(w));
-        return r;
-    }
-    static __device__ __forceinline__ float dot2(uint32_t x, uint32_t w, float c) {
-        return __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2, x), __builtin_bit_cast(f16x2, w), c, false);
-    }
-};
-template <> struct T16<SD_BF16> {
-    typedef bf16x8 Frag;
-    typedef __bf16 E;
-    typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
-    static __device__ __forceinline__ f32x4 mma(const Frag &a, const Frag &b, const f32x4 &c) {
-        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-    }
-    static __device__ __forceinline__ f32x16 mma32(const Frag &a, const Frag &b, const f32x16 &c) {
-        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-    }
-    static __device__ __forceinline__ uint16_t bits(float f) {
-        return __builtin_bit_cast(uint16_t, (__bf16)f);
-    }
-    static __device__ __forceinline__ float dot2z(uint32_t x, uint32_t w) {
-        float r;
-        asm("v_dot2_f32_bf16 %0, %1, %2, 0" : "=v"(r) : "v"(x), "v"(w));
-        return r;
-    }
-    static __device__ __forceinline__ float dot2(uint32_t x, uint32_t w, float c) {
-        return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, x), __builtin_bit_cast(bf16x2, w), c, false);
-    }
-};
-
-// two floats -> one packed 16-bit pair (v_cvt_pk_f16_f32 / v_cvt_pk_bf16_f32, RNE)
-template <typename E>
-__device__ __forceinline__ uint32_t sd_pack2(float a, float b) {
-    typedef __attribute__((ext_vector_type(2))) float f32x2;
-    typedef __attribute__((ext_vector_type(2))) E e2;
-    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, e2));
-}
-
-// 16-bit halves of a packed pair -> f32
-template <int P> __device__ __forceinline__ float sd_unpack_lo(uint32_t d) {
-    if (P == SD_BF16) return bf16lo(d);
-    return (float)__builtin_bit_cast(f16x2, d)[0];
-}
-template <int P> __device__ __forceinline__ float sd_unpack_hi(uint32_t d) {
-    if (P == SD_BF16) return bf16hi(d);
-    return (float)__builtin_bit_cast(f16x2, d)[1];
-}
-
-// blend weights as the ray pass stores them: (w00, w01), (w10, w11) packed in E
-template <int P>
-__device__ __forceinline__ uint4 sd_pack_w(float w00, float w01, float w10, float w11) {
-    typedef typename T16<P>::E E;
-    return uint4{sd_pack2<E>(w00, w01), sd_pack2<E>(w10, w11), 0u, 0u};
-}
-
-// 8 channels of one sample from its two pair rows: a, b = row y0 (channels 0-3, 4-7),
-// c, d = row y1
-template <int P>
-__device__ __forceinline__ typename T16<P>::Frag sd_blend_pair(const uint4 &a, const uint4 &b,
-                                                              const uint4 &c, const uint4 &d,
-                                                              const uint4 &wp) {
-    typedef T16<P> Tr;
-    const uint32_t R0[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    const uint32_t R1[8] = {c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
-    uint32_t o[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const float lo = Tr::dot2(R0[2 * i], wp.x, Tr::dot2z(R1[2 * i], wp.y));
-        const float hi = Tr::dot2(R0[2 * i + 1], wp.x, Tr::dot2z(R1[2 * i + 1], wp.y));
-        o[i] = sd_pack2<typename Tr::E>(lo, hi);
-    }
-    return __builtin_bit_cast(typename Tr::Frag, uint4{o[0], o[1], o[2], o[3]});
-}
 
 // ---------------------------------------------------------------------------
-// k_project: P[b][pix][n] = sum_c W_in[n][c] G[b][c][pix] + b_in[n]   (n < 128),
-// stored pair-interleaved: P2[b][pix][n] = (P[pix][n], P[right(pix)][n]) with
-// right(pix) = pix + 1, or pix itself in the last column (x1 = min(x0 + 1, W - 1) of
-// grid_sample's border padding), so one 16-byte load of a row gives both horizontal
-// taps of 4 channels.  One wave = 32 pixel columns x 128 hidden = 4 tiles of 32x32x16,
-// K = C in chunks of 16; waves step by 31 pixels so that column 31 (the next wave's
-// first pixel) supplies the right neighbour of column 30 (lane exchange, no reload).
+// k_project: P[b][pix][n] = sum_c W_in[n][c] G[b][c][pix] + b_in[n]   (n < 128), stored
+// plain (B, Hf, Wf, 128) in the 16-bit MLP dtype: 256 B per grid pixel, so the two
+// horizontal bilinear taps of a sample (x0, x0 + 1) are 512 contiguous bytes.  One wave =
+// 32 pixel columns x 128 hidden = 4 tiles of 32x32x16, K = C in chunks of 16.
 // A = the sd_mlp layer-1 fragments of the grid columns (LDS); B = 8 channels of the
 // lane's pixel read from NCHW (32 consecutive floats per channel across a half).
 // ---------------------------------------------------------------------------
@@ -165,12 +69,12 @@ k_project(const float *__restrict__ grid, int64_t B, int C, int64_t HW, int W, c
     const Frag *lw = (const Frag *)lds;
     const int lane = threadIdx.x & 63, h = lane >> 5, li = lane & 31;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t ntile = (HW + 30) / 31, total = B * ntile;
+    const int64_t ntile = (HW + 31) / 32, total = B * ntile;
     for (int64_t task = (int64_t)blockIdx.x * (SD_PWG / 64) + wave; task < total;
          task += (int64_t)gridDim.x * (SD_PWG / 64)) {
         const int64_t b = task / ntile;
-        const int64_t pix = (task - b * ntile) * 31 + li;
-        const bool valid = li < 31 && pix < HW;
+        const int64_t pix = (task - b * ntile) * 32 + li;
+        const bool valid = pix < HW;
         const float *gp = grid + b * C * HW + (pix < HW ? pix : HW - 1) + (int64_t)(8 * h) * HW;
         f32x16 acc[4];
 #pragma unroll
@@ -210,95 +114,28 @@ k_project(const float *__restrict__ grid, int64_t B, int C, int64_t HW, int W, c
             kstep(q + 1, x1);
         }
         if (q < nq) kstep(q, x0);
-        // own values packed in hidden pairs; the right neighbour's from lane + 1
-        const bool last_col = (pix % W) == W - 1;
-        const int src = (lane + 1) << 2;
+        if (valid) {
+            uint2 *op = (uint2 *)(out + (b * HW + pix) * (SD_DH / 2));
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
+            for (int t = 0; t < 4; ++t)
 #pragma unroll
-            for (int r4 = 0; r4 < 4; ++r4) {
-                // accumulator rows 4 r4 .. 4 r4 + 3 = hidden 32 t + 8 r4 + 4 h + 0..3
-                const uint32_t o01 = sd_pack2<typename Tr::E>(acc[t][4 * r4], acc[t][4 * r4 + 1]);
-                const uint32_t o23 = sd_pack2<typename Tr::E>(acc[t][4 * r4 + 2], acc[t][4 * r4 + 3]);
-                uint32_t n01 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)o01);
-                uint32_t n23 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)o23);
-                if (last_col) { n01 = o01; n23 = o23; }
-                if (valid) {
-                    const uint4 v = {__builtin_amdgcn_perm(n01, o01, 0x05040100u),
-                                     __builtin_amdgcn_perm(n01, o01, 0x07060302u),
-                                     __builtin_amdgcn_perm(n23, o23, 0x05040100u),
-                                     __builtin_amdgcn_perm(n23, o23, 0x07060302u)};
-                    *(uint4 *)(out + (b * HW + pix) * SD_DH + 32 * t + 8 * r4 + 4 * h) = v;
-                }
-            }
+                for (int r4 = 0; r4 < 4; ++r4)
+                    // accumulator rows 4 r4 .. 4 r4 + 3 = hidden 32 t + 8 r4 + 4 h + 0..3
+                    op[(32 * t + 8 * r4 + 4 * h) / 4] =
+                        uint2{sd_pack2<typename Tr::E>(acc[t][4 * r4], acc[t][4 * r4 + 1]),
+                              sd_pack2<typename Tr::E>(acc[t][4 * r4 + 2], acc[t][4 * r4 + 3])};
+        }
     }
 }
 
 // ---------------------------------------------------------------------------
 // render helpers
 // ---------------------------------------------------------------------------
-// DPP with "old" = 1.0 for lanes whose source is outside the row (bound_ctrl off)
-#define SD_DPP1(x, ctrl) \
-    __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, 1.f), \
-                                                          __builtin_bit_cast(int, (x)), (ctrl), 0xf, 0xf, false))
-#define SD_DPP0(x, ctrl) \
-    __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, (x)), (ctrl), 0xf, 0xf, true))
-
-// inclusive product scan over the 16 lanes of every row (row_shr 1, 2, 4, 8)
-__device__ __forceinline__ float sd_scan_mul16(float x) {
-    x *= SD_DPP1(x, 0x111);
-    x *= SD_DPP1(x, 0x112);
-    x *= SD_DPP1(x, 0x114);
-    x *= SD_DPP1(x, 0x118);
-    return x;
-}
-// sum over the 16 lanes of every row, result in every lane (row_ror 8, 4, 2, 1)
-__device__ __forceinline__ float sd_rowsum16(float x) {
-    x += SD_DPP0(x, 0x128);
-    x += SD_DPP0(x, 0x124);
-    x += SD_DPP0(x, 0x122);
-    x += SD_DPP0(x, 0x121);
-    return x;
-}
-
-// sin of an angle given in revolutions (x / 2 pi): one range reduction + v_sin_f32
-__device__ __forceinline__ float sd_sin_rev(float r) {
-    return __builtin_amdgcn_sinf(__builtin_amdgcn_fractf(r));
-}
-
-// Positional-code fragment of chunk pc for lane group g (element e):
-//   G = 2 pc + (g >> 1), phase = g & 1 (0: sin, 1: cos = sin(x + pi/2))
-//   G < 3, e < 6 : sin(v[e % 3] * 1.5 * 2^(2G + (e >= 3)) + phase * pi/2)
-//   G = 0, e >= 6: raw inputs (g = 0: x, y; g = 1: z~, 0)
-//   otherwise don't-care: the packed code weights of those slots are zero
-//   (scenedino_amd/mlp_pack.py: proj_pe_col gives the W_in column of every slot).
-// The angle is formed in revolutions, fmaf(v * 4^(g >> 1), 1.5 * 2^k / 2 pi, phase / 4).
-template <typename Frag, typename E>
-__device__ __forceinline__ Frag sd_code_frag(const float v[3], int pc, int g) {
-    const float ph = (g & 1) ? 0.25f : 0.f;
-    const float ls = (g >> 1) ? 4.f : 1.f;
-    const float u[3] = {v[0] * ls, v[1] * ls, v[2] * ls};
-    float r[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        if (e < 6) {
-            const float f = 1.5f * (float)(1 << (4 * pc + (e >= 3 ? 1 : 0))) * 0.15915494309189535f;
-            r[e] = sd_sin_rev(fmaf(u[e % 3], f, ph));
-        } else if (pc == 0) {
-            r[e] = (g >> 1) ? 0.f : (g == 0 ? v[e - 6] : (e == 6 ? v[2] : 0.f));
-        } else {
-            r[e] = 0.f;
-        }
-    }
-    const uint4 u4 = {sd_pack2<E>(r[0], r[1]), sd_pack2<E>(r[2], r[3]), sd_pack2<E>(r[4], r[5]),
-                      sd_pack2<E>(r[6], r[7])};
-    return __builtin_bit_cast(Frag, u4);
-}
 
 // Per-sample record written by the ray pass into wave-private LDS, quad-major
 // ([q][k][4 words], q = 0 .. RS/4-1) so that both the ray pass (lane = sample) and the
 // item reads (lane j = sample) are conflict-free 16-byte accesses:
-//   q0: byte offsets pix * 512 of the pair rows y0 and y1 at column x0 in the pair-
+//   q0: byte offsets pix * 256 of the taps (x0, y0) and (x0, y1) in the plain P
 //       interleaved P (bit 0 of the first: outside the encoder frustum; bits 0..3 of
 //       the second: outside render view 0..3), 2 spare words
 //   q1: bilinear weights pre-packed in the blend's operand format (T16<P>::pack_w)
@@ -329,8 +166,8 @@ static inline bool sd_head_hc(int D) {
 #endif
 
 struct PItem {
-    int ray, sub, sbi, n;
-    uint32_t o[2];  // pair-row byte offsets (+ 32 g) inside the batch element's P plane
+    int ray, sub, sbi, n, rr;  // rr: the real ray of the (virtual) ray index
+    uint32_t o[2];  // tap (x0, y0) / (x0, y1) byte offsets (+ 16 g) inside the P plane
     uint4 wp;       // packed blend weights
     float v[3];
     float zk, delta;
@@ -343,22 +180,15 @@ struct PRaw { uint4 a, b, c, d; };
 
 // chunk q (channels 32 q .. 32 q + 31; this lane's group: 8 of them = 32 bytes per row)
 __device__ __forceinline__ PRaw sd_pload(const PItem &it, int q) {
-    const uint32_t s = (uint32_t)q * 128u;
+    const uint32_t s = (uint32_t)q * 64u;
     PRaw r;
     r.a = sd_ld128(it.rs, it.o[0], s);
-    r.b = sd_ld128(it.rs, it.o[0] + 16u, s);
+    r.b = sd_ld128(it.rs, it.o[0] + 256u, s);
     r.c = sd_ld128(it.rs, it.o[1], s);
-    r.d = sd_ld128(it.rs, it.o[1] + 16u, s);
+    r.d = sd_ld128(it.rs, it.o[1] + 256u, s);
     return r;
 }
 
-// ReLU of two packed 16-bit values (bf16 or f16): a negative value has the sign bit
-// set, i.e. is a negative int16, so max_i16(x, 0) clamps it to +0.
-__device__ __forceinline__ uint32_t sd_relu2(uint32_t x) {
-    typedef __attribute__((ext_vector_type(2))) short s16x2;
-    const s16x2 v = __builtin_bit_cast(s16x2, x);
-    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(v, (s16x2){0, 0}));
-}
 
 // LDS image of the render kernel: [code 2][8][64] | [sigma 4][64] | [dino D/16][4][64]
 // (16 B per lane entry), then per wave SD_RECBUF x K sample records.
@@ -368,12 +198,12 @@ __device__ __forceinline__ uint32_t sd_relu2(uint32_t x) {
 
 // wave-uniform cursor with the wave's ray ordinal n (selects the record buffer)
 struct RCursor {
-    int ray, sub, sbi, n;
+    int ray, sub, sbi, n, rr;
 };
 
 template <int P, int NV, int NDT>
 __global__ void __launch_bounds__(SD_RWG) __attribute__((amdgpu_waves_per_eu(SD_RWAVES)))
-k_render_proj(const sd_render_args a, const sd_head m) {
+k_render_proj(const sd_render_args a, const sd_head m, const int32_t *__restrict__ list) {
     typedef T16<P> Tr;
     typedef typename Tr::Frag Frag;
     typedef typename Tr::E E;
@@ -401,11 +231,25 @@ k_render_proj(const sd_render_args a, const sd_head m) {
     const int K = a.K, nsub = K >> 4, nv = NV > 0 ? NV : a.nv;
     const int RQ = sd_rec_words(nv) / 4;  // 16-byte quads per record
     uint4 *recs = (uint4 *)(lds + (SD_LDS_OUT + NDT * 4 * SD_WAVE) * 16) + wave * SD_RECBUF * K * RQ;
-    const uint32_t plane_bytes = (uint32_t)a.Hf * a.Wf * SD_DH * 4;
+    const uint32_t plane_bytes = (uint32_t)a.Hf * a.Wf * SD_DH * 2;
     const int64_t cplane = (int64_t)a.Hc * a.Wc * 4;
-    const int nwaves = gridDim.x * (SD_RWG / 64);
-    const int ray0 = blockIdx.x * (SD_RWG / 64) + wave;
-    const int R = (int)a.R, rps = (int)a.rays_per_sb;
+    // XCD-aware ray ranges: workgroups b, b + 8, ... share one XCD (round-robin dispatch,
+    // a speed assumption only), so XCD x gets the contiguous rays [x R/8, (x+1) R/8): the
+    // P rows its rays' epipolar lines cross stay in that XCD's 4 MiB L2 instead of every
+    // XCD streaming all of P.  R below is this range's end.
+    const int nx = (gridDim.x % 8 == 0) ? 8 : 1;
+    const int xcd = blockIdx.x % nx;
+    const int nwaves = (gridDim.x / nx) * (SD_RWG / 64);
+    const int rps = (int)a.rays_per_sb;
+    // list != NULL (fallback behind the tile kernel): the rays of the groups listed in
+    // list[1 .. list[0]] (8 consecutive rays each) form the virtual ray sequence
+    const int Rreal = (int)a.R;
+    const int64_t RA = list ? (int64_t)__builtin_amdgcn_readfirstlane(list[0]) * 8 : a.R;
+    auto rmap = [&](int v) {
+        return list ? min(list[1 + (v >> 3)] * 8 + (v & 7), Rreal - 1) : v;
+    };
+    const int R = (int)(RA * (xcd + 1) / nx);
+    const int ray0 = (int)(RA * xcd / nx) + (blockIdx.x / nx) * (SD_RWG / 64) + wave;
     if (ray0 >= R) return;
     const int nitems = ((R - ray0 + nwaves - 1) / nwaves) * nsub;
     // in-kernel z (a.z == NULL): sd_sample_z's arithmetic, jitter from the counter RNG
@@ -418,7 +262,8 @@ k_render_proj(const sd_render_args a, const sd_head m) {
             c.ray += nwaves;
             c.sub = 0;
             c.n++;
-            c.sbi = (int)((unsigned)c.ray / (unsigned)rps);
+            c.rr = rmap(c.ray);
+            c.sbi = (int)((unsigned)c.rr / (unsigned)rps);
         }
         return c;
     };
@@ -496,8 +341,8 @@ k_render_proj(const sd_render_args a, const sd_head m) {
                         invc |= (ic ? 1u : 0u) << v;
                     }
                 }
-                rb[0 * K + k] = uint4{(uint32_t)geo.t.i00 * 512u | (geo.inv_f ? 1u : 0u),
-                                      (uint32_t)geo.t.i10 * 512u | invc, 0u, 0u};
+                rb[0 * K + k] = uint4{(uint32_t)geo.t.i00 * 256u | (geo.inv_f ? 1u : 0u),
+                                      (uint32_t)geo.t.i10 * 256u | invc, 0u, 0u};
                 rb[1 * K + k] = sd_pack_w<P>(geo.t.w00, geo.t.w01, geo.t.w10, geo.t.w11);
                 rb[2 * K + k] = __builtin_bit_cast(uint4, f32x4{geo.v[0], geo.v[1], geo.v[2], z0});
                 if (!(DEFER && p == 0))
@@ -530,6 +375,7 @@ k_render_proj(const sd_render_args a, const sd_head m) {
     // ---- item open: this lane's sample record from LDS -------------------------------
     auto open_item = [&](const RCursor &c, PItem &it) {
         it.ray = c.ray;
+        it.rr = c.rr;
         it.sub = c.sub;
         it.sbi = c.sbi;
         it.n = c.n;
@@ -539,9 +385,9 @@ k_render_proj(const sd_render_args a, const sd_head m) {
         const uint4 q1 = rb[K + k];
         const f32x4 q2 = __builtin_bit_cast(f32x4, rb[2 * K + k]);
         const f32x4 q3 = __builtin_bit_cast(f32x4, rb[3 * K + k]);
-        const uint32_t lo = 32u * (uint32_t)g;
-        it.o[0] = (q0.x & ~511u) + lo;
-        it.o[1] = (q0.y & ~511u) + lo;
+        const uint32_t lo = 16u * (uint32_t)g;
+        it.o[0] = (q0.x & ~255u) + lo;
+        it.o[1] = (q0.y & ~255u) + lo;
         it.inv_f = q0.x & 1u;
         const int vv = NV == 1 ? 0 : g;
         it.invc = (q0.y >> vv) & 1u;
@@ -564,13 +410,14 @@ k_render_proj(const sd_render_args a, const sd_head m) {
     };
 
     // prologue: records of the first ray, item 0 open with its taps in flight
-    RCursor c0 = {ray0, 0, (int)((unsigned)ray0 / (unsigned)rps), 0};
+    const int rr0 = rmap(ray0);
+    RCursor c0 = {ray0, 0, (int)((unsigned)rr0 / (unsigned)rps), 0, rr0};
     float zq[2 * MAXP];
-    load_ray_z(c0.ray, zq);
-    ray_pass(c0.ray, c0.sbi, 0, zq);
+    load_ray_z(c0.rr, zq);
+    ray_pass(c0.rr, c0.sbi, 0, zq);
     ray_col(0);
     const bool more = ray0 + nwaves < R;
-    if (more) load_ray_z(ray0 + nwaves, zq);  // z of the wave's second ray in flight
+    if (more) load_ray_z(rmap(ray0 + nwaves), zq);  // z of the wave's second ray in flight
     PItem cur;
     open_item(c0, cur);
     RCursor c1 = advance(c0);
@@ -596,17 +443,17 @@ k_render_proj(const sd_render_args a, const sd_head m) {
         if (SD_RECBUF == 2) {
             // first item of a ray: records of the wave's next ray into the other buffer
             if (cur.sub == 0 && cur.ray + nwaves < R) {
-                const int nr = cur.ray + nwaves;
-                ray_pass(nr, (int)((unsigned)nr / (unsigned)rps), (cur.n + 1) & 1, zq);
+                const int nr = cur.ray + nwaves, nrr = rmap(nr);
+                ray_pass(nrr, (int)((unsigned)nrr / (unsigned)rps), (cur.n + 1) & 1, zq);
                 passed = true;
-                if (nr + nwaves < R) load_ray_z(nr + nwaves, zq);
+                if (nr + nwaves < R) load_ray_z(rmap(nr + nwaves), zq);
             }
         } else if (c1.n != cur.n) {
             // the next item starts the wave's next ray: its records replace this ray's
             // (every record of this ray was read when `cur` was opened)
-            ray_pass(c1.ray, c1.sbi, 0, zq);
+            ray_pass(c1.rr, c1.sbi, 0, zq);
             ray_col(0);
-            if (c1.ray + nwaves < R) load_ray_z(c1.ray + nwaves, zq);
+            if (c1.ray + nwaves < R) load_ray_z(rmap(c1.ray + nwaves), zq);
         }
 #endif
         open_item(c1, nxt);
@@ -619,7 +466,7 @@ k_render_proj(const sd_render_args a, const sd_head m) {
 #define SD_PCHUNK(r, q)                                                        \
         {                                                                      \
             Frag f_ = SD_ABL_NOBLEND ? __builtin_bit_cast(Frag, r.a ^ r.b ^ r.c ^ r.d) \
-                                     : sd_blend_pair<P>(r.a, r.b, r.c, r.d, cur.wp); \
+                                     : sd_blend_plain<P>(r.a, r.b, r.c, r.d, cur.wp); \
             r = sd_pload(nxt, q);                                              \
             acc[2 * q] = Tr::mma(id0, f_, zero4);                              \
             acc[2 * q + 1] = Tr::mma(id1, f_, zero4);                          \
@@ -698,7 +545,7 @@ k_render_proj(const sd_render_args a, const sd_head m) {
         }
 
         // per-sample outputs: wave-uniform ray base + 32-bit lane offset
-        const int64_t rk = (int64_t)cur.ray * K;
+        const int64_t rk = (int64_t)cur.rr * K;
         if (g == 0) {
             if (a.weights) (a.weights + rk)[k] = w;
             if (a.alphas) (a.alphas + rk)[k] = alpha;
@@ -729,12 +576,12 @@ k_render_proj(const sd_render_args a, const sd_head m) {
                     f32x4 res;
 #pragma unroll
                     for (int r = 0; r < 4; ++r) res[r] = v[r] + wsum * bd[r];
-                    *(f32x4 *)(a.dino + (int64_t)cur.ray * m.D + dim) = res;
+                    *(f32x4 *)(a.dino + (int64_t)cur.rr * a.ld_dino + dim) = res;
                 }
                 dacc[dt] = zero4;
             }
             if (HC) {
-                float *hs = a.work + (int64_t)cur.ray * SD_HC_STRIDE;
+                float *hs = a.work + (int64_t)cur.rr * SD_HC_STRIDE;
 #pragma unroll
                 for (int t = 0; t < 8; ++t) {
                     f32x4 v;
@@ -745,9 +592,9 @@ k_render_proj(const sd_render_args a, const sd_head m) {
                 }
                 if (lane == 0) hs[SD_DH] = wsum;
             }
-            if (lane == 0) a.depth[cur.ray] = dsum;
+            if (lane == 0) a.depth[(int64_t)cur.rr * a.ld_depth] = dsum;
             if (j == 0 && g < nv) {
-                float *rp = a.rgb + (int64_t)cur.ray * 3 * nv + 3 * g;
+                float *rp = a.rgb + (int64_t)cur.rr * a.ld_rgb + 3 * g;
                 rp[0] = c0s; rp[1] = c1s; rp[2] = c2s;
             }
             Tc = 1.f; dpart = 0.f; wpart = 0.f;
@@ -770,7 +617,8 @@ k_render_proj(const sd_render_args a, const sd_head m) {
 // ---------------------------------------------------------------------------
 template <int P>
 __global__ void __launch_bounds__(SD_PWG)
-k_head_hc(const float *__restrict__ work, int64_t R, const sd_head m, float *__restrict__ dino) {
+k_head_hc(const float *__restrict__ work, int64_t R, const sd_head m, float *__restrict__ dino,
+          int64_t ld_dino, const int32_t *__restrict__ list) {
     typedef T16<P> Tr;
     typedef typename Tr::Frag Frag;
     typedef typename Tr::E E;
@@ -785,10 +633,13 @@ k_head_hc(const float *__restrict__ work, int64_t R, const sd_head m, float *__r
     const Frag *lw = (const Frag *)lds;
     const int lane = threadIdx.x & 63, j = lane & 15, g = lane >> 4;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t ntile = (R + 15) / 16;
+    // list != NULL: the rays of the listed groups (see k_render_proj)
+    const int64_t RA = list ? (int64_t)__builtin_amdgcn_readfirstlane(list[0]) * 8 : R;
+    const int64_t ntile = (RA + 15) / 16;
     for (int64_t tile = (int64_t)blockIdx.x * (SD_PWG / 64) + wave; tile < ntile;
          tile += (int64_t)gridDim.x * (SD_PWG / 64)) {
-        const int64_t ray = tile * 16 + j;
+        const int64_t v = min(tile * 16 + j, RA - 1);
+        const int64_t ray = list ? min((int64_t)list[1 + (v >> 3)] * 8 + (v & 7), R - 1) : tile * 16 + j;
         const float *hs = work + (ray < R ? ray : R - 1) * SD_HC_STRIDE;
         Frag B[4];
 #pragma unroll
@@ -810,7 +661,7 @@ k_head_hc(const float *__restrict__ work, int64_t R, const sd_head m, float *__r
             f32x4 res;
 #pragma unroll
             for (int r = 0; r < 4; ++r) res[r] = o[r] + ws * bd[r];
-            if (ray < R) *(f32x4 *)(dino + ray * m.D + dim) = res;
+            if (ray < R) *(f32x4 *)(dino + ray * ld_dino + dim) = res;
         }
     }
 }
@@ -858,7 +709,7 @@ extern "C" int sd_project_grid(const float *grid, int64_t B, int64_t Hf, int64_t
     }
     hipStream_t s = (hipStream_t)stream;
     int64_t nblk;
-    const int64_t work = B * ((HW + 30) / 31);
+    const int64_t work = B * ((HW + 31) / 32);
     if (m->dtype == SD_F16) {
         sd_launch_proj(k_project<SD_F16>, work, lds_bytes, s, nblk);
         hipLaunchKernelGGL(k_project<SD_F16>, dim3((unsigned)nblk), dim3(SD_PWG), lds_bytes, s,
@@ -872,7 +723,8 @@ extern "C" int sd_project_grid(const float *grid, int64_t B, int64_t Hf, int64_t
 }
 
 template <int P, int NV, int NDT>
-static int sd_rp_launch(const sd_render_args &a, const sd_head &m, hipStream_t s) {
+static int sd_rp_launch(const sd_render_args &a, const sd_head &m, hipStream_t s,
+                        const int32_t *list) {
     const int lds_bytes = (SD_LDS_OUT + NDT * 4 * SD_WAVE) * 16 +
                           (SD_RWG / 64) * SD_RECBUF * a.K * sd_rec_words(a.nv) * 4;
     if (lds_bytes > 160 * 1024) {
@@ -882,26 +734,29 @@ static int sd_rp_launch(const sd_render_args &a, const sd_head &m, hipStream_t s
     int64_t nblk;
     sd_launch_proj(k_render_proj<P, NV, NDT>, a.R, lds_bytes, s, nblk, SD_RWG);
     hipLaunchKernelGGL((k_render_proj<P, NV, NDT>), dim3((unsigned)nblk), dim3(SD_RWG), lds_bytes,
-                       s, a, m);
+                       s, a, m, list);
     return sd_check_err();
 }
 
 template <int P, int NV>
-static int sd_rp_ndt(const sd_render_args &a, const sd_head &m, hipStream_t s) {
-    if (!sd_head_hc(m.D)) {
+static int sd_rp_ndt(const sd_render_args &a, const sd_head &m, hipStream_t s,
+                     const int32_t *list = nullptr) {
+    // list mode (overflow fallback, usually empty): the folded head where it exists, so
+    // no second launch
+    if (!sd_head_hc(m.D) || (list && (m.D == 32 || m.D == 64 || m.D == 128))) {
         switch (m.D / 16) {
-            case 2: return sd_rp_launch<P, NV, 2>(a, m, s);
-            case 4: return sd_rp_launch<P, NV, 4>(a, m, s);
-            case 8: return sd_rp_launch<P, NV, 8>(a, m, s);
+            case 2: return sd_rp_launch<P, NV, 2>(a, m, s, list);
+            case 4: return sd_rp_launch<P, NV, 4>(a, m, s, list);
+            case 8: return sd_rp_launch<P, NV, 8>(a, m, s, list);
         }
     }
-    int rc = sd_rp_launch<P, NV, 0>(a, m, s);
+    int rc = sd_rp_launch<P, NV, 0>(a, m, s, list);
     if (rc) return rc;
     const int lds_bytes = (m.D >> 4) * 4 * SD_WAVE * 16;
     int64_t nblk;
     sd_launch_proj(k_head_hc<P>, (a.R + 15) / 16, lds_bytes, s, nblk);
     hipLaunchKernelGGL(k_head_hc<P>, dim3((unsigned)nblk), dim3(SD_PWG), lds_bytes, s, a.work, a.R,
-                       m, a.dino);
+                       m, a.dino, a.ld_dino, list);
     return sd_check_err();
 }
 
@@ -910,9 +765,17 @@ static int sd_rp_nv(const sd_render_args &a, const sd_head &m, hipStream_t s) {
     return a.nv == 1 ? sd_rp_ndt<P, 1>(a, m, s) : sd_rp_ndt<P, 0>(a, m, s);
 }
 
-extern "C" int64_t sd_render_proj_work_bytes(int64_t R, int32_t D) {
+// work = [hidden-composite scratch of the per-ray kernel][overflow list of the tile kernel]
+static int64_t sd_hc_bytes(int64_t R, int32_t D) {
     return sd_head_hc(D) ? R * SD_HC_STRIDE * (int64_t)sizeof(float) : 0;
 }
+extern "C" int64_t sd_render_proj_work_bytes(int64_t R, int32_t D) {
+    return sd_hc_bytes(R, D) + ((4 * (1 + (R + 7) / 8) + 15) / 16) * 16;
+}
+
+extern "C" int sd_render_tile_ok(const sd_render_args *a, const sd_head *m);
+extern "C" int sd_render_tile_launch(const sd_render_args *a, const sd_head *m, int32_t *ovf,
+                                     void *stream);
 
 extern "C" int sd_render_proj(const sd_render_args *args, const sd_head *m, void *stream) {
     if (!args || !m || !m->w_pe || !m->w_sig || !m->w_out || !m->b_dino ||
@@ -921,22 +784,39 @@ extern "C" int sd_render_proj(const sd_render_args *args, const sd_head *m, void
         sd_set_error("sd_render_proj: invalid head (16-bit dtype, D % 16 == 0, D <= 512)");
         return -1;
     }
-    if (sd_head_hc(m->D) && !args->work) {
-        sd_set_error("sd_render_proj: this D needs args->work (sd_render_proj_work_bytes)");
+    if (!args->work) {
+        sd_set_error("sd_render_proj: args->work is required (sd_render_proj_work_bytes)");
         return -1;
     }
-    const sd_render_args &a = *args;
+    sd_render_args a = *args;  // output strides normalised below (0 = dense)
     if (a.R < 0 || a.R >= (1LL << 31) || a.K <= 0 || (a.K % 16) || a.K > 128 || a.ray_dim < 6 ||
         a.rays_per_sb <= 0 || !a.rays || (!a.z && a.ray_dim < 8) ||
         !a.grid || !a.cam_f || !a.depth || !a.dino || a.Hf <= 0 || a.Wf <= 0 ||
-        a.nv < 0 || a.nv > SD_MAX_NV || (int64_t)a.Hf * a.Wf * SD_DH * 4 >= (1LL << 32) ||
+        a.nv < 0 || a.nv > SD_MAX_NV || (int64_t)a.Hf * a.Wf * SD_DH * 2 >= (1LL << 32) ||
         (a.nv > 0 && (!a.img || !a.cam_c || !a.rgb || a.Hc <= 0 || a.Wc <= 0))) {
         sd_set_error("sd_render_proj: invalid argument (K % 16 == 0, K <= 128, nv <= 4, "
                      "P plane < 4 GiB)");
         return -1;
     }
+    if (a.ld_depth < 0 || a.ld_dino < 0 || a.ld_rgb < 0 ||
+        (a.ld_dino && a.ld_dino < m->D) || (a.ld_rgb && a.ld_rgb < 3 * a.nv)) {
+        sd_set_error("sd_render_proj: output row strides must be 0 (dense) or >= the row width");
+        return -1;
+    }
+    if (!a.ld_depth) a.ld_depth = 1;
+    if (!a.ld_dino) a.ld_dino = m->D;
+    if (!a.ld_rgb) a.ld_rgb = 3 * a.nv;
     if (a.R == 0) return 0;
     hipStream_t s = (hipStream_t)stream;
+    if (sd_render_tile_ok(&a, m)) {
+        // LDS-staged tile kernel (sdhip_tile.hip); groups whose tap box does not fit a tile
+        // buffer are listed and rendered by the per-ray kernel behind it
+        int32_t *ovf = (int32_t *)((uint8_t *)a.work + sd_hc_bytes(a.R, m->D));
+        int rc = sd_render_tile_launch(&a, m, ovf, stream);
+        if (rc) return rc;
+        if (m->dtype == SD_F16) return sd_rp_ndt<SD_F16, 1>(a, *m, s, ovf);
+        return sd_rp_ndt<SD_BF16, 1>(a, *m, s, ovf);
+    }
     if (m->dtype == SD_F16) return sd_rp_nv<SD_F16>(a, *m, s);
     return sd_rp_nv<SD_BF16>(a, *m, s);
 }

@@ -1,0 +1,667 @@
+// sdhip_tile.hip -- LDS-staged projected-grid render (gfx950 / CDNA4, 16-bit modes).
+//
+// Same computation as k_render_proj (sdhip_proj.hip: NeRFRenderer.composite over
+// BTSNet.forward, nerf.py:230-449 / bts.py:271-595, on the projected grid
+// P = W_in[:, :C] G + b_in), organised so that the bilinear P taps come from LDS instead
+// of the vector-memory path.  Per sample the taps are 4 x 256 B; through global loads
+// every byte passes the CU's texture path (~64 B/clk), which bounds k_render_proj.  Rays
+// of neighbouring pixels sample neighbouring texels, so one workgroup renders a GROUP of
+// 8 consecutive rays at a time (one per wave) and stages the bounding box of all their
+// taps, read once from L2 by LDS-DMA, in LDS.
+//
+// Workgroup = 8 waves, one workgroup per CU.  Step n: wave w renders ray 8 G_n + w.
+//   item 0    ray pass of the wave's NEXT ray (geometry, taps, colours -> LDS records,
+//             tap bounding box -> LDS), the DINO head of the previous group (below),
+//             then item 0 of the current ray
+//   barrier X union of the next group's boxes; if it fits the tile buffer, every wave
+//             issues its share of the LDS-DMA of those P texels (else the group goes to
+//             the overflow list and the fallback kernel renders it)
+//   items 1.. of the current ray (taps from the current tile buffer), ray epilogue:
+//             depth / colour stored, the composited hidden sum_k w_k relu(h_k) -> LDS
+//   vmcnt(0), barrier Y
+// Blend as MFMA: hidden[h][j] = sum_{tap q, sample s} P_q(s)[h] * Wb[(s, q)][j] with the
+// block-diagonal bilinear weights Wb[(s, q)][j] = w_q(j) [s == j]; A (P taps) is read with
+// ds_read_b64_tr_b16 (lane 4q + p of a 16-lane group addresses tap q of the group's
+// sample, columns 4p..4p+3; lane i receives hidden 16 t + i of the 4 taps).  Per 16-sample
+// item: 2 K-chunks of 8 samples x 8 hidden tiles = 16 MFMA 16x16x32, no blend VALU.
+// Then as k_render_proj: + W_code . code (16 MFMA), ReLU, sigma (4 MFMA), softplus,
+// alpha, DPP transmittance scan, and hidden-space compositing (v_dot2 of the packed
+// hidden pairs with (w, 0) / (0, w)).  The output layer is linear, so
+//   dino = sum_k w_k (W h_k + b) = W (sum_k w_k h_k) + b sum_k w_k          (nerf.py:394)
+// and is applied per GROUP: hsum of the 8 rays as the B operand (8 of 16 columns),
+// D / 16 MFMA tiles spread over the waves.
+#include "sdhip_render.h"
+
+#define ST_WAVES 8
+#define ST_WG (64 * ST_WAVES)
+#define ST_TEX 288          // LDS bytes per staged texel: 256 B of P + 32 B pad
+#define ST_TEXQ 18          // 16-byte chunks per staged texel
+#define ST_MAXP 2           // K <= 128 (two samples per lane in the ray pass)
+
+// diagnostic ablation switches (timing experiments only; outputs are wrong when set)
+#ifndef ST_PIPE
+#define ST_PIPE 0           // 1: item i + 1's MLP beside item i's compositing (measured slower)
+#endif
+#ifndef ST_ABL_NOHEAD
+#define ST_ABL_NOHEAD 0
+#endif
+#ifndef ST_ABL_NORAY
+#define ST_ABL_NORAY 0
+#endif
+#ifndef ST_ABL_NODMA
+#define ST_ABL_NODMA 0
+#endif
+#ifndef ST_ABL_NOITEM
+#define ST_ABL_NOITEM 0
+#endif
+#ifndef ST_ABL_NOTR
+#define ST_ABL_NOTR 0
+#endif
+#ifndef ST_ABL_NOPE
+#define ST_ABL_NOPE 0
+#endif
+#ifndef ST_ABL_NOCODE
+#define ST_ABL_NOCODE 0
+#endif
+#ifndef ST_ABL_NOHC
+#define ST_ABL_NOHC 0
+#endif
+#ifndef ST_ABL_NOSIG
+#define ST_ABL_NOSIG 0
+#endif
+
+struct st_args {
+    sd_render_args a;
+    sd_head m;
+    int32_t *ovf;           // [0]: overflow count, [1 + i]: overflowed group index
+    int32_t ngroups;        // ceil(R / 8)
+    int32_t tile_bytes;     // bytes per tile buffer (multiple of 1024)
+};
+
+// LDS image (byte offsets)
+#define ST_L_PE 0                              // [2][8][64] x 16 B code A fragments
+#define ST_L_SIG (ST_L_PE + 16 * 64 * 16)      // [4][64] x 16 B sigma A fragments
+#define ST_L_BOX (ST_L_SIG + 4 * 64 * 16)      // [2][8 waves][2] u32 (min, max) packed
+#define ST_L_HS (ST_L_BOX + 2 * 8 * 8)         // [8 rays][128] 16-bit hidden sums
+#define ST_L_WS (ST_L_HS + 8 * 128 * 2)        // [8] f32 weight sums
+#define ST_L_REC (ST_L_WS + 8 * 4)             // records: [8 waves][2][K] x 40 B
+static_assert(ST_L_REC % 16 == 0, "record area alignment");
+
+__host__ __device__ constexpr int st_rec_bytes(int K) { return ST_WAVES * 2 * K * 40; }
+
+// packed u16x2 (x | y << 16) component-wise min / max
+__device__ __forceinline__ uint32_t st_min2(uint32_t a, uint32_t b) {
+    typedef __attribute__((ext_vector_type(2))) unsigned short u16x2;
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a),
+                                                                  __builtin_bit_cast(u16x2, b)));
+}
+__device__ __forceinline__ uint32_t st_max2(uint32_t a, uint32_t b) {
+    typedef __attribute__((ext_vector_type(2))) unsigned short u16x2;
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2, a),
+                                                                  __builtin_bit_cast(u16x2, b)));
+}
+__device__ __forceinline__ uint32_t st_wave_min2(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = st_min2(v, (uint32_t)__shfl_xor((int)v, o, 64));
+    return v;
+}
+__device__ __forceinline__ uint32_t st_wave_max2(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = st_max2(v, (uint32_t)__shfl_xor((int)v, o, 64));
+    return v;
+}
+
+// tile pitch (texels per staged row): pitch mod 8 in 2..6, so that the four taps
+// n, n + 1, n + pitch, n + pitch + 1 of a sample (288 B = 8 banks apart per texel) land
+// on four disjoint 8-bank groups of a transposed read
+__device__ __forceinline__ int st_pitch(int tw) {
+    const int r = tw & 7;
+    return tw + (r == 7 ? 3 : r == 0 ? 2 : r == 1 ? 1 : 0);
+}
+
+__device__ __forceinline__ void st_barrier_lds() {
+    // wave's LDS writes visible, then the workgroup barrier; vector-memory loads (and
+    // LDS-DMA) stay in flight across it
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+
+__device__ __forceinline__ uint2 st_tr(uint32_t addr) {
+    const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4 *)(uintptr_t)addr);
+    return __builtin_bit_cast(uint2, v);
+}
+
+template <int P>
+__global__ void __launch_bounds__(ST_WG) __attribute__((amdgpu_waves_per_eu(2)))
+k_render_tile(const st_args sa) {
+    typedef T16<P> Tr;
+    typedef typename Tr::Frag Frag;
+    typedef typename Tr::E E;
+    const sd_render_args &a = sa.a;
+    const sd_head &m = sa.m;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    {
+        const uint4 *pe = (const uint4 *)m.w_pe, *sg = (const uint4 *)m.w_sig;
+        uint4 *d = (uint4 *)lds;
+        for (int i = threadIdx.x; i < 16 * SD_WAVE; i += blockDim.x) d[ST_L_PE / 16 + i] = pe[i];
+        for (int i = threadIdx.x; i < 4 * SD_WAVE; i += blockDim.x) d[ST_L_SIG / 16 + i] = sg[i];
+    }
+    const Frag *lf = (const Frag *)lds;
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_void *)lds;  // LDS byte address of lds[0]
+
+    const int lane = threadIdx.x & 63, j = lane & 15, g = lane >> 4;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int K = a.K, nsub = K >> 4;
+    const int R = (int)a.R, rps = (int)a.rays_per_sb;
+    const int D = m.D, ndt = D >> 4;
+    const int Wf = a.Wf, Hf = a.Hf;
+    const uint32_t plane_bytes = (uint32_t)Hf * Wf * SD_DH * 2;
+
+    // records: SoA per (wave, buffer): q0 [K] x 16 B | q1 [K] x 16 B | c [K] x 8 B
+    //   q0 = {x0 | y0 << 15 | inv_f << 30 | invc << 31, (w00, w01), (w10, w11), r}
+    //   q1 = {x, y, z~, z}   c = {g, b}
+    const uint32_t rec_base = ST_L_REC + (uint32_t)wave * 2 * K * 40;
+    auto rq0 = [&](int buf) { return (uint4 *)(lds + rec_base + buf * K * 40); };
+    auto rq1 = [&](int buf) { return (f32x4 *)(lds + rec_base + buf * K * 40 + K * 16); };
+    auto rqc = [&](int buf) { return (float2 *)(lds + rec_base + buf * K * 40 + K * 32); };
+    const uint32_t tile0 = ST_L_REC + st_rec_bytes(K);
+    const int tcap = sa.tile_bytes / ST_TEX;
+
+    // XCD-aware group ranges (workgroups b, b + 8, ... share an XCD, speed only)
+    const int NG = sa.ngroups;
+    const int nx = (gridDim.x % 8 == 0) ? 8 : 1;
+    const int xcd = blockIdx.x % nx, lb = blockIdx.x / nx, nwg = gridDim.x / nx;
+    const int glo = (int)((int64_t)NG * xcd / nx), ghi = (int)((int64_t)NG * (xcd + 1) / nx);
+    const int gfirst = glo + lb;
+    const int nsteps = gfirst < ghi ? (ghi - gfirst + nwg - 1) / nwg : 0;
+    __syncthreads();
+    if (nsteps == 0) return;  // workgroup-uniform
+
+    const float zstep = (float)(1.0 / (double)K), zend = (float)(1.0 - 1.0 / (double)K);
+    const int64_t cplane = (int64_t)a.Hc * a.Wc * 4;
+
+    // ---- ray pass: lane = sample k = 64 p + lane --------------------------------------
+    auto load_ray_z = [&](int ray, float zq[2 * ST_MAXP]) {
+        float zo[ST_MAXP];
+        if (a.z) {
+            const float *zr = a.z + (int64_t)ray * K;
+#pragma unroll
+            for (int p = 0; p < ST_MAXP; ++p) zo[p] = zr[min(64 * p + lane, K - 1)];
+        } else {
+            sd_cfloat *rr = (sd_cfloat *)(a.rays + (int64_t)ray * a.ray_dim);
+            const float near = rr[6], far = rr[7];
+            const uint64_t base = a.z_offset + (uint64_t)ray * (uint64_t)K;
+            zo[1] = 0.f;
+#pragma unroll
+            for (int p = 0; p < ST_MAXP; ++p) {
+                if (64 * p >= K) break;  // wave-uniform: K <= 64 draws one sample per lane
+                const int k = min(64 * p + lane, K - 1);
+                zo[p] = sd_z_sample(near, far, K, k, sd_uniform(a.z_seed, base + k), zstep, zend,
+                                    a.z_lindisp);
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < ST_MAXP; ++p) {
+            float nx2 = __shfl_down(zo[p], 1, 64);
+            const float first_next = p + 1 < ST_MAXP
+                ? __builtin_bit_cast(float, __builtin_amdgcn_readlane(
+                      __builtin_bit_cast(int, zo[p + 1 < ST_MAXP ? p + 1 : p]), 0))
+                : zo[p];
+            if (lane == 63) nx2 = (p + 1 < ST_MAXP && 64 * (p + 1) < K) ? first_next : zo[p];
+            zq[2 * p] = zo[p];
+            zq[2 * p + 1] = nx2;
+        }
+    };
+    // the colour texel loads of sample k = lane are left in flight (cpend) and finished
+    // by ray_col at the end of the item that ran the pass
+    ColPend cpend;
+    uint32_t cp_x0y0 = 0;
+    auto ray_pass = [&](int ray, int buf, int slot) {
+        uint32_t bmin = 0xffffffffu, bmax = 0u;
+        if (ray < R) {
+            const int sbi = (int)((unsigned)ray / (unsigned)rps);
+            float zq[2 * ST_MAXP];
+            load_ray_z(ray, zq);
+            sd_cfloat *rr = (sd_cfloat *)(a.rays + (int64_t)ray * a.ray_dim);
+            const float ox = rr[0], oy = rr[1], oz = rr[2], dx = rr[3], dy = rr[4], dz = rr[5];
+            uint4 *r0 = rq0(buf);
+            f32x4 *r1 = rq1(buf);
+            float2 *rc = rqc(buf);
+#pragma unroll
+            for (int p = 0; p < ST_MAXP; ++p) {
+                const int k = 64 * p + lane;
+                if (64 * p < K && k < K) {
+                    const float z0 = zq[2 * p];
+                    const float px = ox + z0 * dx, py = oy + z0 * dy, pz = oz + z0 * dz;  // nerf.py:252
+                    const PointGeo geo = sd_point_geo<true>((sd_cfloat *)(a.cam_f + sbi * 21), px, py, pz,
+                                                            Wf, Hf);
+                    const uint32_t x0 = (uint32_t)geo.t.x0, y0 = (uint32_t)geo.t.y0;
+                    bool ic;
+                    const Taps tc = sd_color_taps((sd_cfloat *)(a.cam_c + sbi * 21), a.Wc, a.Hc, px, py,
+                                                  pz, ic);
+                    const uint32_t xy = x0 | (y0 << 15) | (geo.inv_f ? 1u << 30 : 0u) |
+                                        (ic ? 1u << 31 : 0u);
+                    const uint4 wp = sd_pack_w<P>(geo.t.w00, geo.t.w01, geo.t.w10, geo.t.w11);
+                    r1[k] = f32x4{geo.v[0], geo.v[1], geo.v[2], z0};
+                    if (p == 0) {
+                        sd_color_issue(a.img + (int64_t)sbi * cplane, tc, cpend);
+                        cp_x0y0 = xy;
+                        r0[k] = uint4{xy, wp.x, wp.y, 0u};  // colour word written by ray_col
+                    } else {
+                        float col[3];
+                        sd_sample_rgb(a.img + (int64_t)sbi * cplane, tc, col);
+                        r0[k] = uint4{xy, wp.x, wp.y, __builtin_bit_cast(uint32_t, col[0])};
+                        rc[k] = float2{col[1], col[2]};
+                    }
+                    const uint32_t lo = x0 | (y0 << 16);
+                    bmin = st_min2(bmin, lo);
+                    bmax = st_max2(bmax, lo + 0x00010001u);
+                }
+            }
+        }
+        bmin = st_wave_min2(bmin);
+        bmax = st_wave_max2(bmax);
+        if (lane == 0) *(uint2 *)(lds + ST_L_BOX + (slot * ST_WAVES + wave) * 8) = uint2{bmin, bmax};
+    };
+    auto ray_col = [&](int ray, int buf) {
+        if (ray < R && lane < K) {
+            float col[3];
+            sd_color_finish(cpend, col);
+            rq0(buf)[lane].w = __builtin_bit_cast(uint32_t, col[0]);
+            rqc(buf)[lane] = float2{col[1], col[2]};
+        }
+    };
+
+    // ---- per-step tile geometry (workgroup-uniform) -----------------------------------
+    struct Tile {
+        int bx0, by0, pitch, ok;
+    };
+    // union of the 8 wave boxes of slot; issues this wave's share of the LDS-DMA into
+    // tile buffer tb; returns the geometry (ok = 0: overflow, or no valid ray)
+    auto stage = [&](int slot, int tb, int grp, int sbi) {
+        const uint4 *bx = (const uint4 *)(lds + ST_L_BOX + slot * ST_WAVES * 8);
+        uint32_t mn = 0xffffffffu, mx = 0u;
+#pragma unroll
+        for (int i = 0; i < ST_WAVES / 2; ++i) {
+            const uint4 v = bx[i];
+            mn = st_min2(mn, st_min2(v.x, v.z));
+            mx = st_max2(mx, st_max2(v.y, v.w));
+        }
+        mn = __builtin_amdgcn_readfirstlane(mn);
+        mx = __builtin_amdgcn_readfirstlane(mx);
+        Tile t;
+        t.bx0 = (int)(mn & 0xffffu);
+        t.by0 = (int)(mn >> 16);
+        const int tw = (int)(mx & 0xffffu) - t.bx0 + 1, th = (int)(mx >> 16) - t.by0 + 1;
+        t.pitch = tw > 0 ? st_pitch(tw) : 1;
+        const int ntex = th * t.pitch;
+        const int nchunk = ntex * ST_TEXQ;
+        const int ninstr = (nchunk + 63) >> 6;
+        t.ok = (mn != 0xffffffffu) && tw > 0 && th > 0 && ninstr * 1024 <= sa.tile_bytes;
+        if (mn == 0xffffffffu) return t;  // no valid ray in the group
+        if (!t.ok) {
+            if (wave == 0 && lane == 0) {
+                const int i = atomicAdd(sa.ovf, 1);
+                sa.ovf[1 + i] = grp;
+            }
+            return t;
+        }
+        const uint8_t *plane = (const uint8_t *)a.grid + (int64_t)sbi * plane_bytes;
+        const float inv_pitch = 1.f / (float)t.pitch;
+        const uint32_t dst0 = tile0 + (uint32_t)tb * (uint32_t)sa.tile_bytes;
+        for (int i = wave; i < ninstr; i += ST_WAVES) {
+            const uint32_t ci = (uint32_t)i * 64u + (uint32_t)lane;
+            const uint32_t n = __umulhi(ci, 238609295u);  // ci / 18
+            const uint32_t part = ci - 18u * n;
+            const int ty = (int)(((float)n + 0.5f) * inv_pitch);
+            const int tx = (int)n - ty * t.pitch;
+            const int sx = min(max(t.bx0 + tx, 0), Wf - 1), sy = min(max(t.by0 + ty, 0), Hf - 1);
+            const uint8_t *src = plane + ((int64_t)sy * Wf + sx) * 256 + (part < 16u ? part : 0u) * 16u;
+            if (!ST_ABL_NODMA) __builtin_amdgcn_global_load_lds((const void *)src,
+                                             (lds_void *)(lds + dst0 + (uint32_t)i * 1024u), 16, 0, 0);
+        }
+        return t;
+    };
+
+    // ---- DINO head of one group (hsum of its 8 rays in LDS) ---------------------------
+    // W_dino fragments of the wave's first head tile (dt = wave), loaded one phase ahead
+    Frag Wh[4];
+    auto head_prefetch = [&]() {
+        if (wave < ndt) {
+            const Frag *wo = (const Frag *)m.w_out + (int64_t)wave * 4 * SD_WAVE + lane;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) Wh[s] = wo[s * SD_WAVE];
+        }
+    };
+    auto head = [&](int grp) {
+        if (wave >= ndt) return;
+        const int slot = j & 7;
+        Frag Bh[4];
+        const uint8_t *hs = lds + ST_L_HS + slot * 256;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const uint2 lo = *(const uint2 *)(hs + (32 * s + 4 * g) * 2);
+            const uint2 hi = *(const uint2 *)(hs + (32 * s + 16 + 4 * g) * 2);
+            Bh[s] = __builtin_bit_cast(Frag, uint4{lo.x, lo.y, hi.x, hi.y});
+        }
+        const float ws = *(const float *)(lds + ST_L_WS + slot * 4);
+        const int ray = 8 * grp + j;
+        const bool store = j < 8 && ray < R;
+        for (int dt = wave; dt < ndt; dt += ST_WAVES) {
+            const Frag *wo = (const Frag *)m.w_out + (int64_t)dt * 4 * SD_WAVE + lane;
+            f32x4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < 4; ++s) o = Tr::mma(dt == wave ? Wh[s] : wo[s * SD_WAVE], Bh[s], o);
+            // rows 4 g + r of tile dt = dims 16 dt + 4 g + r, column j = ray slot
+            const int dim = 16 * dt + 4 * g;
+            const f32x4 bd = *(const f32x4 *)(m.b_dino + dim);
+            f32x4 res;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) res[r] = o[r] + ws * bd[r];
+            if (store) *(f32x4 *)(a.dino + (int64_t)ray * a.ld_dino + dim) = res;
+        }
+    };
+
+    // per-lane constant part of the transposed-read addresses: tap q = (lane & 15) >> 2
+    // of a sample, columns 4 p .. 4 p + 3
+    const int tq = (lane & 15) >> 2, tp = lane & 3;
+    // B operand masks: lane (j, g) carries sample j's weights in K-chunk j >> 3 iff
+    // ((j & 7) >> 1) == g, at elements 4 (j & 1) .. + 3
+    const bool bsel = ((j & 7) >> 1) == g;
+    const bool bc0 = bsel && (j >> 3) == 0, bc1 = bsel && (j >> 3) == 1;
+    const bool br1 = (j & 1) != 0;
+    const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+
+    // ---- prologue: records + tile of step 0 -------------------------------------------
+    int grp = gfirst;
+    int ray = 8 * grp + wave;
+    int sbi = (int)((unsigned)min(8 * grp, R - 1) / (unsigned)rps);
+    ray_pass(ray, 0, 0);
+    ray_col(ray, 0);
+    st_barrier_lds();
+    Tile cur = stage(0, 0, grp, sbi);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    int prev_grp = -1, prev_ok = 0;
+    for (int n = 0; n < nsteps; ++n) {
+        const int buf = n & 1;
+        const bool has_next = n + 1 < nsteps;
+        const int ngrp = grp + nwg;
+        const int nray = 8 * ngrp + wave;
+        const int nsbi = has_next ? (int)((unsigned)min(8 * ngrp, R - 1) / (unsigned)rps) : 0;
+        const bool active = cur.ok && ray < R;
+        const uint32_t tileb = lds0 + tile0 + (uint32_t)buf * (uint32_t)sa.tile_bytes;
+        const int toff = (tq & 1) + (tq >> 1) * cur.pitch;
+        const uint32_t lane_off = (uint32_t)toff * ST_TEX + 8u * (uint32_t)tp;
+
+        float Tc = 1.f, dpart = 0.f, wpart = 0.f, cpart[3] = {0.f, 0.f, 0.f};
+        f32x4 hacc[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) hacc[t] = zero4;
+
+        // An item is split in two so that consecutive items overlap (software pipeline):
+        // A = records, taps, MFMA MLP, sigma, alpha, local transmittance scan;
+        // B = weights with the carried transmittance, compositing sums, per-sample outputs.
+        struct IState {
+            Frag X[4];
+            float alpha, excl, tmul, zk, col[3];
+            uint32_t flags;  // bit 0: outside the encoder frustum, bit 1: outside the render view
+        };
+        auto itemA = [&](int sub, IState &st) {
+            const int k = sub * 16 + j;
+            const uint4 q0 = rq0(buf)[k];
+            const f32x4 q1 = rq1(buf)[k];
+            const float2 cgb = rqc(buf)[k];
+            const float znext = k + 1 < K ? rq1(buf)[k + 1][3] : 0.f;
+            const uint32_t xy = q0.x;
+            const int x0 = (int)(xy & 0x7fffu), y0 = (int)((xy >> 15) & 0x7fffu);
+            st.flags = ((xy >> 30) & 1u) | ((xy >> 30) & 2u);
+            const float v[3] = {q1[0], q1[1], q1[2]};
+            st.zk = q1[3];
+            const float delta = k + 1 < K ? znext - st.zk : 1e10f;
+            st.col[0] = __builtin_bit_cast(float, q0.w);
+            st.col[1] = cgb.x;
+            st.col[2] = cgb.y;
+            // this lane's sample: LDS byte address of its tap (x0, y0)
+            const int nb = (int)tileb + ((y0 - cur.by0) * cur.pitch + (x0 - cur.bx0)) * ST_TEX;
+            uint32_t base[2][2];
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+                for (int r = 0; r < 2; ++r)
+                    base[c][r] = (uint32_t)__builtin_amdgcn_ds_bpermute((8 * c + 2 * g + r) << 2, nb) +
+                                 lane_off;
+            // block-diagonal weight fragments of the two K-chunks
+            const uint32_t w01 = q0.y, w23 = q0.z;
+            const uint4 b0 = {bc0 && !br1 ? w01 : 0u, bc0 && !br1 ? w23 : 0u,
+                              bc0 && br1 ? w01 : 0u, bc0 && br1 ? w23 : 0u};
+            const uint4 b1 = {bc1 && !br1 ? w01 : 0u, bc1 && !br1 ? w23 : 0u,
+                              bc1 && br1 ? w01 : 0u, bc1 && br1 ? w23 : 0u};
+            const Frag B0 = __builtin_bit_cast(Frag, b0), B1 = __builtin_bit_cast(Frag, b1);
+            f32x4 acc[8];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+#if ST_ABL_NOTR
+                const uint2 a00 = {base[0][0] + t, base[0][1]}, a01 = {base[1][0], base[1][1] + t};
+                const uint2 a10 = a01, a11 = a00;
+#else
+                const uint2 a00 = st_tr(base[0][0] + 32u * t), a01 = st_tr(base[0][1] + 32u * t);
+                const uint2 a10 = st_tr(base[1][0] + 32u * t), a11 = st_tr(base[1][1] + 32u * t);
+#endif
+                const Frag A0 = __builtin_bit_cast(Frag, uint4{a00.x, a00.y, a01.x, a01.y});
+                const Frag A1 = __builtin_bit_cast(Frag, uint4{a10.x, a10.y, a11.x, a11.y});
+                acc[t] = Tr::mma(A0, B0, zero4);
+                acc[t] = Tr::mma(A1, B1, acc[t]);
+            }
+            // positional-code columns
+            const int lo = sd_opaque0();
+            const Frag *lw = lf + lo;
+#pragma unroll
+            for (int pc = 0; pc < 2; ++pc) {
+#if ST_ABL_NOPE
+                Frag f;
+                for (int e = 0; e < 8; ++e) f[e] = (E)v[e % 3];
+#else
+                const Frag f = sd_code_frag<Frag, E>(v, pc, g);
+#endif
+#pragma unroll
+                for (int t = 0; t < 8; ++t)
+                    if (!ST_ABL_NOCODE || t == 0)
+                        acc[t] = Tr::mma(lw[ST_L_PE / 16 + (pc * 8 + t) * SD_WAVE + lane], f, acc[t]);
+            }
+#pragma unroll
+            for (int s2 = 0; s2 < 4; ++s2) {
+                const uint4 u = {sd_relu2(sd_pack2<E>(acc[2 * s2][0], acc[2 * s2][1])),
+                                 sd_relu2(sd_pack2<E>(acc[2 * s2][2], acc[2 * s2][3])),
+                                 sd_relu2(sd_pack2<E>(acc[2 * s2 + 1][0], acc[2 * s2 + 1][1])),
+                                 sd_relu2(sd_pack2<E>(acc[2 * s2 + 1][2], acc[2 * s2 + 1][3]))};
+                st.X[s2] = __builtin_bit_cast(Frag, u);
+            }
+#if ST_ABL_NOSIG
+            const float sigma = __builtin_bit_cast(float, __builtin_bit_cast(uint4, st.X[0]).x & 0x3fffffffu) + m.b_sigma;
+#else
+            f32x4 sg = zero4;
+#pragma unroll
+            for (int s2 = 0; s2 < 4; ++s2) sg = Tr::mma(lw[ST_L_SIG / 16 + s2 * SD_WAVE + lane], st.X[s2], sg);
+            const float sv = sg[0] + m.b_sigma;
+            const float sigma = sv > 20.f ? sv : __logf(1.f + __expf(sv));
+#endif
+            // alpha compositing (nerf.py:376-389)
+            float alpha = 1.f - __expf(-fabsf(delta) * fmaxf(sigma, 0.f));
+            if (a.hard_alpha_cap && k == K - 1) alpha = 1.f;
+            const float incl = sd_scan_mul16((1.f - alpha) + 1e-10f);
+            st.alpha = alpha;
+            st.excl = SD_DPP1(incl, 0x111);
+            st.tmul = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, incl), 15));
+        };
+        auto itemB = [&](int sub, const IState &st) {
+            const int k = sub * 16 + j;
+            const float w = st.alpha * (Tc * st.excl);
+            Tc *= st.tmul;
+            dpart += w * st.zk;
+            wpart += w;
+            cpart[0] += w * st.col[0];
+            cpart[1] += w * st.col[1];
+            cpart[2] += w * st.col[2];
+            // hidden-space compositing: hacc += w relu(h), two hidden per v_dot2
+            const uint32_t wl = sd_pack2<E>(w, 0.f), wh = sd_pack2<E>(0.f, w);
+#pragma unroll
+            for (int s2 = 0; s2 < 4; ++s2) {
+                const uint4 u = __builtin_bit_cast(uint4, st.X[s2]);
+                const uint32_t d4[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int t = 2 * s2 + (q >> 1), r = 2 * (q & 1);
+                    if (ST_ABL_NOHC && (s2 | q)) continue;
+                    hacc[t][r] = Tr::dot2(d4[q], wl, hacc[t][r]);
+                    hacc[t][r + 1] = Tr::dot2(d4[q], wh, hacc[t][r + 1]);
+                }
+            }
+            const int64_t rk = (int64_t)ray * K;
+            if (g == 0) {
+                if (a.weights) (a.weights + rk)[k] = w;
+                if (a.alphas) (a.alphas + rk)[k] = st.alpha;
+                if (a.invalid_f) (a.invalid_f + rk)[k] = (st.flags & 1u) ? 1 : 0;
+                if (a.invalid) (a.invalid + rk)[k] = st.flags ? 1.f : 0.f;
+                if (a.rgb_samps) {
+                    float *rsp = a.rgb_samps + (rk + k) * 3;
+                    rsp[0] = st.col[0]; rsp[1] = st.col[1]; rsp[2] = st.col[2];
+                }
+            }
+        };
+
+        // item 0 with the next ray's pass and the previous group's head
+        if (prev_ok && !ST_ABL_NOHEAD) head_prefetch();
+        if (has_next && (!ST_ABL_NORAY || n == 0)) ray_pass(nray, buf ^ 1, buf ^ 1);
+        if (prev_ok && !ST_ABL_NOHEAD) head(prev_grp);
+        IState s0, s1;
+        if (active && !ST_ABL_NOITEM) itemA(0, s0);
+        if (has_next && (!ST_ABL_NORAY || n == 0)) ray_col(nray, buf ^ 1);
+        st_barrier_lds();  // X: next boxes visible; the head has read the hsum area
+        Tile nxt = {0, 0, 1, 0};
+        if (has_next) nxt = stage(buf ^ 1, buf ^ 1, ngrp, nsbi);
+#if ST_PIPE
+        if (active && !ST_ABL_NOITEM) {
+            // items 1 .. nsub-1, item i + 1's A beside item i's B (ping-pong states)
+            int sub = 1;
+            for (; sub + 1 < nsub; sub += 2) {
+                itemA(sub, s1);
+                itemB(sub - 1, s0);
+                itemA(sub + 1, s0);
+                itemB(sub, s1);
+            }
+            if (sub < nsub) {
+                itemA(sub, s1);
+                itemB(sub - 1, s0);
+                itemB(sub, s1);
+            } else {
+                itemB(sub - 1, s0);
+            }
+        }
+#else
+        if (active && !ST_ABL_NOITEM) {
+            itemB(0, s0);
+            for (int sub = 1; sub < nsub; ++sub) {
+                itemA(sub, s1);
+                itemB(sub, s1);
+            }
+        }
+#endif
+        if (active) {
+            // ray epilogue: sums over the 16 sample lanes of every row
+            const float dsum = sd_rowsum16(dpart), wsum = sd_rowsum16(wpart);
+            const float c0s = sd_rowsum16(cpart[0]), c1s = sd_rowsum16(cpart[1]),
+                        c2s = sd_rowsum16(cpart[2]);
+            uint8_t *hs = lds + ST_L_HS + wave * 256;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                f32x4 vsum;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) vsum[r] = sd_rowsum16(hacc[t][r]);
+                // hidden 16 t + 4 g + r
+                if (j == 0)
+                    *(uint2 *)(hs + (16 * t + 4 * g) * 2) =
+                        uint2{sd_pack2<E>(vsum[0], vsum[1]), sd_pack2<E>(vsum[2], vsum[3])};
+            }
+            if (lane == 0) {
+                *(float *)(lds + ST_L_WS + wave * 4) = wsum;
+                a.depth[(int64_t)ray * a.ld_depth] = dsum;
+                float *rp = a.rgb + (int64_t)ray * a.ld_rgb;
+                rp[0] = c0s; rp[1] = c1s; rp[2] = c2s;
+            }
+        }
+        prev_grp = grp;
+        prev_ok = cur.ok;
+        grp = ngrp;
+        ray = nray;
+        sbi = nsbi;
+        cur = nxt;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed
+        st_barrier_lds();  // Y: next tile complete; hsum of this group written
+    }
+    if (prev_ok) {
+        head_prefetch();
+        head(prev_grp);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+static int sd_check_last(const char *what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        sd_set_error(hipGetErrorString(e));
+        (void)what;
+        return -2;
+    }
+    return 0;
+}
+
+static int st_tile_bytes(int K) {
+    const int fixed = ST_L_REC + st_rec_bytes(K);
+    const int avail = 160 * 1024 - fixed;
+    return ((avail / 2) / 1024) * 1024;
+}
+
+// Can the tile kernel take this render?  (colour in exactly one render view, batches of
+// whole groups, K <= 128, room for one tile buffer pair.)
+extern "C" int sd_render_tile_ok(const sd_render_args *a, const sd_head *m) {
+    return a->nv == 1 && a->K % 16 == 0 && a->K <= 128 && a->rays_per_sb % 8 == 0 &&
+           m->D % 16 == 0 && m->D <= 512 && a->Wf < 32768 && a->Hf < 32768 &&
+           st_tile_bytes(a->K) >= 16 * 1024;
+}
+
+// Launch; ovf: device int32 [1 + ceil(R/8)] zeroed at [0] by this call.
+extern "C" int sd_render_tile_launch(const sd_render_args *a, const sd_head *m, int32_t *ovf,
+                                     void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    st_args sa;
+    sa.a = *a;
+    sa.m = *m;
+    sa.ovf = ovf;
+    sa.ngroups = (int)((a->R + 7) / 8);
+    sa.tile_bytes = st_tile_bytes(a->K);
+    const int lds_bytes = ST_L_REC + st_rec_bytes(a->K) + 2 * sa.tile_bytes;
+    if (hipMemsetAsync(ovf, 0, sizeof(int32_t), s) != hipSuccess) {
+        sd_set_error("sd_render_proj: overflow counter reset failed");
+        return -2;
+    }
+    int ncu = 0, dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+        ncu = 256;
+    if (m->dtype == SD_F16) {
+        (void)hipFuncSetAttribute((const void *)k_render_tile<SD_F16>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+        hipLaunchKernelGGL(k_render_tile<SD_F16>, dim3((unsigned)ncu), dim3(ST_WG), lds_bytes, s, sa);
+    } else {
+        (void)hipFuncSetAttribute((const void *)k_render_tile<SD_BF16>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+        hipLaunchKernelGGL(k_render_tile<SD_BF16>, dim3((unsigned)ncu), dim3(ST_WG), lds_bytes, s, sa);
+    }
+    return sd_check_last("sd_render_proj (tile kernel)");
+}

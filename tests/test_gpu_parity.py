@@ -191,17 +191,12 @@ def test_projected_grid_vs_dense_projection(precision):
     b_out = torch.randn(65, generator=g) * 0.1
     dt = _lib.SD_BF16 if precision == "bf16" else _lib.SD_F16
     pk = PackedMLP(W_in.to(DEV), b_in.to(DEV), W_out.to(DEV), b_out.to(DEV), dt)
-    P2 = _lib.project_grid(grid.to(DEV), pk.rec, dt).double().cpu()   # (2, Hf, Wf, 128, 2)
-    assert P2.shape == (2, Hf, Wf, 128, 2)
-    P = P2[..., 0]
+    P = _lib.project_grid(grid.to(DEV), pk.rec, dt).double().cpu()   # (2, Hf, Wf, 128)
+    assert P.shape == (2, Hf, Wf, 128)
     tdt = _lib.TORCH_DTYPE[dt]
     ref = torch.einsum("nc,bchw->bhwn", W_in[:, :C].to(tdt).double(), grid.to(tdt).double()) \
         + b_in.double()
     assert rel_l2(P, ref) < (4e-3 if precision == "bf16" else 1e-3)
-    # pair slot: the right neighbour's row (border: the last column pairs with itself),
-    # bit-identical to that pixel's own slot (waves overlap by one column, 31-pixel steps)
-    right = torch.clamp(torch.arange(Wf) + 1, max=Wf - 1)
-    assert torch.equal(P2[..., 1], P[:, :, right])
 
 
 def test_render_full_192x640x64_vs_reference_subsample():
