@@ -153,7 +153,7 @@ int sd_project_grid(const float *grid_nchw, int64_t B, int64_t Hf, int64_t Wf,
 /* Head of the projected render: code columns of W_in and the output layer, packed
  * for 16x16x32 MFMA (scenedino_amd/mlp_pack.py documents the fragment maps). */
 typedef struct sd_head {
-    const void *w_pe;      /* [2][8][64][8] code-column A fragments, dtype           */
+    const void *w_pe;      /* [8][64][8] ++ [8][64][4] code-column A fragments, dtype */
     const void *w_sig;     /* [4][64][8]    W_out row 0 (sigma) A fragments, dtype    */
     const void *w_out;     /* [D/16][4][64][8] W_out rows 1..D A fragments, dtype     */
     const float *b_dino;   /* b_out[1:1+D]                                            */

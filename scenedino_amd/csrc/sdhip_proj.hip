@@ -25,6 +25,7 @@
 // Pipelining: the z values of item i+2 and the P-tap loads of item i+1 are in flight
 // while item i computes.
 #include "sdhip_render.h"
+#include <stdlib.h>
 
 // diagnostic ablation switches (timing experiments only; outputs are wrong when set)
 #ifndef SD_ABL_NORAYPASS
@@ -193,7 +194,8 @@ __device__ __forceinline__ PRaw sd_pload(const PItem &it, int q) {
 // LDS image of the render kernel: [code 2][8][64] | [sigma 4][64] | [dino D/16][4][64]
 // (16 B per lane entry), then per wave SD_RECBUF x K sample records.
 #define SD_LDS_PE 0
-#define SD_LDS_SIG (SD_LDS_PE + 16 * SD_WAVE)
+#define SD_LDS_PE1 (SD_LDS_PE + 8 * SD_WAVE)   // 16x16x16 code fragments (8 B per lane entry)
+#define SD_LDS_SIG (SD_LDS_PE + 12 * SD_WAVE)
 #define SD_LDS_OUT (SD_LDS_SIG + 4 * SD_WAVE)
 
 // wave-uniform cursor with the wave's ray ordinal n (selects the record buffer)
@@ -206,13 +208,14 @@ __global__ void __launch_bounds__(SD_RWG) __attribute__((amdgpu_waves_per_eu(SD_
 k_render_proj(const sd_render_args a, const sd_head m, const int32_t *__restrict__ list) {
     typedef T16<P> Tr;
     typedef typename Tr::Frag Frag;
+    typedef typename Tr::Frag4 Frag4;
     typedef typename Tr::E E;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     {
         uint4 *d = (uint4 *)lds;
         const uint4 *pe = (const uint4 *)m.w_pe, *sg = (const uint4 *)m.w_sig,
                     *wo = (const uint4 *)m.w_out;
-        for (int i = threadIdx.x; i < 16 * SD_WAVE; i += blockDim.x) d[SD_LDS_PE + i] = pe[i];
+        for (int i = threadIdx.x; i < 12 * SD_WAVE; i += blockDim.x) d[SD_LDS_PE + i] = pe[i];
         for (int i = threadIdx.x; i < 4 * SD_WAVE; i += blockDim.x) d[SD_LDS_SIG + i] = sg[i];
         for (int i = threadIdx.x; i < NDT * 4 * SD_WAVE; i += blockDim.x) d[SD_LDS_OUT + i] = wo[i];
         __syncthreads();
@@ -477,17 +480,21 @@ k_render_proj(const sd_render_args a, const sd_head m, const int32_t *__restrict
         SD_PCHUNK(r3, 3)
 #undef SD_PCHUNK
         // positional-code columns
-#pragma unroll
-        for (int pc = 0; pc < 2; ++pc) {
+        {
+            Frag f0;
+            Frag4 f1;
 #if SD_ABL_NOPE
-            Frag f;
-            for (int e = 0; e < 8; ++e) f[e] = (E)cur.v[e % 3];
+            for (int e = 0; e < 8; ++e) f0[e] = (E)cur.v[e % 3];
+            f1 = __builtin_bit_cast(Frag4, uint2{__builtin_bit_cast(uint32_t, cur.v[0]), 0u});
 #else
-            const Frag f = sd_code_frag<Frag, E>(cur.v, pc, g);
+            sd_code_frags<Frag, Frag4, E>(cur.v, g, f0, f1);
 #endif
+            const Frag4 *lw1 = (const Frag4 *)(lds + SD_LDS_PE1 * 16) + lo;
+            // all 16x16x32 steps first, then the 16x16x16 ones (see sdhip_tile.hip)
 #pragma unroll
-            for (int t = 0; t < 8; ++t)
-                acc[t] = Tr::mma(lw[SD_LDS_PE + (pc * 8 + t) * SD_WAVE + lane], f, acc[t]);
+            for (int t = 0; t < 8; ++t) acc[t] = Tr::mma(lw[SD_LDS_PE + t * SD_WAVE + lane], f0, acc[t]);
+#pragma unroll
+            for (int t = 0; t < 8; ++t) acc[t] = Tr::mma16(lw1[t * SD_WAVE + lane], f1, acc[t]);
         }
         // 16-bit operand fragments (accumulator-as-operand), ReLU on the packed values
         Frag X[4];
@@ -808,7 +815,8 @@ extern "C" int sd_render_proj(const sd_render_args *args, const sd_head *m, void
     if (!a.ld_rgb) a.ld_rgb = 3 * a.nv;
     if (a.R == 0) return 0;
     hipStream_t s = (hipStream_t)stream;
-    if (sd_render_tile_ok(&a, m)) {
+    static const bool no_tile = getenv("SDHIP_NO_TILE") != nullptr;  // diagnostic A/B switch
+    if (!no_tile && sd_render_tile_ok(&a, m)) {
         // LDS-staged tile kernel (sdhip_tile.hip); groups whose tap box does not fit a tile
         // buffer are listed and rendered by the per-ray kernel behind it
         int32_t *ovf = (int32_t *)((uint8_t *)a.work + sd_hc_bytes(a.R, m->D));

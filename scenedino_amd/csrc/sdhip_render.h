@@ -1,6 +1,9 @@
 // sdhip_render.h -- device helpers shared by the gfx950 projected-grid render kernels
 // (sdhip_proj.hip: per-ray global gather; sdhip_tile.hip: LDS-staged tap tiles).
 #pragma once
+#ifndef SD_PE_DIRECT
+#define SD_PE_DIRECT 0
+#endif
 #include "sdhip_point.h"
 
 // 16-bit element traits.  Blend of the pair-interleaved projected grid (k_project):
@@ -8,9 +11,16 @@
 // sample is two v_dot2 per channel, row y0 . (w00, w01) + row y1 . (w10, w11), in f32
 // with one rounding to the 16-bit operand type.
 template <int P> struct T16;
+typedef __attribute__((ext_vector_type(4))) short sd_s16x4;
+typedef __attribute__((ext_vector_type(4))) _Float16 sd_f16x4;
+
 template <> struct T16<SD_F16> {
     typedef f16x8 Frag;
+    typedef sd_f16x4 Frag4;  // 16x16x16 operand (4 elements per lane)
     typedef _Float16 E;
+    static __device__ __forceinline__ f32x4 mma16(const Frag4 &a, const Frag4 &b, const f32x4 &c) {
+        return __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c, 0, 0, 0);
+    }
     static __device__ __forceinline__ f32x4 mma(const Frag &a, const Frag &b, const f32x4 &c) {
         return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
     }
@@ -32,7 +42,11 @@ template <> struct T16<SD_F16> {
 };
 template <> struct T16<SD_BF16> {
     typedef bf16x8 Frag;
+    typedef sd_s16x4 Frag4;  // 16x16x16 operand (4 elements per lane)
     typedef __bf16 E;
+    static __device__ __forceinline__ f32x4 mma16(const Frag4 &a, const Frag4 &b, const f32x4 &c) {
+        return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+    }
     typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
     static __device__ __forceinline__ f32x4 mma(const Frag &a, const Frag &b, const f32x4 &c) {
         return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
@@ -133,33 +147,48 @@ __device__ __forceinline__ float sd_sin_rev(float r) {
     return __builtin_amdgcn_sinf(__builtin_amdgcn_fractf(r));
 }
 
-// Positional-code fragment of chunk pc for lane group g (element e):
-//   G = 2 pc + (g >> 1), phase = g & 1 (0: sin, 1: cos = sin(x + pi/2))
-//   G < 3, e < 6 : sin(v[e % 3] * 1.5 * 2^(2G + (e >= 3)) + phase * pi/2)
-//   G = 0, e >= 6: raw inputs (g = 0: x, y; g = 1: z~, 0)
-//   otherwise don't-care: the packed code weights of those slots are zero
-//   (scenedino_amd/mlp_pack.py: proj_pe_col gives the W_in column of every slot).
-// The angle is formed in revolutions, fmaf(v * 4^(g >> 1), 1.5 * 2^k / 2 pi, phase / 4).
-template <typename Frag, typename E>
-__device__ __forceinline__ Frag sd_code_frag(const float v[3], int pc, int g) {
-    const float ph = (g & 1) ? 0.25f : 0.f;
-    const float ls = (g >> 1) ? 4.f : 1.f;
-    const float u[3] = {v[0] * ls, v[1] * ls, v[2] * ls};
-    float r[8];
+// Positional code (encoding_mode._z + PositionalEncoding, positional_encoding.py:13-80:
+// [x, y, z~, sin / cos(1.5 * 2^f * coord), f = 0..5]) of one sample, spread over its 4
+// lane groups: group c < 3 holds coordinate c's 12 sinusoids, group 3 the raw inputs.
+//   f0 (16x16x32 operand): c < 3: slot 2 f + ph = sin (ph 0) / cos (ph 1) at f = 0..3;
+//                          c = 3: x, y, z~, then zeros
+//   f1 (16x16x16 operand): c < 3: slot 2 (f - 4) + ph at f = 4, 5;  c = 3: zeros
+// (scenedino_amd/mlp_pack.py: proj_pe_col gives the W_in column of every slot).  f = 0 and
+// f = 3 are evaluated directly (angle in revolutions, one range reduction + v_sin_f32);
+// f = 1, 2, 4, 5 by double-angle steps sin 2a = 2 sin a cos a, cos 2a = 1 - 2 sin^2 a.
+template <typename Frag, typename Frag4, typename E>
+__device__ __forceinline__ void sd_code_frags(const float v[3], int g, Frag &f0, Frag4 &f1) {
+    const float u = g == 0 ? v[0] : (g == 1 ? v[1] : v[2]);
+    const float r0 = u * (float)(1.5 / 6.283185307179586);
+    const float r3 = u * (float)(12.0 / 6.283185307179586);
+    float s[6], c[6];
+    s[0] = sd_sin_rev(r0);
+    c[0] = sd_sin_rev(r0 + 0.25f);
+    s[3] = sd_sin_rev(r3);
+    c[3] = sd_sin_rev(r3 + 0.25f);
+#if SD_PE_DIRECT
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        if (e < 6) {
-            const float f = 1.5f * (float)(1 << (4 * pc + (e >= 3 ? 1 : 0))) * 0.15915494309189535f;
-            r[e] = sd_sin_rev(fmaf(u[e % 3], f, ph));
-        } else if (pc == 0) {
-            r[e] = (g >> 1) ? 0.f : (g == 0 ? v[e - 6] : (e == 6 ? v[2] : 0.f));
-        } else {
-            r[e] = 0.f;
-        }
+    for (int f = 0; f < 6; ++f) {
+        const float rf = u * (float)(1.5 / 6.283185307179586) * (float)(1 << f);
+        s[f] = sd_sin_rev(rf);
+        c[f] = sd_sin_rev(rf + 0.25f);
     }
-    const uint4 u4 = {sd_pack2<E>(r[0], r[1]), sd_pack2<E>(r[2], r[3]), sd_pack2<E>(r[4], r[5]),
-                      sd_pack2<E>(r[6], r[7])};
-    return __builtin_bit_cast(Frag, u4);
+#else
+#pragma unroll
+    for (int f = 0; f < 5; ++f) {
+        if (f == 2) continue;
+        s[f + 1] = (s[f] + s[f]) * c[f];
+        c[f + 1] = fmaf(-2.f * s[f], s[f], 1.f);
+    }
+#endif
+    const bool raw = g == 3;
+    const uint4 u4 = {raw ? sd_pack2<E>(v[0], v[1]) : sd_pack2<E>(s[0], c[0]),
+                      raw ? sd_pack2<E>(v[2], 0.f) : sd_pack2<E>(s[1], c[1]),
+                      raw ? 0u : sd_pack2<E>(s[2], c[2]),
+                      raw ? 0u : sd_pack2<E>(s[3], c[3])};
+    f0 = __builtin_bit_cast(Frag, u4);
+    const uint2 u2 = {raw ? 0u : sd_pack2<E>(s[4], c[4]), raw ? 0u : sd_pack2<E>(s[5], c[5])};
+    f1 = __builtin_bit_cast(Frag4, u2);
 }
 
 // ReLU of two packed 16-bit values (bf16 or f16): a negative value has the sign bit

@@ -79,8 +79,9 @@ struct st_args {
 };
 
 // LDS image (byte offsets)
-#define ST_L_PE 0                              // [2][8][64] x 16 B code A fragments
-#define ST_L_SIG (ST_L_PE + 16 * 64 * 16)      // [4][64] x 16 B sigma A fragments
+#define ST_L_PE 0                              // [8][64] x 16 B code A fragments (16x16x32)
+#define ST_L_PE1 (ST_L_PE + 8 * 64 * 16)      // [8][64] x 8 B code A fragments (16x16x16)
+#define ST_L_SIG (ST_L_PE1 + 8 * 64 * 8)      // [4][64] x 16 B sigma A fragments
 #define ST_L_BOX (ST_L_SIG + 4 * 64 * 16)      // [2][8 waves][2] u32 (min, max) packed
 #define ST_L_HS (ST_L_BOX + 2 * 8 * 8)         // [8 rays][128] 16-bit hidden sums
 #define ST_L_WS (ST_L_HS + 8 * 128 * 2)        // [8] f32 weight sums
@@ -138,6 +139,7 @@ __global__ void __launch_bounds__(ST_WG) __attribute__((amdgpu_waves_per_eu(2)))
 k_render_tile(const st_args sa) {
     typedef T16<P> Tr;
     typedef typename Tr::Frag Frag;
+    typedef typename Tr::Frag4 Frag4;
     typedef typename Tr::E E;
     const sd_render_args &a = sa.a;
     const sd_head &m = sa.m;
@@ -145,7 +147,7 @@ k_render_tile(const st_args sa) {
     {
         const uint4 *pe = (const uint4 *)m.w_pe, *sg = (const uint4 *)m.w_sig;
         uint4 *d = (uint4 *)lds;
-        for (int i = threadIdx.x; i < 16 * SD_WAVE; i += blockDim.x) d[ST_L_PE / 16 + i] = pe[i];
+        for (int i = threadIdx.x; i < 12 * SD_WAVE; i += blockDim.x) d[ST_L_PE / 16 + i] = pe[i];
         for (int i = threadIdx.x; i < 4 * SD_WAVE; i += blockDim.x) d[ST_L_SIG / 16 + i] = sg[i];
     }
     const Frag *lf = (const Frag *)lds;
@@ -459,18 +461,27 @@ k_render_tile(const st_args sa) {
             // positional-code columns
             const int lo = sd_opaque0();
             const Frag *lw = lf + lo;
-#pragma unroll
-            for (int pc = 0; pc < 2; ++pc) {
+            {
+                Frag f0;
+                Frag4 f1;
 #if ST_ABL_NOPE
-                Frag f;
-                for (int e = 0; e < 8; ++e) f[e] = (E)v[e % 3];
+                for (int e = 0; e < 8; ++e) f0[e] = (E)v[e % 3];
+                f1 = __builtin_bit_cast(Frag4, uint2{__builtin_bit_cast(uint32_t, v[0]), 0u});
 #else
-                const Frag f = sd_code_frag<Frag, E>(v, pc, g);
+                sd_code_frags<Frag, Frag4, E>(v, g, f0, f1);
 #endif
+                const Frag4 *lw1 = (const Frag4 *)(lds + ST_L_PE1) + lo;
+                // all 16x16x32 steps first, then the 16x16x16 ones: a 16x16x16 MFMA whose
+                // accumulator input is the result of the directly preceding 16x16x32 MFMA
+                // read a stale accumulator (hipcc 7.2, gfx950, VGPR-form accumulators)
 #pragma unroll
                 for (int t = 0; t < 8; ++t)
                     if (!ST_ABL_NOCODE || t == 0)
-                        acc[t] = Tr::mma(lw[ST_L_PE / 16 + (pc * 8 + t) * SD_WAVE + lane], f, acc[t]);
+                        acc[t] = Tr::mma(lw[ST_L_PE / 16 + t * SD_WAVE + lane], f0, acc[t]);
+#pragma unroll
+                for (int t = 0; t < 8; ++t)
+                    if (!ST_ABL_NOCODE || t == 0)
+                        acc[t] = Tr::mma16(lw1[t * SD_WAVE + lane], f1, acc[t]);
             }
 #pragma unroll
             for (int s2 = 0; s2 < 4; ++s2) {

@@ -17,7 +17,9 @@ is (r & 3) + 8 (r >> 2) + 4 h, column l & 31):
 Projected-grid head (16x16x32 MFMA, sdhip_proj.hip; lane l, sample/row i = l & 15,
 group g = l >> 4; hidden index of operand element e in k-step s:
 hid(s, g, e) = 32 s + 16 (e >> 2) + 4 g + (e & 3)):
-  code A      : w_pe[pc][t][l][e]  = W_in[16 t + (l & 15)][C + proj_pe_col(pc, g, e)]
+  code A      : w_pe = [chunk 0: t][l][e < 8] ++ [chunk 1: t][l][e < 4],
+                w_pe[pc][t][l][e] = W_in[16 t + (l & 15)][C + proj_pe_col(pc, g, e)]
+                (chunk 1 is the 16x16x16 operand: lane l holds k = 4 g + e)
   sigma A     : w_sig[s][l][e]     = W_out[0][hid(s, g, e)]
   dino A      : w_out16[dt][s][l][e] = W_out[1 + 16 dt + (l & 15)][hid(s, g, e)]
 """
@@ -49,16 +51,15 @@ def pe_slot_to_ref_col(pc: int, h: int, j: int) -> int:
 
 
 def proj_pe_col(pc: int, g: int, e: int) -> int:
-    """Code column (0..38) feeding element e of code chunk pc for lane group g in the
-    projected-grid kernel (sd_code_frag in sdhip_proj.hip); -1 = zero."""
-    G = 2 * pc + (g >> 1)
-    ph = g & 1
-    if G < 3 and e < 6:
-        fi = 2 * G + (1 if e >= 3 else 0)
-        return 3 + 3 * (2 * fi + ph) + e % 3
-    if G == 0 and e >= 6:
-        return {(0, 6): 0, (0, 7): 1, (1, 6): 2}.get((g, e), -1)
-    return -1
+    """Code column (0..38) feeding element e of code chunk pc (0: 16x16x32 operand, 8
+    slots; 1: 16x16x16 operand, 4 slots) for lane group g in the projected-grid kernels
+    (sd_code_frags, sdhip_render.h); -1 = zero.  Group c < 3 carries coordinate c's
+    sinusoids (slot 2 f' + ph, f = f' + 4 pc), group 3 the raw inputs.  Reference order
+    (positional_encoding.py:75-79): [x, y, z~] then sin / cos at frequency f for dims 0..2."""
+    if g == 3:
+        return e if (pc == 0 and e < 3) else -1
+    f, ph = 4 * pc + (e >> 1), e & 1
+    return 3 + 6 * f + 3 * ph + g
 
 
 @functools.lru_cache(maxsize=8)
@@ -66,15 +67,16 @@ def _proj_tables(C: int, D: int):
     lanes = np.arange(64)
     li, gg = lanes & 15, lanes >> 4
     e = np.arange(8)
-    pe_rows = np.zeros((2, 8, 64, 8), np.int64)
-    pe_cols = np.zeros((2, 8, 64, 8), np.int64)
-    for pc in range(2):
+    # chunk 0: [8 tiles][64 lanes][8 slots]; chunk 1: [8 tiles][64 lanes][4 slots], flattened
+    pe_rows, pe_cols = [], []
+    for pc, ne in ((0, 8), (1, 4)):
         for t in range(8):
             for l in range(64):
-                for k in range(8):
+                for k in range(ne):
                     c = proj_pe_col(pc, l >> 4, k)
-                    pe_rows[pc, t, l, k] = 16 * t + (l & 15)
-                    pe_cols[pc, t, l, k] = C + c if c >= 0 else -1
+                    pe_rows.append(16 * t + (l & 15))
+                    pe_cols.append(C + c if c >= 0 else -1)
+    pe_rows, pe_cols = np.array(pe_rows, np.int64), np.array(pe_cols, np.int64)
     s = np.arange(4)[:, None, None]
     hid = 32 * s + 16 * (e[None, None, :] >> 2) + 4 * gg[None, :, None] + (e[None, None, :] & 3)
     hid = np.broadcast_to(hid, (4, 64, 8))

@@ -29,6 +29,21 @@ def mfma_16x16x32(a_frag, b_frag, acc):
     return out
 
 
+def mfma_16x16x16(a_frag, b_frag, acc):
+    """a_frag, b_frag: (64, 4) -- A[i = l & 15][k = 4 (l >> 4) + e]; acc: (64, 4)."""
+    A = np.zeros((16, 16)); Bm = np.zeros((16, 16))
+    for l in range(64):
+        for e in range(4):
+            A[LI[l], 4 * GG[l] + e] = a_frag[l, e]
+            Bm[4 * GG[l] + e, LI[l]] = b_frag[l, e]
+    Dm = A @ Bm
+    out = acc.copy()
+    for l in range(64):
+        for r in range(4):
+            out[l, r] += Dm[4 * GG[l] + r, LI[l]]
+    return out
+
+
 def identity_frag(which):
     f = np.zeros((64, 8))
     for l in range(64):
@@ -38,17 +53,16 @@ def identity_frag(which):
 
 
 def code_frag(v, pc, g):
-    """sd_code_frag of sdhip_proj.hip for one sample (v = [x, y, z~])."""
-    out = np.zeros(8)
-    phase = np.float32(np.pi / 2) if g & 1 else 0.0
-    lscale = 4.0 if g >> 1 else 1.0
-    on = 2 * pc + (g >> 1) < 3
-    for e in range(8):
-        if e < 6:
-            f = 1.5 * (1 << (4 * pc + (1 if e >= 3 else 0))) * lscale
-            out[e] = np.sin(v[e % 3] * f + phase) if on else 0.0
-        elif pc == 0:
-            out[e] = 0.0 if g >> 1 else (v[e - 6] if g == 0 else (v[2] if e == 6 else 0.0))
+    """sd_code_frags of sdhip_render.h for one sample (v = [x, y, z~]), exact math:
+    chunk 0 has 8 slots, chunk 1 (the 16x16x16 operand) 4."""
+    out = np.zeros(8 if pc == 0 else 4)
+    if g == 3:
+        if pc == 0:
+            out[:3] = v
+        return out
+    for e in range(len(out)):
+        f, ph = 4 * pc + (e >> 1), e & 1
+        out[e] = np.sin(v[g] * 1.5 * 2.0 ** f + ph * np.pi / 2)
     return out
 
 
@@ -58,7 +72,7 @@ def ref_code(v):
     for i in range(6):
         for ph in range(2):
             for d in range(3):
-                c.append(np.sin(ph * np.float32(np.pi / 2) + v[d] * freqs[i]))
+                c.append(np.sin(ph * np.pi / 2 + v[d] * freqs[i]))
     return np.array(c)
 
 
@@ -69,7 +83,7 @@ def test_code_slots_cover_the_reference_code_once():
     for pc in range(2):
         for g in range(4):
             vals = code_frag(v, pc, g)
-            for e in range(8):
+            for e in range(len(vals)):
                 c = proj_pe_col(pc, g, e)
                 if c < 0:
                     assert vals[e] == 0
@@ -103,10 +117,13 @@ def test_projected_head_reproduces_dense_mlp(D):
         acc[2 * q] = mfma_16x16x32(I0, b, acc[2 * q])
         acc[2 * q + 1] = mfma_16x16x32(I1, b, acc[2 * q + 1])
     wpe = f(pk.w_pe16)
-    for pc in range(2):
-        b = np.array([code_frag(V[LI[l]], pc, GG[l]) for l in range(64)])
-        for t in range(8):
-            acc[t] = mfma_16x16x32(wpe[pc, t], b, acc[t])
+    wpe0 = wpe[:8 * 64 * 8].reshape(8, 64, 8)
+    wpe1 = wpe[8 * 64 * 8:].reshape(8, 64, 4)
+    b0 = np.array([code_frag(V[LI[l]], 0, GG[l]) for l in range(64)])
+    b1 = np.array([code_frag(V[LI[l]], 1, GG[l]) for l in range(64)])
+    for t in range(8):
+        acc[t] = mfma_16x16x32(wpe0[t], b0, acc[t])
+        acc[t] = mfma_16x16x16(wpe1[t], b1, acc[t])
     # dense reference with the same (bf16-rounded) code weights
     Wpe_bf = W_in[:, C:].to(torch.bfloat16).double().numpy()
     codes = np.array([ref_code(V[i]) for i in range(16)])
