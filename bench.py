@@ -6,15 +6,19 @@ Workload (BASELINE.json configs[1]): one 192x640 frame per 
 ResnetFC 295->128->65 (random kaiming init), lindisp stratified sampling, bf16.
 A "step" = ImageRaySampler.sample (sd_gen_rays) -> the frame's device-side state
 (sd_pack_image, sd_cam_records) -> projected grid P = W_in G + b_in (sd_project_grid) ->
-fused render (sd_render_proj: z sampling, points, projection, code, P gather, MFMA MLP,
-colours, alpha compositing) for one frame per GPU; for N>1 every rank renders its own
-frame (C3: frames sharded 1-per-GPU) and the rendered maps (depth, DINO, RGB) are
-all-gathered over RCCL.
-The ViT/DPT encoder is not part of the timed step (separate scope row).
+fused render (sd_render_proj: LDS-staged tile kernel + overflow fallback; z sampling,
+points, projection, code, P gather, MFMA MLP, colours, alpha compositing).  The C2 step is
+timed at two render poses, the encoder view and a 0.5 m lateral / 2 deg yaw offset view
+(SURVEY §8(d)); ``value`` is the slower of the two.  For N > 1 every rank renders its own
+frame (C3: frames sharded 1-per-GPU) straight into packed [depth | dino | rgb] rows that
+are all-gathered over RCCL (all_gather_into_tensor, overlapped with the next frame).
+The ViT/DPT encoder is not part of the timed step (separate scope row, ``end_to_end``).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--precision bf16|fp32]
-N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
-Rank 0 prints ONE JSON line.
+--gpus N > 1 without a torchrun environment launches N rank processes itself
+(torch.distributed.run, 127.0.0.1) before touching the GPU; under torchrun WORLD_SIZE must
+equal N.  --dist-backend gloo: ranks share one GPU and gather through host memory (a
+dry run of the multi-rank path on a one-GPU box).  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -75,13 +79,7 @@ def make_scene(frame_seed: int, device, precision="bf16", offset_pose=False):
     Ks = torch.tensor(KITTI_K, device=device).view(1, 1, 3, 3)
     poses = torch.eye(4, device=device).view(1, 1, 4, 4)
     net.encode(images, Ks, poses, ids_encoder=[0], ids_render=[0])
-    render_pose = poses.clone()
-    if offset_pose:  # 0.5 m lateral / 2 deg yaw render pose (SURVEY §8(d) second run)
-        import math
-        a = math.radians(2.0)
-        render_pose[0, 0, 0, 0] = math.cos(a); render_pose[0, 0, 0, 2] = math.sin(a)
-        render_pose[0, 0, 2, 0] = -math.sin(a); render_pose[0, 0, 2, 2] = math.cos(a)
-        render_pose[0, 0, 0, 3] = 0.5
+    render_pose = offset_render_pose(poses) if offset_pose else poses.clone()
     renderer = NeRFRenderer(n_coarse=K_SAMPLES, lindisp=True, hard_alpha_cap=False,
                             eval_batch_size=65536)
     wrapper = renderer.bind_parallel(net, gpus=None).eval()
@@ -170,9 +168,21 @@ class KernelTimer:
         return sum(ts) / len(ts) if ts else 0.0
 
 
-def cpu_baseline(budget_s: float = 20.0):
+def offset_render_pose(pose):
+    """The 0.5 m lateral / 2 deg yaw render pose of SURVEY §8(d) (second timed run)."""
+    import math
+    p = pose.clone()
+    a = math.radians(2.0)
+    p[..., 0, 0] = math.cos(a); p[..., 0, 2] = math.sin(a)
+    p[..., 2, 0] = -math.sin(a); p[..., 2, 2] = math.cos(a)
+    p[..., 0, 3] = 0.5
+    return p
+
+
+def cpu_baseline(budget_s: float = 20.0, offset_pose: bool = True):
     """Oracle (pure-PyTorch CPU restatement of the reference, fp32) on the host cores:
-    renders whole image rows of the same C2 frame until ~budget_s of CPU work."""
+    renders whole image rows of the same C2 frame (rays from the offset render pose, as
+    the reported GPU value) until ~budget_s of CPU work."""
     from oracle import render_oracle as O
 
     threads = int(os.environ.get("SD_CPU_THREADS", min(16, os.cpu_count() or 1)))
@@ -185,7 +195,8 @@ def cpu_baseline(budget_s: float = 20.0):
     head = ResnetFC(d_in=D_IN, d_out=1 + D_DINO, n_blocks=0, d_hidden=D_HIDDEN)
     Kn = torch.tensor(KITTI_K)
     pose = torch.eye(4)
-    rays = O.gen_rays(pose.view(1, 4, 4), Kn.view(1, 3, 3), H, W)
+    ray_pose = offset_render_pose(pose) if offset_pose else pose
+    rays = O.gen_rays(ray_pose.view(1, 4, 4), Kn.view(1, 3, 3), H, W)
     w2c = torch.inverse(pose).view(1, 4, 4)
     imgs = (images * 0.5 + 0.5)
     args = (grid, w2c, Kn.view(1, 3, 3), imgs, w2c.view(1, 1, 4, 4), Kn.view(1, 1, 3, 3),
@@ -215,25 +226,24 @@ def cpu_baseline(budget_s: float = 20.0):
     except OSError:
         pass
     return {"value": done_rays / dt, "unit": "rays/s", "cores": threads, "kind": "port",
-            "sample": f"{done_rays} rays ({row} of {H} rows) of the same 192x640x64 frame, "
+            "sample": f"{done_rays} rays ({row} of {H} rows) of the same 192x640x64 frame"
+                      f"{' (offset render pose)' if offset_pose else ''}, "
                       f"fp32 torch-CPU oracle restatement, {dt:.1f} s on {threads} threads "
                       f"({cpu}); encoder excluded"}
 
 
-def _traffic_from_profile(proj):
-    """HBM bytes per frame of the rendering kernels, from the committed rocprofv3 PMC
-    summary of this bench command (profiles/*_traffic.json, tools/traffic_json.py; PMC
-    counters cannot be read from inside the timed process)."""
+def _traffic_from_profile(pose):
+    """HBM bytes per frame of the rendering kernels at one render pose, from the committed
+    rocprofv3 PMC summary of this bench command (profiles/*_traffic_<pose>.json written by
+    tools/traffic_json.py; PMC counters cannot be read from inside the timed process)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_traffic_{pose}.json")))
     if not files:
         return None
     try:
         d = json.load(open(files[-1]))
-        ks = ("k_project", "k_render_proj") if proj else ("k_render<",)
-        tot = sum(d["kernels"][k]["hbm_bytes"] for k in ks)
-        if proj and "k_head_hc" in d["kernels"]:  # launched inside sd_render_proj (timed with it)
-            tot += d["kernels"]["k_head_hc"]["hbm_bytes"]
+        tot = sum(v["hbm_bytes"] for k, v in d["kernels"].items()
+                  if k in ("k_project", "k_render_tile", "k_render_proj", "k_head_hc"))
     except (KeyError, TypeError, ValueError):
         return None
     return tot, os.path.relpath(files[-1], ROOT) + " (rocprofv3 PMC, per frame)"
@@ -243,18 +253,21 @@ SEG_FLOPS_ALGO = 2 * (64 * 128 + 128 * 768) + 2 * (768 * 64 + 768 * 768 + 768 * 
 SEG_FLOPS_EXEC = 2 * (64 * 128 + 2 * 768 * 128 + 64 * 128 + 64 * 768)
 
 
-def main_c5(args, world, rank, local_rank, dist, device):
-    """C5 (BASELINE configs[4]): SSCBench voxel query, 256x256x32 voxels per GPU frame:
+def main_c5(args, world, rank, local_rank, dist, device, host_stage=False):
+    """C5 (BASELINE configs[4]): SSCBench voxel query, one 256x256x32 voxel grid per frame:
     voxel centres (sd_voxel_points, once per run as the reference does) -> per frame:
     grid packing (sd_pack_grid) + field query without colours (sd_field_query) + folded
     transform_expand / stego / k-means head with the alpha-weighted class pick
-    (sd_seg_query) + 3x3x3 density grow.  ViT-B/8-shaped 256x384x1280 grid, d_full 768."""
+    (sd_seg_query) + 3x3x3 density grow.  ViT-B/8-shaped 256x384x1280 grid, d_full 768.
+    N > 1: the frame's voxels are split into x-slabs [256 g / N, 256 (g+1) / N) (one halo
+    plane each side for the grow), every rank queries its slab and the sigma / class slabs
+    are all-gathered (strong scaling of one frame)."""
     from scenedino_amd import _lib, sscbench
     from scenedino_amd.models.backbones.dino import MlpDimReduction
     from scenedino_amd.downstream_head import SemanticHead
     global HF, WF
     HF, WF = 384, 1280
-    net, _, _, _, _, _ = make_scene(rank, device, args.precision)
+    net, _, _, _, _, _ = make_scene(0 if dist else rank, device, args.precision)
     torch.manual_seed(5)
     net.encoder.dim_reduction = MlpDimReduction(768, 64, 128).to(device).eval()
     net.downstream_head = SemanticHead(19, 19, 768, 64).to(device).eval()
@@ -265,9 +278,18 @@ def main_c5(args, world, rank, local_rank, dist, device):
     timer = KernelTimer()
     net.kernel_timer = timer
 
+    def predict(p):
+        sig, seg = net.predict_voxels(p.reshape(1, -1, 3), voxel_size=sscbench.VOXEL_SIZE)
+        return sig.reshape(-1), seg.reshape(-1)
+
     def step():
         net._grid_cache = None
-        return sscbench.query_voxels(net, pts, dims)
+        if not dist:
+            return sscbench.query_voxels(net, pts, dims)
+        sig, seg = sscbench.query_voxels_slab(predict, pts, dims, rank, world)
+        if host_stage:
+            return sscbench.gather_slabs(sig.cpu(), seg.cpu(), dims)
+        return sscbench.gather_slabs(sig, seg, dims)
 
     with torch.no_grad():
         for _ in range(args.warmup):
@@ -291,20 +313,24 @@ def main_c5(args, world, rank, local_rank, dist, device):
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed, seg_ms, field_ms = (float(v) for v in t)
     if rank == 0:
-        algo = n_vox * SEG_FLOPS_ALGO
-        exe = n_vox * SEG_FLOPS_EXEC
+        n_launch = n_vox  # voxels per k_seg_head launch (dist: this rank's slab + halo planes)
+        if dist:
+            x0, x1 = sscbench.slab_range(dims[0], rank, world)
+            n_launch = (min(x1 + 1, dims[0]) - max(x0 - 1, 0)) * dims[1] * dims[2]
+        algo = n_launch * SEG_FLOPS_ALGO
+        exe = n_launch * SEG_FLOPS_EXEC
         line = {
             "metric": "SSCBench voxel-grid query, voxels/sec (256x256x32 grid per frame)",
-            "value": world * n_vox * args.steps / elapsed, "unit": "voxels/s", "n_gpus": world,
+            "value": n_vox * args.steps / elapsed, "unit": "voxels/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": 1e3 * elapsed / args.steps, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
+            "scaling": "strong", "vs_baseline": None, "dtype": args.precision,
             "data": "synthetic (seeded image, N(0,1) 256x384x1280 grid, random-init ResnetFC / "
                     "MlpDimReduction / SemanticHead)",
             "config": {"workload": "C5: SSCBench 256x256x32 voxel query, ViT-B/8-shaped "
                                    "256x384x1280 grid, d_full 768, stego_kmeans, alpha-weighted "
                                    "class pick + grow", "voxels_per_frame": n_vox,
-                       "parallelism": f"frames{world}"},
+                       "parallelism": (f"xslab{world}+allgather" if world > 1 else "1 frame")},
             "roofline": {
                 "kernel": "k_seg_head (sd_seg_query)", "bound": "mfma",
                 "achieved": algo / (seg_ms * 1e-3) / 1e12, "peak": PEAK_TFLOPS["bf16"],
@@ -314,7 +340,7 @@ def main_c5(args, world, rank, local_rank, dist, device):
                 "executed_tflops": exe / (seg_ms * 1e-3) / 1e12,
                 "executed_frac": exe / (seg_ms * 1e-3) / 1e12 / PEAK_TFLOPS["bf16"],
                 "field_query_ms": field_ms,
-                "field_query_tflops": n_vox * mlp_flops_per_point() / (field_ms * 1e-3) / 1e12,
+                "field_query_tflops": n_launch * mlp_flops_per_point() / (field_ms * 1e-3) / 1e12,
             },
         }
         print(json.dumps(line), flush=True)
@@ -589,13 +615,174 @@ def main_train(args, world, rank, device):
         print(json.dumps(line), flush=True)
 
 
+def _launch_ranks(args) -> int:
+    """--gpus N outside torchrun: start N rank processes (this process has not touched
+    the GPU: device counting aside, nothing in bench.py initialises HIP before here) and
+    return their exit status."""
+    import socket
+    import subprocess
+    so = socket.socket()
+    so.bind(("127.0.0.1", 0))
+    port = so.getsockname()[1]
+    so.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def c2_pose_run(args, world, rank, device, dist, offset_pose, host_stage):
+    """Time the C2 step at one render pose (all ranks; max over ranks)."""
+    from scenedino_amd import distributed as sdd
+    net, renderer, wrapper, sampler, pose, Ks = make_scene(rank, device, args.precision,
+                                                          offset_pose)
+    R = H * W
+    gather = sdd.MapGather(R, 1 + D_DINO + 3, device, host_stage=host_stage) if dist else None
+    net.fused_mode = args.mode
+    timer = KernelTimer()
+    net.kernel_timer = timer
+
+    def step(i):
+        if gather is not None:  # frame f on rank f; maps rendered into the gather send slot
+            net.render_into = gather.send(i)
+        out = render_step(net, wrapper, sampler, pose, Ks)
+        if gather is not None:
+            gather.start(i)
+        return out
+
+    for i in range(args.warmup):
+        step(i)
+    if gather is not None:
+        gather.wait_all()
+    torch.cuda.synchronize()
+    if dist:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    timer.on = True
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    if gather is not None:
+        gather.wait_all()
+    torch.cuda.synchronize()
+    if dist:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    timer.on = False
+    render_ms, proj_ms = timer.mean_ms("render"), timer.mean_ms("project")
+    if dist:
+        t = torch.tensor([elapsed, render_ms, proj_ms], device=device, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed, render_ms, proj_ms = float(t[0]), float(t[1]), float(t[2])
+    proj = net._use_proj()
+    res = {"value": world * R * args.steps / elapsed, "ms_per_step": 1e3 * elapsed / args.steps,
+           "render_kernel_ms": render_ms, "project_kernel_ms": proj_ms, "proj": proj}
+    if gather is not None and rank == 0:
+        res["gathered_maps"] = list(gather.recv[0].shape)
+    net.render_into = None
+    del net, wrapper, renderer, gather
+    torch.cuda.empty_cache()
+    return res
+
+
+def main_c2(args, world, rank, device, dist, host_stage):
+    poses = {"identity": False, "offset": True}
+    if args.offset_pose:
+        poses = {"offset": True}
+    runs = {name: c2_pose_run(args, world, rank, device, dist, off, host_stage)
+            for name, off in poses.items()}
+    if rank != 0:
+        return
+    slow = min(runs, key=lambda k: runs[k]["value"])
+    r = runs[slow]
+    R = H * W
+    # SURVEY §8(d) algorithmic work: 92,160 FLOP per point (the reference MLP), over the
+    # kernels that turn the encoded grid into rendered maps
+    kern_ms = r["render_kernel_ms"] + r["project_kernel_ms"]
+    flops = R * K_SAMPLES * mlp_flops_per_point()
+    achieved = flops / (kern_ms * 1e-3) / 1e12
+    peak = PEAK_TFLOPS[args.precision]
+    if r["proj"]:
+        # what the matrix cores execute per 16-sample item (k_render_tile): blend 16 x
+        # 16x16x32, code 8 x 16x16x32 + 8 x 16x16x16, sigma 4 x 16x16x32; DINO head per
+        # 8-ray group D/16 x 4 x 16x16x32; plus the projection P = W G (k_project)
+        mac_item = 16 * 8192 + 8 * 8192 + 8 * 4096 + 4 * 8192
+        exec_flops = (HF * WF * 2 * C_GRID * D_HIDDEN
+                      + (R * K_SAMPLES // 16) * 2 * mac_item
+                      + (R // 8) * (D_DINO // 16) * 4 * 2 * 8192)
+    else:
+        exec_flops = flops
+    line = {
+        "metric": f"rendered rays/sec, KITTI-360 192x640x{K_SAMPLES}-sample frustum",
+        "value": r["value"],
+        "unit": "rays/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": r["ms_per_step"],
+        "ms_per_frame": r["ms_per_step"],
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.precision,
+        "data": "synthetic (seeded U[-1,1) image, N(0,1) 256x192x640 feature grid, "
+                "kaiming-init ResnetFC; no dataset/checkpoint offline)",
+        "config": {
+            "workload": ("C2: KITTI-360 192x640 frustum, 64 samples/ray, ViT-S/16-shaped "
+                         "256x192x640 DPT feature grid, ResnetFC 295-128-65, lindisp"
+                         if args.config == "c2" else
+                         "C4: KITTI-360 192x640 frustum, 128 samples/ray, DINOv2-B/14-shaped "
+                         "256x192x640 DPT feature grid, ResnetFC 295-128-385 (384-d field), "
+                         "lindisp") +
+                        f"; render poses {'/'.join(runs)}, value = the slower ({slow})",
+            "frames_per_gpu": 1, "rays_per_frame": R, "samples_per_ray": K_SAMPLES,
+            "grid": [C_GRID, HF, WF], "parallelism": f"frames{world}" +
+            (f"+{'rccl' if not host_stage else 'gloo-host'}_allgather" if world > 1 else ""),
+            "dist_world_size": world,
+        },
+        "poses": {k: {kk: v[kk] for kk in ("value", "ms_per_step", "render_kernel_ms",
+                                          "project_kernel_ms")} for k, v in runs.items()},
+        "roofline": {
+            "kernel": ("k_project + k_render_tile (+ k_render_proj overflow) "
+                       "(sd_project_grid + sd_render_proj)" if r["proj"] else
+                       "k_render (sd_render_fused)"),
+            "pose": slow,
+            "bound": "mfma",
+            "achieved": achieved,
+            "peak": peak,
+            "unit": "TFLOP/s",
+            "frac": achieved / peak,
+            "traffic": None,
+            "kernel_ms": kern_ms,
+            "render_kernel_ms": r["render_kernel_ms"],
+            "project_kernel_ms": r["project_kernel_ms"],
+            "algorithmic_flops_per_launch": flops,
+            "executed_mfma_flops_per_launch": exec_flops,
+            "executed_tflops": exec_flops / (kern_ms * 1e-3) / 1e12,
+        },
+    }
+    if "gathered_maps" in r:
+        line["config"]["gathered_maps"] = r["gathered_maps"]
+    tr = _traffic_from_profile(slow) if args.config == "c2" else None
+    if tr is not None:
+        line["roofline"]["traffic"] = tr[0]
+        line["roofline"]["traffic_source"] = tr[1]
+    if args.config == "c2" and not args.no_end_to_end and world == 1:
+        line["end_to_end"] = end_to_end(args, device, rank)
+    if not args.no_cpu_baseline and world == 1:
+        line["cpu_baseline"] = cpu_baseline(args.cpu_budget, offset_pose=(slow == "offset"))
+    print(json.dumps(line), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp16", "fp32"])
-    ap.add_argument("--offset-pose", action="store_true")
+    ap.add_argument("--offset-pose", action="store_true",
+                    help="c2/c4: time only the offset render pose (default: both poses)")
     ap.add_argument("--mode", default="proj", choices=["proj", "grid"],
                     help="16-bit render kernel: projected grid (default) or per-sample grid")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -611,145 +798,49 @@ def main():
     ap.add_argument("--no-end-to-end", action="store_true",
                     help="c2: skip the encode + render frame timing reported beside value")
     ap.add_argument("--models", default="", help="--config encode/vit: comma list of "
-                    "vit-s16, vit-b8 (default both)")
+                    "vit-s16, vit-b8, dinov2-b14 (default all)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: ranks share GPU 0 and exchange through host memory (dry run)")
     args = ap.parse_args()
     global K_SAMPLES, D_DINO
     if args.config == "c4":
         K_SAMPLES, D_DINO = 128, 384
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     dist = world > 1
+    host_stage = dist and args.dist_backend == "gloo"
+    dev_index = local_rank
+    if host_stage:  # dry run: every rank on one shared GPU
+        dev_index = local_rank % max(torch.cuda.device_count(), 1)
     if dist:
         import torch.distributed as tdist
-        torch.cuda.set_device(local_rank)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    device = torch.device("cuda", local_rank)
+        torch.cuda.set_device(dev_index)
+        if host_stage:
+            tdist.init_process_group("gloo")
+        else:
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        if tdist.get_world_size() != args.gpus:
+            raise SystemExit("bench.py: process-group size differs from --gpus")
+    device = torch.device("cuda", dev_index)
 
     from scenedino_amd import _lib
     _lib.load()
-    if args.config in ("c5", "vit", "encode", "train"):
-        if args.config == "train":
-            main_train(args, world, rank, device)
-        elif args.config == "c5":
-            main_c5(args, world, rank, local_rank, dist, device)
-        elif args.config == "vit":
-            main_vit(args, world, rank, device)
-        else:
-            main_encode(args, world, rank, device)
-        if dist:
-            tdist.barrier()
-            tdist.destroy_process_group()
-        return
-    net, renderer, wrapper, sampler, pose, Ks = make_scene(rank, device, args.precision,
-                                                          args.offset_pose)
-    R = H * W
-    gather_bufs = None
-    if dist:
-        from scenedino_amd import distributed as sdd
-        gather_bufs = [torch.empty(R, 1 + D_DINO + 3, device=device) for _ in range(world)]
-
-    net.fused_mode = args.mode
-    timer = KernelTimer()
-    net.kernel_timer = timer
-
-    def step():
-        out = render_step(net, wrapper, sampler, pose, Ks)
-        if dist:  # frame f on rank f; one RCCL all-gather of the packed rendered maps
-            sdd.gather_maps(sdd.pack_maps(out["coarse"]), out=gather_bufs)
-        return out
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if dist:
-        tdist.barrier()
-    torch.cuda.synchronize()
-    timer.on = True
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if dist:
-        tdist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    render_ms, proj_ms = timer.mean_ms("render"), timer.mean_ms("project")
-    if dist:
-        t = torch.tensor([elapsed, render_ms, proj_ms], device=device, dtype=torch.float64)
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        elapsed, render_ms, proj_ms = float(t[0]), float(t[1]), float(t[2])
-
-    if rank == 0:
-        total_rays = world * R * args.steps
-        ms_per_step = 1e3 * elapsed / args.steps
-        # SURVEY §8(d) algorithmic work: 92,160 FLOP per point (the reference MLP),
-        # over the kernels that turn the encoded grid into rendered maps
-        proj = net._use_proj()
-        kern_ms = render_ms + proj_ms
-        flops = R * K_SAMPLES * mlp_flops_per_point()
-        achieved = flops / (kern_ms * 1e-3) / 1e12
-        peak = PEAK_TFLOPS[args.precision]
-        if proj:  # what the matrix cores actually execute (P = W G projection + code/head)
-            hc = _lib.render_proj_work_bytes(R, D_DINO) > 0  # head applied per ray
-            exec_flops = (HF * WF * 2 * C_GRID * D_HIDDEN
-                          + R * K_SAMPLES * 2 * (39 * D_HIDDEN + D_HIDDEN * (1 + (0 if hc else D_DINO)))
-                          + (R * 2 * D_HIDDEN * D_DINO if hc else 0))
-        else:
-            exec_flops = flops
-        line = {
-            "metric": f"rendered rays/sec, KITTI-360 192x640x{K_SAMPLES}-sample frustum",
-            "value": total_rays / elapsed,
-            "unit": "rays/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": ms_per_step,
-            "ms_per_frame": ms_per_step,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": args.precision,
-            "data": "synthetic (seeded U[-1,1) image, N(0,1) 256x192x640 feature grid, "
-                    "kaiming-init ResnetFC; no dataset/checkpoint offline)",
-            "config": {
-                "workload": ("C2: KITTI-360 192x640 frustum, 64 samples/ray, ViT-S/16-shaped "
-                             "256x192x640 DPT feature grid, ResnetFC 295-128-65, lindisp"
-                             if args.config == "c2" else
-                             "C4: KITTI-360 192x640 frustum, 128 samples/ray, DINOv2-B/14-shaped "
-                             "256x192x640 DPT feature grid, ResnetFC 295-128-385 (384-d field), "
-                             "lindisp") + (", offset render pose" if args.offset_pose else ""),
-                "frames_per_gpu": 1, "rays_per_frame": R, "samples_per_ray": K_SAMPLES,
-                "grid": [C_GRID, HF, WF], "parallelism": f"frames{world}" +
-                ("+rccl_allgather" if world > 1 else ""),
-            },
-            "roofline": {
-                "kernel": ("k_project + k_render_proj (sd_project_grid + sd_render_proj)"
-                           if proj else "k_render (sd_render_fused)"),
-                "bound": "mfma",
-                "achieved": achieved,
-                "peak": peak,
-                "unit": "TFLOP/s",
-                "frac": achieved / peak,
-                "traffic": None,
-                "kernel_ms": kern_ms,
-                "render_kernel_ms": render_ms,
-                "project_kernel_ms": proj_ms,
-                "algorithmic_flops_per_launch": flops,
-                "executed_mfma_flops_per_launch": exec_flops,
-                "executed_tflops": exec_flops / (kern_ms * 1e-3) / 1e12,
-            },
-        }
-        tr = _traffic_from_profile(proj) if args.config == "c2" else None
-        if tr is not None:
-            line["roofline"]["traffic"] = tr[0]
-            line["roofline"]["traffic_source"] = tr[1]
-        if args.config == "c2" and not args.no_end_to_end and world == 1:
-            line["end_to_end"] = end_to_end(args, device, rank)
-        if not args.no_cpu_baseline and world == 1:
-            line["cpu_baseline"] = cpu_baseline(args.cpu_budget)
-        print(json.dumps(line), flush=True)
+    if args.config == "train":
+        main_train(args, world, rank, device)
+    elif args.config == "c5":
+        main_c5(args, world, rank, local_rank, dist, device, host_stage)
+    elif args.config == "vit":
+        main_vit(args, world, rank, device)
+    elif args.config == "encode":
+        main_encode(args, world, rank, device)
+    else:
+        main_c2(args, world, rank, device, dist, host_stage)
     if dist:
         tdist.barrier()
         tdist.destroy_process_group()

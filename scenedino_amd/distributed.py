@@ -2,9 +2,15 @@
 
 Frames are independent units: frame f renders on rank f % world (C3, 1 frame per GPU)
 with no data-path collective; the only exchange is one all-gather of the rendered
-maps (depth, DINO, colour) so every rank (or rank 0) holds the full batch.  Within a
+maps (depth, DINO, colour) so every rank (or rank 0) holds the full batch.  The render
+kernel writes its maps straight into packed [depth | dino | rgb] rows (BTSNet.render_into,
+sd_render_args output strides), which are the send buffer of ONE all_gather_into_tensor
+into a preallocated (world, R, 1 + D + 3 nv) receive buffer; MapGather double-buffers both
+so that frame i's gather (RCCL's own stream) overlaps frame i+1's render.  Within a
 frame, contiguous row bands of the image can be rendered on different ranks (ray-tile
 mode) -- each rank then owns a contiguous slice of the ray index r = (v H + y) W + x.
+The SSCBench voxel query (C5) shards by x-slabs of the voxel grid (slab_range,
+query_voxels_slab in scenedino_amd/sscbench.py) and all-gathers the slabs the same way.
 
 The reference has no multi-GPU inference path of its own (NeRFRenderer.bind_parallel
 wraps torch DataParallel only when `gpus` is given, scenedino/renderer/nerf.py:641-658,
@@ -60,17 +66,67 @@ def allreduce_grads(params, group=None) -> None:
     path of scenedino_amd/autograd.py on each): average the parameter gradients with ONE
     all-reduce of a flat bucket (the ResnetFC's 46 k parameters are far below a ring's
     per-link latency floor, so one collective beats one per tensor).  Replaces what
-    DistributedDataParallel does for the reference's trainer (base_trainer.py)."""
+    DistributedDataParallel does for the reference's trainer (base_trainer.py).  Every
+    parameter that requires a gradient has a slot in the bucket (zeros where this rank
+    produced no gradient), so the layout is identical on every rank."""
     import torch.distributed as dist
-    ps = [p for p in params if p.grad is not None]
+    ps = [p for p in params if p.requires_grad]
     if not ps:
         return
     world = dist.get_world_size(group)
-    flat = torch.cat([p.grad.reshape(-1) for p in ps])
+    dev = ps[0].device
+    flat = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1).to(dev)
+                      for p in ps])
     dist.all_reduce(flat, group=group)
     flat /= world
     o = 0
     for p in ps:
-        n = p.grad.numel()
-        p.grad.copy_(flat[o:o + n].view_as(p.grad))
+        n = p.numel()
+        g = flat[o:o + n].view_as(p)
+        if p.grad is None:
+            p.grad = g.clone()
+        else:
+            p.grad.copy_(g)
         o += n
+
+
+class MapGather:
+    """Asynchronous all-gather of every rank's packed rendered maps, ``depth`` slots deep.
+
+    ``send(i)`` returns the (R, width) float32 send buffer of frame i (after waiting for
+    the gather that last used that slot), ``start(i)`` launches the gather of frame i
+    (all_gather_into_tensor into ``recv[i % depth]``, (world, R, width)), ``wait_all()``
+    completes every outstanding gather.  With ``host_stage`` (gloo on one shared GPU: the
+    dry-run of a multi-rank launch) the maps go through host memory synchronously."""
+
+    def __init__(self, R: int, width: int, device, group=None, depth: int = 2,
+                 host_stage: bool = False):
+        import torch.distributed as dist
+        self.dist, self.group, self.depth, self.host = dist, group, depth, host_stage
+        self.world = dist.get_world_size(group)
+        self._send = [torch.empty(R, width, device=device) for _ in range(depth)]
+        rdev = "cpu" if host_stage else device
+        self.recv = [torch.empty(self.world, R, width, device=rdev) for _ in range(depth)]
+        self._work = [None] * depth
+
+    def send(self, i: int) -> torch.Tensor:
+        k = i % self.depth
+        if self._work[k] is not None:
+            self._work[k].wait()
+            self._work[k] = None
+        return self._send[k]
+
+    def start(self, i: int) -> None:
+        k = i % self.depth
+        if self.host:
+            h = self._send[k].cpu()
+            self.dist.all_gather(list(self.recv[k].unbind(0)), h, group=self.group)
+            return
+        self._work[k] = self.dist.all_gather_into_tensor(self.recv[k], self._send[k],
+                                                         group=self.group, async_op=True)
+
+    def wait_all(self) -> None:
+        for k in range(self.depth):
+            if self._work[k] is not None:
+                self._work[k].wait()
+                self._work[k] = None

@@ -86,6 +86,7 @@ class BTSNet(nn.Module):
         # (sd_render_fused, also the only fp32 path)
         self.fused_mode = conf.get("fused_mode", "proj")
         self.kernel_timer = None  # optional: .start(name) / .stop(name) around launches
+        self.render_into = None   # optional (R, 1 + D + 3 nv) f32 buffer for depth|dino|rgb
         self._packed = None
         self._packed_key = None
         self._grid_cache = None
@@ -336,10 +337,23 @@ class BTSNet(nn.Module):
                              f"encoded batch ({gc['B']})")
         dev = rays.device
         nv = gc["nv"]
+        maps = getattr(self, "render_into", None)
+        if maps is not None:
+            # render straight into packed [depth | dino | rgb] rows (the all-gather send
+            # buffer of the multi-GPU path): strided views, no pack copy
+            if not proj or tuple(maps.shape) != (R, 1 + m.D + 3 * nv) or maps.stride(1) != 1 \
+                    or maps.dtype != torch.float32 or maps.device != dev:
+                raise ValueError(f"render_into must be a float32 ({R}, {1 + m.D + 3 * nv}) row-major "
+                                 "tensor on the render device (16-bit projected render)")
+            depth, dino, rgb = maps[:, 0], maps[:, 1:1 + m.D], maps[:, 1 + m.D:]
+        else:
+            depth = torch.empty(R, device=dev)
+            dino = torch.empty(R, m.D, device=dev)
+            rgb = torch.empty(R, 3 * nv, device=dev)
         out = {
-            "depth": torch.empty(R, device=dev),
-            "dino": torch.empty(R, m.D, device=dev),
-            "rgb": torch.empty(R, 3 * nv, device=dev),
+            "depth": depth,
+            "dino": dino,
+            "rgb": rgb,
             "invalid": torch.empty(R, K, nv, device=dev),
             "invalid_f": torch.empty(R, K, device=dev, dtype=torch.bool),  # bytes 0 / 1
             "weights": torch.empty(R, K, device=dev) if want_weights else None,
@@ -361,7 +375,10 @@ class BTSNet(nn.Module):
             alphas=out["alphas"].data_ptr() if want_alphas else None,
             invalid=out["invalid"].data_ptr(), invalid_f=out["invalid_f"].data_ptr(),
             rgb_samps=out["rgb_samps"].data_ptr() if want_rgb_samps else None,
-            z_lindisp=int(bool(lindisp)), z_seed=(z_seed or 0) & (2**64 - 1), z_offset=0)
+            z_lindisp=int(bool(lindisp)), z_seed=(z_seed or 0) & (2**64 - 1), z_offset=0,
+            ld_depth=depth.stride(0) if maps is not None else 0,
+            ld_dino=dino.stride(0) if maps is not None else 0,
+            ld_rgb=rgb.stride(0) if maps is not None else 0)
         if proj:
             wb = _lib.render_proj_work_bytes(R, m.D)
             work = torch.empty(wb // 4, device=dev) if wb > 0 else None

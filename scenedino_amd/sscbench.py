@@ -77,10 +77,56 @@ def query_voxels(net, pts, dims, prediction_mode="stego_kmeans", grow=USE_GROW):
     nx, ny, nz = dims
     sigma, seg = net.predict_voxels(pts.reshape(1, -1, 3), voxel_size=VOXEL_SIZE,
                                     prediction_mode=prediction_mode)
-    sigmas = sigma.view(nx, ny, nz)
+    sigmas = sigma.reshape(nx, ny, nz)
     if grow:  # :755-756
         sigmas = F.max_pool3d(sigmas.unsqueeze(0), kernel_size=3, stride=1, padding=1).squeeze(0)
-    return sigmas, seg.view(nx, ny, nz)
+    return sigmas, seg.reshape(nx, ny, nz)
+
+
+def slab_range(nx: int, rank: int, world: int) -> tuple[int, int]:
+    """x-slab [x0, x1) of the voxel grid rendered by ``rank`` (C5 splits the
+    256 x-planes, [32 g, 32 g + 32) on 8 GPUs); slabs differ by at most one plane."""
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError(f"bad rank {rank} / world {world}")
+    base, extra = divmod(nx, world)
+    x0 = rank * base + min(rank, extra)
+    return x0, x0 + base + (1 if rank < extra else 0)
+
+
+def query_voxels_slab(predict, pts, dims, rank, world, grow=USE_GROW):
+    """This rank's x-slab of query_voxels.  ``predict(points (P, 3)) -> (sigma (P,),
+    seg (P,))`` evaluates the field + head on a contiguous run of voxel centres (the flat
+    index (ix ny + iy) nz + iz keeps every x-plane contiguous).  The 3x3x3 grow max-pool
+    needs one neighbouring x-plane on each side: those halo planes are queried too and
+    dropped after pooling, so the gathered slabs equal the unsharded result bit for bit.
+    Returns sigmas (x1 - x0, ny, nz), segs (x1 - x0, ny, nz)."""
+    nx, ny, nz = dims
+    x0, x1 = slab_range(nx, rank, world)
+    h0 = max(x0 - 1, 0) if grow else x0
+    h1 = min(x1 + 1, nx) if grow else x1
+    plane = ny * nz
+    sig, seg = predict(pts[h0 * plane:h1 * plane])
+    sig = sig.reshape(h1 - h0, ny, nz)
+    if grow:
+        sig = F.max_pool3d(sig.unsqueeze(0), kernel_size=3, stride=1, padding=1).squeeze(0)
+    lo = x0 - h0
+    return (sig[lo:lo + x1 - x0].contiguous(),
+            seg.reshape(h1 - h0, ny, nz)[lo:lo + x1 - x0].contiguous())
+
+
+def gather_slabs(sigmas, segs, dims, group=None):
+    """All-gather every rank's x-slab (equal slabs: world divides nx) into the full
+    (nx, ny, nz) grids on every rank: one all_gather_into_tensor per output."""
+    import torch.distributed as dist
+    nx, ny, nz = dims
+    world = dist.get_world_size(group)
+    if nx % world:
+        raise ValueError("gather_slabs needs world | nx (equal slabs)")
+    full_s = torch.empty(nx, ny, nz, dtype=sigmas.dtype, device=sigmas.device)
+    full_g = torch.empty(nx, ny, nz, dtype=segs.dtype, device=segs.device)
+    dist.all_gather_into_tensor(full_s, sigmas, group=group)
+    dist.all_gather_into_tensor(full_g, segs, group=group)
+    return full_s, full_g
 
 
 def downsample_and_predict(data, net, pts, factor, prediction_mode, vis=False, feat_vis=False):

@@ -93,13 +93,15 @@ def _grad_worker(rank, world, port, q):
         lin = torch.nn.Linear(5, 3)
         g = torch.Generator().manual_seed(rank)
         lin.weight.grad = torch.randn(3, 5, generator=g)
-        lin.bias.grad = torch.randn(3, generator=g)
+        b = torch.randn(3, generator=g)
+        lin.bias.grad = b if rank == 0 else None  # rank 1 produced no bias gradient
         sdd.allreduce_grads(lin.parameters())
         ws, bs = [], []
         for r in range(world):
             g2 = torch.Generator().manual_seed(r)
             ws.append(torch.randn(3, 5, generator=g2))
-            bs.append(torch.randn(3, generator=g2))
+            b2 = torch.randn(3, generator=g2)
+            bs.append(b2 if r == 0 else torch.zeros(3))
         ok = torch.allclose(lin.weight.grad, sum(ws) / world, atol=1e-6) and \
             torch.allclose(lin.bias.grad, sum(bs) / world, atol=1e-6)
         dist.barrier()
@@ -121,3 +123,88 @@ def test_allreduce_grads_gloo_world2():
         assert p.exitcode == 0
     res = dict(q.get(timeout=10) for _ in range(world))
     assert res == {0: True, 1: True}
+
+
+def _spawn(target, world, *args):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+        assert p.exitcode == 0
+    return dict(q.get(timeout=10) for _ in range(world))
+
+
+def _mapgather_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        R, width = 40, 68
+        mg = sdd.MapGather(R, width, "cpu", depth=2, host_stage=True)
+        ok = True
+        for i in range(5):  # frames i: rank r's maps = f(r, i)
+            buf = mg.send(i)
+            buf.copy_(torch.full((R, width), 100.0 * rank + i))
+            mg.start(i)
+            got = mg.recv[i % 2]
+            for r in range(world):
+                ok &= bool((got[r] == 100.0 * r + i).all())
+        mg.wait_all()
+        dist.barrier()
+        q.put((rank, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_map_gather_host_stage_gloo_world2():
+    assert _spawn(_mapgather_worker, 2) == {0: True, 1: True}
+
+
+def _slab_predict(p):
+    """A deterministic stand-in for the field + head (GPU-free): sigma and class of a
+    voxel centre from its coordinates."""
+    sig = torch.sin(3.1 * p[:, 0]) + torch.cos(1.7 * p[:, 1]) * p[:, 2]
+    seg = ((p[:, 0] * 7 + p[:, 1] * 3).floor().remainder(19)).to(torch.uint8)
+    return sig, seg
+
+
+def _slab_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from scenedino_amd import sscbench
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dims = (16, 6, 5)
+        g = torch.Generator().manual_seed(3)
+        pts = torch.rand(dims[0] * dims[1] * dims[2], 3, generator=g) * 4 - 2
+        sig, seg = sscbench.query_voxels_slab(_slab_predict, pts, dims, rank, world)
+        full_s, full_g = sscbench.gather_slabs(sig, seg, dims)
+        # unsharded reference: the whole grid, grown by the 3x3x3 max-pool
+        rs, rg = _slab_predict(pts)
+        rs = torch.nn.functional.max_pool3d(rs.reshape(1, *dims), 3, 1, 1).reshape(dims)
+        ok = torch.equal(full_s, rs) and torch.equal(full_g, rg.reshape(dims))
+        dist.barrier()
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_voxel_slabs_gloo_world2_equal_unsharded():
+    assert _spawn(_slab_worker, 2) == {0: True, 1: True}
+
+
+def test_slab_range_partition():
+    from scenedino_amd import sscbench
+    for world in (1, 2, 3, 8):
+        xs = []
+        for r in range(world):
+            a, b = sscbench.slab_range(256, r, world)
+            xs += list(range(a, b))
+        assert xs == list(range(256))
+    assert sscbench.slab_range(256, 3, 8) == (96, 128)

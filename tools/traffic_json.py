@@ -16,7 +16,7 @@ vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in sorted(glob.glob(os.path.join(d, "pmc*", "*counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"]
-        for k in ("k_render_proj", "k_project", "k_head_hc", "k_render<", "k_field_gather_bwd",
+        for k in ("k_render_tile", "k_render_proj", "k_project", "k_head_hc", "k_render<", "k_field_gather_bwd",
                   "k_field_gather", "k_composite_bwd", "k_unpack_grid", "k_pack_grid",
                   "k_field"):
             if k in name:
