@@ -52,12 +52,27 @@ class GatherAcc:
     handed to autograd by the first chunk of the backward pass (the others return no
     gradient), instead of one zeroed 4 x 126 MB buffer per chunk summed by autograd.
     Autograd runs the grid's node only after every chunk's backward, so the buffer is
-    complete when it is read."""
+    complete when it is read.  A backward pass is identified by autograd's graph-task id,
+    not by counting chunks: chunks outside the loss's graph never run their backward, and
+    a retained graph can be walked again; the buffer is released by a callback at the end
+    of the pass."""
 
     def __init__(self):
         self.n = 0        # FieldGather calls recorded in the forward pass
-        self.left = 0     # chunks still to run in the current backward pass
+        self.task = None  # graph task the buffer belongs to
         self.buf = None
+
+    def take(self, shape, device):
+        """(buffer, first) for the running backward pass."""
+        task = torch._C._current_graph_task_id()
+        if self.buf is None or self.task != task:
+            self.task, self.buf = task, torch.zeros(shape, device=device)
+            torch.autograd.Variable._execution_engine.queue_callback(self._release)
+            return self.buf, True
+        return self.buf, False
+
+    def _release(self):
+        self.task, self.buf = None, None
 
 
 class FieldGather(torch.autograd.Function):
@@ -87,19 +102,10 @@ class FieldGather(torch.autograd.Function):
         if not ctx.needs_input_grad[0] or gx is None:
             return None, None, None, None, None, None, None
         B, Hf, Wf, C = ctx.grid_shape
-        acc = ctx.acc
-        first = acc.left == 0
-        if first:
-            acc.left = acc.n
-            acc.buf = torch.zeros(B, Hf, Wf, C, device=xyz.device)
+        buf, first = ctx.acc.take((B, Hf, Wf, C), xyz.device)
         gx = gx.float().contiguous()  # f32 rows for the scatter (see _lib.field_gather_bwd)
-        _timed("gather_bwd", lambda: _lib.field_gather_bwd(xyz, gx, cam_f, Hf, Wf, C,
-                                                           dgrid=acc.buf))
-        acc.left -= 1
-        out = acc.buf if first else None
-        if acc.left == 0:
-            acc.buf = None
-        return out, None, None, None, None, None, None
+        _timed("gather_bwd", lambda: _lib.field_gather_bwd(xyz, gx, cam_f, Hf, Wf, C, dgrid=buf))
+        return (buf if first else None), None, None, None, None, None, None
 
 
 def _wgrad(a, b):

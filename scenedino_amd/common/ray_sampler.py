@@ -120,4 +120,8 @@ class ImageRaySampler(RaySampler):
             else:
                 ps = isqrt((n * v_in * H * W * d) // g.numel())
                 render_dict["dino_gt"] = g.view(n, v_in, H // ps, W // ps, d)
+            if "dino_artifacts" in render_dict:  # ray_sampler.py:599-605
+                art = render_dict["dino_artifacts"]
+                ps = isqrt((n * v_in * H * W * d) // art.numel())
+                render_dict["dino_artifacts"] = art.view(n, v_in, H // ps, W // ps, d)
         return render_dict

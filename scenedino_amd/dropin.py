@@ -25,11 +25,16 @@ import sys
 import types
 
 
+_NATIVE_ENCODER = True
+
+
 def _ref_make_model(config, downstream_config=None):
     from . import models as amd_models
     from .models.backbones import make_backbone as amd_make_backbone
     try:
         # the native DINOv2Module (ViT + DPT as one HIP graph; same parameter names)
+        if not _NATIVE_ENCODER:
+            raise NotImplementedError("native encoder disabled (install(native_encoder=False))")
         encoder = amd_make_backbone(config["encoder"])
     except NotImplementedError:
         # encoder variants this build does not cover (non-DPT decoders, register / FiT3D
@@ -45,9 +50,17 @@ def _ref_make_model(config, downstream_config=None):
                                  downstream_head=downstream_head)
 
 
-def install():
+def install(native_encoder: bool = True):
     """Alias scenedino.renderer / scenedino.models.make_model / ImageRaySampler to the
-    MI355X build.  Call before the first ``import scenedino...``."""
+    MI355X build.  Call before the first ``import scenedino...``.
+
+    native_encoder=False keeps the image encoder entirely the reference's (its timm ViT and
+    DPTHead with autograd): use it for train.py when the encoder or the DPT decoder is
+    trained -- the native ViT / DPT kernels are forward-only and DINOv2Module refuses a
+    training forward with trainable parameters rather than drop their gradients.  The
+    field / render path (BTSNet, NeRFRenderer, ImageRaySampler) is the build's either way."""
+    global _NATIVE_ENCODER
+    _NATIVE_ENCODER = bool(native_encoder)
     from . import renderer as amd_renderer
     from .common import ray_sampler as amd_rs
     from .models import bts as amd_bts
@@ -73,7 +86,8 @@ def install():
     # downsampler and the dimension reduction stay the reference's modules (BTSNet reads
     # dim_reduction's parameters for the fused sd_seg_query head).
     try:
-        dm = importlib.import_module("scenedino.models.backbones.dino.dinov2_module")
+        dm = importlib.import_module("scenedino.models.backbones.dino.dinov2_module") \
+            if native_encoder else None
     except ImportError:  # the reference's encoder dependencies (timm, torchvision) absent
         dm = None
     if dm is not None:

@@ -201,8 +201,20 @@ class DINOv2Module(nn.Module):
                     gt_f = self.gt_encoder(x.flip([-1]))[-1]
                     return [F.normalize(gt_f.flip([-1]) + gt_0, dim=1)]
                 return [gt_0]
-        if torch.is_grad_enabled() and not self.encoder_frozen and self.training:
-            raise NotImplementedError("scenedino_amd encoder: no backward kernels; use no_grad")
+        if torch.is_grad_enabled() and self.training:
+            # The reference runs the DPT decoder with autograd (only the ViT sits under
+            # no_grad when encoder_freeze, dinov2_module.py:176-183) and trains it in its own
+            # Adam group (trainer.py:567-570).  These kernels have no backward: refuse
+            # rather than silently leave the decoder (or ViT) parameters without gradients.
+            trainable = [n for n, p in self.named_parameters() if p.requires_grad and
+                         (n.startswith("decoder.") or (n.startswith("encoder.") and
+                                                       not self.encoder_frozen))]
+            if trainable:
+                raise NotImplementedError(
+                    "scenedino_amd DINOv2Module: the ViT / DPT kernels are forward-only; "
+                    f"{len(trainable)} trainable encoder/decoder parameters (e.g. {trainable[0]}) "
+                    "would get no gradient.  Train with the reference backbone (dropin keeps "
+                    "scenedino.models.backbones for training) or freeze them (requires_grad_(False)).")
         with torch.no_grad():
             return self._predict(x)
 

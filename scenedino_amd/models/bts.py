@@ -119,7 +119,9 @@ class BTSNet(nn.Module):
                images_alt=None, combine_ids=None, color_frame_filter=None,
                loss_feature_grid_shift=None):
         """Same semantics as bts.py:112-259 (encoder call, pose inversion, stored grids)."""
-        if combine_ids is not None or loss_feature_grid_shift not in (None, (0, 0)):
+        shift = (None if loss_feature_grid_shift is None
+                 else tuple(int(v) for v in loss_feature_grid_shift))  # trainer passes a tensor
+        if combine_ids is not None or shift not in (None, (0, 0)):
             raise NotImplementedError("combine_ids / loss_feature_grid_shift are training-only "
                                       "options outside the MI355X hot path")
         with torch.autocast(device_type=images.device.type, enabled=False):

@@ -18,6 +18,8 @@ the reference's ``torch.rand_like`` draw (nerf.py:134) with given values.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .. import _lib, autograd
@@ -72,6 +74,8 @@ class NeRFRenderer(torch.nn.Module):
         self.render_flow = render_flow
         self.normalize_dino = normalize_dino
         self.z_jitter = None          # parity hook (see module docstring)
+        # debug flag: the reference's per-call NaN guard (nerf.py:428-432; host sync)
+        self.check_nan = os.environ.get("SCENEDINO_AMD_NAN_CHECK", "0") == "1"
         self._rng_offset = 0
         self._want = None             # per-forward: which per-sample outputs are written
         self._z_seed = None           # per-forward: in-kernel z sampling seed
@@ -160,9 +164,25 @@ class NeRFRenderer(torch.nn.Module):
                 if weights is None:
                     raise RuntimeError("white_bkgd needs the per-sample weights")
                 rgb_final = rgb_final + 1 - weights.sum(dim=1).unsqueeze(-1)
+            if self.check_nan:
+                self._nan_guard(weights, rgb_final, depth_final, alphas, invalid, z_samp)
             ray_info = rays[:, None, 8:] if r_dim > 8 else None
             return (weights, rgb_final, depth_final, alphas, invalid, z_samp, rgbs, ray_info,
                     None, state_dicts)
+
+    @staticmethod
+    def _nan_guard(weights, rgb_final, depth_final, alphas, invalid, z_samp):
+        """The reference's NaN check of every composite call (nerf.py:428-432): print the
+        offending tensor and exit().  Behind ``check_nan`` (a debug flag, env
+        SCENEDINO_AMD_NAN_CHECK=1) because each check is a device -> host sync; tensors the
+        fused path does not produce (None) are skipped."""
+        for name, x in [("weights", weights), ("rgb_final", rgb_final),
+                        ("depth_final", depth_final), ("alphas", alphas), ("invalid", invalid),
+                        ("z_samp", z_samp)]:
+            if x is not None and torch.is_floating_point(x) and bool(torch.isnan(x).any()):
+                print(f"Detected NaN in {name} ({x.dtype}):")
+                print(x)
+                exit()
 
     def _fused_ok(self, model, K):
         return (hasattr(model, "render_fused") and not getattr(model, "use_viewdirs", False)

@@ -349,6 +349,45 @@ def fx_render_full_digest(ref):
     )
 
 
+def fx_render_full_offset(ref):
+    """The BASELINE C2 shape (192x640x64, fp32 reference) at the full 256x192x640 feature
+    grid, rays from the 0.5 m lateral / 2 deg yaw render pose of SURVEY §8(d) (encoder and
+    colour view at the identity): strided subsample of every output, digests of the full
+    masks, summary statistics."""
+    import hashlib
+    H, W, K = 192, 640, 64
+    n, C, gh, gw = 1, 256, 192, 640
+    images, Ks, poses, grid = make_scene(n, 1, C, gh, gw, H, W, seed=61)
+    net = build_net(ref, grid)
+    net.encode(images, Ks, poses, ids_encoder=[0], ids_render=[0])
+    renderer = ref.NeRFRenderer(n_coarse=K, lindisp=True, hard_alpha_cap=False,
+                                eval_batch_size=65536)
+    wrapper = renderer.bind_parallel(net, gpus=None).eval()
+    sampler = ref.ImageRaySampler(z_near=3, z_far=80, height=H, width=W)
+    render_pose = make_pose(2.0, 0.5).view(1, 1, 4, 4)
+    rays, _ = sampler.sample(None, render_pose, Ks[:, :1])
+    u = torch.rand(rays.shape[1], K, generator=torch.Generator().manual_seed(62))
+    with torch.no_grad(), injected_rand(u):
+        out = wrapper(rays, want_weights=True, want_alphas=True)
+    c = out["coarse"]
+    idx = np.arange(0, H * W, 61)
+    sha = lambda t: hashlib.sha256(np.ascontiguousarray(np32(t)).tobytes()).hexdigest()
+    np.savez_compressed(
+        os.path.join(HERE, "render_full_offset.npz"),
+        scene_seed=np.int64(61), u_seed=np.int64(62), idx=idx,
+        render_pose=np32(render_pose),
+        depth=np32(c["depth"])[0, idx], dino=np32(c["dino_features"])[0, idx],
+        rgb=np32(c["rgb"])[0, idx], weights=np32(c["weights"])[0, idx],
+        alphas=np32(c["alphas"])[0, idx],
+        invalid_sha256=np.array(sha(c["invalid"])),
+        invalid_features_sha256=np.array(sha(c["invalid_features"])),
+        invalid_shape=np.array(c["invalid"].shape), invalid_features_shape=np.array(c["invalid_features"].shape),
+        depth_mean=np.float64(c["depth"].double().mean()),
+        dino_abs_mean=np.float64(c["dino_features"].double().abs().mean()),
+        weights_sum_mean=np.float64(c["weights"].double().sum(-1).mean()),
+    )
+
+
 def load_reference_seg():
     """The reference's MlpDimReduction and SemanticHead pieces (CPU).  semantic_head.py
     imports the CRF helper (pydensecrf, torchvision.transforms.functional: absent here,
@@ -472,6 +511,76 @@ def fx_dpt():
                         out=np32(out).astype(np.float16), out_norm=np.float64(out.double().norm()))
 
 
+def fx_state_dict_manifest(ref):
+    """Key -> shape manifest of the reference modules whose parameters the build must load
+    unchanged (checkpoint.pt, load_state_dict(strict=False), demo_utils/utils.py:52-55):
+    ResnetFC / BTSNet heads (models/__init__.py:30-44, configs/model/dino_downsampler.yaml),
+    NeRFRenderer buffers (nerf.py:106-111), DPTHead for ViT-S and ViT-B embeddings
+    (dpt_head.py:179-236), MlpDimReduction (dim_reduction.py:15-25) and SemanticHead
+    (semantic_head.py:40-100, both head variants).  Shapes only -- no weights."""
+    import importlib.util
+    man = {}
+    sd_shapes = lambda m, drop=(): {k: list(v.shape) for k, v in m.state_dict().items()
+                                     if not k.startswith(drop)}
+    head = ref.ResnetFC(d_in=295, d_out=65, n_blocks=0, d_hidden=128)
+    man["resnetfc"] = sd_shapes(head)
+    net = build_net(ref, torch.zeros(1, 256, 4, 8))
+    man["btsnet"] = sd_shapes(net, drop=("encoder.",))
+    man["nerf_renderer"] = sd_shapes(ref.NeRFRenderer(n_coarse=32, lindisp=True))
+    spec = importlib.util.spec_from_file_location(
+        "ref_dpt_head", os.path.join(REF, "scenedino/models/backbones/dino/dpt_head.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    for embed, name in ((384, "dpt_head_vits"), (768, "dpt_head_vitb")):
+        dpt = mod.DPTHead(embed_dims=embed, post_process_channels=[64, 64, 128, 256],
+                          readout_type="ignore", patch_size=16, d_out=256, expand_channels=False)
+        man[name] = sd_shapes(dpt)
+    MlpDimReduction, sh = load_reference_seg()
+    man["mlp_dim_reduction"] = sd_shapes(MlpDimReduction(768, 64, latent_channels=128))
+    zeros, tensor_to = torch.zeros, torch.Tensor.to
+    torch.zeros = lambda *a, **kw: zeros(*a, **{k: v for k, v in kw.items() if k != "device"})
+    torch.Tensor.to = lambda self, *a, **kw: self if a and a[0] == "cuda" else tensor_to(self, *a, **kw)
+    try:
+        for mlp, name in ((False, "semantic_head"), (True, "semantic_head_mlp")):
+            head = sh.SemanticHead(19, 19, 768, 64, buffer_size=2, patch_sample_size=4,
+                                   knn_neighbors=4, mode="3d", mlp_head=mlp, apply_crf=False)
+            man[name] = sd_shapes(head)
+    finally:
+        torch.zeros, torch.Tensor.to = zeros, tensor_to
+    with open(os.path.join(HERE, "state_dict_manifest.json"), "w") as f:
+        json.dump(man, f, indent=0, sort_keys=True)
+
+
+def _reconstruct_input(n=2, v=1, H=8, W=16, K=5, vr=1, ch=3, D=6, ps=4, upscaled=False):
+    """A render dict shaped as the renderer returns it (SB = n super-batches of v*H*W rays),
+    values = arange (views keep them), with every key ImageRaySampler.reconstruct handles."""
+    R = v * H * W
+    t = lambda *s: torch.arange(int(np.prod(s)), dtype=torch.float32).view(*s)
+    part = {"rgb": t(n, R, vr * ch), "weights": t(n, R, K), "depth": t(n, R),
+            "invalid": t(n, R, K, vr), "invalid_features": t(n, R, K, vr), "alphas": t(n, R, K),
+            "z_samps": t(n, R, K), "rgb_samps": t(n, R, K, vr * ch), "ray_info": t(n, R, 3),
+            "extras": t(n, R, 2), "dino_features": t(n, R, D)}
+    gh = H if upscaled else H // ps
+    gw = W if upscaled else W // ps
+    return {"coarse": part, "rgb_gt": t(n, R, ch), "dino_gt": t(n, v * gh * gw, D),
+            "dino_artifacts": t(n, v * gh * gw, D)}
+
+
+def fx_reconstruct(ref):
+    """ImageRaySampler.reconstruct (ray_sampler.py:515-607) output shapes, including the
+    dino_gt / dino_artifacts patch-grid branch (:587-605), for patch and upscaled targets."""
+    out = {}
+    for upscaled in (False, True):
+        s = ref.ImageRaySampler(z_near=3, z_far=80, height=8, width=16, channels=3,
+                                dino_upscaled=upscaled)
+        d = s.reconstruct(_reconstruct_input(upscaled=upscaled))
+        shapes = {k: list(v.shape) for k, v in d.items() if torch.is_tensor(v)}
+        shapes.update({"coarse." + k: list(v.shape) for k, v in d["coarse"].items()})
+        out["upscaled" if upscaled else "patch"] = shapes
+    with open(os.path.join(HERE, "reconstruct_shapes.json"), "w") as f:
+        json.dump(out, f, indent=0, sort_keys=True)
+
+
 def main():
     torch.set_num_threads(8)
     if os.environ.get("GOLDEN_ONLY") == "dpt":
@@ -485,6 +594,18 @@ def main():
         print("seg / voxel fixtures written to", HERE)
         return
     ref = load_reference()
+    if os.environ.get("GOLDEN_ONLY") == "full_offset":
+        fx_render_full_offset(ref)
+        print("full offset-pose fixture written to", HERE)
+        return
+    if os.environ.get("GOLDEN_ONLY") == "reconstruct":
+        fx_reconstruct(ref)
+        print("reconstruct fixture written to", HERE)
+        return
+    if os.environ.get("GOLDEN_ONLY") == "manifest":
+        fx_state_dict_manifest(ref)
+        print("state_dict manifest written to", HERE)
+        return
     fx_gen_rays(ref)
     fx_sample_z(ref)
     fx_field_query(ref)
@@ -493,6 +614,9 @@ def main():
     fx_render(ref, "sb2_nv2_k16", n=2, nv_render=2, K=16, hard_cap=False, H=16, W=48, seed=51)
     if os.environ.get("GOLDEN_FULL", "1") == "1":
         fx_render_full_digest(ref)
+        fx_render_full_offset(ref)
+    fx_state_dict_manifest(ref)
+    fx_reconstruct(ref)
     print("golden fixtures written to", HERE)
 
 

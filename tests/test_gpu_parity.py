@@ -2,15 +2,19 @@
 against golden vectors produced by the reference itself (tests/golden/make_golden.py)
 and against the CPU oracle.
 
-Tolerances (written here):
-  * ray generation, z sampling: bit-exact.
-  * fp32 path (f32 grid + exact-f32 MFMA): |d| <= atol + rtol*|ref| with rtol 1e-4,
-    atol 2e-5 (weights/alphas/rgb), 2e-4 (dino), 1e-3 m (depth);
-    invalid masks: identical.
-  * bf16 / fp16 paths (16-bit grid or projected grid + 16-bit MFMA, fp32
-    accumulate), both kernels ("proj": sd_project_grid + sd_render_proj, "grid":
-    sd_render_fused): rel-L2 <= 1e-2 on dino features and colour, depth rel-L2 <=
-    1e-2, weights max |d| <= 2e-2 and rel-L2 <= 2e-2; invalid masks identical.
+Tolerances (written here; SURVEY.md §8(c), measured maxima in DESIGN.md §4 from
+tools/parity_report.py):
+  * ray generation, z sampling, invalid masks: bit-exact.
+  * fp32 path (f32 grid + exact-f32 MFMA): |d| <= atol + 1e-5 |ref| per output with atol
+    1e-6 for depth / weights / alphas and the FP32_ATOL values below where the reference's
+    own fp32 rounding order sets the floor (colour samples: one ulp of the projected
+    coordinate times the random test image's gradient; DINO: 128-term dot products of a
+    295-term layer; the full-grid offset render: the same through 64 composited samples).
+  * 16-bit paths (bf16 / fp16 operands, fp32 accumulate; "proj": sd_project_grid +
+    sd_render_proj = tile kernel + overflow fallback, "grid": sd_render_fused): weights
+    max |d| <= 2e-3, DINO and colour rel-L2 <= 1e-2, depth max |d| <= 1e-2 m (fp16) /
+    5e-2 m (bf16: an 8-bit mantissa on sigma moves alpha by ~1e-3 at samples up to 30 m
+    apart) and depth rel-L2 <= 2e-3.
 """
 import hashlib
 import json
@@ -37,6 +41,26 @@ def _need_gpu():
 
 def T(a):
     return torch.as_tensor(np.asarray(a)).to(DEV)
+
+
+FP32_ATOL = {"depth": 1e-6, "weights": 1e-6, "alphas": 1e-6, "rgb": 1e-5, "rgb_samps": 1e-5,
+             "dino_features": 1e-5, "dino": 1e-5, "sigma": 1e-6}
+# the full 256x192x640-grid render from the offset pose (64 samples through the scan)
+FP32_ATOL_FULL = {"depth": 1e-6, "weights": 1e-5, "alphas": 1e-4, "rgb": 1e-5, "dino": 5e-5}
+LOWP_DEPTH_MAX = {"bf16": 5e-2, "fp16": 1e-2}
+
+
+def check_lowp(c, ref, precision, rgb=True):
+    """The 16-bit tolerances of the module docstring (c: outputs, ref: reference arrays
+    keyed like c)."""
+    dw = (torch.as_tensor(c["weights"]).double().cpu() - torch.as_tensor(np.asarray(ref["weights"])).double().reshape(c["weights"].shape)).abs()
+    assert float(dw.max()) <= 2e-3, f"{precision} weights max |d| {float(dw.max()):.3g}"
+    dd = (torch.as_tensor(c["depth"]).double().cpu() - torch.as_tensor(np.asarray(ref["depth"])).double().reshape(c["depth"].shape)).abs()
+    assert float(dd.max()) <= LOWP_DEPTH_MAX[precision], f"{precision} depth max |d| {float(dd.max()):.3g}"
+    assert rel_l2(c["depth"], ref["depth"]) <= 2e-3
+    assert rel_l2(c["dino_features"], ref["dino_features"]) <= 1e-2
+    if rgb:
+        assert rel_l2(c["rgb"], ref["rgb"]) <= 1e-2
 
 
 def close(a, ref, rtol, atol, what):
@@ -113,10 +137,23 @@ def test_field_query_vs_reference(precision):
     assert extras is None
     assert torch.equal(invalid.cpu(), torch.from_numpy(d["invalid"]))
     assert torch.equal(sd["invalid_features"].cpu(), torch.from_numpy(d["invalid_features"]))
-    close(rgb, d["rgb"], 1e-4, 2e-5, "rgb")
+    close(rgb, d["rgb"], 1e-5, FP32_ATOL["rgb"], "rgb")
     if precision == "fp32":
-        close(sigma, d["sigma"], 1e-4, 2e-5, "sigma")
-        close(sd["dino_features"], d["dino"], 1e-4, 2e-4, "dino")
+        # the fixture samples points up to 5 m behind the camera: there z~ = encoding of
+        # 1 / clamp(z, 1e-3) reaches ~6e3 and the top positional frequency's argument
+        # ~3e5 rad, whose fp32 ulp (0.03 rad) is above any sin tolerance -- such points are
+        # held to the 16-bit bound, all others (z_cam >= 1 m) to the fp32 one
+        xyz = torch.as_tensor(d["xyz"]).double().reshape(-1, 3)
+        w2c = torch.inverse(torch.as_tensor(d["poses"]).double()[0, 0])
+        zc = xyz @ w2c[2, :3] + w2c[2, 3]
+        ok = zc >= 1.0
+        sig = sigma.reshape(-1)
+        dn = sd["dino_features"].reshape(-1, sd["dino_features"].shape[-1])
+        close(sig.cpu()[ok], torch.as_tensor(d["sigma"]).reshape(-1)[ok], 1e-5, FP32_ATOL["sigma"], "sigma")
+        close(dn.cpu()[ok], torch.as_tensor(d["dino"]).reshape(dn.shape)[ok], 1e-5, FP32_ATOL["dino"], "dino")
+        assert int(ok.sum()) > 0.8 * ok.numel()
+        assert rel_l2(sig.cpu()[~ok], torch.as_tensor(d["sigma"]).reshape(-1)[~ok]) < 1e-3
+        assert rel_l2(dn.cpu()[~ok], torch.as_tensor(d["dino"]).reshape(dn.shape)[~ok]) < 1e-3
     else:
         assert rel_l2(sigma, d["sigma"]) < 2e-2
         assert rel_l2(sd["dino_features"], d["dino"]) < 1e-2
@@ -149,13 +186,9 @@ def test_render_fp32_vs_reference(fx):
     assert torch.equal(c["invalid"].cpu(), torch.from_numpy(d["invalid"]))
     assert torch.equal(c["invalid_features"].cpu(), torch.from_numpy(d["invalid_features"]))
     assert torch.equal(c["ray_info"].cpu(), torch.from_numpy(d["ray_info"]))
-    close(c["weights"], d["weights"], 1e-4, 2e-5, "weights")
-    close(c["alphas"], d["alphas"], 1e-4, 2e-5, "alphas")
-    close(c["depth"], d["depth"], 1e-4, 1e-3, "depth")
-    close(c["rgb"], d["rgb"], 1e-4, 2e-5, "rgb")
-    close(c["rgb_samps"], d["rgb_samps"], 1e-4, 2e-5, "rgb_samps")
-    close(c["dino_features"], d["dino_features"], 1e-4, 2e-4, "dino")
-    close(out["state_dict"]["dino_features"], d["sd_dino"], 1e-4, 2e-4, "state_dict dino")
+    for k in ("weights", "alphas", "depth", "rgb", "rgb_samps", "dino_features"):
+        close(c[k], d[k], 1e-5, FP32_ATOL[k], k)
+    close(out["state_dict"]["dino_features"], d["sd_dino"], 1e-5, FP32_ATOL["dino"], "state_dict dino")
     for k in ("rgb", "depth", "invalid", "weights", "alphas", "z_samps", "rgb_samps",
               "dino_features", "invalid_features", "ray_info"):
         assert tuple(c[k].shape) == d[k].shape, k
@@ -169,12 +202,8 @@ def test_render_lowp_vs_reference(fx, precision, mode):
     c = _render(d, precision, mode=mode)["coarse"]
     assert torch.equal(c["invalid"].cpu(), torch.from_numpy(d["invalid"]))
     assert torch.equal(c["invalid_features"].cpu(), torch.from_numpy(d["invalid_features"]))
-    assert rel_l2(c["dino_features"], d["dino_features"]) < 1e-2
-    assert rel_l2(c["rgb"], d["rgb"]) < 1e-2
-    assert rel_l2(c["depth"], d["depth"]) < 1e-2
-    assert rel_l2(c["weights"], d["weights"]) < 2e-2
-    assert float((c["weights"].cpu() - torch.from_numpy(d["weights"])).abs().max()) < 2e-2
-    assert rel_l2(c["rgb_samps"], d["rgb_samps"]) < 1e-5
+    check_lowp(c, d, precision)
+    close(c["rgb_samps"], d["rgb_samps"], 1e-5, FP32_ATOL["rgb_samps"], "rgb_samps")
 
 
 @pytest.mark.parametrize("precision", ["bf16", "fp16"])
@@ -230,11 +259,11 @@ def test_render_full_192x640x64_vs_reference_subsample():
     with torch.no_grad():
         c = r.bind_parallel(net).eval()(rays, want_weights=True, want_alphas=True)["coarse"]
     idx = torch.from_numpy(d["idx"])
-    close(c["depth"][0].cpu()[idx], d["depth"], 1e-4, 1e-3, "depth")
-    close(c["dino_features"][0].cpu()[idx], d["dino"], 1e-4, 2e-4, "dino")
-    close(c["rgb"][0].cpu()[idx], d["rgb"], 1e-4, 2e-5, "rgb")
-    close(c["weights"][0].cpu()[idx], d["weights"], 1e-4, 2e-5, "weights")
-    assert abs(float(c["depth"].double().mean()) - float(d["depth_mean"])) < 1e-3
+    close(c["depth"][0].cpu()[idx], d["depth"], 1e-5, FP32_ATOL["depth"], "depth")
+    close(c["dino_features"][0].cpu()[idx], d["dino"], 1e-5, FP32_ATOL["dino"], "dino")
+    close(c["rgb"][0].cpu()[idx], d["rgb"], 1e-5, FP32_ATOL["rgb"], "rgb")
+    close(c["weights"][0].cpu()[idx], d["weights"], 1e-5, FP32_ATOL["weights"], "weights")
+    assert abs(float(c["depth"].double().mean()) - float(d["depth_mean"])) < 1e-5
 
 
 # --------------------------------------------------------------------------- vs oracle
@@ -279,7 +308,7 @@ def test_generic_composite_path_matches_fused():
         a = r(Foreign(net), T(d["rays"]), want_weights=True, want_alphas=True)["coarse"]
         b = r(net, T(d["rays"]), want_weights=True, want_alphas=True)["coarse"]
     for k in ("weights", "alphas", "depth", "rgb", "dino_features"):
-        close(a[k], b[k].cpu(), 1e-4, 2e-4, k)
+        close(a[k], b[k].cpu(), 1e-5, FP32_ATOL[k], k)
     assert torch.equal(a["invalid"].cpu(), b["invalid"].cpu())
 
 
@@ -310,12 +339,10 @@ def test_ragged_ray_count_and_offset_pose(precision, n_coarse):
                    torch.from_numpy(d["b_in"]), torch.from_numpy(d["W_out"]),
                    torch.from_numpy(d["b_out"]), sb=1)
     if precision == "fp32":
-        close(c["depth"], ref["depth"], 1e-4, 1e-3, "depth")
-        close(c["dino_features"], ref["dino_features"], 1e-4, 2e-4, "dino")
-        close(c["weights"], ref["weights"], 1e-4, 2e-5, "weights")
+        for k in ("depth", "dino_features", "weights", "rgb"):
+            close(c[k], ref[k], 1e-5, FP32_ATOL[k], k)
     else:
-        assert rel_l2(c["dino_features"], ref["dino_features"]) < 1e-2
-        assert rel_l2(c["depth"], ref["depth"]) < 1e-2
+        check_lowp(c, ref, precision)
     assert torch.equal(c["invalid"].cpu(), ref["invalid"])
 
 
@@ -349,10 +376,37 @@ def test_render_full_192x640x64_projected_vs_reference_subsample(precision):
     with torch.no_grad():
         c = r.bind_parallel(net).eval()(rays, want_weights=True, want_alphas=True)["coarse"]
     idx = torch.from_numpy(d["idx"])
-    assert rel_l2(c["depth"][0].cpu()[idx], d["depth"]) < 1e-2
-    assert rel_l2(c["dino_features"][0].cpu()[idx], d["dino"]) < 1e-2
-    assert rel_l2(c["rgb"][0].cpu()[idx], d["rgb"]) < 1e-2
-    assert rel_l2(c["weights"][0].cpu()[idx], d["weights"]) < 2e-2
+    sub = {"depth": c["depth"][0].cpu()[idx], "dino_features": c["dino_features"][0].cpu()[idx],
+           "rgb": c["rgb"][0].cpu()[idx], "weights": c["weights"][0].cpu()[idx]}
+    check_lowp(sub, {"depth": d["depth"], "dino_features": d["dino"], "rgb": d["rgb"],
+                     "weights": d["weights"]}, precision)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16", "fp16"])
+def test_render_full_offset_pose_vs_reference(precision):
+    """BASELINE C2 shape at the full 256x192x640 grid, rays from the 0.5 m / 2 deg offset
+    render pose (SURVEY §8(d) second run; make_golden.fx_render_full_offset): every
+    sample of a ray projects onto a different texel -- the tile kernel's staged P boxes
+    and its overflow fallback both run.  Masks bit-exact over the whole frame (SHA-256)."""
+    import hashlib
+    from _fullscene import render_full_offset
+    d = load("render_full_offset.npz")
+    c = render_full_offset(d, precision, DEV)
+    sha = lambda t: hashlib.sha256(t.cpu().numpy().tobytes()).hexdigest()
+    assert list(c["invalid"].shape) == list(d["invalid_shape"])
+    assert sha(c["invalid"]) == str(d["invalid_sha256"])
+    assert sha(c["invalid_features"]) == str(d["invalid_features_sha256"])
+    idx = torch.from_numpy(d["idx"])
+    sub = {k: c[k][0].cpu()[idx] for k in ("depth", "dino_features", "rgb", "weights", "alphas")}
+    if precision == "fp32":
+        for k, rk in (("depth", "depth"), ("weights", "weights"), ("alphas", "alphas"),
+                      ("rgb", "rgb"), ("dino_features", "dino")):
+            close(sub[k], d[rk], 1e-5, FP32_ATOL_FULL[rk], k)
+        assert abs(float(c["depth"].double().mean()) - float(d["depth_mean"])) < 1e-5
+    else:
+        check_lowp(sub, {"depth": d["depth"], "dino_features": d["dino"], "rgb": d["rgb"],
+                         "weights": d["weights"]}, precision)
+        assert abs(float(c["depth"].double().mean()) - float(d["depth_mean"])) < 1e-3
 
 
 @pytest.mark.parametrize("fx", ["render_k64_cap1.npz", "render_sb2_nv2_k16.npz"])

@@ -11,7 +11,7 @@ grid), sd_seg_query against the fixtures and the oracle.  Tolerances (written he
   * dino_full (transform_expand, bf16 MFMA, fp32 accumulate): rel-L2 <= 1e-2 per point set,
     max |d| <= 1.5e-2 (unit vectors).
   * labels: identical wherever the reference's top-2 cosine margin exceeds 2e-2 (a bf16
-    field can only flip near-ties), and >= 97 % agreement overall.
+    field can only flip near-ties), and >= 99 % agreement overall.
 """
 import hashlib
 import json
@@ -200,7 +200,8 @@ def _label_check(labels, ref_scores, ref_labels, what):
     sure = margin > 2e-2
     assert (labels[sure] == ref_labels[sure]).all(), f"{what}: clear-margin label mismatch"
     agree = (labels == ref_labels).mean()
-    assert agree >= 0.97, f"{what}: label agreement {agree:.4f}"
+    print(f"{what}: label agreement {agree:.4f}")
+    assert agree >= 0.99, f"{what}: label agreement {agree:.4f}"
 
 
 @pytest.mark.gpu

@@ -338,3 +338,36 @@ def test_field_gather_autocast_rows_gpu(dt):
     ref = _lib.field_gather_bwd(xyz.cuda(), gx.float(), cam_f, gn.shape[1], gn.shape[2],
                                 gn.shape[3])
     assert rel_l2(g1.grad, ref) < 1e-6
+
+
+def test_gather_accumulator_passes_cpu(monkeypatch):
+    """GatherAcc hands one buffer per backward pass to autograd, also when a chunk lies
+    outside the loss's graph (its backward never runs) and when a retained graph is walked
+    again (a chunk-count scheme drops the grid gradient there).  The gather and
+    its scatter are stand-ins here: x = 0 rows, scatter adds sum(gx) * (row count) to
+    dgrid[0, 0, 0, 0], so the grid gradient is a plain function of which chunks ran."""
+    from scenedino_amd import autograd as ag
+
+    def fake_gather(xyz, grid, cam_f, img, cam_c, colors, dtype):
+        B, P, _ = xyz.shape
+        return torch.zeros(B, P, grid.shape[-1] + 40, dtype=dtype), None, None, None
+
+    def fake_bwd(xyz, gx, cam_f, Hf, Wf, C, dgrid):
+        dgrid[0, 0, 0, 0] += gx.sum()
+        return dgrid
+
+    monkeypatch.setattr(ag._lib, "field_gather", fake_gather)
+    monkeypatch.setattr(ag._lib, "field_gather_bwd", fake_bwd)
+    grid = torch.zeros(1, 2, 3, 4, requires_grad=True)
+    acc = ag.GatherAcc()
+    parts = [ag.FieldGather.apply(grid, torch.zeros(1, n, 3), None, None, None, False, acc)[0]
+             for n in (5, 7, 9)]
+    loss = parts[0].sum() + 2 * parts[2].sum()  # chunk 1 is outside the graph
+    for _ in range(2):
+        grid.grad = None
+        loss.backward(retain_graph=True)
+        assert grid.grad[0, 0, 0, 0].item() == 5 * 44 + 2 * 9 * 44
+        assert acc.buf is None  # released at the end of the pass
+    grid.grad = None
+    (3 * parts[1].sum()).backward()
+    assert grid.grad[0, 0, 0, 0].item() == 3 * 7 * 44
