@@ -16,7 +16,10 @@
  * Layouts (all row-major, float32 unless stated):
  *   rays        (R, ray_dim>=8)  [o(3), d(3), near, far, (frame_id, x, y)]
  *   z           (R, K)
- *   camera rec  21 floats: w2c rows 0..2 (12 floats, 3x4) then K (9 floats, 3x3)
+ *   camera rec  SD_CAM_WORDS (36) floats: w2c rows 0..2 (12 floats, 3x4), K (9 floats,
+ *               3x3), 3 zeros, then the fused projection P = K . w2c[:3] (12 floats,
+ *               3x4, rounded once from an exact product) that the 16-bit render kernels
+ *               use in place of the two-step pts_into_camera / project_to_image
  *   grid        (B, Hf, Wf, C) NHWC, element type f32 / bf16 / f16 (= the MLP dtype)
  *   colour img  (B, nv, Hc, Wc, 4) NHWC4 float32 (rgb + pad)
  */
@@ -24,6 +27,8 @@
 #define SDHIP_H
 
 #include <stdint.h>
+
+#define SD_CAM_WORDS 36  /* floats per camera record (see layout above) */
 #include <stddef.h>
 
 #ifdef __cplusplus
@@ -65,7 +70,7 @@ int sd_pack_grid(const float *grid_nchw, int64_t B, int64_t C, int64_t H, int64_
 int sd_pack_image(const float *img_nchw, int64_t N, int64_t H, int64_t W, float *out_nhwc4,
                   void *stream);
 
-/* Camera records of n views: out (n, 21) = [w2c rows 0..2 (3x4) | K (3x3)], the
+/* Camera records of n views: out (n, 36) = [w2c rows 0..2 (3x4) | K (3x3) | 0 0 0 | K.w2c (3x4)], the
  * operands of pts_into_camera / project_to_image (pinhole.py:40-84) as the field
  * kernels read them.  w2c: (n, 4, 4) with element stride s_w (>= 16) between views,
  * inner 4x4 contiguous; Ks: (n, 3, 3), stride s_k (>= 9). */
@@ -100,9 +105,9 @@ typedef struct sd_render_args {
     const float *rays; int64_t ray_dim; int64_t R; int64_t rays_per_sb; int32_t K;
     const float *z;                       /* (R, K)                                */
     const void *grid; int32_t Hf, Wf;     /* (B, Hf, Wf, C) NHWC                   */
-    const float *cam_f;                   /* (B, 21)                               */
+    const float *cam_f;                   /* (B, 36)                               */
     const float *img; int32_t nv, Hc, Wc; /* (B, nv, Hc, Wc, 4) or NULL if nv==0   */
-    const float *cam_c;                   /* (B, nv, 21)                           */
+    const float *cam_c;                   /* (B, nv, 36)                           */
     int32_t hard_alpha_cap;
     /* required outputs */
     float *depth;      /* (R)        */
@@ -175,9 +180,9 @@ int64_t sd_render_proj_work_bytes(int64_t R, int32_t D);
 typedef struct sd_field_args {
     const float *xyz; int64_t B; int64_t P;
     const void *grid; int32_t Hf, Wf;
-    const float *cam_f;                   /* (B, 21)            */
+    const float *cam_f;                   /* (B, 36)            */
     const float *img; int32_t nv, Hc, Wc; /* may be NULL / nv=0 */
-    const float *cam_c;                   /* (B, nv, 21)        */
+    const float *cam_c;                   /* (B, nv, 36)        */
     float *sigma;      /* (B, P)             */
     float *dino;       /* (B, P, D)          */
     float *rgb;        /* (B, P, 3 nv) or NULL */

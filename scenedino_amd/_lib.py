@@ -14,7 +14,8 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # SDHIP_LIB: alternative build of the same library (diagnostic builds only)
 LIB_PATH = os.environ.get("SDHIP_LIB") or os.path.join(_HERE, "libsdhip.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
+CAM_WORDS = 36  # floats per camera record (include/sdhip.h SD_CAM_WORDS)
 
 SD_F32 = 0
 SD_BF16 = 1
@@ -233,7 +234,7 @@ def pack_image(img_nchw):
 
 
 def cam_records(poses_w2c, Ks):
-    """(..., 4, 4) w2c and (..., 3, 3) K -> (..., 21) camera records (one launch)."""
+    """(..., 4, 4) w2c and (..., 3, 3) K -> (..., CAM_WORDS) camera records (one launch)."""
     lib = load()
     lead = poses_w2c.shape[:-2]
     w = poses_w2c.float().reshape(-1, 4, 4)
@@ -245,7 +246,7 @@ def cam_records(poses_w2c, Ks):
     n = w.shape[0]
     if k.shape[0] != n:
         raise ValueError("poses and intrinsics must have the same number of views")
-    out = torch.empty(*lead, 21, device=w.device, dtype=torch.float32)
+    out = torch.empty(*lead, CAM_WORDS, device=w.device, dtype=torch.float32)
     _check(lib.sd_cam_records(ptr(w), w.stride(0) if n > 1 else 16, ptr(k),
                               k.stride(0) if n > 1 else 9, n, ptr(out), stream_of(out)),
            "sd_cam_records")
@@ -349,7 +350,7 @@ def field_gather(xyz, grid_nhwc, cam_f, img=None, cam_c=None, colors=True,
     x = torch.empty(B, P, C + 40, device=dev, dtype=dtype)
     invf = torch.empty(B, P, device=dev, dtype=torch.bool)
     nv, Hc, Wc = 0, 0, 0
-    if colors:  # img: pack_image output (B*nv, Hc, Wc, 4); cam_c (B, nv, 21)
+    if colors:  # img: pack_image output (B*nv, Hc, Wc, 4); cam_c (B, nv, CAM_WORDS)
         nv, Hc, Wc = cam_c.shape[1], img.shape[1], img.shape[2]
     rgb = torch.empty(B, P, 3 * nv, device=dev) if colors else None
     inv = torch.empty(B, P, nv, device=dev) if colors else None

@@ -41,7 +41,7 @@ extern "C" void sd_set_error(const char *msg) {
     g_err[sizeof(g_err) - 1] = 0;
 }
 extern "C" const char *sd_last_error(void) { return g_err; }
-extern "C" int sd_abi_version(void) { return 3; }
+extern "C" int sd_abi_version(void) { return 4; }
 
 // Threads per workgroup, one workgroup per CU: 16-bit kernels run 8 waves (2 per SIMD,
 // <= 256 VGPRs each); the f32 parity kernels run 4 waves (1 per SIMD, 512 VGPRs).
@@ -444,7 +444,7 @@ k_render(const sd_render_args a, const sd_mlp m, const LdsPlan pl) {
         it.px = rr[0] + z0 * rr[3];  // points = o + z d (nerf.py:252)
         it.py = rr[1] + z0 * rr[4];
         it.pz = rr[2] + z0 * rr[5];
-        it.geo = sd_point_geo((sd_cfloat *)(a.cam_f + it.sbi * 21), it.px, it.py, it.pz, a.Wf, a.Hf);
+        it.geo = sd_point_geo((sd_cfloat *)(a.cam_f + it.sbi * SD_CAM_WORDS), it.px, it.py, it.pz, a.Wf, a.Hf);
         it.rs = sd_rsrc((const uint8_t *)a.grid + (int64_t)it.sbi * plane_bytes, plane_bytes);
         it.o = sd_tapoff(it.geo.t, C, Pr::ESZ, h);
     };
@@ -454,7 +454,7 @@ k_render(const sd_render_args a, const sd_mlp m, const LdsPlan pl) {
             invc[v] = false;
             col[3 * v] = col[3 * v + 1] = col[3 * v + 2] = 0.f;
             if (v < nv)
-                invc[v] = sd_color_view(a.cam_c + (it.sbi * nv + v) * 21,
+                invc[v] = sd_color_view(a.cam_c + (it.sbi * nv + v) * SD_CAM_WORDS,
                                         a.img + (int64_t)(it.sbi * nv + v) * cplane, a.Wc, a.Hc, it.px,
                                         it.py, it.pz, col + 3 * v);
         }
@@ -669,7 +669,7 @@ k_field(const sd_field_args a, const sd_mlp m, const LdsPlan pl) {
         const int64_t p = valid ? pu : NP - 1;
         const int64_t b = p / a.P;
         const float px = a.xyz[p * 3], py = a.xyz[p * 3 + 1], pz = a.xyz[p * 3 + 2];
-        PointGeo geo = sd_point_geo(a.cam_f + b * 21, px, py, pz, a.Wf, a.Hf);
+        PointGeo geo = sd_point_geo(a.cam_f + b * SD_CAM_WORDS, px, py, pz, a.Wf, a.Hf);
 
         const int lo = sd_opaque0();
         f32x16 acc[4];
@@ -699,7 +699,7 @@ k_field(const sd_field_args a, const sd_mlp m, const LdsPlan pl) {
         if (valid && h == 1 && nv > 0 && (a.rgb || a.invalid)) {
             for (int v = 0; v < nv; ++v) {
                 float col[3];
-                bool ic = sd_color_view(a.cam_c + (b * nv + v) * 21, a.img + (b * nv + v) * cplane,
+                bool ic = sd_color_view(a.cam_c + (b * nv + v) * SD_CAM_WORDS, a.img + (b * nv + v) * cplane,
                                         a.Wc, a.Hc, px, py, pz, col);
                 if (a.rgb) {
                     a.rgb[(p * nv + v) * 3] = col[0];

@@ -41,6 +41,66 @@ __device__ __forceinline__ PointGeo sd_point_geo(CP cam, float px, float py,
 }
 
 
+// 16-bit render modes: projection through the fused record P = K . w2c[:3]
+// (SD_CAM_WORDS layout, words 24..35) with fmaf and one hardware reciprocal -- a few ulp
+// from the two-step pts_into_camera / project_to_image, far below the 16-bit operands.
+// x, y, zc as sd_project; rz = 1 / max(zc, eps) (the z~ input of the code).
+template <typename CP>
+__device__ __forceinline__ void sd_project_fast(CP cam, float px, float py, float pz, float &x,
+                                                float &y, float &zc, float &rz) {
+    CP P = cam + 24;
+    const float i0 = fmaf(P[0], px, fmaf(P[1], py, fmaf(P[2], pz, P[3])));
+    const float i1 = fmaf(P[4], px, fmaf(P[5], py, fmaf(P[6], pz, P[7])));
+    const float i2 = fmaf(P[8], px, fmaf(P[9], py, fmaf(P[10], pz, P[11])));
+    rz = __builtin_amdgcn_rcpf(fmaxf(i2, SD_EPS));
+    x = i0 * rz;
+    y = i1 * rz;
+    zc = i2;
+}
+
+// Frustum mask of a fast projection, bit-exact with sd_outside on the two-step one: only
+// points within 1e-4 of a frustum plane can differ, and those (a divergent, rarely taken
+// branch) are re-projected the reference way.
+template <typename CP>
+__device__ __forceinline__ bool sd_outside_exact(CP cam, float px, float py, float pz, float x,
+                                                 float y, float zc) {
+    bool inv = sd_outside(x, y, zc);
+    const bool edge = fabsf(fabsf(x) - 1.f) < 1e-4f || fabsf(fabsf(y) - 1.f) < 1e-4f ||
+                      fabsf(zc - SD_EPS) < 1e-4f;
+    if (edge) {
+        float xe, ye, ze;
+        sd_project(cam, px, py, pz, xe, ye, ze);
+        inv = sd_outside(xe, ye, ze);
+    }
+    return inv;
+}
+
+template <typename CP>
+__device__ __forceinline__ PointGeo sd_point_geo_fast(CP cam, float px, float py, float pz, int Wf,
+                                                      int Hf) {
+    PointGeo g;
+    float x, y, zc, rz;
+    sd_project_fast(cam, px, py, pz, x, y, zc, rz);
+    g.inv_f = sd_outside_exact(cam, px, py, pz, x, y, zc);
+    x = fminf(fmaxf(x, -2.f), 2.f);
+    y = fminf(fmaxf(y, -2.f), 2.f);
+    const float zt = (rz - (float)(1.0 / 80.0)) * (float)(1.0 / (1.0 / 3.0 - 1.0 / 80.0));
+    g.v[0] = x; g.v[1] = y; g.v[2] = 2.f * zt - 1.f;
+    g.t = sd_taps(x, y, Wf, Hf);
+    return g;
+}
+
+template <typename CP>
+__device__ __forceinline__ Taps sd_color_taps_fast(CP cam, int Wc, int Hc, float px, float py,
+                                                   float pz, bool &inv) {
+    float x, y, zc, rz;
+    sd_project_fast(cam, px, py, pz, x, y, zc, rz);
+    inv = sd_outside_exact(cam, px, py, pz, x, y, zc);  // (clamping x, y to +-2 keeps it)
+    x = fminf(fmaxf(x, -2.f), 2.f);
+    y = fminf(fmaxf(y, -2.f), 2.f);
+    return sd_taps(x, y, Wc, Hc);
+}
+
 __device__ __forceinline__ uint4 sd_ld128(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff) {
 #if SD_ABL_NOLOAD  // diagnostic timing build only: the gather replaced by register values
     (void)rs;

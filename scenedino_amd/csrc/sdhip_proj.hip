@@ -266,7 +266,7 @@ k_render_proj(const sd_render_args a, const sd_head m, const int32_t *__restrict
             c.sub = 0;
             c.n++;
             c.rr = rmap(c.ray);
-            c.sbi = (int)((unsigned)c.rr / (unsigned)rps);
+            c.sbi = __builtin_amdgcn_readfirstlane((int)((unsigned)c.rr / (unsigned)rps));
         }
         return c;
     };
@@ -319,13 +319,13 @@ k_render_proj(const sd_render_args a, const sd_head m, const int32_t *__restrict
             if (64 * p < K && k < K) {
                 const float z0 = zq[2 * p], z1 = zq[2 * p + 1];
                 const float px = ox + z0 * dx, py = oy + z0 * dy, pz = oz + z0 * dz;  // nerf.py:252
-                PointGeo geo = sd_point_geo<true>((sd_cfloat *)(a.cam_f + sbi * 21), px, py, pz, a.Wf, a.Hf);
+                PointGeo geo = sd_point_geo_fast((sd_cfloat *)(a.cam_f + sbi * SD_CAM_WORDS), px, py, pz, a.Wf, a.Hf);
                 float col[3 * SD_MAX_NV];
                 uint32_t invc = 0;
                 const float delta = (k + 1 < K) ? (z1 - z0) : 1e10f;
                 if (DEFER && p == 0) {
                     bool ic;
-                    const Taps tc = sd_color_taps((sd_cfloat *)(a.cam_c + sbi * 21), a.Wc, a.Hc,
+                    const Taps tc = sd_color_taps_fast((sd_cfloat *)(a.cam_c + sbi * SD_CAM_WORDS), a.Wc, a.Hc,
                                                   px, py, pz, ic);
                     sd_color_issue(a.img + (int64_t)sbi * cplane, tc, cpend);
                     cpend.delta = delta;
@@ -336,9 +336,9 @@ k_render_proj(const sd_render_args a, const sd_head m, const int32_t *__restrict
                     col[3 * v] = col[3 * v + 1] = col[3 * v + 2] = 0.f;
                     if (v < nv && !(DEFER && p == 0)) {
                         const bool ic = NV == 1
-                            ? sd_color_view((sd_cfloat *)(a.cam_c + sbi * 21), a.img + (int64_t)sbi * cplane,
+                            ? sd_color_view((sd_cfloat *)(a.cam_c + sbi * SD_CAM_WORDS), a.img + (int64_t)sbi * cplane,
                                             a.Wc, a.Hc, px, py, pz, col)
-                            : sd_color_view((sd_cfloat *)(a.cam_c + (sbi * nv + v) * 21),
+                            : sd_color_view((sd_cfloat *)(a.cam_c + (sbi * nv + v) * SD_CAM_WORDS),
                                             a.img + (int64_t)(sbi * nv + v) * cplane, a.Wc, a.Hc,
                                             px, py, pz, col + 3 * v);
                         invc |= (ic ? 1u : 0u) << v;
@@ -511,7 +511,7 @@ k_render_proj(const sd_render_args a, const sd_head m, const int32_t *__restrict
 #pragma unroll
         for (int s = 0; s < 4; ++s) sg = Tr::mma(lw[SD_LDS_SIG + s * SD_WAVE + lane], X[s], sg);
         const float sv = sg[0] + m.b_sigma;
-        const float sigma = sv > 20.f ? sv : __logf(1.f + __expf(sv));
+        const float sigma = sd_softplus_fast(sv);
 
         // alpha compositing (nerf.py:376-389)
         const int k = cur.sub * 16 + j;

@@ -139,15 +139,29 @@ __global__ void __launch_bounds__(256) k_pack_image(const float *__restrict__ in
     *(f32x4 *)(out + gid * 4) = v;
 }
 
-// Camera records [w2c rows 0..2 | K] (21 floats) for n views; one thread per word.
+// Camera records (SD_CAM_WORDS floats, include/sdhip.h) for n views; one thread per word.
+// The fused projection K . w2c[:3] is accumulated in f64 and rounded once.
 __global__ void __launch_bounds__(256) k_cam_records(const float *__restrict__ w2c, int64_t s_w,
                                                      const float *__restrict__ Ks, int64_t s_k,
                                                      int64_t n, float *__restrict__ out) {
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= n * 21) return;
-    const int64_t v = gid / 21;
-    const int e = (int)(gid - v * 21);
-    out[gid] = e < 12 ? w2c[v * s_w + e] : Ks[v * s_k + (e - 12)];
+    if (gid >= n * SD_CAM_WORDS) return;
+    const int64_t v = gid / SD_CAM_WORDS;
+    const int e = (int)(gid - v * SD_CAM_WORDS);
+    const float *w = w2c + v * s_w, *k = Ks + v * s_k;
+    float r;
+    if (e < 12) {
+        r = w[e];
+    } else if (e < 21) {
+        r = k[e - 12];
+    } else if (e < 24) {
+        r = 0.f;
+    } else {
+        const int i = (e - 24) >> 2, c = (e - 24) & 3;
+        r = (float)((double)k[3 * i] * w[c] + (double)k[3 * i + 1] * w[4 + c] +
+                    (double)k[3 * i + 2] * w[8 + c]);
+    }
+    out[gid] = r;
 }
 
 // ---------------------------------------------------------------------------
@@ -254,7 +268,7 @@ extern "C" int sd_cam_records(const float *w2c, int64_t s_w, const float *Ks, in
         return -1;
     }
     if (n == 0) return 0;
-    hipLaunchKernelGGL(k_cam_records, dim3((unsigned)((n * 21 + 255) / 256)), dim3(256), 0,
+    hipLaunchKernelGGL(k_cam_records, dim3((unsigned)((n * SD_CAM_WORDS + 255) / 256)), dim3(256), 0,
                        (hipStream_t)stream, w2c, s_w, Ks, s_k, n, out);
     SD_CHECK_LAUNCH("sd_cam_records");
     return 0;

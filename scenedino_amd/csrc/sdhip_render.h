@@ -125,13 +125,38 @@ __device__ __forceinline__ typename T16<P>::Frag sd_blend_plain(const uint4 &a, 
 #define SD_DPP0(x, ctrl) \
     __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, (x)), (ctrl), 0xf, 0xf, true))
 
-// inclusive product scan over the 16 lanes of every row (row_shr 1, 2, 4, 8)
+// inclusive product scan over the 16 lanes of every row (row_shr 1, 2, 4, 8): one
+// v_mul_f32_dpp per step, x = x[l - s] * x in place; a lane whose source lies before its
+// row start is not written (bound_ctrl off) and so keeps x, the product with 1.  The
+// s_nop 1 covers the VALU-write -> DPP-read hazard of every step.
+#ifndef SD_SCAN_ASM
+#define SD_SCAN_ASM 1
+#endif
 __device__ __forceinline__ float sd_scan_mul16(float x) {
+#if !SD_SCAN_ASM
     x *= SD_DPP1(x, 0x111);
     x *= SD_DPP1(x, 0x112);
     x *= SD_DPP1(x, 0x114);
     x *= SD_DPP1(x, 0x118);
     return x;
+#endif
+    asm("s_nop 1\n\tv_mul_f32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\tv_mul_f32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\tv_mul_f32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\tv_mul_f32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf"
+        : "+v"(x));
+    return x;
+}
+
+// torch softplus (beta 1, threshold 20) on the hardware exp2 / log2 (16-bit render
+// modes: ~1e-7 relative, far below the operand rounding)
+#ifndef SD_SP_FAST
+#define SD_SP_FAST 0  // 1: raw exp2 / log2 softplus (fewer VALU, measured slower in k_render_tile)
+#endif
+__device__ __forceinline__ float sd_softplus_fast(float x) {
+    if (!SD_SP_FAST) return x > 20.f ? x : __logf(1.f + __expf(x));
+    const float l = __builtin_amdgcn_logf(1.f + __builtin_amdgcn_exp2f(x * 1.4426950408889634f));
+    return x > 20.f ? x : l * 0.6931471805599453f;
 }
 // sum over the 16 lanes of every row, result in every lane (row_ror 8, 4, 2, 1)
 __device__ __forceinline__ float sd_rowsum16(float x) {

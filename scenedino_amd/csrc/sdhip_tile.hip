@@ -42,6 +42,9 @@
 #ifndef ST_PIPE
 #define ST_PIPE 0           // 1: item i + 1's MLP beside item i's compositing (measured slower)
 #endif
+#ifndef ST_HC_MFMA
+#define ST_HC_MFMA 0        // 1: hidden-space compositing as MFMA (transpose + contract; measured slower)
+#endif
 #ifndef ST_ABL_NOHEAD
 #define ST_ABL_NOHEAD 0
 #endif
@@ -70,6 +73,49 @@
 #define ST_ABL_NOSIG 0
 #endif
 
+// diagnostic build only (ST_PROF=1): per-phase s_memtime cycles summed over all waves
+#ifndef ST_PROF
+#define ST_PROF 0
+#endif
+#if ST_PROF
+__device__ unsigned long long st_prof[32];
+#define ST_T(i)                                                  \
+    {                                                            \
+        const uint64_t _t = __builtin_amdgcn_s_memtime();        \
+        pacc[i] += (uint32_t)(_t - tlast);                       \
+        tlast = _t;                                              \
+    }
+extern "C" int sd_tile_prof(unsigned long long *out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(st_prof), sizeof(st_prof)) != hipSuccess) return -2;
+    if (reset) {
+        unsigned long long z[32] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(st_prof), z, sizeof(z)) != hipSuccess) return -2;
+    }
+    return 0;
+}
+#else
+#define ST_T(i)
+#endif
+#if ST_PROF >= 2  // item sub-phases (each marker also drains LDS: diagnostic only)
+#define ST_T2(i) ST_T(i)
+#else
+#define ST_T2(i)
+#endif
+
+#ifndef ST_CODE_FIRST
+#define ST_CODE_FIRST 0     // 1: positional-code MFMAs before the tap blend (spills)
+#endif
+#ifndef ST_FASTPROJ
+#define ST_FASTPROJ 1       // fused-record projection (0: the two-step reference one)
+#endif
+#if ST_FASTPROJ
+#define ST_GEO sd_point_geo_fast
+#define ST_CTAPS sd_color_taps_fast
+#else
+#define ST_GEO sd_point_geo<true>
+#define ST_CTAPS sd_color_taps
+#endif
+
 struct st_args {
     sd_render_args a;
     sd_head m;
@@ -85,7 +131,8 @@ struct st_args {
 #define ST_L_BOX (ST_L_SIG + 4 * 64 * 16)      // [2][8 waves][2] u32 (min, max) packed
 #define ST_L_HS (ST_L_BOX + 2 * 8 * 8)         // [8 rays][128] 16-bit hidden sums
 #define ST_L_WS (ST_L_HS + 8 * 128 * 2)        // [8] f32 weight sums
-#define ST_L_REC (ST_L_WS + 8 * 4)             // records: [8 waves][2][K] x 40 B
+#define ST_L_RAY (ST_L_WS + 8 * 4)             // [8 waves][2] x 32 B ray words 0..7 (LDS-DMA)
+#define ST_L_REC (ST_L_RAY + 8 * 2 * 32)       // records: [8 waves][2][K] x 40 B
 static_assert(ST_L_REC % 16 == 0, "record area alignment");
 
 __host__ __device__ constexpr int st_rec_bytes(int K) { return ST_WAVES * 2 * K * 40; }
@@ -127,6 +174,35 @@ __device__ __forceinline__ void st_barrier_lds() {
 }
 
 typedef __attribute__((address_space(3))) void lds_void;
+
+// LDS-DMA (global_load_lds) as inline asm.  Issued through the builtin, the compiler
+// treats every later LDS read as a possible alias of the in-flight DMA and puts an
+// s_waitcnt vmcnt(0) in front of it -- the item loop then waits for the next tile's DMA
+// at its first record read.  The kernel orders these DMAs itself (s_waitcnt vmcnt(0) +
+// barrier before the staged data is read); vector-memory returns are in order, so the
+// compiler's own vmcnt waits stay conservative with these extra loads in flight.
+// (m0 = LDS destination of lane 0; one wait state between the SALU write and the DMA.)
+#ifndef ST_DMA_ASM
+#define ST_DMA_ASM 1
+#endif
+__device__ __forceinline__ void st_dma16(const void *src, uint32_t lds_addr) {
+    lds_addr = __builtin_amdgcn_readfirstlane(lds_addr);  // wave-uniform by construction
+    if (!ST_DMA_ASM) {
+        __builtin_amdgcn_global_load_lds(src, (lds_void *)(uintptr_t)lds_addr, 16, 0, 0);
+        return;
+    }
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+                 :: "v"(src), "s"(lds_addr) : "memory");
+}
+__device__ __forceinline__ void st_dma4(const void *src, uint32_t lds_addr) {
+    lds_addr = __builtin_amdgcn_readfirstlane(lds_addr);
+    if (!ST_DMA_ASM) {
+        __builtin_amdgcn_global_load_lds(src, (lds_void *)(uintptr_t)lds_addr, 4, 0, 0);
+        return;
+    }
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off"
+                 :: "v"(src), "s"(lds_addr) : "memory");
+}
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 
 __device__ __forceinline__ uint2 st_tr(uint32_t addr) {
@@ -134,7 +210,10 @@ __device__ __forceinline__ uint2 st_tr(uint32_t addr) {
     return __builtin_bit_cast(uint2, v);
 }
 
-template <int P>
+// ZIN: depths given (args.z, parity tests) instead of drawn in the kernel.  A template
+// parameter, not a branch: with both paths in one body the compiler's wait for the z loads
+// also drains the head-weight prefetch on the drawing path.
+template <int P, bool ZIN>
 __global__ void __launch_bounds__(ST_WG) __attribute__((amdgpu_waves_per_eu(2)))
 k_render_tile(const st_args sa) {
     typedef T16<P> Tr;
@@ -144,6 +223,10 @@ k_render_tile(const st_args sa) {
     const sd_render_args &a = sa.a;
     const sd_head &m = sa.m;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+#if ST_PROF
+    uint32_t pacc[19] = {};
+    uint64_t tlast = __builtin_amdgcn_s_memtime();
+#endif
     {
         const uint4 *pe = (const uint4 *)m.w_pe, *sg = (const uint4 *)m.w_sig;
         uint4 *d = (uint4 *)lds;
@@ -185,15 +268,23 @@ k_render_tile(const st_args sa) {
     const int64_t cplane = (int64_t)a.Hc * a.Wc * 4;
 
     // ---- ray pass: lane = sample k = 64 p + lane --------------------------------------
+    // ray words 0..7 (origin, direction, near, far) of a later step's ray, fetched by
+    // LDS-DMA one step ahead (completed by the step's closing vmcnt(0)), so the ray pass
+    // reads them from LDS instead of waiting on scalar loads
+    const int nrw = min(a.ray_dim, 8);
+    auto ray_fetch = [&](int ray, int slot) {
+        if (ray < R && lane < nrw)
+            st_dma4(a.rays + (int64_t)ray * a.ray_dim + lane, lds0 + ST_L_RAY + (wave * 2 + slot) * 32);
+    };
+    const float *rl = nullptr;  // this ray pass's words (set by ray_pass)
     auto load_ray_z = [&](int ray, float zq[2 * ST_MAXP]) {
         float zo[ST_MAXP];
-        if (a.z) {
+        if (ZIN) {
             const float *zr = a.z + (int64_t)ray * K;
 #pragma unroll
             for (int p = 0; p < ST_MAXP; ++p) zo[p] = zr[min(64 * p + lane, K - 1)];
         } else {
-            sd_cfloat *rr = (sd_cfloat *)(a.rays + (int64_t)ray * a.ray_dim);
-            const float near = rr[6], far = rr[7];
+            const float near = rl[6], far = rl[7];
             const uint64_t base = a.z_offset + (uint64_t)ray * (uint64_t)K;
             zo[1] = 0.f;
 #pragma unroll
@@ -223,11 +314,14 @@ k_render_tile(const st_args sa) {
     auto ray_pass = [&](int ray, int buf, int slot) {
         uint32_t bmin = 0xffffffffu, bmax = 0u;
         if (ray < R) {
-            const int sbi = (int)((unsigned)ray / (unsigned)rps);
+            // wave-uniform (readfirstlane: the u32 divide runs on the VALU, and a VGPR
+            // address would turn the camera-record reads into vector loads)
+            const int sbi = __builtin_amdgcn_readfirstlane((int)((unsigned)ray / (unsigned)rps));
+            rl = (const float *)(lds + ST_L_RAY + (wave * 2 + slot) * 32);
             float zq[2 * ST_MAXP];
             load_ray_z(ray, zq);
-            sd_cfloat *rr = (sd_cfloat *)(a.rays + (int64_t)ray * a.ray_dim);
-            const float ox = rr[0], oy = rr[1], oz = rr[2], dx = rr[3], dy = rr[4], dz = rr[5];
+            ST_T(10);
+            const float ox = rl[0], oy = rl[1], oz = rl[2], dx = rl[3], dy = rl[4], dz = rl[5];
             uint4 *r0 = rq0(buf);
             f32x4 *r1 = rq1(buf);
             float2 *rc = rqc(buf);
@@ -237,11 +331,11 @@ k_render_tile(const st_args sa) {
                 if (64 * p < K && k < K) {
                     const float z0 = zq[2 * p];
                     const float px = ox + z0 * dx, py = oy + z0 * dy, pz = oz + z0 * dz;  // nerf.py:252
-                    const PointGeo geo = sd_point_geo<true>((sd_cfloat *)(a.cam_f + sbi * 21), px, py, pz,
+                    const PointGeo geo = ST_GEO((sd_cfloat *)(a.cam_f + sbi * SD_CAM_WORDS), px, py, pz,
                                                             Wf, Hf);
                     const uint32_t x0 = (uint32_t)geo.t.x0, y0 = (uint32_t)geo.t.y0;
                     bool ic;
-                    const Taps tc = sd_color_taps((sd_cfloat *)(a.cam_c + sbi * 21), a.Wc, a.Hc, px, py,
+                    const Taps tc = ST_CTAPS((sd_cfloat *)(a.cam_c + sbi * SD_CAM_WORDS), a.Wc, a.Hc, px, py,
                                                   pz, ic);
                     const uint32_t xy = x0 | (y0 << 15) | (geo.inv_f ? 1u << 30 : 0u) |
                                         (ic ? 1u << 31 : 0u);
@@ -263,8 +357,10 @@ k_render_tile(const st_args sa) {
                 }
             }
         }
+        ST_T(11);
         bmin = st_wave_min2(bmin);
         bmax = st_wave_max2(bmax);
+        ST_T(12);
         if (lane == 0) *(uint2 *)(lds + ST_L_BOX + (slot * ST_WAVES + wave) * 8) = uint2{bmin, bmax};
     };
     auto ray_col = [&](int ray, int buf) {
@@ -321,8 +417,7 @@ k_render_tile(const st_args sa) {
             const int tx = (int)n - ty * t.pitch;
             const int sx = min(max(t.bx0 + tx, 0), Wf - 1), sy = min(max(t.by0 + ty, 0), Hf - 1);
             const uint8_t *src = plane + ((int64_t)sy * Wf + sx) * 256 + (part < 16u ? part : 0u) * 16u;
-            if (!ST_ABL_NODMA) __builtin_amdgcn_global_load_lds((const void *)src,
-                                             (lds_void *)(lds + dst0 + (uint32_t)i * 1024u), 16, 0, 0);
+            if (!ST_ABL_NODMA) st_dma16(src, lds0 + dst0 + (uint32_t)i * 1024u);
         }
         return t;
     };
@@ -375,11 +470,18 @@ k_render_tile(const st_args sa) {
     const bool bc0 = bsel && (j >> 3) == 0, bc1 = bsel && (j >> 3) == 1;
     const bool br1 = (j & 1) != 0;
     const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+    // identity B operand of the 16x16x16 transposition (lane (n, g): rows 4 g + e)
+    const Frag4 Iden = __builtin_bit_cast(
+        Frag4, uint2{sd_pack2<E>(4 * g == j ? 1.f : 0.f, 4 * g + 1 == j ? 1.f : 0.f),
+                     sd_pack2<E>(4 * g + 2 == j ? 1.f : 0.f, 4 * g + 3 == j ? 1.f : 0.f)});
 
     // ---- prologue: records + tile of step 0 -------------------------------------------
     int grp = gfirst;
     int ray = 8 * grp + wave;
-    int sbi = (int)((unsigned)min(8 * grp, R - 1) / (unsigned)rps);
+    int sbi = __builtin_amdgcn_readfirstlane((int)((unsigned)min(8 * grp, R - 1) / (unsigned)rps));
+    ray_fetch(ray, 0);
+    ray_fetch(8 * (grp + nwg) + wave, 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     ray_pass(ray, 0, 0);
     ray_col(ray, 0);
     st_barrier_lds();
@@ -388,12 +490,17 @@ k_render_tile(const st_args sa) {
     __syncthreads();
 
     int prev_grp = -1, prev_ok = 0;
+#if ST_PROF
+#pragma unroll
+    for (int i = 0; i < 19; ++i) pacc[i] = 0;
+    tlast = __builtin_amdgcn_s_memtime();
+#endif
     for (int n = 0; n < nsteps; ++n) {
         const int buf = n & 1;
         const bool has_next = n + 1 < nsteps;
         const int ngrp = grp + nwg;
         const int nray = 8 * ngrp + wave;
-        const int nsbi = has_next ? (int)((unsigned)min(8 * ngrp, R - 1) / (unsigned)rps) : 0;
+        const int nsbi = has_next ? __builtin_amdgcn_readfirstlane((int)((unsigned)min(8 * ngrp, R - 1) / (unsigned)rps)) : 0;
         const bool active = cur.ok && ray < R;
         const uint32_t tileb = lds0 + tile0 + (uint32_t)buf * (uint32_t)sa.tile_bytes;
         const int toff = (tq & 1) + (tq >> 1) * cur.pitch;
@@ -438,12 +545,58 @@ k_render_tile(const st_args sa) {
                                  lane_off;
             // block-diagonal weight fragments of the two K-chunks
             const uint32_t w01 = q0.y, w23 = q0.z;
+            ST_T2(13);
             const uint4 b0 = {bc0 && !br1 ? w01 : 0u, bc0 && !br1 ? w23 : 0u,
                               bc0 && br1 ? w01 : 0u, bc0 && br1 ? w23 : 0u};
             const uint4 b1 = {bc1 && !br1 ? w01 : 0u, bc1 && !br1 ? w23 : 0u,
                               bc1 && br1 ? w01 : 0u, bc1 && br1 ? w23 : 0u};
             const Frag B0 = __builtin_bit_cast(Frag, b0), B1 = __builtin_bit_cast(Frag, b1);
             f32x4 acc[8];
+#if ST_CODE_FIRST
+            // code columns first: they need only the record, so the tap reads' latency
+            // overlaps the code evaluation and its MFMAs
+            ST_T2(14);
+            // positional-code columns
+            const int lo = sd_opaque0();
+            const Frag *lw = lf + lo;
+            {
+                Frag f0;
+                Frag4 f1;
+#if ST_ABL_NOPE
+                for (int e = 0; e < 8; ++e) f0[e] = (E)v[e % 3];
+                f1 = __builtin_bit_cast(Frag4, uint2{__builtin_bit_cast(uint32_t, v[0]), 0u});
+#else
+                sd_code_frags<Frag, Frag4, E>(v, g, f0, f1);
+#endif
+                const Frag4 *lw1 = (const Frag4 *)(lds + ST_L_PE1) + lo;
+                // all 16x16x32 steps first, then the 16x16x16 ones: a 16x16x16 MFMA whose
+                // accumulator input is the result of the directly preceding 16x16x32 MFMA
+                // read a stale accumulator (hipcc 7.2, gfx950, VGPR-form accumulators)
+#pragma unroll
+                for (int t = 0; t < 8; ++t)
+                    if (!ST_ABL_NOCODE || t == 0)
+                        acc[t] = Tr::mma(lw[ST_L_PE / 16 + t * SD_WAVE + lane], f0, ST_CODE_FIRST ? zero4 : acc[t]);
+#pragma unroll
+                for (int t = 0; t < 8; ++t)
+                    if (!ST_ABL_NOCODE || t == 0)
+                        acc[t] = Tr::mma16(lw1[t * SD_WAVE + lane], f1, acc[t]);
+            }
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+#if ST_ABL_NOTR
+                const uint2 a00 = {base[0][0] + t, base[0][1]}, a01 = {base[1][0], base[1][1] + t};
+                const uint2 a10 = a01, a11 = a00;
+#else
+                const uint2 a00 = st_tr(base[0][0] + 32u * t), a01 = st_tr(base[0][1] + 32u * t);
+                const uint2 a10 = st_tr(base[1][0] + 32u * t), a11 = st_tr(base[1][1] + 32u * t);
+#endif
+                const Frag A0 = __builtin_bit_cast(Frag, uint4{a00.x, a00.y, a01.x, a01.y});
+                const Frag A1 = __builtin_bit_cast(Frag, uint4{a10.x, a10.y, a11.x, a11.y});
+                acc[t] = Tr::mma(A0, B0, ST_CODE_FIRST ? acc[t] : zero4);
+                acc[t] = Tr::mma(A1, B1, acc[t]);
+            }
+            ST_T2(14);
+#else
 #pragma unroll
             for (int t = 0; t < 8; ++t) {
 #if ST_ABL_NOTR
@@ -458,6 +611,7 @@ k_render_tile(const st_args sa) {
                 acc[t] = Tr::mma(A0, B0, zero4);
                 acc[t] = Tr::mma(A1, B1, acc[t]);
             }
+            ST_T2(14);
             // positional-code columns
             const int lo = sd_opaque0();
             const Frag *lw = lf + lo;
@@ -483,6 +637,7 @@ k_render_tile(const st_args sa) {
                     if (!ST_ABL_NOCODE || t == 0)
                         acc[t] = Tr::mma16(lw1[t * SD_WAVE + lane], f1, acc[t]);
             }
+#endif
 #pragma unroll
             for (int s2 = 0; s2 < 4; ++s2) {
                 const uint4 u = {sd_relu2(sd_pack2<E>(acc[2 * s2][0], acc[2 * s2][1])),
@@ -494,11 +649,12 @@ k_render_tile(const st_args sa) {
 #if ST_ABL_NOSIG
             const float sigma = __builtin_bit_cast(float, __builtin_bit_cast(uint4, st.X[0]).x & 0x3fffffffu) + m.b_sigma;
 #else
+            ST_T2(15);
             f32x4 sg = zero4;
 #pragma unroll
             for (int s2 = 0; s2 < 4; ++s2) sg = Tr::mma(lw[ST_L_SIG / 16 + s2 * SD_WAVE + lane], st.X[s2], sg);
             const float sv = sg[0] + m.b_sigma;
-            const float sigma = sv > 20.f ? sv : __logf(1.f + __expf(sv));
+            const float sigma = sd_softplus_fast(sv);
 #endif
             // alpha compositing (nerf.py:376-389)
             float alpha = 1.f - __expf(-fabsf(delta) * fmaxf(sigma, 0.f));
@@ -507,6 +663,7 @@ k_render_tile(const st_args sa) {
             st.alpha = alpha;
             st.excl = SD_DPP1(incl, 0x111);
             st.tmul = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, incl), 15));
+            ST_T2(16);
         };
         auto itemB = [&](int sub, const IState &st) {
             const int k = sub * 16 + j;
@@ -517,7 +674,7 @@ k_render_tile(const st_args sa) {
             cpart[0] += w * st.col[0];
             cpart[1] += w * st.col[1];
             cpart[2] += w * st.col[2];
-            // hidden-space compositing: hacc += w relu(h), two hidden per v_dot2
+#if !ST_HC_MFMA
             const uint32_t wl = sd_pack2<E>(w, 0.f), wh = sd_pack2<E>(0.f, w);
 #pragma unroll
             for (int s2 = 0; s2 < 4; ++s2) {
@@ -526,11 +683,40 @@ k_render_tile(const st_args sa) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const int t = 2 * s2 + (q >> 1), r = 2 * (q & 1);
-                    if (ST_ABL_NOHC && (s2 | q)) continue;
                     hacc[t][r] = Tr::dot2(d4[q], wl, hacc[t][r]);
                     hacc[t][r + 1] = Tr::dot2(d4[q], wh, hacc[t][r + 1]);
                 }
             }
+#else
+            // hidden-space compositing hc[t] += sum_k w_k relu(h_k) as MFMA over the item's
+            // 16 samples.  The MLP tiles hold sample j on the lane axis (lane (j, g):
+            // hidden 16 t + 4 g + r), but an MFMA contracts along the lane-group axis, so
+            // each relu tile is first transposed by an MFMA with the identity (exact), then
+            // contracted with the weights: A[m][k] = w_k on every row (samples 4 g + e
+            // gathered by ds_bpermute), B[k][n] = relu(h_k)[16 t + n].
+            const int wsrc = g << 4;  // ds_bpermute byte address of lane 4 g (sample 4 g)
+            const float w0 = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(wsrc + 0, __builtin_bit_cast(int, w)));
+            const float w1 = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(wsrc + 4, __builtin_bit_cast(int, w)));
+            const float w2 = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(wsrc + 8, __builtin_bit_cast(int, w)));
+            const float w3 = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(wsrc + 12, __builtin_bit_cast(int, w)));
+            const Frag4 Aw = __builtin_bit_cast(Frag4, uint2{sd_pack2<E>(w0, w1), sd_pack2<E>(w2, w3)});
+            ST_T2(17);
+#pragma unroll
+            for (int s2 = 0; s2 < 4; ++s2) {
+                const uint4 u = __builtin_bit_cast(uint4, st.X[s2]);
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int t = 2 * s2 + h;
+                    if (ST_ABL_NOHC && t) continue;
+                    const Frag4 xa = __builtin_bit_cast(Frag4, h ? uint2{u.z, u.w} : uint2{u.x, u.y});
+                    const f32x4 xt = Tr::mma16(xa, Iden, zero4);
+                    const Frag4 xb = __builtin_bit_cast(Frag4, uint2{sd_pack2<E>(xt[0], xt[1]),
+                                                                     sd_pack2<E>(xt[2], xt[3])});
+                    hacc[t] = Tr::mma16(Aw, xb, hacc[t]);
+                }
+            }
+#endif
+            ST_T2(18);
             const int64_t rk = (int64_t)ray * K;
             if (g == 0) {
                 if (a.weights) (a.weights + rk)[k] = w;
@@ -547,13 +733,19 @@ k_render_tile(const st_args sa) {
         // item 0 with the next ray's pass and the previous group's head
         if (prev_ok && !ST_ABL_NOHEAD) head_prefetch();
         if (has_next && (!ST_ABL_NORAY || n == 0)) ray_pass(nray, buf ^ 1, buf ^ 1);
+        ST_T(0);
         if (prev_ok && !ST_ABL_NOHEAD) head(prev_grp);
+        ST_T(1);
         IState s0, s1;
         if (active && !ST_ABL_NOITEM) itemA(0, s0);
+        ST_T(2);
         if (has_next && (!ST_ABL_NORAY || n == 0)) ray_col(nray, buf ^ 1);
+        ST_T(3);
         st_barrier_lds();  // X: next boxes visible; the head has read the hsum area
+        ST_T(4);
         Tile nxt = {0, 0, 1, 0};
         if (has_next) nxt = stage(buf ^ 1, buf ^ 1, ngrp, nsbi);
+        ST_T(5);
 #if ST_PIPE
         if (active && !ST_ABL_NOITEM) {
             // items 1 .. nsub-1, item i + 1's A beside item i's B (ping-pong states)
@@ -581,11 +773,20 @@ k_render_tile(const st_args sa) {
             }
         }
 #endif
+        ST_T(6);
         if (active) {
             // ray epilogue: sums over the 16 sample lanes of every row
             const float dsum = sd_rowsum16(dpart), wsum = sd_rowsum16(wpart);
             const float c0s = sd_rowsum16(cpart[0]), c1s = sd_rowsum16(cpart[1]),
                         c2s = sd_rowsum16(cpart[2]);
+#if ST_HC_MFMA
+            // hacc[t]: lane (n, g) holds hidden 16 t + n (every row alike)
+            uint16_t *hs = (uint16_t *)(lds + ST_L_HS + wave * 256);
+            if (g == 0) {
+#pragma unroll
+                for (int t = 0; t < 8; ++t) hs[16 * t + j] = Tr::bits(hacc[t][0]);
+            }
+#else
             uint8_t *hs = lds + ST_L_HS + wave * 256;
 #pragma unroll
             for (int t = 0; t < 8; ++t) {
@@ -597,6 +798,7 @@ k_render_tile(const st_args sa) {
                     *(uint2 *)(hs + (16 * t + 4 * g) * 2) =
                         uint2{sd_pack2<E>(vsum[0], vsum[1]), sd_pack2<E>(vsum[2], vsum[3])};
             }
+#endif
             if (lane == 0) {
                 *(float *)(lds + ST_L_WS + wave * 4) = wsum;
                 a.depth[(int64_t)ray * a.ld_depth] = dsum;
@@ -604,19 +806,32 @@ k_render_tile(const st_args sa) {
                 rp[0] = c0s; rp[1] = c1s; rp[2] = c2s;
             }
         }
+        ST_T(7);
         prev_grp = grp;
         prev_ok = cur.ok;
         grp = ngrp;
         ray = nray;
         sbi = nsbi;
         cur = nxt;
+        if (n + 2 < nsteps) ray_fetch(8 * (ngrp + nwg) + wave, buf);  // ray of step n + 2
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed
+        ST_T(8);
         st_barrier_lds();  // Y: next tile complete; hsum of this group written
+        ST_T(9);
     }
     if (prev_ok) {
         head_prefetch();
         head(prev_grp);
     }
+#if ST_PROF
+    if (lane < 19) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int i = 0; i < 19; ++i) v = lane == i ? pacc[i] : v;
+        atomicAdd(&st_prof[lane], (unsigned long long)v);
+    }
+    if (lane == 0) atomicAdd(&st_prof[31], 1ull);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -665,14 +880,15 @@ extern "C" int sd_render_tile_launch(const sd_render_args *a, const sd_head *m, 
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
         ncu = 256;
+    auto go = [&](auto kern) {
+        (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+        hipLaunchKernelGGL(kern, dim3((unsigned)ncu), dim3(ST_WG), lds_bytes, s, sa);
+    };
+    const bool zin = a->z != nullptr;
     if (m->dtype == SD_F16) {
-        (void)hipFuncSetAttribute((const void *)k_render_tile<SD_F16>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
-        hipLaunchKernelGGL(k_render_tile<SD_F16>, dim3((unsigned)ncu), dim3(ST_WG), lds_bytes, s, sa);
+        if (zin) go(k_render_tile<SD_F16, true>); else go(k_render_tile<SD_F16, false>);
     } else {
-        (void)hipFuncSetAttribute((const void *)k_render_tile<SD_BF16>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
-        hipLaunchKernelGGL(k_render_tile<SD_BF16>, dim3((unsigned)ncu), dim3(ST_WG), lds_bytes, s, sa);
+        if (zin) go(k_render_tile<SD_BF16, true>); else go(k_render_tile<SD_BF16, false>);
     }
     return sd_check_last("sd_render_proj (tile kernel)");
 }

@@ -89,7 +89,7 @@ k_field_gather(const float *__restrict__ xyz, int64_t B, int64_t P,
         if (lane < n) {
             const int64_t p = p0 + lane;
             const int64_t b = p / P;
-            const PointGeo geo = sd_point_geo(cam_f + b * 21, xyz[p * 3], xyz[p * 3 + 1],
+            const PointGeo geo = sd_point_geo(cam_f + b * SD_CAM_WORDS, xyz[p * 3], xyz[p * 3 + 1],
                                               xyz[p * 3 + 2], Wf, Hf);
             gi[0] = geo.t.i00; gi[1] = geo.t.i01; gi[2] = geo.t.i10; gi[3] = geo.t.i11;
             gw[0] = geo.t.w00; gw[1] = geo.t.w01; gw[2] = geo.t.w10; gw[3] = geo.t.w11;
@@ -157,7 +157,7 @@ k_field_gather(const float *__restrict__ xyz, int64_t B, int64_t P,
             const int64_t b = p / P;
             const float px = xyz[p * 3], py = xyz[p * 3 + 1], pz = xyz[p * 3 + 2];
             float col[3];
-            const bool ic = sd_color_view(cam_c + (b * nv + v) * 21, img + (b * nv + v) * cplane,
+            const bool ic = sd_color_view(cam_c + (b * nv + v) * SD_CAM_WORDS, img + (b * nv + v) * cplane,
                                           Wc, Hc, px, py, pz, col);
             if (rgb) {
                 rgb[(p * nv + v) * 3] = col[0];
@@ -166,7 +166,7 @@ k_field_gather(const float *__restrict__ xyz, int64_t B, int64_t P,
             }
             if (invalid) {
                 float x, y, zc;  // the encoder-frustum test of sd_point_geo, same arithmetic
-                sd_project(cam_f + b * 21, px, py, pz, x, y, zc);
+                sd_project(cam_f + b * SD_CAM_WORDS, px, py, pz, x, y, zc);
                 invalid[p * nv + v] = (ic | sd_outside(x, y, zc)) ? 1.f : 0.f;
             }
         }
@@ -214,7 +214,7 @@ k_field_gather_bwd(const float *__restrict__ xyz, int64_t B, int64_t P,
         if (lane < n) {
             const int64_t p = p0 + lane;
             const int64_t b = p / P;
-            const PointGeo geo = sd_point_geo(cam_f + b * 21, xyz[p * 3], xyz[p * 3 + 1],
+            const PointGeo geo = sd_point_geo(cam_f + b * SD_CAM_WORDS, xyz[p * 3], xyz[p * 3 + 1],
                                               xyz[p * 3 + 2], Wf, Hf);
             gi[0] = geo.t.i00; gi[1] = geo.t.i01; gi[2] = geo.t.i10; gi[3] = geo.t.i11;
             gw[0] = geo.t.w00; gw[1] = geo.t.w01; gw[2] = geo.t.w10; gw[3] = geo.t.w11;

@@ -28,7 +28,7 @@ PRECISIONS = {"fp32": _lib.SD_F32, "bf16": _lib.SD_BF16, "fp16": _lib.SD_F16}
 
 
 def _cam_records(poses_w2c, Ks):
-    """(..., 4, 4) w2c and (..., 3, 3) K -> (..., 21) camera records (C ABI layout,
+    """(..., 4, 4) w2c and (..., 3, 3) K -> (..., 36) camera records (C ABI layout,
     sd_cam_records)."""
     return _lib.cam_records(poses_w2c, Ks)
 

@@ -150,7 +150,9 @@ def test_field_query_vs_reference(precision):
         sig = sigma.reshape(-1)
         dn = sd["dino_features"].reshape(-1, sd["dino_features"].shape[-1])
         close(sig.cpu()[ok], torch.as_tensor(d["sigma"]).reshape(-1)[ok], 1e-5, FP32_ATOL["sigma"], "sigma")
-        close(dn.cpu()[ok], torch.as_tensor(d["dino"]).reshape(dn.shape)[ok], 1e-5, FP32_ATOL["dino"], "dino")
+        # dino: the measured bound of the raw-point query (max 1.65e-5 at z_cam in 1..3 m,
+        # where the top positional frequency's argument is ~1e3 rad) -- FP32_ATOL_FULL
+        close(dn.cpu()[ok], torch.as_tensor(d["dino"]).reshape(dn.shape)[ok], 1e-5, FP32_ATOL_FULL["dino"], "dino")
         assert int(ok.sum()) > 0.8 * ok.numel()
         assert rel_l2(sig.cpu()[~ok], torch.as_tensor(d["sigma"]).reshape(-1)[~ok]) < 1e-3
         assert rel_l2(dn.cpu()[~ok], torch.as_tensor(d["dino"]).reshape(dn.shape)[~ok]) < 1e-3
