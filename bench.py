@@ -690,6 +690,8 @@ def main_c2(args, world, rank, device, dist, host_stage):
     poses = {"identity": False, "offset": True}
     if args.offset_pose:
         poses = {"offset": True}
+    elif args.identity_pose:
+        poses = {"identity": False}
     runs = {name: c2_pose_run(args, world, rank, device, dist, off, host_stage)
             for name, off in poses.items()}
     if rank != 0:
@@ -783,6 +785,8 @@ def main():
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp16", "fp32"])
     ap.add_argument("--offset-pose", action="store_true",
                     help="c2/c4: time only the offset render pose (default: both poses)")
+    ap.add_argument("--identity-pose", action="store_true",
+                    help="c2: time only the identity render pose (profiling runs)")
     ap.add_argument("--mode", default="proj", choices=["proj", "grid"],
                     help="16-bit render kernel: projected grid (default) or per-sample grid")
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -211,6 +211,14 @@ k_render_proj(const sd_render_args a, const sd_head m, const int32_t *__restrict
     typedef typename Tr::Frag4 Frag4;
     typedef typename Tr::E E;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    if (list) {
+        // list mode: workgroups without a listed ray leave before staging the weights (the
+        // list is usually short or empty; the grid is sized for the worst case)
+        const int nx0 = (gridDim.x % 8 == 0) ? 8 : 1;
+        const int64_t ra = (int64_t)__builtin_amdgcn_readfirstlane(list[0]) * 8;
+        const int64_t x0 = blockIdx.x % nx0;
+        if ((ra * x0 / nx0) + (int64_t)(blockIdx.x / nx0) * (SD_RWG / 64) >= ra * (x0 + 1) / nx0) return;
+    }
     {
         uint4 *d = (uint4 *)lds;
         const uint4 *pe = (const uint4 *)m.w_pe, *sg = (const uint4 *)m.w_sig,

@@ -128,8 +128,8 @@ struct st_args {
 #define ST_L_PE 0                              // [8][64] x 16 B code A fragments (16x16x32)
 #define ST_L_PE1 (ST_L_PE + 8 * 64 * 16)      // [8][64] x 8 B code A fragments (16x16x16)
 #define ST_L_SIG (ST_L_PE1 + 8 * 64 * 8)      // [4][64] x 16 B sigma A fragments
-#define ST_L_BOX (ST_L_SIG + 4 * 64 * 16)      // [2][8 waves][2] u32 (min, max) packed
-#define ST_L_HS (ST_L_BOX + 2 * 8 * 8)         // [8 rays][128] 16-bit hidden sums
+#define ST_L_BOX (ST_L_SIG + 4 * 64 * 16)      // [2][8 waves][2 halves] u32 (min, max) packed
+#define ST_L_HS (ST_L_BOX + 2 * 8 * 16)        // [8 rays][128] 16-bit hidden sums
 #define ST_L_WS (ST_L_HS + 8 * 128 * 2)        // [8] f32 weight sums
 #define ST_L_RAY (ST_L_WS + 8 * 4)             // [8 waves][2] x 32 B ray words 0..7 (LDS-DMA)
 #define ST_L_REC (ST_L_RAY + 8 * 2 * 32)       // records: [8 waves][2][K] x 40 B
@@ -311,8 +311,11 @@ k_render_tile(const st_args sa) {
     // by ray_col at the end of the item that ran the pass
     ColPend cpend;
     uint32_t cp_x0y0 = 0;
+    // tap boxes per half ray: samples [0, kh) and [kh, K), kh = 16 (nsub / 2) -- a group
+    // whose whole box does not fit a tile buffer is staged and rendered half by half
+    const int kh = 16 * (nsub >> 1);
     auto ray_pass = [&](int ray, int buf, int slot) {
-        uint32_t bmin = 0xffffffffu, bmax = 0u;
+        uint32_t bmin0 = 0xffffffffu, bmax0 = 0u, bmin1 = 0xffffffffu, bmax1 = 0u;
         if (ray < R) {
             // wave-uniform (readfirstlane: the u32 divide runs on the VALU, and a VGPR
             // address would turn the camera-record reads into vector loads)
@@ -352,16 +355,39 @@ k_render_tile(const st_args sa) {
                         rc[k] = float2{col[1], col[2]};
                     }
                     const uint32_t lo = x0 | (y0 << 16);
-                    bmin = st_min2(bmin, lo);
-                    bmax = st_max2(bmax, lo + 0x00010001u);
+                    if (k < kh) {
+                        bmin0 = st_min2(bmin0, lo);
+                        bmax0 = st_max2(bmax0, lo + 0x00010001u);
+                    } else {
+                        bmin1 = st_min2(bmin1, lo);
+                        bmax1 = st_max2(bmax1, lo + 0x00010001u);
+                    }
                 }
             }
         }
         ST_T(11);
-        bmin = st_wave_min2(bmin);
-        bmax = st_wave_max2(bmax);
+        if (K == 64) {
+            // one sample per lane, halves = lanes [0, 32) and [32, 64): a butterfly over
+            // xor 1 .. 16 reduces each half in place (lanes 0 and 32 hold the results)
+            uint32_t mnv = lane < 32 ? bmin0 : bmin1, mxv = lane < 32 ? bmax0 : bmax1;
+#pragma unroll
+            for (int o = 16; o >= 1; o >>= 1) {
+                mnv = st_min2(mnv, (uint32_t)__shfl_xor((int)mnv, o, 64));
+                mxv = st_max2(mxv, (uint32_t)__shfl_xor((int)mxv, o, 64));
+            }
+            bmin0 = __builtin_amdgcn_readlane(mnv, 0);
+            bmax0 = __builtin_amdgcn_readlane(mxv, 0);
+            bmin1 = __builtin_amdgcn_readlane(mnv, 32);
+            bmax1 = __builtin_amdgcn_readlane(mxv, 32);
+        } else {
+            bmin0 = st_wave_min2(bmin0);
+            bmax0 = st_wave_max2(bmax0);
+            bmin1 = st_wave_min2(bmin1);
+            bmax1 = st_wave_max2(bmax1);
+        }
         ST_T(12);
-        if (lane == 0) *(uint2 *)(lds + ST_L_BOX + (slot * ST_WAVES + wave) * 8) = uint2{bmin, bmax};
+        if (lane == 0)
+            *(uint4 *)(lds + ST_L_BOX + (slot * ST_WAVES + wave) * 16) = uint4{bmin0, bmax0, bmin1, bmax1};
     };
     auto ray_col = [&](int ray, int buf) {
         if (ray < R && lane < K) {
@@ -374,42 +400,39 @@ k_render_tile(const st_args sa) {
 
     // ---- per-step tile geometry (workgroup-uniform) -----------------------------------
     struct Tile {
-        int bx0, by0, pitch, ok;
+        int bx0, by0, pitch, ok, split, ninstr;
     };
-    // union of the 8 wave boxes of slot; issues this wave's share of the LDS-DMA into
-    // tile buffer tb; returns the geometry (ok = 0: overflow, or no valid ray)
-    auto stage = [&](int slot, int tb, int grp, int sbi) {
-        const uint4 *bx = (const uint4 *)(lds + ST_L_BOX + slot * ST_WAVES * 8);
-        uint32_t mn = 0xffffffffu, mx = 0u;
+    // union of the 8 waves' boxes of slot: which = 0 / 1 (half ray), 2 (whole ray)
+    auto box_union = [&](int slot, int which, uint32_t &mn, uint32_t &mx) {
+        const uint4 *bx = (const uint4 *)(lds + ST_L_BOX + slot * ST_WAVES * 16);
+        mn = 0xffffffffu;
+        mx = 0u;
 #pragma unroll
-        for (int i = 0; i < ST_WAVES / 2; ++i) {
+        for (int i = 0; i < ST_WAVES; ++i) {
             const uint4 v = bx[i];
-            mn = st_min2(mn, st_min2(v.x, v.z));
-            mx = st_max2(mx, st_max2(v.y, v.w));
+            mn = st_min2(mn, which == 0 ? v.x : which == 1 ? v.z : st_min2(v.x, v.z));
+            mx = st_max2(mx, which == 0 ? v.y : which == 1 ? v.w : st_max2(v.y, v.w));
         }
         mn = __builtin_amdgcn_readfirstlane(mn);
         mx = __builtin_amdgcn_readfirstlane(mx);
+    };
+    auto geom = [&](uint32_t mn, uint32_t mx) {
         Tile t;
         t.bx0 = (int)(mn & 0xffffu);
         t.by0 = (int)(mn >> 16);
         const int tw = (int)(mx & 0xffffu) - t.bx0 + 1, th = (int)(mx >> 16) - t.by0 + 1;
         t.pitch = tw > 0 ? st_pitch(tw) : 1;
-        const int ntex = th * t.pitch;
-        const int nchunk = ntex * ST_TEXQ;
-        const int ninstr = (nchunk + 63) >> 6;
-        t.ok = (mn != 0xffffffffu) && tw > 0 && th > 0 && ninstr * 1024 <= sa.tile_bytes;
-        if (mn == 0xffffffffu) return t;  // no valid ray in the group
-        if (!t.ok) {
-            if (wave == 0 && lane == 0) {
-                const int i = atomicAdd(sa.ovf, 1);
-                sa.ovf[1 + i] = grp;
-            }
-            return t;
-        }
+        t.ninstr = (th * t.pitch * ST_TEXQ + 63) >> 6;  // 1-KiB DMA instructions
+        t.ok = (mn != 0xffffffffu) && tw > 0 && th > 0 && t.ninstr * 1024 <= sa.tile_bytes;
+        t.split = 0;
+        return t;
+    };
+    // this wave's share of the LDS-DMA of tile t's texels into tile buffer tb
+    auto dma = [&](const Tile &t, int tb, int sbi) {
         const uint8_t *plane = (const uint8_t *)a.grid + (int64_t)sbi * plane_bytes;
         const float inv_pitch = 1.f / (float)t.pitch;
         const uint32_t dst0 = tile0 + (uint32_t)tb * (uint32_t)sa.tile_bytes;
-        for (int i = wave; i < ninstr; i += ST_WAVES) {
+        for (int i = wave; i < t.ninstr; i += ST_WAVES) {
             const uint32_t ci = (uint32_t)i * 64u + (uint32_t)lane;
             const uint32_t n = __umulhi(ci, 238609295u);  // ci / 18
             const uint32_t part = ci - 18u * n;
@@ -419,6 +442,33 @@ k_render_tile(const st_args sa) {
             const uint8_t *src = plane + ((int64_t)sy * Wf + sx) * 256 + (part < 16u ? part : 0u) * 16u;
             if (!ST_ABL_NODMA) st_dma16(src, lds0 + dst0 + (uint32_t)i * 1024u);
         }
+    };
+    // geometry of slot's group for tile buffer tb, DMA issued: the whole box if it fits,
+    // else (nsub >= 2) the first half's box when both halves fit (split = 1: the second
+    // half is staged mid-step), else the group goes to the overflow list (ok = 0)
+    auto stage = [&](int slot, int tb, int grp, int sbi) {
+        uint32_t mn, mx;
+        box_union(slot, 2, mn, mx);
+        Tile t = geom(mn, mx);
+        if (mn == 0xffffffffu) return t;  // no valid ray in the group
+        if (!t.ok && nsub >= 2 && !ST_PIPE) {
+            uint32_t mn0, mx0, mn1, mx1;
+            box_union(slot, 0, mn0, mx0);
+            box_union(slot, 1, mn1, mx1);
+            const Tile h0 = geom(mn0, mx0), h1 = geom(mn1, mx1);
+            if (h0.ok && h1.ok) {
+                t = h0;
+                t.split = 1;
+            }
+        }
+        if (!t.ok) {
+            if (wave == 0 && lane == 0) {
+                const int i = atomicAdd(sa.ovf, 1);
+                sa.ovf[1 + i] = grp;
+            }
+            return t;
+        }
+        dma(t, tb, sbi);
         return t;
     };
 
@@ -503,8 +553,7 @@ k_render_tile(const st_args sa) {
         const int nsbi = has_next ? __builtin_amdgcn_readfirstlane((int)((unsigned)min(8 * ngrp, R - 1) / (unsigned)rps)) : 0;
         const bool active = cur.ok && ray < R;
         const uint32_t tileb = lds0 + tile0 + (uint32_t)buf * (uint32_t)sa.tile_bytes;
-        const int toff = (tq & 1) + (tq >> 1) * cur.pitch;
-        const uint32_t lane_off = (uint32_t)toff * ST_TEX + 8u * (uint32_t)tp;
+        uint32_t lane_off = (uint32_t)((tq & 1) + (tq >> 1) * cur.pitch) * ST_TEX + 8u * (uint32_t)tp;
 
         float Tc = 1.f, dpart = 0.f, wpart = 0.f, cpart[3] = {0.f, 0.f, 0.f};
         f32x4 hacc[8];
@@ -743,7 +792,7 @@ k_render_tile(const st_args sa) {
         ST_T(3);
         st_barrier_lds();  // X: next boxes visible; the head has read the hsum area
         ST_T(4);
-        Tile nxt = {0, 0, 1, 0};
+        Tile nxt = {0, 0, 1, 0, 0, 0};
         if (has_next) nxt = stage(buf ^ 1, buf ^ 1, ngrp, nsbi);
         ST_T(5);
 #if ST_PIPE
@@ -765,11 +814,25 @@ k_render_tile(const st_args sa) {
             }
         }
 #else
-        if (active && !ST_ABL_NOITEM) {
-            itemB(0, s0);
-            for (int sub = 1; sub < nsub; ++sub) {
-                itemA(sub, s1);
-                itemB(sub, s1);
+        // split group: items of the first half ray from the current tile, then the second
+        // half's box is staged into the same buffer (workgroup-uniform branch, taken by
+        // every wave: it holds barriers).  One item loop for both cases keeps the kernel
+        // small (a second inlined copy of the items measured slower).
+        const int nfirst = cur.split ? (nsub >> 1) : nsub;
+        for (int sub = 0; sub < nsub; ++sub) {
+            if (sub == nfirst) {
+                st_barrier_lds();  // every wave is done with the first half's taps
+                uint32_t mn1, mx1;
+                box_union(buf, 1, mn1, mx1);
+                cur = geom(mn1, mx1);  // fits: checked when the split was chosen
+                dma(cur, buf, sbi);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                st_barrier_lds();
+                lane_off = (uint32_t)((tq & 1) + (tq >> 1) * cur.pitch) * ST_TEX + 8u * (uint32_t)tp;
+            }
+            if (active && !ST_ABL_NOITEM) {
+                if (sub) itemA(sub, s0);
+                itemB(sub, s0);
             }
         }
 #endif
