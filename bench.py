@@ -359,7 +359,8 @@ def main_vit(args, world, rank, device):
     token grids, all libsdhip.so kernels."""
     from scenedino_amd.models.backbones.dino.vit import DINOv2Encoder
     results = {}
-    models = {"vit-s16": ("vit-s", "v1_16"), "vit-b8": ("vit-b", "v1")}
+    models = {"vit-s16": ("vit-s", "v1_16"), "vit-b8": ("vit-b", "v1"),
+              "dinov2-b14": ("vit-b", "v2")}  # C4 (configs[3]): 192x640 resized to 168x560
     if args.models:
         models = {k: models[k] for k in args.models.split(",")}
     for name, (arch, ver) in models.items():
@@ -377,9 +378,10 @@ def main_vit(args, world, rank, device):
             dt = (time.perf_counter() - t0) / args.steps
         vit = enc.model.vit
         p, C = vit.patch_size, vit.embed_dim
-        Np = (H // p) * (W // p)
+        rh, rw = enc.resize if enc.resize is not None else (H, W)
+        Np = (rh // p) * (rw // p)
         fl = vit_flops(Np + 1, C, len(vit.blocks), p, Np)
-        results[name] = {"ms_per_pass": dt * 1e3, "tokens": Np + 1, "dim": C,
+        results[name] = {"ms_per_pass": dt * 1e3, "tokens": Np + 1, "dim": C, "patch": p,
                          "gflop_per_pass": fl / 1e9, "tflops": fl / dt / 1e12,
                          "frac_bf16_peak": fl / dt / 1e12 / PEAK_TFLOPS["bf16"]}
     first = next(iter(results))
@@ -429,7 +431,8 @@ def main_encode(args, world, rank, device):
     (the reference's fresh tensor)."""
     from scenedino_amd.models.backbones import make_backbone
     results = {}
-    models = {"vit-s16": ("vit-s", "v1_16"), "vit-b8": ("vit-b", "v1")}
+    models = {"vit-s16": ("vit-s", "v1_16"), "vit-b8": ("vit-b", "v1"),
+              "dinov2-b14": ("vit-b", "v2")}  # C4 (configs[3]): 192x640 resized to 168x560
     if args.models:
         models = {k: models[k] for k in args.models.split(",")}
     for name, (arch, ver) in models.items():
@@ -454,7 +457,8 @@ def main_encode(args, world, rank, device):
             out_shape = list(m(img)[0].shape)
         vit = m.encoder.model.vit
         p, C = vit.patch_size, vit.embed_dim
-        gh, gw = H // p, W // p
+        rh, rw = m.encoder.resize if m.encoder.resize is not None else (H, W)
+        gh, gw = rh // p, rw // p
         fv = vit_flops(gh * gw + 1, C, len(vit.blocks), p, gh * gw)
         fd = dpt_flops(m.decoder, gh, gw)
         results[name] = {"ms_per_pass": dt * 1e3, "out_shape": out_shape,
