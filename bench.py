@@ -267,7 +267,9 @@ def main_c5(args, world, rank, local_rank, dist, device, host_stage=False):
     from scenedino_amd.downstream_head import SemanticHead
     global HF, WF
     HF, WF = 384, 1280
-    net, _, _, _, _, _ = make_scene(0 if dist else rank, device, args.precision)
+    seg_fp8 = args.precision == "fp8"  # configs[4]: fp8 MFMA in the voxel MLP chain
+    net, _, _, _, _, _ = make_scene(0 if dist else rank, device, "bf16" if seg_fp8 else args.precision)
+    net.seg_precision = "fp8" if seg_fp8 else "bf16"
     torch.manual_seed(5)
     net.encoder.dim_reduction = MlpDimReduction(768, 64, 128).to(device).eval()
     net.downstream_head = SemanticHead(19, 19, 768, 64).to(device).eval()
@@ -324,7 +326,8 @@ def main_c5(args, world, rank, local_rank, dist, device, host_stage=False):
             "value": n_vox * args.steps / elapsed, "unit": "voxels/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": 1e3 * elapsed / args.steps, "higher_is_better": True,
-            "scaling": "strong", "vs_baseline": None, "dtype": args.precision,
+            "scaling": "strong", "vs_baseline": None,
+            "dtype": ("fp8 e4m3 (k_seg_head norm product) + bf16" if seg_fp8 else args.precision),
             "data": "synthetic (seeded image, N(0,1) 256x384x1280 grid, random-init ResnetFC / "
                     "MlpDimReduction / SemanticHead)",
             "config": {"workload": "C5: SSCBench 256x256x32 voxel query, ViT-B/8-shaped "
@@ -786,7 +789,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp16", "fp32"])
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp16", "fp32", "fp8"],
+                    help="fp8: --config c5 only (fp8 MFMA norm product in k_seg_head)")
     ap.add_argument("--offset-pose", action="store_true",
                     help="c2/c4: time only the offset render pose (default: both poses)")
     ap.add_argument("--identity-pose", action="store_true",
@@ -810,6 +814,8 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: ranks share GPU 0 and exchange through host memory (dry run)")
     args = ap.parse_args()
+    if args.precision == "fp8" and args.config != "c5":
+        ap.error("--precision fp8 is the C5 voxel MLP chain (--config c5)")
     global K_SAMPLES, D_DINO
     if args.config == "c4":
         K_SAMPLES, D_DINO = 128, 384

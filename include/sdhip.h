@@ -271,6 +271,13 @@ typedef struct sd_seg_head {
     int32_t d_latent;      /* 128                                                      */
     int32_t d_full;        /* multiple of 32 (768)                                     */
     int32_t d_code;        /* 64                                                       */
+    /* optional fp8 norm product (NULL: bf16 w2).  OCP e4m3 fragments of W2 * 2^-e_w for
+     * v_mfma_scale_f32_32x32x64_f8f6f4, [d_full/32][d_latent/64][64][32] bytes, k order
+     * the fp8 accumulator-as-operand permutation (scenedino_amd/seg_pack.py); used for
+     * |W2 h + b2| of the labels/seg outputs (dino_full keeps the bf16 w2)            */
+    const void *w2_f8;
+    float w2_f8_scale;     /* 2^e_w                                                    */
+    int32_t pad0;
 } sd_seg_head;
 
 /* Per-point segmentation head on P DINO codes dino (P, d_in) f32.

@@ -101,9 +101,19 @@ __device__ __forceinline__ f32x16 sg_rows(const float *__restrict__ vec, int t, 
 }
 
 #define SG_MFMA(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_bf16((a), (b), (c), 0, 0, 0)
+typedef __attribute__((ext_vector_type(8))) int i32x8_t;
+// OCP e4m3 x e4m3 -> f32, 32x32x64, unit scales (E8M0 127): lane l holds A[l & 31][32 (l >> 5)
+// + j] / B[32 (l >> 5) + j][l & 31] in byte j (tools/probe/mfma_f8.hip)
+#define SG_MFMA8(a, b, c) \
+    __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4((a), (b), (c), 0, 0, 0, 127, 0, 127)
+
+__device__ __forceinline__ uint32_t sg_bf16_bits(__bf16 v) { return (uint32_t)__builtin_bit_cast(unsigned short, v); }
 
 // MODE bit 0: write dino_full (transform_expand output); bit 1: segmentation head.
-template <int MODE>
+// F8 (labels / seg only): the norm product |W2 h + b2| on fp8 MFMA -- h quantised to e4m3
+// with a per-point power-of-two scale (its largest value lands in [128, 256)), W2 with the
+// per-tensor one of the packed record; the scales leave in the f32 epilogue (exact).
+template <int MODE, bool F8>
 __global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const float *__restrict__ dino,
                                                             int64_t P, int32_t DF,
                                                             const float *__restrict__ sigma,
@@ -170,7 +180,76 @@ __global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const float *__restr
 
     // ---- n = max(|W2 h + b2|, 1e-12)  (F.normalize, dim_reduction.py:25) ----
     float rinv[SG_NT], den[SG_NT];
-    {
+    if (F8) {
+        // h as fp8 B operands: k-step s (64 hidden), byte j of lane half hh = hidden
+        // 32 (2 s + (j >> 4)) + (jj & 3) + 8 (jj >> 2) + 4 hh, jj = j & 15 -- the rows this
+        // lane holds of layer-1 tiles 2 s and 2 s + 1 (register jj = hb[2 tile + (jj >> 3)][jj & 7])
+        i32x8_t h8[SG_NT][2];
+        float scp[SG_NT];
+#pragma unroll
+        for (int ct = 0; ct < SG_NT; ++ct) {
+            uint32_t mx = 0;  // h >= 0: the largest bf16 bit pattern is the largest value
+#pragma unroll
+            for (int q = 0; q < SG_DL / 16; ++q)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) mx = max(mx, sg_bf16_bits(hb[ct][q][e]));
+            mx = max(mx, (uint32_t)__shfl_xor((int)mx, 32));
+            const int eb = max((int)((mx >> 7) & 0xffu), 8);  // biased exponent of max h
+            const float mul = __uint_as_float((uint32_t)(261 - eb) << 23);  // 2^(134 - eb)
+            scp[ct] = __uint_as_float((uint32_t)(eb - 7) << 23) * h.w2_f8_scale;
+#pragma unroll
+            for (int st = 0; st < 2; ++st)
+#pragma unroll
+                for (int w = 0; w < 8; ++w) {
+                    const int tile = 2 * st + (w >> 2), q = 2 * tile + ((w & 3) >> 1), e0 = 4 * (w & 1);
+                    float v[4];
+#pragma unroll
+                    for (int b = 0; b < 4; ++b)
+                        v[b] = __uint_as_float(sg_bf16_bits(hb[ct][q][e0 + b]) << 16) * mul;
+                    int word = __builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], 0, false);
+                    word = __builtin_amdgcn_cvt_pk_fp8_f32(v[2], v[3], word, true);
+                    h8[ct][st][w] = word;
+                }
+        }
+        float ss[SG_NT];
+#pragma unroll
+        for (int ct = 0; ct < SG_NT; ++ct) ss[ct] = 0.f;
+        const i32x8_t *w2 = (const i32x8_t *)h.w2_f8;
+        i32x8_t cur[2];
+        f32x16 bb = sg_rows(h.b2, 0, hh);
+#pragma unroll
+        for (int st = 0; st < 2; ++st) cur[st] = w2[st * 64 + lane];
+        for (int t = 0; t < T2; ++t) {
+            const int tn = t + 1 < T2 ? t + 1 : t;
+            i32x8_t nxt[2];
+#pragma unroll
+            for (int st = 0; st < 2; ++st) nxt[st] = w2[(tn * 2 + st) * 64 + lane];
+            const f32x16 bbn = sg_rows(h.b2, tn, hh);
+            f32x16 acc[SG_NT];
+#pragma unroll
+            for (int ct = 0; ct < SG_NT; ++ct) acc[ct] = sg_zero16();
+#pragma unroll
+            for (int st = 0; st < 2; ++st)
+#pragma unroll
+                for (int ct = 0; ct < SG_NT; ++ct) acc[ct] = SG_MFMA8(cur[st], h8[ct][st], acc[ct]);
+#pragma unroll
+            for (int ct = 0; ct < SG_NT; ++ct)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const float e = fmaf(acc[ct][i], scp[ct], bb[i]);
+                    ss[ct] = fmaf(e, e, ss[ct]);
+                }
+#pragma unroll
+            for (int st = 0; st < 2; ++st) cur[st] = nxt[st];
+            bb = bbn;
+        }
+#pragma unroll
+        for (int ct = 0; ct < SG_NT; ++ct) {
+            const float tot = ss[ct] + __shfl_xor(ss[ct], 32);
+            den[ct] = fmaxf(sqrtf(tot), 1e-12f);
+            rinv[ct] = 1.f / den[ct];
+        }
+    } else {
         float ss[SG_NT];
 #pragma unroll
         for (int ct = 0; ct < SG_NT; ++ct) ss[ct] = 0.f;
@@ -426,20 +505,19 @@ extern "C" int sd_seg_query(const float *dino, int64_t P, const sd_seg_head *h,
     const float neg_vox = -voxel_size;
     hipStream_t s = (hipStream_t)stream;
     const int mode = (dino_full ? 1 : 0) | (want_seg ? 2 : 0);
+    // fp8 norm only for the labels / seg outputs (dino_full is the bf16 expansion)
+    const bool f8 = h->w2_f8 != nullptr && mode == 2;
+#define SG_LAUNCH(M, F)                                                                            \
+    hipLaunchKernelGGL((k_seg_head<M, F>), dim3((unsigned)nblk), dim3(SG_WAVES * 64), 0, s, dino, P, \
+                       h->d_full, sigma, neg_vox, *h, labels, seg, dino_full)
     switch (mode) {
-    case 1:
-        hipLaunchKernelGGL(k_seg_head<1>, dim3((unsigned)nblk), dim3(SG_WAVES * 64), 0, s, dino,
-                           P, h->d_full, sigma, neg_vox, *h, labels, seg, dino_full);
-        break;
+    case 1: SG_LAUNCH(1, false); break;
     case 2:
-        hipLaunchKernelGGL(k_seg_head<2>, dim3((unsigned)nblk), dim3(SG_WAVES * 64), 0, s, dino,
-                           P, h->d_full, sigma, neg_vox, *h, labels, seg, dino_full);
+        if (f8) SG_LAUNCH(2, true); else SG_LAUNCH(2, false);
         break;
-    default:
-        hipLaunchKernelGGL(k_seg_head<3>, dim3((unsigned)nblk), dim3(SG_WAVES * 64), 0, s, dino,
-                           P, h->d_full, sigma, neg_vox, *h, labels, seg, dino_full);
-        break;
+    default: SG_LAUNCH(3, false); break;
     }
+#undef SG_LAUNCH
     if (hipGetLastError() != hipSuccess) {
         sd_set_error("sd_seg_query: launch failed");
         return -2;

@@ -476,10 +476,12 @@ class BTSNet(nn.Module):
         dh = self.downstream_head if with_head else None
         stego = getattr(dh, "stego_head", None) if dh is not None else None
         clus = getattr(dh, "stego_cluster_head", None) if dh is not None else None
-        key = seg_key(dr, stego, clus) + (with_head,)
+        fp8 = getattr(self, "seg_precision", "bf16") == "fp8"
+        key = seg_key(dr, stego, clus) + (with_head, fp8)
         cache = getattr(self, "_seg_cache", None)
         if cache is None or cache[0] != key:
-            rec = PackedSegHead(dr, stego, clus, device=dr.linear_in.weight.device)
+            rec = PackedSegHead(dr, stego, clus, device=dr.linear_in.weight.device,
+                                fp8=fp8 and with_head)
             self._seg_cache = cache = (key, rec)
         return cache[1]
 

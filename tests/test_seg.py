@@ -111,21 +111,53 @@ def _to_regs(acc):
     return regs
 
 
-def _emulate(pk, x):
-    """The k_seg_head register program for 32 points, in fp64."""
+def _e4m3(v):
+    """float -> nearest OCP e4m3 value (RNE, as v_cvt_pk_fp8_f32 and torch)."""
+    return v.float().to(torch.float8_e4m3fn).double()
+
+
+def _norm_fp8(pk, regs_h):
+    """k_seg_head<2, F8>'s norm |W2 h + b2| from the packed fp8 fragments: regs_h[t] (64
+    lanes, 16) are the bf16 layer-1 registers of tile t; returns n per lane (64,)."""
+    hb = torch.stack(regs_h).float().to(torch.bfloat16).double()            # (4, 64, 16)
+    mx = hb.amax(dim=(0, 2))
+    mx = torch.maximum(mx[:32], mx[32:]).repeat(2)
+    eb = torch.where(mx > 0, torch.floor(torch.log2(mx.clamp_min(1e-300))) + 127, torch.zeros_like(mx))
+    eb = eb.clamp_min(8)
+    mul, scp = 2.0 ** (134 - eb), 2.0 ** (eb - 134) * pk.w2_f8_scale
+    h8 = []
+    for st in range(2):
+        j = torch.arange(32)
+        vals = hb[2 * st + (j >> 4), :, j & 15].t()                          # (64 lanes, 32)
+        h8.append(_e4m3(vals * mul[:, None]))
+    A = pk.w2_f8.view(torch.float8_e4m3fn).double()                          # (T2, 2, 64, 32)
+    ss = torch.zeros(64, dtype=torch.float64)
+    for t in range(pk.d_full // 32):
+        acc = sum(A[t, st, :32] @ h8[st][:32].t() + A[t, st, 32:] @ h8[st][32:].t() for st in range(2))
+        e = _to_regs(acc) * scp[:, None] + pk.b2[t].repeat_interleave(32, 0)
+        ss += (e * e).sum(1)
+    return (ss[:32] + ss[32:]).sqrt().clamp_min(1e-12).repeat(2)
+
+
+def _emulate(pk, x, fp8=False):
+    """The k_seg_head register program for 32 points, in fp64 (fp8: the F8 norm)."""
     B = lambda regs, s: regs[:, 8 * s:8 * s + 8]
     xb = [torch.cat([x[:, 16 * s:16 * s + 8], x[:, 16 * s + 8:16 * s + 16]], 0) for s in range(4)]
-    hb = []
+    hb, regs_h = [], []
     for t in range(4):
         acc = sum(_mfma(pk.w1[t, s], xb[s]) for s in range(4))
         regs = torch.relu(_to_regs(acc) + pk.b1[t].repeat_interleave(32, 0))
         hb += [B(regs, 0), B(regs, 1)]
+        regs_h.append(regs)
     T2 = pk.d_full // 32
-    ss = torch.zeros(64, dtype=torch.float64)
-    for t in range(T2):
-        e = _to_regs(sum(_mfma(pk.w2[t, q], hb[q]) for q in range(8))) + pk.b2[t].repeat_interleave(32, 0)
-        ss += (e * e).sum(1)
-    n = (ss[:32] + ss[32:]).sqrt().clamp_min(1e-12).repeat(2).unsqueeze(1)
+    if fp8:
+        n = _norm_fp8(pk, regs_h).unsqueeze(1)
+    else:
+        ss = torch.zeros(64, dtype=torch.float64)
+        for t in range(T2):
+            e = _to_regs(sum(_mfma(pk.w2[t, q], hb[q]) for q in range(8))) + pk.b2[t].repeat_interleave(32, 0)
+            ss += (e * e).sum(1)
+        n = (ss[:32] + ss[32:]).sqrt().clamp_min(1e-12).repeat(2).unsqueeze(1)
     sacc = []
     for rt in range(2):
         a = _to_regs(sum(_mfma(pk.wl[rt, q], hb[q]) for q in range(8)))
@@ -159,6 +191,44 @@ def test_packed_fragments_emulate_reference_chain():
     assert torch.allclose(got_dir, ref_dir, atol=1e-9)
     got_labels = pd["assign"][scores.argmax(1)]
     assert (got_labels == labels).all()
+
+
+@pytest.mark.parametrize("d_full", [768, 384])
+def test_packed_fp8_norm_emulation(d_full):
+    """BASELINE configs[4] fp8: the F8 kernel's norm (e4m3 W2 fragments with the record's
+    per-tensor scale, h in e4m3 with a per-point power-of-two scale) emulated from the
+    packed record: the norm within 1 % of the exact one, and the labels of 2048 fixture
+    points (bf16-rounded fragments elsewhere, as the kernel) >= 99 % equal to the
+    reference's own (tests/golden/seg_head.npz)."""
+    from scenedino_amd.seg_pack import PackedSegHead
+    d = load("seg_head.npz")
+    t = f"_{d_full}"
+    p = seg_params(d, t, torch.float64)
+    dr, st, cl = modules_from({k: v.float() if v.is_floating_point() else v for k, v in p.items()})
+    pk = PackedSegHead(dr, st, cl, frag_dtype=torch.float64, fp8=True)
+    assert pk.w2_f8.dtype == torch.uint8 and tuple(pk.w2_f8.shape) == (d_full // 32, 2, 64, 32)
+    pd = {k: v.double() if v.is_floating_point() else v for k, v in p.items()}
+    pd["centres"] = torch.as_tensor(d["centres" + t]).double()
+    x_all = torch.as_tensor(d["x" + t]).double()
+    labels = []
+    for i in range(0, x_all.shape[0], 32):
+        x = x_all[i:i + 32]
+        scores = _emulate(pk, x, fp8=True)
+        labels.append(pd["assign"][scores.argmax(1)])
+        if i == 0:  # the norm itself against the exact one
+            h = torch.relu(x @ pd["W1"].t() + pd["b1"])
+            n_ref = (h @ pd["W2"].t() + pd["b2"]).norm(dim=1)
+            regs_h = []
+            B_ = lambda regs, s: regs[:, 8 * s:8 * s + 8]
+            xb = [torch.cat([x[:, 16 * s:16 * s + 8], x[:, 16 * s + 8:16 * s + 16]], 0) for s in range(4)]
+            for tt in range(4):
+                acc = sum(_mfma(pk.w1[tt, s], xb[s]) for s in range(4))
+                regs_h.append(torch.relu(_to_regs(acc) + pk.b1[tt].repeat_interleave(32, 0)))
+            n8 = _norm_fp8(pk, regs_h)[:32]
+            assert ((n8 - n_ref).abs() / n_ref).max() < 2e-2  # e4m3 W2 and h: measured 1.3e-2
+    labels = torch.cat(labels)
+    _, ref_scores, _ = SO.seg_head(torch.as_tensor(d["x" + t]), seg_params(d, t))
+    _label_check(labels, ref_scores, d["labels" + t], "fp8 emulation")
 
 
 # ------------------------------------------------------------------------ GPU tests
@@ -229,6 +299,36 @@ def test_seg_query_vs_reference(gpu, d_full):
     pk_e = PackedSegHead(dr)
     _, _, f2 = _lib.seg_query(x, pk_e.rec, want_labels=False, want_full=True)
     assert torch.equal(f2, full)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d_full", [768, 384])
+def test_seg_query_fp8_vs_reference(gpu, d_full):
+    """BASELINE configs[4] fp8 record (k_seg_head<2, F8>): labels >= 99 % equal to the
+    reference's and identical wherever its top-2 margin exceeds 2e-2; the alpha pick on top;
+    dino_full requests keep the bf16 expansion."""
+    from scenedino_amd import _lib
+    from scenedino_amd.seg_pack import PackedSegHead
+    d = load("seg_head.npz")
+    t = f"_{d_full}"
+    p = seg_params(d, t)
+    dr, st, cl = (m.to(gpu) for m in modules_from(p))
+    pk = PackedSegHead(dr, st, cl, fp8=True)
+    x = torch.as_tensor(d["x" + t]).to(gpu)
+    labels, _, _ = _lib.seg_query(x, pk.rec, want_labels=True)
+    _, ref_scores, _ = SO.seg_head(torch.as_tensor(d["x" + t]), p)
+    _label_check(labels.cpu(), ref_scores, d["labels" + t], "fp8 labels")
+    # densities are softplus outputs (>= 0); a quarter exactly 0 (alpha 0 -> class 0)
+    sigma = torch.rand(x.shape[0], generator=torch.Generator().manual_seed(4)) * 2
+    sigma[::4] = 0
+    sigma = sigma.to(gpu)
+    l2, seg, _ = _lib.seg_query(x, pk.rec, want_labels=True, want_seg=True, sigma=sigma, voxel_size=0.2)
+    assert torch.equal(l2, labels)
+    ref_seg = SO.alpha_seg(sigma.cpu(), labels.cpu().long())
+    assert torch.equal(seg.cpu().long(), ref_seg)
+    _, _, full8 = _lib.seg_query(x, pk.rec, want_labels=True, want_full=True)
+    _, _, full16 = _lib.seg_query(x, PackedSegHead(dr, st, cl).rec, want_labels=True, want_full=True)
+    assert torch.equal(full8, full16)
 
 
 @pytest.mark.gpu
