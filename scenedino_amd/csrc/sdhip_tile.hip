@@ -148,16 +148,34 @@ __device__ __forceinline__ uint32_t st_max2(uint32_t a, uint32_t b) {
     return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2, a),
                                                                   __builtin_bit_cast(u16x2, b)));
 }
-__device__ __forceinline__ uint32_t st_wave_min2(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = st_min2(v, (uint32_t)__shfl_xor((int)v, o, 64));
+// component-wise min / max over each 16-lane row by DPP (quad_perm xor 1, xor 2,
+// row_half_mirror, row_mirror: every step's sources are inside the row), no LDS round trip
+template <bool MAX>
+__device__ __forceinline__ uint32_t st_row_red2(uint32_t v) {
+#define ST_RSTEP(ctrl)                                                                        \
+    {                                                                                         \
+        const uint32_t o = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, (ctrl), 0xf, 0xf, false); \
+        v = MAX ? st_max2(v, o) : st_min2(v, o);                                              \
+    }
+    ST_RSTEP(0xB1)
+    ST_RSTEP(0x4E)
+    ST_RSTEP(0x141)
+    ST_RSTEP(0x140)
+#undef ST_RSTEP
     return v;
 }
-__device__ __forceinline__ uint32_t st_wave_max2(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = st_max2(v, (uint32_t)__shfl_xor((int)v, o, 64));
-    return v;
+// row-reduced value -> wave-uniform reduction of rows [r0, r1]
+template <bool MAX>
+__device__ __forceinline__ uint32_t st_rows2(uint32_t v, int r0, int r1) {
+    uint32_t acc = (uint32_t)__builtin_amdgcn_readlane((int)v, 16 * r0);
+    for (int r = r0 + 1; r <= r1; ++r) {
+        const uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)v, 16 * r);
+        acc = MAX ? st_max2(acc, o) : st_min2(acc, o);
+    }
+    return acc;
 }
+__device__ __forceinline__ uint32_t st_wave_min2(uint32_t v) { return st_rows2<false>(st_row_red2<false>(v), 0, 3); }
+__device__ __forceinline__ uint32_t st_wave_max2(uint32_t v) { return st_rows2<true>(st_row_red2<true>(v), 0, 3); }
 
 // tile pitch (texels per staged row): pitch mod 8 in 2..6, so that the four taps
 // n, n + 1, n + pitch, n + pitch + 1 of a sample (288 B = 8 banks apart per texel) land
@@ -367,18 +385,13 @@ k_render_tile(const st_args sa) {
         }
         ST_T(11);
         if (K == 64) {
-            // one sample per lane, halves = lanes [0, 32) and [32, 64): a butterfly over
-            // xor 1 .. 16 reduces each half in place (lanes 0 and 32 hold the results)
-            uint32_t mnv = lane < 32 ? bmin0 : bmin1, mxv = lane < 32 ? bmax0 : bmax1;
-#pragma unroll
-            for (int o = 16; o >= 1; o >>= 1) {
-                mnv = st_min2(mnv, (uint32_t)__shfl_xor((int)mnv, o, 64));
-                mxv = st_max2(mxv, (uint32_t)__shfl_xor((int)mxv, o, 64));
-            }
-            bmin0 = __builtin_amdgcn_readlane(mnv, 0);
-            bmax0 = __builtin_amdgcn_readlane(mxv, 0);
-            bmin1 = __builtin_amdgcn_readlane(mnv, 32);
-            bmax1 = __builtin_amdgcn_readlane(mxv, 32);
+            // one sample per lane, halves = lanes [0, 32) and [32, 64): rows 0-1 / 2-3
+            const uint32_t mnv = st_row_red2<false>(lane < 32 ? bmin0 : bmin1);
+            const uint32_t mxv = st_row_red2<true>(lane < 32 ? bmax0 : bmax1);
+            bmin0 = st_rows2<false>(mnv, 0, 1);
+            bmax0 = st_rows2<true>(mxv, 0, 1);
+            bmin1 = st_rows2<false>(mnv, 2, 3);
+            bmax1 = st_rows2<true>(mxv, 2, 3);
         } else {
             bmin0 = st_wave_min2(bmin0);
             bmax0 = st_wave_max2(bmax0);
