@@ -137,9 +137,15 @@ def end_to_end(args, device, rank):
             "ms_per_frame": dt * 1e3, "rays_per_s": H * W / dt}
 
 
-def render_step(net, wrapper, sampler, pose, Ks):
+def render_step(net, wrapper, sampler, pose, Ks, band=None):
+    """One C2 frame: rays of the render pose, then the fused render.  band = (r0, r1):
+    only rays [r0, r1) of the frame (ray-tile sharding; the renderer keys its in-kernel
+    depth jitter by the frame ray index, so the band matches the whole-frame render)."""
     net._grid_cache = None  # re-pack / re-project the (freshly encoded) grid every frame
     rays, _ = sampler.sample(None, pose, Ks)
+    if band is not None:
+        rays = rays[:, band[0]:band[1]]
+        wrapper.renderer.ray_offset = band[0]
     return wrapper(rays, want_weights=False, want_alphas=False)
 
 
@@ -641,10 +647,20 @@ def _launch_ranks(args) -> int:
 def c2_pose_run(args, world, rank, device, dist, offset_pose, host_stage):
     """Time the C2 step at one render pose (all ranks; max over ranks)."""
     from scenedino_amd import distributed as sdd
-    net, renderer, wrapper, sampler, pose, Ks = make_scene(rank, device, args.precision,
-                                                          offset_pose)
+    rows = dist and args.shard == "rows"
+    # frames: frame r on rank r (weak scaling); rows: every rank encodes the same frame and
+    # renders its band of rows [H g / N, H (g + 1) / N) (strong scaling of one frame)
+    net, renderer, wrapper, sampler, pose, Ks = make_scene(0 if rows else rank, device,
+                                                          args.precision, offset_pose)
     R = H * W
-    gather = sdd.MapGather(R, 1 + D_DINO + 3, device, host_stage=host_stage) if dist else None
+    band = None
+    if rows:
+        y0, y1 = sdd.row_band(H, rank, world)
+        if (y1 - y0) != H // world or H % world:
+            raise ValueError(f"--shard rows needs H ({H}) divisible by the world size ({world})")
+        band = (y0 * W, y1 * W)
+    Rr = band[1] - band[0] if band else R
+    gather = sdd.MapGather(Rr, 1 + D_DINO + 3, device, host_stage=host_stage) if dist else None
     net.fused_mode = args.mode
     timer = KernelTimer()
     net.kernel_timer = timer
@@ -652,7 +668,7 @@ def c2_pose_run(args, world, rank, device, dist, offset_pose, host_stage):
     def step(i):
         if gather is not None:  # frame f on rank f; maps rendered into the gather send slot
             net.render_into = gather.send(i)
-        out = render_step(net, wrapper, sampler, pose, Ks)
+        out = render_step(net, wrapper, sampler, pose, Ks, band)
         if gather is not None:
             gather.start(i)
         return out
@@ -683,7 +699,8 @@ def c2_pose_run(args, world, rank, device, dist, offset_pose, host_stage):
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed, render_ms, proj_ms = float(t[0]), float(t[1]), float(t[2])
     proj = net._use_proj()
-    res = {"value": world * R * args.steps / elapsed, "ms_per_step": 1e3 * elapsed / args.steps,
+    res = {"value": (R if rows else world * R) * args.steps / elapsed,
+           "ms_per_step": 1e3 * elapsed / args.steps,
            "render_kernel_ms": render_ms, "project_kernel_ms": proj_ms, "proj": proj}
     if gather is not None and rank == 0:
         res["gathered_maps"] = list(gather.recv[0].shape)
@@ -703,6 +720,7 @@ def main_c2(args, world, rank, device, dist, host_stage):
             for name, off in poses.items()}
     if rank != 0:
         return
+    rows = dist and args.shard == "rows"
     slow = min(runs, key=lambda k: runs[k]["value"])
     r = runs[slow]
     R = H * W
@@ -730,9 +748,9 @@ def main_c2(args, world, rank, device, dist, host_stage):
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": r["ms_per_step"],
-        "ms_per_frame": r["ms_per_step"],
+        "ms_per_frame": r["ms_per_step"] / (1 if rows else world),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if rows else "weak",
         "vs_baseline": None,
         "dtype": args.precision,
         "data": "synthetic (seeded U[-1,1) image, N(0,1) 256x192x640 feature grid, "
@@ -746,7 +764,8 @@ def main_c2(args, world, rank, device, dist, host_stage):
                          "lindisp") +
                         f"; render poses {'/'.join(runs)}, value = the slower ({slow})",
             "frames_per_gpu": 1, "rays_per_frame": R, "samples_per_ray": K_SAMPLES,
-            "grid": [C_GRID, HF, WF], "parallelism": f"frames{world}" +
+            "grid": [C_GRID, HF, WF],
+            "parallelism": (f"rows{world}" if rows else f"frames{world}") +
             (f"+{'rccl' if not host_stage else 'gloo-host'}_allgather" if world > 1 else ""),
             "dist_world_size": world,
         },
@@ -793,6 +812,9 @@ def main():
                     help="fp8: --config c5 only (fp8 MFMA norm product in k_seg_head)")
     ap.add_argument("--offset-pose", action="store_true",
                     help="c2/c4: time only the offset render pose (default: both poses)")
+    ap.add_argument("--shard", default="frames", choices=["frames", "rows"],
+                    help="c2 with N > 1: frames (frame r on rank r, configs[2]) or rows (one "
+                         "frame's row bands across ranks, the north star's ray tiles)")
     ap.add_argument("--identity-pose", action="store_true",
                     help="c2: time only the identity render pose (profiling runs)")
     ap.add_argument("--mode", default="proj", choices=["proj", "grid"],

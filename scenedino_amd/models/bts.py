@@ -314,7 +314,7 @@ class BTSNet(nn.Module):
 
     # -- hot path -------------------------------------------------------------
     def render_fused(self, rays, z, sb, hard_alpha_cap, want_weights=True, want_alphas=True,
-                     want_rgb_samps=False, K=None, z_seed=None, lindisp=True):
+                     want_rgb_samps=False, K=None, z_seed=None, lindisp=True, z_offset=0):
         """Fused field query + alpha compositing for all rays (used by NeRFRenderer).
         rays (R, ray_dim) fp32, z (R, K) fp32 on the GPU; R = sb * rays_per_sb.
         z None: K depths per ray drawn as sd_sample_z(seed=z_seed, lindisp) would -- inside
@@ -331,7 +331,7 @@ class BTSNet(nn.Module):
             if K is None or z_seed is None:
                 raise ValueError("render_fused: z=None needs K and z_seed")
             if not proj:
-                z = _lib.sample_z(rays, K, lindisp, seed=z_seed)
+                z = _lib.sample_z(rays, K, lindisp, seed=z_seed, offset=int(z_offset))
         R = rays.shape[0]
         K = z.shape[1] if z is not None else K
         if R % sb or gc["B"] != sb:
@@ -377,7 +377,7 @@ class BTSNet(nn.Module):
             alphas=out["alphas"].data_ptr() if want_alphas else None,
             invalid=out["invalid"].data_ptr(), invalid_f=out["invalid_f"].data_ptr(),
             rgb_samps=out["rgb_samps"].data_ptr() if want_rgb_samps else None,
-            z_lindisp=int(bool(lindisp)), z_seed=(z_seed or 0) & (2**64 - 1), z_offset=0,
+            z_lindisp=int(bool(lindisp)), z_seed=(z_seed or 0) & (2**64 - 1), z_offset=int(z_offset),
             ld_depth=depth.stride(0) if maps is not None else 0,
             ld_dino=dino.stride(0) if maps is not None else 0,
             ld_rgb=rgb.stride(0) if maps is not None else 0)

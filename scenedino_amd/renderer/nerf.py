@@ -77,6 +77,10 @@ class NeRFRenderer(torch.nn.Module):
         # debug flag: the reference's per-call NaN guard (nerf.py:428-432; host sync)
         self.check_nan = os.environ.get("SCENEDINO_AMD_NAN_CHECK", "0") == "1"
         self._rng_offset = 0
+        # index of this call's first ray within its frame: the in-kernel z jitter is keyed
+        # by the ray's frame index, so a row band rendered alone (ray-tile sharding) draws
+        # the same depths as the whole frame would
+        self.ray_offset = 0
         self._want = None             # per-forward: which per-sample outputs are written
         self._z_seed = None           # per-forward: in-kernel z sampling seed
 
@@ -150,7 +154,8 @@ class NeRFRenderer(torch.nn.Module):
                                        want_weights=want.get("weights", True),
                                        want_alphas=want.get("alphas", True),
                                        want_rgb_samps=want.get("rgb_samps", False),
-                                       K=K, z_seed=self._z_seed, lindisp=self.lindisp)
+                                       K=K, z_seed=self._z_seed, lindisp=self.lindisp,
+                                       z_offset=self.ray_offset * K)
                 weights, alphas = o["weights"], o["alphas"]
                 rgb_final, depth_final = o["rgb"], o["depth"]
                 invalid = o["invalid"]
