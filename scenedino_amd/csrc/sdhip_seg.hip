@@ -25,7 +25,9 @@
 //
 // Work unit: one wave = SG_NT x 32 points (lane = point, as the accumulator columns of
 // v_mfma_f32_32x32x16_bf16); weights are the MFMA A operands (rows = output features),
-// read straight from L2 as 1-KiB fragments (each feeds SG_NT MFMAs).  Hidden vectors
+// 1-KiB fragments (each feeds SG_NT MFMAs).  The big products (W2, M + Wn2) stream their
+// weight tiles through LDS, double-buffered and shared by the workgroup's 8 waves
+// (2 per SIMD); the small ones (W1, L) read their fragments from L2.  Hidden vectors
 // never leave the registers: an accumulator tile is converted in place into the B operand
 // of the next product (k order permuted; the host packs the A operands to match, see
 // scenedino_amd/seg_pack.py).
@@ -33,8 +35,12 @@
 
 extern "C" void sd_set_error(const char *msg);
 
-#define SG_NT 4        // 32-point column tiles per wave
-#define SG_WAVES 4     // waves per workgroup (one per SIMD)
+#ifndef SG_NT
+#define SG_NT 2        // 32-point column tiles per wave (2: 2 waves per SIMD, measured -11 % vs 4)
+#endif
+#ifndef SG_WAVES
+#define SG_WAVES 8     // waves per workgroup (two per SIMD), sharing the LDS weight stream
+#endif
 #define SG_DR 64       // reduced DINO dims (MlpDimReduction reduced_channels)
 #define SG_DL 128      // latent dims (MlpDimReduction latent_channels)
 #define SG_DC 64       // stego code dims
@@ -109,6 +115,16 @@ typedef __attribute__((ext_vector_type(8))) int i32x8_t;
 
 __device__ __forceinline__ uint32_t sg_bf16_bits(__bf16 v) { return (uint32_t)__builtin_bit_cast(unsigned short, v); }
 
+// Weight tiles are streamed through LDS, shared by the workgroup's 4 waves (each wave used
+// to read every fragment from L2 itself): 1-KiB pieces by LDS-DMA, issued as inline asm so
+// that the compiler does not fence every LDS read behind the DMA (m0 = LDS destination).
+#define SG_SLOT (12 * 1024)  // one tile: 8 bf16 fragments (+ 4 Wn2 fragments) or 4 KiB fp8
+__device__ __forceinline__ void sg_dma1k(const uint8_t *src, uint32_t lds_dst, int lane) {
+    lds_dst = __builtin_amdgcn_readfirstlane(lds_dst);
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+                 :: "v"(src + lane * 16), "s"(lds_dst) : "memory");
+}
+
 // MODE bit 0: write dino_full (transform_expand output); bit 1: segmentation head.
 // F8 (labels / seg only): the norm product |W2 h + b2| on fp8 MFMA -- h quantised to e4m3
 // with a per-point power-of-two scale (its largest value lands in [128, 256)), W2 with the
@@ -127,8 +143,20 @@ __global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const float *__restr
     const int wave = threadIdx.x >> 6;
     const int r = lane & 31, hh = lane >> 5;
     const int64_t base = ((int64_t)blockIdx.x * SG_WAVES + wave) * (32 * SG_NT);
-    if (base >= P) return;  // wave-uniform
+    // workgroup-uniform exit only: the weight stream below has barriers (waves past P run
+    // on zero inputs and store nothing)
+    if ((int64_t)blockIdx.x * SG_WAVES * (32 * SG_NT) >= P) return;
     const int T2 = DF / 32;
+    extern __shared__ __attribute__((aligned(16))) uint8_t sg_lds[];
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void *)sg_lds;
+    // stage tile pieces [0, n) (1 KiB each, piece i from src(i)) into slot; wave w issues w, w + 4, ...
+    auto stage = [&](int slot, int n, auto src) {
+        for (int i = wave; i < n; i += SG_WAVES) sg_dma1k(src(i), lds0 + slot * SG_SLOT + i * 1024, lane);
+    };
+    auto landed = [&]() {  // this wave's DMA done, then every wave's (and the previous slot free)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    };
 
     // ---- layer 1: h = relu(W1 x + b1) -> B operands hb[ct][k-step 0..7] ----
     bf16x8 hb[SG_NT][SG_DL / 16];
@@ -214,16 +242,18 @@ __global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const float *__restr
         float ss[SG_NT];
 #pragma unroll
         for (int ct = 0; ct < SG_NT; ++ct) ss[ct] = 0.f;
-        const i32x8_t *w2 = (const i32x8_t *)h.w2_f8;
-        i32x8_t cur[2];
+        const uint8_t *w2 = (const uint8_t *)h.w2_f8;  // tile t: 4 KiB at t * 4096
+        auto src = [&](int t) { return [=](int i) { return w2 + (int64_t)t * 4096 + i * 1024; }; };
+        stage(0, 4, src(0));
         f32x16 bb = sg_rows(h.b2, 0, hh);
-#pragma unroll
-        for (int st = 0; st < 2; ++st) cur[st] = w2[st * 64 + lane];
         for (int t = 0; t < T2; ++t) {
+            landed();
+            if (t + 1 < T2) stage((t + 1) & 1, 4, src(t + 1));
             const int tn = t + 1 < T2 ? t + 1 : t;
-            i32x8_t nxt[2];
+            i32x8_t cur[2];
+            const i32x8_t *sl = (const i32x8_t *)(sg_lds + (t & 1) * SG_SLOT);
 #pragma unroll
-            for (int st = 0; st < 2; ++st) nxt[st] = w2[(tn * 2 + st) * 64 + lane];
+            for (int st = 0; st < 2; ++st) cur[st] = sl[st * 64 + lane];
             const f32x16 bbn = sg_rows(h.b2, tn, hh);
             f32x16 acc[SG_NT];
 #pragma unroll
@@ -239,8 +269,6 @@ __global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const float *__restr
                     const float e = fmaf(acc[ct][i], scp[ct], bb[i]);
                     ss[ct] = fmaf(e, e, ss[ct]);
                 }
-#pragma unroll
-            for (int st = 0; st < 2; ++st) cur[st] = nxt[st];
             bb = bbn;
         }
 #pragma unroll
@@ -253,18 +281,19 @@ __global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const float *__restr
         float ss[SG_NT];
 #pragma unroll
         for (int ct = 0; ct < SG_NT; ++ct) ss[ct] = 0.f;
-        const bf16x8 *w2 = (const bf16x8 *)h.w2;
-        // software pipeline: the fragments and bias rows of tile t + 1 are loaded while
-        // tile t runs on the matrix cores (one wave per SIMD: no other wave hides L2)
-        bf16x8 cur[SG_DL / 16];
+        const uint8_t *w2 = (const uint8_t *)h.w2;  // tile t: 8 fragments at t * 8 KiB
+        auto src = [&](int t) { return [=](int i) { return w2 + (int64_t)t * 8192 + i * 1024; }; };
+        // tile t + 1 streams into the other LDS slot while tile t runs on the matrix cores
+        stage(0, 8, src(0));
         f32x16 bb = sg_rows(h.b2, 0, hh);
-#pragma unroll
-        for (int q = 0; q < SG_DL / 16; ++q) cur[q] = w2[q * 64 + lane];
         for (int t = 0; t < T2; ++t) {
+            landed();
+            if (t + 1 < T2) stage((t + 1) & 1, 8, src(t + 1));
             const int tn = t + 1 < T2 ? t + 1 : t;
-            bf16x8 nxt[SG_DL / 16];
+            bf16x8 cur[SG_DL / 16];
+            const bf16x8 *sl = (const bf16x8 *)(sg_lds + (t & 1) * SG_SLOT);
 #pragma unroll
-            for (int q = 0; q < SG_DL / 16; ++q) nxt[q] = w2[(tn * (SG_DL / 16) + q) * 64 + lane];
+            for (int q = 0; q < SG_DL / 16; ++q) cur[q] = sl[q * 64 + lane];
             const f32x16 bbn = sg_rows(h.b2, tn, hh);
             f32x16 acc[SG_NT];
 #pragma unroll
@@ -280,8 +309,6 @@ __global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const float *__restr
                     const float e = acc[ct][i] + bb[i];
                     ss[ct] = fmaf(e, e, ss[ct]);
                 }
-#pragma unroll
-            for (int q = 0; q < SG_DL / 16; ++q) cur[q] = nxt[q];
             bb = bbn;
         }
 #pragma unroll
@@ -349,27 +376,30 @@ __global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const float *__restr
     // ---- stego: nonlinear path, u = relu((M h + Wn1 b2) / n + bn1) per 32-row tile,
     //      consumed at once by Wn2 (64 x 768) ----
     {
-        const bf16x8 *wm = (const bf16x8 *)h.wm;
-        const bf16x8 *wn2 = (const bf16x8 *)h.wn2;
+        const uint8_t *wm = (const uint8_t *)h.wm, *wn2 = (const uint8_t *)h.wn2;
         const int KS = DF / 16;
-        bf16x8 cur[SG_DL / 16], cw[SG_DC / 32][2];
+        // tile t: M fragments (t, 0..7) at t * 8 KiB, then Wn2 fragments (rt, 2 t + s)
+        auto src = [&](int t) {
+            return [=](int i) {
+                return i < 8 ? wm + (int64_t)t * 8192 + i * 1024
+                             : wn2 + ((int64_t)((i - 8) >> 1) * KS + 2 * t + ((i - 8) & 1)) * 1024;
+            };
+        };
+        landed();  // the norm loop's last slot is free
+        stage(0, 12, src(0));
         f32x16 mb = sg_rows(h.bm, 0, hh), nb = sg_rows(h.bn1, 0, hh);
-#pragma unroll
-        for (int q = 0; q < SG_DL / 16; ++q) cur[q] = wm[q * 64 + lane];
-#pragma unroll
-        for (int rt = 0; rt < SG_DC / 32; ++rt)
-#pragma unroll
-            for (int s = 0; s < 2; ++s) cw[rt][s] = wn2[(rt * KS + s) * 64 + lane];
         for (int t = 0; t < T2; ++t) {
-            // tile t + 1's fragments and bias rows in flight under tile t's MFMAs
+            landed();
+            if (t + 1 < T2) stage((t + 1) & 1, 12, src(t + 1));
             const int tn = t + 1 < T2 ? t + 1 : t;
-            bf16x8 nxt[SG_DL / 16], nw[SG_DC / 32][2];
+            const bf16x8 *sl = (const bf16x8 *)(sg_lds + (t & 1) * SG_SLOT);
+            bf16x8 cur[SG_DL / 16], cw[SG_DC / 32][2];
 #pragma unroll
-            for (int q = 0; q < SG_DL / 16; ++q) nxt[q] = wm[(tn * (SG_DL / 16) + q) * 64 + lane];
+            for (int q = 0; q < SG_DL / 16; ++q) cur[q] = sl[q * 64 + lane];
 #pragma unroll
             for (int rt = 0; rt < SG_DC / 32; ++rt)
 #pragma unroll
-                for (int s = 0; s < 2; ++s) nw[rt][s] = wn2[(rt * KS + 2 * tn + s) * 64 + lane];
+                for (int s2 = 0; s2 < 2; ++s2) cw[rt][s2] = sl[(8 + 2 * rt + s2) * 64 + lane];
             const f32x16 mbn = sg_rows(h.bm, tn, hh), nbn = sg_rows(h.bn1, tn, hh);
             f32x16 acc[SG_NT];
 #pragma unroll
@@ -394,12 +424,6 @@ __global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const float *__restr
 #pragma unroll
                     for (int ct = 0; ct < SG_NT; ++ct)
                         sacc[ct][rt] = SG_MFMA(cw[rt][s], ub[ct][s], sacc[ct][rt]);
-#pragma unroll
-            for (int q = 0; q < SG_DL / 16; ++q) cur[q] = nxt[q];
-#pragma unroll
-            for (int rt = 0; rt < SG_DC / 32; ++rt)
-#pragma unroll
-                for (int s = 0; s < 2; ++s) cw[rt][s] = nw[rt][s];
             mb = mbn;
             nb = nbn;
         }
@@ -508,7 +532,7 @@ extern "C" int sd_seg_query(const float *dino, int64_t P, const sd_seg_head *h,
     // fp8 norm only for the labels / seg outputs (dino_full is the bf16 expansion)
     const bool f8 = h->w2_f8 != nullptr && mode == 2;
 #define SG_LAUNCH(M, F)                                                                            \
-    hipLaunchKernelGGL((k_seg_head<M, F>), dim3((unsigned)nblk), dim3(SG_WAVES * 64), 0, s, dino, P, \
+    hipLaunchKernelGGL((k_seg_head<M, F>), dim3((unsigned)nblk), dim3(SG_WAVES * 64), 2 * SG_SLOT, s, dino, P, \
                        h->d_full, sigma, neg_vox, *h, labels, seg, dino_full)
     switch (mode) {
     case 1: SG_LAUNCH(1, false); break;
