@@ -92,6 +92,10 @@ typedef struct sd_mlp {
     int32_t dtype;         /* SD_F32 (exact-f32 MFMA), SD_BF16 or SD_F16 (16-bit MFMA,   */
                            /* f32 accumulate); the grid must be packed in the same dtype  */
     int32_t d_hidden;      /* must be 128                                                  */
+    const float *b_empty_h; /* learn_empty (bts.py:311-319), NULL if off: [4][2][16]       */
+                           /* b_in + W_in[:, :C] . empty_feature in accumulator-row order:  */
+                           /* the layer-1 pre-code activation of a point outside the       */
+                           /* encoder frustum (sd_render_fused / sd_field_query only)       */
 } sd_mlp;
 
 /* Fused coarse render of R rays x K samples: point generation, projection into the
@@ -378,6 +382,48 @@ int sd_tokens_to_nhwc(const float *x, int32_t B, int32_t T, int32_t C, int32_t n
  * (FeatureFusionBlock, dpt_head.py:157): in (B, H, W, C) -> out (B, 2H, 2W, C). */
 int sd_upsample2x(const void *in, int32_t B, int32_t H, int32_t W, int32_t C, void *out,
                   void *stream);
+
+/* ---- SSCBench scoring (sdhip_ssc.hip) --------------------------------------- */
+
+/* Camera field-of-view mask of the voxel grid (uint8 0/1, flat index as sd_voxel_points):
+ * generate_point_grid's fov_mask (sscbench/point_utils.py:17-82, get_fov_mask :6-15) with
+ * TSDFVolume.cam2pix (sscbench/fusion.py:222-232): fp64 camera points, pixel =
+ * round-half-even(x fx / z + cx) with fx, fy, cx, cy the f32-rounded intrinsics, inside
+ * [0, img_w) x [0, img_h) and z > 0.  origin (3), T (12: rows 0..2 of the 4x4) and cam_k
+ * (9, row-major 3x3) are HOST pointers read during the call. */
+int sd_voxel_fov(const double *origin, double vox, int64_t nx, int64_t ny, int64_t nz,
+                 const double *T, const double *cam_k, int img_w, int img_h, uint8_t *fov_out,
+                 void *stream);
+
+/* Scoring configuration of sd_ssc_confusion (HOST struct, read during the call). */
+typedef struct sd_ssc_args {
+    float sigma_cutoff;          /* SIGMA_CUTOFF (evaluate_model_sscbench.py:57): 0.2         */
+    int32_t additional_invalids; /* USE_ADDITIONAL_INVALIDS (:52)                            */
+    int32_t inv_zmax;            /* identify_additional_invalids' height cut (:821): 7        */
+    int32_t n_sizes;             /* evaluation ranges (SIZES, :49), at most 4                 */
+    int32_t crop_x[4];           /* range s keeps x in [0, crop_x[s]) ...                     */
+    int32_t crop_y0[4];          /* ... and y in [crop_y0[s], crop_y1[s]) (:496-501)          */
+    int32_t crop_y1[4];
+    int32_t n_pred_labels;       /* classes of the prediction (19 cityscapes classes)         */
+    uint8_t pred_lut[256];       /* cityscapes_to_label (label_maps.yaml), values 0..15       */
+    uint8_t target_lut[256];     /* sscbench_to_label (255 -> 255)                            */
+    uint8_t target_known[256];   /* 1 where the raw target value is a key of sscbench_to_label */
+    int32_t n_target_labels;     /* number of keys (informational, > 0)                       */
+} sd_ssc_args;
+
+/* One frame's SSCBench counts (evaluate_model_sscbench.py:366-367 convert_voxels,
+ * :452-456 identify_additional_invalids (:814-827), :492 the density cut-off, :496-525
+ * compute_occupancy_numbers / _segmentation / _recall_segmentation (:862-925)): conf
+ * (n_sizes*256 + 1) uint32 on the device receives, per range s, the 16 x 16 matrix
+ * conf[s][16 y_true + y_pred] over the voxels with y_true != 255 inside the FOV, and in its
+ * last word the number of voxels whose label has no lookup-table entry (the reference's
+ * dict lookup raises on those; the caller must too).  pred (nx,ny,nz) uint8 cityscapes
+ * classes, sigma (nx,ny,nz) f32 (grown densities), target (nx,ny,nz) uint8 raw SSCBench
+ * labels, fov (nx,ny,nz) uint8; all device, 16-byte aligned, nz a multiple of 16 (<= 64).
+ * conf is zeroed on the stream first. */
+int sd_ssc_confusion(const uint8_t *pred, const float *sigma, const uint8_t *target,
+                     const uint8_t *fov, int64_t nx, int64_t ny, int64_t nz,
+                     const sd_ssc_args *args, uint32_t *conf, void *stream);
 
 #ifdef __cplusplus
 }

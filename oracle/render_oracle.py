@@ -101,9 +101,11 @@ def positional_code(xy, z, d_min=3.0, d_max=80.0, num_freqs=6, freq_factor=1.5):
 
 
 def field_query(xyz, grid, w2c_f, K_f, imgs, w2c_c, K_c, W_in, b_in, W_out, b_out,
-                with_colors=True):
+                with_colors=True, empty_feature=None):
     """xyz (B,P,3) -> dict(sigma (B,P), dino (B,P,D), rgb (B,P,3nv),
-    invalid (B,P,nv) bool, invalid_features (B,P) bool)."""
+    invalid (B,P,nv) bool, invalid_features (B,P) bool).  ``empty_feature`` (C,): the
+    learn_empty substitution of bts.py:311-319 (features of points outside the encoder
+    frustum replaced by the learned vector)."""
     B, P, _ = xyz.shape
     C = grid.shape[1]
     xy, z = _project(xyz, w2c_f.unsqueeze(1), K_f.unsqueeze(1))  # (B,1,P,*)
@@ -112,6 +114,8 @@ def field_query(xyz, grid, w2c_f, K_f, imgs, w2c_c, K_c, W_in, b_in, W_out, b_ou
     code = positional_code(xy[:, 0], z[:, 0])  # (B,P,39)
     feat = F.grid_sample(grid, xy.view(B, 1, P, 2), mode="bilinear", padding_mode="border",
                          align_corners=False).view(B, C, P).permute(0, 2, 1)
+    if empty_feature is not None:
+        feat = torch.where(inv_f.unsqueeze(-1), empty_feature.view(1, 1, C), feat)
     x = torch.cat((feat, code), -1)  # (B,P,C+39)
     h = torch.relu(x @ W_in.t() + b_in)
     out = h @ W_out.t() + b_out
@@ -155,7 +159,7 @@ def composite(z, sigma, dino, rgb, hard_alpha_cap=False):
 
 
 def render(rays, u, grid, w2c_f, K_f, imgs, w2c_c, K_c, W_in, b_in, W_out, b_out,
-           sb, lindisp=True, hard_alpha_cap=False, chunk_rays=None):
+           sb, lindisp=True, hard_alpha_cap=False, chunk_rays=None, empty_feature=None):
     """Full coarse render.  rays (SB*B', 11); grid (SB,C,h,w); per-superbatch cameras.
     Returns the reference's ``coarse`` dict layout (nerf.py:541-598)."""
     R = rays.shape[0]
@@ -173,7 +177,8 @@ def render(rays, u, grid, w2c_f, K_f, imgs, w2c_c, K_c, W_in, b_in, W_out, b_out
     step = (chunk_rays or Rb) * K
     for s0 in range(0, Rb * K, step):
         sl = slice(s0, min(s0 + step, Rb * K))
-        r = field_query(pts[:, sl], grid, w2c_f, K_f, imgs, w2c_c, K_c, W_in, b_in, W_out, b_out)
+        r = field_query(pts[:, sl], grid, w2c_f, K_f, imgs, w2c_c, K_c, W_in, b_in, W_out, b_out,
+                        empty_feature=empty_feature)
         sig[:, sl], din[:, sl], col[:, sl] = r["sigma"], r["dino"], r["rgb"]
         inv[:, sl], invf[:, sl] = r["invalid"], r["invalid_features"]
     c = composite(z, sig.view(R, K), din.view(R, K, D), col.view(R, K, 3 * nv), hard_alpha_cap)

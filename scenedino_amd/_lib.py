@@ -14,7 +14,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # SDHIP_LIB: alternative build of the same library (diagnostic builds only)
 LIB_PATH = os.environ.get("SDHIP_LIB") or os.path.join(_HERE, "libsdhip.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 CAM_WORDS = 36  # floats per camera record (include/sdhip.h SD_CAM_WORDS)
 
 SD_F32 = 0
@@ -33,6 +33,7 @@ class SdMlp(ctypes.Structure):
         ("w_in", _vp), ("b_in_h", _vp), ("w_sig_h", _vp), ("b_sigma", ctypes.c_float),
         ("w_out", _vp), ("b_dino", _vp),
         ("C", _i32), ("D", _i32), ("dtype", _i32), ("d_hidden", _i32),
+        ("b_empty_h", _vp),
     ]
 
 
@@ -96,6 +97,17 @@ class SdGemmArgs(ctypes.Structure):
     ]
 
 
+class SdSscArgs(ctypes.Structure):
+    """sd_ssc_args (include/sdhip.h): SSCBench scoring configuration."""
+    _fields_ = [
+        ("sigma_cutoff", ctypes.c_float), ("additional_invalids", _i32), ("inv_zmax", _i32),
+        ("n_sizes", _i32), ("crop_x", _i32 * 4), ("crop_y0", _i32 * 4), ("crop_y1", _i32 * 4),
+        ("n_pred_labels", _i32), ("pred_lut", ctypes.c_uint8 * 256),
+        ("target_lut", ctypes.c_uint8 * 256), ("target_known", ctypes.c_uint8 * 256),
+        ("n_target_labels", _i32),
+    ]
+
+
 (SD_EPI_BF16, SD_EPI_GELU, SD_EPI_F32, SD_EPI_RESID, SD_EPI_QKV, SD_EPI_PATCH, SD_EPI_SHUF,
  SD_EPI_NCHW) = range(8)
 
@@ -126,6 +138,11 @@ SIGNATURES = {
                         ctypes.POINTER(ctypes.c_double), _vp, _vp],
     "sd_seg_query": [_vp, _i64, ctypes.POINTER(SdSegHead), _vp, ctypes.c_float, _vp, _vp, _vp,
                      _vp],
+    "sd_voxel_fov": [ctypes.POINTER(ctypes.c_double), ctypes.c_double, _i64, _i64, _i64,
+                     ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), _i32, _i32,
+                     _vp, _vp],
+    "sd_ssc_confusion": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, ctypes.POINTER(SdSscArgs), _vp,
+                         _vp],
     "sd_gemm": [ctypes.POINTER(SdGemmArgs), _vp],
     "sd_attention": [_vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, ctypes.c_float, _vp, _vp],
     "sd_layernorm": [_vp, _i64, _i32, _vp, _vp, ctypes.c_float, _vp, _i32, _vp],
@@ -284,6 +301,31 @@ def field_query(args: SdFieldArgs, mlp: SdMlp, ref_tensor):
     lib = load()
     _check(lib.sd_field_query(ctypes.byref(args), ctypes.byref(mlp), stream_of(ref_tensor)),
            "sd_field_query")
+
+
+def voxel_fov(origin, voxel_size, dims, T, cam_k, img_w, img_h, device):
+    """SSCBench field-of-view mask (sd_voxel_fov): (nx*ny*nz,) uint8 0/1 on device."""
+    lib = load()
+    nx, ny, nz = (int(d) for d in dims)
+    o = (ctypes.c_double * 3)(*[float(v) for v in origin])
+    Tm = torch.as_tensor(T, dtype=torch.float64).reshape(-1, 4)[:3].flatten().tolist()
+    t = (ctypes.c_double * 12)(*Tm)
+    km = (ctypes.c_double * 9)(*torch.as_tensor(cam_k, dtype=torch.float64)
+                               .reshape(3, 3).flatten().tolist())
+    out = torch.empty(nx * ny * nz, device=device, dtype=torch.uint8)
+    _check(lib.sd_voxel_fov(o, float(voxel_size), nx, ny, nz, t, km, int(img_w), int(img_h),
+                            ptr(out), stream_of(out)), "sd_voxel_fov")
+    return out
+
+
+def ssc_confusion(pred, sigma, target, fov, args: SdSscArgs, conf):
+    """One frame's SSCBench confusion matrices (sd_ssc_confusion) into ``conf``
+    ((n_sizes*256 + 1,) int32 viewed as uint32, device)."""
+    lib = load()
+    nx, ny, nz = (int(d) for d in pred.shape)
+    _check(lib.sd_ssc_confusion(ptr(pred), ptr(sigma), ptr(target), ptr(fov), nx, ny, nz,
+                                ctypes.byref(args), ptr(conf), stream_of(conf)),
+           "sd_ssc_confusion")
 
 
 def voxel_points(origin, voxel_size, dims, T, device):

@@ -41,7 +41,7 @@ extern "C" void sd_set_error(const char *msg) {
     g_err[sizeof(g_err) - 1] = 0;
 }
 extern "C" const char *sd_last_error(void) { return g_err; }
-extern "C" int sd_abi_version(void) { return 5; }
+extern "C" int sd_abi_version(void) { return 6; }
 
 // Threads per workgroup, one workgroup per CU: 16-bit kernels run 8 waves (2 per SIMD,
 // <= 256 VGPRs each); the f32 parity kernels run 4 waves (1 per SIMD, 512 VGPRs).
@@ -286,13 +286,30 @@ template <> struct Prec<SD_F32> {
         Pr::mma1(lw, (qq), lane, f_, acc);                                    \
     } while (0)
 
+// learn_empty (bts.py:311-319): a point outside the encoder frustum sees the learned
+// empty feature e instead of its grid sample, so once the grid chunks are accumulated its
+// column restarts from b_in + W_in[:, :C] e (LDS rows lds_be) before the code chunks.
+__device__ __forceinline__ void sd_empty_sub(f32x16 acc[4], const float *lds_be, int h, bool inv) {
+    if (__builtin_amdgcn_ballot_w64(inv) == 0) return;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const f32x4 *bb = (const f32x4 *)(lds_be + (t * 2 + h) * 16);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            f32x4 b = bb[q];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[t][4 * q + i] = inv ? b[i] : acc[t][4 * q + i];
+        }
+    }
+}
+
 // First layer over all C/16 grid chunks + 3 code chunks, with a DEPTH-deep tap-load
 // pipeline held in registers (C % (16 DEPTH) == 0).  acc holds the initial
 // accumulator (b_in).  rs: buffer descriptor over this batch element's grid plane.
 template <int P>
 __device__ __forceinline__ void sd_layer1(__amdgpu_buffer_rsrc_t rs, int C, const PointGeo &geo,
                                           const uint8_t *lw, int lane, f32x16 acc[4],
-                                          uint32_t base = 0) {
+                                          uint32_t base = 0, const float *lds_be = nullptr) {
     typedef Prec<P> Pr;
     const int h = lane >> 5;
     const int nq = C >> 4;
@@ -321,6 +338,7 @@ __device__ __forceinline__ void sd_layer1(__amdgpu_buffer_rsrc_t rs, int C, cons
         SD_STEP(r0, q, false);
         SD_STEP(r1, q + 1, false);
     }
+    if (lds_be) sd_empty_sub(acc, lds_be, h, geo.inv_f);
 #pragma unroll
     for (int pc = 0; pc < SD_PE_CHUNKS; ++pc) {
         float f[8];
@@ -363,7 +381,8 @@ __device__ __forceinline__ float sd_relu_sigma(f32x16 acc[4], const float *lds_w
     return s;
 }
 
-// LDS image: [W_in fragments | W_out fragments (if they fit) | b_in rows | w_sigma rows]
+// LDS image: [W_in fragments | W_out fragments (if they fit) | b_in rows | w_sigma rows |
+// learn_empty rows]
 struct LdsPlan {
     int win_bytes, wout_bytes, wout_in_lds, total;
 };
@@ -381,6 +400,7 @@ __device__ __forceinline__ void sd_stage(uint8_t *lds, const sd_mlp &m, const Ld
     for (int i = threadIdx.x; i < 128; i += blockDim.x) {
         fb[i] = m.b_in_h[i];
         fb[128 + i] = m.w_sig_h[i];
+        if (m.b_empty_h) fb[256 + i] = m.b_empty_h[i];
     }
     __syncthreads();
 }
@@ -532,6 +552,7 @@ k_render(const sd_render_args a, const sd_mlp m, const LdsPlan pl) {
             r3 = Pr::load(nxt.rs, nxt.o, 3);
         }
 
+        if (m.b_empty_h) sd_empty_sub(acc, lds_ws + 128 + lo, h, cur.geo.inv_f);
         // positional-code chunks of this item
 #pragma unroll
         for (int pc = 0; pc < SD_PE_CHUNKS; ++pc) {
@@ -674,7 +695,8 @@ k_field(const sd_field_args a, const sd_mlp m, const LdsPlan pl) {
         const int lo = sd_opaque0();
         f32x16 acc[4];
         sd_init_bias(acc, lds_b + lo, h);
-        sd_layer1<P>(rs, C, geo, lds + lo, lane, acc, (uint32_t)(b * plane_bytes));
+        sd_layer1<P>(rs, C, geo, lds + lo, lane, acc, (uint32_t)(b * plane_bytes),
+                     m.b_empty_h ? lds_ws + 128 + lo : nullptr);
         float s = sd_relu_sigma(acc, lds_ws + lo, h);
         s += __shfl_xor(s, 32);
         const float sigma = sd_softplus(s + m.b_sigma);
@@ -775,7 +797,7 @@ static int sd_plan(const sd_mlp *m, LdsPlan *pl) {
     int esz = m->dtype == SD_F32 ? 4 : 2;
     pl->win_bytes = nq * 4 * SD_WAVE * 8 * esz;
     pl->wout_bytes = (m->D / 32) * 4 * SD_WAVE * (m->dtype == SD_F32 ? 64 : 32);
-    int rest = 256 * 4;
+    int rest = 384 * 4;  // b_in, w_sigma, learn_empty rows
     pl->wout_in_lds = m->dtype != SD_F32;
     pl->total = pl->win_bytes + (pl->wout_in_lds ? pl->wout_bytes : 0) + rest;
     if (pl->total > 160 * 1024) {

@@ -145,7 +145,7 @@ class PackedMLP:
     """Device buffers + the ctypes ``sd_mlp`` record.  Keep the object alive while
     kernels that use it may run."""
 
-    def __init__(self, W_in, b_in, W_out, b_out, dtype: int):
+    def __init__(self, W_in, b_in, W_out, b_out, dtype: int, empty_feature=None):
         W_in = W_in.detach().float()
         b_in = b_in.detach().float()
         W_out = W_out.detach().float()
@@ -166,6 +166,11 @@ class PackedMLP:
         self.w_in = w1.to(tdt).contiguous()
         self.b_in_h = b_in[ix["accrow"]].contiguous()
         self.w_sig_h = W_out[0][ix["accrow"]].contiguous()
+        self.b_empty_h = None
+        if empty_feature is not None:  # learn_empty (bts.py:311-319): b_in + W_in[:, :C] e
+            e = empty_feature.detach().to(device=dev, dtype=torch.float64)
+            be = b_in.double() + W_in[:, :C].double() @ e
+            self.b_empty_h = be.float()[ix["accrow"]].contiguous()
         if D % 32:  # the 32x32 grid / field kernels need D % 32 == 0 (they reject NULL)
             self.w_out = None
         elif dtype != _lib.SD_F32:
@@ -190,7 +195,8 @@ class PackedMLP:
             w_in=self.w_in.data_ptr(), b_in_h=self.b_in_h.data_ptr(),
             w_sig_h=self.w_sig_h.data_ptr(), b_sigma=self.b_sigma,
             w_out=self.w_out.data_ptr() if self.w_out is not None else None,
-            b_dino=self.b_dino.data_ptr(), C=C, D=D, dtype=dtype, d_hidden=dh)
+            b_dino=self.b_dino.data_ptr(), C=C, D=D, dtype=dtype, d_hidden=dh,
+            b_empty_h=self.b_empty_h.data_ptr() if self.b_empty_h is not None else None)
 
 
 def param_key(*ts):

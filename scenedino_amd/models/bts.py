@@ -203,7 +203,9 @@ class BTSNet(nn.Module):
     def _use_proj(self) -> bool:
         if self.fused_mode not in ("proj", "grid"):
             raise ValueError("fused_mode must be 'proj' or 'grid'")
-        return self.fused_mode == "proj" and self.precision != "fp32"
+        # learn_empty substitutes a learned vector for out-of-frustum samples: the projected
+        # grid has no slot for it, so those models render through the grid kernel
+        return self.fused_mode == "proj" and self.precision != "fp32" and not self.learn_empty
 
     def fused_supported(self, K: int) -> bool:
         """The projected 16-bit render kernel takes K % 16 == 0, K <= 128 and D % 16 == 0,
@@ -234,9 +236,10 @@ class BTSNet(nn.Module):
         if len(self.heads) != 1:
             raise NotImplementedError("fused field kernel supports a single prediction head")
         ps = (head.lin_in.weight, head.lin_in.bias, head.lin_out.weight, head.lin_out.bias)
-        key = param_key(*ps) + (self.precision,)
+        empty = self.empty_feature if self.learn_empty else None
+        key = param_key(*ps, *([empty] if empty is not None else [])) + (self.precision,)
         if self._packed is None or self._packed_key != key:
-            self._packed = PackedMLP(*ps, dtype=self._dtype())
+            self._packed = PackedMLP(*ps, dtype=self._dtype(), empty_feature=empty)
             self._packed_key = key
         return self._packed
 
@@ -250,8 +253,6 @@ class BTSNet(nn.Module):
         if nvf != 1:
             raise NotImplementedError("the field kernels take exactly one encoder view "
                                       "(ids_encoder=[0], as every shipped config)")
-        if self.learn_empty:
-            raise NotImplementedError("learn_empty=True is not used by any shipped config")
         imgs = self.grid_c_imgs
         n, nv, c3, H, W = imgs.shape
         img = _lib.pack_image(imgs.reshape(n * nv, c3, H, W).float().contiguous())
@@ -449,6 +450,10 @@ class BTSNet(nn.Module):
         x, invf, rgb, inv = FieldGather.apply(nh[1], xyz.float().contiguous(), gc["cam_f"],
                                               gc["img"], gc["cam_c"], True, nh[2])
         x = x.reshape(n * P, -1)
+        if self.learn_empty:  # bts.py:311-319: out-of-frustum samples see the learned vector
+            C = gc["C"]
+            e = self.empty_feature.to(x.dtype).view(1, C)
+            x = torch.cat((torch.where(invf.reshape(-1, 1), e, x[:, :C]), x[:, C:]), 1)
         if (type(head).__name__ == "ResnetFC" and getattr(head, "n_blocks", 1) == 0
                 and getattr(head, "d_latent", 1) == 0 and isinstance(head.activation, nn.ReLU)
                 and getattr(head, "view_number", None) in (None, 0)):

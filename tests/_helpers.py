@@ -31,7 +31,8 @@ MODEL_CONF = {"predict_dino": True, "dino_dims": 64, "learn_empty": False, "code
               "inv_z": True, "z_near": 3, "z_far": 80, "sample_color": True}
 
 
-def build_net(grid, W_in, b_in, W_out, b_out, precision="fp32", device="cuda", mode="proj"):
+def build_net(grid, W_in, b_in, W_out, b_out, precision="fp32", device="cuda", mode="proj",
+              empty_feature=None):
     from scenedino_amd.models import BTSNet
     from scenedino_amd.models.prediction_heads import ResnetFC
     from scenedino_amd.common.positional_encoding import PositionalEncoding
@@ -46,14 +47,18 @@ def build_net(grid, W_in, b_in, W_out, b_out, precision="fp32", device="cuda", m
         head.lin_in.bias.copy_(torch.as_tensor(b_in))
         head.lin_out.weight.copy_(torch.as_tensor(W_out))
         head.lin_out.bias.copy_(torch.as_tensor(b_out))
-    conf = dict(MODEL_CONF, dino_dims=D, precision=precision, fused_mode=mode)
+    conf = dict(MODEL_CONF, dino_dims=D, precision=precision, fused_mode=mode,
+                learn_empty=empty_feature is not None)
     net = BTSNet(conf, enc, code, {"normal_head": head}, final_pred_head="normal_head")
+    if empty_feature is not None:
+        with torch.no_grad():
+            net.empty_feature.copy_(torch.as_tensor(np.asarray(empty_feature)))
     return net.to(device).eval()
 
 
 def net_from_fixture(d, precision="fp32", device="cuda", mode="proj"):
     net = build_net(d["grid"], d["W_in"], d["b_in"], d["W_out"], d["b_out"], precision, device,
-                    mode)
+                    mode, empty_feature=d["empty_feature"] if "empty_feature" in d else None)
     nv = int(d["nv_render"]) if "nv_render" in d else 1
     T = lambda k: torch.as_tensor(d[k]).to(device)
     net.encode(T("images"), T("Ks"), T("poses"), ids_encoder=[0], ids_render=list(range(nv)))

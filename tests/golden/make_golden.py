@@ -20,6 +20,7 @@ Fixtures written (all float32 unless noted):
   field_query.npz         BTSNet.forward on raw points (sigma, dino, rgb, invalid)
   render_*.npz            NeRFRenderer(...).forward through BTSNet, 24x80 frames
   render_full_digest.json summary statistics of a 192x640x64 reference render
+  ssc_scoring.json        SSCBench FOV mask digest + per-frame counts (fx_ssc_scoring)
 """
 from __future__ import annotations
 
@@ -144,11 +145,11 @@ def make_pose(yaw_deg, tx, ty=0.0, tz=0.0):
     return torch.from_numpy(p)
 
 
-def build_net(ref, grid, n_views_enc=1, dino_dims=64, d_hidden=128, seed=2):
+def build_net(ref, grid, n_views_enc=1, dino_dims=64, d_hidden=128, seed=2, learn_empty=False):
     conf = {
         "predict_dino": True,
         "dino_dims": dino_dims,
-        "learn_empty": False,
+        "learn_empty": learn_empty,
         "code_mode": "z",
         "inv_z": True,
         "z_near": 3,
@@ -166,6 +167,10 @@ def build_net(ref, grid, n_views_enc=1, dino_dims=64, d_hidden=128, seed=2):
         head.lin_in.bias.copy_(0.1 * torch.randn(d_hidden, generator=g))
         head.lin_out.bias.copy_(0.1 * torch.randn(1 + dino_dims, generator=g))
     net = ref.BTSNet(conf, enc, code, {"normal_head": head}, final_pred_head="normal_head")
+    if learn_empty:  # bts.py:90-93 draws it from the global RNG; make it seeded
+        with torch.no_grad():
+            net.empty_feature.copy_(torch.randn(enc.latent_size,
+                                                generator=torch.Generator().manual_seed(seed + 7)))
     return net.eval()
 
 
@@ -262,11 +267,11 @@ def make_scene(n, nv_render, C, gh, gw, H, W, seed, offset_render=True):
     return images, Ks, poses, grid
 
 
-def fx_field_query(ref):
+def fx_field_query(ref, learn_empty=False):
     """BTSNet.forward on raw world points (the SSCBench / inference_3d call)."""
     n, C, gh, gw, H, W = 1, 256, 12, 40, 24, 80
     images, Ks, poses, grid = make_scene(n, 1, C, gh, gw, H, W, seed=11)
-    net = build_net(ref, grid)
+    net = build_net(ref, grid, learn_empty=learn_empty)
     net.encode(images, Ks, poses, ids_encoder=[0], ids_render=[0])
     g = torch.Generator().manual_seed(12)
     P = 4096
@@ -277,8 +282,9 @@ def fx_field_query(ref):
     with torch.no_grad():
         rgb, invalid, sigma, extras, sd = net(xyz)
     head = net.heads["normal_head"]
+    extra = {"empty_feature": np32(net.empty_feature)} if learn_empty else {}
     np.savez_compressed(
-        os.path.join(HERE, "field_query.npz"),
+        os.path.join(HERE, "field_query_empty.npz" if learn_empty else "field_query.npz"), **extra,
         images=np32(images), Ks=np32(Ks), poses=np32(poses), grid=np32(grid),
         W_in=np32(head.lin_in.weight), b_in=np32(head.lin_in.bias),
         W_out=np32(head.lin_out.weight), b_out=np32(head.lin_out.bias),
@@ -287,17 +293,21 @@ def fx_field_query(ref):
     )
 
 
-def fx_render(ref, name, n, nv_render, K, hard_cap, H=24, W=80, gh=12, gw=40, seed=21):
+def fx_render(ref, name, n, nv_render, K, hard_cap, H=24, W=80, gh=12, gw=40, seed=21,
+              learn_empty=False, render_offset=None):
     C = 256
     images, Ks, poses, grid = make_scene(n, nv_render, C, gh, gw, H, W, seed=seed)
-    net = build_net(ref, grid.view(n, C, gh, gw))
+    net = build_net(ref, grid.view(n, C, gh, gw), learn_empty=learn_empty)
     net.encode(images, Ks, poses, ids_encoder=[0], ids_render=list(range(nv_render)))
     renderer = ref.NeRFRenderer(n_coarse=K, lindisp=True, hard_alpha_cap=hard_cap,
                                 eval_batch_size=65536)
     wrapper = renderer.bind_parallel(net, gpus=None).eval()
     sampler = ref.ImageRaySampler(z_near=3, z_far=80, height=H, width=W)
     # render view: view 0 of each batch element (the encoder view), as the demo does
-    rays, _ = sampler.sample(None, poses[:, :1], Ks[:, :1])
+    rpose = poses[:, :1]
+    if render_offset is not None:  # render from a moved camera: rays leave the encoder frustum
+        rpose = rpose @ make_pose(*render_offset).view(1, 1, 4, 4)
+    rays, _ = sampler.sample(None, rpose, Ks[:, :1])
     g = torch.Generator().manual_seed(seed + 1)
     u = torch.rand(rays.shape[0] * rays.shape[1], K, generator=g)
     with torch.no_grad(), injected_rand(u):
@@ -305,8 +315,9 @@ def fx_render(ref, name, n, nv_render, K, hard_cap, H=24, W=80, gh=12, gw=40, se
                       want_rgb_samps=True)
     c = out["coarse"]
     head = net.heads["normal_head"]
+    extra = {"empty_feature": np32(net.empty_feature)} if learn_empty else {}
     np.savez_compressed(
-        os.path.join(HERE, f"render_{name}.npz"),
+        os.path.join(HERE, f"render_{name}.npz"), **extra,
         images=np32(images), Ks=np32(Ks), poses=np32(poses), grid=np32(grid),
         W_in=np32(head.lin_in.weight), b_in=np32(head.lin_in.bias),
         W_out=np32(head.lin_out.weight), b_out=np32(head.lin_out.bias),
@@ -475,6 +486,94 @@ def fx_voxel_points():
                    "slice_stride": 2049, "slice": pts[sel].tolist()}, f)
 
 
+def _ref_functions(path, names, ns, cls=None):
+    """Execute the named top-level (or ``cls`` static-method) function definitions of a
+    reference file, decorators dropped, in namespace ``ns``; returns ns.  Used where the
+    module itself cannot be imported here (hydra, matplotlib, numba, skimage at import)."""
+    import ast
+    src = open(path).read()
+    tree = ast.parse(src)
+    body = tree.body
+    if cls is not None:
+        body = [n for n in tree.body if isinstance(n, ast.ClassDef) and n.name == cls][0].body
+    defs = []
+    for n in body:
+        if isinstance(n, ast.FunctionDef) and n.name in names:
+            n.decorator_list = []
+            defs.append(n)
+    assert {d.name for d in defs} == set(names), (path, names)
+    exec(compile(ast.Module(body=defs, type_ignores=[]), path, "exec"), ns)
+    return ns
+
+
+def fx_ssc_scoring():
+    """SSCBench scoring (sscbench/evaluate_model_sscbench.py): the FOV mask from the
+    reference's generate_point_grid (point_utils.py:17-82) with its cam2pix (fusion.py:222-232,
+    the numba loop run as plain Python: f64 arithmetic either way) and rigid_transform
+    (fusion.py:407-411); vox2world (numba; numpy 2 scalar promotion would differ) is the
+    restatement pinned by voxel_points.json.  Then, on the seeded frames of
+    tests/_ssc_inputs.py, the reference's own convert_voxels / identify_additional_invalids /
+    compute_occupancy_numbers(_segmentation) / compute_occupancy_recall_segmentation, glued
+    as the main loop does (:366-367, 452-456, 492, 496-507)."""
+    import yaml
+    sys.path.insert(0, os.path.dirname(HERE))
+    from _ssc_inputs import make_frame
+    ssc = os.path.join(REF, "sscbench")
+    fus = _ref_functions(os.path.join(ssc, "fusion.py"), ["rigid_transform"], {"np": np})
+    fus = _ref_functions(os.path.join(ssc, "fusion.py"), ["cam2pix"], dict(fus, prange=range),
+                         cls="TSDFVolume")
+
+    def vox2world(vol_origin, vox_coords, vox_size, offsets=(0.5, 0.5, 0.5)):
+        o32 = np.asarray(vol_origin).astype(np.float32).astype(np.float64)
+        c = vox_coords.astype(np.float32).astype(np.float64)
+        return ((o32[None] + vox_size * c) + vox_size * 0.5).astype(np.float32)
+
+    tsdf = types.SimpleNamespace(vox2world=vox2world, cam2pix=fus["cam2pix"])
+    pu = _ref_functions(os.path.join(ssc, "point_utils.py"),
+                        ["generate_point_grid", "read_calib"],
+                        {"np": np, "TSDFVolume": tsdf, "rigid_transform": fus["rigid_transform"]})
+    gps = _ref_functions(os.path.join(ssc, "generate_ply_sequence.py"), ["get_cam_k"], {"np": np})
+    calib = pu["read_calib"]()
+    _, fov = pu["generate_point_grid"](vox_origin=np.array([0, -25.6, -2]),
+                                       scene_size=(51.2, 51.2, 6.4), voxel_size=0.2,
+                                       cam_E=calib["Tr"], cam_k=gps["get_cam_k"]())
+    fov = fov.reshape(256, 256, 32)
+    ev = _ref_functions(os.path.join(ssc, "evaluate_model_sscbench.py"),
+                        ["convert_voxels", "identify_additional_invalids",
+                         "compute_occupancy_numbers", "compute_occupancy_numbers_segmentation",
+                         "compute_occupancy_recall_segmentation"], {"np": np})
+    with open(os.path.join(ssc, "label_maps.yaml")) as f:
+        label_maps = yaml.safe_load(f)
+    frames = []
+    for seed in (0, 1):
+        sigmas, segs, gt = make_frame(seed)
+        segs = ev["convert_voxels"](segs.astype(np.float64), label_maps["cityscapes_to_label"])
+        target = ev["convert_voxels"](gt.astype(int), label_maps["sscbench_to_label"])
+        invalids = ev["identify_additional_invalids"](target)
+        target[invalids == 1] = 255
+        segs[sigmas < 0.2] = 0
+        per = {}
+        for size in (12.8, 25.6, 51.2):
+            n = int(size // 0.2)
+            sl = (slice(None, n), slice(128 - n // 2, 128 + n // 2), slice(None))
+            tp, fp, tn, fn = ev["compute_occupancy_numbers"](
+                y_pred=segs[sl], y_true=target[sl], fov_mask=fov[sl])
+            tps, fps, tns, fns, conf = ev["compute_occupancy_numbers_segmentation"](
+                y_pred=segs[sl], y_true=target[sl], fov_mask=fov[sl], labels=label_maps["labels"])
+            tpr, sumr = ev["compute_occupancy_recall_segmentation"](
+                y_pred=segs[sl], y_true=target[sl], fov_mask=fov[sl], labels=label_maps["labels"])
+            per[str(size)] = {"tp": int(tp), "fp": int(fp), "tn": int(tn), "fn": int(fn),
+                              "tp_seg": tps.astype(int).tolist(), "fp_seg": fps.astype(int).tolist(),
+                              "tn_seg": tns.astype(int).tolist(), "fn_seg": fns.astype(int).tolist(),
+                              "confusion_seg": conf.astype(int).tolist(),
+                              "tp_recall_seg": tpr.astype(int).tolist(),
+                              "sum_recall_seg": sumr.astype(int).tolist()}
+        frames.append({"seed": seed, "n_additional_invalids": int(invalids.sum()), "sizes": per})
+    with open(os.path.join(HERE, "ssc_scoring.json"), "w") as f:
+        json.dump({"fov_sha256": hashlib.sha256(fov.astype(np.uint8).tobytes()).hexdigest(),
+                   "fov_count": int(fov.sum()), "label_maps": label_maps, "frames": frames}, f)
+
+
 def det_fill(module, seed):
     """Deterministic parameter fill by sorted state_dict name (shared with tests/test_dpt.py):
     weights N(0, 1/fan) with fan = numel of one output slice, vectors N(0, 0.05^2)."""
@@ -587,6 +686,10 @@ def main():
         fx_dpt()
         print("dpt fixture written to", HERE)
         return
+    if os.environ.get("GOLDEN_ONLY") == "ssc":
+        fx_ssc_scoring()
+        print("ssc scoring fixture written to", HERE)
+        return
     if os.environ.get("GOLDEN_ONLY") == "seg":
         _install_stubs()
         fx_seg_head()
@@ -594,6 +697,12 @@ def main():
         print("seg / voxel fixtures written to", HERE)
         return
     ref = load_reference()
+    if os.environ.get("GOLDEN_ONLY") == "empty":
+        fx_field_query(ref, learn_empty=True)
+        fx_render(ref, "sb2_k32_empty", n=2, nv_render=1, K=32, hard_cap=False, H=16, W=48,
+                  seed=61, learn_empty=True, render_offset=(12.0, 1.5))
+        print("learn_empty fixtures written to", HERE)
+        return
     if os.environ.get("GOLDEN_ONLY") == "full_offset":
         fx_render_full_offset(ref)
         print("full offset-pose fixture written to", HERE)
@@ -617,6 +726,10 @@ def main():
         fx_render_full_offset(ref)
     fx_state_dict_manifest(ref)
     fx_reconstruct(ref)
+    fx_field_query(ref, learn_empty=True)
+    fx_render(ref, "sb2_k32_empty", n=2, nv_render=1, K=32, hard_cap=False, H=16, W=48,
+              seed=61, learn_empty=True, render_offset=(12.0, 1.5))
+    fx_ssc_scoring()
     print("golden fixtures written to", HERE)
 
 

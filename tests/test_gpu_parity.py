@@ -129,8 +129,11 @@ def test_sample_z_rng_mode_stratified():
 
 # --------------------------------------------------------------------------- field query
 @pytest.mark.parametrize("precision", ["fp32", "bf16", "fp16"])
-def test_field_query_vs_reference(precision):
-    d = load("field_query.npz")
+@pytest.mark.parametrize("fx", ["field_query.npz", "field_query_empty.npz"])
+def test_field_query_vs_reference(precision, fx):
+    """field_query_empty: learn_empty=True (bts.py:311-319), 18 % of the points outside the
+    encoder frustum see the learned vector (the layer-1 restart in sd_empty_sub)."""
+    d = load(fx)
     net = net_from_fixture(d, precision)
     with torch.no_grad():
         rgb, invalid, sigma, extras, sd = net(T(d["xyz"]))
@@ -176,7 +179,11 @@ def _render(d, precision, want_rgb_samps=True, mode="proj"):
     return out
 
 
-FIXTURES = ["render_k32_cap0.npz", "render_k64_cap1.npz", "render_sb2_nv2_k16.npz"]
+# render_sb2_k32_empty: learn_empty=True rendered from a camera 12 deg / 1.5 m off the
+# encoder view (29 % of the samples outside the encoder frustum; 16-bit "proj" models
+# with learn_empty render through the grid kernel)
+FIXTURES = ["render_k32_cap0.npz", "render_k64_cap1.npz", "render_sb2_nv2_k16.npz",
+            "render_sb2_k32_empty.npz"]
 
 
 @pytest.mark.parametrize("fx", FIXTURES)

@@ -45,13 +45,15 @@ def test_torch_oracle_gen_rays_and_z():
     assert torch.equal(z, torch.from_numpy(s["z_64_1"]))
 
 
-def test_torch_oracle_field_query_bit_exact():
-    d = load("field_query.npz")
+@pytest.mark.parametrize("fx", ["field_query.npz", "field_query_empty.npz"])
+def test_torch_oracle_field_query_bit_exact(fx):
+    d = load(fx)
     T = torch.from_numpy
     w2c = torch.inverse(T(d["poses"]))
     r = O.field_query(T(d["xyz"]), T(d["grid"]), w2c[:, 0], T(d["Ks"])[:, 0],
                       T(d["images"]) * 0.5 + 0.5, w2c, T(d["Ks"]), T(d["W_in"]), T(d["b_in"]),
-                      T(d["W_out"]), T(d["b_out"]))
+                      T(d["W_out"]), T(d["b_out"]),
+                      empty_feature=T(d["empty_feature"]) if "empty_feature" in d else None)
     assert torch.equal(r["sigma"], T(d["sigma"])[..., 0])
     assert torch.equal(r["dino"], T(d["dino"]))
     assert torch.equal(r["rgb"], T(d["rgb"]))
@@ -59,7 +61,7 @@ def test_torch_oracle_field_query_bit_exact():
 
 
 @pytest.mark.parametrize("fx", ["render_k32_cap0.npz", "render_k64_cap1.npz",
-                                "render_sb2_nv2_k16.npz"])
+                                "render_sb2_nv2_k16.npz", "render_sb2_k32_empty.npz"])
 def test_torch_oracle_render_matches_reference(fx):
     d = load(fx)
     T = torch.from_numpy
@@ -70,7 +72,8 @@ def test_torch_oracle_render_matches_reference(fx):
     out = O.render(T(d["rays"]).reshape(-1, 11), T(d["u"]), T(d["grid"]), w2c[:, 0], Ks[:, 0],
                    T(d["images"])[:, :nv] * 0.5 + 0.5, w2c[:, :nv], Ks[:, :nv], T(d["W_in"]),
                    T(d["b_in"]), T(d["W_out"]), T(d["b_out"]), sb=sb,
-                   hard_alpha_cap=bool(d["hard_cap"]))
+                   hard_alpha_cap=bool(d["hard_cap"]),
+                   empty_feature=T(d["empty_feature"]) if "empty_feature" in d else None)
     for k in ("rgb", "depth", "invalid", "weights", "alphas", "z_samps", "rgb_samps",
               "dino_features", "ray_info"):
         ref = T(d[k])

@@ -173,11 +173,13 @@ def test_grid_layout_and_field_mlp_gpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("hard", [False, True])
-def test_train_mode_render_gradients_gpu(hard):
+@pytest.mark.parametrize("hard,empty", [(False, False), (True, False), (False, True)])
+def test_train_mode_render_gradients_gpu(hard, empty):
     """train(): NeRFRenderer -> BTSNet.forward (sd_field_gather, ResnetFC, softplus) ->
     sd_composite; loss.backward() reaches the feature grid and every head parameter
-    with the reference's gradients (oracle.render under CPU autograd)."""
+    with the reference's gradients (oracle.render under CPU autograd).  ``empty``:
+    learn_empty (bts.py:311-319) with a render pose that leaves the encoder frustum, so the
+    learned vector receives the gradient of the out-of-frustum samples."""
     from scenedino_amd.common.ray_sampler import ImageRaySampler
     from scenedino_amd.renderer import NeRFRenderer
     g = torch.Generator().manual_seed(5)
@@ -192,12 +194,20 @@ def test_train_mode_render_gradients_gpu(hard):
     Kn = KN.view(1, 1, 3, 3)
     u = torch.rand(H * W, K, generator=g)
     dev = "cuda"
-    net = build_net(grid, W_in, b_in, W_out, b_out, "fp32", dev)
+    e = torch.randn(C, generator=g) if empty else None
+    net = build_net(grid, W_in, b_in, W_out, b_out, "fp32", dev, empty_feature=e)
     net.encode(images.to(dev), Kn.to(dev), pose.to(dev), ids_encoder=[0], ids_render=[0])
     leaf = net.grid_f_features[0].detach().clone().requires_grad_(True)
     net.grid_f_features[0] = leaf
     net.train()
-    rays, _ = ImageRaySampler(3, 80, H, W).sample(None, pose.to(dev), Kn.to(dev))
+    rpose = pose
+    if empty:  # 12 deg yaw + 1.5 m: about a third of the samples leave the encoder frustum
+        a = np.deg2rad(12.0)
+        m = torch.eye(4)
+        m[0, 0], m[0, 2], m[2, 0], m[2, 2] = np.cos(a), np.sin(a), -np.sin(a), np.cos(a)
+        m[0, 3] = 1.5
+        rpose = pose @ m.view(1, 1, 4, 4)
+    rays, _ = ImageRaySampler(3, 80, H, W).sample(None, rpose.to(dev), Kn.to(dev))
     r = NeRFRenderer(n_coarse=K, lindisp=True, hard_alpha_cap=hard, eval_batch_size=4096)
     r.z_jitter = u.to(dev)
     out = r.bind_parallel(net).train()(rays, want_weights=True)["coarse"]
@@ -212,9 +222,13 @@ def test_train_mode_render_gradients_gpu(hard):
 
     lg = grid.clone().requires_grad_(True)
     ps = [t.clone().requires_grad_(True) for t in (W_in, b_in, W_out, b_out)]
+    le = e.clone().requires_grad_(True) if empty else None
     w2c = torch.inverse(pose)
     ref = O.render(rays[0].cpu(), u, lg, w2c[:, 0], Kn[:, 0], images * 0.5 + 0.5, w2c, Kn,
-                   *ps, sb=1, hard_alpha_cap=hard)
+                   *ps, sb=1, hard_alpha_cap=hard, empty_feature=le)
+    if empty:
+        frac = float(ref["invalid_features"].float().mean())
+        assert 0.1 < frac < 0.9, frac
     for k in ("weights", "depth", "dino_features", "rgb"):
         assert rel_l2(out[k].detach(), ref[k].detach()) < 1e-4, k
     rl = ((ref["weights"] * gw).sum() + (ref["depth"] * gd).sum() +
@@ -225,6 +239,8 @@ def test_train_mode_render_gradients_gpu(hard):
     for p, q, name in zip((head.lin_in.weight, head.lin_in.bias, head.lin_out.weight,
                            head.lin_out.bias), ps, ("W_in", "b_in", "W_out", "b_out")):
         assert rel_l2(p.grad, q.grad) < 1e-3, name
+    if empty:
+        assert rel_l2(net.empty_feature.grad, le.grad) < 1e-3
 
 
 @pytest.mark.gpu
