@@ -506,7 +506,7 @@ def main_train(args, world, rank, device):
     from scenedino_amd.models.prediction_heads import ResnetFC
     from scenedino_amd.common.positional_encoding import PositionalEncoding
     from scenedino_amd.renderer import NeRFRenderer
-    from scenedino_amd.common.ray_sampler import ImageRaySampler
+    from scenedino_amd.common.ray_sampler import PatchRaySampler
     NB, RB, KT, PS = 4, 2048, 32, 8
     g = torch.Generator(device=device).manual_seed(rank)
     grid = torch.randn(NB, C_GRID, HF, WF, device=device, generator=g)
@@ -534,27 +534,23 @@ def main_train(args, world, rank, device):
         ray_poses[:, 0, 0, 0] = math.cos(a); ray_poses[:, 0, 0, 2] = math.sin(a)
         ray_poses[:, 0, 2, 0] = -math.sin(a); ray_poses[:, 0, 2, 2] = math.cos(a)
         ray_poses[:, 0, 0, 3] = 0.5
-    all_rays, _ = ImageRaySampler(3, 80, H, W).sample(None, ray_poses, Ks)  # (NB, H*W, 11)
+    # training/scenedino.yaml + train_scenedino_kitti_360.yaml: patch 8, 2048 rays, snapped
+    sampler = PatchRaySampler(3, 80, RB, PS, snap_to_grid=True, dino_upscaled=False)
+    dino_gt_map = torch.randn(NB, 1, D_DINO, H // PS, W // PS, device=device, generator=g)
     # the grid is an activation (the encoder's output): its gradient is computed, the
     # optimizer steps the head (a frozen-encoder config; encoder backward is not ours)
     opt = torch.optim.Adam(head.parameters(), lr=1e-4)
     amp = not args.no_amp  # train_scenedino_kitti_360.yaml: with_amp: true (fp16 autocast)
-    target_dino = torch.randn(NB, RB, D_DINO, device=device, generator=g)
-    target_rgb = torch.rand(NB, RB, 3, device=device, generator=g)
     npatch = RB // (PS * PS)
-    oy, ox = torch.meshgrid(torch.arange(PS, device=device), torch.arange(PS, device=device),
-                            indexing="ij")
 
     def step():
-        # PatchRaySampler-shaped batch: npatch random 8x8 patches per frame
-        py = torch.randint(0, H - PS + 1, (NB, npatch, 1, 1), device=device, generator=g)
-        px = torch.randint(0, W - PS + 1, (NB, npatch, 1, 1), device=device, generator=g)
-        idx = ((py + oy) * W + (px + ox)).reshape(NB, RB)
-        rays = torch.gather(all_rays, 1, idx.unsqueeze(-1).expand(NB, RB, all_rays.shape[-1]))
+        # PatchRaySampler batch (device rays + rgb / per-patch DINO targets)
+        rays, rgb_gt, dino_gt = sampler.sample(images, ray_poses, Ks, dino_features=dino_gt_map)
         with torch.autocast("cuda", dtype=torch.float16, enabled=amp):
             out = wrapper(rays, want_weights=True)["coarse"]
-            loss = ((out["dino_features"].float() - target_dino) ** 2).mean() + \
-                (out["rgb"].float() - target_rgb).abs().mean()
+            pd = out["dino_features"].float().view(NB, npatch, PS * PS, D_DINO).mean(2)
+            loss = ((pd - dino_gt) ** 2).mean() + \
+                (out["rgb"].float() - (rgb_gt * 0.5 + 0.5)).abs().mean()
         opt.zero_grad(set_to_none=True)
         leaf.grad = None
         loss.backward()
@@ -609,7 +605,8 @@ def main_train(args, world, rank, device):
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "fp16 autocast MLP, fp32 gather / compositing" if amp else "fp32",
         "data": "synthetic (N(0,1) 4x256x192x640 grid, U[-1,1) images, random targets)",
-        "config": {"workload": "train: 4 frames x 2048 rays (8x8 patches) x 32 samples, "
+        "config": {"workload": "train: 4 frames x 2048 rays (PatchRaySampler: 32 snapped 8x8 "
+                               "patches) x 32 samples, "
                                "hard_alpha_cap, ResnetFC 295-128-65, Adam step on the head, "
                                "grid gradient computed" +
                                (", rays from an offset view" if args.offset_pose else

@@ -53,6 +53,34 @@ int sd_gen_rays(const float *poses_c2w, const float *Ks, const float *frame_ids,
                 int64_t n_views, int64_t H, int64_t W, float z_near, float z_far,
                 float *rays_out, void *stream);
 
+/* Patch ray sampling (training batches): PatchRaySampler.sample with snap_to_grid
+ * (scenedino/common/ray_sampler.py:136-287).  The caller draws the patch positions with the
+ * reference's own RNG calls (host) and passes them as patches (B, n_patches, 4) int32:
+ * [view, top-left y, top-left x, DINO cell row * dino_w + col].  Only the sampled pixels'
+ * rays are generated (bit-exact with sd_gen_rays / util.gen_rays); the rgb target
+ * (images (B, V, channels, H, W)) and the DINO target (dino (B, V, dino_c, dino_h, dino_w):
+ * per pixel if dino_upscaled, else one row per patch) are gathered alongside.
+ * Outputs: rays (B, n_patches*ph*pw, 11), rgb_out (B, n_patches*ph*pw, channels),
+ * dino_out (B, n_patches*ph*pw, dino_c) or (B, n_patches, dino_c); rgb_out / dino_out may
+ * be NULL.  All pointers are device pointers except the struct itself. */
+typedef struct sd_patch_args {
+    const float *poses;      /* (B, V, 4, 4) camera-to-world                               */
+    const float *Ks;         /* (B, V, 3, 3) normalised intrinsics                         */
+    const float *frame_ids;  /* (V) ray frame-id column                                    */
+    const int32_t *patches;  /* (B, n_patches, 4)                                          */
+    const float *images;     /* (B, V, channels, H, W) or NULL                             */
+    const float *dino;       /* (B, V, dino_c, dino_h, dino_w) or NULL                     */
+    float *rays;
+    float *rgb_out;
+    float *dino_out;
+    int64_t B, V, H, W;
+    int32_t n_patches, ph, pw, channels;
+    int32_t dino_c, dino_h, dino_w, dino_upscaled;
+    float z_near, z_far;
+} sd_patch_args;
+
+int sd_patch_rays(const sd_patch_args *args, void *stream);
+
 /* Stratified inverse-depth (lindisp) or linear z sampling.
  * Replaces NeRFRenderer.sample_coarse (scenedino/renderer/nerf.py:121-141).
  * u == NULL: jitter drawn from a counter-based RNG keyed by (seed, offset);
@@ -382,6 +410,36 @@ int sd_tokens_to_nhwc(const float *x, int32_t B, int32_t T, int32_t C, int32_t n
  * (FeatureFusionBlock, dpt_head.py:157): in (B, H, W, C) -> out (B, 2H, 2W, C). */
 int sd_upsample2x(const void *in, int32_t B, int32_t H, int32_t W, int32_t C, void *out,
                   void *stream);
+
+/* ---- training loss: PatchSalienceDownsampler (sdhip_down.hip) -------------- */
+
+/* PatchSalienceDownsampler.forward_patches (scenedino/models/backbones/dino/downsampler.py:
+ * 82-98): N patches of S = ph*pw feature vectors (C channels, x (N, S, C) f32): salience
+ * s = w.x + b (1x1 conv), weights a = softmax(s * pw + pb) over the patch, out = sum a x,
+ * L2-normalised if normalize.  sd_salience_fwd writes out (N, C), sal (N, S) and wmap (N, S)
+ * (either may be NULL) and ynorm (N) (|sum a x|, needed by the backward when normalising).
+ * sd_salience_bwd takes g_out (N, C) and optionally g_sal / g_wmap (N, S), reads x, out,
+ * sal, wmap, ynorm, and writes gx (N, S, C) plus per-patch partial parameter gradients
+ * gw_part (N, C), gpw_part / gpb_part (N, S), gb_part (N) (the caller sums over N).
+ * S <= 1024, C <= 1024, C % 4 == 0; x, w, out, g_out, gx, gw_part 16-byte aligned. */
+typedef struct sd_salience_args {
+    const float *x;
+    const float *w;        /* conv.weight (C)                                              */
+    float b;               /* conv.bias                                                    */
+    const float *pw;       /* patch_weight (S)                                             */
+    const float *pb;       /* patch_bias (S)                                               */
+    int64_t N;
+    int32_t S, C, normalize, pad;
+    float *out;            /* forward output; backward input                               */
+    float *sal;            /* forward output; backward input                               */
+    float *wmap;           /* forward output; backward input                               */
+    float *ynorm;          /* forward output; backward input                               */
+    const float *g_out, *g_sal, *g_wmap;
+    float *gx, *gw_part, *gpw_part, *gpb_part, *gb_part;
+} sd_salience_args;
+
+int sd_salience_fwd(const sd_salience_args *args, void *stream);
+int sd_salience_bwd(const sd_salience_args *args, void *stream);
 
 /* ---- SSCBench scoring (sdhip_ssc.hip) --------------------------------------- */
 

@@ -53,6 +53,34 @@ def gen_rays(poses_c2w, Ks, H, W, z_near=3.0, z_far=80.0, frame_ids=None):
     return rays.reshape(-1, 11)
 
 
+def patch_sample(images, poses_c2w, Ks, patches, ph, pw, dino=None, dino_upscaled=False,
+                 z_near=3.0, z_far=80.0):
+    """PatchRaySampler.sample's gathers (ray_sampler.py:171-287) given the drawn patches
+    (n, P, 4) = [view, y, x, DINO cell row * dino_w + col]: full-frame rays then the
+    patch pixels, the rgb target and the DINO target (per pixel or per patch)."""
+    n, v, c, h, w = images.shape
+    rays_all, rgb_all, dino_all = [], [], []
+    for b in range(n):
+        rays = gen_rays(poses_c2w[b], Ks[b], h, w, z_near, z_far).view(v, h, w, 11)
+        img = images[b].permute(0, 2, 3, 1)
+        rr, cc, dd = [], [], []
+        for vv, y, x, cell in patches[b].tolist():
+            rr.append(rays[vv, y:y + ph, x:x + pw].reshape(-1, 11))
+            cc.append(img[vv, y:y + ph, x:x + pw].reshape(-1, c))
+            if dino is not None:
+                dn = dino[b].permute(0, 2, 3, 1)
+                if dino_upscaled:
+                    dd.append(dn[vv, y:y + ph, x:x + pw].reshape(-1, dn.shape[-1]))
+                else:
+                    dd.append(dn[vv].reshape(-1, dn.shape[-1])[cell].view(1, -1))
+        rays_all.append(torch.cat(rr))
+        rgb_all.append(torch.cat(cc))
+        if dino is not None:
+            dino_all.append(torch.cat(dd))
+    out = (torch.stack(rays_all), torch.stack(rgb_all))
+    return out + ((torch.stack(dino_all),) if dino is not None else ())
+
+
 # --------------------------------------------------------------------------
 # a5: stratified z sampling (nerf.py:121-141), jitter u injected
 # --------------------------------------------------------------------------

@@ -97,6 +97,29 @@ class SdGemmArgs(ctypes.Structure):
     ]
 
 
+class SdPatchArgs(ctypes.Structure):
+    """sd_patch_args (include/sdhip.h): PatchRaySampler batch."""
+    _fields_ = [
+        ("poses", _vp), ("Ks", _vp), ("frame_ids", _vp), ("patches", _vp), ("images", _vp),
+        ("dino", _vp), ("rays", _vp), ("rgb_out", _vp), ("dino_out", _vp),
+        ("B", _i64), ("V", _i64), ("H", _i64), ("W", _i64),
+        ("n_patches", _i32), ("ph", _i32), ("pw", _i32), ("channels", _i32),
+        ("dino_c", _i32), ("dino_h", _i32), ("dino_w", _i32), ("dino_upscaled", _i32),
+        ("z_near", ctypes.c_float), ("z_far", ctypes.c_float),
+    ]
+
+
+class SdSalienceArgs(ctypes.Structure):
+    """sd_salience_args (include/sdhip.h): PatchSalienceDownsampler forward / backward."""
+    _fields_ = [
+        ("x", _vp), ("w", _vp), ("b", ctypes.c_float), ("pw", _vp), ("pb", _vp), ("N", _i64),
+        ("S", _i32), ("C", _i32), ("normalize", _i32), ("pad", _i32),
+        ("out", _vp), ("sal", _vp), ("wmap", _vp), ("ynorm", _vp),
+        ("g_out", _vp), ("g_sal", _vp), ("g_wmap", _vp),
+        ("gx", _vp), ("gw_part", _vp), ("gpw_part", _vp), ("gpb_part", _vp), ("gb_part", _vp),
+    ]
+
+
 class SdSscArgs(ctypes.Structure):
     """sd_ssc_args (include/sdhip.h): SSCBench scoring configuration."""
     _fields_ = [
@@ -118,6 +141,7 @@ SIGNATURES = {
     "sd_gen_rays": [_vp, _vp, _vp, _i64, _i64, _i64, ctypes.c_float, ctypes.c_float, _vp, _vp],
     "sd_sample_z": [_vp, _i64, _i64, _i64, ctypes.c_int, _vp, ctypes.c_uint64, ctypes.c_uint64,
                     _vp, _vp],
+    "sd_patch_rays": [ctypes.POINTER(SdPatchArgs), _vp],
     "sd_pack_grid": [_vp, _i64, _i64, _i64, _i64, ctypes.c_int, _vp, _vp],
     "sd_pack_image": [_vp, _i64, _i64, _i64, _vp, _vp],
     "sd_cam_records": [_vp, _i64, _vp, _i64, _i64, _vp, _vp],
@@ -143,6 +167,8 @@ SIGNATURES = {
                      _vp, _vp],
     "sd_ssc_confusion": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, ctypes.POINTER(SdSscArgs), _vp,
                          _vp],
+    "sd_salience_fwd": [ctypes.POINTER(SdSalienceArgs), _vp],
+    "sd_salience_bwd": [ctypes.POINTER(SdSalienceArgs), _vp],
     "sd_gemm": [ctypes.POINTER(SdGemmArgs), _vp],
     "sd_attention": [_vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, ctypes.c_float, _vp, _vp],
     "sd_layernorm": [_vp, _i64, _i32, _vp, _vp, ctypes.c_float, _vp, _i32, _vp],
@@ -214,6 +240,21 @@ def gen_rays(poses_c2w, Ks, frame_ids, H, W, z_near, z_far):
                            ptr(_req(frame_ids, "frame_ids")), v, H, W, float(z_near),
                            float(z_far), ptr(out), stream_of(out)), "sd_gen_rays")
     return out
+
+
+def salience_fwd(args: SdSalienceArgs, ref_tensor):
+    lib = load()
+    _check(lib.sd_salience_fwd(ctypes.byref(args), stream_of(ref_tensor)), "sd_salience_fwd")
+
+
+def salience_bwd(args: SdSalienceArgs, ref_tensor):
+    lib = load()
+    _check(lib.sd_salience_bwd(ctypes.byref(args), stream_of(ref_tensor)), "sd_salience_bwd")
+
+
+def patch_rays(args: SdPatchArgs, ref_tensor):
+    lib = load()
+    _check(lib.sd_patch_rays(ctypes.byref(args), stream_of(ref_tensor)), "sd_patch_rays")
 
 
 def sample_z(rays, K, lindisp, u=None, seed=0, offset=0, out=None):

@@ -199,3 +199,58 @@ def composite(z, sigma, feat, rgb, hard_alpha_cap):
     return _lib.composite(z.float().contiguous(), sigma.float().contiguous(),
                           feat.float().contiguous() if feat is not None else None,
                           rgb.float().contiguous() if rgb is not None else None, hard_alpha_cap)
+
+
+class SalienceDownsample(torch.autograd.Function):
+    """PatchSalienceDownsampler.forward_patches (downsampler.py:82-98) on the device:
+    sd_salience_fwd / sd_salience_bwd.  x (N, S, C) f32 -> out (N, C), salience (N, S),
+    weight map (N, S); gradients reach x, the 1x1 conv (w, b) and patch_weight / bias."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, pw, pb, normalize):
+        N, S, C = x.shape
+        wshape = w.shape
+        x = x.float().contiguous()
+        w = w.float().reshape(C).contiguous()
+        pw_ = pw.float().reshape(S).contiguous()
+        pb_ = pb.float().reshape(S).contiguous()
+        out = torch.empty(N, C, device=x.device)
+        sal = torch.empty(N, S, device=x.device)
+        wmap = torch.empty(N, S, device=x.device)
+        ynorm = torch.empty(N, device=x.device)
+        bias = float(b.reshape(-1)[0].item()) if b is not None else 0.0
+        a = _lib.SdSalienceArgs(x=x.data_ptr(), w=w.data_ptr(), b=bias, pw=pw_.data_ptr(),
+                                pb=pb_.data_ptr(), N=N, S=S, C=C, normalize=int(bool(normalize)),
+                                out=out.data_ptr(), sal=sal.data_ptr(), wmap=wmap.data_ptr(),
+                                ynorm=ynorm.data_ptr())
+        _timed("salience", lambda: _lib.salience_fwd(a, x))
+        ctx.save_for_backward(x, w, pw_, pb_, out, sal, wmap, ynorm)
+        ctx.normalize, ctx.bias, ctx.has_b = bool(normalize), bias, b is not None
+        ctx.pshape = (pw.shape, pb.shape, wshape)
+        return out, sal, wmap
+
+    @staticmethod
+    def backward(ctx, g_out, g_sal, g_wmap):
+        x, w, pw_, pb_, out, sal, wmap, ynorm = ctx.saved_tensors
+        N, S, C = x.shape
+        if g_out is None:
+            g_out = torch.zeros_like(out)
+        g_out = g_out.float().contiguous()
+        g_sal = g_sal.float().contiguous() if g_sal is not None else None
+        g_wmap = g_wmap.float().contiguous() if g_wmap is not None else None
+        gx = torch.empty_like(x)
+        gw = torch.empty(N, C, device=x.device)
+        gpw = torch.empty(N, S, device=x.device)
+        gpb = torch.empty(N, S, device=x.device)
+        gb = torch.empty(N, device=x.device)
+        a = _lib.SdSalienceArgs(
+            x=x.data_ptr(), w=w.data_ptr(), b=ctx.bias, pw=pw_.data_ptr(), pb=pb_.data_ptr(),
+            N=N, S=S, C=C, normalize=int(ctx.normalize), out=out.data_ptr(), sal=sal.data_ptr(),
+            wmap=wmap.data_ptr(), ynorm=ynorm.data_ptr(), g_out=g_out.data_ptr(),
+            g_sal=g_sal.data_ptr() if g_sal is not None else None,
+            g_wmap=g_wmap.data_ptr() if g_wmap is not None else None,
+            gx=gx.data_ptr(), gw_part=gw.data_ptr(), gpw_part=gpw.data_ptr(),
+            gpb_part=gpb.data_ptr(), gb_part=gb.data_ptr())
+        _timed("salience_bwd", lambda: _lib.salience_bwd(a, x))
+        return (gx, gw.sum(0).reshape(ctx.pshape[2]), gb.sum().reshape(1) if ctx.has_b else None,
+                gpw.sum(0).reshape(ctx.pshape[0]), gpb.sum(0).reshape(ctx.pshape[1]), None)

@@ -13,7 +13,7 @@ after the prefix; this loader
   * accepts the older ``{"model": state_dict}`` layout (utils.py:54 comment),
   * loads into a BTSNet or a ``bind_parallel`` wrapper (``net`` + ``renderer``),
   * ignores (and reports) the training-only modules this build does not construct
-    (``encoder.downsampler.*`` of the loss, ``encoder.visualization.*``), as strict=False
+    (``encoder.visualization.*``, ``encoder.gt_wrapper.*``), as strict=False
     does in the reference,
   * but fails loudly when a parameter the kernels read is missing or mis-shaped (the
     reference would silently keep random weights there).
@@ -33,7 +33,7 @@ PREFIX_NET = "renderer.net."
 PREFIX_RENDERER = "renderer.renderer."
 # modules of the reference DINOv2Module that this build does not construct (training loss /
 # TensorBoard colouring): their keys are reported, not loaded
-IGNORED_SUBTREES = ("encoder.downsampler.", "encoder.visualization.", "encoder.gt_wrapper.")
+IGNORED_SUBTREES = ("encoder.visualization.", "encoder.gt_wrapper.")
 
 
 @dataclass

@@ -1,5 +1,5 @@
-"""Full-image ray sampler (mirror of scenedino.common.ray_sampler.ImageRaySampler,
-/root/reference/scenedino/common/ray_sampler.py:421-607).
+"""Ray samplers (mirrors of scenedino.common.ray_sampler.ImageRaySampler,
+/root/reference/scenedino/common/ray_sampler.py:421-607, and PatchRaySampler, :136-377).
 
 Ray generation runs in the bit-exact ``sd_gen_rays`` gfx950 kernel (replacing
 util.unproj_map + util.gen_rays, util.py:113-158 / 253-285).  Output layout is the
@@ -25,6 +25,149 @@ class RaySampler:
 
     def reconstruct(self, render_dict):
         raise NotImplementedError
+
+
+class PatchRaySampler(RaySampler):
+    """Training batches of square-grid patches (ray_sampler.py:136-377).
+
+    ``sample`` draws the patch positions with exactly the reference's torch.randint calls
+    (global CPU generator, same order: per frame view / row / column), so a seeded run picks
+    the same patches; the rays of only the sampled pixels, the rgb target and the DINO
+    target are then produced on the device by ``sd_patch_rays`` (rays bit-exact with
+    util.gen_rays).  ``snap_to_grid=False`` raises NotImplementedError after drawing, as the
+    reference does (:234-235)."""
+
+    def __init__(self, z_near: float, z_far: float, ray_batch_size: int, patch_size,
+                 channels: int = 3, snap_to_grid: bool = False, dino_upscaled: bool = False):
+        super().__init__(z_near, z_far)
+        self.ray_batch_size = ray_batch_size
+        self.channels = channels
+        self.snap_to_grid = snap_to_grid
+        self.dino_upscaled = dino_upscaled
+        if isinstance(patch_size, int):
+            self.patch_size_x, self.patch_size_y = patch_size, patch_size
+        elif isinstance(patch_size, (tuple, list)):
+            self.patch_size_y, self.patch_size_x = patch_size[0], patch_size[1]
+        else:
+            raise ValueError("Invalid format for patch size")
+        assert (ray_batch_size % (self.patch_size_x * self.patch_size_y)) == 0
+        self._patch_count = self.ray_batch_size // (self.patch_size_x * self.patch_size_y)
+        self._ids_cache = {}
+
+    def _draw(self, n, v, h, w, dino_hw, loss_feature_grid_shift):
+        """The reference's per-frame randint draws (:215-226) -> (n, patches, 4) int32:
+        [view, y, x, DINO cell row * dino_w + col] (:228-245)."""
+        psy, psx, pc = self.patch_size_y, self.patch_size_x, self._patch_count
+        shift = None
+        if loss_feature_grid_shift is not None:
+            shift = [int(t) for t in loss_feature_grid_shift]
+        out = torch.empty(n, pc, 4, dtype=torch.int32)
+        for n_ in range(n):
+            cv = torch.randint(0, v, (pc,))
+            if self.snap_to_grid:
+                if shift is not None:
+                    cy = torch.randint(0, h // psy - 1, (pc,))
+                    cx = torch.randint(0, w // psx - 1, (pc,))
+                else:
+                    cy = torch.randint(0, h // psy, (pc,))
+                    cx = torch.randint(0, w // psx, (pc,))
+            else:
+                torch.randint(0, h - psy, (pc,))
+                torch.randint(0, w - psx, (pc,))
+                raise NotImplementedError
+            if shift is not None:
+                y = (shift[0] % psy) + psy * cy
+                x = (shift[1] % psx) + psx * cx
+                gy = cy + (1 if shift[0] < 0 else 0)
+                gx = cx + (1 if shift[1] < 0 else 0)
+            else:
+                y, x, gy, gx = psy * cy, psx * cx, cy, cx
+            dw = dino_hw[1] if dino_hw is not None else 0
+            out[n_] = torch.stack((cv, y, x, gy * dw + gx), 1).to(torch.int32)
+        return out
+
+    def sample(self, images, poses, projs, image_ids=None, dino_features=None,
+               loss_feature_grid_shift=None):
+        n, v, c, h, w = images.shape
+        self.channels = c
+        device = images.device
+        psy, psx, pc = self.patch_size_y, self.patch_size_x, self._patch_count
+        dino_hw = tuple(dino_features.shape[-2:]) if dino_features is not None else None
+        patches = self._draw(n, v, h, w, dino_hw, loss_feature_grid_shift)
+        if device.type != "cuda":
+            raise RuntimeError("PatchRaySampler: the device sampler needs CUDA (HIP) tensors")
+        patches = patches.to(device, non_blocking=True)
+        if image_ids is None:
+            key = (v, str(device))
+            ids = self._ids_cache.get(key)
+            if ids is None:
+                ids = self._ids_cache[key] = torch.arange(v, device=device, dtype=torch.float32)
+        else:
+            ids = torch.tensor(image_ids, device=device, dtype=torch.float32)
+        npts = pc * psy * psx
+        poses_f = poses.float().contiguous()
+        Ks_f = projs.float().contiguous()
+        imgs = images.float().contiguous()
+        rays = torch.empty(n, npts, 11, device=device)
+        rgb = torch.empty(n, npts, c, device=device)
+        a = _lib.SdPatchArgs(
+            poses=poses_f.data_ptr(), Ks=Ks_f.data_ptr(), frame_ids=ids.data_ptr(),
+            patches=patches.data_ptr(), images=imgs.data_ptr(), rays=rays.data_ptr(),
+            rgb_out=rgb.data_ptr(), B=n, V=v, H=h, W=w, n_patches=pc, ph=psy, pw=psx,
+            channels=c, z_near=float(self.z_near), z_far=float(self.z_far))
+        dino_gt = None
+        if dino_features is not None:
+            dc = dino_features.shape[2]
+            dino = dino_features.float().contiguous()
+            dino_gt = torch.empty(n, npts if self.dino_upscaled else pc, dc, device=device)
+            a.dino, a.dino_out = dino.data_ptr(), dino_gt.data_ptr()
+            a.dino_c, a.dino_h, a.dino_w = dc, dino_hw[0], dino_hw[1]
+            a.dino_upscaled = int(bool(self.dino_upscaled))
+        _lib.patch_rays(a, rays)
+        if dino_features is not None:
+            return rays, rgb, dino_gt
+        return rays, rgb
+
+    def reconstruct(self, render_dict, channels=None, dino_channels=None):
+        """:289-377: reshape the flat patch batch into (n, patches, ph, pw, ...) views."""
+        psy, psx, pc = self.patch_size_y, self.patch_size_x, self._patch_count
+        n = None
+        for name, part in render_dict.items():
+            if not isinstance(part, dict) or "rgb" not in part:
+                continue
+            channels = self.channels if channels is None else channels
+            rgb_gt = render_dict["rgb_gt"]
+            dino_gt = render_dict["dino_gt"]
+            n, n_pts, v_c = part["rgb"].shape
+            v = v_c // channels
+            k = part["weights"].shape[-1]
+            part["rgb"] = part["rgb"].view(n, pc, psy, psx, v, channels)
+            part["weights"] = part["weights"].view(n, pc, psy, psx, k)
+            part["depth"] = part["depth"].view(n, pc, psy, psx)
+            part["invalid"] = part["invalid"].view(n, pc, psy, psx, k, v)
+            if "alphas" in part:
+                part["alphas"] = part["alphas"].view(n, pc, psy, psx, k)
+            if "z_samps" in part:
+                part["z_samps"] = part["z_samps"].view(n, pc, psy, psx, k)
+            if "rgb_samps" in part:
+                part["rgb_samps"] = part["rgb_samps"].view(n, pc, psy, psx, k, v, channels)
+            if "ray_info" in part:
+                part["ray_info"] = part["ray_info"].view(n, pc, psy, psx, part["ray_info"].shape[-1])
+            if "extras" in part:
+                part["extras"] = part["extras"].view(n, pc, psy, psx, part["extras"].shape[-1])
+            if "dino_features" in part:
+                part["dino_features"] = part["dino_features"].view(
+                    n, pc, psy, psx, 1, part["dino_features"].shape[-1])
+            render_dict[name] = part
+        render_dict["rgb_gt"] = rgb_gt.view(n, pc, psy, psx, channels)
+        d = dino_gt.shape[-1]
+        if self.dino_upscaled:
+            render_dict["dino_gt"] = dino_gt.view(n, pc, psy, psx, d)
+        else:
+            render_dict["dino_gt"] = dino_gt.view(n, pc, d)
+        if "dino_artifacts" in render_dict:
+            render_dict["dino_artifacts"] = render_dict["dino_artifacts"].view(n, pc, d)
+        return render_dict
 
 
 class ImageRaySampler(RaySampler):

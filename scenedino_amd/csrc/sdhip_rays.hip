@@ -6,6 +6,32 @@
 // sd_pack_*   : NCHW -> NHWC layout steps feeding the fused gather kernels.
 #include "sdhip_common.h"
 
+// One frustum ray (11 floats) of pixel (x, y) in a W x H view: unproj_map + gen_rays +
+// the frame id / NDC columns of the samplers, in the reference's fp32 operation order.
+__device__ __forceinline__ void sd_ray_at(const float *__restrict__ P, const float *__restrict__ K,
+                                          int64_t x, int64_t y, int64_t W, int64_t H, float xs,
+                                          float xe, float ys, float ye, float z_near, float z_far,
+                                          float frame_id, float *__restrict__ r) {
+    float xi = sd_linspace_at(xs, xe, W, x);
+    float yi = sd_linspace_at(ys, ye, H, y);
+    float ux = (xi - K[2]) / K[0];
+    float uy = (yi - K[5]) / K[4];
+    float uz = 1.0f;
+    // torch.norm over the last dim of 3: fma chain, then IEEE sqrt (verified bit-exact).
+    float nrm = sqrtf(fmaf(uz, uz, fmaf(uy, uy, ux * ux)));
+    ux = ux / nrm; uy = uy / nrm; uz = uz / nrm;
+    r[0] = P[3]; r[1] = P[7]; r[2] = P[11];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        float a = P[i * 4 + 0] * ux;
+        float b = P[i * 4 + 1] * uy;
+        float c = P[i * 4 + 2] * uz;
+        r[3 + i] = (a + b) + c;  // 3x3 matmul: separately rounded, left to right
+    }
+    r[6] = z_near; r[7] = z_far; r[8] = frame_id;
+    r[9] = xi; r[10] = yi;
+}
+
 // One thread per (view, pixel).  Output row = 11 floats.
 __global__ void __launch_bounds__(256) k_gen_rays(const float *__restrict__ poses,
                                                   const float *__restrict__ Ks,
@@ -19,27 +45,52 @@ __global__ void __launch_bounds__(256) k_gen_rays(const float *__restrict__ pose
     if (gid >= n_views * npix) return;
     int64_t v = gid / npix, p = gid - v * npix;
     int64_t y = p / W, x = p - y * W;
-    const float *P = poses + v * 16;
-    const float *K = Ks + v * 9;
-    float xi = sd_linspace_at(xs, xe, W, x);
-    float yi = sd_linspace_at(ys, ye, H, y);
-    float ux = (xi - K[2]) / K[0];
-    float uy = (yi - K[5]) / K[4];
-    float uz = 1.0f;
-    // torch.norm over the last dim of 3: fma chain, then IEEE sqrt (verified bit-exact).
-    float nrm = sqrtf(fmaf(uz, uz, fmaf(uy, uy, ux * ux)));
-    ux = ux / nrm; uy = uy / nrm; uz = uz / nrm;
-    float *r = rays + gid * 11;
-    r[0] = P[3]; r[1] = P[7]; r[2] = P[11];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        float a = P[i * 4 + 0] * ux;
-        float b = P[i * 4 + 1] * uy;
-        float c = P[i * 4 + 2] * uz;
-        r[3 + i] = (a + b) + c;  // 3x3 matmul: separately rounded, left to right
+    sd_ray_at(poses + v * 16, Ks + v * 9, x, y, W, H, xs, xe, ys, ye, z_near, z_far,
+              frame_ids[v], rays + gid * 11);
+}
+
+// PatchRaySampler.sample (ray_sampler.py:171-287) for snap-to-grid patches: one thread per
+// sampled ray (frame b, patch q, row py, column px).  patches (B, nq, 4) int32 holds the
+// patch's view, top-left pixel (y, x) and its feature-grid cell index (row * Wd + col of
+// the non-upscaled DINO target).  Writes the ray (only the sampled pixels are generated),
+// the rgb target and, if requested, the per-pixel (upscaled) DINO target; the per-patch
+// DINO target rows come from k_patch_dino.
+__global__ void __launch_bounds__(256) k_patch_rays(const sd_patch_args a, float xs, float xe,
+                                                    float ys, float ye) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t pp = (int64_t)a.ph * a.pw;
+    const int64_t per_b = (int64_t)a.n_patches * pp;
+    if (gid >= a.B * per_b) return;
+    const int64_t b = gid / per_b, rem = gid - b * per_b;
+    const int64_t q = rem / pp, pix = rem - q * pp;
+    const int py = (int)(pix / a.pw), px = (int)(pix - (int64_t)py * a.pw);
+    const int32_t *pt = a.patches + (b * a.n_patches + q) * 4;
+    const int64_t v = pt[0], y = pt[1] + py, x = pt[2] + px;
+    const int64_t bv = b * a.V + v;
+    sd_ray_at(a.poses + bv * 16, a.Ks + bv * 9, x, y, a.W, a.H, xs, xe, ys, ye, a.z_near, a.z_far,
+              a.frame_ids[v], a.rays + gid * 11);
+    const int64_t plane = a.H * a.W;
+    if (a.rgb_out) {
+        const float *img = a.images + bv * a.channels * plane + y * a.W + x;
+        for (int c = 0; c < a.channels; ++c) a.rgb_out[gid * a.channels + c] = img[c * plane];
     }
-    r[6] = z_near; r[7] = z_far; r[8] = frame_ids[v];
-    r[9] = xi; r[10] = yi;
+    if (a.dino_out && a.dino_upscaled) {  // dino (B, V, dc, H, W) at the pixel
+        const float *d = a.dino + bv * (int64_t)a.dino_c * plane + y * a.W + x;
+        for (int c = 0; c < a.dino_c; ++c) a.dino_out[gid * a.dino_c + c] = d[c * plane];
+    }
+}
+
+// Per-patch DINO target rows (non-upscaled): one thread per (frame, patch, channel).
+__global__ void __launch_bounds__(256) k_patch_dino(const sd_patch_args a) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t per_b = (int64_t)a.n_patches * a.dino_c;
+    if (gid >= a.B * per_b) return;
+    const int64_t b = gid / per_b, rem = gid - b * per_b;
+    const int64_t q = rem / a.dino_c, c = rem - q * a.dino_c;
+    const int32_t *pt = a.patches + (b * a.n_patches + q) * 4;
+    const int64_t bv = b * a.V + pt[0];
+    const int64_t dplane = (int64_t)a.dino_h * a.dino_w;
+    a.dino_out[gid] = a.dino[(bv * a.dino_c + c) * dplane + pt[3]];
 }
 
 __global__ void __launch_bounds__(256) k_sample_z(const float *__restrict__ rays, int64_t R,
@@ -192,6 +243,32 @@ extern "C" int sd_gen_rays(const float *poses_c2w, const float *Ks, const float 
                        (hipStream_t)stream, poses_c2w, Ks, frame_ids, n_views, H, W, xs, xe, ys,
                        ye, z_near, z_far, rays_out);
     SD_CHECK_LAUNCH("sd_gen_rays");
+    return 0;
+}
+
+extern "C" int sd_patch_rays(const sd_patch_args *a, void *stream) {
+    if (!a || !a->poses || !a->Ks || !a->frame_ids || !a->patches || !a->rays || a->B <= 0 ||
+        a->V <= 0 || a->H <= 0 || a->W <= 0 || a->ph <= 0 || a->pw <= 0 || a->n_patches <= 0 ||
+        (a->rgb_out && (!a->images || a->channels <= 0)) ||
+        (a->dino_out && (!a->dino || a->dino_c <= 0 ||
+                         (a->dino_upscaled ? (a->dino_h != a->H || a->dino_w != a->W)
+                                           : (a->dino_h <= 0 || a->dino_w <= 0))))) {
+        sd_set_error("sd_patch_rays: invalid argument");
+        return -1;
+    }
+    double pwd = 2.0 / (double)a->W, phd = 2.0 / (double)a->H;
+    float xs = (float)(-1.0 + 0.5 * pwd), xe = (float)(1.0 - 0.5 * pwd);
+    float ys = (float)(-1.0 + 0.5 * phd), ye = (float)(1.0 - 0.5 * phd);
+    const int64_t n = a->B * a->n_patches * (int64_t)a->ph * a->pw;
+    hipLaunchKernelGGL(k_patch_rays, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, *a, xs, xe, ys, ye);
+    SD_CHECK_LAUNCH("sd_patch_rays");
+    if (a->dino_out && !a->dino_upscaled) {
+        const int64_t nd = a->B * a->n_patches * (int64_t)a->dino_c;
+        hipLaunchKernelGGL(k_patch_dino, dim3((unsigned)((nd + 255) / 256)), dim3(256), 0,
+                           (hipStream_t)stream, *a);
+        SD_CHECK_LAUNCH("sd_patch_rays (dino)");
+    }
     return 0;
 }
 

@@ -11,10 +11,11 @@ NHWC operand layout without a transposition, and the ~170 launches of a 192x640 
 replayed by one graph launch (the DPT's last convolution is launched after the replay so
 that it writes the caller's fresh output tensor).
 
-Out of scope (training-loss machinery, SURVEY §8 "out"): the feature-upsampling GT
-wrappers of ``mode="upsample-gt"`` (upsampler.py, kornia) and the ``featup`` /
-``bilinear`` downsamplers of the loss; ``downsample`` returns None as the reference's does
-when no downsampler is built, and raises for a configured one.  ``VisualizationModule``
+The loss-side downsampler (``downsampler_arch``: ``featup`` = PatchSalienceDownsampler on
+the sd_salience kernels, ``bilinear``) is built as in the reference (same
+``encoder.downsampler.*`` checkpoint keys).  Out of scope (training-loss machinery, SURVEY
+§8 "out"): the feature-upsampling GT wrappers of ``mode="upsample-gt"`` (upsampler.py,
+kornia).  ``VisualizationModule``
 (PCA / k-means colouring of feature maps for TensorBoard) is not built.
 """
 from __future__ import annotations
@@ -26,6 +27,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from .dim_reduction import MlpDimReduction, NoDimReduction
+from .downsampler import BilinearDownsampler, PatchSalienceDownsampler
 from .dpt_head import DPTHead
 from .vit import DINOv2Encoder, _param_key, vit_forward
 
@@ -96,6 +98,15 @@ def build_decoder(decoder_arch: str, patch_size: int, image_size: Tuple[int, int
     raise NotImplementedError(f"decoder_arch {decoder_arch!r}")
 
 
+def build_downsampler(arch: str, dim: int, patch_size: int):
+    """dinov2_module.py:59-66."""
+    if arch == "featup":
+        return PatchSalienceDownsampler(dim, patch_size=patch_size, normalize_features=True)
+    if arch == "bilinear":
+        return BilinearDownsampler(patch_size=patch_size)
+    raise NotImplementedError(f"downsampler {arch!r}")
+
+
 def build_dim_reduction(arch: str, full_channels: int, reduced_channels: int):
     """dinov2_module.py:79-88."""
     if arch == "none":
@@ -145,6 +156,9 @@ class DINOv2Module(nn.Module):
             raise NotImplementedError(f"mode {mode!r}")
         self.mode = mode
         self.downsampler = None
+        if mode == "downsample-prediction" and downsampler_arch is not None:
+            self.downsampler = build_downsampler(downsampler_arch, self.gt_encoder.latent_size,
+                                                 self.gt_encoder.patch_size)
         self.extra_outs = 0
         self.latent_size = decoder_out_dim
         self.dino_pca_dim = dino_pca_dim
@@ -220,10 +234,9 @@ class DINOv2Module(nn.Module):
 
     def downsample(self, x, mode="patch"):
         """dinov2_module.py:185-189."""
-        if self.downsampler_arch is None:
+        if self.downsampler is None:
             return None
-        raise NotImplementedError(f"downsampler {self.downsampler_arch!r} belongs to the "
-                                  "training loss, outside the MI355X hot path")
+        return self.downsampler(x, mode)
 
     def expand_dim(self, features):
         """dinov2_module.py:191-192."""

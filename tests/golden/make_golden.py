@@ -574,6 +574,71 @@ def fx_ssc_scoring():
                    "fov_count": int(fov.sum()), "label_maps": label_maps, "frames": frames}, f)
 
 
+def fx_patch_sampler(ref):
+    """PatchRaySampler.sample (ray_sampler.py:136-287) with snap_to_grid: three cases on
+    seeded inputs, the global torch RNG seeded before each call (its randint draws pick
+    the patches)."""
+    from scenedino.common.ray_sampler import PatchRaySampler
+    g = torch.Generator().manual_seed(71)
+    n, v, c, h, w = 2, 2, 3, 24, 80
+    images = torch.rand(n, v, c, h, w, generator=g) * 2 - 1
+    K = torch.tensor(KITTI_K)
+    Ks = K.view(1, 1, 3, 3).repeat(n, v, 1, 1)
+    poses = torch.stack([torch.stack([make_pose(3.0 * b + 1.1 * vv, 0.3 * vv, 0.1 * b)
+                                      for vv in range(v)]) for b in range(n)])
+    dino = torch.randn(n, v, 16, 3, 10, generator=g)
+    dino_up = torch.randn(n, v, 8, h, w, generator=g)
+    cases = {
+        "grid": dict(ps=8, rb=512, up=False, shift=None, seed=5),
+        "shift": dict(ps=8, rb=512, up=False, shift=(-3, 5), seed=6),
+        "upscaled": dict(ps=(4, 8), rb=64, up=True, shift=None, seed=7),
+    }
+    out = {"images": np32(images), "Ks": np32(Ks), "poses": np32(poses), "dino": np32(dino),
+           "dino_up": np32(dino_up)}
+    for name, cs in cases.items():
+        smp = PatchRaySampler(3.0, 80.0, cs["rb"], cs["ps"], snap_to_grid=True,
+                              dino_upscaled=cs["up"])
+        torch.manual_seed(cs["seed"])
+        shift = torch.tensor(cs["shift"]) if cs["shift"] is not None else None
+        rays, rgb, dg = smp.sample(images, poses, Ks, dino_features=dino_up if cs["up"] else dino,
+                                   loss_feature_grid_shift=shift)
+        out[f"{name}_rays"], out[f"{name}_rgb"], out[f"{name}_dino"] = np32(rays), np32(rgb), np32(dg)
+        out[f"{name}_meta"] = np.array([cs["rb"], *(cs["ps"] if isinstance(cs["ps"], tuple) else (cs["ps"],) * 2),
+                                        int(cs["up"]), cs["seed"],
+                                        *(cs["shift"] if cs["shift"] else (0, 0)),
+                                        int(cs["shift"] is not None)], np.int64)
+    np.savez_compressed(os.path.join(HERE, "patch_sampler.npz"), **out)
+
+
+def fx_salience_downsampler():
+    """PatchSalienceDownsampler (models/backbones/dino/downsampler.py:31-98), featup with
+    normalize_features=True as build_downsampler makes it (dinov2_module.py:59-62): forward
+    (patch mode) and the autograd gradients of a seeded linear loss of its output."""
+    _install_stubs()
+    for sub in ("scenedino.models.backbones", "scenedino.models.backbones.dino"):
+        m = types.ModuleType(sub)  # bare packages: skip the heavy backbone __init__ imports
+        m.__path__ = [os.path.join(REF, *sub.split("."))]
+        sys.modules[sub] = m
+    from scenedino.models.backbones.dino.downsampler import PatchSalienceDownsampler
+    out = {}
+    for name, (n, p, ps, c) in {"p8c64": (2, 5, 8, 64), "p14c768": (1, 3, 14, 768)}.items():
+        torch.manual_seed(81)
+        m = PatchSalienceDownsampler(c, ps, True)
+        g = torch.Generator().manual_seed(82)
+        x = torch.randn(n, p, ps, ps, 1, c, generator=g).requires_grad_(True)
+        gout = torch.randn(n, p, 1, c, generator=g)
+        res, sal, wmap, pwb = m(x, "patch")
+        (res * gout).sum().backward()
+        out.update({f"{name}_x": np32(x), f"{name}_gout": np32(gout),
+                    f"{name}_conv_w": np32(m.conv.weight), f"{name}_conv_b": np32(m.conv.bias),
+                    f"{name}_pw": np32(m.patch_weight), f"{name}_pb": np32(m.patch_bias),
+                    f"{name}_out": np32(res), f"{name}_sal": np32(sal), f"{name}_wmap": np32(wmap),
+                    f"{name}_gx": np32(x.grad), f"{name}_gconv_w": np32(m.conv.weight.grad),
+                    f"{name}_gconv_b": np32(m.conv.bias.grad), f"{name}_gpw": np32(m.patch_weight.grad),
+                    f"{name}_gpb": np32(m.patch_bias.grad)})
+    np.savez_compressed(os.path.join(HERE, "salience_downsampler.npz"), **out)
+
+
 def det_fill(module, seed):
     """Deterministic parameter fill by sorted state_dict name (shared with tests/test_dpt.py):
     weights N(0, 1/fan) with fan = numel of one output slice, vectors N(0, 0.05^2)."""
@@ -686,6 +751,10 @@ def main():
         fx_dpt()
         print("dpt fixture written to", HERE)
         return
+    if os.environ.get("GOLDEN_ONLY") == "salience":
+        fx_salience_downsampler()
+        print("salience downsampler fixture written to", HERE)
+        return
     if os.environ.get("GOLDEN_ONLY") == "ssc":
         fx_ssc_scoring()
         print("ssc scoring fixture written to", HERE)
@@ -697,6 +766,10 @@ def main():
         print("seg / voxel fixtures written to", HERE)
         return
     ref = load_reference()
+    if os.environ.get("GOLDEN_ONLY") == "patch":
+        fx_patch_sampler(ref)
+        print("patch sampler fixture written to", HERE)
+        return
     if os.environ.get("GOLDEN_ONLY") == "empty":
         fx_field_query(ref, learn_empty=True)
         fx_render(ref, "sb2_k32_empty", n=2, nv_render=1, K=32, hard_cap=False, H=16, W=48,
@@ -730,6 +803,8 @@ def main():
     fx_render(ref, "sb2_k32_empty", n=2, nv_render=1, K=32, hard_cap=False, H=16, W=48,
               seed=61, learn_empty=True, render_offset=(12.0, 1.5))
     fx_ssc_scoring()
+    fx_patch_sampler(ref)
+    fx_salience_downsampler()
     print("golden fixtures written to", HERE)
 
 

@@ -52,7 +52,8 @@ def test_struct_layouts_match_the_c_header(tmp_path):
     structs = {"sd_mlp": _lib.SdMlp, "sd_render_args": _lib.SdRenderArgs,
                "sd_field_args": _lib.SdFieldArgs, "sd_head": _lib.SdHead,
                "sd_seg_head": _lib.SdSegHead, "sd_gemm_args": _lib.SdGemmArgs,
-               "sd_ssc_args": _lib.SdSscArgs}
+               "sd_ssc_args": _lib.SdSscArgs, "sd_patch_args": _lib.SdPatchArgs,
+               "sd_salience_args": _lib.SdSalienceArgs}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "sdhip.h"', "int main(void){"]
     for cname, py in structs.items():
         lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
