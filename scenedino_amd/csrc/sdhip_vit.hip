@@ -20,7 +20,10 @@
 //   k_tokens_to_grid   drop prefix tokens, (B,T,C) -> (B,C,h,w), optional L2 normalise
 //                      (vit.py:188, dinov2_module.py:270-287).
 // Residual stream x is fp32 (B*T, C); GEMM operands bf16; all accumulation fp32.
+#include <cstdlib>
+
 #include "sdhip_common.h"
+#include "sdhip_point.h"
 
 extern "C" void sd_set_error(const char *msg);
 
@@ -471,145 +474,251 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
 // ---------------------------------------------------------------------------
 // flash attention (head_dim 64)
 // ---------------------------------------------------------------------------
+// A wave owns 32 queries of one (batch, head) and walks 64-key blocks with an online
+// softmax: S^T = K Q^T (2 tiles of 32 keys x 4 k-steps, v_mfma_f32_32x32x16_bf16: a query's
+// scores sit in its lane), P straight from the S^T accumulator into the B operand of
+// O^T += V^T P (2 head-dim tiles x 2 key tiles x 2 k-steps).  The K rows of a 32-key tile
+// are fed to the MFMA in the order at_perm (bits 2 and 3 of the row swapped): then the keys
+// a lane holds for k-step s of the P operand are 8 consecutive keys, so every K and V^T
+// fragment is one 16-B load (from LDS or straight from L2) with no register shuffles.
+//   k_attn_lds : 4 waves = 128 consecutive queries share each K / V^T block, staged once
+//                per workgroup through double-buffered LDS (one barrier per block).
+//   k_attn_dir : 4 waves = 32 queries x 4 key quarters (fills the chip when there are few
+//                query tiles, e.g. 481-token ViTs); fragments loaded straight from L2 into
+//                registers a block ahead; the 4 partial softmax states merge through LDS.
+// exp2 in the log2 domain (scores scaled by scale * log2 e) on the raw v_exp_f32; the O
+// rescale is skipped while no query's running maximum moved.
 #define AT_HD 64
-
 #define AT_ROW 72  // bf16 per LDS tile row: 64 + 8 pad (144-B rows: conflict-free b128 reads)
 
-__global__ void __launch_bounds__(256) k_attn(const __bf16 *__restrict__ Q,
-                                              const __bf16 *__restrict__ K,
-                                              const __bf16 *__restrict__ Vt, int T, int Tp,
-                                              int H, float sl2e, __bf16 *__restrict__ out) {
-    // One workgroup = 32 queries of one (batch, head); its 4 waves split the 64-key blocks
-    // (wave w takes blocks w, w+4, ...), each keeping its own running (max, sum, O^T), and
-    // combine them through LDS at the end (a batch-1 ViT-B/8 has only 12 heads x 61 query
-    // tiles: without the split, fewer waves than SIMDs).  A block's K (64 keys x 64) and V^T
-    // (64 x 64 keys) tiles are contiguous 128-B rows in HBM: each wave streams them with
-    // 16-B coalesced loads (prefetched one block ahead in registers) into its own LDS tiles,
-    // and the MFMA fragments are read from there.
-    __shared__ __attribute__((aligned(16))) __bf16 s_kv[4][2][64 * AT_ROW];  // [wave][K | V^T]
-    __shared__ float s_m[4][64], s_l[4][64];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+__device__ __forceinline__ int at_perm(int r) { return (r & ~12) | ((r & 4) << 1) | ((r & 8) >> 1); }
+
+struct AtState {
+    f32x16 o[2];
+    float m, l;
+};
+
+// key of accumulator register i (lane half h) of S^T tile t under at_perm
+__device__ __forceinline__ int at_key(int t, int i, int h) {
+    return 32 * t + 16 * (i >> 3) + 8 * h + 4 * ((i >> 2) & 1) + (i & 3);
+}
+
+__device__ __forceinline__ void at_block(AtState &S, const bf16x8 qb[4], const bf16x8 kf[2][4],
+                                         const bf16x8 vf[2][2][2], int kb, int T, int h,
+                                         float sl2e) {
+    f32x16 st[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        st[t] = vt_zero16();
+#pragma unroll
+        for (int s = 0; s < 4; ++s) st[t] = VT_MFMA(kf[t][s], qb[s], st[t]);
+    }
+    if (kb + 64 > T) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                if (kb + at_key(t, i, h) >= T) st[t][i] = -INFINITY;
+    }
+    float mx = st[0][0];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) mx = fmaxf(mx, st[t][i]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    const float mnew = fmaxf(S.m, mx * sl2e);
+    const float alpha = __builtin_amdgcn_exp2f(S.m - mnew);
+    S.m = mnew;
+    bf16x8 pb[2][2];
+    float ps = 0.f;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const float p = __builtin_amdgcn_exp2f(fmaf(st[t][i], sl2e, -mnew));
+            ps += p;
+            pb[t][i >> 3][i & 7] = (__bf16)p;
+        }
+    S.l = fmaf(S.l, alpha, ps);
+    if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {
+#pragma unroll
+        for (int ht = 0; ht < 2; ++ht)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) S.o[ht][i] *= alpha;
+    }
+#pragma unroll
+    for (int ht = 0; ht < 2; ++ht)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) S.o[ht] = VT_MFMA(vf[ht][t][s], pb[t][s], S.o[ht]);
+}
+
+// Q^T as B operand: lane (query r, half h), k-step s: Q[q][16 s + 8 h + j]
+__device__ __forceinline__ void at_load_q(const __bf16 *Qh, int q, int T, int h, bf16x8 qb[4]) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        if (q < T)
+            qb[s] = *(const bf16x8 *)(Qh + (int64_t)q * AT_HD + 16 * s + 8 * h);
+        else
+#pragma unroll
+            for (int j = 0; j < 8; ++j) qb[s][j] = (__bf16)0.f;
+    }
+}
+
+// out[b, q, head * 64 + e] = O^T[e][q] / l: registers i of tile ht hold e = 32 ht + 8 (i >> 2)
+// + 4 h + (i & 3) -> four 8-B stores per tile
+__device__ __forceinline__ void at_store(const f32x16 o[2], float inv, __bf16 *dst, int h) {
+#pragma unroll
+    for (int ht = 0; ht < 2; ++ht)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            bf16x4 v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = (__bf16)(o[ht][4 * g + e] * inv);
+            *(bf16x4 *)(dst + 32 * ht + 8 * g + 4 * h) = v;
+        }
+}
+
+__global__ void __launch_bounds__(256) k_attn_lds(const __bf16 *__restrict__ Q,
+                                                  const __bf16 *__restrict__ K,
+                                                  const __bf16 *__restrict__ Vt, int T, int Tp,
+                                                  int H, float sl2e, __bf16 *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) __bf16 s_kv[2][2][64 * AT_ROW];  // [buf][K | V^T]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, h = lane >> 5;
     const int bh = blockIdx.y;
-    const int q0 = blockIdx.x * 32;
-    const __bf16 *Qh = Q + (int64_t)bh * T * AT_HD;
+    const int q = blockIdx.x * 128 + 32 * wave + r;
     const __bf16 *Kh = K + (int64_t)bh * Tp * AT_HD;
     const __bf16 *Vh = Vt + (int64_t)bh * AT_HD * Tp;
-    __bf16 *sK = s_kv[wave][0];
-    __bf16 *sV = s_kv[wave][1];
-
-    // Q^T as B operand: lane (query r, half h), k-step s: Q[q][16 s + 8 h + j]
-    bf16x8 qb[AT_HD / 16];
-    {
-        const int q = q0 + r;
-#pragma unroll
-        for (int s = 0; s < AT_HD / 16; ++s) {
-            if (q < T)
-                qb[s] = *(const bf16x8 *)(Qh + (int64_t)q * AT_HD + 16 * s + 8 * h);
-            else
-#pragma unroll
-                for (int j = 0; j < 8; ++j) qb[s][j] = (__bf16)0.f;
-        }
-    }
-    f32x16 o[2];
-    o[0] = vt_zero16();
-    o[1] = vt_zero16();
-    float mrun = -INFINITY, lsum = 0.f;
-
-    // staging registers: chunk c = lane + 64 i (i < 8) of a 64 x 128-B tile, row c / 8,
-    // 16-B column c % 8
-    bf16x8 gk[8], gv[8];
+    bf16x8 qb[4];
+    at_load_q(Q + (int64_t)bh * T * AT_HD, q, T, h, qb);
+    AtState S;
+    S.o[0] = vt_zero16();
+    S.o[1] = vt_zero16();
+    S.m = -INFINITY;
+    S.l = 0.f;
+    // staging: chunk c = tid + 256 i of a 64-row x 128-B tile, row c / 8, 16-B column c % 8
+    bf16x8 gk[2], gv[2];
     auto gload = [&](int kb) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int c = lane + 64 * i, row = c >> 3, col = (c & 7) * 8;
+        for (int i = 0; i < 2; ++i) {
+            const int c = tid + 256 * i, row = c >> 3, col = (c & 7) * 8;
             gk[i] = *(const bf16x8 *)(Kh + (int64_t)(kb + row) * AT_HD + col);
             gv[i] = *(const bf16x8 *)(Vh + (int64_t)row * Tp + kb + col);
         }
     };
-    if (64 * wave < Tp) gload(64 * wave);
-    for (int kb = 64 * wave; kb < Tp; kb += 256) {
+    auto swrite = [&](int buf) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int c = lane + 64 * i, row = c >> 3, col = (c & 7) * 8;
-            *(bf16x8 *)(sK + row * AT_ROW + col) = gk[i];
-            *(bf16x8 *)(sV + row * AT_ROW + col) = gv[i];
+        for (int i = 0; i < 2; ++i) {
+            const int c = tid + 256 * i, row = c >> 3, col = (c & 7) * 8;
+            *(bf16x8 *)(s_kv[buf][0] + row * AT_ROW + col) = gk[i];
+            *(bf16x8 *)(s_kv[buf][1] + row * AT_ROW + col) = gv[i];
         }
-        if (kb + 256 < Tp) gload(kb + 256);  // next block in flight under this one
-        // S^T tiles: keys kb + 32 t + row, queries on the lanes
-        f32x16 st[2];
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            st[t] = vt_zero16();
-#pragma unroll
-            for (int s = 0; s < AT_HD / 16; ++s)
-                st[t] = VT_MFMA(*(const bf16x8 *)(sK + (32 * t + r) * AT_ROW + 16 * s + 8 * h),
-                                qb[s], st[t]);
-        }
-        // mask keys >= T (zero-padded rows of the last block)
-        if (kb + 64 > T) {
-#pragma unroll
-            for (int t = 0; t < 2; ++t)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const int key = kb + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
-                    if (key >= T) st[t][i] = -INFINITY;
-                }
-        }
-        float mx = -INFINITY;
+    };
+    gload(0);
+    swrite(0);
+    __syncthreads();
+    const int nb = Tp >> 6;
+    const int pr = at_perm(r);
+    for (int b = 0; b < nb; ++b) {
+        if (b + 1 < nb) gload(64 * (b + 1));
+        const __bf16 *sK = s_kv[b & 1][0], *sV = s_kv[b & 1][1];
+        bf16x8 kf[2][4], vf[2][2][2];
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
-            for (int i = 0; i < 16; ++i) mx = fmaxf(mx, st[t][i]);
-        mx = fmaxf(mx, __shfl_xor(mx, 32));
-        const float mnew = fmaxf(mrun, mx * sl2e);
-        const float alpha = exp2f(mrun - mnew);
-        mrun = mnew;
-        bf16x8 pb[2][2];
-        float ps = 0.f;
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const float p = exp2f(fmaf(st[t][i], sl2e, -mnew));
-                ps += p;
-                pb[t][i >> 3][i & 7] = (__bf16)p;
-            }
-        lsum = fmaf(lsum, alpha, ps);
+            for (int s = 0; s < 4; ++s)
+                kf[t][s] = *(const bf16x8 *)(sK + (32 * t + pr) * AT_ROW + 16 * s + 8 * h);
 #pragma unroll
         for (int ht = 0; ht < 2; ++ht)
 #pragma unroll
-            for (int i = 0; i < 16; ++i) o[ht][i] *= alpha;
-        // O^T += V^T P: A = V^T rows (head dim), k = keys in the accumulator-operand order
-        // (element j of lane half h: key 32 t + 16 s + 8 (j >> 2) + 4 h + (j & 3))
+            for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int ht = 0; ht < 2; ++ht) {
-            const __bf16 *vr = sV + (32 * ht + r) * AT_ROW + 4 * h;
+                for (int s = 0; s < 2; ++s)
+                    vf[ht][t][s] =
+                        *(const bf16x8 *)(sV + (32 * ht + r) * AT_ROW + 32 * t + 16 * s + 8 * h);
+        at_block(S, qb, kf, vf, 64 * b, T, h, sl2e);
+        if (b + 1 < nb) swrite((b + 1) & 1);
+        __syncthreads();
+    }
+    const float l = S.l + __shfl_xor(S.l, 32);
+    if (q < T) {
+        const int bb = bh / H, head = bh - bb * H;
+        at_store(S.o, 1.f / l, out + ((int64_t)bb * T + q) * (int64_t)(H * AT_HD) + head * AT_HD, h);
+    }
+}
+
+__global__ void __launch_bounds__(256) k_attn_dir(const __bf16 *__restrict__ Q,
+                                                  const __bf16 *__restrict__ K,
+                                                  const __bf16 *__restrict__ Vt, int T, int Tp,
+                                                  int H, float sl2e, __bf16 *__restrict__ out) {
+    __shared__ float s_o[4][2][16][64];  // [wave][hd tile][acc register][lane]
+    __shared__ float s_m[4][64], s_l[4][64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int bh = blockIdx.y;
+    const int q = blockIdx.x * 32 + r;
+    bf16x8 qb[4];
+    at_load_q(Q + (int64_t)bh * T * AT_HD, q, T, h, qb);
+    AtState S;
+    S.o[0] = vt_zero16();
+    S.o[1] = vt_zero16();
+    S.m = -INFINITY;
+    S.l = 0.f;
+    // K rows (at_perm order) and V^T rows of this lane as byte offsets into the head's planes
+    const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<__bf16 *>(K + (int64_t)bh * Tp * AT_HD), 0, (uint32_t)Tp * AT_HD * 2, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<__bf16 *>(Vt + (int64_t)bh * AT_HD * Tp), 0, (uint32_t)Tp * AT_HD * 2, 0x00020000);
+    const uint32_t ko = (uint32_t)(at_perm(r) * AT_HD + 8 * h) * 2;
+    const uint32_t vo = (uint32_t)(r * Tp + 8 * h) * 2;
+    const uint32_t vrow32 = (uint32_t)(32 * Tp) * 2;
+    bf16x8 kf[2][4], vf[2][2][2], kn[2][4], vn[2][2][2];
+    auto fload = [&](int kb, bf16x8 (&kd)[2][4], bf16x8 (&vd)[2][2][2]) {
+        const uint32_t ks = (uint32_t)kb * AT_HD * 2, vs = (uint32_t)kb * 2;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+                kd[t][s] = __builtin_bit_cast(
+                    bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rk, ko + (32 * t * AT_HD + 16 * s) * 2, ks, 0));
+#pragma unroll
+        for (int ht = 0; ht < 2; ++ht)
 #pragma unroll
             for (int t = 0; t < 2; ++t)
 #pragma unroll
-                for (int s = 0; s < 2; ++s) {
-                    const bf16x4 lo = *(const bf16x4 *)(vr + 32 * t + 16 * s);
-                    const bf16x4 hi = *(const bf16x4 *)(vr + 32 * t + 16 * s + 8);
-                    bf16x8 a;
+                for (int s = 0; s < 2; ++s)
+                    vd[ht][t][s] = __builtin_bit_cast(
+                        bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                    rv, vo + ht * vrow32 + (32 * t + 16 * s) * 2, vs, 0));
+    };
+    int kb = 64 * wave;
+    if (kb < Tp) fload(kb, kf, vf);
+    for (; kb < Tp; kb += 256) {
+        const bool more = kb + 256 < Tp;
+        if (more) fload(kb + 256, kn, vn);  // next block in flight under this one
+        at_block(S, qb, kf, vf, kb, T, h, sl2e);
+        if (more) {
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        a[j] = lo[j];
-                        a[4 + j] = hi[j];
-                    }
-                    o[ht] = VT_MFMA(a, pb[t][s], o[ht]);
-                }
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int s = 0; s < 4; ++s) kf[t][s] = kn[t][s];
+#pragma unroll
+            for (int ht = 0; ht < 2; ++ht)
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+#pragma unroll
+                    for (int s = 0; s < 2; ++s) vf[ht][t][s] = vn[ht][t][s];
         }
     }
-    // combine the 4 waves' partial softmax states (the K / V tiles are dead: reuse them)
-    __syncthreads();
-    float *s_o = (float *)&s_kv[0][0][0];  // [wave][hd tile][acc register][lane]
-    s_m[wave][lane] = mrun;                 // identical in both halves
-    s_l[wave][lane] = lsum;                 // per-half partial sums
+    // merge the 4 waves' partial softmax states
+    s_m[wave][lane] = S.m;  // identical in both halves
+    s_l[wave][lane] = S.l;  // per-half partial sums
 #pragma unroll
     for (int ht = 0; ht < 2; ++ht)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) s_o[((wave * 2 + ht) * 16 + i) * 64 + lane] = o[ht][i];
+        for (int i = 0; i < 16; ++i) s_o[wave][ht][i][lane] = S.o[ht][i];
     __syncthreads();
     float M = -INFINITY;
 #pragma unroll
@@ -618,11 +727,10 @@ __global__ void __launch_bounds__(256) k_attn(const __bf16 *__restrict__ Q,
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
         const float mw = s_m[w][lane];
-        fw[w] = mw == -INFINITY ? 0.f : exp2f(mw - M);  // a wave with no key block
+        fw[w] = mw == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(mw - M);  // a wave with no block
         L = fmaf(fw[w], s_l[w][r] + s_l[w][r + 32], L);
     }
     const float inv = 1.f / L;
-    const int q = q0 + r;
     if (q < T) {
         // wave w writes accumulator registers 4w..4w+3 of both head-dim tiles:
         // rows 32 ht + 8 w + 4 h + e (4 contiguous head-dim values, one 8-B store)
@@ -635,8 +743,7 @@ __global__ void __launch_bounds__(256) k_attn(const __bf16 *__restrict__ Q,
             for (int e = 0; e < 4; ++e) {
                 float acc = 0.f;
 #pragma unroll
-                for (int w = 0; w < 4; ++w)
-                    acc = fmaf(fw[w], s_o[((w * 2 + ht) * 16 + 4 * wave + e) * 64 + lane], acc);
+                for (int w = 0; w < 4; ++w) acc = fmaf(fw[w], s_o[w][ht][4 * wave + e][lane], acc);
                 v[e] = (__bf16)(acc * inv);
             }
             *(bf16x4 *)(dst + 32 * ht + 8 * wave + 4 * h) = v;
@@ -901,10 +1008,25 @@ extern "C" int sd_attention(const void *q, const void *k, const void *vt, int32_
         sd_set_error("sd_attention: invalid argument (head_dim 64, tokens_pad % 64 == 0)");
         return -1;
     }
-    dim3 grid((unsigned)((tokens + 31) / 32), (unsigned)(B * heads));
-    hipLaunchKernelGGL(k_attn, grid, dim3(256), 0, (hipStream_t)stream, (const __bf16 *)q,
-                       (const __bf16 *)k, (const __bf16 *)vt, tokens, tokens_pad, heads,
-                       scale * 1.4426950408889634f, (__bf16 *)out);
+    // 128-query workgroups sharing K / V^T through LDS once they cover half the CUs
+    // (ViT-B/8, 1921 tokens x 12 heads: 30.7 us vs 47.7 us split); below that 32-query
+    // workgroups splitting the keys (481 tokens: 7.9 us vs 10.5 us).  SD_ATTN=lds / dir
+    // forces one (A/B runs).
+    const float sl2e = scale * 1.4426950408889634f;
+    const int64_t wg128 = (int64_t)((tokens + 127) / 128) * B * heads;
+    const char *force = getenv("SD_ATTN");
+    const bool lds = (force && force[0]) ? force[0] == 'l' : 2 * wg128 >= (int64_t)sd_num_cus();
+    if (lds) {
+        dim3 grid((unsigned)((tokens + 127) / 128), (unsigned)(B * heads));
+        hipLaunchKernelGGL(k_attn_lds, grid, dim3(256), 0, (hipStream_t)stream, (const __bf16 *)q,
+                           (const __bf16 *)k, (const __bf16 *)vt, tokens, tokens_pad, heads, sl2e,
+                           (__bf16 *)out);
+    } else {
+        dim3 grid((unsigned)((tokens + 31) / 32), (unsigned)(B * heads));
+        hipLaunchKernelGGL(k_attn_dir, grid, dim3(256), 0, (hipStream_t)stream, (const __bf16 *)q,
+                           (const __bf16 *)k, (const __bf16 *)vt, tokens, tokens_pad, heads, sl2e,
+                           (__bf16 *)out);
+    }
     if (hipGetLastError() != hipSuccess) {
         sd_set_error("sd_attention: launch failed");
         return -2;
