@@ -58,6 +58,15 @@ class FixedGridEncoder(torch.nn.Module):
         return [self.grid]
 
 
+GRID_LAYOUT = "nhwc"  # --grid-layout: the native encoder's DPT writes channels-last grids
+
+
+def _layout(grid):
+    """The synthetic grid in the layout the native encoder delivers (channels-last, a
+    (B, C, H, W) view of NHWC storage) or, --grid-layout nchw, the reference's NCHW."""
+    return grid.contiguous(memory_format=torch.channels_last) if GRID_LAYOUT == "nhwc" else grid
+
+
 def make_scene(frame_seed: int, device, precision="bf16", offset_pose=False):
     """Synthetic inputs of SURVEY.md §8(d): image U[-1,1) (seed frame), grid N(0,1)
     (seed 1+frame), MLP kaiming (seed 2)."""
@@ -69,7 +78,8 @@ def make_scene(frame_seed: int, device, precision="bf16", offset_pose=False):
 
     g = torch.Generator().manual_seed(frame_seed)
     images = (torch.rand(1, 1, 3, H, W, generator=g) * 2 - 1).to(device)
-    grid = torch.randn(1, C_GRID, HF, WF, generator=torch.Generator().manual_seed(1 + frame_seed))
+    grid = _layout(torch.randn(1, C_GRID, HF, WF,
+                               generator=torch.Generator().manual_seed(1 + frame_seed)))
     torch.manual_seed(2)
     head = ResnetFC(d_in=D_IN, d_out=1 + D_DINO, n_blocks=0, d_hidden=D_HIDDEN)
     conf = {"predict_dino": True, "dino_dims": D_DINO, "learn_empty": False, "code_mode": "z",
@@ -509,7 +519,7 @@ def main_train(args, world, rank, device):
     from scenedino_amd.common.ray_sampler import PatchRaySampler
     NB, RB, KT, PS = 4, 2048, 32, 8
     g = torch.Generator(device=device).manual_seed(rank)
-    grid = torch.randn(NB, C_GRID, HF, WF, device=device, generator=g)
+    grid = _layout(torch.randn(NB, C_GRID, HF, WF, device=device, generator=g))
     torch.manual_seed(2)
     head = ResnetFC(d_in=D_IN, d_out=1 + D_DINO, n_blocks=0, d_hidden=D_HIDDEN)
     conf = {"predict_dino": True, "dino_dims": D_DINO, "learn_empty": False, "code_mode": "z",
@@ -817,6 +827,9 @@ def main():
     ap.add_argument("--mode", default="proj", choices=["proj", "grid"],
                     help="16-bit render kernel: projected grid (default) or per-sample grid")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--grid-layout", default="nhwc", choices=["nhwc", "nchw"],
+                    help="synthetic feature-grid layout: nhwc = channels-last, what the native "
+                         "encoder writes (default); nchw = the reference's contiguous layout")
     ap.add_argument("--config", default="c2", choices=["c2", "c4", "c5", "vit", "encode", "train"],
                     help="c2: BASELINE configs[1] (K=64, D=64, the metric's config); c4: "
                          "configs[3] render shape (K=128, 384-d feature field); c5: "
@@ -835,7 +848,8 @@ def main():
     args = ap.parse_args()
     if args.precision == "fp8" and args.config != "c5":
         ap.error("--precision fp8 is the C5 voxel MLP chain (--config c5)")
-    global K_SAMPLES, D_DINO
+    global K_SAMPLES, D_DINO, GRID_LAYOUT
+    GRID_LAYOUT = args.grid_layout
     if args.config == "c4":
         K_SAMPLES, D_DINO = 128, 384
 

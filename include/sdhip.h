@@ -81,6 +81,11 @@ typedef struct sd_patch_args {
 
 int sd_patch_rays(const sd_patch_args *args, void *stream);
 
+/* Channels-last f32 grid (n elements, n % 4 == 0) -> dtype (SD_BF16 / SD_F16), same layout:
+ * the NHWC gather operand of sd_render_fused / sd_field_query when the grid already is
+ * channels-last (sd_pack_grid transposes an NCHW one). */
+int sd_cast_grid(const float *grid_nhwc, int64_t n, int dtype, void *out, void *stream);
+
 /* Stratified inverse-depth (lindisp) or linear z sampling.
  * Replaces NeRFRenderer.sample_coarse (scenedino/renderer/nerf.py:121-141).
  * u == NULL: jitter drawn from a counter-based RNG keyed by (seed, offset);
@@ -186,6 +191,11 @@ int sd_render_fused(const sd_render_args *args, const sd_mlp *mlp, void *stream)
  * Uses mlp->w_in chunks 0..C/16-1 and mlp->b_in_h. */
 int sd_project_grid(const float *grid_nchw, int64_t B, int64_t Hf, int64_t Wf,
                     const sd_mlp *mlp, void *out, void *stream);
+
+/* Same from a channels-last grid (B, Hf, Wf, C) float32 -- the layout the native encoder's
+ * DPT writes (its NCHW-shaped grid_f_features is a permuted view of it). */
+int sd_project_grid_nhwc(const float *grid_nhwc, int64_t B, int64_t Hf, int64_t Wf,
+                         const sd_mlp *mlp, void *out, void *stream);
 
 /* Head of the projected render: code columns of W_in and the output layer, packed
  * for 16x16x32 MFMA (scenedino_amd/mlp_pack.py documents the fragment maps). */

@@ -154,6 +154,8 @@ SIGNATURES = {
     "sd_composite_bwd": [_vp, _vp, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp, _vp,
                          _vp, _vp, _vp, _vp, _vp],
     "sd_project_grid": [_vp, _i64, _i64, _i64, ctypes.POINTER(SdMlp), _vp, _vp],
+    "sd_project_grid_nhwc": [_vp, _i64, _i64, _i64, ctypes.POINTER(SdMlp), _vp, _vp],
+    "sd_cast_grid": [_vp, _i64, ctypes.c_int, _vp, _vp],
     "sd_render_proj": [ctypes.POINTER(SdRenderArgs), ctypes.POINTER(SdHead), _vp],
     "sd_render_proj_work_bytes": [_i64, _i32],
     "sd_composite": [_vp, _vp, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp,
@@ -272,11 +274,27 @@ def sample_z(rays, K, lindisp, u=None, seed=0, offset=0, out=None):
     return z
 
 
-def pack_grid(grid_nchw, dtype):
+def channels_last(g: torch.Tensor) -> bool:
+    """(B, C, H, W) tensor whose storage is NHWC (the native encoder's grid layout)."""
+    return g.dim() == 4 and not g.is_contiguous() and g.permute(0, 2, 3, 1).is_contiguous()
+
+
+def pack_grid(grid, dtype):
+    """(B, C, H, W) f32 grid -> NHWC (B, H, W, C) in dtype: sd_pack_grid transposes an NCHW
+    grid; a channels-last one is returned as its NHWC view (f32) or cast (sd_cast_grid)."""
     lib = load()
-    B, C, H, W = grid_nchw.shape
-    out = torch.empty(B, H, W, C, device=grid_nchw.device, dtype=TORCH_DTYPE[dtype])
-    _check(lib.sd_pack_grid(ptr(_req(grid_nchw, "grid")), B, C, H, W, dtype, ptr(out),
+    B, C, H, W = grid.shape
+    if channels_last(grid):
+        nhwc = _req(grid.permute(0, 2, 3, 1), "grid")
+        if dtype == SD_F32:
+            return nhwc
+        out = torch.empty(B, H, W, C, device=grid.device, dtype=TORCH_DTYPE[dtype])
+        _check(lib.sd_cast_grid(ptr(nhwc), nhwc.numel(), dtype, ptr(out), stream_of(out)),
+               "sd_cast_grid")
+        return out
+    grid = grid.contiguous()
+    out = torch.empty(B, H, W, C, device=grid.device, dtype=TORCH_DTYPE[dtype])
+    _check(lib.sd_pack_grid(ptr(_req(grid, "grid")), B, C, H, W, dtype, ptr(out),
                             stream_of(out)), "sd_pack_grid")
     return out
 
@@ -317,13 +335,18 @@ def render_fused(args: SdRenderArgs, mlp: SdMlp, ref_tensor):
            "sd_render_fused")
 
 
-def project_grid(grid_nchw, mlp: SdMlp, dtype):
+def project_grid(grid, mlp: SdMlp, dtype):
     """P = W_in[:, :C] . grid + b_in per pixel: (B, Hf, Wf, 128) in dtype (plain NHWC,
-    256 B per pixel)."""
+    256 B per pixel).  grid (B, C, Hf, Wf) f32, NCHW or channels-last."""
     lib = load()
-    B, C, H, W = grid_nchw.shape
-    out = torch.empty(B, H, W, 128, device=grid_nchw.device, dtype=TORCH_DTYPE[dtype])
-    _check(lib.sd_project_grid(ptr(_req(grid_nchw, "grid")), B, H, W, ctypes.byref(mlp),
+    B, C, H, W = grid.shape
+    out = torch.empty(B, H, W, 128, device=grid.device, dtype=TORCH_DTYPE[dtype])
+    if channels_last(grid):
+        _check(lib.sd_project_grid_nhwc(ptr(_req(grid.permute(0, 2, 3, 1), "grid")), B, H, W,
+                                        ctypes.byref(mlp), ptr(out), stream_of(out)),
+               "sd_project_grid_nhwc")
+        return out
+    _check(lib.sd_project_grid(ptr(_req(grid.contiguous(), "grid")), B, H, W, ctypes.byref(mlp),
                                ptr(out), stream_of(out)), "sd_project_grid")
     return out
 

@@ -35,14 +35,22 @@ def _timed(name, fn):
 
 
 class GridNHWC(torch.autograd.Function):
-    """NCHW f32 grid (B, C, Hf, Wf) -> NHWC f32 (sd_pack_grid); backward sd_unpack_grid."""
+    """(B, C, Hf, Wf) f32 grid -> NHWC f32 for the gather.  A channels-last grid (the
+    native encoder's output) is used in place and its gradient handed back channels-last:
+    no copy either way.  An NCHW grid is transposed by sd_pack_grid, its gradient back by
+    sd_unpack_grid."""
 
     @staticmethod
-    def forward(ctx, grid_nchw):
-        return _lib.pack_grid(grid_nchw.float().contiguous(), _lib.SD_F32)
+    def forward(ctx, grid):
+        ctx.cl = _lib.channels_last(grid)
+        if ctx.cl:
+            return grid.float().permute(0, 2, 3, 1)
+        return _lib.pack_grid(grid.float().contiguous(), _lib.SD_F32)
 
     @staticmethod
     def backward(ctx, g):
+        if ctx.cl:
+            return g.float().contiguous().permute(0, 3, 1, 2)
         return _lib.unpack_grid(g.float().contiguous())
 
 

@@ -51,9 +51,10 @@
 // horizontal bilinear taps of a sample (x0, x0 + 1) are 512 contiguous bytes.  One wave =
 // 32 pixel columns x 128 hidden = 4 tiles of 32x32x16, K = C in chunks of 16.
 // A = the sd_mlp layer-1 fragments of the grid columns (LDS); B = 8 channels of the
-// lane's pixel read from NCHW (32 consecutive floats per channel across a half).
+// lane's pixel read from NCHW (32 consecutive floats per channel across a half) or, NHWC
+// (the native encoder's channels-last grid), as two 16-B loads of the pixel's row.
 // ---------------------------------------------------------------------------
-template <int P>
+template <int P, bool NHWC>
 __global__ void __launch_bounds__(SD_PWG)
 k_project(const float *__restrict__ grid, int64_t B, int C, int64_t HW, int W, const sd_mlp m,
           uint32_t *__restrict__ out) {
@@ -76,7 +77,10 @@ k_project(const float *__restrict__ grid, int64_t B, int C, int64_t HW, int W, c
         const int64_t b = task / ntile;
         const int64_t pix = (task - b * ntile) * 32 + li;
         const bool valid = pix < HW;
-        const float *gp = grid + b * C * HW + (pix < HW ? pix : HW - 1) + (int64_t)(8 * h) * HW;
+        const int64_t pc = pix < HW ? pix : HW - 1;
+        // channel c of this lane's pixel: gp[c * cs]
+        const int64_t cs = NHWC ? 1 : HW;
+        const float *gp = NHWC ? grid + (b * HW + pc) * C + 8 * h : grid + b * C * HW + pc + (int64_t)(8 * h) * HW;
         f32x16 acc[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
@@ -92,19 +96,19 @@ k_project(const float *__restrict__ grid, int64_t B, int C, int64_t HW, int W, c
         // is HBM-bound and one step per wave does not cover the latency
         float x0[8], x1[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) x0[e] = gp[e * HW];
+        for (int e = 0; e < 8; ++e) x0[e] = gp[e * cs];
         if (nq > 1) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) x1[e] = gp[(int64_t)16 * HW + e * HW];
+            for (int e = 0; e < 8; ++e) x1[e] = gp[16 * cs + e * cs];
         }
         auto kstep = [&](int q, float (&x)[8]) {
             Frag f;
 #pragma unroll
             for (int e = 0; e < 8; ++e) f[e] = (typename Tr::E)x[e];
             if (q + 2 < nq) {
-                const float *gn = gp + (int64_t)(16 * (q + 2)) * HW;
+                const float *gn = gp + (int64_t)(16 * (q + 2)) * cs;
 #pragma unroll
-                for (int e = 0; e < 8; ++e) x[e] = gn[e * HW];
+                for (int e = 0; e < 8; ++e) x[e] = gn[e * cs];
             }
 #pragma unroll
             for (int t = 0; t < 4; ++t) acc[t] = Tr::mma32(lw[(q * 4 + t) * SD_WAVE + lane], f, acc[t]);
@@ -708,8 +712,8 @@ static int sd_check_err() {
     return 0;
 }
 
-extern "C" int sd_project_grid(const float *grid, int64_t B, int64_t Hf, int64_t Wf,
-                               const sd_mlp *m, void *out, void *stream) {
+static int sd_project_any(const float *grid, int64_t B, int64_t Hf, int64_t Wf, const sd_mlp *m,
+                          void *out, void *stream, bool nhwc) {
     if (!grid || !m || !out || !m->w_in || !m->b_in_h || B <= 0 || Hf <= 0 || Wf <= 0 ||
         m->d_hidden != SD_DH || m->C <= 0 || (m->C % 64) ||
         (m->dtype != SD_BF16 && m->dtype != SD_F16)) {
@@ -725,16 +729,33 @@ extern "C" int sd_project_grid(const float *grid, int64_t B, int64_t Hf, int64_t
     hipStream_t s = (hipStream_t)stream;
     int64_t nblk;
     const int64_t work = B * ((HW + 31) / 32);
+#define SD_PROJ_LAUNCH(PP, NH)                                                                  \
+    do {                                                                                        \
+        sd_launch_proj(k_project<PP, NH>, work, lds_bytes, s, nblk);                            \
+        hipLaunchKernelGGL((k_project<PP, NH>), dim3((unsigned)nblk), dim3(SD_PWG), lds_bytes, s, \
+                           grid, B, m->C, HW, (int)Wf, *m, (uint32_t *)out);                    \
+    } while (0)
     if (m->dtype == SD_F16) {
-        sd_launch_proj(k_project<SD_F16>, work, lds_bytes, s, nblk);
-        hipLaunchKernelGGL(k_project<SD_F16>, dim3((unsigned)nblk), dim3(SD_PWG), lds_bytes, s,
-                           grid, B, m->C, HW, (int)Wf, *m, (uint32_t *)out);
+        if (nhwc) SD_PROJ_LAUNCH(SD_F16, true); else SD_PROJ_LAUNCH(SD_F16, false);
     } else {
-        sd_launch_proj(k_project<SD_BF16>, work, lds_bytes, s, nblk);
-        hipLaunchKernelGGL(k_project<SD_BF16>, dim3((unsigned)nblk), dim3(SD_PWG), lds_bytes, s,
-                           grid, B, m->C, HW, (int)Wf, *m, (uint32_t *)out);
+        if (nhwc) SD_PROJ_LAUNCH(SD_BF16, true); else SD_PROJ_LAUNCH(SD_BF16, false);
     }
+#undef SD_PROJ_LAUNCH
     return sd_check_err();
+}
+
+extern "C" int sd_project_grid(const float *grid, int64_t B, int64_t Hf, int64_t Wf,
+                               const sd_mlp *m, void *out, void *stream) {
+    return sd_project_any(grid, B, Hf, Wf, m, out, stream, false);
+}
+
+extern "C" int sd_project_grid_nhwc(const float *grid, int64_t B, int64_t Hf, int64_t Wf,
+                                    const sd_mlp *m, void *out, void *stream) {
+    if (((uintptr_t)grid & 15)) {
+        sd_set_error("sd_project_grid_nhwc: grid must be 16-byte aligned");
+        return -1;
+    }
+    return sd_project_any(grid, B, Hf, Wf, m, out, stream, true);
 }
 
 template <int P, int NV, int NDT>

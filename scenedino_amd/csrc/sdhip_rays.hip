@@ -272,6 +272,41 @@ extern "C" int sd_patch_rays(const sd_patch_args *a, void *stream) {
     return 0;
 }
 
+// channels-last f32 grid -> the MLP dtype, same layout (4 elements per thread)
+template <int DT>
+__global__ void __launch_bounds__(256) k_cast_grid(const float4 *__restrict__ in, int64_t n4,
+                                                   void *__restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n4) return;
+    const float4 v = in[i];
+    if (DT == SD_BF16) {
+        typedef __attribute__((ext_vector_type(4))) __bf16 b4;
+        ((b4 *)out)[i] = b4{(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+    } else {
+        typedef __attribute__((ext_vector_type(4))) _Float16 h4;
+        ((h4 *)out)[i] = h4{(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
+    }
+}
+
+extern "C" int sd_cast_grid(const float *grid_nhwc, int64_t n, int dtype, void *out, void *stream) {
+    if (!grid_nhwc || !out || n < 0 || n % 4 || (dtype != SD_BF16 && dtype != SD_F16) ||
+        (((uintptr_t)grid_nhwc | (uintptr_t)out) & 15)) {
+        sd_set_error("sd_cast_grid: invalid argument (16-bit dtype, n % 4 == 0, aligned)");
+        return -1;
+    }
+    if (n == 0) return 0;
+    const int64_t n4 = n / 4;
+    dim3 g((unsigned)((n4 + 255) / 256));
+    if (dtype == SD_BF16)
+        hipLaunchKernelGGL(k_cast_grid<SD_BF16>, g, dim3(256), 0, (hipStream_t)stream,
+                           (const float4 *)grid_nhwc, n4, out);
+    else
+        hipLaunchKernelGGL(k_cast_grid<SD_F16>, g, dim3(256), 0, (hipStream_t)stream,
+                           (const float4 *)grid_nhwc, n4, out);
+    SD_CHECK_LAUNCH("sd_cast_grid");
+    return 0;
+}
+
 extern "C" int sd_sample_z(const float *rays, int64_t R, int64_t ray_dim, int64_t K, int lindisp,
                            const float *u, uint64_t seed, uint64_t offset, float *z_out,
                            void *stream) {

@@ -149,7 +149,7 @@ class DPTHead(nn.Module):
         return P
 
     def forward_nhwc(self, xs, last: bool = True):
-        """xs: 4 NHWC bf16 tensors (B, h, w, embed) -> [NCHW f32 (B, d_out, H, W)].
+        """xs: 4 NHWC bf16 tensors (B, h, w, embed) -> [f32 (B, d_out, H, W), channels-last].
         ``last=False`` stops before the final convolution and returns its NHWC bf16 input
         (``forward_last`` applies it: the graph-captured pass leaves that one launch out,
         so its output is a fresh tensor instead of a copy of a graph-owned buffer)."""
@@ -198,9 +198,13 @@ class DPTHead(nn.Module):
         return self.forward_last(out) if last else out
 
     def forward_last(self, x):
-        """output_head.head_modules[2] (3x3 conv) on NHWC bf16 -> [NCHW f32 grid]."""
+        """output_head.head_modules[2] (3x3 conv) on NHWC bf16 -> [(B, C, H, W) f32 grid].
+        The grid is written channels-last (the GEMM's natural, coalesced output rows) and
+        returned as its (B, C, H, W) permuted view: the reference's shape and values, and
+        the layout every grid consumer here reads without a transposition
+        (sd_project_grid_nhwc, sd_cast_grid, the training gather)."""
         w2, b2 = self._pack()["head2"]
-        return [_lib.conv3x3(x, w2, b2, epi=_lib.SD_EPI_NCHW)]
+        return [_lib.conv3x3(x, w2, b2, epi=_lib.SD_EPI_F32).permute(0, 3, 1, 2)]
 
     def forward(self, inputs):
         """dpt_head.py:226-236: list of 4 NCHW grids -> [NCHW f32 grid]."""

@@ -269,13 +269,13 @@ class BTSNet(nn.Module):
     def _grid_nhwc(self, gc):
         """Encoder grid packed NHWC in the MLP dtype (sd_render_fused / sd_field_query)."""
         if gc["grid"] is None:
-            gc["grid"] = _lib.pack_grid(gc["grid_nchw"].float().contiguous(), self._dtype())
+            gc["grid"] = _lib.pack_grid(gc["grid_nchw"].float(), self._dtype())
         return gc["grid"]
 
     def _grid_proj(self, gc, m):
         """Projected grid P = W_in[:, :C] G + b_in, (B, Hf, Wf, 128) (sd_render_proj)."""
         if gc["proj"] is None or gc["proj_key"] != self._packed_key:
-            g = gc["grid_nchw"].float().contiguous()
+            g = gc["grid_nchw"].float()  # NCHW or the native encoder's channels-last grid
             gc["proj"] = self._timed("project", lambda: _lib.project_grid(g, m.rec, m.dtype))
             gc["proj_key"] = self._packed_key
         return gc["proj"]

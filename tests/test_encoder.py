@@ -113,6 +113,9 @@ def test_encoder_module_vs_oracles(gpu, conf):
         out = m(x.to(gpu))
         gt = m(x.to(gpu), ground_truth=True)
     assert len(out) == 1 and out[0].shape == (2, 256, H, W)
+    from scenedino_amd import _lib
+    if conf.get("decoder_arch") == "dpt":  # the DPT writes the grid channels-last
+        assert _lib.channels_last(out[0])
     xr = x
     if m.encoder.resize is not None:
         xr = torch.nn.functional.interpolate(x, size=m.encoder.resize, mode="bilinear",

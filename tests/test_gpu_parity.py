@@ -165,9 +165,15 @@ def test_field_query_vs_reference(precision, fx):
 
 
 # --------------------------------------------------------------------------- full render
-def _render(d, precision, want_rgb_samps=True, mode="proj"):
+def _render(d, precision, want_rgb_samps=True, mode="proj", channels_last=False):
     from scenedino_amd.renderer import NeRFRenderer
     net = net_from_fixture(d, precision, mode=mode)
+    if channels_last:  # the native encoder's grid layout: (B, C, H, W) view of NHWC storage
+        g = net.grid_f_features[0]
+        B, nv, C, H, W = g.shape
+        net.grid_f_features[0] = (g.reshape(B * nv, C, H, W)
+                                  .contiguous(memory_format=torch.channels_last)
+                                  .view(B, nv, C, H, W))
     K = int(d["K"])
     r = NeRFRenderer(n_coarse=K, lindisp=True, hard_alpha_cap=bool(d["hard_cap"]),
                      eval_batch_size=65536)
@@ -213,6 +219,20 @@ def test_render_lowp_vs_reference(fx, precision, mode):
     assert torch.equal(c["invalid_features"].cpu(), torch.from_numpy(d["invalid_features"]))
     check_lowp(c, d, precision)
     close(c["rgb_samps"], d["rgb_samps"], 1e-5, FP32_ATOL["rgb_samps"], "rgb_samps")
+
+
+@pytest.mark.parametrize("precision,mode", [("bf16", "proj"), ("fp16", "proj"), ("bf16", "grid"),
+                                            ("fp32", "grid")])
+def test_channels_last_grid_bit_equal(precision, mode):
+    """A channels-last grid (what the native DPT writes) renders bit-equal to the same grid
+    in NCHW: sd_project_grid_nhwc / sd_cast_grid read it in place of the transposing
+    sd_project_grid / sd_pack_grid, with the same arithmetic."""
+    from scenedino_amd import _lib
+    d = load("render_sb2_nv2_k16.npz")
+    a = _render(d, precision, mode=mode)["coarse"]
+    b = _render(d, precision, mode=mode, channels_last=True)["coarse"]
+    for k in ("weights", "alphas", "depth", "rgb", "dino_features", "invalid", "invalid_features"):
+        assert torch.equal(a[k], b[k]), k
 
 
 @pytest.mark.parametrize("precision", ["bf16", "fp16"])

@@ -173,8 +173,9 @@ def test_grid_layout_and_field_mlp_gpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("hard,empty", [(False, False), (True, False), (False, True)])
-def test_train_mode_render_gradients_gpu(hard, empty):
+@pytest.mark.parametrize("hard,empty,cl", [(False, False, False), (True, False, False),
+                                           (False, True, False), (False, False, True)])
+def test_train_mode_render_gradients_gpu(hard, empty, cl):
     """train(): NeRFRenderer -> BTSNet.forward (sd_field_gather, ResnetFC, softplus) ->
     sd_composite; loss.backward() reaches the feature grid and every head parameter
     with the reference's gradients (oracle.render under CPU autograd).  ``empty``:
@@ -197,7 +198,12 @@ def test_train_mode_render_gradients_gpu(hard, empty):
     e = torch.randn(C, generator=g) if empty else None
     net = build_net(grid, W_in, b_in, W_out, b_out, "fp32", dev, empty_feature=e)
     net.encode(images.to(dev), Kn.to(dev), pose.to(dev), ids_encoder=[0], ids_render=[0])
-    leaf = net.grid_f_features[0].detach().clone().requires_grad_(True)
+    leaf = net.grid_f_features[0].detach().clone()
+    if cl:  # channels-last grid (the native encoder's layout): gathered and scattered in place
+        B_, nv_, C_, H_, W_ = leaf.shape
+        leaf = (leaf.reshape(B_ * nv_, C_, H_, W_).contiguous(memory_format=torch.channels_last)
+                .view(B_, nv_, C_, H_, W_))
+    leaf.requires_grad_(True)
     net.grid_f_features[0] = leaf
     net.train()
     rpose = pose
@@ -236,6 +242,9 @@ def test_train_mode_render_gradients_gpu(hard, empty):
     rl.backward()
     assert leaf.grad is not None
     assert rel_l2(leaf.grad.reshape(lg.shape), lg.grad) < 1e-3
+    if cl:  # the gradient came back in the grid's own layout (no transposition pass)
+        from scenedino_amd import _lib
+        assert _lib.channels_last(leaf.grad.reshape(lg.shape))
     for p, q, name in zip((head.lin_in.weight, head.lin_in.bias, head.lin_out.weight,
                            head.lin_out.bias), ps, ("W_in", "b_in", "W_out", "b_out")):
         assert rel_l2(p.grad, q.grad) < 1e-3, name
