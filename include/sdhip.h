@@ -421,6 +421,38 @@ int sd_tokens_to_nhwc(const float *x, int32_t B, int32_t T, int32_t C, int32_t n
 int sd_upsample2x(const void *in, int32_t B, int32_t H, int32_t W, int32_t C, void *out,
                   void *stream);
 
+/* ---- training path: fused ResnetFC MLP (sdhip_mlp.hip) ---------------------- */
+
+/* ResnetFC(n_blocks=0) forward / backward of the training path under autocast
+ * (scenedino/models/prediction_heads/resnetfc.py:135-203, bts.py:516-541 softplus,
+ * scenedino/training/base_trainer.py:223,251 with_amp), on the sd_field_gather rows
+ * x (N, ldx) = [feat (C) | code | 1] in dtype (SD_F16 / SD_BF16).  Fragments pre-packed by
+ * the host (scenedino_amd/mlp_pack.py PackedTrainMLP documents the maps).
+ * sd_mlp_train_fwd: h (N, 136) dtype = [relu(W_in x + b_in) | 1 | 0..], sigma (N) f32 =
+ *   softplus(out_0), dino (N, D) f32 = out_1..D.
+ * sd_mlp_train_bwd: from d_sigma (N), d_dino (N, D) f32: dy (N, 72) dtype = [d dino | d out_0
+ *   | 0..], dh (N, 128) dtype = d relu-input, dx (N, ldx) f32 = [dH W_in[:, :C] | 0..];
+ *   the weight gradients are dh^T x and dy^T h (caller's GEMMs).  D <= 64, C % 32 == 0. */
+typedef struct sd_mlp_train_args {
+    const void *x;
+    int64_t N;
+    int32_t ldx, kx;       /* row length of x / dx, used columns (d_in + 1)              */
+    int32_t dtype, D, C, pad;
+    const void *w1f;       /* [4][ceil(kx/16)][64][8]  [W_in | b_in] A fragments          */
+    const void *w2f;       /* [ceil((D+1)/32)][8][64][8] W_out B fragments (dino, out_0)   */
+    const float *b_out;    /* (1 + D)                                                     */
+    void *h;
+    float *sigma, *dino;
+    const float *d_sigma, *d_dino;
+    const void *wtf;       /* [4][ceil((D+1)/16)][64][8] W_out^T A fragments              */
+    const void *wxf;       /* [C/32][8][64][8] W_in B fragments (dX)                       */
+    void *dy, *dh;
+    float *dx;
+} sd_mlp_train_args;
+
+int sd_mlp_train_fwd(const sd_mlp_train_args *args, void *stream);
+int sd_mlp_train_bwd(const sd_mlp_train_args *args, void *stream);
+
 /* ---- training loss: PatchSalienceDownsampler (sdhip_down.hip) -------------- */
 
 /* PatchSalienceDownsampler.forward_patches (scenedino/models/backbones/dino/downsampler.py:

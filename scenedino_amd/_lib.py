@@ -109,6 +109,16 @@ class SdPatchArgs(ctypes.Structure):
     ]
 
 
+class SdMlpTrainArgs(ctypes.Structure):
+    """sd_mlp_train_args (include/sdhip.h): fused training MLP."""
+    _fields_ = [
+        ("x", _vp), ("N", _i64), ("ldx", _i32), ("kx", _i32), ("dtype", _i32), ("D", _i32),
+        ("C", _i32), ("pad", _i32), ("w1f", _vp), ("w2f", _vp), ("b_out", _vp), ("h", _vp),
+        ("sigma", _vp), ("dino", _vp), ("d_sigma", _vp), ("d_dino", _vp), ("wtf", _vp),
+        ("wxf", _vp), ("dy", _vp), ("dh", _vp), ("dx", _vp),
+    ]
+
+
 class SdSalienceArgs(ctypes.Structure):
     """sd_salience_args (include/sdhip.h): PatchSalienceDownsampler forward / backward."""
     _fields_ = [
@@ -169,6 +179,8 @@ SIGNATURES = {
                      _vp, _vp],
     "sd_ssc_confusion": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, ctypes.POINTER(SdSscArgs), _vp,
                          _vp],
+    "sd_mlp_train_fwd": [ctypes.POINTER(SdMlpTrainArgs), _vp],
+    "sd_mlp_train_bwd": [ctypes.POINTER(SdMlpTrainArgs), _vp],
     "sd_salience_fwd": [ctypes.POINTER(SdSalienceArgs), _vp],
     "sd_salience_bwd": [ctypes.POINTER(SdSalienceArgs), _vp],
     "sd_gemm": [ctypes.POINTER(SdGemmArgs), _vp],
@@ -242,6 +254,16 @@ def gen_rays(poses_c2w, Ks, frame_ids, H, W, z_near, z_far):
                            ptr(_req(frame_ids, "frame_ids")), v, H, W, float(z_near),
                            float(z_far), ptr(out), stream_of(out)), "sd_gen_rays")
     return out
+
+
+def mlp_train_fwd(args: SdMlpTrainArgs, ref_tensor):
+    lib = load()
+    _check(lib.sd_mlp_train_fwd(ctypes.byref(args), stream_of(ref_tensor)), "sd_mlp_train_fwd")
+
+
+def mlp_train_bwd(args: SdMlpTrainArgs, ref_tensor):
+    lib = load()
+    _check(lib.sd_mlp_train_bwd(ctypes.byref(args), stream_of(ref_tensor)), "sd_mlp_train_bwd")
 
 
 def salience_fwd(args: SdSalienceArgs, ref_tensor):

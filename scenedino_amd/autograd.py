@@ -172,6 +172,133 @@ class FieldMLP(torch.autograd.Function):
                 dWo[:, :dh_].contiguous(), dWo[:, dh_].contiguous())
 
 
+_train_pack = {}
+
+
+def _packed_train(w_in, b_in, w_out, b_out, dtype, C):
+    from .mlp_pack import PackedTrainMLP, param_key
+    key = param_key(w_in, b_in, w_out, b_out) + (dtype, C)
+    p = _train_pack.get("p")
+    if p is None or _train_pack.get("key") != key:
+        p = PackedTrainMLP(w_in, b_in, w_out, b_out, dtype, C)
+        _train_pack["p"], _train_pack["key"] = p, key
+    return p
+
+
+class FieldMLPFused(torch.autograd.Function):
+    """The training MLP under autocast as two fused kernels (csrc/sdhip_mlp.hip):
+    forward sd_mlp_train_fwd (layer 1 + ReLU + layer 2 + softplus: returns sigma (N) and
+    dino (N, D) f32), backward sd_mlp_train_bwd (dX for the gather's scatter, dH and dY
+    rows) + the two weight-gradient GEMMs dW1 = dH^T X, dW_o = dY^T [H | 1] (biases from
+    the ones columns).  x_aug (N, d_in + 1) f16 / bf16 rows of sd_field_gather."""
+
+    @staticmethod
+    def forward(ctx, x_aug, w_in, b_in, w_out, b_out):
+        N, ldx = x_aug.shape
+        dh, d_in = w_in.shape
+        D = w_out.shape[0] - 1
+        dt = _lib.SD_OF_TORCH[x_aug.dtype]
+        C = d_in - 39
+        p = _packed_train(w_in, b_in, w_out, b_out, dt, C)
+        x_aug = x_aug.contiguous()
+        dev = x_aug.device
+        h = torch.empty(N, 136, device=dev, dtype=x_aug.dtype)
+        sigma = torch.empty(N, device=dev)
+        dino = torch.empty(N, D, device=dev)
+        a = _lib.SdMlpTrainArgs(x=x_aug.data_ptr(), N=N, ldx=ldx, kx=d_in + 1, dtype=dt, D=D, C=C,
+                                w1f=p.w1f.data_ptr(), w2f=p.w2f.data_ptr(),
+                                b_out=p.b_out.data_ptr(), h=h.data_ptr(), sigma=sigma.data_ptr(),
+                                dino=dino.data_ptr())
+        _timed("mlp", lambda: _lib.mlp_train_fwd(a, x_aug))
+        ctx.save_for_backward(x_aug, h, sigma)
+        ctx.p, ctx.meta = p, (N, ldx, d_in, D, C, dt, w_in.dtype)
+        return sigma, dino
+
+    @staticmethod
+    def backward(ctx, g_sigma, g_dino):
+        dx, *rest = FieldMLPFused.grads(ctx, g_sigma, g_dino)
+        return (dx if ctx.needs_input_grad[0] else None, *rest)
+
+    @staticmethod
+    def grads(ctx, g_sigma, g_dino):
+        """(dX (N, ldx) f32, dW_in, db_in, dW_out, db_out) of the saved forward."""
+        x_aug, h, sigma = ctx.saved_tensors
+        p = ctx.p
+        N, ldx, d_in, D, C, dt, pdt = ctx.meta
+        dev = x_aug.device
+        g_sigma = (g_sigma if g_sigma is not None else torch.zeros(N, device=dev)).float().contiguous()
+        g_dino = (g_dino if g_dino is not None else torch.zeros(N, D, device=dev)).float().contiguous()
+        dy = torch.empty(N, 72, device=dev, dtype=x_aug.dtype)
+        dh = torch.empty(N, 128, device=dev, dtype=x_aug.dtype)
+        dx = torch.empty(N, ldx, device=dev)
+        a = _lib.SdMlpTrainArgs(x=x_aug.data_ptr(), N=N, ldx=ldx, kx=d_in + 1, dtype=dt, D=D, C=C,
+                                h=h.data_ptr(), sigma=sigma.data_ptr(), d_sigma=g_sigma.data_ptr(),
+                                d_dino=g_dino.data_ptr(), wtf=p.wtf.data_ptr(),
+                                wxf=p.wxf.data_ptr(), dy=dy.data_ptr(), dh=dh.data_ptr(),
+                                dx=dx.data_ptr())
+        _timed("mlp_bwd", lambda: _lib.mlp_train_bwd(a, x_aug))
+        dW1 = _wgrad(dh, x_aug)             # (128, d_in + 1): [dW_in | db_in]
+        dWo = _wgrad(dy, h)                 # (72, 136): rows dino 0..D-1, out_0; col 128 bias
+        dw_out = torch.cat((dWo[D:D + 1, :128], dWo[:D, :128]), 0)
+        db_out = torch.cat((dWo[D:D + 1, 128], dWo[:D, 128]), 0)
+        return (dx, dW1[:, :d_in].to(pdt).contiguous(), dW1[:, d_in].to(pdt).contiguous(),
+                dw_out.to(pdt).contiguous(), db_out.to(pdt).contiguous())
+
+
+class FieldGatherMLP(torch.autograd.Function):
+    """FieldGather -> FieldMLPFused as ONE autograd node (training under autocast): the
+    backward hands the MLP's f32 dX rows straight to the gather's scatter -- autograd would
+    otherwise cast the gradient of the 16-bit rows to their dtype and back (two passes
+    over N x (C + 40)).  learn_empty (bts.py:311-319): out-of-frustum rows take the empty
+    feature; its gradient is the sum of their dX rows, which the scatter then skips."""
+
+    @staticmethod
+    def forward(ctx, grid_nhwc, xyz, cam_f, img, cam_c, colors, acc, empty, w_in, b_in, w_out,
+                b_out):
+        dt = torch.get_autocast_dtype("cuda")
+        x, invf, rgb, inv = _timed("gather", lambda: _lib.field_gather(
+            xyz, grid_nhwc, cam_f, img, cam_c, colors, dtype=dt))
+        B, P, ldx = x.shape
+        N = B * P
+        x = x.view(N, ldx)
+        C = grid_nhwc.shape[-1]
+        if empty is not None:
+            m = invf.reshape(N, 1)
+            x[:, :C] = torch.where(m, empty.to(dt).view(1, C), x[:, :C])
+        sigma, dino = FieldMLPFused.forward(ctx, x, w_in, b_in, w_out, b_out)
+        ctx.xyz, ctx.cam_f, ctx.grid_shape = xyz, cam_f, tuple(grid_nhwc.shape)
+        ctx.acc = acc if acc is not None else GatherAcc()
+        ctx.acc.n += 1
+        ctx.invf = invf if empty is not None else None
+        ctx.empty_dtype = empty.dtype if empty is not None else None
+        outs = [t for t in (invf, rgb, inv) if t is not None]
+        ctx.mark_non_differentiable(*outs)
+        return sigma.view(B, P), dino.view(B, P, -1), invf, rgb, inv
+
+    @staticmethod
+    def backward(ctx, g_sigma, g_dino, *_):
+        N = ctx.meta[0]
+        gs = g_sigma.reshape(N) if g_sigma is not None else None
+        gd = g_dino.reshape(N, -1) if g_dino is not None else None
+        dx, dw_in, db_in, dw_out, db_out = FieldMLPFused.grads(ctx, gs, gd)
+        B, Hf, Wf, C = ctx.grid_shape
+        d_empty = None
+        if ctx.invf is not None:
+            m = ctx.invf.reshape(N, 1)
+            d_empty = torch.where(m, dx[:, :C], torch.zeros((), device=dx.device)).sum(0)
+            dx[:, :C] = torch.where(m, torch.zeros((), device=dx.device), dx[:, :C])
+            d_empty = d_empty.to(ctx.empty_dtype)
+        d_grid = None
+        if ctx.needs_input_grad[0]:
+            buf, first = ctx.acc.take((B, Hf, Wf, C), dx.device)
+            xyz, cam_f = ctx.xyz, ctx.cam_f
+            _timed("gather_bwd", lambda: _lib.field_gather_bwd(xyz, dx, cam_f, Hf, Wf, C,
+                                                               dgrid=buf))
+            d_grid = buf if first else None
+        return (d_grid, None, None, None, None, None, None, d_empty, dw_in, db_in, dw_out,
+                db_out)
+
+
 class Composite(torch.autograd.Function):
     """Alpha compositing (nerf.py:376-405) with the sd_composite_bwd backward.
     z, sigma (R, K); feat (R, K, F) | None; rgb (R, K, Cc) | None.  Returns

@@ -201,3 +201,78 @@ class PackedMLP:
 
 def param_key(*ts):
     return tuple((t.data_ptr(), t._version, tuple(t.shape), str(t.device)) for t in ts)
+
+
+# ---------------------------------------------------------------------------
+# training-path MLP (csrc/sdhip_mlp.hip): 32x32x16 MFMA fragments, lane l = 32 h + r holds
+# 8 consecutive k elements 8 h .. 8 h + 7 of its row (A) / column (B) r.  Operands fed from
+# an accumulator tile use the permuted k order kappa(s, h, j) = 16 s + 8 (j >> 2) + 4 h + (j & 3).
+# ---------------------------------------------------------------------------
+_TRAIN_IDX = {}
+
+
+def _train_index(d_in: int, D: int, C: int, dev):
+    """Flat gather index of all four training fragment arrays into the source vector
+    src = [W1 (128 x kx, row-major) | Wo (D+1 x 128: dino rows, then out_0) | 0]:
+    w1f [4][KS][64][8], w2f [U][8][64][8], wtf [4][KO][64][8], wxf [C/32][8][64][8].
+    Built once per shape (the optimizer changes the weights every step, not the maps)."""
+    key = (d_in, D, C, str(dev))
+    if key in _TRAIN_IDX:
+        return _TRAIN_IDX[key]
+    kx = d_in + 1
+    KS, U, KO = (kx + 15) // 16, (D + 1 + 31) // 32, (D + 1 + 15) // 16
+    n_w1 = D_HIDDEN * kx
+    zero = n_w1 + (D + 1) * D_HIDDEN
+    l = torch.arange(64).view(1, 64, 1)
+    r, h = l & 31, l >> 5
+    j = torch.arange(8).view(1, 1, 8)
+
+    def lin(n):  # k = 16 s + 8 h + j
+        return 16 * torch.arange(n).view(-1, 1, 1) + 8 * h + j
+
+    def kap(n):  # permuted k of an accumulator-fed operand
+        return 16 * torch.arange(n).view(-1, 1, 1) + 8 * (j >> 2) + 4 * h + (j & 3)
+
+    parts = []
+    for t in range(4):  # W1 rows (hidden), k = x column
+        row, k = 32 * t + r, lin(KS)
+        parts.append(torch.where(k < kx, row * kx + k, zero))
+    for u in range(U):  # Wo rows (outputs), k = hidden (permuted)
+        row, k = 32 * u + r, kap(8)
+        parts.append(torch.where(row < D + 1, n_w1 + row * D_HIDDEN + k, zero).expand(8, 64, 8))
+    for t in range(4):  # Wo^T rows (hidden), k = output
+        hid, k = 32 * t + r, lin(KO)
+        parts.append(torch.where(k < D + 1, n_w1 + k * D_HIDDEN + hid, zero))
+    for u in range(C // 32):  # W_in^T rows (input column c), k = hidden (permuted)
+        c, k = 32 * u + r, kap(8)
+        parts.append((k * kx + c).expand(8, 64, 8))
+    idx = torch.cat([p.reshape(-1) for p in parts]).to(dev)
+    sizes = (4 * KS * 512, U * 8 * 512, 4 * KO * 512, (C // 32) * 8 * 512)
+    _TRAIN_IDX[key] = (idx, sizes, (KS, U, KO))
+    return _TRAIN_IDX[key]
+
+
+class PackedTrainMLP:
+    """Fragments of the fused training MLP (sd_mlp_train_fwd / _bwd) for ResnetFC weights
+    W_in (128, d_in), b_in, W_out (1 + D, 128), b_out; dtype SD_F16 / SD_BF16.  One gather
+    of the flattened weights through a cached index (_train_index) per weight version."""
+
+    def __init__(self, W_in, b_in, W_out, b_out, dtype: int, C: int):
+        dev = W_in.device
+        dh, d_in = W_in.shape
+        D = W_out.shape[0] - 1
+        if dh != D_HIDDEN or D > 64 or C % 32:
+            raise NotImplementedError("fused training MLP: d_hidden 128, D <= 64, C % 32 == 0")
+        idx, sizes, (KS, U, KO) = _train_index(d_in, D, C, dev)
+        with torch.no_grad():
+            src = torch.cat((torch.cat((W_in, b_in[:, None]), 1).reshape(-1),
+                             W_out[1:].reshape(-1), W_out[:1].reshape(-1),
+                             torch.zeros(1, device=dev, dtype=W_in.dtype)))
+            frags = src.float()[idx].to(_lib.TORCH_DTYPE[dtype])
+        a, b, c, d = torch.split(frags, sizes)
+        self.w1f = a.view(4, KS, 64, 8)
+        self.w2f = b.view(U, 8, 64, 8)
+        self.wtf = c.view(4, KO, 64, 8)
+        self.wxf = d.view(C // 32, 8, 64, 8)
+        self.b_out = b_out.detach().float().contiguous()
+        self.D, self.C, self.kx, self.dtype = D, C, d_in + 1, dtype

@@ -421,12 +421,24 @@ class BTSNet(nn.Module):
         self._timed("field", lambda: _lib.field_query(args, m.rec, xyz))
         return sigma, dino, rgb, inv, invf
 
+    @staticmethod
+    def _fused_train_mlp(head, C) -> bool:
+        """Training under a 16-bit autocast with the shipped head (ResnetFC n_blocks = 0,
+        ReLU, d_hidden 128, D <= 64): gather + MLP as the fused sd_mlp_train kernels."""
+        return (torch.is_autocast_enabled("cuda")
+                and torch.get_autocast_dtype("cuda") in (torch.float16, torch.bfloat16)
+                and type(head).__name__ == "ResnetFC" and getattr(head, "n_blocks", 1) == 0
+                and getattr(head, "d_latent", 1) == 0 and isinstance(head.activation, nn.ReLU)
+                and getattr(head, "view_number", None) in (None, 0)
+                and head.lin_in.weight.shape[0] == 128 and head.lin_out.weight.shape[0] <= 65
+                and C % 32 == 0)
+
     def _query_diff(self, xyz):
         """query() with autograd (training path, scenedino_amd/autograd.py): the grid is
         gathered by sd_field_gather (backward sd_field_gather_bwd) and the prediction head
         runs as its own nn.Linear layers, so gradients reach grid_f_features and the head
         parameters as in bts.py:476-595."""
-        from ..autograd import FieldGather, FieldMLP, GatherAcc, GridNHWC
+        from ..autograd import FieldGather, FieldGatherMLP, FieldMLP, GatherAcc, GridNHWC
         self._check_supported()
         head = self.heads[self.final_pred_head]
         if len(self.heads) != 1:
@@ -447,6 +459,12 @@ class BTSNet(nn.Module):
             nh = (key, GridNHWC.apply(g0), GatherAcc())
             if self._in_pass:
                 self._pass_nhwc = nh
+        if self._fused_train_mlp(head, gc["C"]):
+            sigma, dino, invf, rgb, inv = FieldGatherMLP.apply(
+                nh[1], xyz.float().contiguous(), gc["cam_f"], gc["img"], gc["cam_c"], True, nh[2],
+                self.empty_feature if self.learn_empty else None, head.lin_in.weight,
+                head.lin_in.bias, head.lin_out.weight, head.lin_out.bias)
+            return sigma, dino, rgb, inv, invf
         x, invf, rgb, inv = FieldGather.apply(nh[1], xyz.float().contiguous(), gc["cam_f"],
                                               gc["img"], gc["cam_c"], True, nh[2])
         x = x.reshape(n * P, -1)

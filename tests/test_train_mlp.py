@@ -1,0 +1,82 @@
+"""Fused training MLP (csrc/sdhip_mlp.hip; resnetfc.py:135-203 under autocast, SURVEY
+§8(f) rank 1): fragment maps on CPU (unpacked back to the weights), then the kernels vs the
+reference op sequence (nn.Linear pair under torch.autocast, softplus) on the GPU.
+Tolerances: outputs rel-L2 <= 1e-2, gradients rel-L2 <= 2e-2 (16-bit operands, as the
+autocast reference)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from _helpers import rel_l2
+from scenedino_amd import _lib
+from scenedino_amd.mlp_pack import PackedTrainMLP
+
+
+def _weights(seed, d_in=295, D=64):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(128, d_in, generator=g) * 0.08, torch.randn(128, generator=g) * 0.1,
+            torch.randn(1 + D, 128, generator=g) * 0.1, torch.randn(1 + D, generator=g) * 0.1)
+
+
+def _kap(s, h, j):
+    return 16 * s + 8 * (j >> 2) + 4 * h + (j & 3)
+
+
+def test_fragment_maps_unpack_to_the_weights():
+    W_in, b_in, W_out, b_out = _weights(1)
+    p = PackedTrainMLP(W_in, b_in, W_out, b_out, _lib.SD_F16, 256)
+    W1 = torch.cat((W_in, b_in[:, None]), 1)
+    Wo = torch.cat((W_out[1:], W_out[:1]), 0)  # dino rows, then out_0
+    got1 = torch.zeros(128, 19 * 16)
+    got2 = torch.zeros(96, 128)
+    gott = torch.zeros(128, 80)
+    gotx = torch.zeros(256, 128)
+    for l in range(64):
+        r, h = l & 31, l >> 5
+        for j in range(8):
+            for t in range(4):
+                for s in range(19):
+                    got1[32 * t + r, 16 * s + 8 * h + j] = p.w1f[t, s, l, j].float()
+                for s in range(5):
+                    gott[32 * t + r, 16 * s + 8 * h + j] = p.wtf[t, s, l, j].float()
+            for s in range(8):
+                for u in range(3):
+                    got2[32 * u + r, _kap(s, h, j)] = p.w2f[u, s, l, j].float()
+                for u in range(8):
+                    gotx[32 * u + r, _kap(s, h, j)] = p.wxf[u, s, l, j].float()
+    f16 = lambda t: t.half().float()
+    assert torch.equal(got1[:, :296], f16(W1)) and not got1[:, 296:].any()
+    assert torch.equal(got2[:65], f16(Wo)) and not got2[65:].any()
+    assert torch.equal(gott[:, :65], f16(Wo.t())) and not gott[:, 65:].any()
+    assert torch.equal(gotx, f16(W_in[:, :256].t()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [262144, 1000, 37])
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+def test_fused_mlp_vs_autocast_linear(N, dt):
+    from scenedino_amd.autograd import FieldMLPFused
+    dev = "cuda"
+    W_in, b_in, W_out, b_out = (t.to(dev) for t in _weights(2))
+    g = torch.Generator(device=dev).manual_seed(3)
+    x = torch.randn(N, 296, device=dev, generator=g)
+    x[:, 295] = 1.0
+    x = x.to(dt)
+    ps = [t.clone().requires_grad_(True) for t in (W_in, b_in, W_out, b_out)]
+    xr = x.clone().requires_grad_(True)
+    sig, dino = FieldMLPFused.apply(xr, *ps)
+    gs = torch.randn(N, device=dev, generator=g)
+    gd = torch.randn(N, 64, device=dev, generator=g)
+    ((sig * gs).sum() + (dino * gd).sum()).backward()
+    # reference: the nn.Linear pair under autocast (bts.py:502-541)
+    qs = [t.clone().requires_grad_(True) for t in (W_in, b_in, W_out, b_out)]
+    xq = x.clone().requires_grad_(True)
+    with torch.autocast("cuda", dtype=dt):
+        out = F.linear(torch.relu(F.linear(xq[:, :295], qs[0], qs[1])), qs[2], qs[3])
+    sr, dr = F.softplus(out[:, 0].float()), out[:, 1:].float()
+    ((sr * gs).sum() + (dr * gd).sum()).backward()
+    assert rel_l2(sig, sr) <= 1e-2 and rel_l2(dino, dr) <= 1e-2
+    assert rel_l2(xr.grad[:, :256].float(), xq.grad[:, :256].float()) <= 2e-2
+    assert not xr.grad[:, 256:].any()
+    for a, b, name in zip(ps, qs, ("W_in", "b_in", "W_out", "b_out")):
+        assert rel_l2(a.grad, b.grad) <= 2e-2, name
