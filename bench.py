@@ -601,11 +601,11 @@ def main_train(args, world, rank, device):
     # texel quad; depends on the geometry) -- counted as the dX reads only, the floor
     bwd_bytes = chunk * 4 * C_GRID
     traffic, tsrc = None, None
-    tf = os.path.join(ROOT, "profiles", "r1_train_pmc.json")
+    tf = os.path.join(ROOT, "profiles", "r2_train_traffic.json")
     if os.path.exists(tf):
         try:
             traffic = json.load(open(tf))["kernels"]["k_field_gather_bwd"]["hbm_bytes"]
-            tsrc = "profiles/r1_train_pmc.json (rocprofv3 PMC, per launch)"
+            tsrc = "profiles/r2_train_traffic.json (rocprofv3 PMC, per launch)"
         except (KeyError, TypeError, ValueError):
             traffic = None
     line = {

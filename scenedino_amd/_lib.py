@@ -113,7 +113,7 @@ class SdMlpTrainArgs(ctypes.Structure):
     """sd_mlp_train_args (include/sdhip.h): fused training MLP."""
     _fields_ = [
         ("x", _vp), ("N", _i64), ("ldx", _i32), ("kx", _i32), ("dtype", _i32), ("D", _i32),
-        ("C", _i32), ("pad", _i32), ("w1f", _vp), ("w2f", _vp), ("b_out", _vp), ("h", _vp),
+        ("C", _i32), ("lddx", _i32), ("w1f", _vp), ("w2f", _vp), ("b_out", _vp), ("h", _vp),
         ("sigma", _vp), ("dino", _vp), ("d_sigma", _vp), ("d_dino", _vp), ("wtf", _vp),
         ("wxf", _vp), ("dy", _vp), ("dh", _vp), ("dx", _vp),
     ]

@@ -216,12 +216,13 @@ class FieldMLPFused(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g_sigma, g_dino):
-        dx, *rest = FieldMLPFused.grads(ctx, g_sigma, g_dino)
+        dx, *rest = FieldMLPFused.grads(ctx, g_sigma, g_dino, full_rows=True)
         return (dx if ctx.needs_input_grad[0] else None, *rest)
 
     @staticmethod
-    def grads(ctx, g_sigma, g_dino):
-        """(dX (N, ldx) f32, dW_in, db_in, dW_out, db_out) of the saved forward."""
+    def grads(ctx, g_sigma, g_dino, full_rows=False):
+        """(dX f32, dW_in, db_in, dW_out, db_out) of the saved forward; dX rows are the C
+        feature columns, or (full_rows) as wide as x with zero code / ones columns."""
         x_aug, h, sigma = ctx.saved_tensors
         p = ctx.p
         N, ldx, d_in, D, C, dt, pdt = ctx.meta
@@ -230,9 +231,9 @@ class FieldMLPFused(torch.autograd.Function):
         g_dino = (g_dino if g_dino is not None else torch.zeros(N, D, device=dev)).float().contiguous()
         dy = torch.empty(N, 72, device=dev, dtype=x_aug.dtype)
         dh = torch.empty(N, 128, device=dev, dtype=x_aug.dtype)
-        dx = torch.empty(N, ldx, device=dev)
+        dx = torch.empty(N, ldx if full_rows else C, device=dev)
         a = _lib.SdMlpTrainArgs(x=x_aug.data_ptr(), N=N, ldx=ldx, kx=d_in + 1, dtype=dt, D=D, C=C,
-                                h=h.data_ptr(), sigma=sigma.data_ptr(), d_sigma=g_sigma.data_ptr(),
+                                lddx=dx.shape[1], h=h.data_ptr(), sigma=sigma.data_ptr(), d_sigma=g_sigma.data_ptr(),
                                 d_dino=g_dino.data_ptr(), wtf=p.wtf.data_ptr(),
                                 wxf=p.wxf.data_ptr(), dy=dy.data_ptr(), dh=dh.data_ptr(),
                                 dx=dx.data_ptr())

@@ -244,14 +244,14 @@ __global__ void __launch_bounds__(ML_WAVES * 64) k_mlp_bwd(const sd_mlp_train_ar
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 const int64_t p = p0 + 8 * (i >> 2) + 4 * h + (i & 3);
-                if (p < a.N) a.dx[p * a.ldx + col] = o[i];
+                if (p < a.N) a.dx[p * a.lddx + col] = o[i];
             }
         }
-        // the code / ones columns of dX carry no gradient: zeros
-        for (int c = a.C + lane; c < a.ldx; c += 64)
+        // the code / ones columns of dX (if the caller's rows have them) carry no gradient
+        for (int c = a.C + lane; c < a.lddx; c += 64)
             for (int i = 0; i < 32; ++i) {
                 const int64_t p = p0 + i;
-                if (p < a.N) a.dx[p * a.ldx + c] = 0.f;
+                if (p < a.N) a.dx[p * a.lddx + c] = 0.f;
             }
     }
 }
@@ -262,7 +262,7 @@ static int ml_check(const sd_mlp_train_args *a, bool bwd) {
         a->C > a->kx || a->N * a->ldx * 2 >= (1LL << 32))
         return 0;
     if (!bwd) return a->x && a->w1f && a->w2f && a->b_out && a->h && a->sigma && a->dino;
-    return a->wtf && a->wxf && a->h && a->sigma && a->d_sigma && a->d_dino && a->dy && a->dh &&
+    return a->lddx >= a->C && a->lddx <= a->ldx && a->wtf && a->wxf && a->h && a->sigma && a->d_sigma && a->d_dino && a->dy && a->dh &&
            a->dx;
 }
 
