@@ -96,6 +96,7 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
     // buffers) so that global stores are 16-B vectors along the output's contiguous axis
     // (pixels for NCHW, channels otherwise) instead of 2-B lane scatters.
     constexpr bool STAGED = EPI == SD_EPI_BF16 || EPI == SD_EPI_GELU || EPI == SD_EPI_SHUF ||
+                            EPI == SD_EPI_F32 ||
                             EPI == SD_EPI_NCHW;
     constexpr int OST = EPI == SD_EPI_NCHW ? BN + 1 : BN + 8;  // fp32 words per staged row
     constexpr int KL_BYTES = 2 * (BM + BN) * GLDS * 2;
@@ -298,6 +299,7 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
             }
         } else {
             // phase 2: thread = 8 consecutive columns of one row -> one 16-B bf16 store
+            // (f32 output: two)
             const int cout = EPI == SD_EPI_SHUF ? (int)(g.N / (g.shuf_k * g.shuf_k)) : 0;
             const bool vec = EPI == SD_EPI_SHUF ? (cout & 7) == 0 : (g.ldo & 7) == 0;
 #pragma unroll 4
@@ -350,6 +352,16 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
                     }
                 } else {
                     base = m * g.ldo + n;
+                }
+                if (EPI == SD_EPI_F32) {  // f32 rows (the channels-last DPT grid): 2 x 16 B
+                    float *o = (float *)g.out + base;
+                    if (full) {
+                        *(vf4 *)o = vf4{v[0], v[1], v[2], v[3]};
+                        *(vf4 *)(o + 4) = vf4{v[4], v[5], v[6], v[7]};
+                    } else {
+                        for (int u = 0; u < 8 && n + u < g.N; ++u) o[u] = v[u];
+                    }
+                    continue;
                 }
                 if (full) {
                     bf16x8 o;
