@@ -431,7 +431,7 @@ int sd_upsample2x(const void *in, int32_t B, int32_t H, int32_t W, int32_t C, vo
  * sd_mlp_train_fwd: h (N, 136) dtype = [relu(W_in x + b_in) | 1 | 0..], sigma (N) f32 =
  *   softplus(out_0), dino (N, D) f32 = out_1..D.
  * sd_mlp_train_bwd: from d_sigma (N), d_dino (N, D) f32: dy (N, 72) dtype = [d dino | d out_0
- *   | 0..], dh (N, 128) dtype = d relu-input, dx (N, lddx) f32 = [dH W_in[:, :C] | 0..];
+ *   | 0..], dh (N, 128) dtype = d relu-input, dx (N, lddx) dx_dtype = [dH W_in[:, :C] | 0..];
  *   the weight gradients are dh^T x and dy^T h (caller's GEMMs).  D <= 64, C % 32 == 0. */
 typedef struct sd_mlp_train_args {
     const void *x;
@@ -439,6 +439,8 @@ typedef struct sd_mlp_train_args {
     int32_t ldx, kx;       /* row length of x / dx, used columns (d_in + 1)              */
     int32_t dtype, D, C;
     int32_t lddx;          /* row length of dx (C: feature columns only; ldx: + zero columns) */
+    int32_t dx_dtype;      /* SD_F32, or dtype: 16-bit dx rows (the autocast gradient dtype)  */
+    int32_t pad;
     const void *w1f;       /* [4][ceil(kx/16)][64][8]  [W_in | b_in] A fragments          */
     const void *w2f;       /* [ceil((D+1)/32)][8][64][8] W_out B fragments (dino, out_0)   */
     const float *b_out;    /* (1 + D)                                                     */
@@ -448,7 +450,7 @@ typedef struct sd_mlp_train_args {
     const void *wtf;       /* [4][ceil((D+1)/16)][64][8] W_out^T A fragments              */
     const void *wxf;       /* [C/32][8][64][8] W_in B fragments (dX)                       */
     void *dy, *dh;
-    float *dx;
+    void *dx;
 } sd_mlp_train_args;
 
 int sd_mlp_train_fwd(const sd_mlp_train_args *args, void *stream);

@@ -113,7 +113,7 @@ class SdMlpTrainArgs(ctypes.Structure):
     """sd_mlp_train_args (include/sdhip.h): fused training MLP."""
     _fields_ = [
         ("x", _vp), ("N", _i64), ("ldx", _i32), ("kx", _i32), ("dtype", _i32), ("D", _i32),
-        ("C", _i32), ("lddx", _i32), ("w1f", _vp), ("w2f", _vp), ("b_out", _vp), ("h", _vp),
+        ("C", _i32), ("lddx", _i32), ("dx_dtype", _i32), ("pad", _i32), ("w1f", _vp), ("w2f", _vp), ("b_out", _vp), ("h", _vp),
         ("sigma", _vp), ("dino", _vp), ("d_sigma", _vp), ("d_dino", _vp), ("wtf", _vp),
         ("wxf", _vp), ("dy", _vp), ("dh", _vp), ("dx", _vp),
     ]
@@ -491,13 +491,13 @@ def field_gather(xyz, grid_nhwc, cam_f, img=None, cam_c=None, colors=True,
 
 
 def field_gather_bwd(xyz, dx, cam_f, Hf, Wf, C, dgrid=None):
-    """sd_field_gather_bwd: dx (B,P,>=C) -> dgrid (B,Hf,Wf,C) f32 (zeros, or accumulated
-    into the given dgrid)."""
+    """sd_field_gather_bwd: dx (B,P,>=C) f32 / f16 / bf16 rows -> dgrid (B,Hf,Wf,C) f32
+    (zeros, or accumulated into the given dgrid)."""
     lib = load()
     B, P, _ = xyz.shape
-    # f32 rows: the kernel's 4-byte lane loads keep its atomics lane-contiguous; 16-bit rows
-    # (sd_field_gather_bwd accepts them) measured slower than one conversion pass
-    dx = dx.float().contiguous()
+    if dx.dtype not in (torch.float32, torch.float16, torch.bfloat16):
+        dx = dx.float()
+    dx = dx.contiguous()
     if dgrid is None:
         dgrid = torch.zeros(B, Hf, Wf, C, device=xyz.device)
     _req(dgrid, "dgrid")

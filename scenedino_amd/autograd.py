@@ -220,9 +220,11 @@ class FieldMLPFused(torch.autograd.Function):
         return (dx if ctx.needs_input_grad[0] else None, *rest)
 
     @staticmethod
-    def grads(ctx, g_sigma, g_dino, full_rows=False):
-        """(dX f32, dW_in, db_in, dW_out, db_out) of the saved forward; dX rows are the C
-        feature columns, or (full_rows) as wide as x with zero code / ones columns."""
+    def grads(ctx, g_sigma, g_dino, full_rows=False, dx16=False):
+        """(dX, dW_in, db_in, dW_out, db_out) of the saved forward; dX rows are the C
+        feature columns, or (full_rows) as wide as x with zero code / ones columns; f32, or
+        (dx16) in x's 16-bit dtype -- the dtype the reference's autocast Linear backward
+        hands to grid_sample's backward."""
         x_aug, h, sigma = ctx.saved_tensors
         p = ctx.p
         N, ldx, d_in, D, C, dt, pdt = ctx.meta
@@ -231,9 +233,11 @@ class FieldMLPFused(torch.autograd.Function):
         g_dino = (g_dino if g_dino is not None else torch.zeros(N, D, device=dev)).float().contiguous()
         dy = torch.empty(N, 72, device=dev, dtype=x_aug.dtype)
         dh = torch.empty(N, 128, device=dev, dtype=x_aug.dtype)
-        dx = torch.empty(N, ldx if full_rows else C, device=dev)
+        dx = torch.empty(N, ldx if full_rows else C, device=dev,
+                         dtype=x_aug.dtype if dx16 else torch.float32)
         a = _lib.SdMlpTrainArgs(x=x_aug.data_ptr(), N=N, ldx=ldx, kx=d_in + 1, dtype=dt, D=D, C=C,
-                                lddx=dx.shape[1], h=h.data_ptr(), sigma=sigma.data_ptr(), d_sigma=g_sigma.data_ptr(),
+                                lddx=dx.shape[1], dx_dtype=dt if dx16 else _lib.SD_F32,
+                                h=h.data_ptr(), sigma=sigma.data_ptr(), d_sigma=g_sigma.data_ptr(),
                                 d_dino=g_dino.data_ptr(), wtf=p.wtf.data_ptr(),
                                 wxf=p.wxf.data_ptr(), dy=dy.data_ptr(), dh=dh.data_ptr(),
                                 dx=dx.data_ptr())
@@ -244,6 +248,12 @@ class FieldMLPFused(torch.autograd.Function):
         db_out = torch.cat((dWo[D:D + 1, 128], dWo[:D, 128]), 0)
         return (dx, dW1[:, :d_in].to(pdt).contiguous(), dW1[:, d_in].to(pdt).contiguous(),
                 dw_out.to(pdt).contiguous(), db_out.to(pdt).contiguous())
+
+
+# 16-bit dX rows from the fused MLP backward into the gather's scatter (the autocast
+# gradient dtype; halves the dX bytes): measured slower overall -- k_mlp_bwd 125 -> 103 us
+# but k_field_gather_bwd 140 -> 223 us on 2-byte lane loads -- so f32 rows by default
+DX16 = False
 
 
 class FieldGatherMLP(torch.autograd.Function):
@@ -281,7 +291,7 @@ class FieldGatherMLP(torch.autograd.Function):
         N = ctx.meta[0]
         gs = g_sigma.reshape(N) if g_sigma is not None else None
         gd = g_dino.reshape(N, -1) if g_dino is not None else None
-        dx, dw_in, db_in, dw_out, db_out = FieldMLPFused.grads(ctx, gs, gd)
+        dx, dw_in, db_in, dw_out, db_out = FieldMLPFused.grads(ctx, gs, gd, dx16=DX16)
         B, Hf, Wf, C = ctx.grid_shape
         d_empty = None
         if ctx.invf is not None:

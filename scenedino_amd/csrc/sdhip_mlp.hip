@@ -241,17 +241,28 @@ __global__ void __launch_bounds__(ML_WAVES * 64) k_mlp_bwd(const sd_mlp_train_ar
 #pragma unroll
             for (int s = 0; s < 8; ++s) o = Tr::mma32(af[s], wx[(u * 8 + s) * 64 + lane], o);
             const int col = 32 * u + r;
+            if (a.dx_dtype == SD_F32) {
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int64_t p = p0 + 8 * (i >> 2) + 4 * h + (i & 3);
-                if (p < a.N) a.dx[p * a.lddx + col] = o[i];
+                for (int i = 0; i < 16; ++i) {
+                    const int64_t p = p0 + 8 * (i >> 2) + 4 * h + (i & 3);
+                    if (p < a.N) ((float *)a.dx)[p * a.lddx + col] = o[i];
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int64_t p = p0 + 8 * (i >> 2) + 4 * h + (i & 3);
+                    if (p < a.N) ((E *)a.dx)[p * a.lddx + col] = (E)o[i];
+                }
             }
         }
         // the code / ones columns of dX (if the caller's rows have them) carry no gradient
         for (int c = a.C + lane; c < a.lddx; c += 64)
             for (int i = 0; i < 32; ++i) {
                 const int64_t p = p0 + i;
-                if (p < a.N) a.dx[p * a.lddx + c] = 0.f;
+                if (p < a.N) {
+                    if (a.dx_dtype == SD_F32) ((float *)a.dx)[p * a.lddx + c] = 0.f;
+                    else ((E *)a.dx)[p * a.lddx + c] = (E)0.f;
+                }
             }
     }
 }
@@ -262,7 +273,7 @@ static int ml_check(const sd_mlp_train_args *a, bool bwd) {
         a->C > a->kx || a->N * a->ldx * 2 >= (1LL << 32))
         return 0;
     if (!bwd) return a->x && a->w1f && a->w2f && a->b_out && a->h && a->sigma && a->dino;
-    return a->lddx >= a->C && a->lddx <= a->ldx && a->wtf && a->wxf && a->h && a->sigma && a->d_sigma && a->d_dino && a->dy && a->dh &&
+    return a->lddx >= a->C && a->lddx <= a->ldx && (a->dx_dtype == SD_F32 || a->dx_dtype == a->dtype) && a->wtf && a->wxf && a->h && a->sigma && a->d_sigma && a->d_dino && a->dy && a->dh &&
            a->dx;
 }
 
