@@ -453,6 +453,20 @@ typedef struct sd_mlp_train_args {
     void *dx;
 } sd_mlp_train_args;
 
+/* Weight gradients of the training MLP: part[w] (Ma_pad x Nb_pad f32, pads to 32) =
+ * sum over workgroup w's contiguous range of the N points of A[p]^T B[p], A (N, lda) and
+ * B (N, ldb) 16-bit rows of which the first Ma / Nb columns are used (dW1 = dH^T X,
+ * dW_o = dY^T [H | 1]); the caller sums the nparts partials.  Ma <= 128, Nb <= 320,
+ * both multiples of 8. */
+typedef struct sd_wgrad_args {
+    const void *a, *b;
+    int64_t N;
+    int32_t lda, ldb, Ma, Nb, dtype, nparts;
+    float *part;           /* (nparts, Ma_pad, Nb_pad)                                    */
+} sd_wgrad_args;
+
+int sd_wgrad(const sd_wgrad_args *args, void *stream);
+
 int sd_mlp_train_fwd(const sd_mlp_train_args *args, void *stream);
 int sd_mlp_train_bwd(const sd_mlp_train_args *args, void *stream);
 

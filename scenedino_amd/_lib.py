@@ -119,6 +119,12 @@ class SdMlpTrainArgs(ctypes.Structure):
     ]
 
 
+class SdWgradArgs(ctypes.Structure):
+    """sd_wgrad_args (include/sdhip.h): training-MLP weight gradients."""
+    _fields_ = [("a", _vp), ("b", _vp), ("N", _i64), ("lda", _i32), ("ldb", _i32),
+                ("Ma", _i32), ("Nb", _i32), ("dtype", _i32), ("nparts", _i32), ("part", _vp)]
+
+
 class SdSalienceArgs(ctypes.Structure):
     """sd_salience_args (include/sdhip.h): PatchSalienceDownsampler forward / backward."""
     _fields_ = [
@@ -181,6 +187,7 @@ SIGNATURES = {
                          _vp],
     "sd_mlp_train_fwd": [ctypes.POINTER(SdMlpTrainArgs), _vp],
     "sd_mlp_train_bwd": [ctypes.POINTER(SdMlpTrainArgs), _vp],
+    "sd_wgrad": [ctypes.POINTER(SdWgradArgs), _vp],
     "sd_salience_fwd": [ctypes.POINTER(SdSalienceArgs), _vp],
     "sd_salience_bwd": [ctypes.POINTER(SdSalienceArgs), _vp],
     "sd_gemm": [ctypes.POINTER(SdGemmArgs), _vp],
@@ -264,6 +271,23 @@ def mlp_train_fwd(args: SdMlpTrainArgs, ref_tensor):
 def mlp_train_bwd(args: SdMlpTrainArgs, ref_tensor):
     lib = load()
     _check(lib.sd_mlp_train_bwd(ctypes.byref(args), stream_of(ref_tensor)), "sd_mlp_train_bwd")
+
+
+def wgrad(a, b, Ma, Nb, nparts=None):
+    """sum_p a[p, :Ma]^T b[p, :Nb] over the rows of two 16-bit (N, *) matrices (sd_wgrad):
+    (Ma, Nb) f32."""
+    lib = load()
+    N = a.shape[0]
+    MaP, NbP = (Ma + 31) // 32 * 32, (Nb + 31) // 32 * 32
+    if nparts is None:  # ~2 workgroups per CU over the column splits (5 tiles each)
+        splits = (NbP // 32 + 4) // 5
+        nparts = max(1, min(512 // splits, (N + 511) // 512))
+    part = torch.empty(nparts, MaP, NbP, device=a.device)
+    g = SdWgradArgs(a=a.data_ptr(), b=b.data_ptr(), N=N, lda=a.stride(0), ldb=b.stride(0),
+                    Ma=Ma, Nb=Nb, dtype=SD_OF_TORCH[a.dtype], nparts=nparts,
+                    part=part.data_ptr())
+    _check(lib.sd_wgrad(ctypes.byref(g), stream_of(a)), "sd_wgrad")
+    return part.sum(0)[:Ma, :Nb]
 
 
 def salience_fwd(args: SdSalienceArgs, ref_tensor):

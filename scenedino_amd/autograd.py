@@ -242,8 +242,8 @@ class FieldMLPFused(torch.autograd.Function):
                                 wxf=p.wxf.data_ptr(), dy=dy.data_ptr(), dh=dh.data_ptr(),
                                 dx=dx.data_ptr())
         _timed("mlp_bwd", lambda: _lib.mlp_train_bwd(a, x_aug))
-        dW1 = _wgrad(dh, x_aug)             # (128, d_in + 1): [dW_in | db_in]
-        dWo = _wgrad(dy, h)                 # (72, 136): rows dino 0..D-1, out_0; col 128 bias
+        dW1 = _lib.wgrad(dh, x_aug, 128, d_in + 1)   # (128, d_in + 1): [dW_in | db_in]
+        dWo = _lib.wgrad(dy, h, 72, 136)             # rows dino 0..D-1, out_0; col 128 bias
         dw_out = torch.cat((dWo[D:D + 1, :128], dWo[:D, :128]), 0)
         db_out = torch.cat((dWo[D:D + 1, 128], dWo[:D, 128]), 0)
         return (dx, dW1[:, :d_in].to(pdt).contiguous(), dW1[:, d_in].to(pdt).contiguous(),

@@ -324,3 +324,178 @@ extern "C" int sd_mlp_train_bwd(const sd_mlp_train_args *a, void *stream) {
     if (a->dtype == SD_F16) return ml_launch(k_mlp_bwd<SD_F16>, a, lds, (hipStream_t)stream);
     return ml_launch(k_mlp_bwd<SD_BF16>, a, lds, (hipStream_t)stream);
 }
+
+// ---------------------------------------------------------------------------
+// weight gradients of the training MLP: C = A^T B over the N points, A (N, Ma) and B (N, Nb)
+// 16-bit rows (dW1 = dH^T X, dW_o = dY^T [H | 1]).  A workgroup (4 waves) sums a contiguous
+// range of points into a partial (Ma x Nb) f32 tile set; the partials are summed by the
+// caller (deterministic).  Both operands have k = points, the slow axis of their rows: each
+// 32-point chunk is staged row-major in LDS and read back transposed by
+// ds_read_b64_tr_b16 (4 rows x 16 columns per 16-lane group, delivered column-major), so
+// lane (row / column r, half h) gets the 8 points 8 h .. 8 h + 7 of its row / column.
+// Wave w owns output row tile w (Ma <= 128) and every column tile (its A fragment re-used
+// across the row).
+// ---------------------------------------------------------------------------
+#define WG_MAXT 10  // column tiles per wave (Nb <= 320)
+#define WG_MAXLD 8  // 16-B staging loads per thread per 32-point chunk
+
+typedef __attribute__((ext_vector_type(4))) short wg_s16x4;
+
+__device__ __forceinline__ uint2 wg_tr(const void *lds_addr) {
+    const wg_s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) wg_s16x4 *)(uintptr_t)lds_addr);
+    return __builtin_bit_cast(uint2, v);
+}
+
+template <int P, int NT>
+__global__ void __launch_bounds__(256) k_wgrad(const sd_wgrad_args g) {
+    typedef T16<P> Tr;
+    typedef typename Tr::Frag Frag;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int MaP = (g.Ma + 31) & ~31, NbP = (g.Nb + 31) & ~31;
+    // column split blockIdx.y: columns [nb0, nb0 + nbw) of B, NT tiles of 32
+    const int nb0 = blockIdx.y * NT * 32;
+    const int nbw = g.Nb - nb0 < NT * 32 ? g.Nb - nb0 : NT * 32;
+    const int rsa = MaP + 8, rsb = NT * 32 + 8;  // LDS row strides (elements; 16-B multiples)
+    uint16_t *sA = (uint16_t *)lds;
+    uint16_t *sB = sA + 32 * rsa;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int mt = MaP >> 5;
+    // zero the padding columns once (loads never write them)
+    for (int i = tid; i < 32 * rsa; i += 256) sA[i] = 0;
+    for (int i = tid; i < 32 * rsb; i += 256) sB[i] = 0;
+    __syncthreads();
+    // this workgroup's points [p_lo, p_hi)
+    const int64_t per = (g.N + gridDim.x - 1) / gridDim.x;
+    const int64_t p_lo = (int64_t)blockIdx.x * per;
+    const int64_t p_hi = p_lo + per < g.N ? p_lo + per : g.N;
+    // 16-B chunks of one 32-row chunk: A (32 x Ma), B (32 x Nb)
+    const int ca = g.Ma / 8, cb = nbw / 8;  // chunks per row (Ma, Nb multiples of 8)
+    const int nca = 32 * ca, ncb = 32 * cb;
+    const int nld = (nca + ncb + 255) / 256;  // loads per thread
+    // transposed-read lane address: group G = lane >> 4 (col base 16 (G & 1), k base
+    // 8 (G >> 1)), lane 4 q + p of the group: row (k) kb + q, columns cb + 4 p .. + 3
+    const int G = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+    const int kb = 8 * (G >> 1), cbase = 16 * (G & 1) + 4 * pp;
+    // wave w owns output row tile w (Ma <= 128) and all NT column tiles
+    const bool own = wave < mt;
+    f32x16 acc[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+    uint4 st[WG_MAXLD];  // staged chunk pieces (nld <= WG_MAXLD)
+    auto gload = [&](int64_t p0) {
+#pragma unroll
+        for (int i = 0; i < WG_MAXLD; ++i) {
+            const int c = tid + 256 * i;
+            if (i < nld && c < nca + ncb) {
+                if (c < nca) {
+                    const int row = c / ca, col = (c - row * ca) * 8;
+                    const int64_t p = p0 + row;
+                    st[i] = p < p_hi ? *(const uint4 *)((const uint16_t *)g.a + p * g.lda + col)
+                                     : uint4{0u, 0u, 0u, 0u};
+                } else {
+                    const int cc = c - nca, row = cc / cb, col = (cc - row * cb) * 8;
+                    const int64_t p = p0 + row;
+                    st[i] = p < p_hi ? *(const uint4 *)((const uint16_t *)g.b + p * g.ldb + nb0 + col)
+                                     : uint4{0u, 0u, 0u, 0u};
+                }
+            }
+        }
+    };
+    auto lstore = [&]() {
+#pragma unroll
+        for (int i = 0; i < WG_MAXLD; ++i) {
+            const int c = tid + 256 * i;
+            if (i < nld && c < nca + ncb) {
+                if (c < nca) {
+                    const int row = c / ca, col = (c - row * ca) * 8;
+                    *(uint4 *)(sA + row * rsa + col) = st[i];
+                } else {
+                    const int cc = c - nca, row = cc / cb, col = (cc - row * cb) * 8;
+                    *(uint4 *)(sB + row * rsb + col) = st[i];
+                }
+            }
+        }
+    };
+    if (p_lo < p_hi) gload(p_lo);
+    for (int64_t p0 = p_lo; p0 < p_hi; p0 += 32) {
+        __syncthreads();  // the previous chunk's reads are done
+        lstore();
+        __syncthreads();
+        if (p0 + 32 < p_hi) gload(p0 + 32);  // next chunk in flight under this one
+        if (own) {
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {  // two k-steps of 16 points
+                const uint16_t *ra = sA + (16 * s + kb + q) * rsa + 32 * wave + cbase;
+                const uint2 a0 = wg_tr(ra), a1 = wg_tr(ra + 4 * rsa);
+                const Frag af = __builtin_bit_cast(Frag, uint4{a0.x, a0.y, a1.x, a1.y});
+#pragma unroll
+                for (int j = 0; j < NT; ++j) {
+                    const uint16_t *rb = sB + (16 * s + kb + q) * rsb + 32 * j + cbase;
+                    const uint2 b0 = wg_tr(rb), b1 = wg_tr(rb + 4 * rsb);
+                    const Frag bf = __builtin_bit_cast(Frag, uint4{b0.x, b0.y, b1.x, b1.y});
+                    acc[j] = Tr::mma32(af, bf, acc[j]);
+                }
+            }
+        }
+    }
+    // partial tile: acc[i][j] register e = C[32 ti + 8 (e >> 2) + 4 h + (e & 3)][32 j + r]
+    float *out = g.part + (int64_t)blockIdx.x * MaP * NbP;
+    if (own) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e)
+                if (32 * j < nbw)
+                    out[(int64_t)(32 * wave + 8 * (e >> 2) + 4 * h + (e & 3)) * NbP + nb0 + 32 * j + r] =
+                        acc[j][e];
+    }
+}
+
+extern "C" int sd_wgrad(const sd_wgrad_args *g, void *stream) {
+    if (!g || !g->a || !g->b || !g->part || g->N < 0 || g->Ma <= 0 || g->Nb <= 0 ||
+        g->Ma % 8 || g->Nb % 8 || g->Ma > 128 || g->Nb > 32 * WG_MAXT || g->lda < g->Ma ||
+        g->ldb < g->Nb || g->lda % 8 || g->ldb % 8 || g->nparts <= 0 ||
+        (g->dtype != SD_F16 && g->dtype != SD_BF16) ||
+        (32 * (g->Ma / 8) + 32 * (g->Nb / 8) + 255) / 256 > WG_MAXLD) {
+        sd_set_error("sd_wgrad: invalid argument (16-bit rows, Ma <= 128, Nb <= 320, "
+                     "multiples of 8)");
+        return -1;
+    }
+    const int MaP = (g->Ma + 31) & ~31, NbP = (g->Nb + 31) & ~31;
+    const int lds = 32 * (MaP + 8 + 5 * 32 + 8) * 2;
+    if (g->N == 0) {
+        if (hipMemsetAsync(g->part, 0, (size_t)g->nparts * MaP * NbP * 4, (hipStream_t)stream) !=
+            hipSuccess) {
+            sd_set_error("sd_wgrad: memset failed");
+            return -2;
+        }
+        return 0;
+    }
+    // column tiles per workgroup: at most 5 (<= ~200 VGPRs: two waves per SIMD), the rest
+    // of the columns split over gridDim.y
+    const int nt_all = NbP / 32;
+    const int ncs = (nt_all + 4) / 5;
+    const int nt = (nt_all + ncs - 1) / ncs;
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 grid((unsigned)g->nparts, (unsigned)ncs);
+#define WG_CASE(NT_)                                                                             \
+    case NT_:                                                                                    \
+        if (g->dtype == SD_F16)                                                                  \
+            hipLaunchKernelGGL((k_wgrad<SD_F16, NT_>), grid, dim3(256), lds, st, *g);            \
+        else                                                                                     \
+            hipLaunchKernelGGL((k_wgrad<SD_BF16, NT_>), grid, dim3(256), lds, st, *g);           \
+        break;
+    switch (nt) {
+        WG_CASE(1) WG_CASE(2) WG_CASE(3) WG_CASE(4) WG_CASE(5)
+    }
+#undef WG_CASE
+    if (hipGetLastError() != hipSuccess) {
+        sd_set_error("sd_wgrad: launch failed");
+        return -2;
+    }
+    return 0;
+}

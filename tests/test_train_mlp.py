@@ -80,3 +80,18 @@ def test_fused_mlp_vs_autocast_linear(N, dt):
     assert not xr.grad[:, 256:].any()
     for a, b, name in zip(ps, qs, ("W_in", "b_in", "W_out", "b_out")):
         assert rel_l2(a.grad, b.grad) <= 2e-2, name
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,Ma,Nb,lda,ldb", [(262144, 128, 296, 128, 296), (262144, 72, 136, 72, 136),
+                                            (1000, 128, 296, 136, 304), (37, 72, 136, 72, 136)])
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+def test_wgrad_kernel_vs_matmul(N, Ma, Nb, lda, ldb, dt):
+    """sd_wgrad (the training MLP's weight gradients, A^T B over the points) vs an f64
+    matmul of the same 16-bit operands: rel-L2 <= 1e-5 (f32 accumulation order only)."""
+    g = torch.Generator(device="cuda").manual_seed(N + Ma)
+    a = torch.randn(N, lda, device="cuda", generator=g).to(dt)
+    b = torch.randn(N, ldb, device="cuda", generator=g).to(dt)
+    got = _lib.wgrad(a, b, Ma, Nb)
+    ref = a[:, :Ma].double().t() @ b[:, :Nb].double()
+    assert rel_l2(got, ref) <= 1e-5
