@@ -549,7 +549,9 @@ def main_train(args, world, rank, device):
     dino_gt_map = torch.randn(NB, 1, D_DINO, H // PS, W // PS, device=device, generator=g)
     # the grid is an activation (the encoder's output): its gradient is computed, the
     # optimizer steps the head (a frozen-encoder config; encoder backward is not ours)
-    opt = torch.optim.Adam(head.parameters(), lr=1e-4)
+    # Adam as one fused kernel over the head's parameters (torch's fused implementation, the
+    # same update as the reference's Adam: base_trainer.py optimizer)
+    opt = torch.optim.Adam(head.parameters(), lr=1e-4, fused=True)
     amp = not args.no_amp  # train_scenedino_kitti_360.yaml: with_amp: true (fp16 autocast)
     npatch = RB // (PS * PS)
 

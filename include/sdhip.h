@@ -484,7 +484,7 @@ int sd_mlp_train_bwd(const sd_mlp_train_args *args, void *stream);
 typedef struct sd_salience_args {
     const float *x;
     const float *w;        /* conv.weight (C)                                              */
-    float b;               /* conv.bias                                                    */
+    const float *b;        /* conv.bias (1, device; NULL: no bias)                          */
     const float *pw;       /* patch_weight (S)                                             */
     const float *pb;       /* patch_bias (S)                                               */
     int64_t N;

@@ -128,7 +128,7 @@ class SdWgradArgs(ctypes.Structure):
 class SdSalienceArgs(ctypes.Structure):
     """sd_salience_args (include/sdhip.h): PatchSalienceDownsampler forward / backward."""
     _fields_ = [
-        ("x", _vp), ("w", _vp), ("b", ctypes.c_float), ("pw", _vp), ("pb", _vp), ("N", _i64),
+        ("x", _vp), ("w", _vp), ("b", _vp), ("pw", _vp), ("pb", _vp), ("N", _i64),
         ("S", _i32), ("C", _i32), ("normalize", _i32), ("pad", _i32),
         ("out", _vp), ("sal", _vp), ("wmap", _vp), ("ynorm", _vp),
         ("g_out", _vp), ("g_sal", _vp), ("g_wmap", _vp),

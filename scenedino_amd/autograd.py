@@ -364,14 +364,15 @@ class SalienceDownsample(torch.autograd.Function):
         sal = torch.empty(N, S, device=x.device)
         wmap = torch.empty(N, S, device=x.device)
         ynorm = torch.empty(N, device=x.device)
-        bias = float(b.reshape(-1)[0].item()) if b is not None else 0.0
-        a = _lib.SdSalienceArgs(x=x.data_ptr(), w=w.data_ptr(), b=bias, pw=pw_.data_ptr(),
+        bias = b.detach().float().reshape(-1).contiguous() if b is not None else None
+        a = _lib.SdSalienceArgs(x=x.data_ptr(), w=w.data_ptr(),
+                                b=bias.data_ptr() if bias is not None else None, pw=pw_.data_ptr(),
                                 pb=pb_.data_ptr(), N=N, S=S, C=C, normalize=int(bool(normalize)),
                                 out=out.data_ptr(), sal=sal.data_ptr(), wmap=wmap.data_ptr(),
                                 ynorm=ynorm.data_ptr())
         _timed("salience", lambda: _lib.salience_fwd(a, x))
         ctx.save_for_backward(x, w, pw_, pb_, out, sal, wmap, ynorm)
-        ctx.normalize, ctx.bias, ctx.has_b = bool(normalize), bias, b is not None
+        ctx.normalize, ctx.has_b = bool(normalize), b is not None
         ctx.pshape = (pw.shape, pb.shape, wshape)
         return out, sal, wmap
 
@@ -390,7 +391,7 @@ class SalienceDownsample(torch.autograd.Function):
         gpb = torch.empty(N, S, device=x.device)
         gb = torch.empty(N, device=x.device)
         a = _lib.SdSalienceArgs(
-            x=x.data_ptr(), w=w.data_ptr(), b=ctx.bias, pw=pw_.data_ptr(), pb=pb_.data_ptr(),
+            x=x.data_ptr(), w=w.data_ptr(), b=None, pw=pw_.data_ptr(), pb=pb_.data_ptr(),
             N=N, S=S, C=C, normalize=int(ctx.normalize), out=out.data_ptr(), sal=sal.data_ptr(),
             wmap=wmap.data_ptr(), ynorm=ynorm.data_ptr(), g_out=g_out.data_ptr(),
             g_sal=g_sal.data_ptr() if g_sal is not None else None,

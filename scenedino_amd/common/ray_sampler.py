@@ -53,6 +53,8 @@ class PatchRaySampler(RaySampler):
         assert (ray_batch_size % (self.patch_size_x * self.patch_size_y)) == 0
         self._patch_count = self.ray_batch_size // (self.patch_size_x * self.patch_size_y)
         self._ids_cache = {}
+        self._ring = [None, None]  # pinned host staging of the drawn patches (+ copy event)
+        self._slot = 0
 
     def _draw(self, n, v, h, w, dino_hw, loss_feature_grid_shift):
         """The reference's per-frame randint draws (:215-226) -> (n, patches, 4) int32:
@@ -86,6 +88,25 @@ class PatchRaySampler(RaySampler):
             out[n_] = torch.stack((cv, y, x, gy * dw + gx), 1).to(torch.int32)
         return out
 
+    def _upload(self, patches, device):
+        """Host -> device copy of the drawn patches through a 2-slot pinned ring: a copy from
+        pageable memory would block the host until the stream drained (a device sync per
+        training step); a slot is reused only after its previous copy has completed."""
+        slot = self._slot
+        self._slot ^= 1
+        ent = self._ring[slot]
+        if ent is None or ent[0].shape != patches.shape:
+            ent = self._ring[slot] = [torch.empty(patches.shape, dtype=patches.dtype,
+                                                  pin_memory=True), None]
+        if ent[1] is not None:
+            ent[1].synchronize()
+        ent[0].copy_(patches)
+        out = ent[0].to(device, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(device))
+        ent[1] = ev
+        return out
+
     def sample(self, images, poses, projs, image_ids=None, dino_features=None,
                loss_feature_grid_shift=None):
         n, v, c, h, w = images.shape
@@ -96,7 +117,7 @@ class PatchRaySampler(RaySampler):
         patches = self._draw(n, v, h, w, dino_hw, loss_feature_grid_shift)
         if device.type != "cuda":
             raise RuntimeError("PatchRaySampler: the device sampler needs CUDA (HIP) tensors")
-        patches = patches.to(device, non_blocking=True)
+        patches = self._upload(patches, device)
         if image_ids is None:
             key = (v, str(device))
             ids = self._ids_cache.get(key)

@@ -92,7 +92,7 @@ __global__ void __launch_bounds__(DS_T) k_salience_fwd(const sd_salience_args g)
     for (int i = wave; i < S; i += 4) {
         const float d = ds_dot(xp + (int64_t)i * C, s_w, C, lane);
         if (lane == 0) {
-            const float s = d + g.b;
+            const float s = d + (g.b ? g.b[0] : 0.f);
             s_s[i] = s;
             s_a[i] = fmaf(s, g.pw[i], g.pb[i]);
         }

@@ -226,10 +226,12 @@ class NeRFRenderer(torch.nn.Module):
         finally:
             if hooks:
                 model.end_pass()
-        rgbs = torch.cat(rgbs_all, dim=dim).reshape(B, K, -1).float().contiguous()
-        invalid = torch.cat(inv_all, dim=dim).reshape(B, K, -1)
-        sigmas = torch.cat(sig_all, dim=dim).reshape(B, K).float().contiguous()
-        state_dicts = {k: torch.cat([s[k] for s in sds], dim=dim) for k in sds[0]} if sds else None
+        # (one chunk -- the training path -- is used as is: torch.cat copies even one tensor)
+        cat = lambda xs: xs[0] if len(xs) == 1 else torch.cat(xs, dim=dim)
+        rgbs = cat(rgbs_all).reshape(B, K, -1).float().contiguous()
+        invalid = cat(inv_all).reshape(B, K, -1)
+        sigmas = cat(sig_all).reshape(B, K).float().contiguous()
+        state_dicts = {k: cat([s[k] for s in sds]) for k in sds[0]} if sds else None
         if state_dicts is not None:
             state_dicts = {k: v.reshape(B, K, *v.shape[2:]) for k, v in state_dicts.items()}
         feat = state_dicts["dino_features"].float().contiguous() if state_dicts else None
