@@ -243,6 +243,22 @@ class BTSNet(nn.Module):
             self._packed_key = key
         return self._packed
 
+    def _mlp_projq(self):
+        """Field MLP over the projected grid: first layer [I_128 | W_in's code columns] with
+        a zero bias (P already holds W_in[:, :C] G + b_in), the output layer unchanged."""
+        head = self.heads[self.final_pred_head]
+        self._mlp()
+        key = self._packed_key
+        if getattr(self, "_packed_q", None) is None or self._packed_q[0] != key:
+            W_in, W_out = head.lin_in.weight.detach(), head.lin_out.weight.detach()
+            C = W_in.shape[1] - self.code_xyz.d_out
+            dh = W_in.shape[0]
+            Wq = torch.cat((torch.eye(dh, device=W_in.device, dtype=W_in.dtype), W_in[:, C:]), 1)
+            bq = torch.zeros(dh, device=W_in.device, dtype=W_in.dtype)
+            self._packed_q = (key, PackedMLP(Wq, bq, W_out, head.lin_out.bias.detach(),
+                                             dtype=self._dtype()))
+        return self._packed_q[1]
+
     def _grids(self):
         g = self.grid_f_features[self._scale]
         key = (id(g), g._version, id(self.grid_c_imgs), self.grid_c_imgs._version,
@@ -400,6 +416,15 @@ class BTSNet(nn.Module):
         gc = self._grids()
         if gc["C"] != m.C:
             raise ValueError(f"feature grid has {gc['C']} channels, the MLP expects {m.C}")
+        if self._use_proj():
+            # 16-bit projected mode: the same field kernel on the projected grid P
+            # (B, Hf, Wf, 128) = W_in[:, :C] G + b_in with an identity first layer for its
+            # 128 columns (gather 4 x 256 B per point instead of 4 x 512 B, 8 instead of 16
+            # grid k-steps); P is the one the renders use, projected once per encode
+            grid = self._grid_proj(gc, m)
+            m = self._mlp_projq()
+        else:
+            grid = self._grid_nhwc(gc)
         n, P, _ = xyz.shape
         if n != gc["B"]:
             raise ValueError(f"xyz batch {n} != encoded batch {gc['B']}")
@@ -412,7 +437,7 @@ class BTSNet(nn.Module):
         inv = torch.empty(n, P, nv, device=dev) if colors else None
         invf = torch.empty(n, P, device=dev, dtype=torch.bool)  # bytes 0 / 1
         args = _lib.SdFieldArgs(
-            xyz=xyz.data_ptr(), B=n, P=P, grid=self._grid_nhwc(gc).data_ptr(), Hf=gc["Hf"],
+            xyz=xyz.data_ptr(), B=n, P=P, grid=grid.data_ptr(), Hf=gc["Hf"],
             Wf=gc["Wf"],
             cam_f=gc["cam_f"].data_ptr(), img=gc["img"].data_ptr() if colors else None, nv=nv,
             Hc=gc["Hc"], Wc=gc["Wc"], cam_c=gc["cam_c"].data_ptr(), sigma=sigma.data_ptr(),
