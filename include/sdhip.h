@@ -306,7 +306,9 @@ typedef struct sd_seg_head {
     const float *bm;       /* [d_full/32][2][16]  Wn1 b2                              */
     const float *bn1;      /* [d_full/32][2][16]                                      */
     const void *wn2;       /* bf16 [d_code/32][d_full/16][64][8]                      */
-    const float *centres;  /* [n_clusters][d_code/32][2][16] normalised centres       */
+    const void *centres;   /* normalised centres as bf16 A fragments, hi and lo halves:
+                            * [ceil(n_clusters/32)][2][d_code/16][64][8], rows = clusters
+                            * (zero rows pad the last tile), permuted k order          */
     const int32_t *assign; /* [n_clusters] pseudo_assignment                           */
     int32_t n_clusters;    /* 1..256                                                   */
     int32_t d_in;          /* 64  (reduced DINO dims)                                  */
@@ -320,6 +322,13 @@ typedef struct sd_seg_head {
     const void *w2_f8;
     float w2_f8_scale;     /* 2^e_w                                                    */
     int32_t pad0;
+    /* the norm by the Gram form |e|^2 = h^T G h + 2 g.h + |b2|^2 (every bf16 launch):
+     * G = W2^T W2 as bf16 hi + lo fragments, tile t = 16 fragments (hi k-steps 0..7,
+     * lo 0..7), [d_latent/32][16][64][8], permuted k order                           */
+    const void *wg;
+    const float *g2;       /* [d_latent/32][2][16]  2 W2^T b2                         */
+    float b2sq;            /* |b2|^2                                                   */
+    int32_t pad1;
 } sd_seg_head;
 
 /* Per-point segmentation head on P DINO codes dino (P, d_in) f32.

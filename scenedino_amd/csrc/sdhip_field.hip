@@ -41,7 +41,7 @@ extern "C" void sd_set_error(const char *msg) {
     g_err[sizeof(g_err) - 1] = 0;
 }
 extern "C" const char *sd_last_error(void) { return g_err; }
-extern "C" int sd_abi_version(void) { return 6; }
+extern "C" int sd_abi_version(void) { return 7; }
 
 // Threads per workgroup, one workgroup per CU: 16-bit kernels run 8 waves (2 per SIMD,
 // <= 256 VGPRs each); the f32 parity kernels run 4 waves (1 per SIMD, 512 VGPRs).

@@ -20,12 +20,18 @@
 //         = (L h + Wl b2) / n + bl + bn2 + Wn2 relu((M h + Wn1 b2) / n + bn1)
 //   with L = Wl W2 (64 x 128) and M = Wn1 W2 (768 x 128) folded once on the host: the
 //   768 x 768 product of the reference becomes a 768 x 128 one.  The class is
-//   argmax_k <stego / |stego|, c_k / |c_k|> = argmax_k <stego, c_k / |c_k|> (a positive
-//   scale does not move an argmax), evaluated in fp32.
+//   argmax_k <stego / |stego|, c_k / |c_k|> = argmax_k <n stego, c_k / |c_k|> (a positive
+//   scale does not move an argmax), so the kernel forms n stego (n u = relu(M h + Wn1 b2 +
+//   n bn1): the biases enter as accumulator inits, no per-element rescale) and scores it
+//   on the matrix cores with hi + lo bf16 operands (fp32-grade).
+//
+// The norm: |e|^2 = h^T G h + 2 (W2^T b2).h + |b2|^2 with G = W2^T W2 (d_latent x
+// d_latent, folded on the host, bf16 hi + lo fragments): 64 MFMAs per 32 points instead of
+// the 768 x 128 product (the fp8 record keeps that product on fp8 MFMA).
 //
 // Work unit: one wave = SG_NT x 32 points (lane = point, as the accumulator columns of
 // v_mfma_f32_32x32x16_bf16); weights are the MFMA A operands (rows = output features),
-// 1-KiB fragments (each feeds SG_NT MFMAs).  The big products (W2, M + Wn2) stream their
+// 1-KiB fragments (each feeds SG_NT MFMAs).  The big products (Gram, M + Wn2) stream their
 // weight tiles through LDS, double-buffered and shared by the workgroup's 8 waves
 // (2 per SIMD); the small ones (W1, L) read their fragments from L2.  Hidden vectors
 // never leave the registers: an accumulator tile is converted in place into the B operand
@@ -115,10 +121,33 @@ typedef __attribute__((ext_vector_type(8))) int i32x8_t;
 
 __device__ __forceinline__ uint32_t sg_bf16_bits(__bf16 v) { return (uint32_t)__builtin_bit_cast(unsigned short, v); }
 
+// element e of a bf16x8 register quad as f32; volatile so that the unpacking stays in the
+// Gram epilogue (hoisted, h's 128 unpacked values would spill)
+__device__ __forceinline__ float sg_bf16_at(bf16x8 v, int e) {
+    typedef __attribute__((ext_vector_type(4))) uint32_t u32x4_t;
+    const uint32_t w = __builtin_bit_cast(u32x4_t, v)[e >> 1];
+    float r;
+    if (e & 1) asm volatile("v_and_b32 %0, 0xffff0000, %1" : "=v"(r) : "v"(w));
+    else asm volatile("v_lshlrev_b32 %0, 16, %1" : "=v"(r) : "v"(w));
+    return r;
+}
+
+// relu(acc[8 s .. 8 s + 7]) as a bf16 B operand: round to bf16 (RNE), then max with +0 on
+// the 16-bit patterns (a negative bf16 is a negative int16): one v_pk_max_i16 per pair
+__device__ __forceinline__ bf16x8 sg_relu_b(const f32x16 &acc, int s) {
+    typedef __attribute__((ext_vector_type(8))) short s16x8_t;
+    bf16x8 r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = (__bf16)acc[8 * s + j];
+    s16x8_t v = __builtin_bit_cast(s16x8_t, r);
+    v = __builtin_elementwise_max(v, (s16x8_t)0);
+    return __builtin_bit_cast(bf16x8, v);
+}
+
 // Weight tiles are streamed through LDS, shared by the workgroup's 4 waves (each wave used
 // to read every fragment from L2 itself): 1-KiB pieces by LDS-DMA, issued as inline asm so
 // that the compiler does not fence every LDS read behind the DMA (m0 = LDS destination).
-#define SG_SLOT (12 * 1024)  // one tile: 8 bf16 fragments (+ 4 Wn2 fragments) or 4 KiB fp8
+#define SG_SLOT (16 * 1024)  // one tile: 16 Gram fragments, 8 M + 4 Wn2 fragments or 4 KiB fp8
 __device__ __forceinline__ void sg_dma1k(const uint8_t *src, uint32_t lds_dst, int lane) {
     lds_dst = __builtin_amdgcn_readfirstlane(lds_dst);
     asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
@@ -157,6 +186,17 @@ __global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const float *__restr
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     };
+    // Gram tile t: 16 fragments at t * 16 KiB
+    auto gsrc = [&](int t) { return [=](int i) { return (const uint8_t *)h.wg + (int64_t)t * 16384 + i * 1024; }; };
+    // M tile t: M fragments (t, 0..7) at t * 8 KiB, then Wn2 fragments (rt, 2 t + s)
+    const int KS = DF / 16;
+    auto msrc = [&](int t) {
+        return [=](int i) {
+            return i < 8 ? (const uint8_t *)h.wm + (int64_t)t * 8192 + i * 1024
+                         : (const uint8_t *)h.wn2 + ((int64_t)((i - 8) >> 1) * KS + 2 * t + ((i - 8) & 1)) * 1024;
+        };
+    };
+    if (!F8) stage(0, 16, gsrc(0));  // lands while layer 1 runs
 
     // ---- layer 1: h = relu(W1 x + b1) -> B operands hb[ct][k-step 0..7] ----
     bf16x8 hb[SG_NT][SG_DL / 16];
@@ -186,28 +226,26 @@ __global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const float *__restr
         const bf16x8 *w1 = (const bf16x8 *)h.w1;
 #pragma unroll
         for (int t = 0; t < SG_DL / 32; ++t) {
+            const f32x16 bb = sg_rows(h.b1, t, hh);  // the bias rides in as the accumulator
             f32x16 acc[SG_NT];
 #pragma unroll
-            for (int ct = 0; ct < SG_NT; ++ct) acc[ct] = sg_zero16();
+            for (int ct = 0; ct < SG_NT; ++ct) acc[ct] = bb;
 #pragma unroll
             for (int s = 0; s < SG_DR / 16; ++s) {
                 const bf16x8 a = w1[(t * (SG_DR / 16) + s) * 64 + lane];
 #pragma unroll
                 for (int ct = 0; ct < SG_NT; ++ct) acc[ct] = SG_MFMA(a, xb[ct][s], acc[ct]);
             }
-            const f32x16 bb = sg_rows(h.b1, t, hh);
 #pragma unroll
-            for (int ct = 0; ct < SG_NT; ++ct)
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    hb[ct][2 * t][j] = (__bf16)fmaxf(acc[ct][j] + bb[j], 0.f);
-                    hb[ct][2 * t + 1][j] = (__bf16)fmaxf(acc[ct][8 + j] + bb[8 + j], 0.f);
-                }
+            for (int ct = 0; ct < SG_NT; ++ct) {
+                hb[ct][2 * t] = sg_relu_b(acc[ct], 0);
+                hb[ct][2 * t + 1] = sg_relu_b(acc[ct], 1);
+            }
         }
     }
 
     // ---- n = max(|W2 h + b2|, 1e-12)  (F.normalize, dim_reduction.py:25) ----
-    float rinv[SG_NT], den[SG_NT];
+    float den[SG_NT];
     if (F8) {
         // h as fp8 B operands: k-step s (64 hidden), byte j of lane half hh = hidden
         // 32 (2 s + (j >> 4)) + (jj & 3) + 8 (jj >> 2) + 4 hh, jj = j & 15 -- the rows this
@@ -275,47 +313,40 @@ __global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const float *__restr
         for (int ct = 0; ct < SG_NT; ++ct) {
             const float tot = ss[ct] + __shfl_xor(ss[ct], 32);
             den[ct] = fmaxf(sqrtf(tot), 1e-12f);
-            rinv[ct] = 1.f / den[ct];
         }
     } else {
+        // Gram form: |e|^2 = sum_i h_i ((G h)_i + g2_i) + |b2|^2, G = W2^T W2 as bf16 hi + lo
+        // fragments (64 MFMAs per 32 points in place of the d_full x d_latent product's
+        // 192); the rows of G h land in the registers that hold the same rows of h
         float ss[SG_NT];
 #pragma unroll
         for (int ct = 0; ct < SG_NT; ++ct) ss[ct] = 0.f;
-        const uint8_t *w2 = (const uint8_t *)h.w2;  // tile t: 8 fragments at t * 8 KiB
-        auto src = [&](int t) { return [=](int i) { return w2 + (int64_t)t * 8192 + i * 1024; }; };
-        // tile t + 1 streams into the other LDS slot while tile t runs on the matrix cores
-        stage(0, 8, src(0));
-        f32x16 bb = sg_rows(h.b2, 0, hh);
-        for (int t = 0; t < T2; ++t) {
+#pragma unroll  // (h's registers are indexed by t)
+        for (int t = 0; t < SG_DL / 32; ++t) {
             landed();
-            if (t + 1 < T2) stage((t + 1) & 1, 8, src(t + 1));
-            const int tn = t + 1 < T2 ? t + 1 : t;
-            bf16x8 cur[SG_DL / 16];
+            if (t + 1 < SG_DL / 32) stage((t + 1) & 1, 16, gsrc(t + 1));
+            else if (SEG) stage(0, 12, msrc(0));  // the M loop's first tile
             const bf16x8 *sl = (const bf16x8 *)(sg_lds + (t & 1) * SG_SLOT);
-#pragma unroll
-            for (int q = 0; q < SG_DL / 16; ++q) cur[q] = sl[q * 64 + lane];
-            const f32x16 bbn = sg_rows(h.b2, tn, hh);
             f32x16 acc[SG_NT];
 #pragma unroll
             for (int ct = 0; ct < SG_NT; ++ct) acc[ct] = sg_zero16();
 #pragma unroll
-            for (int q = 0; q < SG_DL / 16; ++q)
+            for (int q = 0; q < 2 * (SG_DL / 16); ++q) {
+                const bf16x8 a = sl[q * 64 + lane];
 #pragma unroll
-                for (int ct = 0; ct < SG_NT; ++ct) acc[ct] = SG_MFMA(cur[q], hb[ct][q], acc[ct]);
+                for (int ct = 0; ct < SG_NT; ++ct) acc[ct] = SG_MFMA(a, hb[ct][q & 7], acc[ct]);
+            }
+            const f32x16 gg = sg_rows(h.g2, t, hh);
 #pragma unroll
             for (int ct = 0; ct < SG_NT; ++ct)
 #pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const float e = acc[ct][i] + bb[i];
-                    ss[ct] = fmaf(e, e, ss[ct]);
-                }
-            bb = bbn;
+                for (int i = 0; i < 16; ++i)
+                    ss[ct] = fmaf(sg_bf16_at(hb[ct][2 * t + (i >> 3)], i & 7), acc[ct][i] + gg[i], ss[ct]);
         }
 #pragma unroll
         for (int ct = 0; ct < SG_NT; ++ct) {
-            const float tot = ss[ct] + __shfl_xor(ss[ct], 32);
+            const float tot = fmaxf(ss[ct] + __shfl_xor(ss[ct], 32) + h.b2sq, 0.f);
             den[ct] = fmaxf(sqrtf(tot), 1e-12f);
-            rinv[ct] = 1.f / den[ct];
         }
     }
 
@@ -350,47 +381,40 @@ __global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const float *__restr
     }
     if (!SEG) return;
 
-    // ---- stego: linear path folded to L (64 x 128) ----
+    // ---- the stego code times n (a positive scale the k-means argmax ignores):
+    //      n stego = L h + Wl b2 + n (bl + bn2) + Wn2 relu(M h + Wn1 b2 + n bn1),
+    //      every bias entering as an MFMA accumulator init ----
+    // linear path folded to L (64 x 128)
     f32x16 sacc[SG_NT][SG_DC / 32];
     {
         const bf16x8 *wl = (const bf16x8 *)h.wl;
 #pragma unroll
         for (int rt = 0; rt < SG_DC / 32; ++rt) {
+            const f32x16 lb = sg_rows(h.bl, rt, hh);
+            const f32x16 ob = sg_rows(h.bo, rt, hh);
 #pragma unroll
-            for (int ct = 0; ct < SG_NT; ++ct) sacc[ct][rt] = sg_zero16();
+            for (int ct = 0; ct < SG_NT; ++ct)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) sacc[ct][rt][i] = fmaf(den[ct], ob[i], lb[i]);
 #pragma unroll
             for (int q = 0; q < SG_DL / 16; ++q) {
                 const bf16x8 a = wl[(rt * (SG_DL / 16) + q) * 64 + lane];
 #pragma unroll
                 for (int ct = 0; ct < SG_NT; ++ct) sacc[ct][rt] = SG_MFMA(a, hb[ct][q], sacc[ct][rt]);
             }
-            const f32x16 lb = sg_rows(h.bl, rt, hh);
-            const f32x16 ob = sg_rows(h.bo, rt, hh);
-#pragma unroll
-            for (int ct = 0; ct < SG_NT; ++ct)
-#pragma unroll
-                for (int i = 0; i < 16; ++i)
-                    sacc[ct][rt][i] = fmaf(sacc[ct][rt][i] + lb[i], rinv[ct], ob[i]);
         }
     }
-    // ---- stego: nonlinear path, u = relu((M h + Wn1 b2) / n + bn1) per 32-row tile,
-    //      consumed at once by Wn2 (64 x 768) ----
+    // nonlinear path, n u = relu(M h + Wn1 b2 + n bn1) per 32-row tile, consumed at once by
+    // Wn2 (64 x 768)
     {
-        const uint8_t *wm = (const uint8_t *)h.wm, *wn2 = (const uint8_t *)h.wn2;
-        const int KS = DF / 16;
-        // tile t: M fragments (t, 0..7) at t * 8 KiB, then Wn2 fragments (rt, 2 t + s)
-        auto src = [&](int t) {
-            return [=](int i) {
-                return i < 8 ? wm + (int64_t)t * 8192 + i * 1024
-                             : wn2 + ((int64_t)((i - 8) >> 1) * KS + 2 * t + ((i - 8) & 1)) * 1024;
-            };
-        };
-        landed();  // the norm loop's last slot is free
-        stage(0, 12, src(0));
+        if (F8) {  // (the Gram loop staged tile 0 already)
+            landed();  // the norm loop's last slot is free
+            stage(0, 12, msrc(0));
+        }
         f32x16 mb = sg_rows(h.bm, 0, hh), nb = sg_rows(h.bn1, 0, hh);
         for (int t = 0; t < T2; ++t) {
             landed();
-            if (t + 1 < T2) stage((t + 1) & 1, 12, src(t + 1));
+            if (t + 1 < T2) stage((t + 1) & 1, 12, msrc(t + 1));
             const int tn = t + 1 < T2 ? t + 1 : t;
             const bf16x8 *sl = (const bf16x8 *)(sg_lds + (t & 1) * SG_SLOT);
             bf16x8 cur[SG_DL / 16], cw[SG_DC / 32][2];
@@ -403,20 +427,19 @@ __global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const float *__restr
             const f32x16 mbn = sg_rows(h.bm, tn, hh), nbn = sg_rows(h.bn1, tn, hh);
             f32x16 acc[SG_NT];
 #pragma unroll
-            for (int ct = 0; ct < SG_NT; ++ct) acc[ct] = sg_zero16();
+            for (int ct = 0; ct < SG_NT; ++ct)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) acc[ct][i] = fmaf(den[ct], nb[i], mb[i]);
 #pragma unroll
             for (int q = 0; q < SG_DL / 16; ++q)
 #pragma unroll
                 for (int ct = 0; ct < SG_NT; ++ct) acc[ct] = SG_MFMA(cur[q], hb[ct][q], acc[ct]);
             bf16x8 ub[SG_NT][2];
 #pragma unroll
-            for (int ct = 0; ct < SG_NT; ++ct)
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    ub[ct][0][j] = (__bf16)fmaxf(fmaf(acc[ct][j] + mb[j], rinv[ct], nb[j]), 0.f);
-                    ub[ct][1][j] =
-                        (__bf16)fmaxf(fmaf(acc[ct][8 + j] + mb[8 + j], rinv[ct], nb[8 + j]), 0.f);
-                }
+            for (int ct = 0; ct < SG_NT; ++ct) {
+                ub[ct][0] = sg_relu_b(acc[ct], 0);
+                ub[ct][1] = sg_relu_b(acc[ct], 1);
+            }
 #pragma unroll
             for (int rt = 0; rt < SG_DC / 32; ++rt)
 #pragma unroll
@@ -429,8 +452,22 @@ __global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const float *__restr
         }
     }
 
-    // ---- cosine k-means: argmax_k <stego, c_k/|c_k|> in fp32 (first maximum wins,
-    //      as torch.argmax) -> pseudo_assignment ----
+    // ---- cosine k-means: argmax_k <n stego, c_k/|c_k|> (first maximum wins, as
+    //      torch.argmax) -> pseudo_assignment.  The scores as one MFMA tile per 32
+    //      clusters (rows) x 32 points: stego and the centres as bf16 hi + lo operands
+    //      (hi hi + hi lo + lo hi: fp32-grade scores) ----
+    bf16x8 shi[SG_NT][SG_DC / 16], slo[SG_NT][SG_DC / 16];
+#pragma unroll
+    for (int ct = 0; ct < SG_NT; ++ct)
+#pragma unroll
+        for (int q = 0; q < SG_DC / 16; ++q)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float v = sacc[ct][q >> 1][8 * (q & 1) + j];
+                const __bf16 hi = (__bf16)v;
+                shi[ct][q][j] = hi;
+                slo[ct][q][j] = (__bf16)(v - (float)hi);
+            }
     float best[SG_NT];
     int bi[SG_NT];
 #pragma unroll
@@ -438,22 +475,40 @@ __global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const float *__restr
         best[ct] = -INFINITY;
         bi[ct] = 0;
     }
-    for (int k = 0; k < h.n_clusters; ++k) {
-        const f32x16 c0 = sg_rows(h.centres, 2 * k + 0, hh);  // rows 0..31 (acc order)
-        const f32x16 c1 = sg_rows(h.centres, 2 * k + 1, hh);  // rows 32..63
+    const bf16x8 *wc = (const bf16x8 *)h.centres;  // [tile][hi, lo][k-step][64][8]
+    const int nct = (h.n_clusters + 31) >> 5;
+    for (int c = 0; c < nct; ++c) {
+        bf16x8 ah[SG_DC / 16], al[SG_DC / 16];
+#pragma unroll
+        for (int q = 0; q < SG_DC / 16; ++q) {
+            ah[q] = wc[((2 * c) * (SG_DC / 16) + q) * 64 + lane];
+            al[q] = wc[((2 * c + 1) * (SG_DC / 16) + q) * 64 + lane];
+        }
 #pragma unroll
         for (int ct = 0; ct < SG_NT; ++ct) {
-            float d = 0.f;
+            f32x16 acc = sg_zero16();
 #pragma unroll
-            for (int i = 0; i < 16; ++i) d = fmaf(c0[i], sacc[ct][0][i], d);
+            for (int q = 0; q < SG_DC / 16; ++q) {
+                acc = SG_MFMA(ah[q], shi[ct][q], acc);
+                acc = SG_MFMA(ah[q], slo[ct][q], acc);
+                acc = SG_MFMA(al[q], shi[ct][q], acc);
+            }
+            // this lane's rows in increasing cluster order; padding rows never win
 #pragma unroll
-            for (int i = 0; i < 16; ++i) d = fmaf(c1[i], sacc[ct][1][i], d);
-            d += __shfl_xor(d, 32);
-            if (d > best[ct]) {
-                best[ct] = d;
-                bi[ct] = k;
+            for (int i = 0; i < 16; ++i) {
+                const int k = 32 * c + 8 * (i >> 2) + 4 * hh + (i & 3);
+                if (k < h.n_clusters && acc[i] > best[ct]) {
+                    best[ct] = acc[i];
+                    bi[ct] = k;
+                }
             }
         }
+    }
+#pragma unroll
+    for (int ct = 0; ct < SG_NT; ++ct) {  // the two lane halves: larger score, then lower index
+        const float ob = __shfl_xor(best[ct], 32);
+        const int oi = __shfl_xor(bi[ct], 32);
+        if (ob > best[ct] || (ob == best[ct] && oi < bi[ct])) bi[ct] = oi;
     }
     if (hh == 0) {
 #pragma unroll
@@ -496,7 +551,7 @@ extern "C" int sd_voxel_points(const double *origin, double vox, int64_t nx, int
 }
 
 static int sg_valid(const sd_seg_head *h, int need_seg) {
-    if (!h || !h->w1 || !h->b1 || !h->w2 || !h->b2) return 0;
+    if (!h || !h->w1 || !h->b1 || !h->w2 || !h->b2 || !h->wg || !h->g2) return 0;
     if (h->d_in != SG_DR || h->d_latent != SG_DL || h->d_full <= 0 || h->d_full % 32 ||
         h->d_full > 4096)
         return 0;

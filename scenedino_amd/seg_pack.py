@@ -9,6 +9,10 @@ Folding (exact algebra, done once here in fp64):
     L  = Wl  @ W2   (d_code x d_latent)      bl_f = Wl  @ b2
     M  = Wn1 @ W2   (d_full x d_latent)      bm   = Wn1 @ b2
     bo = bl + bn2
+    G  = W2^T W2    (d_latent x d_latent)    g2 = 2 W2^T b2,  b2sq = |b2|^2
+(|W2 h + b2|^2 = h^T G h + g2.h + b2sq: the norm without the d_full x d_latent product;
+G rides as bf16 hi + lo fragments so the quadratic form does not lose the cancellation
+between W2 h and b2 to G's rounding)
 where W2, b2 = linear_out; Wl, bl = linear_path[0]; Wn1, bn1 = nonlinear_path[0];
 Wn2, bn2 = nonlinear_path[2] (1x1 convolutions viewed as matrices).
 
@@ -19,7 +23,8 @@ accumulator register i of lane half h holds row (i & 3) + 8 (i >> 2) + 4 h):
                 perm(q, h, j)  = 32 (q >> 1) + 16 (q & 1) + 8 (j >> 2) + 4 h + (j & 3)
                 (inputs that are accumulator tiles converted in place: W2, L, M, Wn2)
   row vectors : v[t][h][i]     = vec[32 t + (i & 3) + 8 (i >> 2) + 4 h]
-  centres     : c[k][rt][h][i] = C_norm[k][32 rt + (i & 3) + 8 (i >> 2) + 4 h]
+  centres     : c[k][rt][h][i] = C_norm[k][32 rt + (i & 3) + 8 (i >> 2) + 4 h]  (f32, emulation)
+  wc (record) : the centres as permuted-k A fragments, hi and lo bf16 halves per 32-row tile
 """
 from __future__ import annotations
 
@@ -127,12 +132,18 @@ class PackedSegHead:
         self.w2 = _frag_permuted(W2).to(bf).contiguous()
         self.b2 = b2[_accrow(d_full // 32, dev)].to(fdt).contiguous()
         self.d_in, self.d_latent, self.d_full = d_in, d_latent, d_full
+        G = W2.t() @ W2
+        Ghi = G.to(bf).double()
+        self.wg = torch.cat([_frag_permuted(Ghi), _frag_permuted(G - Ghi)], 1).to(bf).contiguous()
+        self.g2 = (2 * (W2.t() @ b2))[_accrow(d_latent // 32, dev)].to(fdt).contiguous()
+        self.b2sq = float(b2 @ b2)
         self.seg = stego_head is not None and cluster_head is not None
         null = None
         fields = dict(w1=self.w1.data_ptr(), b1=self.b1.data_ptr(), w2=self.w2.data_ptr(),
                       b2=self.b2.data_ptr(), wl=null, bl=null, bo=null, wm=null, bm=null,
                       bn1=null, wn2=null, centres=null, assign=null, n_clusters=0,
-                      d_in=d_in, d_latent=d_latent, d_full=d_full, d_code=0)
+                      d_in=d_in, d_latent=d_latent, d_full=d_full, d_code=0,
+                      wg=self.wg.data_ptr(), g2=self.g2.data_ptr(), b2sq=self.b2sq)
         if self.seg:
             lin = stego_head.linear_path[0]
             nl0, nl2 = stego_head.nonlinear_path[0], stego_head.nonlinear_path[2]
@@ -159,12 +170,19 @@ class PackedSegHead:
             if cn.shape[1] != d_code or not 1 <= n_cl <= 256:
                 raise NotImplementedError("cluster centres must be (1..256, 64)")
             self.centres = cn[:, _accrow(d_code // 32, dev)].contiguous()  # (k, rt, h, 16)
+            # the kernel's copy: hi + lo bf16 A fragments, rows = clusters (zero-padded to
+            # 32 per tile), [tile][hi, lo][k-step][64][8] in the permuted k order
+            nct = (n_cl + 31) // 32
+            cpad = torch.zeros(32 * nct, d_code, dtype=torch.float64, device=dev)
+            cpad[:n_cl] = cn.double()
+            chi = cpad.to(bf).double()
+            self.wc = torch.stack([_frag_permuted(chi), _frag_permuted(cpad - chi)], 1).to(bf).contiguous()
             self.assign = cluster_head.pseudo_assignment.detach().to(dev, torch.int32).contiguous()
             if self.assign.numel() != n_cl:
                 raise ValueError("pseudo_assignment must have one entry per cluster")
             fields.update(wl=self.wl.data_ptr(), bl=self.bl.data_ptr(), bo=self.bo.data_ptr(),
                           wm=self.wm.data_ptr(), bm=self.bm.data_ptr(), bn1=self.bn1.data_ptr(),
-                          wn2=self.wn2.data_ptr(), centres=self.centres.data_ptr(),
+                          wn2=self.wn2.data_ptr(), centres=self.wc.data_ptr(),
                           assign=self.assign.data_ptr(), n_clusters=n_cl, d_code=d_code)
             self.n_clusters, self.d_code = n_cl, d_code
         self.fp8 = bool(fp8)

@@ -153,25 +153,30 @@ def _emulate(pk, x, fp8=False):
     if fp8:
         n = _norm_fp8(pk, regs_h).unsqueeze(1)
     else:
+        # Gram form: |e|^2 = sum_i h_i ((G h)_i + g2_i) + |b2|^2 (hi + lo G fragments)
         ss = torch.zeros(64, dtype=torch.float64)
-        for t in range(T2):
-            e = _to_regs(sum(_mfma(pk.w2[t, q], hb[q]) for q in range(8))) + pk.b2[t].repeat_interleave(32, 0)
-            ss += (e * e).sum(1)
-        n = (ss[:32] + ss[32:]).sqrt().clamp_min(1e-12).repeat(2).unsqueeze(1)
+        for t in range(4):
+            gh = _to_regs(sum(_mfma(pk.wg[t, q], hb[q % 8]) for q in range(16)))
+            ss += (regs_h[t] * (gh + pk.g2[t].repeat_interleave(32, 0))).sum(1)
+        n = (ss[:32] + ss[32:] + pk.b2sq).clamp_min(0).sqrt().clamp_min(1e-12).repeat(2).unsqueeze(1)
+    # n stego: biases as accumulator inits, n u = relu(M h + Wn1 b2 + n bn1)
     sacc = []
     for rt in range(2):
         a = _to_regs(sum(_mfma(pk.wl[rt, q], hb[q]) for q in range(8)))
-        sacc.append((a + pk.bl[rt].repeat_interleave(32, 0)) / n + pk.bo[rt].repeat_interleave(32, 0))
+        sacc.append(a + pk.bl[rt].repeat_interleave(32, 0) + n * pk.bo[rt].repeat_interleave(32, 0))
     for t in range(T2):
         v = _to_regs(sum(_mfma(pk.wm[t, q], hb[q]) for q in range(8)))
-        u = torch.relu((v + pk.bm[t].repeat_interleave(32, 0)) / n + pk.bn1[t].repeat_interleave(32, 0))
+        u = torch.relu(v + pk.bm[t].repeat_interleave(32, 0) + n * pk.bn1[t].repeat_interleave(32, 0))
         for rt in range(2):
             sacc[rt] = sacc[rt] + _to_regs(sum(_mfma(pk.wn2[rt, 2 * t + s], B(u, s)) for s in range(2)))
+    # scores: one MFMA tile per 32 clusters from the record's centre fragments (hi + lo)
+    sb = [B(sacc[q >> 1], q & 1) for q in range(4)]
     scores = []
-    for k in range(pk.n_clusters):
-        d = sum((pk.centres[k, rt].repeat_interleave(32, 0) * sacc[rt]).sum(1) for rt in range(2))
-        scores.append(d[:32] + d[32:])
-    return torch.stack(scores, 1)
+    for c in range(pk.wc.shape[0]):
+        acc = sum(_mfma(pk.wc[c, 0, q] + pk.wc[c, 1, q], sb[q]) for q in range(4))  # (32 cl, 32 pts)
+        scores.append(acc.t())
+    scores = torch.cat(scores, 1)[:, :pk.n_clusters]
+    return scores
 
 
 def test_packed_fragments_emulate_reference_chain():
@@ -191,6 +196,51 @@ def test_packed_fragments_emulate_reference_chain():
     assert torch.allclose(got_dir, ref_dir, atol=1e-9)
     got_labels = pd["assign"][scores.argmax(1)]
     assert (got_labels == labels).all()
+
+
+def test_gram_norm_hi_lo_keeps_cancellation():
+    """The bf16 record's norm |W2 h + b2| is the Gram form h^T G h + g2.h + |b2|^2 with
+    G = W2^T W2 as bf16 hi + lo fragments: emulated from the packed bf16 record it stays
+    within 1e-4 of the exact norm even when b2 cancels 90 % of W2 h (a single bf16 G would
+    not: its rounding error scales with |W2 h|^2 / |e|^2)."""
+    from scenedino_amd.seg_pack import PackedSegHead
+    g = torch.Generator().manual_seed(5)
+    dr = torch.nn.Module()
+    dr.linear_in = torch.nn.Linear(64, 128)
+    dr.linear_out = torch.nn.Linear(128, 768)
+    with torch.no_grad():
+        for p_ in (dr.linear_in.weight, dr.linear_out.weight):
+            p_.copy_(torch.randn(p_.shape, generator=g) / p_.shape[1] ** 0.5)
+        dr.linear_in.bias.copy_(torch.rand(128, generator=g) * 0.5)
+        x0 = torch.randn(64, generator=g)
+        h0 = torch.relu(dr.linear_in.weight @ x0 + dr.linear_in.bias)
+        dr.linear_out.bias.copy_(-0.9 * (dr.linear_out.weight @ h0))
+    pk = PackedSegHead(dr)
+    x = x0 + 0.05 * torch.randn(32, 64, generator=g)
+    W1, b1 = dr.linear_in.weight.double(), dr.linear_in.bias.double()
+    W2, b2 = dr.linear_out.weight.double(), dr.linear_out.bias.double()
+    h = torch.relu(x.double() @ W1.t() + b1).to(torch.bfloat16).double()  # the kernel's h
+    exact = (h @ W2.t() + b2).norm(dim=1)
+    assert (exact / (h @ W2.t()).norm(dim=1)).max() < 0.2  # the cancellation is real
+    # G h from the packed fragments: undo the permuted k order (seg_pack._frag_permuted)
+    wg = pk.wg.double()
+    acc = torch.zeros(32, 128, dtype=torch.float64)
+    for t in range(4):
+        for q in range(16):
+            l = torch.arange(64).view(-1, 1)
+            j = torch.arange(8).view(1, -1)
+            qq = q % 8
+            cols = 32 * (qq >> 1) + 16 * (qq & 1) + 8 * (j >> 2) + 4 * (l >> 5) + (j & 3)
+            A = wg[t, q]                                              # (64, 8)
+            for lane_h in range(2):
+                Ar = A[32 * lane_h:32 * lane_h + 32]                  # rows 32 t + r
+                c = cols[32 * lane_h:32 * lane_h + 32]
+                acc[:, 32 * t:32 * t + 32] += h[:, c[0]] @ Ar.t()
+    g2 = torch.zeros(128, dtype=torch.float64)
+    from scenedino_amd.seg_pack import _accrow
+    g2[_accrow(4, "cpu").reshape(-1)] = pk.g2.double().reshape(-1)
+    got = ((h * (acc + g2)).sum(1) + pk.b2sq).sqrt()
+    assert ((got - exact).abs() / exact).max() < 1e-4
 
 
 @pytest.mark.parametrize("d_full", [768, 384])
@@ -262,7 +312,7 @@ def test_voxel_points_ragged_dims(gpu):
         assert (got == ref).all(), dims
 
 
-def _label_check(labels, ref_scores, ref_labels, what):
+def _label_check(labels, ref_scores, ref_labels, what, min_agree=0.99):
     top2 = ref_scores.topk(2, dim=1).values
     margin = (top2[:, 0] - top2[:, 1]).numpy()
     labels = np.asarray(labels)
@@ -271,7 +321,7 @@ def _label_check(labels, ref_scores, ref_labels, what):
     assert (labels[sure] == ref_labels[sure]).all(), f"{what}: clear-margin label mismatch"
     agree = (labels == ref_labels).mean()
     print(f"{what}: label agreement {agree:.4f}")
-    assert agree >= 0.99, f"{what}: label agreement {agree:.4f}"
+    assert agree >= min_agree, f"{what}: label agreement {agree:.4f}"
 
 
 @pytest.mark.gpu
@@ -329,6 +379,43 @@ def test_seg_query_fp8_vs_reference(gpu, d_full):
     _, _, full8 = _lib.seg_query(x, pk.rec, want_labels=True, want_full=True)
     _, _, full16 = _lib.seg_query(x, PackedSegHead(dr, st, cl).rec, want_labels=True, want_full=True)
     assert torch.equal(full8, full16)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_cl", [1, 5, 33, 70])
+def test_seg_query_cluster_counts_and_ties(gpu, n_cl):
+    """The scores as MFMA tiles of 32 clusters: 1, 5, 33 and 70 clusters (zero-padded
+    tiles never win), an exact duplicate centre (a tie: the first index wins, as
+    torch.argmax), labels equal to the reference chain's wherever its top-2 margin exceeds
+    2e-2."""
+    from scenedino_amd import _lib
+    from scenedino_amd.seg_pack import PackedSegHead
+    from scenedino_amd.downstream_head import KMeansParamHead
+    d = load("seg_head.npz")
+    p = seg_params(d, "_768")
+    dr, st, _ = modules_from(p)
+    g = torch.Generator().manual_seed(n_cl)
+    cl = KMeansParamHead(n_cl, 19, 64)
+    with torch.no_grad():
+        cl.cluster_centers.copy_(torch.randn(n_cl, 64, generator=g))
+        if n_cl > 2:
+            cl.cluster_centers[n_cl - 1] = cl.cluster_centers[1]
+        cl.pseudo_assignment.copy_(torch.arange(n_cl))  # labels = cluster indices
+    pk = PackedSegHead(dr.to(gpu), st.to(gpu), cl.to(gpu))
+    x = torch.as_tensor(d["x_768"]).to(gpu)
+    labels, _, _ = _lib.seg_query(x, pk.rec, want_labels=True)
+    labels = labels.cpu().long()
+    pr = dict(p, centres=cl.cluster_centers.detach().cpu(), assign=torch.arange(n_cl))
+    _, ref_scores, ref_labels = SO.seg_head(torch.as_tensor(d["x_768"]), pr)
+    assert labels.min() >= 0 and labels.max() < n_cl
+    if n_cl > 2:
+        assert not (labels == n_cl - 1).any()  # the duplicate of centre 1 never wins
+    if n_cl == 1:
+        assert (labels == 0).all()
+    else:
+        # random centres leave many points within 2e-2 of a tie (the bf16 M / Wn2 chain
+        # moves those; measured 96 % agreement at 5 clusters): exact on clear margins
+        _label_check(labels, ref_scores, ref_labels, f"{n_cl} clusters", min_agree=0.9)
 
 
 @pytest.mark.gpu
