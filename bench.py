@@ -266,7 +266,11 @@ def _traffic_from_profile(pose):
 
 
 SEG_FLOPS_ALGO = 2 * (64 * 128 + 128 * 768) + 2 * (768 * 64 + 768 * 768 + 768 * 64) + 2 * 19 * 64
-SEG_FLOPS_EXEC = 2 * (64 * 128 + 2 * 768 * 128 + 64 * 128 + 64 * 768)
+# executed MFMA work per voxel: W1, the Gram norm (G = W2^T W2 as hi + lo), L, M, Wn2 and
+# the k-means tile (32 clusters x 64, three hi/lo products); the fp8 record's norm is the
+# 768 x 128 W2 product instead of the Gram form
+SEG_FLOPS_EXEC = 2 * (64 * 128 + 2 * 128 * 128 + 64 * 128 + 768 * 128 + 64 * 768 + 3 * 32 * 64)
+SEG_FLOPS_EXEC_FP8 = SEG_FLOPS_EXEC - 2 * 2 * 128 * 128 + 2 * 768 * 128
 
 
 def main_c5(args, world, rank, local_rank, dist, device, host_stage=False):
@@ -336,7 +340,7 @@ def main_c5(args, world, rank, local_rank, dist, device, host_stage=False):
             x0, x1 = sscbench.slab_range(dims[0], rank, world)
             n_launch = (min(x1 + 1, dims[0]) - max(x0 - 1, 0)) * dims[1] * dims[2]
         algo = n_launch * SEG_FLOPS_ALGO
-        exe = n_launch * SEG_FLOPS_EXEC
+        exe = n_launch * (SEG_FLOPS_EXEC_FP8 if seg_fp8 else SEG_FLOPS_EXEC)
         line = {
             "metric": "SSCBench voxel-grid query, voxels/sec (256x256x32 grid per frame)",
             "value": n_vox * args.steps / elapsed, "unit": "voxels/s", "n_gpus": world,

@@ -32,8 +32,8 @@
 // Work unit: one wave = SG_NT x 32 points (lane = point, as the accumulator columns of
 // v_mfma_f32_32x32x16_bf16); weights are the MFMA A operands (rows = output features),
 // 1-KiB fragments (each feeds SG_NT MFMAs).  The big products (Gram, M + Wn2) stream their
-// weight tiles through LDS, double-buffered and shared by the workgroup's 8 waves
-// (2 per SIMD); the small ones (W1, L) read their fragments from L2.  Hidden vectors
+// weight tiles through LDS, in a ring of slots shared by the workgroup's 4 waves
+// (one per SIMD, two workgroups per CU); the small ones (W1, L) read their fragments from L2.  Hidden vectors
 // never leave the registers: an accumulator tile is converted in place into the B operand
 // of the next product (k order permuted; the host packs the A operands to match, see
 // scenedino_amd/seg_pack.py).
@@ -44,8 +44,12 @@ extern "C" void sd_set_error(const char *msg);
 #ifndef SG_NT
 #define SG_NT 2        // 32-point column tiles per wave (2: 2 waves per SIMD, measured -11 % vs 4)
 #endif
+#ifndef SG_EXP
+#define SG_EXP 0       // timing experiments only, wrong results: 1 no waits, 2 no vmcnt, 3 no DMA, 4 no barrier
+#endif
 #ifndef SG_WAVES
-#define SG_WAVES 8     // waves per workgroup (two per SIMD), sharing the LDS weight stream
+#define SG_WAVES 4     // waves per workgroup sharing the LDS weight stream (two workgroups per
+                       // CU drift apart: one's HBM input phase overlaps the other's MFMAs; -6 %)
 #endif
 #define SG_DR 64       // reduced DINO dims (MlpDimReduction reduced_channels)
 #define SG_DL 128      // latent dims (MlpDimReduction latent_channels)
@@ -148,11 +152,36 @@ __device__ __forceinline__ bf16x8 sg_relu_b(const f32x16 &acc, int s) {
 // to read every fragment from L2 itself): 1-KiB pieces by LDS-DMA, issued as inline asm so
 // that the compiler does not fence every LDS read behind the DMA (m0 = LDS destination).
 #define SG_SLOT (16 * 1024)  // one tile: 16 Gram fragments, 8 M + 4 Wn2 fragments or 4 KiB fp8
+#define SG_NSLOT 3          // LDS slots (the M loop runs three deep)
 __device__ __forceinline__ void sg_dma1k(const uint8_t *src, uint32_t lds_dst, int lane) {
     lds_dst = __builtin_amdgcn_readfirstlane(lds_dst);
     asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
                  :: "v"(src + lane * 16), "s"(lds_dst) : "memory");
 }
+
+// diagnostic build only (SG_PROF=1): per-phase s_memtime cycles summed over all waves
+#ifndef SG_PROF
+#define SG_PROF 0
+#endif
+#if SG_PROF
+__device__ unsigned long long sg_prof[16];
+#define SG_T(i)                                            \
+    {                                                      \
+        const uint64_t _t = __builtin_amdgcn_s_memtime();  \
+        pacc[i] += (uint32_t)(_t - tlast);                 \
+        tlast = _t;                                        \
+    }
+extern "C" int sd_seg_prof(unsigned long long *out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(sg_prof), sizeof(sg_prof)) != hipSuccess) return -2;
+    if (reset) {
+        unsigned long long z[16] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(sg_prof), z, sizeof(z)) != hipSuccess) return -2;
+    }
+    return 0;
+}
+#else
+#define SG_T(i)
+#endif
 
 // MODE bit 0: write dino_full (transform_expand output); bit 1: segmentation head.
 // F8 (labels / seg only): the norm product |W2 h + b2| on fp8 MFMA -- h quantised to e4m3
@@ -169,22 +198,38 @@ __global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const float *__restr
     constexpr bool FULL = MODE & 1;
     constexpr bool SEG = MODE & 2;
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int r = lane & 31, hh = lane >> 5;
     const int64_t base = ((int64_t)blockIdx.x * SG_WAVES + wave) * (32 * SG_NT);
     // workgroup-uniform exit only: the weight stream below has barriers (waves past P run
     // on zero inputs and store nothing)
     if ((int64_t)blockIdx.x * SG_WAVES * (32 * SG_NT) >= P) return;
     const int T2 = DF / 32;
+#if SG_PROF
+    uint32_t pacc[10] = {};
+    uint64_t tlast = __builtin_amdgcn_s_memtime();
+#endif
     extern __shared__ __attribute__((aligned(16))) uint8_t sg_lds[];
     const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void *)sg_lds;
     // stage tile pieces [0, n) (1 KiB each, piece i from src(i)) into slot; wave w issues w, w + 4, ...
     auto stage = [&](int slot, int n, auto src) {
-        for (int i = wave; i < n; i += SG_WAVES) sg_dma1k(src(i), lds0 + slot * SG_SLOT + i * 1024, lane);
+#if SG_EXP != 3
+        // every wave issues the same count (no branch: the loops stay one basic block);
+        // a wave past the last piece re-copies an earlier one (the same bytes)
+#pragma unroll
+        for (int k = 0; k < (n + SG_WAVES - 1) / SG_WAVES; ++k) {
+            const int i = (wave + k * SG_WAVES) % n;
+            sg_dma1k(src(i), lds0 + slot * SG_SLOT + i * 1024, lane);
+        }
+#endif
     };
     auto landed = [&]() {  // this wave's DMA done, then every wave's (and the previous slot free)
+#if SG_EXP != 1 && SG_EXP != 2
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+#if SG_EXP != 1 && SG_EXP != 4
         __syncthreads();
+#endif
     };
     // Gram tile t: 16 fragments at t * 16 KiB
     auto gsrc = [&](int t) { return [=](int i) { return (const uint8_t *)h.wg + (int64_t)t * 16384 + i * 1024; }; };
@@ -197,6 +242,13 @@ __global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const float *__restr
         };
     };
     if (!F8) stage(0, 16, gsrc(0));  // lands while layer 1 runs
+    // the M loop's bias rows (Wn1 b2, bn1; accumulator-row order) in LDS after the slots
+    const float *lds_b = (const float *)(sg_lds + SG_NSLOT * SG_SLOT);
+    if (SEG) {
+        f32x4_t *d = (f32x4_t *)(sg_lds + SG_NSLOT * SG_SLOT);
+        for (int i = threadIdx.x; i < DF / 2; i += SG_WAVES * 64)
+            d[i] = i < DF / 4 ? ((const f32x4_t *)h.bm)[i] : ((const f32x4_t *)h.bn1)[i - DF / 4];
+    }
 
     // ---- layer 1: h = relu(W1 x + b1) -> B operands hb[ct][k-step 0..7] ----
     bf16x8 hb[SG_NT][SG_DL / 16];
@@ -244,6 +296,7 @@ __global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const float *__restr
         }
     }
 
+    SG_T(0);
     // ---- n = max(|W2 h + b2|, 1e-12)  (F.normalize, dim_reduction.py:25) ----
     float den[SG_NT];
     if (F8) {
@@ -350,6 +403,7 @@ __global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const float *__restr
         }
     }
 
+    SG_T(1);
     if (FULL) {  // dino_full = e / n, recomputed with n known (one store per element)
         const bf16x8 *w2 = (const bf16x8 *)h.w2;
         for (int t = 0; t < T2; ++t) {
@@ -404,36 +458,33 @@ __global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const float *__restr
             }
         }
     }
+    SG_T(2);
     // nonlinear path, n u = relu(M h + Wn1 b2 + n bn1) per 32-row tile, consumed at once by
-    // Wn2 (64 x 768)
+    // Wn2 (64 x 768).  Software-pipelined: tile t + 1's M product is issued before tile
+    // t's ReLU epilogue and Wn2 product, so the matrix cores stay fed while the epilogue
+    // runs; three LDS slots (tile t + 2 streams into the slot tile t - 1 left)
     {
         if (F8) {  // (the Gram loop staged tile 0 already)
             landed();  // the norm loop's last slot is free
             stage(0, 12, msrc(0));
         }
-        f32x16 mb = sg_rows(h.bm, 0, hh), nb = sg_rows(h.bn1, 0, hh);
-        for (int t = 0; t < T2; ++t) {
-            landed();
-            if (t + 1 < T2) stage((t + 1) & 1, 12, msrc(t + 1));
-            const int tn = t + 1 < T2 ? t + 1 : t;
-            const bf16x8 *sl = (const bf16x8 *)(sg_lds + (t & 1) * SG_SLOT);
-            bf16x8 cur[SG_DL / 16], cw[SG_DC / 32][2];
+        auto m_issue = [&](int t, f32x16 *acc) {  // tile t (slot t mod 3) into acc
+            const f32x16 mbv = sg_rows(lds_b, t, hh), nbv = sg_rows(lds_b + DF, t, hh);
+            const bf16x8 *sl = (const bf16x8 *)(sg_lds + (t % 3) * SG_SLOT);
+            bf16x8 cur[SG_DL / 16];
 #pragma unroll
             for (int q = 0; q < SG_DL / 16; ++q) cur[q] = sl[q * 64 + lane];
 #pragma unroll
-            for (int rt = 0; rt < SG_DC / 32; ++rt)
-#pragma unroll
-                for (int s2 = 0; s2 < 2; ++s2) cw[rt][s2] = sl[(8 + 2 * rt + s2) * 64 + lane];
-            const f32x16 mbn = sg_rows(h.bm, tn, hh), nbn = sg_rows(h.bn1, tn, hh);
-            f32x16 acc[SG_NT];
-#pragma unroll
             for (int ct = 0; ct < SG_NT; ++ct)
 #pragma unroll
-                for (int i = 0; i < 16; ++i) acc[ct][i] = fmaf(den[ct], nb[i], mb[i]);
+                for (int i = 0; i < 16; ++i) acc[ct][i] = fmaf(den[ct], nbv[i], mbv[i]);
 #pragma unroll
             for (int q = 0; q < SG_DL / 16; ++q)
 #pragma unroll
                 for (int ct = 0; ct < SG_NT; ++ct) acc[ct] = SG_MFMA(cur[q], hb[ct][q], acc[ct]);
+        };
+        auto m_finish = [&](int t, const f32x16 *acc) {  // relu + Wn2 of tile t
+            const bf16x8 *sl = (const bf16x8 *)(sg_lds + (t % 3) * SG_SLOT);
             bf16x8 ub[SG_NT][2];
 #pragma unroll
             for (int ct = 0; ct < SG_NT; ++ct) {
@@ -443,14 +494,35 @@ __global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const float *__restr
 #pragma unroll
             for (int rt = 0; rt < SG_DC / 32; ++rt)
 #pragma unroll
-                for (int s = 0; s < 2; ++s)
+                for (int s = 0; s < 2; ++s) {
+                    const bf16x8 cw = sl[(8 + 2 * rt + s) * 64 + lane];
 #pragma unroll
-                    for (int ct = 0; ct < SG_NT; ++ct)
-                        sacc[ct][rt] = SG_MFMA(cw[rt][s], ub[ct][s], sacc[ct][rt]);
-            mb = mbn;
-            nb = nbn;
+                    for (int ct = 0; ct < SG_NT; ++ct) sacc[ct][rt] = SG_MFMA(cw, ub[ct][s], sacc[ct][rt]);
+                }
+        };
+        f32x16 acc[SG_NT];
+        landed();  // tile 0 in slot 0; every wave is past the norm loop
+        stage(1 % T2, 12, msrc(1 % T2));
+        m_issue(0, acc);
+        for (int t = 0; t + 1 < T2; ++t) {  // (branch-free body; the last tile is peeled)
+            SG_T(3);
+            landed();  // tile t + 1 landed; every wave is done with tile t - 1's slot
+            SG_T(4);
+            // tile t + 2 (past the end: tile T2 - 1 again, into the spare slot)
+            const int t2 = t + 2 < T2 ? t + 2 : T2 - 1;
+            stage((t + 2) % 3, 12, msrc(t2));
+            f32x16 accn[SG_NT];
+            m_issue(t + 1, accn);
+            SG_T(5);
+            m_finish(t, acc);
+            SG_T(6);
+#pragma unroll
+            for (int ct = 0; ct < SG_NT; ++ct) acc[ct] = accn[ct];
         }
+        m_finish(T2 - 1, acc);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the spare slot's DMA (LDS lives on)
     }
+    SG_T(3);
 
     // ---- cosine k-means: argmax_k <n stego, c_k/|c_k|> (first maximum wins, as
     //      torch.argmax) -> pseudo_assignment.  The scores as one MFMA tile per 32
@@ -510,6 +582,11 @@ __global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const float *__restr
         const int oi = __shfl_xor(bi[ct], 32);
         if (ob > best[ct] || (ob == best[ct] && oi < bi[ct])) bi[ct] = oi;
     }
+    SG_T(7);
+#if SG_PROF
+    if (lane < 10) atomicAdd(&sg_prof[lane], (unsigned long long)pacc[lane]);
+    if (lane == 0) atomicAdd(&sg_prof[15], 1ull);
+#endif
     if (hh == 0) {
 #pragma unroll
         for (int ct = 0; ct < SG_NT; ++ct) {
@@ -583,11 +660,12 @@ extern "C" int sd_seg_query(const float *dino, int64_t P, const sd_seg_head *h,
     }
     const float neg_vox = -voxel_size;
     hipStream_t s = (hipStream_t)stream;
+    const size_t lds_bytes = (size_t)SG_NSLOT * SG_SLOT + (want_seg ? 8 * (size_t)h->d_full : 0);
     const int mode = (dino_full ? 1 : 0) | (want_seg ? 2 : 0);
     // fp8 norm only for the labels / seg outputs (dino_full is the bf16 expansion)
     const bool f8 = h->w2_f8 != nullptr && mode == 2;
 #define SG_LAUNCH(M, F)                                                                            \
-    hipLaunchKernelGGL((k_seg_head<M, F>), dim3((unsigned)nblk), dim3(SG_WAVES * 64), 2 * SG_SLOT, s, dino, P, \
+    hipLaunchKernelGGL((k_seg_head<M, F>), dim3((unsigned)nblk), dim3(SG_WAVES * 64), lds_bytes, s, dino, P, \
                        h->d_full, sigma, neg_vox, *h, labels, seg, dino_full)
     switch (mode) {
     case 1: SG_LAUNCH(1, false); break;
