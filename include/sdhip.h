@@ -230,6 +230,9 @@ typedef struct sd_field_args {
     float *rgb;        /* (B, P, 3 nv) or NULL */
     float *invalid;    /* (B, P, nv) or NULL   */
     uint8_t *invalid_f;/* (B, P) or NULL       */
+    int32_t dino_dtype;/* SD_F32 (0), or SD_BF16: dino written as bf16 (the input a
+                        * following sd_seg_query rounds to bf16 anyway: half the bytes) */
+    int32_t pad0;
 } sd_field_args;
 
 int sd_field_query(const sd_field_args *args, const sd_mlp *mlp, void *stream);
@@ -331,7 +334,8 @@ typedef struct sd_seg_head {
     int32_t pad1;
 } sd_seg_head;
 
-/* Per-point segmentation head on P DINO codes dino (P, d_in) f32.
+/* Per-point segmentation head on P DINO codes dino (P, d_in), SD_F32 or SD_BF16 (16-B
+ * aligned; the kernel's first MFMA takes them as bf16 either way).
  * Replaces BTSNet.forward(predict_segmentation=True)'s encoder.expand_dim +
  * downstream_head(..., "stego_kmeans") (bts.py:584-592, dim_reduction.py:22-25,
  * semantic_head.py:107-111,285-373) and, with seg, the SSCBench alpha-weighted class pick
@@ -341,9 +345,9 @@ typedef struct sd_seg_head {
  *                        (needs sigma (P) f32)
  *   dino_full (P, d_full) f32  transform_expand output (L2-normalised)
  * At least one output; labels/seg need the stego fields of h. */
-int sd_seg_query(const float *dino, int64_t P, const sd_seg_head *h, const float *sigma,
-                float voxel_size, int32_t *labels, uint8_t *seg, float *dino_full,
-                void *stream);
+int sd_seg_query(const void *dino, int32_t dino_dtype, int64_t P, const sd_seg_head *h,
+                 const float *sigma, float voxel_size, int32_t *labels, uint8_t *seg,
+                 float *dino_full, void *stream);
 
 /* ---- DINO / DINOv2 ViT encoder (sdhip_vit.hip) -------------------------------
  * Replaces timm's VisionTransformer forward as the reference runs it

@@ -70,6 +70,7 @@ class SdFieldArgs(ctypes.Structure):
         ("img", _vp), ("nv", _i32), ("Hc", _i32), ("Wc", _i32),
         ("cam_c", _vp),
         ("sigma", _vp), ("dino", _vp), ("rgb", _vp), ("invalid", _vp), ("invalid_f", _vp),
+        ("dino_dtype", _i32), ("pad0", _i32),
     ]
 
 
@@ -179,8 +180,8 @@ SIGNATURES = {
                      _vp],
     "sd_voxel_points": [ctypes.POINTER(ctypes.c_double), ctypes.c_double, _i64, _i64, _i64,
                         ctypes.POINTER(ctypes.c_double), _vp, _vp],
-    "sd_seg_query": [_vp, _i64, ctypes.POINTER(SdSegHead), _vp, ctypes.c_float, _vp, _vp, _vp,
-                     _vp],
+    "sd_seg_query": [_vp, _i32, _i64, ctypes.POINTER(SdSegHead), _vp, ctypes.c_float, _vp, _vp,
+                     _vp, _vp],
     "sd_voxel_fov": [ctypes.POINTER(ctypes.c_double), ctypes.c_double, _i64, _i64, _i64,
                      ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), _i32, _i32,
                      _vp, _vp],
@@ -455,10 +456,12 @@ def voxel_points(origin, voxel_size, dims, T, device):
 
 def seg_query(dino, rec: SdSegHead, sigma=None, voxel_size=0.2, want_labels=True,
               want_seg=False, want_full=False):
-    """Folded transform_expand + stego k-means head (sd_seg_query) on dino (P, 64) f32.
-    Returns (labels int32 (P) | None, seg uint8 (P) | None, dino_full (P, d_full) | None)."""
+    """Folded transform_expand + stego k-means head (sd_seg_query) on dino (P, 64) f32 or
+    bf16.  Returns (labels int32 (P) | None, seg uint8 (P) | None, dino_full (P, d_full) |
+    None)."""
     lib = load()
-    _req(dino, "dino")
+    dt = SD_BF16 if dino.dtype == torch.bfloat16 else SD_F32
+    _req(dino, "dino", torch.bfloat16 if dt == SD_BF16 else torch.float32)
     P = dino.shape[0]
     dev = dino.device
     labels = torch.empty(P, device=dev, dtype=torch.int32) if want_labels else None
@@ -468,7 +471,7 @@ def seg_query(dino, rec: SdSegHead, sigma=None, voxel_size=0.2, want_labels=True
         if sigma is None or sigma.numel() != P:
             raise ValueError("seg_query: want_seg needs sigma (P,)")
         _req(sigma, "sigma")
-    _check(lib.sd_seg_query(ptr(dino), P, ctypes.byref(rec), ptr(sigma), float(voxel_size),
+    _check(lib.sd_seg_query(ptr(dino), dt, P, ctypes.byref(rec), ptr(sigma), float(voxel_size),
                             ptr(labels), ptr(seg), ptr(full), stream_of(dino)), "sd_seg_query")
     return labels, seg, full
 

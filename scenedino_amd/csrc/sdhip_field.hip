@@ -708,10 +708,19 @@ k_field(const sd_field_args a, const sd_mlp m, const LdsPlan pl) {
             // O layout: row = point (r&3)+8(r>>2)+4h of this tile, column = dim li
             const int dim = dt * 32 + li;
             const float bd = m.b_dino[dim];
+            if (a.dino_dtype == SD_BF16) {  // (the seg head's input: half the bytes)
+                __bf16 *d16 = (__bf16 *)(void *)a.dino;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int64_t pr = tile * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (pr < NP) a.dino[pr * m.D + dim] = o[r] + bd;
+                for (int r = 0; r < 16; ++r) {
+                    const int64_t pr = tile * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    if (pr < NP) d16[pr * m.D + dim] = (__bf16)(o[r] + bd);
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int64_t pr = tile * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    if (pr < NP) a.dino[pr * m.D + dim] = o[r] + bd;
+                }
             }
         }
         if (valid && h == 0) {
@@ -883,6 +892,7 @@ extern "C" int sd_field_query(const sd_field_args *args, const sd_mlp *mlp, void
     const sd_field_args &a = *args;
     if (a.B <= 0 || a.P < 0 || !a.xyz || !a.grid || !a.cam_f || !a.sigma || !a.dino ||
         a.Hf <= 0 || a.Wf <= 0 || a.nv < 0 || a.nv > SD_MAX_NV ||
+        (a.dino_dtype != SD_F32 && a.dino_dtype != SD_BF16) ||
         a.B * (int64_t)a.Hf * a.Wf * mlp->C * (mlp->dtype == SD_F32 ? 4 : 2) >= (1LL << 32) ||
         (a.nv > 0 && (a.rgb || a.invalid) && (!a.img || !a.cam_c || a.Hc <= 0 || a.Wc <= 0))) {
         sd_set_error("sd_field_query: invalid argument (all grid planes < 4 GiB)");

@@ -188,8 +188,8 @@ extern "C" int sd_seg_prof(unsigned long long *out, int reset) {
 // with a per-point power-of-two scale (its largest value lands in [128, 256)), W2 with the
 // per-tensor one of the packed record; the scales leave in the f32 epilogue (exact).
 template <int MODE, bool F8>
-__global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const float *__restrict__ dino,
-                                                            int64_t P, int32_t DF,
+__global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const void *__restrict__ dino_in,
+                                                            int32_t x16, int64_t P, int32_t DF,
                                                             const float *__restrict__ sigma,
                                                             float neg_vox, sd_seg_head h,
                                                             int32_t *__restrict__ labels,
@@ -257,8 +257,12 @@ __global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const float *__restr
 #pragma unroll
         for (int ct = 0; ct < SG_NT; ++ct) {
             const int64_t p = base + 32 * ct + r;
-            if (p < P) {
-                const f32x4_t *src = (const f32x4_t *)(dino + p * SG_DR);
+            if (p < P && x16) {  // bf16 codes (sd_field_query dino_dtype SD_BF16): as loaded
+                const bf16x8 *src = (const bf16x8 *)dino_in + p * (SG_DR / 8);
+#pragma unroll
+                for (int s = 0; s < SG_DR / 16; ++s) xb[ct][s] = src[2 * s + hh];
+            } else if (p < P) {
+                const f32x4_t *src = (const f32x4_t *)((const float *)dino_in + p * SG_DR);
 #pragma unroll
                 for (int s = 0; s < SG_DR / 16; ++s) {
                     f32x4_t a = src[4 * s + 2 * hh], b = src[4 * s + 2 * hh + 1];
@@ -641,14 +645,16 @@ static int sg_valid(const sd_seg_head *h, int need_seg) {
     return 1;
 }
 
-extern "C" int sd_seg_query(const float *dino, int64_t P, const sd_seg_head *h,
-                            const float *sigma, float voxel_size, int32_t *labels, uint8_t *seg,
-                            float *dino_full, void *stream) {
+extern "C" int sd_seg_query(const void *dino, int32_t dino_dtype, int64_t P,
+                            const sd_seg_head *h, const float *sigma, float voxel_size,
+                            int32_t *labels, uint8_t *seg, float *dino_full, void *stream) {
     const int want_seg = labels != nullptr || seg != nullptr;
     if (!dino || P < 0 || !sg_valid(h, want_seg) || (seg && !sigma) ||
-        (!want_seg && !dino_full)) {
+        (!want_seg && !dino_full) || (dino_dtype != SD_F32 && dino_dtype != SD_BF16) ||
+        ((uintptr_t)dino & 15)) {
         sd_set_error("sd_seg_query: invalid argument (d_in 64, d_latent 128, d_full % 32 == 0, "
-                     "d_code 64, 1..256 clusters; seg needs sigma; at least one output)");
+                     "d_code 64, 1..256 clusters; seg needs sigma; at least one output; dino "
+                     "f32 or bf16, 16-B aligned)");
         return -1;
     }
     if (P == 0) return 0;
@@ -665,7 +671,8 @@ extern "C" int sd_seg_query(const float *dino, int64_t P, const sd_seg_head *h,
     // fp8 norm only for the labels / seg outputs (dino_full is the bf16 expansion)
     const bool f8 = h->w2_f8 != nullptr && mode == 2;
 #define SG_LAUNCH(M, F)                                                                            \
-    hipLaunchKernelGGL((k_seg_head<M, F>), dim3((unsigned)nblk), dim3(SG_WAVES * 64), lds_bytes, s, dino, P, \
+    hipLaunchKernelGGL((k_seg_head<M, F>), dim3((unsigned)nblk), dim3(SG_WAVES * 64), lds_bytes, s, dino, \
+                       (int32_t)(dino_dtype == SD_BF16), P, \
                        h->d_full, sigma, neg_vox, *h, labels, seg, dino_full)
     switch (mode) {
     case 1: SG_LAUNCH(1, false); break;

@@ -407,10 +407,11 @@ class BTSNet(nn.Module):
             self._timed("render", lambda: _lib.render_fused(args, m.rec, rays))
         return out
 
-    def query(self, xyz, colors: bool = True):
+    def query(self, xyz, colors: bool = True, dino_dtype=torch.float32):
         """Raw per-point field: sigma (n,P), dino (n,P,D), rgb (n,P,3nv), invalid (n,P,nv),
         invalid_features (n,P) -- all from sd_field_query.  colors=False skips the colour
-        sampling (the predict_segmentation path, bts.py:528-533): rgb / invalid are None."""
+        sampling (the predict_segmentation path, bts.py:528-533): rgb / invalid are None.
+        dino_dtype bfloat16: dino for sd_seg_query, which rounds its input to bf16 anyway."""
         self._check_supported()
         m = self._mlp()
         gc = self._grids()
@@ -432,7 +433,7 @@ class BTSNet(nn.Module):
         nv = gc["nv"] if colors else 0
         xyz = xyz.float().contiguous()
         sigma = torch.empty(n, P, device=dev)
-        dino = torch.empty(n, P, m.D, device=dev)
+        dino = torch.empty(n, P, m.D, device=dev, dtype=dino_dtype)
         rgb = torch.empty(n, P, 3 * nv, device=dev) if colors else None
         inv = torch.empty(n, P, nv, device=dev) if colors else None
         invf = torch.empty(n, P, device=dev, dtype=torch.bool)  # bytes 0 / 1
@@ -442,7 +443,8 @@ class BTSNet(nn.Module):
             cam_f=gc["cam_f"].data_ptr(), img=gc["img"].data_ptr() if colors else None, nv=nv,
             Hc=gc["Hc"], Wc=gc["Wc"], cam_c=gc["cam_c"].data_ptr(), sigma=sigma.data_ptr(),
             dino=dino.data_ptr(), rgb=rgb.data_ptr() if colors else None,
-            invalid=inv.data_ptr() if colors else None, invalid_f=invf.data_ptr())
+            invalid=inv.data_ptr() if colors else None, invalid_f=invf.data_ptr(),
+            dino_dtype=_lib.SD_BF16 if dino_dtype == torch.bfloat16 else _lib.SD_F32)
         self._timed("field", lambda: _lib.field_query(args, m.rec, xyz))
         return sigma, dino, rgb, inv, invf
 
@@ -543,7 +545,7 @@ class BTSNet(nn.Module):
                                       "(the SSCBench 'scenedino' mode)")
         if self.downstream_head is None:
             raise ValueError("predict_voxels needs a downstream (segmentation) head")
-        sigma, dino, _, _, _ = self.query(xyz, colors=False)
+        sigma, dino, _, _, _ = self.query(xyz, colors=False, dino_dtype=torch.bfloat16)
         rec = self._seg_rec(True)
         P = sigma.numel()
         _, seg, _ = self._timed("seg", lambda: _lib.seg_query(

@@ -164,6 +164,21 @@ def test_field_query_vs_reference(precision, fx):
         assert rel_l2(sd["dino_features"], d["dino"]) < 1e-2
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_field_query_bf16_dino_is_the_rounded_f32(precision):
+    """dino_dtype bf16 (the voxel path's input to sd_seg_query): the same values as the f32
+    output rounded to bf16 (RNE), bit for bit; sigma unchanged."""
+    d = load("field_query.npz")
+    net = net_from_fixture(d, precision)
+    xyz = T(d["xyz"])
+    with torch.no_grad():
+        s32, d32, _, _, _ = net.query(xyz, colors=False)
+        s16, d16, _, _, _ = net.query(xyz, colors=False, dino_dtype=torch.bfloat16)
+    assert d16.dtype == torch.bfloat16
+    assert torch.equal(s16, s32)
+    assert torch.equal(d16, d32.to(torch.bfloat16))
+
+
 # --------------------------------------------------------------------------- full render
 def _render(d, precision, want_rgb_samps=True, mode="proj", channels_last=False):
     from scenedino_amd.renderer import NeRFRenderer

@@ -343,6 +343,9 @@ def test_seg_query_vs_reference(gpu, d_full):
     assert (f - ref).abs().max().item() <= 1.5e-2
     _, ref_scores, ref_labels = SO.seg_head(torch.as_tensor(d["x" + t]), p)
     _label_check(labels.cpu(), ref_scores, d["labels" + t], "labels")
+    # bf16 codes (sd_field_query's dino_dtype SD_BF16): the kernel's own rounding of f32
+    l16, _, f16 = _lib.seg_query(x.to(torch.bfloat16), pk.rec, want_labels=True, want_full=True)
+    assert torch.equal(l16, labels) and torch.equal(f16, full)
     # labels-only and full-only launches give the same results as the combined one
     l2, _, _ = _lib.seg_query(x, pk.rec, want_labels=True)
     assert torch.equal(l2, labels)
