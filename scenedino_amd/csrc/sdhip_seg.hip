@@ -241,7 +241,12 @@ __global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const void *__restri
                          : (const uint8_t *)h.wn2 + ((int64_t)((i - 8) >> 1) * KS + 2 * t + ((i - 8) & 1)) * 1024;
         };
     };
-    if (!F8) stage(0, 16, gsrc(0));  // lands while layer 1 runs
+    // W1 into slot 1 and L into slot 2 (read from LDS by layer 1 / the L path, both done
+    // before those slots take Gram / M tiles), the first Gram tile into slot 0: one wait
+    // for all of it (and the input codes) instead of a chain of L2 round trips
+    stage(1, 16, [&](int i) { return (const uint8_t *)h.w1 + i * 1024; });
+    if (SEG) stage(2, 16, [&](int i) { return (const uint8_t *)h.wl + i * 1024; });
+    if (!F8) stage(0, 16, gsrc(0));
     // the M loop's bias rows (Wn1 b2, bn1; accumulator-row order) in LDS after the slots
     const float *lds_b = (const float *)(sg_lds + SG_NSLOT * SG_SLOT);
     if (SEG) {
@@ -279,7 +284,8 @@ __global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const void *__restri
                     for (int j = 0; j < 8; ++j) xb[ct][s][j] = (__bf16)0.f;
             }
         }
-        const bf16x8 *w1 = (const bf16x8 *)h.w1;
+        landed();  // W1 (and L, Gram tile 0) in LDS
+        const bf16x8 *w1 = (const bf16x8 *)(sg_lds + 1 * SG_SLOT);
 #pragma unroll
         for (int t = 0; t < SG_DL / 32; ++t) {
             const f32x16 bb = sg_rows(h.b1, t, hh);  // the bias rides in as the accumulator
@@ -445,7 +451,7 @@ __global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const void *__restri
     // linear path folded to L (64 x 128)
     f32x16 sacc[SG_NT][SG_DC / 32];
     {
-        const bf16x8 *wl = (const bf16x8 *)h.wl;
+        const bf16x8 *wl = (const bf16x8 *)(sg_lds + 2 * SG_SLOT);  // (staged at the start)
 #pragma unroll
         for (int rt = 0; rt < SG_DC / 32; ++rt) {
             const f32x16 lb = sg_rows(h.bl, rt, hh);
