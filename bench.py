@@ -559,20 +559,35 @@ def main_train(args, world, rank, device):
     amp = not args.no_amp  # train_scenedino_kitti_360.yaml: with_amp: true (fp16 autocast)
     npatch = RB // (PS * PS)
 
+    host = {} if os.environ.get("SCENEDINO_AMD_HOST_PROFILE") == "1" else None
+
+    def mark(name, t0):  # diagnostic: host issue time per phase (no device sync)
+        if host is not None:
+            t1 = time.perf_counter()
+            host[name] = host.get(name, 0.0) + (t1 - t0)
+            return t1
+        return t0
+
     def step():
+        t0 = time.perf_counter()
         # PatchRaySampler batch (device rays + rgb / per-patch DINO targets)
         rays, rgb_gt, dino_gt = sampler.sample(images, ray_poses, Ks, dino_features=dino_gt_map)
+        t0 = mark("sample", t0)
         with torch.autocast("cuda", dtype=torch.float16, enabled=amp):
             out = wrapper(rays, want_weights=True)["coarse"]
+            t0 = mark("forward", t0)
             pd = out["dino_features"].float().view(NB, npatch, PS * PS, D_DINO).mean(2)
             loss = ((pd - dino_gt) ** 2).mean() + \
                 (out["rgb"].float() - (rgb_gt * 0.5 + 0.5)).abs().mean()
+        t0 = mark("loss", t0)
         opt.zero_grad(set_to_none=True)
         leaf.grad = None
         loss.backward()
+        t0 = mark("backward", t0)
         if world > 1:  # data-parallel head: one RCCL all-reduce of the gradient bucket
             sdd.allreduce_grads(head.parameters())
         opt.step()
+        mark("optimizer", t0)
         return loss
 
     timer = KernelTimer()
@@ -584,6 +599,8 @@ def main_train(args, world, rank, device):
         torch.distributed.barrier()
     torch.cuda.synchronize()
     timer.on = True
+    if host is not None:
+        host.clear()  # steady state only
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -594,6 +611,10 @@ def main_train(args, world, rank, device):
     elapsed = time.perf_counter() - t0
     timer.on = False
     sda.kernel_timer = None
+    if host is not None and rank == 0:
+        n = args.steps
+        print("host issue ms per step: " + ", ".join(f"{k} {1e3 * v / n:.3f}" for k, v in host.items()),
+              file=sys.stderr, flush=True)
     ms = {k: timer.mean_ms(k) for k in ("gather", "gather_bwd", "composite_bwd")}
     if world > 1:
         t = torch.tensor([elapsed] + [ms[k] for k in ms], device=device, dtype=torch.float64)
