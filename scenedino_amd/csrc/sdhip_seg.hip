@@ -384,13 +384,10 @@ __global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const void *__restri
         float ss[SG_NT];
 #pragma unroll
         for (int ct = 0; ct < SG_NT; ++ct) ss[ct] = 0.f;
-#pragma unroll  // (h's registers are indexed by t)
-        for (int t = 0; t < SG_DL / 32; ++t) {
-            landed();
-            if (t + 1 < SG_DL / 32) stage((t + 1) & 1, 16, gsrc(t + 1));
-            else if (SEG) stage(0, 12, msrc(0));  // the M loop's first tile
-            const bf16x8 *sl = (const bf16x8 *)(sg_lds + (t & 1) * SG_SLOT);
-            f32x16 acc[SG_NT];
+        // software-pipelined over the 4 tiles (two slots): tile t + 1's product is issued
+        // before tile t's epilogue; tile 0 landed with the layer-1 wait
+        auto g_issue = [&](int slot, f32x16 *acc) {
+            const bf16x8 *sl = (const bf16x8 *)(sg_lds + slot * SG_SLOT);
 #pragma unroll
             for (int ct = 0; ct < SG_NT; ++ct) acc[ct] = sg_zero16();
 #pragma unroll
@@ -399,12 +396,30 @@ __global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const void *__restri
 #pragma unroll
                 for (int ct = 0; ct < SG_NT; ++ct) acc[ct] = SG_MFMA(a, hb[ct][q & 7], acc[ct]);
             }
+        };
+        f32x16 acc[SG_NT];
+        landed();  // every wave is done with W1 (slot 1)
+        stage(1, 16, gsrc(1));
+        g_issue(0, acc);
+#pragma unroll  // (h's registers are indexed by t)
+        for (int t = 0; t < SG_DL / 32; ++t) {
+            f32x16 accn[SG_NT];
+            if (t + 1 < SG_DL / 32) {
+                landed();  // tile t + 1 landed; every wave has issued tile t (its slot is free)
+                if (t + 2 < SG_DL / 32) stage(t & 1, 16, gsrc(t + 2));
+                else if (t + 2 == SG_DL / 32 && SEG) stage(0, 12, msrc(0));  // the M loop's first tile
+                g_issue((t + 1) & 1, accn);
+            }
             const f32x16 gg = sg_rows(h.g2, t, hh);
 #pragma unroll
             for (int ct = 0; ct < SG_NT; ++ct)
 #pragma unroll
                 for (int i = 0; i < 16; ++i)
                     ss[ct] = fmaf(sg_bf16_at(hb[ct][2 * t + (i >> 3)], i & 7), acc[ct][i] + gg[i], ss[ct]);
+            if (t + 1 < SG_DL / 32) {
+#pragma unroll
+                for (int ct = 0; ct < SG_NT; ++ct) acc[ct] = accn[ct];
+            }
         }
 #pragma unroll
         for (int ct = 0; ct < SG_NT; ++ct) {
