@@ -334,6 +334,12 @@ typedef struct sd_seg_head {
     int32_t pad1;
 } sd_seg_head;
 
+/* Grow: out = 3x3x3 max filter of the (nx, ny, nz) f32 density grid in (z fastest),
+ * F.max_pool3d(kernel_size=3, stride=1, padding=1) as evaluate_model_sscbench.py:755-756
+ * applies it (NaN propagates; out-of-grid neighbours never win).  in != out,
+ * nx * ny * nz < 2^31. */
+int sd_grow3(const float *in, int64_t nx, int64_t ny, int64_t nz, float *out, void *stream);
+
 /* Per-point segmentation head on P DINO codes dino (P, d_in), SD_F32 or SD_BF16 (16-B
  * aligned; the kernel's first MFMA takes them as bf16 either way).
  * Replaces BTSNet.forward(predict_segmentation=True)'s encoder.expand_dim +

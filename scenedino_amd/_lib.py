@@ -180,6 +180,7 @@ SIGNATURES = {
                      _vp],
     "sd_voxel_points": [ctypes.POINTER(ctypes.c_double), ctypes.c_double, _i64, _i64, _i64,
                         ctypes.POINTER(ctypes.c_double), _vp, _vp],
+    "sd_grow3": [_vp, _i64, _i64, _i64, _vp, _vp],
     "sd_seg_query": [_vp, _i32, _i64, ctypes.POINTER(SdSegHead), _vp, ctypes.c_float, _vp, _vp,
                      _vp, _vp],
     "sd_voxel_fov": [ctypes.POINTER(ctypes.c_double), ctypes.c_double, _i64, _i64, _i64,
@@ -451,6 +452,19 @@ def voxel_points(origin, voxel_size, dims, T, device):
     out = torch.empty(nx * ny * nz, 3, device=device, dtype=torch.float32)
     _check(lib.sd_voxel_points(o, float(voxel_size), nx, ny, nz, t, ptr(out), stream_of(out)),
            "sd_voxel_points")
+    return out
+
+
+def grow3(sig):
+    """3x3x3 max filter of a (nx, ny, nz) f32 density grid (sd_grow3): F.max_pool3d(
+    sig[None], 3, 1, 1)[0] of evaluate_model_sscbench.py:755-756."""
+    lib = load()
+    _req(sig, "sig")
+    if sig.dim() != 3:
+        raise ValueError("grow3: sig must be (nx, ny, nz)")
+    out = torch.empty_like(sig)
+    _check(lib.sd_grow3(ptr(sig), sig.shape[0], sig.shape[1], sig.shape[2], ptr(out),
+                        stream_of(sig)), "sd_grow3")
     return out
 
 

@@ -95,6 +95,47 @@ __global__ void __launch_bounds__(256) k_voxel_points(VoxConst c, double vox, in
 }
 
 // ---------------------------------------------------------------------------
+// grow: 3x3x3 max filter of the density grid (F.max_pool3d(kernel 3, stride 1, padding 1),
+// evaluate_model_sscbench.py:755-756), separable: a thread takes the max over its voxel's
+// 3 x 3 (x, y) neighbourhood at its own z (9 loads, coalesced along z), the z step reads
+// the neighbours' partial maxima from LDS (a block edge recomputes its outside
+// neighbour).  NaN propagates and the padding never wins, as torch's max pooling.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float sg_nanmax(float m, float v) { return (v > m || v != v) ? v : m; }
+
+__device__ __forceinline__ float sg_max9(const float *__restrict__ in, int x, int y, int z,
+                                         int nx, int ny, int nz) {
+    float m = -INFINITY;
+#pragma unroll
+    for (int dx = -1; dx <= 1; ++dx)
+#pragma unroll
+        for (int dy = -1; dy <= 1; ++dy) {
+            const int xx = x + dx, yy = y + dy;
+            if (xx >= 0 && xx < nx && yy >= 0 && yy < ny)
+                m = sg_nanmax(m, in[((int64_t)xx * ny + yy) * nz + z]);
+        }
+    return m;
+}
+
+__global__ void __launch_bounds__(256) k_grow3(const float *__restrict__ in, int nx, int ny,
+                                               int nz, float *__restrict__ out) {
+    __shared__ float sm[256];
+    const int n = nx * ny * nz;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int ic = i < n ? i : n - 1;
+    const int z = ic % nz, q = ic / nz, y = q % ny, x = q / ny;
+    const float m9 = sg_max9(in, x, y, z, nx, ny, nz);
+    sm[threadIdx.x] = m9;
+    __syncthreads();
+    if (i >= n) return;
+    float m = m9;
+    if (z > 0) m = sg_nanmax(m, threadIdx.x > 0 ? sm[threadIdx.x - 1] : sg_max9(in, x, y, z - 1, nx, ny, nz));
+    if (z + 1 < nz)
+        m = sg_nanmax(m, threadIdx.x < 255 ? sm[threadIdx.x + 1] : sg_max9(in, x, y, z + 1, nx, ny, nz));
+    out[i] = m;
+}
+
+// ---------------------------------------------------------------------------
 // folded transform_expand + stego + k-means head
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ f32x16 sg_zero16() {
@@ -647,6 +688,22 @@ extern "C" int sd_voxel_points(const double *origin, double vox, int64_t nx, int
                        (hipStream_t)stream, c, vox, nx, ny, nz, pts_out);
     if (hipGetLastError() != hipSuccess) {
         sd_set_error("sd_voxel_points: launch failed");
+        return -2;
+    }
+    return 0;
+}
+
+extern "C" int sd_grow3(const float *in, int64_t nx, int64_t ny, int64_t nz, float *out,
+                        void *stream) {
+    if (!in || !out || in == out || nx <= 0 || ny <= 0 || nz <= 0 || nx * ny * nz > 0x7fffff00LL) {
+        sd_set_error("sd_grow3: invalid argument (distinct in / out, positive dims)");
+        return -1;
+    }
+    const int64_t n = nx * ny * nz;
+    hipLaunchKernelGGL(k_grow3, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, in, (int)nx, (int)ny, (int)nz, out);
+    if (hipGetLastError() != hipSuccess) {
+        sd_set_error("sd_grow3: launch failed");
         return -2;
     }
     return 0;

@@ -24,7 +24,6 @@ from __future__ import annotations
 
 import numpy as np
 import torch
-import torch.nn.functional as F
 
 from . import _lib
 
@@ -90,7 +89,7 @@ def query_voxels(net, pts, dims, prediction_mode="stego_kmeans", grow=USE_GROW):
                                     prediction_mode=prediction_mode)
     sigmas = sigma.reshape(nx, ny, nz)
     if grow:  # :755-756
-        sigmas = F.max_pool3d(sigmas.unsqueeze(0), kernel_size=3, stride=1, padding=1).squeeze(0)
+        sigmas = _lib.grow3(sigmas.contiguous())  # = F.max_pool3d(kernel 3, stride 1, pad 1)
     return sigmas, seg.reshape(nx, ny, nz)
 
 
@@ -119,7 +118,7 @@ def query_voxels_slab(predict, pts, dims, rank, world, grow=USE_GROW):
     sig, seg = predict(pts[h0 * plane:h1 * plane])
     sig = sig.reshape(h1 - h0, ny, nz)
     if grow:
-        sig = F.max_pool3d(sig.unsqueeze(0), kernel_size=3, stride=1, padding=1).squeeze(0)
+        sig = _lib.grow3(sig.contiguous())
     lo = x0 - h0
     return (sig[lo:lo + x1 - x0].contiguous(),
             seg.reshape(h1 - h0, ny, nz)[lo:lo + x1 - x0].contiguous())

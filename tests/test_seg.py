@@ -312,6 +312,23 @@ def test_voxel_points_ragged_dims(gpu):
         assert (got == ref).all(), dims
 
 
+@pytest.mark.gpu
+def test_grow3_equals_max_pool3d(gpu):
+    """sd_grow3 vs F.max_pool3d(kernel 3, stride 1, padding 1) (the SSCBench grow,
+    evaluate_model_sscbench.py:755-756): bit-equal on the C5 grid shape and ragged ones,
+    NaN propagating as torch's."""
+    import torch.nn.functional as F
+    from scenedino_amd import _lib
+    g = torch.Generator().manual_seed(9)
+    for dims in ((256, 256, 32), (1, 1, 1), (7, 5, 3), (33, 17, 9)):
+        sig = (torch.rand(dims, generator=g) * 5).to(gpu)
+        if dims == (33, 17, 9):
+            sig[3, 4, 5] = float("nan")
+        ref = F.max_pool3d(sig.unsqueeze(0), kernel_size=3, stride=1, padding=1).squeeze(0)
+        got = _lib.grow3(sig)
+        torch.testing.assert_close(got, ref, rtol=0, atol=0, equal_nan=True)
+
+
 def _label_check(labels, ref_scores, ref_labels, what, min_agree=0.99):
     top2 = ref_scores.topk(2, dim=1).values
     margin = (top2[:, 0] - top2[:, 1]).numpy()
