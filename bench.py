@@ -732,9 +732,14 @@ def c2_pose_run(args, world, rank, device, dist, offset_pose, host_stage):
     torch.cuda.synchronize()
     timer.on = True
     t0 = time.perf_counter()
+    host_ms = 0.0
     for i in range(args.steps):
+        th = time.perf_counter()
         step(args.warmup + i)
+        host_ms += 1e3 * (time.perf_counter() - th)
         timer.tick()
+    if os.environ.get("SCENEDINO_AMD_HOST_PROFILE") == "1" and rank == 0:
+        print(f"host issue ms per frame: {host_ms / args.steps:.3f}", file=sys.stderr, flush=True)
     if gather is not None:
         gather.wait_all()
     torch.cuda.synchronize()
