@@ -103,13 +103,14 @@ def slab_range(nx: int, rank: int, world: int) -> tuple[int, int]:
     return x0, x0 + base + (1 if rank < extra else 0)
 
 
-def query_voxels_slab(predict, pts, dims, rank, world, grow=USE_GROW):
+def query_voxels_slab(predict, pts, dims, rank, world, grow=USE_GROW, grow_fn=None):
     """This rank's x-slab of query_voxels.  ``predict(points (P, 3)) -> (sigma (P,),
     seg (P,))`` evaluates the field + head on a contiguous run of voxel centres (the flat
     index (ix ny + iy) nz + iz keeps every x-plane contiguous).  The 3x3x3 grow max-pool
     needs one neighbouring x-plane on each side: those halo planes are queried too and
     dropped after pooling, so the gathered slabs equal the unsharded result bit for bit.
-    Returns sigmas (x1 - x0, ny, nz), segs (x1 - x0, ny, nz)."""
+    ``grow_fn`` (default sd_grow3) maps a (planes, ny, nz) density block to its 3x3x3 max
+    filter.  Returns sigmas (x1 - x0, ny, nz), segs (x1 - x0, ny, nz)."""
     nx, ny, nz = dims
     x0, x1 = slab_range(nx, rank, world)
     h0 = max(x0 - 1, 0) if grow else x0
@@ -118,7 +119,7 @@ def query_voxels_slab(predict, pts, dims, rank, world, grow=USE_GROW):
     sig, seg = predict(pts[h0 * plane:h1 * plane])
     sig = sig.reshape(h1 - h0, ny, nz)
     if grow:
-        sig = _lib.grow3(sig.contiguous())
+        sig = (grow_fn or _lib.grow3)(sig.contiguous())
     lo = x0 - h0
     return (sig[lo:lo + x1 - x0].contiguous(),
             seg.reshape(h1 - h0, ny, nz)[lo:lo + x1 - x0].contiguous())

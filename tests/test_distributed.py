@@ -183,7 +183,10 @@ def _slab_worker(rank, world, port, q):
         dims = (16, 6, 5)
         g = torch.Generator().manual_seed(3)
         pts = torch.rand(dims[0] * dims[1] * dims[2], 3, generator=g) * 4 - 2
-        sig, seg = sscbench.query_voxels_slab(_slab_predict, pts, dims, rank, world)
+        # CPU stand-ins for the field query and the grow (sd_grow3's parity vs max_pool3d is
+        # tests/test_seg.py::test_grow3_equals_max_pool3d): this test is the halo logic
+        pool = lambda t: torch.nn.functional.max_pool3d(t.unsqueeze(0), 3, 1, 1).squeeze(0)
+        sig, seg = sscbench.query_voxels_slab(_slab_predict, pts, dims, rank, world, grow_fn=pool)
         full_s, full_g = sscbench.gather_slabs(sig, seg, dims)
         # unsharded reference: the whole grid, grown by the 3x3x3 max-pool
         rs, rg = _slab_predict(pts)
