@@ -354,6 +354,16 @@ def main_c5(args, world, rank, local_rank, dist, device, host_stage=False):
             x0, x1 = sscbench.slab_range(dims[0], rank, world)
             n_launch = (min(x1 + 1, dims[0]) - max(x0 - 1, 0)) * dims[1] * dims[2]
         algo = n_launch * SEG_FLOPS_ALGO
+        # HBM bytes per k_seg_head launch (1-GPU launch shape) from the committed PMC
+        # summary (tools/c5_traffic.sh: FETCH_SIZE x 2 + WRITE_SIZE, separate passes)
+        seg_traffic, seg_tsrc = None, None
+        tf = os.path.join(ROOT, "profiles", "r2_c5_traffic.json")
+        if not dist and os.path.exists(tf):
+            try:
+                seg_traffic = json.load(open(tf))["kernels"]["k_seg_head"]["hbm_bytes"]
+                seg_tsrc = "profiles/r2_c5_traffic.json (rocprofv3 PMC, per launch)"
+            except (KeyError, TypeError, ValueError):
+                seg_traffic = None
         exe = n_launch * (SEG_FLOPS_EXEC_FP8 if seg_fp8 else SEG_FLOPS_EXEC)
         line = {
             "metric": "SSCBench voxel-grid query, voxels/sec (256x256x32 grid per frame)",
@@ -372,7 +382,7 @@ def main_c5(args, world, rank, local_rank, dist, device, host_stage=False):
                 "kernel": "k_seg_head (sd_seg_query)", "bound": "mfma",
                 "achieved": algo / (seg_ms * 1e-3) / 1e12, "peak": PEAK_TFLOPS["bf16"],
                 "unit": "TFLOP/s", "frac": algo / (seg_ms * 1e-3) / 1e12 / PEAK_TFLOPS["bf16"],
-                "traffic": None, "kernel_ms": seg_ms,
+                "traffic": seg_traffic, "traffic_source": seg_tsrc, "kernel_ms": seg_ms,
                 "algorithmic_flops_per_launch": algo, "executed_mfma_flops_per_launch": exe,
                 "executed_tflops": exe / (seg_ms * 1e-3) / 1e12,
                 "executed_frac": exe / (seg_ms * 1e-3) / 1e12 / PEAK_TFLOPS["bf16"],
