@@ -10,7 +10,7 @@ fused render (sd_render_proj: LDS-staged tile kernel + overflow fallback; z samp
 points, projection, code, P gather, MFMA MLP, colours, alpha compositing).  The C2 step is
 timed at two render poses, the encoder view and a 0.5 m lateral / 2 deg yaw offset view
 (SURVEY §8(d)); ``value`` is the slower of the two.  For N > 1 every rank renders its own
-frame (C3: frames sharded 1-per-GPU) straight into packed [depth | dino | rgb] rows that
+frame (C3: frames sharded 1-per-GPU) straight into packed [dino | depth | rgb] rows that
 are all-gathered over RCCL (all_gather_into_tensor, overlapped with the next frame).
 The ViT/DPT encoder is not part of the timed step (separate scope row, ``end_to_end``).
 
@@ -37,7 +37,8 @@ sys.path.insert(0, ROOT)
 H, W, K_SAMPLES = 192, 640, 64
 C_GRID, HF, WF = 256, 192, 640
 KITTI_K = [[0.7849, 0.0, -0.0312], [0.0, 2.9391, 0.2701], [0.0, 0.0, 1.0]]
-PEAK_TFLOPS = {"bf16": 2500.0, "fp16": 2500.0, "fp32": 157.3}   # MI355X dense MFMA (MI355X_MICROARCH.md)
+PEAK_TFLOPS = {"bf16": 2500.0, "fp16": 2500.0, "fp32": 157.3,   # MI355X dense MFMA
+               "fp8": 5000.0}                                    # (MI355X_MICROARCH.md)
 D_HIDDEN, D_DINO = 128, 64
 D_IN = C_GRID + 39
 
@@ -67,9 +68,10 @@ def _layout(grid):
     return grid.contiguous(memory_format=torch.channels_last) if GRID_LAYOUT == "nhwc" else grid
 
 
-def make_scene(frame_seed: int, device, precision="bf16", offset_pose=False):
+def make_scene(frame_seed: int, device, precision="bf16", offset_pose=False, grid_hw=None):
     """Synthetic inputs of SURVEY.md §8(d): image U[-1,1) (seed frame), grid N(0,1)
-    (seed 1+frame), MLP kaiming (seed 2)."""
+    (seed 1+frame), MLP kaiming (seed 2).  grid_hw: (Hf, Wf) of the feature grid
+    (default 192x640, ViT-S/16 + DPT; C5 uses ViT-B/8's 384x1280)."""
     from scenedino_amd.models import BTSNet
     from scenedino_amd.models.prediction_heads import ResnetFC
     from scenedino_amd.common.positional_encoding import PositionalEncoding
@@ -78,7 +80,8 @@ def make_scene(frame_seed: int, device, precision="bf16", offset_pose=False):
 
     g = torch.Generator().manual_seed(frame_seed)
     images = (torch.rand(1, 1, 3, H, W, generator=g) * 2 - 1).to(device)
-    grid = _layout(torch.randn(1, C_GRID, HF, WF,
+    hf, wf = grid_hw if grid_hw is not None else (HF, WF)
+    grid = _layout(torch.randn(1, C_GRID, hf, wf,
                                generator=torch.Generator().manual_seed(1 + frame_seed)))
     torch.manual_seed(2)
     head = ResnetFC(d_in=D_IN, d_out=1 + D_DINO, n_blocks=0, d_hidden=D_HIDDEN)
@@ -147,16 +150,18 @@ def end_to_end(args, device, rank):
             "ms_per_frame": dt * 1e3, "rays_per_s": H * W / dt}
 
 
-def render_step(net, wrapper, sampler, pose, Ks, band=None):
-    """One C2 frame: rays of the render pose, then the fused render.  band = (r0, r1):
-    only rays [r0, r1) of the frame (ray-tile sharding; the renderer keys its in-kernel
-    depth jitter by the frame ray index, so the band matches the whole-frame render)."""
+def render_step(net, wrapper, sampler, pose, Ks, band=None, want_weights=True, want_alphas=True):
+    """One C2 frame: rays of the render pose, then the fused render -- with per-sample
+    weights and alphas, as demo_script's render call asks for them
+    (demo_utils/utils.py:223).  band = (r0, r1): only rays [r0, r1) of the frame (ray-tile
+    sharding; the renderer keys its in-kernel depth jitter by the frame ray index, so the
+    band matches the whole-frame render)."""
     net._grid_cache = None  # re-pack / re-project the (freshly encoded) grid every frame
     rays, _ = sampler.sample(None, pose, Ks)
     if band is not None:
         rays = rays[:, band[0]:band[1]]
         wrapper.renderer.ray_offset = band[0]
-    return wrapper(rays, want_weights=False, want_alphas=False)
+    return wrapper(rays, want_weights=want_weights, want_alphas=want_alphas)
 
 
 class KernelTimer:
@@ -211,10 +216,11 @@ def offset_render_pose(pose):
 def cpu_baseline(budget_s: float = 20.0, offset_pose: bool = True):
     """Oracle (pure-PyTorch CPU restatement of the reference, fp32) on the host cores:
     renders whole image rows of the same C2 frame (rays from the offset render pose, as
-    the reported GPU value) until ~budget_s of CPU work."""
+    the reported GPU value) until ~budget_s of CPU work, on os.cpu_count() threads (SURVEY
+    §8(d); SD_CPU_THREADS overrides)."""
     from oracle import render_oracle as O
 
-    threads = int(os.environ.get("SD_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    threads = int(os.environ.get("SD_CPU_THREADS", os.cpu_count() or 1))
     torch.set_num_threads(threads)
     g = torch.Generator().manual_seed(0)
     images = torch.rand(1, 1, 3, H, W, generator=g) * 2 - 1
@@ -254,7 +260,12 @@ def cpu_baseline(budget_s: float = 20.0, offset_pose: bool = True):
                     break
     except OSError:
         pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = None
     return {"value": done_rays / dt, "unit": "rays/s", "cores": threads, "kind": "port",
+            "cpu_count": os.cpu_count(), "affinity_cpus": usable,
             "sample": f"{done_rays} rays ({row} of {H} rows) of the same 192x640x64 frame"
                       f"{' (offset render pose)' if offset_pose else ''}, "
                       f"fp32 torch-CPU oracle restatement, {dt:.1f} s on {threads} threads "
@@ -284,6 +295,31 @@ SEG_FLOPS_ALGO = 2 * (64 * 128 + 128 * 768) + 2 * (768 * 64 + 768 * 768 + 768 * 
 # 768 x 128 W2 product instead of the Gram form
 SEG_FLOPS_EXEC = 2 * (64 * 128 + 2 * 128 * 128 + 64 * 128 + 768 * 128 + 64 * 768 + 3 * 32 * 64)
 SEG_FLOPS_EXEC_FP8 = SEG_FLOPS_EXEC - 2 * 2 * 128 * 128 + 2 * 768 * 128
+SEG_FLOPS_FP8_PART = 2 * 768 * 128  # the norm product |W2 h + b2| on fp8 MFMA
+
+
+C5_GRID_HW = (384, 1280)  # ViT-B/8 + DPT feature grid
+
+
+def c5_scene(device, precision, frame_seed=0):
+    """The C5 scene (BASELINE configs[4]): make_scene on the ViT-B/8-shaped 256x384x1280
+    grid, random-init MlpDimReduction(768, 64, 128) + SemanticHead(19, 19, 768, 64) (seed 5),
+    the SSCBench voxel centres.  precision "fp8": bf16 field, fp8 norm product in the seg
+    head.  Returns (net, pts (n_vox, 3), dims)."""
+    from scenedino_amd import sscbench
+    from scenedino_amd.models.backbones.dino import MlpDimReduction
+    from scenedino_amd.downstream_head import SemanticHead
+    seg_fp8 = precision == "fp8"
+    net, _, _, _, _, _ = make_scene(frame_seed, device, "bf16" if seg_fp8 else precision,
+                                    grid_hw=C5_GRID_HW)
+    net.seg_precision = "fp8" if seg_fp8 else "bf16"
+    torch.manual_seed(5)
+    net.encoder.dim_reduction = MlpDimReduction(768, 64, 128).to(device).eval()
+    net.downstream_head = SemanticHead(19, 19, 768, 64).to(device).eval()
+    net.gt_classes = 19
+    dims = sscbench.grid_dims()
+    pts = sscbench.generate_point_grid(sscbench.read_calib()["Tr"], device=device)
+    return net, pts, dims
 
 
 def main_c5(args, world, rank, local_rank, dist, device, host_stage=False):
@@ -295,20 +331,9 @@ def main_c5(args, world, rank, local_rank, dist, device, host_stage=False):
     N > 1: the frame's voxels are split into x-slabs [256 g / N, 256 (g+1) / N) (one halo
     plane each side for the grow), every rank queries its slab and the sigma / class slabs
     are all-gathered (strong scaling of one frame)."""
-    from scenedino_amd import _lib, sscbench
-    from scenedino_amd.models.backbones.dino import MlpDimReduction
-    from scenedino_amd.downstream_head import SemanticHead
-    global HF, WF
-    HF, WF = 384, 1280
+    from scenedino_amd import sscbench
     seg_fp8 = args.precision == "fp8"  # configs[4]: fp8 MFMA in the voxel MLP chain
-    net, _, _, _, _, _ = make_scene(0 if dist else rank, device, "bf16" if seg_fp8 else args.precision)
-    net.seg_precision = "fp8" if seg_fp8 else "bf16"
-    torch.manual_seed(5)
-    net.encoder.dim_reduction = MlpDimReduction(768, 64, 128).to(device).eval()
-    net.downstream_head = SemanticHead(19, 19, 768, 64).to(device).eval()
-    net.gt_classes = 19
-    dims = sscbench.grid_dims()
-    pts = sscbench.generate_point_grid(sscbench.read_calib()["Tr"], device=device)
+    net, pts, dims = c5_scene(device, args.precision, 0 if dist else rank)
     n_vox = pts.shape[0]
     timer = KernelTimer()
     net.kernel_timer = timer
@@ -353,7 +378,7 @@ def main_c5(args, world, rank, local_rank, dist, device, host_stage=False):
         if dist:
             x0, x1 = sscbench.slab_range(dims[0], rank, world)
             n_launch = (min(x1 + 1, dims[0]) - max(x0 - 1, 0)) * dims[1] * dims[2]
-        algo = n_launch * SEG_FLOPS_ALGO
+        algo = n_launch * SEG_FLOPS_ALGO  # the reference's unfolded head
         # HBM bytes per k_seg_head launch (1-GPU launch shape) from the committed PMC
         # summary (tools/c5_traffic.sh: FETCH_SIZE x 2 + WRITE_SIZE, separate passes)
         seg_traffic, seg_tsrc = None, None
@@ -364,7 +389,14 @@ def main_c5(args, world, rank, local_rank, dist, device, host_stage=False):
                 seg_tsrc = "profiles/r2_c5_traffic.json (rocprofv3 PMC, per launch)"
             except (KeyError, TypeError, ValueError):
                 seg_traffic = None
+        # the roofline is priced on the folded algorithm the kernel runs: its
+        # MFMA FLOPs per voxel, each product at its own dense peak (the fp8 norm product at
+        # 5 PF, the rest at 2.5 PF) -- the reference's FLOPs over the same time exceed the
+        # peak because the fold removes three quarters of them
         exe = n_launch * (SEG_FLOPS_EXEC_FP8 if seg_fp8 else SEG_FLOPS_EXEC)
+        f8 = n_launch * SEG_FLOPS_FP8_PART if seg_fp8 else 0
+        peak_eff = exe / ((exe - f8) / PEAK_TFLOPS["bf16"] + f8 / PEAK_TFLOPS["fp8"])
+        ach = exe / (seg_ms * 1e-3) / 1e12
         line = {
             "metric": "SSCBench voxel-grid query, voxels/sec (256x256x32 grid per frame)",
             "value": n_vox * args.steps / elapsed, "unit": "voxels/s", "n_gpus": world,
@@ -380,12 +412,14 @@ def main_c5(args, world, rank, local_rank, dist, device, host_stage=False):
                        "parallelism": (f"xslab{world}+allgather" if world > 1 else "1 frame")},
             "roofline": {
                 "kernel": "k_seg_head (sd_seg_query)", "bound": "mfma",
-                "achieved": algo / (seg_ms * 1e-3) / 1e12, "peak": PEAK_TFLOPS["bf16"],
-                "unit": "TFLOP/s", "frac": algo / (seg_ms * 1e-3) / 1e12 / PEAK_TFLOPS["bf16"],
+                "achieved": ach, "peak": peak_eff, "unit": "TFLOP/s", "frac": ach / peak_eff,
+                "peak_note": ("fp8 norm product at 5 PF, other products at 2.5 PF (FLOP-"
+                              "weighted)" if seg_fp8 else "bf16 dense MFMA"),
                 "traffic": seg_traffic, "traffic_source": seg_tsrc, "kernel_ms": seg_ms,
-                "algorithmic_flops_per_launch": algo, "executed_mfma_flops_per_launch": exe,
-                "executed_tflops": exe / (seg_ms * 1e-3) / 1e12,
-                "executed_frac": exe / (seg_ms * 1e-3) / 1e12 / PEAK_TFLOPS["bf16"],
+                "algorithmic_flops_per_launch": exe,
+                "algorithm": "folded head (M = Wn1 W2, L = Wl W2, Gram-form norm; DESIGN §5)",
+                "reference_flops_per_launch": algo,
+                "reference_equivalent_tflops": algo / (seg_ms * 1e-3) / 1e12,
                 "field_query_ms": field_ms,
                 "field_query_tflops": n_launch * mlp_flops_per_point() / (field_ms * 1e-3) / 1e12,
             },

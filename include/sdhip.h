@@ -169,7 +169,7 @@ typedef struct sd_render_args {
      * resnetfc.py:199). */
     float *work;
     /* Row strides (in floats) of depth / dino / rgb; 0 = dense (1, D, 3 nv).  Lets the caller
-     * render straight into one packed [depth | dino | rgb] row per ray, e.g. the send buffer
+     * render straight into one packed [dino | depth | rgb] row per ray, e.g. the send buffer
      * of the multi-GPU all-gather (sd_render_proj only; sd_render_fused requires 0). */
     int64_t ld_depth, ld_dino, ld_rgb;
 } sd_render_args;

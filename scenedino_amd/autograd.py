@@ -193,12 +193,16 @@ class FieldMLPFused(torch.autograd.Function):
     the ones columns).  x_aug (N, d_in + 1) f16 / bf16 rows of sd_field_gather."""
 
     @staticmethod
-    def forward(ctx, x_aug, w_in, b_in, w_out, b_out):
+    def forward(ctx, x_aug, w_in, b_in, w_out, b_out, C):
+        """C: the feature columns of x_aug (the grid's channels; the rest of d_in is the
+        positional code)."""
         N, ldx = x_aug.shape
         dh, d_in = w_in.shape
         D = w_out.shape[0] - 1
         dt = _lib.SD_OF_TORCH[x_aug.dtype]
-        C = d_in - 39
+        if not 0 < C < d_in or ldx < d_in + 1:
+            raise ValueError(f"FieldMLPFused: {C} feature columns do not fit rows of width "
+                             f"{ldx} for a {d_in}-input layer")
         p = _packed_train(w_in, b_in, w_out, b_out, dt, C)
         x_aug = x_aug.contiguous()
         dev = x_aug.device
@@ -217,7 +221,7 @@ class FieldMLPFused(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_sigma, g_dino):
         dx, *rest = FieldMLPFused.grads(ctx, g_sigma, g_dino, full_rows=True)
-        return (dx if ctx.needs_input_grad[0] else None, *rest)
+        return (dx if ctx.needs_input_grad[0] else None, *rest, None)
 
     @staticmethod
     def grads(ctx, g_sigma, g_dino, full_rows=False, dx16=False):
@@ -276,7 +280,7 @@ class FieldGatherMLP(torch.autograd.Function):
         if empty is not None:
             m = invf.reshape(N, 1)
             x[:, :C] = torch.where(m, empty.to(dt).view(1, C), x[:, :C])
-        sigma, dino = FieldMLPFused.forward(ctx, x, w_in, b_in, w_out, b_out)
+        sigma, dino = FieldMLPFused.forward(ctx, x, w_in, b_in, w_out, b_out, C)
         ctx.xyz, ctx.cam_f, ctx.grid_shape = xyz, cam_f, tuple(grid_nhwc.shape)
         ctx.acc = acc if acc is not None else GatherAcc()
         ctx.acc.n += 1

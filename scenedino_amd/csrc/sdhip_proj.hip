@@ -839,6 +839,12 @@ extern "C" int sd_render_proj(const sd_render_args *args, const sd_head *m, void
         sd_set_error("sd_render_proj: output row strides must be 0 (dense) or >= the row width");
         return -1;
     }
+    // the dino rows are written as 16-B vectors: the base and the row stride must keep every
+    // row 16-B aligned (packed rows put dino first: [dino | depth | rgb])
+    if (((uintptr_t)a.dino & 15) || (a.ld_dino % 4)) {
+        sd_set_error("sd_render_proj: dino must be 16-B aligned with ld_dino % 4 == 0");
+        return -1;
+    }
     if (!a.ld_depth) a.ld_depth = 1;
     if (!a.ld_dino) a.ld_dino = m->D;
     if (!a.ld_rgb) a.ld_rgb = 3 * a.nv;

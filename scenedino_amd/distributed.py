@@ -3,9 +3,10 @@
 Frames are independent units: frame f renders on rank f % world (C3, 1 frame per GPU)
 with no data-path collective; the only exchange is one all-gather of the rendered
 maps (depth, DINO, colour) so every rank (or rank 0) holds the full batch.  The render
-kernel writes its maps straight into packed [depth | dino | rgb] rows (BTSNet.render_into,
-sd_render_args output strides), which are the send buffer of ONE all_gather_into_tensor
-into a preallocated (world, R, 1 + D + 3 nv) receive buffer; MapGather double-buffers both
+kernel writes its maps straight into packed [dino | depth | rgb] rows (BTSNet.render_into,
+sd_render_args output strides; dino first so its 16-B stores stay aligned), which are the
+send buffer of ONE all_gather_into_tensor into a preallocated (world, R, D + 1 + 3 nv)
+receive buffer; MapGather double-buffers both
 so that frame i's gather (RCCL's own stream) overlaps frame i+1's render.  Within a
 frame, contiguous row bands of the image can be rendered on different ranks (ray-tile
 mode) -- each rank then owns a contiguous slice of the ray index r = (v H + y) W + x.
@@ -39,17 +40,18 @@ def row_band(H: int, rank: int, world: int) -> tuple[int, int]:
 
 
 def pack_maps(coarse: dict) -> torch.Tensor:
-    """Rendered maps of one frame -> one (R, 1 + D + 3 nv) float32 tensor
-    [depth | dino_features | rgb] (one collective instead of three)."""
+    """Rendered maps of one frame -> one (R, D + 1 + 3 nv) float32 tensor
+    [dino_features | depth | rgb] (one collective instead of three; the row layout
+    BTSNet.render_into writes)."""
     depth = coarse["depth"].reshape(-1, 1)
     R = depth.shape[0]
     dino = coarse["dino_features"].reshape(R, -1)
     rgb = coarse["rgb"].reshape(R, -1)
-    return torch.cat((depth.float(), dino.float(), rgb.float()), 1).contiguous()
+    return torch.cat((dino.float(), depth.float(), rgb.float()), 1).contiguous()
 
 
 def unpack_maps(maps: torch.Tensor, D: int) -> dict:
-    return {"depth": maps[:, 0], "dino_features": maps[:, 1:1 + D], "rgb": maps[:, 1 + D:]}
+    return {"depth": maps[:, D], "dino_features": maps[:, :D], "rgb": maps[:, D + 1:]}
 
 
 def gather_maps(maps: torch.Tensor, group=None, out: list | None = None) -> list:
@@ -68,22 +70,31 @@ def allreduce_grads(params, group=None) -> None:
     per-link latency floor, so one collective beats one per tensor).  Replaces what
     DistributedDataParallel does for the reference's trainer (base_trainer.py).  Every
     parameter that requires a gradient has a slot in the bucket (zeros where this rank
-    produced no gradient), so the layout is identical on every rank."""
+    produced no gradient), so the layout is identical on every rank; the bucket ends with
+    one has-gradient flag per parameter, and a parameter no rank produced a gradient for
+    keeps ``grad = None`` as under DDP (Adam skips it: no momentum step, no weight decay
+    on learn_empty's vector or the salience downsampler on steps that do not use them)."""
     import torch.distributed as dist
     ps = [p for p in params if p.requires_grad]
     if not ps:
         return
     world = dist.get_world_size(group)
     dev = ps[0].device
+    has = torch.tensor([0.0 if p.grad is None else 1.0 for p in ps], device=dev)
     flat = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1).to(dev)
-                      for p in ps])
+                      for p in ps] + [has])
     dist.all_reduce(flat, group=group)
+    # the flags are read back (one device sync) only when this rank lacks some gradient
+    any_grad = ((flat[-len(ps):] > 0).tolist() if any(p.grad is None for p in ps)
+                else [True] * len(ps))
     flat /= world
     o = 0
-    for p in ps:
+    for p, used in zip(ps, any_grad):
         n = p.numel()
         g = flat[o:o + n].view_as(p)
-        if p.grad is None:
+        if not used:
+            p.grad = None
+        elif p.grad is None:
             p.grad = g.clone()
         else:
             p.grad.copy_(g)

@@ -44,6 +44,32 @@ def _take(t, ids):
     return t[:, ids]
 
 
+def _crop(img, top: int, left: int, height: int, width: int):
+    """torchvision.transforms.functional.crop on a tensor: a slice, zero-filled where the
+    window leaves the image (torchvision's tensor crop pads the missing border with 0)."""
+    h, w = img.shape[-2:]
+    bottom, right = top + height, left + width
+    if top >= 0 and left >= 0 and bottom <= h and right <= w:
+        return img[..., top:bottom, left:right]
+    pad = (max(-left + min(0, right), 0), max(right - max(w, left), 0),
+           max(-top + min(0, bottom), 0), max(bottom - max(h, top), 0))
+    return F.pad(img[..., max(top, 0):bottom, max(left, 0):right], pad, value=0.0)
+
+
+def shift_loss_images(images_loss, shift, h: int, w: int):
+    """bts.py:197-205: ``transforms.Pad(8, padding_mode="edge")`` then
+    ``functional.crop(i = 8 + shift[0], j = 8 + shift[1], h, w)`` on the (n, v, 3, H, W)
+    loss images.  The reference tests ``shift != (0, 0)``, which is always True for the
+    trainer's tensor and a crop at (8, 8) is the identity, so a zero shift is skipped
+    here (same result, no copy)."""
+    s0, s1 = (int(v) for v in shift)  # the trainer's CPU tensor (no device sync)
+    if (s0, s1) == (0, 0):
+        return images_loss
+    n, v = images_loss.shape[:2]
+    x = F.pad(images_loss.flatten(0, 1), (8, 8, 8, 8), mode="replicate")  # torchvision "edge"
+    return _crop(x, 8 + s0, 8 + s1, h, w).unflatten(0, (n, v))
+
+
 class BTSNet(nn.Module):
     def __init__(self, conf, encoder: nn.Module, code_xyz, heads: dict,
                  final_pred_head: str | None = None, uncertainty_predictor: nn.Module | None = None,
@@ -86,7 +112,7 @@ class BTSNet(nn.Module):
         # (sd_render_fused, also the only fp32 path)
         self.fused_mode = conf.get("fused_mode", "proj")
         self.kernel_timer = None  # optional: .start(name) / .stop(name) around launches
-        self.render_into = None   # optional (R, 1 + D + 3 nv) f32 buffer for depth|dino|rgb
+        self.render_into = None   # optional (R, D + 1 + 3 nv) f32 buffer for dino|depth|rgb
         self._packed = None
         self._packed_key = None
         self._grid_cache = None
@@ -118,12 +144,15 @@ class BTSNet(nn.Module):
     def encode(self, images, Ks, poses_c2w, ids_encoder=None, ids_render=None, ids_loss=None,
                images_alt=None, combine_ids=None, color_frame_filter=None,
                loss_feature_grid_shift=None):
-        """Same semantics as bts.py:112-259 (encoder call, pose inversion, stored grids)."""
-        shift = (None if loss_feature_grid_shift is None
-                 else tuple(int(v) for v in loss_feature_grid_shift))  # trainer passes a tensor
-        if combine_ids is not None or shift not in (None, (0, 0)):
-            raise NotImplementedError("combine_ids / loss_feature_grid_shift are training-only "
-                                      "options outside the MI355X hot path")
+        """Same semantics as bts.py:112-259 (encoder call, pose inversion, stored grids).
+
+        loss_feature_grid_shift (trainer.py:186-198 passes ``torch.randint(-p/2, p/2, (2,))``
+        every training step): the loss images are edge-padded by 8 and cropped at
+        (8 + s0, 8 + s1) before the gt-encoder pass (bts.py:197-205), see
+        ``shift_loss_images``."""
+        if combine_ids is not None:
+            raise NotImplementedError("combine_ids is a multi-view training option outside "
+                                      "the MI355X hot path (every shipped config passes None)")
         with torch.autocast(device_type=images.device.type, enabled=False):
             # torch.inverse's LU (same kernels) without its device-to-host error check,
             # which would stall the launch queue once per frame
@@ -173,6 +202,8 @@ class BTSNet(nn.Module):
         # the ground-truth (loss) features: a second ViT pass (bts.py:207) that only the
         # training loss reads -- run on first access of grid_l_loss_features (SURVEY
         # §8(f) rank 3), so a pure render / voxel query never pays for it
+        if loss_feature_grid_shift is not None:
+            images_loss = shift_loss_images(images_loss, loss_feature_grid_shift, h_, w_)
         gt_in = images_loss.reshape(n_l * nv_l, c_, h_, w_).detach().clone()
         self._loss_pending = (gt_in, n_l, nv_l)
         self._loss_features = None
@@ -358,13 +389,14 @@ class BTSNet(nn.Module):
         nv = gc["nv"]
         maps = getattr(self, "render_into", None)
         if maps is not None:
-            # render straight into packed [depth | dino | rgb] rows (the all-gather send
-            # buffer of the multi-GPU path): strided views, no pack copy
-            if not proj or tuple(maps.shape) != (R, 1 + m.D + 3 * nv) or maps.stride(1) != 1 \
+            # render straight into packed [dino | depth | rgb] rows (the all-gather send
+            # buffer of the multi-GPU path): strided views, no pack copy; dino leads the
+            # row so its 16-B vector stores stay aligned (width 68 at D = 64, nv = 1)
+            if not proj or tuple(maps.shape) != (R, m.D + 1 + 3 * nv) or maps.stride(1) != 1 \
                     or maps.dtype != torch.float32 or maps.device != dev:
-                raise ValueError(f"render_into must be a float32 ({R}, {1 + m.D + 3 * nv}) row-major "
+                raise ValueError(f"render_into must be a float32 ({R}, {m.D + 1 + 3 * nv}) row-major "
                                  "tensor on the render device (16-bit projected render)")
-            depth, dino, rgb = maps[:, 0], maps[:, 1:1 + m.D], maps[:, 1 + m.D:]
+            dino, depth, rgb = maps[:, :m.D], maps[:, m.D], maps[:, m.D + 1:]
         else:
             depth = torch.empty(R, device=dev)
             dino = torch.empty(R, m.D, device=dev)
@@ -448,11 +480,12 @@ class BTSNet(nn.Module):
         self._timed("field", lambda: _lib.field_query(args, m.rec, xyz))
         return sigma, dino, rgb, inv, invf
 
-    @staticmethod
-    def _fused_train_mlp(head, C) -> bool:
+    def _fused_train_mlp(self, head, C) -> bool:
         """Training under a 16-bit autocast with the shipped head (ResnetFC n_blocks = 0,
-        ReLU, d_hidden 128, D <= 64): gather + MLP as the fused sd_mlp_train kernels."""
+        ReLU, d_hidden 128, D <= 64, input = C grid channels + the positional code):
+        gather + MLP as the fused sd_mlp_train kernels."""
         return (torch.is_autocast_enabled("cuda")
+                and head.lin_in.in_features == C + self.code_xyz.d_out
                 and torch.get_autocast_dtype("cuda") in (torch.float16, torch.bfloat16)
                 and type(head).__name__ == "ResnetFC" and getattr(head, "n_blocks", 1) == 0
                 and getattr(head, "d_latent", 1) == 0 and isinstance(head.activation, nn.ReLU)

@@ -29,7 +29,7 @@ def test_pack_unpack_roundtrip():
     c = {"depth": torch.rand(1, R), "dino_features": torch.rand(1, R, D),
          "rgb": torch.rand(1, R, 3 * nv)}
     m = sdd.pack_maps(c)
-    assert m.shape == (R, 1 + D + 3)
+    assert m.shape == (R, D + 1 + 3)
     u = sdd.unpack_maps(m, D)
     assert torch.equal(u["depth"], c["depth"].reshape(R))
     assert torch.equal(u["dino_features"], c["dino_features"].reshape(R, D))
@@ -95,7 +95,8 @@ def _grad_worker(rank, world, port, q):
         lin.weight.grad = torch.randn(3, 5, generator=g)
         b = torch.randn(3, generator=g)
         lin.bias.grad = b if rank == 0 else None  # rank 1 produced no bias gradient
-        sdd.allreduce_grads(lin.parameters())
+        unused = torch.nn.Parameter(torch.zeros(4))  # no gradient on any rank (DDP: stays None)
+        sdd.allreduce_grads(list(lin.parameters()) + [unused])
         ws, bs = [], []
         for r in range(world):
             g2 = torch.Generator().manual_seed(r)
@@ -103,7 +104,7 @@ def _grad_worker(rank, world, port, q):
             b2 = torch.randn(3, generator=g2)
             bs.append(b2 if r == 0 else torch.zeros(3))
         ok = torch.allclose(lin.weight.grad, sum(ws) / world, atol=1e-6) and \
-            torch.allclose(lin.bias.grad, sum(bs) / world, atol=1e-6)
+            torch.allclose(lin.bias.grad, sum(bs) / world, atol=1e-6) and unused.grad is None
         dist.barrier()
         q.put((rank, bool(ok)))
     finally:

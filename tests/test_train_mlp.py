@@ -64,7 +64,7 @@ def test_fused_mlp_vs_autocast_linear(N, dt):
     x = x.to(dt)
     ps = [t.clone().requires_grad_(True) for t in (W_in, b_in, W_out, b_out)]
     xr = x.clone().requires_grad_(True)
-    sig, dino = FieldMLPFused.apply(xr, *ps)
+    sig, dino = FieldMLPFused.apply(xr, *ps, 256)
     gs = torch.randn(N, device=dev, generator=g)
     gd = torch.randn(N, 64, device=dev, generator=g)
     ((sig * gs).sum() + (dino * gd).sum()).backward()
