@@ -213,14 +213,49 @@ def offset_render_pose(pose):
     return p
 
 
+def host_cpus() -> dict:
+    """os.cpu_count(), the affinity mask's CPUs and the cgroup CPU quota (cgroup v2
+    cpu.max or v1 cfs quota / period); usable = the smallest of them."""
+    import math
+    n = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = None
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        try:
+            q = float(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = float(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    # the job's CPU share as the GPU box states it (OMP_NUM_THREADS is set to it there)
+    try:
+        share = int(os.environ.get("OMP_NUM_THREADS", "0")) or None
+    except ValueError:
+        share = None
+    usable = min(v for v in (n, aff, math.ceil(quota) if quota else None, share) if v)
+    return {"cpu_count": n, "affinity": aff, "quota": quota, "share": share,
+            "usable": max(1, usable)}
+
+
 def cpu_baseline(budget_s: float = 20.0, offset_pose: bool = True):
     """Oracle (pure-PyTorch CPU restatement of the reference, fp32) on the host cores:
     renders whole image rows of the same C2 frame (rays from the offset render pose, as
-    the reported GPU value) until ~budget_s of CPU work, on os.cpu_count() threads (SURVEY
-    §8(d); SD_CPU_THREADS overrides)."""
+    the reported GPU value) until ~budget_s of CPU work, on every host CPU this process
+    may use (SURVEY §8(d) asks for os.cpu_count(); that is capped by the affinity mask, the
+    cgroup CPU quota and the job's CPU share (OMP_NUM_THREADS, 16 on the one-GPU box of
+    a 256-CPU host): 256 threads there measured 203 rays/s, oversubscribed, 50x slower
+    than 16; SD_CPU_THREADS overrides)."""
     from oracle import render_oracle as O
 
-    threads = int(os.environ.get("SD_CPU_THREADS", os.cpu_count() or 1))
+    threads = int(os.environ.get("SD_CPU_THREADS", host_cpus()["usable"]))
     torch.set_num_threads(threads)
     g = torch.Generator().manual_seed(0)
     images = torch.rand(1, 1, 3, H, W, generator=g) * 2 - 1
@@ -260,12 +295,10 @@ def cpu_baseline(budget_s: float = 20.0, offset_pose: bool = True):
                     break
     except OSError:
         pass
-    try:
-        usable = len(os.sched_getaffinity(0))
-    except (AttributeError, OSError):
-        usable = None
+    hc = host_cpus()
     return {"value": done_rays / dt, "unit": "rays/s", "cores": threads, "kind": "port",
-            "cpu_count": os.cpu_count(), "affinity_cpus": usable,
+            "cpu_count": hc["cpu_count"], "affinity_cpus": hc["affinity"],
+            "cgroup_cpu_quota": hc["quota"], "job_cpu_share": hc["share"],
             "sample": f"{done_rays} rays ({row} of {H} rows) of the same 192x640x64 frame"
                       f"{' (offset render pose)' if offset_pose else ''}, "
                       f"fp32 torch-CPU oracle restatement, {dt:.1f} s on {threads} threads "
