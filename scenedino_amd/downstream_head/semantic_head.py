@@ -21,6 +21,8 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
+from .. import _lib
+
 
 def _norm(x):
     # semantic_head.py:37-38
@@ -114,8 +116,34 @@ class SemanticHead(nn.Module):
                    knn_neighbors=g("knn_neighbors", 0), mode=g("mode", "2d"),
                    mlp_head=g("mlp_head", False), apply_crf=g("apply_crf", False))
 
+    def _folded_labels(self, features):
+        """segs_pred of mode stego_kmeans for features that MlpDimReduction.transform_expand
+        produced (and nobody modified since): the folded kernel sd_seg_query on the 64-d codes
+        (transform_expand + stego + k-means in registers), or None."""
+        prov = getattr(features, "_sd_expand", None)
+        if prov is None or features.requires_grad or torch.is_grad_enabled() and self.training:
+            return None
+        codes, dr, key, version = prov
+        from ...seg_pack import PackedSegHead, seg_key
+        if features._version != version or seg_key(dr) != key:
+            return None
+        hkey = seg_key(dr, self.stego_head, self.stego_cluster_head)
+        cache = getattr(self, "_fold_cache", None)
+        if cache is None or cache[0] != hkey or cache[1] is not dr:
+            cache = self._fold_cache = (hkey, dr, PackedSegHead(
+                dr, self.stego_head, self.stego_cluster_head, device=codes.device))
+        labels, _, _ = _lib.seg_query(codes, cache[2].rec, want_labels=True)
+        return labels.view(features.shape[:-1]).long()
+
     def forward(self, features, mode="stego_kmeans"):
-        """semantic_head.py:107-120 (segs_pred for the given mode)."""
+        """semantic_head.py:107-120 (segs_pred for the given mode).  stego_kmeans on
+        features straight from MlpDimReduction.transform_expand (the 2-D demo's
+        expand_dim -> downstream_head) runs as the folded sd_seg_query kernel on their
+        64-d codes; any other input or mode evaluates the chain with device tensor ops."""
+        if mode == "stego_kmeans":
+            labels = self._folded_labels(features)
+            if labels is not None:
+                return labels
         features = _norm(features)
         if mode == "stego_kmeans":
             return self.stego_cluster_head(self.stego_head(features))["segs_pred"]

@@ -51,7 +51,13 @@ class MlpDimReduction(nn.Module):
         if torch.is_grad_enabled() and self.training:
             raise NotImplementedError("scenedino_amd: transform_expand has no backward kernel; "
                                       "use eval() / torch.no_grad()")
+        from ....seg_pack import seg_key
         lead = features.shape[:-1]
         x = features.reshape(-1, features.shape[-1]).float().contiguous()
         _, _, full = _lib.seg_query(x, self._rec().rec, want_labels=False, want_full=True)
-        return full.view(*lead, -1)
+        out = full.view(*lead, -1)
+        # provenance for SemanticHead.forward: the expanded features of these codes, so the
+        # 2-D demo's head call on them (demo_utils/utils.py:228-232) runs the folded
+        # stego / k-means kernel on the 64-d codes instead of library GEMMs on 768-d rows
+        out._sd_expand = (x, self, seg_key(self), out._version)
+        return out

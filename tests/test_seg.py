@@ -373,6 +373,48 @@ def test_seg_query_vs_reference(gpu, d_full):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("d_full", [768, 384])
+def test_demo_expand_then_head_runs_folded_kernel(gpu, d_full, monkeypatch):
+    """demo_utils/utils.py:228-232 (inference_rendered_2d): dino_full =
+    encoder.expand_dim(codes), seg = downstream_head(dino_full, "stego_kmeans").  The head
+    call on transform_expand's own output runs sd_seg_query on the 64-d codes (no 768-d
+    GEMMs): labels equal the folded kernel's, and the reference's wherever its margin
+    > 2e-2 (>= 99 % overall).  Features modified after the expansion, or another mode, take
+    the generic device chain."""
+    from scenedino_amd import _lib
+    from scenedino_amd.downstream_head import SemanticHead
+    from scenedino_amd.seg_pack import PackedSegHead
+    d = load("seg_head.npz")
+    t = f"_{d_full}"
+    p = seg_params(d, t)
+    dr, st, cl = (m.to(gpu) for m in modules_from(p))
+    head = SemanticHead(19, 19, d_full, 64).to(gpu).eval()
+    head.stego_head.load_state_dict(st.state_dict())
+    head.stego_cluster_head.load_state_dict(cl.state_dict())
+    x = torch.as_tensor(d["x" + t]).to(gpu).view(8, -1, 64)  # an (H, W, 64) code map
+    calls = []
+    real = _lib.seg_query
+    monkeypatch.setattr(_lib, "seg_query", lambda *a, **k: calls.append(k) or real(*a, **k))
+    with torch.no_grad():
+        full = dr.transform_expand(x)
+        seg = head(full, mode="stego_kmeans")
+    assert [c.get("want_full", False) for c in calls] == [True, False]  # expand, then head
+    assert seg.shape == x.shape[:-1] and seg.dtype == torch.long
+    ref_labels, _, _ = real(x.reshape(-1, 64), PackedSegHead(dr, st, cl).rec, want_labels=True)
+    assert torch.equal(seg.reshape(-1), ref_labels.long())
+    _, ref_scores, _ = SO.seg_head(torch.as_tensor(d["x" + t]), p)
+    _label_check(seg.reshape(-1).cpu(), ref_scores, d["labels" + t], "demo head labels")
+    # generic chain: a modified tensor loses its provenance (and still agrees)
+    with torch.no_grad():
+        full2 = dr.transform_expand(x)
+        full2.mul_(1.0)
+        n = len(calls)
+        seg2 = head(full2, mode="stego_kmeans")
+    assert len(calls) == n
+    _label_check(seg2.reshape(-1).cpu(), ref_scores, d["labels" + t], "generic head labels")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d_full", [768, 384])
 def test_seg_query_fp8_vs_reference(gpu, d_full):
     """BASELINE configs[4] fp8 record (k_seg_head<2, F8>): labels >= 99 % equal to the
     reference's and identical wherever its top-2 margin exceeds 2e-2; the alpha pick on top;
