@@ -219,7 +219,7 @@ k_render_proj(const sd_render_args a, const sd_head m, const int32_t *__restrict
         // list mode: workgroups without a listed ray leave before staging the weights (the
         // list is usually short or empty; the grid is sized for the worst case)
         const int nx0 = (gridDim.x % 8 == 0) ? 8 : 1;
-        const int64_t ra = (int64_t)__builtin_amdgcn_readfirstlane(list[0]) * 8;
+        const int64_t ra = (int64_t)__builtin_amdgcn_readfirstlane(list[0]) * SD_LIST_BLK;
         const int64_t x0 = blockIdx.x % nx0;
         if ((ra * x0 / nx0) + (int64_t)(blockIdx.x / nx0) * (SD_RWG / 64) >= ra * (x0 + 1) / nx0) return;
     }
@@ -256,12 +256,12 @@ k_render_proj(const sd_render_args a, const sd_head m, const int32_t *__restrict
     const int xcd = blockIdx.x % nx;
     const int nwaves = (gridDim.x / nx) * (SD_RWG / 64);
     const int rps = (int)a.rays_per_sb;
-    // list != NULL (fallback behind the tile kernel): the rays of the groups listed in
-    // list[1 .. list[0]] (8 consecutive rays each) form the virtual ray sequence
+    // list != NULL (fallback behind the tile kernel): the rays of the blocks listed in
+    // list[1 .. list[0]] (SD_LIST_BLK consecutive rays each) form the virtual ray sequence
     const int Rreal = (int)a.R;
-    const int64_t RA = list ? (int64_t)__builtin_amdgcn_readfirstlane(list[0]) * 8 : a.R;
+    const int64_t RA = list ? (int64_t)__builtin_amdgcn_readfirstlane(list[0]) * SD_LIST_BLK : a.R;
     auto rmap = [&](int v) {
-        return list ? min(list[1 + (v >> 3)] * 8 + (v & 7), Rreal - 1) : v;
+        return list ? min(list[1 + v / SD_LIST_BLK] * SD_LIST_BLK + v % SD_LIST_BLK, Rreal - 1) : v;
     };
     const int R = (int)(RA * (xcd + 1) / nx);
     const int ray0 = (int)(RA * xcd / nx) + (blockIdx.x / nx) * (SD_RWG / 64) + wave;
@@ -653,12 +653,13 @@ k_head_hc(const float *__restrict__ work, int64_t R, const sd_head m, float *__r
     const int lane = threadIdx.x & 63, j = lane & 15, g = lane >> 4;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // list != NULL: the rays of the listed groups (see k_render_proj)
-    const int64_t RA = list ? (int64_t)__builtin_amdgcn_readfirstlane(list[0]) * 8 : R;
+    const int64_t RA = list ? (int64_t)__builtin_amdgcn_readfirstlane(list[0]) * SD_LIST_BLK : R;
     const int64_t ntile = (RA + 15) / 16;
     for (int64_t tile = (int64_t)blockIdx.x * (SD_PWG / 64) + wave; tile < ntile;
          tile += (int64_t)gridDim.x * (SD_PWG / 64)) {
         const int64_t v = min(tile * 16 + j, RA - 1);
-        const int64_t ray = list ? min((int64_t)list[1 + (v >> 3)] * 8 + (v & 7), R - 1) : tile * 16 + j;
+        const int64_t ray = list ? min((int64_t)list[1 + v / SD_LIST_BLK] * SD_LIST_BLK + v % SD_LIST_BLK, R - 1)
+                                 : tile * 16 + j;
         const float *hs = work + (ray < R ? ray : R - 1) * SD_HC_STRIDE;
         Frag B[4];
 #pragma unroll
@@ -806,7 +807,7 @@ static int64_t sd_hc_bytes(int64_t R, int32_t D) {
     return sd_head_hc(D) ? R * SD_HC_STRIDE * (int64_t)sizeof(float) : 0;
 }
 extern "C" int64_t sd_render_proj_work_bytes(int64_t R, int32_t D) {
-    return sd_hc_bytes(R, D) + ((4 * (1 + (R + 7) / 8) + 15) / 16) * 16;
+    return sd_hc_bytes(R, D) + ((4 * (1 + (R + SD_LIST_BLK - 1) / SD_LIST_BLK) + 15) / 16) * 16;
 }
 
 extern "C" int sd_render_tile_ok(const sd_render_args *a, const sd_head *m);

@@ -3,6 +3,9 @@
 #pragma once
 #ifndef SD_PE_DIRECT
 #define SD_PE_DIRECT 0
+// overflow list of the tile kernel: entries are blocks of SD_LIST_BLK consecutive rays
+// (a group of 8 or 12 rays lists 2 or 3 blocks); the fallback kernels render the blocks
+#define SD_LIST_BLK 4
 #endif
 #include "sdhip_point.h"
 

@@ -32,8 +32,11 @@
 // D / 16 MFMA tiles spread over the waves.
 #include "sdhip_render.h"
 
-#define ST_WAVES 8
-#define ST_WG (64 * ST_WAVES)
+// waves per workgroup = rays per group (NW): 8 (2 waves per SIMD), or for K <= 64 the
+// ST_NW_SMALLK-wave variant (12: 3 waves per SIMD, the kernel compiled for <= 168 VGPRs)
+#ifndef ST_NW_SMALLK
+#define ST_NW_SMALLK 8
+#endif
 #define ST_TEX 288          // LDS bytes per staged texel: 256 B of P + 32 B pad
 #define ST_TEXQ 18          // 16-byte chunks per staged texel
 #define ST_MAXP 2           // K <= 128 (two samples per lane in the ray pass)
@@ -120,7 +123,7 @@ struct st_args {
     sd_render_args a;
     sd_head m;
     int32_t *ovf;           // [0]: overflow count, [1 + i]: overflowed group index
-    int32_t ngroups;        // ceil(R / 8)
+    int32_t ngroups;        // ceil(R / NW)
     int32_t tile_bytes;     // bytes per tile buffer (multiple of 1024)
 };
 
@@ -128,14 +131,15 @@ struct st_args {
 #define ST_L_PE 0                              // [8][64] x 16 B code A fragments (16x16x32)
 #define ST_L_PE1 (ST_L_PE + 8 * 64 * 16)      // [8][64] x 8 B code A fragments (16x16x16)
 #define ST_L_SIG (ST_L_PE1 + 8 * 64 * 8)      // [4][64] x 16 B sigma A fragments
-#define ST_L_BOX (ST_L_SIG + 4 * 64 * 16)      // [2][8 waves][2 halves] u32 (min, max) packed
-#define ST_L_HS (ST_L_BOX + 2 * 8 * 16)        // [8 rays][128] 16-bit hidden sums
-#define ST_L_WS (ST_L_HS + 8 * 128 * 2)        // [8] f32 weight sums
-#define ST_L_RAY (ST_L_WS + 8 * 4)             // [8 waves][2] x 32 B ray words 0..7 (LDS-DMA)
-#define ST_L_REC (ST_L_RAY + 8 * 2 * 32)       // records: [8 waves][2][K] x 40 B
-static_assert(ST_L_REC % 16 == 0, "record area alignment");
+#define ST_L_BOX (ST_L_SIG + 4 * 64 * 16)      // [2][NW waves][2 halves] u32 (min, max) packed
+// then, sized by NW (waves = rays per group):
+__host__ __device__ constexpr int st_l_hs(int nw) { return ST_L_BOX + 2 * nw * 16; }  // [NW rays][128] 16-bit hidden sums
+__host__ __device__ constexpr int st_l_ws(int nw) { return st_l_hs(nw) + nw * 128 * 2; }  // [NW] f32 weight sums
+__host__ __device__ constexpr int st_l_ray(int nw) { return st_l_ws(nw) + 16 * 4; }  // [NW waves][2] x 32 B ray words 0..7 (LDS-DMA)
+__host__ __device__ constexpr int st_l_rec(int nw) { return st_l_ray(nw) + nw * 2 * 32; }  // records: [NW waves][2][K] x 40 B
+static_assert(st_l_rec(8) % 16 == 0 && st_l_rec(12) % 16 == 0, "record area alignment");
 
-__host__ __device__ constexpr int st_rec_bytes(int K) { return ST_WAVES * 2 * K * 40; }
+__host__ __device__ constexpr int st_rec_bytes(int nw, int K) { return nw * 2 * K * 40; }
 
 // packed u16x2 (x | y << 16) component-wise min / max
 __device__ __forceinline__ uint32_t st_min2(uint32_t a, uint32_t b) {
@@ -231,9 +235,12 @@ __device__ __forceinline__ uint2 st_tr(uint32_t addr) {
 // ZIN: depths given (args.z, parity tests) instead of drawn in the kernel.  A template
 // parameter, not a branch: with both paths in one body the compiler's wait for the z loads
 // also drains the head-weight prefetch on the drawing path.
-template <int P, bool ZIN>
-__global__ void __launch_bounds__(ST_WG) __attribute__((amdgpu_waves_per_eu(2)))
+template <int P, bool ZIN, int NW>
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4)))
 k_render_tile(const st_args sa) {
+    constexpr int ST_WAVES = NW;
+    constexpr int ST_L_HS = st_l_hs(NW), ST_L_WS = st_l_ws(NW), ST_L_RAY = st_l_ray(NW),
+                  ST_L_REC = st_l_rec(NW);
     typedef T16<P> Tr;
     typedef typename Tr::Frag Frag;
     typedef typename Tr::Frag4 Frag4;
@@ -269,7 +276,7 @@ k_render_tile(const st_args sa) {
     auto rq0 = [&](int buf) { return (uint4 *)(lds + rec_base + buf * K * 40); };
     auto rq1 = [&](int buf) { return (f32x4 *)(lds + rec_base + buf * K * 40 + K * 16); };
     auto rqc = [&](int buf) { return (float2 *)(lds + rec_base + buf * K * 40 + K * 32); };
-    const uint32_t tile0 = ST_L_REC + st_rec_bytes(K);
+    const uint32_t tile0 = ST_L_REC + st_rec_bytes(NW, K);
     const int tcap = sa.tile_bytes / ST_TEX;
 
     // XCD-aware group ranges (workgroups b, b + 8, ... share an XCD, speed only)
@@ -475,9 +482,10 @@ k_render_tile(const st_args sa) {
             }
         }
         if (!t.ok) {
-            if (wave == 0 && lane == 0) {
-                const int i = atomicAdd(sa.ovf, 1);
-                sa.ovf[1 + i] = grp;
+            if (wave == 0 && lane == 0) {  // the group's rays as NW / SD_LIST_BLK list blocks
+                const int i = atomicAdd(sa.ovf, NW / SD_LIST_BLK);
+                for (int b = 0; b < NW / SD_LIST_BLK; ++b)
+                    sa.ovf[1 + i + b] = grp * (NW / SD_LIST_BLK) + b;
             }
             return t;
         }
@@ -497,7 +505,7 @@ k_render_tile(const st_args sa) {
     };
     auto head = [&](int grp) {
         if (wave >= ndt) return;
-        const int slot = j & 7;
+        const int slot = j < NW ? j : 0;  // B columns j >= NW: not stored
         Frag Bh[4];
         const uint8_t *hs = lds + ST_L_HS + slot * 256;
 #pragma unroll
@@ -507,8 +515,8 @@ k_render_tile(const st_args sa) {
             Bh[s] = __builtin_bit_cast(Frag, uint4{lo.x, lo.y, hi.x, hi.y});
         }
         const float ws = *(const float *)(lds + ST_L_WS + slot * 4);
-        const int ray = 8 * grp + j;
-        const bool store = j < 8 && ray < R;
+        const int ray = NW * grp + j;
+        const bool store = j < NW && ray < R;
         for (int dt = wave; dt < ndt; dt += ST_WAVES) {
             const Frag *wo = (const Frag *)m.w_out + (int64_t)dt * 4 * SD_WAVE + lane;
             f32x4 o = {0.f, 0.f, 0.f, 0.f};
@@ -540,10 +548,10 @@ k_render_tile(const st_args sa) {
 
     // ---- prologue: records + tile of step 0 -------------------------------------------
     int grp = gfirst;
-    int ray = 8 * grp + wave;
-    int sbi = __builtin_amdgcn_readfirstlane((int)((unsigned)min(8 * grp, R - 1) / (unsigned)rps));
+    int ray = NW * grp + wave;
+    int sbi = __builtin_amdgcn_readfirstlane((int)((unsigned)min(NW * grp, R - 1) / (unsigned)rps));
     ray_fetch(ray, 0);
-    ray_fetch(8 * (grp + nwg) + wave, 1);
+    ray_fetch(NW * (grp + nwg) + wave, 1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     ray_pass(ray, 0, 0);
     ray_col(ray, 0);
@@ -562,8 +570,8 @@ k_render_tile(const st_args sa) {
         const int buf = n & 1;
         const bool has_next = n + 1 < nsteps;
         const int ngrp = grp + nwg;
-        const int nray = 8 * ngrp + wave;
-        const int nsbi = has_next ? __builtin_amdgcn_readfirstlane((int)((unsigned)min(8 * ngrp, R - 1) / (unsigned)rps)) : 0;
+        const int nray = NW * ngrp + wave;
+        const int nsbi = has_next ? __builtin_amdgcn_readfirstlane((int)((unsigned)min(NW * ngrp, R - 1) / (unsigned)rps)) : 0;
         const bool active = cur.ok && ray < R;
         const uint32_t tileb = lds0 + tile0 + (uint32_t)buf * (uint32_t)sa.tile_bytes;
         uint32_t lane_off = (uint32_t)((tq & 1) + (tq >> 1) * cur.pitch) * ST_TEX + 8u * (uint32_t)tp;
@@ -889,7 +897,7 @@ k_render_tile(const st_args sa) {
         ray = nray;
         sbi = nsbi;
         cur = nxt;
-        if (n + 2 < nsteps) ray_fetch(8 * (ngrp + nwg) + wave, buf);  // ray of step n + 2
+        if (n + 2 < nsteps) ray_fetch(NW * (ngrp + nwg) + wave, buf);  // ray of step n + 2
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed
         ST_T(8);
         st_barrier_lds();  // Y: next tile complete; hsum of this group written
@@ -923,8 +931,11 @@ static int sd_check_last(const char *what) {
     return 0;
 }
 
+static int st_nw(int K) { return K <= 64 ? ST_NW_SMALLK : 8; }
+
 static int st_tile_bytes(int K) {
-    const int fixed = ST_L_REC + st_rec_bytes(K);
+    const int nw = st_nw(K);
+    const int fixed = st_l_rec(nw) + st_rec_bytes(nw, K);
     const int avail = 160 * 1024 - fixed;
     return ((avail / 2) / 1024) * 1024;
 }
@@ -932,7 +943,7 @@ static int st_tile_bytes(int K) {
 // Can the tile kernel take this render?  (colour in exactly one render view, batches of
 // whole groups, K <= 128, room for one tile buffer pair.)
 extern "C" int sd_render_tile_ok(const sd_render_args *a, const sd_head *m) {
-    return a->nv == 1 && a->K % 16 == 0 && a->K <= 128 && a->rays_per_sb % 8 == 0 &&
+    return a->nv == 1 && a->K % 16 == 0 && a->K <= 128 && a->rays_per_sb % st_nw(a->K) == 0 &&
            m->D % 16 == 0 && m->D <= 512 && a->Wf < 32768 && a->Hf < 32768 &&
            st_tile_bytes(a->K) >= 16 * 1024;
 }
@@ -945,9 +956,10 @@ extern "C" int sd_render_tile_launch(const sd_render_args *a, const sd_head *m, 
     sa.a = *a;
     sa.m = *m;
     sa.ovf = ovf;
-    sa.ngroups = (int)((a->R + 7) / 8);
+    const int nw = st_nw(a->K);
+    sa.ngroups = (int)((a->R + nw - 1) / nw);
     sa.tile_bytes = st_tile_bytes(a->K);
-    const int lds_bytes = ST_L_REC + st_rec_bytes(a->K) + 2 * sa.tile_bytes;
+    const int lds_bytes = st_l_rec(nw) + st_rec_bytes(nw, a->K) + 2 * sa.tile_bytes;
     if (hipMemsetAsync(ovf, 0, sizeof(int32_t), s) != hipSuccess) {
         sd_set_error("sd_render_proj: overflow counter reset failed");
         return -2;
@@ -958,13 +970,20 @@ extern "C" int sd_render_tile_launch(const sd_render_args *a, const sd_head *m, 
         ncu = 256;
     auto go = [&](auto kern) {
         (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
-        hipLaunchKernelGGL(kern, dim3((unsigned)ncu), dim3(ST_WG), lds_bytes, s, sa);
+        hipLaunchKernelGGL(kern, dim3((unsigned)ncu), dim3(64 * nw), lds_bytes, s, sa);
     };
     const bool zin = a->z != nullptr;
-    if (m->dtype == SD_F16) {
-        if (zin) go(k_render_tile<SD_F16, true>); else go(k_render_tile<SD_F16, false>);
-    } else {
-        if (zin) go(k_render_tile<SD_BF16, true>); else go(k_render_tile<SD_BF16, false>);
+#define ST_GO(NWV)                                                                              \
+    if (m->dtype == SD_F16) {                                                                   \
+        if (zin) go(k_render_tile<SD_F16, true, NWV>); else go(k_render_tile<SD_F16, false, NWV>); \
+    } else {                                                                                    \
+        if (zin) go(k_render_tile<SD_BF16, true, NWV>); else go(k_render_tile<SD_BF16, false, NWV>); \
     }
+    if (nw == 8) {
+        ST_GO(8)
+    } else {
+        ST_GO(ST_NW_SMALLK)
+    }
+#undef ST_GO
     return sd_check_last("sd_render_proj (tile kernel)");
 }

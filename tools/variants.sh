@@ -8,7 +8,7 @@ FLAGS=$(python -c "import sys; sys.path.insert(0,'scenedino_amd'); import build;
 SRCS=$(python -c "import sys; sys.path.insert(0,'scenedino_amd'); import build; print(' '.join('scenedino_amd/'+s for s in build.SOURCES))")
 for spec in "$@"; do
   name=${spec%%=*}; extra=${spec#*=}
-  /opt/rocm/bin/hipcc $FLAGS $extra -o scenedino_amd/variants/libsdhip_$name.so $SRCS &
+  /opt/rocm/bin/hipcc $FLAGS -shared $extra -o scenedino_amd/variants/libsdhip_$name.so $SRCS &
 done
 wait
 ls -la scenedino_amd/variants
