@@ -233,6 +233,11 @@ typedef struct sd_field_args {
     int32_t dino_dtype;/* SD_F32 (0), or SD_BF16: dino written as bf16 (the input a
                         * following sd_seg_query rounds to bf16 anyway: half the bytes) */
     int32_t pad0;
+    /* Visiting order of the ceil(B P / 32) tiles of 32 consecutive points, or NULL (natural
+     * order).  Speed only (every output stays at its point's index): an order in which
+     * consecutive tiles project onto neighbouring texels keeps the grid taps in the XCD's
+     * L2 (the SSCBench voxel columns sorted by projected pixel, BTSNet.query). */
+    const int32_t *tile_order;
 } sd_field_args;
 
 int sd_field_query(const sd_field_args *args, const sd_mlp *mlp, void *stream);
@@ -401,6 +406,14 @@ typedef struct sd_gemm_args {
 } sd_gemm_args;
 
 int sd_gemm(const sd_gemm_args *args, void *stream);
+
+/* nn.LayerNorm(K, eps) fused into the prologue of a GEMM (timm Block: norm1 -> attn.qkv,
+ * norm2 -> mlp.fc1, vit.py:112-189 over timm's VisionTransformer): out = EPI(LN(x) W^T + b)
+ * for x (M, K) f32 rows (K = C in {384, 768}), W = args->w (N, K) bf16; args->a is unused.
+ * epi SD_EPI_QKV / SD_EPI_GELU / SD_EPI_BF16 with the sd_gemm fields they read.  The
+ * normalised rows are the bf16 ones sd_layernorm would write (same arithmetic). */
+int sd_ln_gemm(const sd_gemm_args *args, const float *x, const float *ln_w, const float *ln_b,
+               float eps, void *stream);
 
 /* softmax(q k^T * scale) v per (batch, head); q (B,H,T,64), k (B,H,Tp,64),
  * vt (B,H,64,Tp) bf16 with rows/columns T..Tp-1 zero; out (B, T, H*64) bf16. */

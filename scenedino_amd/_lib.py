@@ -14,7 +14,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # SDHIP_LIB: alternative build of the same library (diagnostic builds only)
 LIB_PATH = os.environ.get("SDHIP_LIB") or os.path.join(_HERE, "libsdhip.so")
-ABI_VERSION = 7
+ABI_VERSION = 8
 CAM_WORDS = 36  # floats per camera record (include/sdhip.h SD_CAM_WORDS)
 
 SD_F32 = 0
@@ -70,7 +70,7 @@ class SdFieldArgs(ctypes.Structure):
         ("img", _vp), ("nv", _i32), ("Hc", _i32), ("Wc", _i32),
         ("cam_c", _vp),
         ("sigma", _vp), ("dino", _vp), ("rgb", _vp), ("invalid", _vp), ("invalid_f", _vp),
-        ("dino_dtype", _i32), ("pad0", _i32),
+        ("dino_dtype", _i32), ("pad0", _i32), ("tile_order", _vp),
     ]
 
 
@@ -156,6 +156,7 @@ class SdSscArgs(ctypes.Structure):
 SIGNATURES = {
     "sd_last_error": [],
     "sd_abi_version": [],
+    "sd_ln_gemm": [ctypes.POINTER(SdGemmArgs), _vp, _vp, _vp, ctypes.c_float, _vp],
     "sd_gen_rays": [_vp, _vp, _vp, _i64, _i64, _i64, ctypes.c_float, ctypes.c_float, _vp, _vp],
     "sd_sample_z": [_vp, _i64, _i64, _i64, ctypes.c_int, _vp, ctypes.c_uint64, ctypes.c_uint64,
                     _vp, _vp],
@@ -609,6 +610,24 @@ def gemm(a, w, bias, epi, out=None, gamma=None, qkv=None, tokens=0, heads=0, pos
     if pos is not None:
         g.pos, g.patches = pos.data_ptr(), patches
     _check(lib.sd_gemm(ctypes.byref(g), stream_of(a)), "sd_gemm")
+
+
+def ln_gemm(x, ln_w, ln_b, eps, w, bias, epi, out=None, qkv=None, tokens=0, heads=0):
+    """sd_ln_gemm: LN(x) w^T + bias with the epilogue epi; x (M, C) f32, w (N, C) bf16."""
+    lib = load()
+    M, C = x.shape
+    N = w.shape[0]
+    _req(x, "x")
+    _req(w, "w", torch.bfloat16)
+    g = SdGemmArgs(a=None, lda=C, w=w.data_ptr(), bias=bias.data_ptr() if bias is not None else None,
+                   M=M, N=N, K=C, epi=epi, out=out.data_ptr() if out is not None else None,
+                   ldo=out.stride(-2) if out is not None else 0)
+    if qkv is not None:
+        q, k, vt = qkv
+        g.q, g.k, g.vt = q.data_ptr(), k.data_ptr(), vt.data_ptr()
+        g.tokens, g.heads, g.head_dim, g.tokens_pad = tokens, heads, q.shape[-1], k.shape[-2]
+    _check(lib.sd_ln_gemm(ctypes.byref(g), ptr(x), ptr(_req(ln_w, "ln_w")), ptr(_req(ln_b, "ln_b")),
+                          float(eps), stream_of(x)), "sd_ln_gemm")
 
 
 def attention(q, k, vt, scale, out):

@@ -41,7 +41,7 @@ extern "C" void sd_set_error(const char *msg) {
     g_err[sizeof(g_err) - 1] = 0;
 }
 extern "C" const char *sd_last_error(void) { return g_err; }
-extern "C" int sd_abi_version(void) { return 7; }
+extern "C" int sd_abi_version(void) { return 8; }
 
 // Threads per workgroup, one workgroup per CU: 16-bit kernels run 8 waves (2 per SIMD,
 // <= 256 VGPRs each); the f32 parity kernels run 4 waves (1 per SIMD, 512 VGPRs).
@@ -683,8 +683,15 @@ k_field(const sd_field_args a, const sd_mlp m, const LdsPlan pl) {
     // one descriptor over all batch planes (host checks B * plane < 4 GiB)
     const __amdgpu_buffer_rsrc_t rs = sd_rsrc(a.grid, (uint32_t)(a.B * (int64_t)plane_bytes));
 
-    for (int64_t tile = (int64_t)blockIdx.x * WG<P>::W + wave; tile < ntiles;
-         tile += (int64_t)gridDim.x * WG<P>::W) {
+    // XCD-aware tile ranges (workgroups b, b + 8, ... share an XCD: speed only): XCD x
+    // visits tiles [x T / 8, (x + 1) T / 8) of the (optionally locality-sorted) order, its
+    // workgroups interleaved, so a tile's grid taps are fetched into one XCD's L2
+    const int nx = (gridDim.x % 8 == 0) ? 8 : 1;
+    const int xcd = blockIdx.x % nx, nwg = gridDim.x / nx;
+    const int64_t tend = ntiles * (xcd + 1) / nx;
+    for (int64_t tt = ntiles * xcd / nx + (int64_t)(blockIdx.x / nx) * WG<P>::W + wave; tt < tend;
+         tt += (int64_t)nwg * WG<P>::W) {
+        const int64_t tile = a.tile_order ? (int64_t)a.tile_order[tt] : tt;
         const int64_t pu = tile * 32 + li;
         const bool valid = pu < NP;
         const int64_t p = valid ? pu : NP - 1;

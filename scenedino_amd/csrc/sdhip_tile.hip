@@ -105,6 +105,9 @@ extern "C" int sd_tile_prof(unsigned long long *out, int reset) {
 #define ST_T2(i)
 #endif
 
+#ifndef ST_PREADDR
+#define ST_PREADDR 1        // tap LDS addresses written into the records once the tile is staged
+#endif
 #ifndef ST_CODE_FIRST
 #define ST_CODE_FIRST 0     // 1: positional-code MFMAs before the tap blend (spills)
 #endif
@@ -493,6 +496,35 @@ k_render_tile(const st_args sa) {
         return t;
     };
 
+    // once a group's tile geometry is known (after stage), each wave rewrites its ray's
+    // record words q0.x = {x0 | y0 << 15 | flags << 30} as {LDS byte address of tap (x0, y0)
+    // in tile buffer tb | flags << 30}: an item then reads the 4 tap bases it needs with
+    // two ds_read2_b32 instead of computing its own and exchanging them by ds_bpermute (a
+    // chain of dependent LDS round trips at the head of every item).  Split groups: the
+    // second half ray's samples get the second half's geometry.
+    auto tap_addrs = [&](int rbuf, int tb, const Tile &t, int ray_) {
+        if (!ST_PREADDR || !t.ok || ray_ >= R) return;
+        Tile t2 = t;
+        if (t.split) {
+            uint32_t mn1, mx1;
+            box_union(rbuf, 1, mn1, mx1);
+            t2 = geom(mn1, mx1);
+        }
+        const uint32_t tbase = lds0 + tile0 + (uint32_t)tb * (uint32_t)sa.tile_bytes;
+        uint32_t *w = (uint32_t *)rq0(rbuf);
+#pragma unroll
+        for (int p = 0; p < ST_MAXP; ++p) {
+            const int k = 64 * p + lane;
+            if (64 * p < K && k < K) {
+                const uint32_t xy = w[4 * k];
+                const Tile &tt = (t.split && k >= kh) ? t2 : t;
+                const int x0 = (int)(xy & 0x7fffu), y0 = (int)((xy >> 15) & 0x7fffu);
+                const uint32_t ad = tbase + (uint32_t)(((y0 - tt.by0) * tt.pitch + (x0 - tt.bx0)) * ST_TEX);
+                w[4 * k] = ad | (xy & 0xc0000000u);
+            }
+        }
+    };
+
     // ---- DINO head of one group (hsum of its 8 rays in LDS) ---------------------------
     // W_dino fragments of the wave's first head tile (dt = wave), loaded one phase ahead
     Frag Wh[4];
@@ -557,6 +589,7 @@ k_render_tile(const st_args sa) {
     ray_col(ray, 0);
     st_barrier_lds();
     Tile cur = stage(0, 0, grp, sbi);
+    tap_addrs(0, 0, cur, ray);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
@@ -596,7 +629,6 @@ k_render_tile(const st_args sa) {
             const float2 cgb = rqc(buf)[k];
             const float znext = k + 1 < K ? rq1(buf)[k + 1][3] : 0.f;
             const uint32_t xy = q0.x;
-            const int x0 = (int)(xy & 0x7fffu), y0 = (int)((xy >> 15) & 0x7fffu);
             st.flags = ((xy >> 30) & 1u) | ((xy >> 30) & 2u);
             const float v[3] = {q1[0], q1[1], q1[2]};
             st.zk = q1[3];
@@ -604,15 +636,25 @@ k_render_tile(const st_args sa) {
             st.col[0] = __builtin_bit_cast(float, q0.w);
             st.col[1] = cgb.x;
             st.col[2] = cgb.y;
-            // this lane's sample: LDS byte address of its tap (x0, y0)
-            const int nb = (int)tileb + ((y0 - cur.by0) * cur.pitch + (x0 - cur.bx0)) * ST_TEX;
             uint32_t base[2][2];
+            if (ST_PREADDR) {
+                // tap bases of samples 8 c + 2 g + r, written by tap_addrs
+                const uint32_t *aw = (const uint32_t *)rq0(buf) + 4 * (sub * 16 + 2 * g);
 #pragma unroll
-            for (int c = 0; c < 2; ++c)
+                for (int c = 0; c < 2; ++c)
 #pragma unroll
-                for (int r = 0; r < 2; ++r)
-                    base[c][r] = (uint32_t)__builtin_amdgcn_ds_bpermute((8 * c + 2 * g + r) << 2, nb) +
-                                 lane_off;
+                    for (int r = 0; r < 2; ++r) base[c][r] = (aw[4 * (8 * c + r)] & 0x3ffffu) + lane_off;
+            } else {
+                // this lane's sample: LDS byte address of its tap (x0, y0)
+                const int x0 = (int)(xy & 0x7fffu), y0 = (int)((xy >> 15) & 0x7fffu);
+                const int nb = (int)tileb + ((y0 - cur.by0) * cur.pitch + (x0 - cur.bx0)) * ST_TEX;
+#pragma unroll
+                for (int c = 0; c < 2; ++c)
+#pragma unroll
+                    for (int r = 0; r < 2; ++r)
+                        base[c][r] = (uint32_t)__builtin_amdgcn_ds_bpermute((8 * c + 2 * g + r) << 2, nb) +
+                                     lane_off;
+            }
             // block-diagonal weight fragments of the two K-chunks
             const uint32_t w01 = q0.y, w23 = q0.z;
             ST_T2(13);
@@ -814,7 +856,10 @@ k_render_tile(const st_args sa) {
         st_barrier_lds();  // X: next boxes visible; the head has read the hsum area
         ST_T(4);
         Tile nxt = {0, 0, 1, 0, 0, 0};
-        if (has_next) nxt = stage(buf ^ 1, buf ^ 1, ngrp, nsbi);
+        if (has_next) {
+            nxt = stage(buf ^ 1, buf ^ 1, ngrp, nsbi);
+            tap_addrs(buf ^ 1, buf ^ 1, nxt, nray);
+        }
         ST_T(5);
 #if ST_PIPE
         if (active && !ST_ABL_NOITEM) {

@@ -920,6 +920,130 @@ __global__ void __launch_bounds__(256) k_upsample2x(const __bf16 *__restrict__ i
 }
 
 // ---------------------------------------------------------------------------
+// LayerNorm-prologue GEMM (the ViT's norm1 -> qkv and norm2 -> fc1 at small token counts)
+// ---------------------------------------------------------------------------
+// out = EPI(LN(x) W^T + b) for x (M, C) f32 residual-stream rows and W (N, C) bf16: the
+// LayerNorm runs in the prologue of every 32-row tile (k_layernorm's arithmetic and order,
+// rounded to bf16 as its output is) into LDS, so the normalised rows never reach HBM and the
+// separate norm launch (~5 us at 481 tokens, as long as the GEMM itself) disappears.  The
+// whole K = C of the weight tile is loaded into registers before the norm starts: its
+// latency hides under the norm.  A 256-thread workgroup computes a 32 x 64 tile, wave w
+// the columns 16 w .. 16 w + 15 by v_mfma_f32_16x16x32_bf16 (A from LDS, B from registers).
+#define LG_BM 32
+#define LG_BN 64
+
+template <int PER, int EPI>
+__global__ void __launch_bounds__(256) k_lngemm(sd_gemm_args g, const float *__restrict__ x,
+                                                const float *__restrict__ lw,
+                                                const float *__restrict__ lb, float eps) {
+    constexpr int C = 64 * PER, LDA = C + 8, NK = C / 32;
+    __shared__ __attribute__((aligned(16))) __bf16 sA[LG_BM * LDA];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int j = lane & 15, kq = lane >> 4;
+    const int64_t m0 = (int64_t)blockIdx.y * LG_BM, n0 = (int64_t)blockIdx.x * LG_BN;
+    const int64_t n = n0 + 16 * wave + j;
+    // this lane's weight column (8 consecutive k per K step), all K steps in flight
+    const __bf16 *wr = (const __bf16 *)g.w + min(n, g.N - 1) * C + 8 * kq;
+    bf16x8 wb[NK];
+#pragma unroll
+    for (int s = 0; s < NK; ++s) wb[s] = *(const bf16x8 *)(wr + 32 * s);
+    // LayerNorm of rows 8 w .. 8 w + 7 (one row per pass, lane = columns lane + 64 i)
+    for (int r = 0; r < 8; ++r) {
+        const int rl = 8 * wave + r;
+        const int64_t row = min(m0 + rl, g.M - 1);
+        const float *xr = x + row * C;
+        float v[PER];
+        float sum = 0.f;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            v[i] = xr[lane + 64 * i];
+            sum += v[i];
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) sum += __shfl_xor(sum, off);
+        const float mean = sum / (float)C;
+        float q = 0.f;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const float d = v[i] - mean;
+            q = fmaf(d, d, q);
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) q += __shfl_xor(q, off);
+        const float rstd = 1.f / sqrtf(q / (float)C + eps);
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int c = lane + 64 * i;
+            sA[rl * LDA + c] = (__bf16)((v[i] - mean) * rstd * lw[c] + lb[c]);
+        }
+    }
+    __syncthreads();
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+#pragma unroll
+    for (int s = 0; s < NK; ++s) {
+        const bf16x8 a0 = *(const bf16x8 *)&sA[j * LDA + 32 * s + 8 * kq];
+        const bf16x8 a1 = *(const bf16x8 *)&sA[(16 + j) * LDA + 32 * s + 8 * kq];
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, wb[s], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, wb[s], acc1, 0, 0, 0);
+    }
+    if (n >= g.N) return;
+    // D layout: lane (j, kq) holds rows 4 kq + r of each 16-row tile, column n
+    const float bias = g.bias ? g.bias[n] : 0.f;
+    if (EPI == SD_EPI_QKV) {
+        const int Cq = g.heads * g.head_dim;
+        const int which = (int)(n / Cq), rem = (int)(n - (int64_t)which * Cq);
+        const int head = rem / g.head_dim, e = rem - head * g.head_dim;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const f32x4 a = t ? acc1 : acc0;
+            const int64_t mb = m0 + 16 * t + 4 * kq;
+            if (which == 2) {
+                // V^T: the lane's 4 rows are 4 consecutive tokens of its head-dim row
+                const uint32_t b = (uint32_t)mb / (uint32_t)g.tokens;
+                const int64_t tk = mb - (int64_t)b * g.tokens;
+                __bf16 *dst = (__bf16 *)g.vt + (((int64_t)b * g.heads + head) * g.head_dim + e) * g.tokens_pad + tk;
+                if (mb + 3 < g.M && tk + 3 < g.tokens && (tk & 3) == 0) {
+                    bf16x4 v4;
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) v4[u] = (__bf16)(a[u] + bias);
+                    *(bf16x4 *)dst = v4;
+                    continue;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int64_t m = mb + u;
+                if (m >= g.M) break;
+                const uint32_t b = (uint32_t)m / (uint32_t)g.tokens;
+                const int64_t tk = m - (int64_t)b * g.tokens;
+                const int64_t bh = (int64_t)b * g.heads + head;
+                const __bf16 v = (__bf16)(a[u] + bias);
+                if (which == 0)
+                    ((__bf16 *)g.q)[(bh * g.tokens + tk) * g.head_dim + e] = v;
+                else if (which == 1)
+                    ((__bf16 *)g.k)[(bh * g.tokens_pad + tk) * g.head_dim + e] = v;
+                else
+                    ((__bf16 *)g.vt)[(bh * g.head_dim + e) * g.tokens_pad + tk] = v;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const f32x4 a = t ? acc1 : acc0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int64_t m = m0 + 16 * t + 4 * kq + u;
+                if (m >= g.M) break;
+                float v = a[u] + bias;
+                if (EPI == SD_EPI_GELU) v = vt_gelu(v);
+                ((__bf16 *)g.out)[m * g.ldo + n] = (__bf16)v;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
 template <int BM, int BN, int BK, bool CONV>
@@ -1007,6 +1131,47 @@ extern "C" int sd_gemm(const sd_gemm_args *args, void *stream) {
         vt_pick_gemm<false>(g, s);
     if (hipGetLastError() != hipSuccess) {
         sd_set_error("sd_gemm: launch failed");
+        return -2;
+    }
+    return 0;
+}
+
+extern "C" int sd_ln_gemm(const sd_gemm_args *args, const float *x, const float *ln_w,
+                          const float *ln_b, float eps, void *stream) {
+    if (!args || !x || !ln_w || !ln_b) {
+        sd_set_error("sd_ln_gemm: null argument");
+        return -1;
+    }
+    const sd_gemm_args &g = *args;
+    const int64_t C = g.K;
+    bool ok = g.w && g.M >= 0 && g.N > 0 && (C == 384 || C == 768) &&
+              (g.epi == SD_EPI_QKV || g.epi == SD_EPI_GELU || g.epi == SD_EPI_BF16) &&
+              g.M * C < ((int64_t)1 << 31) && g.N * C < ((int64_t)1 << 31);
+    if (g.epi == SD_EPI_QKV)
+        ok = ok && g.q && g.k && g.vt && g.head_dim > 0 && g.heads > 0 && g.tokens > 0 &&
+             g.tokens_pad >= g.tokens && g.N == 3LL * g.heads * g.head_dim && g.M % g.tokens == 0;
+    else
+        ok = ok && g.out && g.ldo >= g.N;
+    if (!ok) {
+        sd_set_error("sd_ln_gemm: invalid argument (K = C in {384, 768}, epi QKV / GELU / BF16)");
+        return -1;
+    }
+    if (g.M == 0) return 0;
+    dim3 grid((unsigned)((g.N + LG_BN - 1) / LG_BN), (unsigned)((g.M + LG_BM - 1) / LG_BM));
+    hipStream_t s = (hipStream_t)stream;
+#define SD_LG(PER, E) hipLaunchKernelGGL((k_lngemm<PER, E>), grid, dim3(256), 0, s, g, x, ln_w, ln_b, eps)
+    if (C == 384) {
+        if (g.epi == SD_EPI_QKV) SD_LG(6, SD_EPI_QKV);
+        else if (g.epi == SD_EPI_GELU) SD_LG(6, SD_EPI_GELU);
+        else SD_LG(6, SD_EPI_BF16);
+    } else {
+        if (g.epi == SD_EPI_QKV) SD_LG(12, SD_EPI_QKV);
+        else if (g.epi == SD_EPI_GELU) SD_LG(12, SD_EPI_GELU);
+        else SD_LG(12, SD_EPI_BF16);
+    }
+#undef SD_LG
+    if (hipGetLastError() != hipSuccess) {
+        sd_set_error("sd_ln_gemm: launch failed");
         return -2;
     }
     return 0;

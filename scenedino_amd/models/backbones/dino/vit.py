@@ -20,6 +20,8 @@ oracle/vit_oracle.py, a PyTorch fp32 restatement of that block.
 """
 from __future__ import annotations
 
+import os
+
 from typing import Dict, List, Optional, Tuple
 
 import torch
@@ -136,6 +138,11 @@ def _param_key(m: nn.Module):
                  if t is not None)
 
 
+# fuse the block norms into the qkv / fc1 GEMMs (sd_ln_gemm); SCENEDINO_AMD_LN_GEMM=0 keeps
+# the separate sd_layernorm launches (A/B runs)
+LN_GEMM = os.environ.get("SCENEDINO_AMD_LN_GEMM", "1") != "0"
+
+
 def vit_forward(vit: VisionTransformer, images: torch.Tensor, packed: _Packed,
                 intermediate: List[int], nhwc: bool = False):
     """images (B, 3, H, W) in [-1, 1] (DINOv2Encoder input, before _normalize_input) ->
@@ -174,14 +181,25 @@ def vit_forward(vit: VisionTransformer, images: torch.Tensor, packed: _Packed,
     grids = []
     to_grid = _lib.tokens_to_nhwc if nhwc else _lib.tokens_to_grid
     scale = hd ** -0.5
+    # norm1 / norm2 fused into the qkv / fc1 GEMM prologues (sd_ln_gemm) at the widths it
+    # covers; otherwise sd_layernorm + sd_gemm
+    fuse_ln = C in (384, 768) and LN_GEMM
     for i, blk in enumerate(packed.blocks):
-        _lib.layernorm(x, blk["n1w"], blk["n1b"], 1e-6, xn)
-        _lib.gemm(xn, blk["qkv_w"], blk["qkv_b"], _lib.SD_EPI_QKV, qkv=(q, k, vt), tokens=T,
-                  heads=nh)
+        if fuse_ln:
+            _lib.ln_gemm(x, blk["n1w"], blk["n1b"], 1e-6, blk["qkv_w"], blk["qkv_b"],
+                         _lib.SD_EPI_QKV, qkv=(q, k, vt), tokens=T, heads=nh)
+        else:
+            _lib.layernorm(x, blk["n1w"], blk["n1b"], 1e-6, xn)
+            _lib.gemm(xn, blk["qkv_w"], blk["qkv_b"], _lib.SD_EPI_QKV, qkv=(q, k, vt), tokens=T,
+                      heads=nh)
         _lib.attention(q, k, vt, scale, ao)
         _lib.gemm(ao, blk["proj_w"], blk["proj_b"], _lib.SD_EPI_RESID, out=x, gamma=blk["ls1"])
-        _lib.layernorm(x, blk["n2w"], blk["n2b"], 1e-6, xn)
-        _lib.gemm(xn, blk["fc1_w"], blk["fc1_b"], _lib.SD_EPI_GELU, out=hid)
+        if fuse_ln:
+            _lib.ln_gemm(x, blk["n2w"], blk["n2b"], 1e-6, blk["fc1_w"], blk["fc1_b"],
+                         _lib.SD_EPI_GELU, out=hid)
+        else:
+            _lib.layernorm(x, blk["n2w"], blk["n2b"], 1e-6, xn)
+            _lib.gemm(xn, blk["fc1_w"], blk["fc1_b"], _lib.SD_EPI_GELU, out=hid)
         _lib.gemm(hid, blk["fc2_w"], blk["fc2_b"], _lib.SD_EPI_RESID, out=x, gamma=blk["ls2"])
         if i in intermediate:
             grids.append(to_grid(x, B, T, C, 1, gh, gw, False))

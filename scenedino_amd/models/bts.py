@@ -439,11 +439,48 @@ class BTSNet(nn.Module):
             self._timed("render", lambda: _lib.render_fused(args, m.rec, rays))
         return out
 
-    def query(self, xyz, colors: bool = True, dino_dtype=torch.float32):
+    def _tile_order(self, xyz, gc):
+        """Visiting order of sd_field_query's 32-point tiles for large voxel queries: tiles
+        sorted by the 16-texel cell their middle point projects to (column-major over the
+        grid image, points behind the camera last), so the workgroups of an XCD gather
+        neighbouring texels of the projected grid from its L2 instead of every tile
+        fetching its own (SSCBench's (x, y) voxel columns project to vertical segments).
+        Speed only: outputs stay at their point indices.  Cached per (points, camera)."""
+        n, P, _ = xyz.shape
+        NP = n * P
+        nt = (NP + 31) // 32
+        w2c, Ks = self.grid_f_poses_w2c, self.grid_f_Ks
+        key = (xyz.data_ptr(), xyz._version, NP, w2c.data_ptr(), w2c._version, Ks.data_ptr(),
+               Ks._version, gc["Hf"], gc["Wf"])
+        c = getattr(self, "_order_cache", None)
+        if c is not None and c[0] == key:
+            return c[1]
+        dev = xyz.device
+        idx = (torch.arange(nt, device=dev) * 32 + 16).clamp_max(NP - 1)
+        pts = xyz.reshape(NP, 3).float().index_select(0, idx)
+        b = torch.div(idx, P, rounding_mode="floor")
+        R = w2c[:, 0, :3, :3].float()[b]
+        t = w2c[:, 0, :3, 3].float()[b]
+        cam = torch.einsum("tij,tj->ti", R, pts) + t
+        uvw = torch.einsum("tij,tj->ti", Ks[:, 0].float()[b], cam)
+        z = uvw[:, 2]
+        front = z > 1e-3
+        u = (uvw[:, 0] / z.clamp_min(1e-3)).clamp(-2, 2)
+        v = (uvw[:, 1] / z.clamp_min(1e-3)).clamp(-2, 2)
+        ub = ((u + 2) * (gc["Wf"] / 32)).floor()
+        vb = ((v + 2) * (gc["Hf"] / 32)).floor()
+        cell = torch.where(front, ub * 4096 + vb, torch.full_like(ub, 2.0 ** 24))
+        order = torch.argsort(b.double() * 2.0 ** 26 + cell.double(), stable=True).to(torch.int32)
+        self._order_cache = (key, order)
+        return order
+
+    def query(self, xyz, colors: bool = True, dino_dtype=torch.float32, locality=None):
         """Raw per-point field: sigma (n,P), dino (n,P,D), rgb (n,P,3nv), invalid (n,P,nv),
         invalid_features (n,P) -- all from sd_field_query.  colors=False skips the colour
         sampling (the predict_segmentation path, bts.py:528-533): rgb / invalid are None.
-        dino_dtype bfloat16: dino for sd_seg_query, which rounds its input to bf16 anyway."""
+        dino_dtype bfloat16: dino for sd_seg_query, which rounds its input to bf16 anyway.
+        locality (default: colour-free queries of >= 2^18 points, the SSCBench voxels):
+        visit the point tiles in projected-texel order (_tile_order; same outputs)."""
         self._check_supported()
         m = self._mlp()
         gc = self._grids()
@@ -469,6 +506,9 @@ class BTSNet(nn.Module):
         rgb = torch.empty(n, P, 3 * nv, device=dev) if colors else None
         inv = torch.empty(n, P, nv, device=dev) if colors else None
         invf = torch.empty(n, P, device=dev, dtype=torch.bool)  # bytes 0 / 1
+        if locality is None:
+            locality = not colors and n * P >= (1 << 18)
+        order = self._tile_order(xyz, gc) if locality else None
         args = _lib.SdFieldArgs(
             xyz=xyz.data_ptr(), B=n, P=P, grid=grid.data_ptr(), Hf=gc["Hf"],
             Wf=gc["Wf"],
@@ -476,7 +516,8 @@ class BTSNet(nn.Module):
             Hc=gc["Hc"], Wc=gc["Wc"], cam_c=gc["cam_c"].data_ptr(), sigma=sigma.data_ptr(),
             dino=dino.data_ptr(), rgb=rgb.data_ptr() if colors else None,
             invalid=inv.data_ptr() if colors else None, invalid_f=invf.data_ptr(),
-            dino_dtype=_lib.SD_BF16 if dino_dtype == torch.bfloat16 else _lib.SD_F32)
+            dino_dtype=_lib.SD_BF16 if dino_dtype == torch.bfloat16 else _lib.SD_F32,
+            tile_order=order.data_ptr() if order is not None else None)
         self._timed("field", lambda: _lib.field_query(args, m.rec, xyz))
         return sigma, dino, rgb, inv, invf
 

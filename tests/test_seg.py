@@ -572,3 +572,24 @@ def test_sscbench_downsample_and_predict(gpu):
     grown = F.max_pool3d(raw.unsqueeze(0), 3, 1, 1).squeeze(0)
     inner = (slice(129, 255), slice(0, 127))
     np.testing.assert_array_equal(sig[inner], grown[inner].numpy())
+
+
+@pytest.mark.gpu
+def test_voxel_query_tile_order_is_speed_only(gpu):
+    """sd_field_query's tile_order (BTSNet._tile_order: the SSCBench voxel columns visited in
+    projected-texel order, XCD-aware ranges) changes no output bit: sigma, the bf16 codes
+    and the frustum mask equal the natural-order query over the full C5 voxel grid."""
+    import sys
+    from conftest import ROOT
+    sys.path.insert(0, ROOT)
+    import bench
+    net, pts, dims = bench.c5_scene(torch.device(gpu), "bf16", 0)
+    with torch.no_grad():
+        a = net.query(pts.reshape(1, -1, 3), colors=False, dino_dtype=torch.bfloat16, locality=True)
+        b = net.query(pts.reshape(1, -1, 3), colors=False, dino_dtype=torch.bfloat16, locality=False)
+    order = net._order_cache[1]
+    nt = (pts.shape[0] + 31) // 32
+    assert torch.equal(order.sort().values.cpu(), torch.arange(nt, dtype=torch.int32))
+    assert not torch.equal(order.cpu(), torch.arange(nt, dtype=torch.int32))
+    for x, y in ((a[0], b[0]), (a[1], b[1]), (a[4], b[4])):
+        assert torch.equal(x, y)

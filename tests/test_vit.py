@@ -159,6 +159,45 @@ def test_layernorm(gpu, C):
     assert (of - ref).abs().max().item() <= 1e-4
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("C,H,T,B", [(384, 6, 481, 1), (768, 12, 481, 1), (768, 12, 77, 2)])
+def test_ln_gemm_equals_layernorm_then_gemm(gpu, C, H, T, B):
+    """sd_ln_gemm (norm fused into the qkv / fc1 GEMM prologue): its normalised rows are
+    sd_layernorm's bf16 rows, so the products equal the two-launch path up to the GEMM's
+    accumulation order -- checked against the f32 product of sd_layernorm's rows
+    (|d| <= 8e-3 of the output scale, bf16 output rounding) and the qkv scatter layout."""
+    from scenedino_amd import _lib
+    g = torch.Generator().manual_seed(C + T)
+    M = B * T
+    x = (2 * torch.randn(M, C, generator=g) + 0.5).to(gpu)
+    lw = (1 + 0.1 * torch.randn(C, generator=g)).to(gpu)
+    lb = (0.1 * torch.randn(C, generator=g)).to(gpu)
+    xn = torch.empty(M, C, device=gpu, dtype=torch.bfloat16)
+    _lib.layernorm(x, lw, lb, 1e-6, xn)
+    # qkv
+    w = _bf(torch.randn(3 * C, C, generator=g) / math.sqrt(C)).to(gpu)
+    b = (0.1 * torch.randn(3 * C, generator=g)).to(gpu)
+    ref = xn.float() @ w.float().t() + b
+    scale = ref.abs().max().item()
+    Tp = (T + 63) // 64 * 64
+    q = torch.empty(B, H, T, 64, device=gpu, dtype=torch.bfloat16)
+    k = torch.zeros(B, H, Tp, 64, device=gpu, dtype=torch.bfloat16)
+    vt = torch.zeros(B, H, 64, Tp, device=gpu, dtype=torch.bfloat16)
+    _lib.ln_gemm(x, lw, lb, 1e-6, w, b, _lib.SD_EPI_QKV, qkv=(q, k, vt), tokens=T, heads=H)
+    r = ref.view(B, T, 3, H, 64).permute(2, 0, 3, 1, 4)
+    assert (q.float() - r[0]).abs().max().item() <= 8e-3 * scale
+    assert (k[:, :, :T].float() - r[1]).abs().max().item() <= 8e-3 * scale
+    assert (vt[..., :T].float() - r[2].transpose(-1, -2)).abs().max().item() <= 8e-3 * scale
+    assert not k[:, :, T:].any() and not vt[..., T:].any()
+    # fc1 + GELU
+    w1 = _bf(torch.randn(4 * C, C, generator=g) / math.sqrt(C)).to(gpu)
+    b1 = (0.1 * torch.randn(4 * C, generator=g)).to(gpu)
+    ref1 = F.gelu(xn.float() @ w1.float().t() + b1)
+    hid = torch.empty(M, 4 * C, device=gpu, dtype=torch.bfloat16)
+    _lib.ln_gemm(x, lw, lb, 1e-6, w1, b1, _lib.SD_EPI_GELU, out=hid)
+    assert (hid.float() - ref1).abs().max().item() <= 8e-3 * ref1.abs().max().item()
+
+
 def _encoder_check(enc, images, tol=3e-2):
     dev = images.device
     with torch.no_grad():
