@@ -108,6 +108,12 @@ extern "C" int sd_tile_prof(unsigned long long *out, int reset) {
 #ifndef ST_PREADDR
 #define ST_PREADDR 1        // tap LDS addresses written into the records once the tile is staged
 #endif
+#ifndef ST_EPI_STORES
+#define ST_EPI_STORES 1     // per-sample outputs staged in the records, stored per ray (coalesced)
+#endif
+#ifndef ST_BLEND_DEEP
+#define ST_BLEND_DEEP 0     // > 0: tap reads that many blend tiles ahead of the MFMAs
+#endif
 #ifndef ST_CODE_FIRST
 #define ST_CODE_FIRST 0     // 1: positional-code MFMAs before the tap blend (spills)
 #endif
@@ -709,6 +715,30 @@ k_render_tile(const st_args sa) {
             }
             ST_T2(14);
 #else
+#if ST_BLEND_DEEP
+            // the tap reads run ST_BLEND_DEEP tiles ahead of the blend MFMAs (one LDS latency
+            // per item instead of one per tile)
+            uint2 tv[8][4];
+#pragma unroll
+            for (int t = 0; t < ST_BLEND_DEEP; ++t) {
+                tv[t][0] = st_tr(base[0][0] + 32u * t); tv[t][1] = st_tr(base[0][1] + 32u * t);
+                tv[t][2] = st_tr(base[1][0] + 32u * t); tv[t][3] = st_tr(base[1][1] + 32u * t);
+            }
+            __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead (the scheduler sinks them)
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                if (t + ST_BLEND_DEEP < 8) {
+                    const int u = t + ST_BLEND_DEEP;
+                    tv[u][0] = st_tr(base[0][0] + 32u * u); tv[u][1] = st_tr(base[0][1] + 32u * u);
+                    tv[u][2] = st_tr(base[1][0] + 32u * u); tv[u][3] = st_tr(base[1][1] + 32u * u);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                const Frag A0 = __builtin_bit_cast(Frag, uint4{tv[t][0].x, tv[t][0].y, tv[t][1].x, tv[t][1].y});
+                const Frag A1 = __builtin_bit_cast(Frag, uint4{tv[t][2].x, tv[t][2].y, tv[t][3].x, tv[t][3].y});
+                acc[t] = Tr::mma(A0, B0, zero4);
+                acc[t] = Tr::mma(A1, B1, acc[t]);
+            }
+#else
 #pragma unroll
             for (int t = 0; t < 8; ++t) {
 #if ST_ABL_NOTR
@@ -723,6 +753,7 @@ k_render_tile(const st_args sa) {
                 acc[t] = Tr::mma(A0, B0, zero4);
                 acc[t] = Tr::mma(A1, B1, acc[t]);
             }
+#endif
             ST_T2(14);
             // positional-code columns
             const int lo = sd_opaque0();
@@ -829,6 +860,11 @@ k_render_tile(const st_args sa) {
             }
 #endif
             ST_T2(18);
+#if ST_EPI_STORES
+            // weight and alpha into the sample's record (q1.x / .y are dead once itemA has
+            // read the point); the ray epilogue stores every per-sample output coalesced
+            if (g == 0) *(float2 *)&rq1(buf)[k] = float2{w, st.alpha};
+#else
             const int64_t rk = (int64_t)ray * K;
             if (g == 0) {
                 if (a.weights) (a.weights + rk)[k] = w;
@@ -840,6 +876,7 @@ k_render_tile(const st_args sa) {
                     rsp[0] = st.col[0]; rsp[1] = st.col[1]; rsp[2] = st.col[2];
                 }
             }
+#endif
         };
 
         // item 0 with the next ray's pass and the previous group's head
@@ -926,6 +963,30 @@ k_render_tile(const st_args sa) {
                 if (j == 0)
                     *(uint2 *)(hs + (16 * t + 4 * g) * 2) =
                         uint2{sd_pack2<E>(vsum[0], vsum[1]), sd_pack2<E>(vsum[2], vsum[3])};
+            }
+#endif
+#if ST_EPI_STORES
+            {
+                // per-sample outputs, lane = sample (one coalesced store per array)
+                const int64_t rk = (int64_t)ray * K;
+#pragma unroll
+                for (int p = 0; p < ST_MAXP; ++p) {
+                    const int k = 64 * p + lane;
+                    if (64 * p < K && k < K) {
+                        const f32x4 q1v = rq1(buf)[k];
+                        const uint4 q0v = rq0(buf)[k];
+                        const uint32_t fl = q0v.x >> 30;
+                        if (a.weights) a.weights[rk + k] = q1v[0];
+                        if (a.alphas) a.alphas[rk + k] = q1v[1];
+                        if (a.invalid_f) a.invalid_f[rk + k] = (uint8_t)(fl & 1u);
+                        if (a.invalid) a.invalid[rk + k] = fl ? 1.f : 0.f;
+                        if (a.rgb_samps) {
+                            const float2 cgb = rqc(buf)[k];
+                            float *rsp = a.rgb_samps + (rk + k) * 3;
+                            rsp[0] = __builtin_bit_cast(float, q0v.w); rsp[1] = cgb.x; rsp[2] = cgb.y;
+                        }
+                    }
+                }
             }
 #endif
             if (lane == 0) {

@@ -920,6 +920,73 @@ __global__ void __launch_bounds__(256) k_upsample2x(const __bf16 *__restrict__ i
 }
 
 // ---------------------------------------------------------------------------
+// Register-streaming split-K GEMM for small M (the ViT's proj / fc2 at 481 tokens)
+// ---------------------------------------------------------------------------
+// One 256-thread workgroup per 32 x 32 output tile; wave w owns the K quarter
+// [w K / 4, (w + 1) K / 4) and streams its A and W fragments straight from memory into
+// registers (16 B per lane per 32x32x16 step, both operands K-contiguous), up to GD_CHUNK
+// steps in flight: no LDS staging and no barrier inside the K loop, whose per-step
+// global -> LDS -> barrier round trips bound k_gemm's split-K tile at this size.  The four
+// partial tiles are summed through LDS in wave order (deterministic), then the epilogue.
+#define GD_CHUNK 8
+
+template <int EPI>
+__global__ void __launch_bounds__(256) k_gemm_dir(sd_gemm_args g) {
+    __shared__ __attribute__((aligned(16))) float part[3 * 16 * 64];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int r = lane & 31, h = lane >> 5;
+    const int64_t m0 = (int64_t)blockIdx.y * 32, n0 = (int64_t)blockIdx.x * 32;
+    const int64_t kq = g.K / 4, k0 = wave * kq;
+    const int S = (int)(kq / 16);
+    const __bf16 *ar = (const __bf16 *)g.a + min(m0 + r, g.M - 1) * g.lda + k0 + 8 * h;
+    const __bf16 *br = (const __bf16 *)g.w + min(n0 + r, g.N - 1) * g.K + k0 + 8 * h;
+    f32x16 acc = vt_zero16();
+    for (int c = 0; c < S; c += GD_CHUNK) {
+        bf16x8 fa[GD_CHUNK], fb[GD_CHUNK];
+#pragma unroll
+        for (int i = 0; i < GD_CHUNK; ++i) {
+            const int st = min(c + i, S - 1);
+            fa[i] = *(const bf16x8 *)(ar + 16 * st);
+            fb[i] = *(const bf16x8 *)(br + 16 * st);
+        }
+#pragma unroll
+        for (int i = 0; i < GD_CHUNK; ++i)
+            if (c + i < S) acc = VT_MFMA(fa[i], fb[i], acc);
+    }
+    if (wave > 0) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) part[((wave - 1) * 16 + q) * 64 + lane] = acc[q];
+    }
+    __syncthreads();
+    if (wave != 0) return;
+#pragma unroll
+    for (int w = 0; w < 3; ++w)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[q] += part[(w * 16 + q) * 64 + lane];
+    const int64_t n = n0 + r;
+    if (n >= g.N) return;
+    const float bias = g.bias ? g.bias[n] : 0.f;
+    const float gam = (EPI == SD_EPI_RESID && g.gamma) ? g.gamma[n] : 1.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int64_t m = m0 + (q & 3) + 8 * (q >> 2) + 4 * h;
+        if (m >= g.M) continue;
+        const float v = acc[q] + bias;
+        if (EPI == SD_EPI_RESID) {
+            float *o = (float *)g.out + m * g.ldo + n;
+            *o = *o + gam * v;
+        } else if (EPI == SD_EPI_F32) {
+            ((float *)g.out)[m * g.ldo + n] = v;
+        } else if (EPI == SD_EPI_GELU) {
+            ((__bf16 *)g.out)[m * g.ldo + n] = (__bf16)vt_gelu(v);
+        } else {
+            ((__bf16 *)g.out)[m * g.ldo + n] = (__bf16)v;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // LayerNorm-prologue GEMM (the ViT's norm1 -> qkv and norm2 -> fc1 at small token counts)
 // ---------------------------------------------------------------------------
 // out = EPI(LN(x) W^T + b) for x (M, C) f32 residual-stream rows and W (N, C) bf16: the
@@ -1065,6 +1132,10 @@ static void vt_launch_gemm(const sd_gemm_args &g, hipStream_t s) {
 #define SD_CONV_SK_MID 256  // conv: split-K tiles below this many 64x64 tiles (1024: no gain)
 #endif
 
+#ifndef SD_GEMM_DIR
+#define SD_GEMM_DIR 1  // small-M non-conv GEMMs on k_gemm_dir (0: k_gemm's split-K tile)
+#endif
+
 template <bool CONV>
 static void vt_pick_gemm(const sd_gemm_args &g, hipStream_t s) {
     // K steps of 64 whenever K allows (half the barriers, twice the work under each
@@ -1074,6 +1145,18 @@ static void vt_pick_gemm(const sd_gemm_args &g, hipStream_t s) {
     // conv: a 128-deep K step must stay inside one 3x3 tap (Cin % 128 == 0); the DPT's
     // low-resolution 256-channel convolutions (12x40, 24x80) are exactly these small-M,
     // large-K GEMMs
+    if (!CONV && SD_GEMM_DIR && mid < 256 && g.K % 64 == 0 && g.lda % 8 == 0 &&
+        (g.epi == SD_EPI_RESID || g.epi == SD_EPI_F32 || g.epi == SD_EPI_GELU ||
+         (g.epi == SD_EPI_BF16 && !g.res && !g.res2))) {
+        dim3 grid((unsigned)((g.N + 31) / 32), (unsigned)((g.M + 31) / 32));
+        switch (g.epi) {
+        case SD_EPI_RESID: hipLaunchKernelGGL(k_gemm_dir<SD_EPI_RESID>, grid, dim3(256), 0, s, g); break;
+        case SD_EPI_F32: hipLaunchKernelGGL(k_gemm_dir<SD_EPI_F32>, grid, dim3(256), 0, s, g); break;
+        case SD_EPI_GELU: hipLaunchKernelGGL(k_gemm_dir<SD_EPI_GELU>, grid, dim3(256), 0, s, g); break;
+        default: hipLaunchKernelGGL(k_gemm_dir<SD_EPI_BF16>, grid, dim3(256), 0, s, g); break;
+        }
+        return;
+    }
     if ((CONV ? g.Cin % 128 == 0 && mid < SD_CONV_SK_MID : mid < 256) && g.K % 128 == 0 &&
         g.K >= 256) {
         vt_launch_gemm<32, 32, 128, CONV>(g, s);  // split-K over the 4 waves

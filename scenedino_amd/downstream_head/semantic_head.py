@@ -124,7 +124,7 @@ class SemanticHead(nn.Module):
         if prov is None or features.requires_grad or torch.is_grad_enabled() and self.training:
             return None
         codes, dr, key, version = prov
-        from ...seg_pack import PackedSegHead, seg_key
+        from ..seg_pack import PackedSegHead, seg_key
         if features._version != version or seg_key(dr) != key:
             return None
         hkey = seg_key(dr, self.stego_head, self.stego_cluster_head)
