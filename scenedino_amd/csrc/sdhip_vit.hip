@@ -21,6 +21,7 @@
 //                      (vit.py:188, dinov2_module.py:270-287).
 // Residual stream x is fp32 (B*T, C); GEMM operands bf16; all accumulation fp32.
 #include <cstdlib>
+#include <cstring>
 
 #include "sdhip_common.h"
 #include "sdhip_point.h"
@@ -661,12 +662,15 @@ __global__ void __launch_bounds__(256) k_attn_lds(const __bf16 *__restrict__ Q,
     }
 }
 
-__global__ void __launch_bounds__(256) k_attn_dir(const __bf16 *__restrict__ Q,
+// NW = 4 or 8 waves: 32 queries x NW key slices (8 at >= 512 padded keys: one 64-key block
+// per wave at 481 tokens instead of two in a row)
+template <int NW>
+__global__ void __launch_bounds__(64 * NW) k_attn_dir(const __bf16 *__restrict__ Q,
                                                   const __bf16 *__restrict__ K,
                                                   const __bf16 *__restrict__ Vt, int T, int Tp,
                                                   int H, float sl2e, __bf16 *__restrict__ out) {
-    __shared__ float s_o[4][2][16][64];  // [wave][hd tile][acc register][lane]
-    __shared__ float s_m[4][64], s_l[4][64];
+    __shared__ float s_o[NW][2][16][64];  // [wave][hd tile][acc register][lane]
+    __shared__ float s_m[NW][64], s_l[NW][64];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, h = lane >> 5;
     const int bh = blockIdx.y;
@@ -707,9 +711,9 @@ __global__ void __launch_bounds__(256) k_attn_dir(const __bf16 *__restrict__ Q,
     };
     int kb = 64 * wave;
     if (kb < Tp) fload(kb, kf, vf);
-    for (; kb < Tp; kb += 256) {
-        const bool more = kb + 256 < Tp;
-        if (more) fload(kb + 256, kn, vn);  // next block in flight under this one
+    for (; kb < Tp; kb += 64 * NW) {
+        const bool more = kb + 64 * NW < Tp;
+        if (more) fload(kb + 64 * NW, kn, vn);  // next block in flight under this one
         at_block(S, qb, kf, vf, kb, T, h, sl2e);
         if (more) {
 #pragma unroll
@@ -724,7 +728,7 @@ __global__ void __launch_bounds__(256) k_attn_dir(const __bf16 *__restrict__ Q,
                     for (int s = 0; s < 2; ++s) vf[ht][t][s] = vn[ht][t][s];
         }
     }
-    // merge the 4 waves' partial softmax states
+    // merge the NW waves' partial softmax states
     s_m[wave][lane] = S.m;  // identical in both halves
     s_l[wave][lane] = S.l;  // per-half partial sums
 #pragma unroll
@@ -734,31 +738,34 @@ __global__ void __launch_bounds__(256) k_attn_dir(const __bf16 *__restrict__ Q,
     __syncthreads();
     float M = -INFINITY;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) M = fmaxf(M, s_m[w][lane]);
-    float fw[4], L = 0.f;
+    for (int w = 0; w < NW; ++w) M = fmaxf(M, s_m[w][lane]);
+    float fw[NW], L = 0.f;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
+    for (int w = 0; w < NW; ++w) {
         const float mw = s_m[w][lane];
         fw[w] = mw == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(mw - M);  // a wave with no block
         L = fmaf(fw[w], s_l[w][r] + s_l[w][r + 32], L);
     }
     const float inv = 1.f / L;
     if (q < T) {
-        // wave w writes accumulator registers 4w..4w+3 of both head-dim tiles:
-        // rows 32 ht + 8 w + 4 h + e (4 contiguous head-dim values, one 8-B store)
+        // wave w writes accumulator registers 4 (w % 4) .. + 3 of head-dim tile(s)
+        // w / 4 (NW = 8) or both (NW = 4): rows 32 ht + 8 (w % 4) + 4 h + e (4 contiguous
+        // head-dim values, one 8-B store)
         const int b = bh / H, head = bh - b * H;
         __bf16 *dst = out + ((int64_t)b * T + q) * (int64_t)(H * AT_HD) + head * AT_HD;
+        const int wq = wave & 3;
 #pragma unroll
         for (int ht = 0; ht < 2; ++ht) {
+            if (NW == 8 && ht != (wave >> 2)) continue;
             bf16x4 v;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 float acc = 0.f;
 #pragma unroll
-                for (int w = 0; w < 4; ++w) acc = fmaf(fw[w], s_o[w][ht][4 * wave + e][lane], acc);
+                for (int w = 0; w < NW; ++w) acc = fmaf(fw[w], s_o[w][ht][4 * wq + e][lane], acc);
                 v[e] = (__bf16)(acc * inv);
             }
-            *(bf16x4 *)(dst + 32 * ht + 8 * wave + 4 * h) = v;
+            *(bf16x4 *)(dst + 32 * ht + 8 * wq + 4 * h) = v;
         }
     }
 }
@@ -1275,6 +1282,7 @@ extern "C" int sd_attention(const void *q, const void *k, const void *vt, int32_
     const float sl2e = scale * 1.4426950408889634f;
     const int64_t wg128 = (int64_t)((tokens + 127) / 128) * B * heads;
     const char *force = getenv("SD_ATTN");
+    // SD_ATTN=lds / dir forces one (dir4: the 4-wave dir kernel)
     const bool lds = (force && force[0]) ? force[0] == 'l' : 2 * wg128 >= (int64_t)sd_num_cus();
     if (lds) {
         dim3 grid((unsigned)((tokens + 127) / 128), (unsigned)(B * heads));
@@ -1283,9 +1291,14 @@ extern "C" int sd_attention(const void *q, const void *k, const void *vt, int32_
                            (__bf16 *)out);
     } else {
         dim3 grid((unsigned)((tokens + 31) / 32), (unsigned)(B * heads));
-        hipLaunchKernelGGL(k_attn_dir, grid, dim3(256), 0, (hipStream_t)stream, (const __bf16 *)q,
-                           (const __bf16 *)k, (const __bf16 *)vt, tokens, tokens_pad, heads, sl2e,
-                           (__bf16 *)out);
+        if (tokens_pad >= 512 && !(force && strcmp(force, "dir4") == 0))
+            hipLaunchKernelGGL(k_attn_dir<8>, grid, dim3(512), 0, (hipStream_t)stream, (const __bf16 *)q,
+                               (const __bf16 *)k, (const __bf16 *)vt, tokens, tokens_pad, heads, sl2e,
+                               (__bf16 *)out);
+        else
+            hipLaunchKernelGGL(k_attn_dir<4>, grid, dim3(256), 0, (hipStream_t)stream, (const __bf16 *)q,
+                               (const __bf16 *)k, (const __bf16 *)vt, tokens, tokens_pad, heads, sl2e,
+                               (__bf16 *)out);
     }
     if (hipGetLastError() != hipSuccess) {
         sd_set_error("sd_attention: launch failed");
