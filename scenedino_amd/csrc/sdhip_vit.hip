@@ -662,15 +662,12 @@ __global__ void __launch_bounds__(256) k_attn_lds(const __bf16 *__restrict__ Q,
     }
 }
 
-// NW = 4 or 8 waves: 32 queries x NW key slices (8 at >= 512 padded keys: one 64-key block
-// per wave at 481 tokens instead of two in a row)
-template <int NW>
-__global__ void __launch_bounds__(64 * NW) k_attn_dir(const __bf16 *__restrict__ Q,
+__global__ void __launch_bounds__(256) k_attn_dir(const __bf16 *__restrict__ Q,
                                                   const __bf16 *__restrict__ K,
                                                   const __bf16 *__restrict__ Vt, int T, int Tp,
                                                   int H, float sl2e, __bf16 *__restrict__ out) {
-    __shared__ float s_o[NW][2][16][64];  // [wave][hd tile][acc register][lane]
-    __shared__ float s_m[NW][64], s_l[NW][64];
+    __shared__ float s_o[4][2][16][64];  // [wave][hd tile][acc register][lane]
+    __shared__ float s_m[4][64], s_l[4][64];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, h = lane >> 5;
     const int bh = blockIdx.y;
@@ -711,9 +708,9 @@ __global__ void __launch_bounds__(64 * NW) k_attn_dir(const __bf16 *__restrict__
     };
     int kb = 64 * wave;
     if (kb < Tp) fload(kb, kf, vf);
-    for (; kb < Tp; kb += 64 * NW) {
-        const bool more = kb + 64 * NW < Tp;
-        if (more) fload(kb + 64 * NW, kn, vn);  // next block in flight under this one
+    for (; kb < Tp; kb += 256) {
+        const bool more = kb + 256 < Tp;
+        if (more) fload(kb + 256, kn, vn);  // next block in flight under this one
         at_block(S, qb, kf, vf, kb, T, h, sl2e);
         if (more) {
 #pragma unroll
@@ -728,7 +725,7 @@ __global__ void __launch_bounds__(64 * NW) k_attn_dir(const __bf16 *__restrict__
                     for (int s = 0; s < 2; ++s) vf[ht][t][s] = vn[ht][t][s];
         }
     }
-    // merge the NW waves' partial softmax states
+    // merge the 4 waves' partial softmax states
     s_m[wave][lane] = S.m;  // identical in both halves
     s_l[wave][lane] = S.l;  // per-half partial sums
 #pragma unroll
@@ -738,34 +735,31 @@ __global__ void __launch_bounds__(64 * NW) k_attn_dir(const __bf16 *__restrict__
     __syncthreads();
     float M = -INFINITY;
 #pragma unroll
-    for (int w = 0; w < NW; ++w) M = fmaxf(M, s_m[w][lane]);
-    float fw[NW], L = 0.f;
+    for (int w = 0; w < 4; ++w) M = fmaxf(M, s_m[w][lane]);
+    float fw[4], L = 0.f;
 #pragma unroll
-    for (int w = 0; w < NW; ++w) {
+    for (int w = 0; w < 4; ++w) {
         const float mw = s_m[w][lane];
         fw[w] = mw == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(mw - M);  // a wave with no block
         L = fmaf(fw[w], s_l[w][r] + s_l[w][r + 32], L);
     }
     const float inv = 1.f / L;
     if (q < T) {
-        // wave w writes accumulator registers 4 (w % 4) .. + 3 of head-dim tile(s)
-        // w / 4 (NW = 8) or both (NW = 4): rows 32 ht + 8 (w % 4) + 4 h + e (4 contiguous
-        // head-dim values, one 8-B store)
+        // wave w writes accumulator registers 4w..4w+3 of both head-dim tiles:
+        // rows 32 ht + 8 w + 4 h + e (4 contiguous head-dim values, one 8-B store)
         const int b = bh / H, head = bh - b * H;
         __bf16 *dst = out + ((int64_t)b * T + q) * (int64_t)(H * AT_HD) + head * AT_HD;
-        const int wq = wave & 3;
 #pragma unroll
         for (int ht = 0; ht < 2; ++ht) {
-            if (NW == 8 && ht != (wave >> 2)) continue;
             bf16x4 v;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 float acc = 0.f;
 #pragma unroll
-                for (int w = 0; w < NW; ++w) acc = fmaf(fw[w], s_o[w][ht][4 * wq + e][lane], acc);
+                for (int w = 0; w < 4; ++w) acc = fmaf(fw[w], s_o[w][ht][4 * wave + e][lane], acc);
                 v[e] = (__bf16)(acc * inv);
             }
-            *(bf16x4 *)(dst + 32 * ht + 8 * wq + 4 * h) = v;
+            *(bf16x4 *)(dst + 32 * ht + 8 * wave + 4 * h) = v;
         }
     }
 }
@@ -927,73 +921,6 @@ __global__ void __launch_bounds__(256) k_upsample2x(const __bf16 *__restrict__ i
 }
 
 // ---------------------------------------------------------------------------
-// Register-streaming split-K GEMM for small M (the ViT's proj / fc2 at 481 tokens)
-// ---------------------------------------------------------------------------
-// One 256-thread workgroup per 32 x 32 output tile; wave w owns the K quarter
-// [w K / 4, (w + 1) K / 4) and streams its A and W fragments straight from memory into
-// registers (16 B per lane per 32x32x16 step, both operands K-contiguous), up to GD_CHUNK
-// steps in flight: no LDS staging and no barrier inside the K loop, whose per-step
-// global -> LDS -> barrier round trips bound k_gemm's split-K tile at this size.  The four
-// partial tiles are summed through LDS in wave order (deterministic), then the epilogue.
-#define GD_CHUNK 8
-
-template <int EPI>
-__global__ void __launch_bounds__(256) k_gemm_dir(sd_gemm_args g) {
-    __shared__ __attribute__((aligned(16))) float part[3 * 16 * 64];
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int r = lane & 31, h = lane >> 5;
-    const int64_t m0 = (int64_t)blockIdx.y * 32, n0 = (int64_t)blockIdx.x * 32;
-    const int64_t kq = g.K / 4, k0 = wave * kq;
-    const int S = (int)(kq / 16);
-    const __bf16 *ar = (const __bf16 *)g.a + min(m0 + r, g.M - 1) * g.lda + k0 + 8 * h;
-    const __bf16 *br = (const __bf16 *)g.w + min(n0 + r, g.N - 1) * g.K + k0 + 8 * h;
-    f32x16 acc = vt_zero16();
-    for (int c = 0; c < S; c += GD_CHUNK) {
-        bf16x8 fa[GD_CHUNK], fb[GD_CHUNK];
-#pragma unroll
-        for (int i = 0; i < GD_CHUNK; ++i) {
-            const int st = min(c + i, S - 1);
-            fa[i] = *(const bf16x8 *)(ar + 16 * st);
-            fb[i] = *(const bf16x8 *)(br + 16 * st);
-        }
-#pragma unroll
-        for (int i = 0; i < GD_CHUNK; ++i)
-            if (c + i < S) acc = VT_MFMA(fa[i], fb[i], acc);
-    }
-    if (wave > 0) {
-#pragma unroll
-        for (int q = 0; q < 16; ++q) part[((wave - 1) * 16 + q) * 64 + lane] = acc[q];
-    }
-    __syncthreads();
-    if (wave != 0) return;
-#pragma unroll
-    for (int w = 0; w < 3; ++w)
-#pragma unroll
-        for (int q = 0; q < 16; ++q) acc[q] += part[(w * 16 + q) * 64 + lane];
-    const int64_t n = n0 + r;
-    if (n >= g.N) return;
-    const float bias = g.bias ? g.bias[n] : 0.f;
-    const float gam = (EPI == SD_EPI_RESID && g.gamma) ? g.gamma[n] : 1.f;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        const int64_t m = m0 + (q & 3) + 8 * (q >> 2) + 4 * h;
-        if (m >= g.M) continue;
-        const float v = acc[q] + bias;
-        if (EPI == SD_EPI_RESID) {
-            float *o = (float *)g.out + m * g.ldo + n;
-            *o = *o + gam * v;
-        } else if (EPI == SD_EPI_F32) {
-            ((float *)g.out)[m * g.ldo + n] = v;
-        } else if (EPI == SD_EPI_GELU) {
-            ((__bf16 *)g.out)[m * g.ldo + n] = (__bf16)vt_gelu(v);
-        } else {
-            ((__bf16 *)g.out)[m * g.ldo + n] = (__bf16)v;
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
 // LayerNorm-prologue GEMM (the ViT's norm1 -> qkv and norm2 -> fc1 at small token counts)
 // ---------------------------------------------------------------------------
 // out = EPI(LN(x) W^T + b) for x (M, C) f32 residual-stream rows and W (N, C) bf16: the
@@ -1022,34 +949,55 @@ __global__ void __launch_bounds__(256) k_lngemm(sd_gemm_args g, const float *__r
     bf16x8 wb[NK];
 #pragma unroll
     for (int s = 0; s < NK; ++s) wb[s] = *(const bf16x8 *)(wr + 32 * s);
-    // LayerNorm of rows 8 w .. 8 w + 7 (one row per pass, lane = columns lane + 64 i)
-    for (int r = 0; r < 8; ++r) {
-        const int rl = 8 * wave + r;
-        const int64_t row = min(m0 + rl, g.M - 1);
-        const float *xr = x + row * C;
-        float v[PER];
-        float sum = 0.f;
+    // LayerNorm of rows 8 w .. 8 w + 7 (lane = columns lane + 64 i), RB rows at a time with
+    // all their loads issued first (one memory latency per batch, the reductions of the
+    // batch's rows interleaved)
+    constexpr int RB = PER <= 6 ? 8 : 4;
 #pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            v[i] = xr[lane + 64 * i];
-            sum += v[i];
+    for (int r0 = 0; r0 < 8; r0 += RB) {
+        float v[RB][PER];
+#pragma unroll
+        for (int rr = 0; rr < RB; ++rr) {
+            const float *xr = x + min(m0 + 8 * wave + r0 + rr, g.M - 1) * C;
+#pragma unroll
+            for (int i = 0; i < PER; ++i) v[rr][i] = xr[lane + 64 * i];
+        }
+        float mean[RB], rstd[RB];
+#pragma unroll
+        for (int rr = 0; rr < RB; ++rr) {
+            float sum = 0.f;
+#pragma unroll
+            for (int i = 0; i < PER; ++i) sum += v[rr][i];
+            mean[rr] = sum;
         }
 #pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) sum += __shfl_xor(sum, off);
-        const float mean = sum / (float)C;
-        float q = 0.f;
+        for (int off = 32; off >= 1; off >>= 1)
 #pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const float d = v[i] - mean;
-            q = fmaf(d, d, q);
+            for (int rr = 0; rr < RB; ++rr) mean[rr] += __shfl_xor(mean[rr], off);
+#pragma unroll
+        for (int rr = 0; rr < RB; ++rr) {
+            mean[rr] = mean[rr] / (float)C;
+            float q = 0.f;
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const float d = v[rr][i] - mean[rr];
+                q = fmaf(d, d, q);
+            }
+            rstd[rr] = q;
         }
 #pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) q += __shfl_xor(q, off);
-        const float rstd = 1.f / sqrtf(q / (float)C + eps);
+        for (int off = 32; off >= 1; off >>= 1)
 #pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const int c = lane + 64 * i;
-            sA[rl * LDA + c] = (__bf16)((v[i] - mean) * rstd * lw[c] + lb[c]);
+            for (int rr = 0; rr < RB; ++rr) rstd[rr] += __shfl_xor(rstd[rr], off);
+#pragma unroll
+        for (int rr = 0; rr < RB; ++rr) {
+            const float rs = 1.f / sqrtf(rstd[rr] / (float)C + eps);
+            const int rl = 8 * wave + r0 + rr;
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int c = lane + 64 * i;
+                sA[rl * LDA + c] = (__bf16)((v[rr][i] - mean[rr]) * rs * lw[c] + lb[c]);
+            }
         }
     }
     __syncthreads();
@@ -1139,10 +1087,6 @@ static void vt_launch_gemm(const sd_gemm_args &g, hipStream_t s) {
 #define SD_CONV_SK_MID 256  // conv: split-K tiles below this many 64x64 tiles (1024: no gain)
 #endif
 
-#ifndef SD_GEMM_DIR
-#define SD_GEMM_DIR 1  // small-M non-conv GEMMs on k_gemm_dir (0: k_gemm's split-K tile)
-#endif
-
 template <bool CONV>
 static void vt_pick_gemm(const sd_gemm_args &g, hipStream_t s) {
     // K steps of 64 whenever K allows (half the barriers, twice the work under each
@@ -1152,18 +1096,6 @@ static void vt_pick_gemm(const sd_gemm_args &g, hipStream_t s) {
     // conv: a 128-deep K step must stay inside one 3x3 tap (Cin % 128 == 0); the DPT's
     // low-resolution 256-channel convolutions (12x40, 24x80) are exactly these small-M,
     // large-K GEMMs
-    if (!CONV && SD_GEMM_DIR && mid < 256 && g.K % 64 == 0 && g.lda % 8 == 0 &&
-        (g.epi == SD_EPI_RESID || g.epi == SD_EPI_F32 || g.epi == SD_EPI_GELU ||
-         (g.epi == SD_EPI_BF16 && !g.res && !g.res2))) {
-        dim3 grid((unsigned)((g.N + 31) / 32), (unsigned)((g.M + 31) / 32));
-        switch (g.epi) {
-        case SD_EPI_RESID: hipLaunchKernelGGL(k_gemm_dir<SD_EPI_RESID>, grid, dim3(256), 0, s, g); break;
-        case SD_EPI_F32: hipLaunchKernelGGL(k_gemm_dir<SD_EPI_F32>, grid, dim3(256), 0, s, g); break;
-        case SD_EPI_GELU: hipLaunchKernelGGL(k_gemm_dir<SD_EPI_GELU>, grid, dim3(256), 0, s, g); break;
-        default: hipLaunchKernelGGL(k_gemm_dir<SD_EPI_BF16>, grid, dim3(256), 0, s, g); break;
-        }
-        return;
-    }
     if ((CONV ? g.Cin % 128 == 0 && mid < SD_CONV_SK_MID : mid < 256) && g.K % 128 == 0 &&
         g.K >= 256) {
         vt_launch_gemm<32, 32, 128, CONV>(g, s);  // split-K over the 4 waves
@@ -1282,7 +1214,6 @@ extern "C" int sd_attention(const void *q, const void *k, const void *vt, int32_
     const float sl2e = scale * 1.4426950408889634f;
     const int64_t wg128 = (int64_t)((tokens + 127) / 128) * B * heads;
     const char *force = getenv("SD_ATTN");
-    // SD_ATTN=lds / dir forces one (dir4: the 4-wave dir kernel)
     const bool lds = (force && force[0]) ? force[0] == 'l' : 2 * wg128 >= (int64_t)sd_num_cus();
     if (lds) {
         dim3 grid((unsigned)((tokens + 127) / 128), (unsigned)(B * heads));
@@ -1291,14 +1222,9 @@ extern "C" int sd_attention(const void *q, const void *k, const void *vt, int32_
                            (__bf16 *)out);
     } else {
         dim3 grid((unsigned)((tokens + 31) / 32), (unsigned)(B * heads));
-        if (tokens_pad >= 512 && !(force && strcmp(force, "dir4") == 0))
-            hipLaunchKernelGGL(k_attn_dir<8>, grid, dim3(512), 0, (hipStream_t)stream, (const __bf16 *)q,
-                               (const __bf16 *)k, (const __bf16 *)vt, tokens, tokens_pad, heads, sl2e,
-                               (__bf16 *)out);
-        else
-            hipLaunchKernelGGL(k_attn_dir<4>, grid, dim3(256), 0, (hipStream_t)stream, (const __bf16 *)q,
-                               (const __bf16 *)k, (const __bf16 *)vt, tokens, tokens_pad, heads, sl2e,
-                               (__bf16 *)out);
+        hipLaunchKernelGGL(k_attn_dir, grid, dim3(256), 0, (hipStream_t)stream, (const __bf16 *)q,
+                           (const __bf16 *)k, (const __bf16 *)vt, tokens, tokens_pad, heads, sl2e,
+                           (__bf16 *)out);
     }
     if (hipGetLastError() != hipSuccess) {
         sd_set_error("sd_attention: launch failed");
