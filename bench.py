@@ -707,25 +707,37 @@ def main_train(args, world, rank, device):
         n = args.steps
         print("host issue ms per step: " + ", ".join(f"{k} {1e3 * v / n:.3f}" for k, v in host.items()),
               file=sys.stderr, flush=True)
-    ms = {k: timer.mean_ms(k) for k in ("gather", "gather_bwd", "composite_bwd")}
+    ms = {k: timer.mean_ms(k) for k in ("gather", "gather_bwd", "composite_bwd", "mlp_bwd")}
     if world > 1:
         t = torch.tensor([elapsed] + [ms[k] for k in ms], device=device, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t[0])
         ms = {k: float(v) for k, v in zip(ms, t[1:])}
     n_pts = NB * RB * KT
-    chunk = n_pts  # points per k_field_gather_bwd launch (training path: one per pass)
-    # compulsory HBM bytes of one scatter launch: the C feature columns of the dX rows
-    # (4 C B per point) + the touched grid-gradient pixels written once (4 taps x 4 C B per
-    # texel quad; depends on the geometry) -- counted as the dX reads only, the floor
-    bwd_bytes = chunk * 4 * C_GRID
+    chunk = n_pts  # points per backward launch (training path: one per pass)
+    fused = amp and sda.FUSED_SCATTER
+    if fused:
+        # k_mlp_bwd with the grid_sample backward fused (ml_scatter): per point it reads
+        # d_sigma, sigma (4 + 4), d_dino (4 D), the saved H row (2 x 136) and xyz (12), and
+        # writes the dY (2 x 72) and dH (2 x 128) rows of the weight-gradient GEMMs = 948 B;
+        # the grid-gradient atomics depend on the geometry and are left out of the floor
+        kname, kkey, tkey = "k_mlp_bwd + fused grid_sample backward (sd_mlp_train_bwd)", \
+            "mlp_bwd", "k_mlp_bwd"
+        bwd_bytes = chunk * (8 + 4 * D_DINO + 2 * 136 + 12 + 2 * 72 + 2 * 128)
+    else:
+        # compulsory HBM bytes of one scatter launch: the C feature columns of the dX rows
+        # (4 C B per point) + the touched grid-gradient pixels written once (4 taps x 4 C B
+        # per texel quad; depends on the geometry) -- counted as the dX reads only, the floor
+        kname, kkey, tkey = "k_field_gather_bwd (sd_field_gather_bwd)", "gather_bwd", \
+            "k_field_gather_bwd"
+        bwd_bytes = chunk * 4 * C_GRID
     traffic, tsrc = None, None
-    tf = os.path.join(ROOT, "profiles", "r2_train_traffic.json")
-    if os.path.exists(tf):
+    for tf in ("r3_train_traffic.json", "r2_train_traffic.json"):
         try:
-            traffic = json.load(open(tf))["kernels"]["k_field_gather_bwd"]["hbm_bytes"]
-            tsrc = "profiles/r2_train_traffic.json (rocprofv3 PMC, per launch)"
-        except (KeyError, TypeError, ValueError):
+            traffic = json.load(open(os.path.join(ROOT, "profiles", tf)))["kernels"][tkey]["hbm_bytes"]
+            tsrc = f"profiles/{tf} (rocprofv3 PMC, per launch)"
+            break
+        except (OSError, KeyError, TypeError, ValueError):
             traffic = None
     line = {
         "metric": "training rays/sec (render forward + backward into grid and ResnetFC)",
@@ -742,13 +754,14 @@ def main_train(args, world, rank, device):
                                 ", rays from the encoder view"),
                    "points_per_step": n_pts,
                    "parallelism": f"dp{world} (4 frames per GPU, head gradients all-reduced)"},
-        "roofline": {"kernel": "k_field_gather_bwd (sd_field_gather_bwd)", "bound": "hbm",
+        "roofline": {"kernel": kname, "bound": "hbm",
                      "algorithmic_bytes_per_launch": bwd_bytes,
-                     "achieved": bwd_bytes / (ms["gather_bwd"] * 1e-3) / 1e9, "peak": 8000.0,
-                     "unit": "GB/s",
-                     "frac": bwd_bytes / (ms["gather_bwd"] * 1e-3) / 1e9 / 8000.0,
-                     "traffic": traffic, "traffic_source": tsrc, "kernel_ms": ms["gather_bwd"],
-                     "gather_ms": ms["gather"], "composite_bwd_ms": ms["composite_bwd"]},
+                     "achieved": bwd_bytes / (ms[kkey] * 1e-3) / 1e9 if ms[kkey] else None,
+                     "peak": 8000.0, "unit": "GB/s",
+                     "frac": bwd_bytes / (ms[kkey] * 1e-3) / 1e9 / 8000.0 if ms[kkey] else None,
+                     "traffic": traffic, "traffic_source": tsrc, "kernel_ms": ms[kkey],
+                     "gather_ms": ms["gather"], "composite_bwd_ms": ms["composite_bwd"],
+                     "mlp_bwd_ms": ms["mlp_bwd"], "gather_bwd_ms": ms["gather_bwd"]},
     }
     if rank == 0:
         print(json.dumps(line), flush=True)

@@ -464,7 +464,13 @@ int sd_upsample2x(const void *in, int32_t B, int32_t H, int32_t W, int32_t C, vo
  *   softplus(out_0), dino (N, D) f32 = out_1..D.
  * sd_mlp_train_bwd: from d_sigma (N), d_dino (N, D) f32: dy (N, 72) dtype = [d dino | d out_0
  *   | 0..], dh (N, 128) dtype = d relu-input, dx (N, lddx) dx_dtype = [dH W_in[:, :C] | 0..];
- *   the weight gradients are dh^T x and dy^T h (caller's GEMMs).  D <= 64, C % 32 == 0. */
+ *   the weight gradients are dh^T x and dy^T h (caller's GEMMs).  D <= 64, C % 32 == 0.
+ *   Fused grid_sample backward (dgrid != NULL; replaces dx + sd_field_gather_bwd, bts.py:
+ *   299-309): dX[:, :C], rounded to dtype like the autocast Linear's input gradient, is
+ *   scattered with the forward gather's bilinear weights straight into the NHWC f32 grid
+ *   gradient dgrid (N / P, Hf, Wf, C) (f32 atomics; the rows never reach HBM).  xyz (N, 3)
+ *   are the points, P the points per encoder frame, cam_f the (N / P) encoder camera
+ *   records; dx may then be NULL.  (N / P) * Hf * Wf * C < 2^31. */
 typedef struct sd_mlp_train_args {
     const void *x;
     int64_t N;
@@ -483,6 +489,11 @@ typedef struct sd_mlp_train_args {
     const void *wxf;       /* [C/32][8][64][8] W_in B fragments (dX)                       */
     void *dy, *dh;
     void *dx;
+    const float *xyz;      /* fused scatter (dgrid != NULL): (N, 3) points                  */
+    const float *cam_f;    /* (N / P, SD_CAM_WORDS) encoder camera records                 */
+    float *dgrid;          /* (N / P, Hf, Wf, C) f32, accumulated into; NULL: write dx       */
+    int64_t P;
+    int32_t Hf, Wf;
 } sd_mlp_train_args;
 
 /* Weight gradients of the training MLP: part[w] (Ma_pad x Nb_pad f32, pads to 32) =

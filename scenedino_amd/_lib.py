@@ -14,7 +14,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # SDHIP_LIB: alternative build of the same library (diagnostic builds only)
 LIB_PATH = os.environ.get("SDHIP_LIB") or os.path.join(_HERE, "libsdhip.so")
-ABI_VERSION = 8
+ABI_VERSION = 9
 CAM_WORDS = 36  # floats per camera record (include/sdhip.h SD_CAM_WORDS)
 
 SD_F32 = 0
@@ -117,7 +117,8 @@ class SdMlpTrainArgs(ctypes.Structure):
         ("x", _vp), ("N", _i64), ("ldx", _i32), ("kx", _i32), ("dtype", _i32), ("D", _i32),
         ("C", _i32), ("lddx", _i32), ("dx_dtype", _i32), ("pad", _i32), ("w1f", _vp), ("w2f", _vp), ("b_out", _vp), ("h", _vp),
         ("sigma", _vp), ("dino", _vp), ("d_sigma", _vp), ("d_dino", _vp), ("wtf", _vp),
-        ("wxf", _vp), ("dy", _vp), ("dh", _vp), ("dx", _vp),
+        ("wxf", _vp), ("dy", _vp), ("dh", _vp), ("dx", _vp), ("xyz", _vp), ("cam_f", _vp),
+        ("dgrid", _vp), ("P", _i64), ("Hf", _i32), ("Wf", _i32),
     ]
 
 

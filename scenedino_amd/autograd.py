@@ -16,6 +16,8 @@ No CPU fallback: every op here is a HIP kernel or a torch GPU op.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib
@@ -224,11 +226,13 @@ class FieldMLPFused(torch.autograd.Function):
         return (dx if ctx.needs_input_grad[0] else None, *rest, None)
 
     @staticmethod
-    def grads(ctx, g_sigma, g_dino, full_rows=False, dx16=False):
+    def grads(ctx, g_sigma, g_dino, full_rows=False, dx16=False, scatter=None):
         """(dX, dW_in, db_in, dW_out, db_out) of the saved forward; dX rows are the C
         feature columns, or (full_rows) as wide as x with zero code / ones columns; f32, or
         (dx16) in x's 16-bit dtype -- the dtype the reference's autocast Linear backward
-        hands to grid_sample's backward."""
+        hands to grid_sample's backward.  ``scatter = (xyz (B, P, 3), cam_f, Hf, Wf, dgrid)``:
+        the grid_sample backward fused into the kernel -- dX (in x's dtype) goes straight
+        into the NHWC f32 grid gradient dgrid, and dX is returned as None."""
         x_aug, h, sigma = ctx.saved_tensors
         p = ctx.p
         N, ldx, d_in, D, C, dt, pdt = ctx.meta
@@ -237,14 +241,24 @@ class FieldMLPFused(torch.autograd.Function):
         g_dino = (g_dino if g_dino is not None else torch.zeros(N, D, device=dev)).float().contiguous()
         dy = torch.empty(N, 72, device=dev, dtype=x_aug.dtype)
         dh = torch.empty(N, 128, device=dev, dtype=x_aug.dtype)
-        dx = torch.empty(N, ldx if full_rows else C, device=dev,
-                         dtype=x_aug.dtype if dx16 else torch.float32)
         a = _lib.SdMlpTrainArgs(x=x_aug.data_ptr(), N=N, ldx=ldx, kx=d_in + 1, dtype=dt, D=D, C=C,
-                                lddx=dx.shape[1], dx_dtype=dt if dx16 else _lib.SD_F32,
                                 h=h.data_ptr(), sigma=sigma.data_ptr(), d_sigma=g_sigma.data_ptr(),
                                 d_dino=g_dino.data_ptr(), wtf=p.wtf.data_ptr(),
-                                wxf=p.wxf.data_ptr(), dy=dy.data_ptr(), dh=dh.data_ptr(),
-                                dx=dx.data_ptr())
+                                wxf=p.wxf.data_ptr(), dy=dy.data_ptr(), dh=dh.data_ptr())
+        if scatter is not None:
+            xyz, cam_f, Hf, Wf, dgrid = scatter
+            xyz = xyz.contiguous()
+            assert xyz.shape[0] * xyz.shape[1] == N and dgrid.dtype == torch.float32 and \
+                dgrid.is_contiguous() and dgrid.shape == (xyz.shape[0], Hf, Wf, C)
+            dx = None
+            a.dx_dtype, a.lddx = dt, C
+            a.xyz, a.cam_f, a.dgrid = xyz.data_ptr(), cam_f.data_ptr(), dgrid.data_ptr()
+            a.P, a.Hf, a.Wf = xyz.shape[1], Hf, Wf
+        else:
+            dx = torch.empty(N, ldx if full_rows else C, device=dev,
+                             dtype=x_aug.dtype if dx16 else torch.float32)
+            a.lddx, a.dx_dtype = dx.shape[1], dt if dx16 else _lib.SD_F32
+            a.dx = dx.data_ptr()
         _timed("mlp_bwd", lambda: _lib.mlp_train_bwd(a, x_aug))
         dW1 = _lib.wgrad(dh, x_aug, 128, d_in + 1)   # (128, d_in + 1): [dW_in | db_in]
         dWo = _lib.wgrad(dy, h, 72, 136)             # rows dino 0..D-1, out_0; col 128 bias
@@ -256,8 +270,11 @@ class FieldMLPFused(torch.autograd.Function):
 
 # 16-bit dX rows from the fused MLP backward into the gather's scatter (the autocast
 # gradient dtype; halves the dX bytes): measured slower overall -- k_mlp_bwd 125 -> 103 us
-# but k_field_gather_bwd 140 -> 223 us on 2-byte lane loads -- so f32 rows by default
+# but k_field_gather_bwd 140 -> 223 us on 2-byte lane loads -- so f32 rows when unfused
 DX16 = False
+# the grid_sample backward fused into k_mlp_bwd (ml_scatter): no dX rows in HBM at all.
+# SCENEDINO_AMD_FUSED_SCATTER=0 restores dX rows + k_field_gather_bwd (A/B diagnostics)
+FUSED_SCATTER = os.environ.get("SCENEDINO_AMD_FUSED_SCATTER", "1") != "0"
 
 
 class FieldGatherMLP(torch.autograd.Function):
@@ -295,8 +312,19 @@ class FieldGatherMLP(torch.autograd.Function):
         N = ctx.meta[0]
         gs = g_sigma.reshape(N) if g_sigma is not None else None
         gd = g_dino.reshape(N, -1) if g_dino is not None else None
-        dx, dw_in, db_in, dw_out, db_out = FieldMLPFused.grads(ctx, gs, gd, dx16=DX16)
         B, Hf, Wf, C = ctx.grid_shape
+        if FUSED_SCATTER and ctx.invf is None:  # (learn_empty rows need their dX: unfused)
+            d_grid = None
+            if ctx.needs_input_grad[0]:
+                buf, first = ctx.acc.take((B, Hf, Wf, C), ctx.xyz.device)
+                sc = (ctx.xyz, ctx.cam_f, Hf, Wf, buf)
+                _, dw_in, db_in, dw_out, db_out = FieldMLPFused.grads(ctx, gs, gd, scatter=sc)
+                d_grid = buf if first else None
+            else:
+                _, dw_in, db_in, dw_out, db_out = FieldMLPFused.grads(ctx, gs, gd, dx16=True)
+            return (d_grid, None, None, None, None, None, None, None, dw_in, db_in, dw_out,
+                    db_out)
+        dx, dw_in, db_in, dw_out, db_out = FieldMLPFused.grads(ctx, gs, gd, dx16=DX16)
         d_empty = None
         if ctx.invf is not None:
             m = ctx.invf.reshape(N, 1)

@@ -32,6 +32,7 @@
 // PositionalEncoding + encoding_mode._z (common/positional_encoding.py:13-80),
 // pinhole projection (common/cameras/pinhole.py:40-112).
 #include "sdhip_point.h"
+#include "sdhip_render.h"
 
 #include <string.h>
 
@@ -41,7 +42,7 @@ extern "C" void sd_set_error(const char *msg) {
     g_err[sizeof(g_err) - 1] = 0;
 }
 extern "C" const char *sd_last_error(void) { return g_err; }
-extern "C" int sd_abi_version(void) { return 8; }
+extern "C" int sd_abi_version(void) { return 9; }
 
 // Threads per workgroup, one workgroup per CU: 16-bit kernels run 8 waves (2 per SIMD,
 // <= 256 VGPRs each); the f32 parity kernels run 4 waves (1 per SIMD, 512 VGPRs).
@@ -100,6 +101,13 @@ __device__ __forceinline__ Raw16 sd_load16(__amdgpu_buffer_rsrc_t rs, const TapO
     return r;
 }
 
+// 16-bit field blends: 1 = v_perm + v_dot2 with (w00, w01), (w10, w11) packed in the grid's
+// 16-bit type (the projected render kernels' form: ~half the VALU of the unpack + FMA chain,
+// the weights rounded to the operand type like the MFMA blend of k_render_tile)
+#ifndef SD_FQ_DOT2
+#define SD_FQ_DOT2 1
+#endif
+
 template <> struct Prec<SD_BF16> {
     typedef uint16_t G;
     typedef Raw16 Raw;
@@ -116,6 +124,8 @@ template <> struct Prec<SD_BF16> {
         return fmaf(vd, t.w11, fmaf(vc, t.w10, fmaf(vb, t.w01, va * t.w00)));
     }
     static __device__ __forceinline__ Frag blend(const Raw &r, const Taps &t) {
+        if (SD_FQ_DOT2)  // horizontal tap pairs by v_perm, two v_dot2 per channel
+            return sd_blend_plain<SD_BF16>(r.a, r.b, r.c, r.d, sd_pack_w<SD_BF16>(t.w00, t.w01, t.w10, t.w11));
         uint32_t A[4] = {r.a.x, r.a.y, r.a.z, r.a.w}, B[4] = {r.b.x, r.b.y, r.b.z, r.b.w};
         uint32_t Cc[4] = {r.c.x, r.c.y, r.c.z, r.c.w}, D[4] = {r.d.x, r.d.y, r.d.z, r.d.w};
         Frag o;
@@ -694,6 +704,9 @@ k_field(const sd_field_args a, const sd_mlp m, const LdsPlan pl) {
     const int64_t cplane = (int64_t)a.Hc * a.Wc * 4;
     // one descriptor over all batch planes (host checks B * plane < 4 GiB)
     const __amdgpu_buffer_rsrc_t rs = sd_rsrc(a.grid, (uint32_t)(a.B * (int64_t)plane_bytes));
+    // the dino output (NP x D, f32 or bf16; < 4 GiB, checked by the host)
+    const __amdgpu_buffer_rsrc_t rdino =
+        sd_rsrc(a.dino, (uint32_t)(NP * m.D * (a.dino_dtype == SD_BF16 ? 2 : 4)));
 
     // XCD-aware tile ranges (workgroups b, b + 8, ... share an XCD: speed only): XCD x
     // visits tiles [x T / 8, (x + 1) T / 8) of the (optionally locality-sorted) order, its
@@ -814,18 +827,22 @@ k_field(const sd_field_args a, const sd_mlp m, const LdsPlan pl) {
             const float bd = m.b_dino[dim];
             if (SD_FQ_ABL_NOSTORE) {
                 if (ov[0] == 12345.f) a.dino[tile] = ov[1];  // keep the product alive
-            } else if (a.dino_dtype == SD_BF16) {  // (the seg head's input: half the bytes)
-                __bf16 *d16 = (__bf16 *)(void *)a.dino;
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int64_t pr = tile * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    if (pr < NP) d16[pr * m.D + dim] = (__bf16)(ov[r] + bd);
-                }
             } else {
+                // buffer stores at per-lane byte offsets (row, column dim): rows past the
+                // last point fall outside the descriptor's range (the range check covers the
+                // vector + instruction offset, not the scalar one: the row goes in the
+                // vector offset) and are dropped -- no bounds test per store
+                const uint32_t esz = a.dino_dtype == SD_BF16 ? 2u : 4u;
+                const uint32_t vo = (uint32_t)(((tile * 32 + 4 * h) * m.D + dim) * esz);
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    const int64_t pr = tile * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    if (pr < NP) a.dino[pr * m.D + dim] = ov[r] + bd;
+                    const uint32_t ro = vo + (uint32_t)(((r & 3) + 8 * (r >> 2)) * m.D) * esz;
+                    if (a.dino_dtype == SD_BF16)
+                        __builtin_amdgcn_raw_buffer_store_b16(
+                            __builtin_bit_cast(uint16_t, (__bf16)(ov[r] + bd)), rdino, ro, 0, 0);
+                    else
+                        __builtin_amdgcn_raw_buffer_store_b32(
+                            __builtin_bit_cast(uint32_t, ov[r] + bd), rdino, ro, 0, 0);
                 }
             }
         }
@@ -1001,6 +1018,7 @@ extern "C" int sd_field_query(const sd_field_args *args, const sd_mlp *mlp, void
     if (a.B <= 0 || a.P < 0 || !a.xyz || !a.grid || !a.cam_f || !a.sigma || !a.dino ||
         a.Hf <= 0 || a.Wf <= 0 || a.nv < 0 || a.nv > SD_MAX_NV ||
         (a.dino_dtype != SD_F32 && a.dino_dtype != SD_BF16) ||
+        a.B * a.P * (int64_t)mlp->D * (a.dino_dtype == SD_BF16 ? 2 : 4) >= (1LL << 32) ||
         a.B * (int64_t)a.Hf * a.Wf * mlp->C * (mlp->dtype == SD_F32 ? 4 : 2) >= (1LL << 32) ||
         (a.nv > 0 && (a.rgb || a.invalid) && (!a.img || !a.cam_c || a.Hc <= 0 || a.Wc <= 0))) {
         sd_set_error("sd_field_query: invalid argument (all grid planes < 4 GiB)");

@@ -6,7 +6,8 @@
 //               out = H W_o^T + b_o, sigma = softplus(out_0) (bts.py:516-541, threshold 20),
 //               dino = out_1..D; H is kept (16-bit, + a ones column) for the backward.
 //   k_mlp_bwd : dY = [d dino | d sigma . sigmoid(out_0)], dH^T = (W_o^T dY^T) * [H > 0],
-//               dX = dH W_in[:, :C] (f32 rows for sd_field_gather_bwd); dY and dH rows are
+//               dX = dH W_in[:, :C] (f32 rows for sd_field_gather_bwd, or -- dgrid set --
+//               scattered straight into the grid gradient, ml_scatter); dY and dH rows are
 //               written for the weight-gradient GEMMs (dW1 = dH^T X, dW_o = dY^T [H | 1]).
 //
 // Work unit: one wave = 32 points (MFMA v_mfma_f32_32x32x16_{f16,bf16}), 8 waves per
@@ -136,7 +137,149 @@ __global__ void __launch_bounds__(ML_WAVES * 64) k_mlp_fwd(const sd_mlp_train_ar
     }
 }
 
+// ---------------------------------------------------------------------------
+// Fused grid_sample backward of k_mlp_bwd (dgrid != NULL; bts.py:299-309).  The wave's 32
+// points split into runs of consecutive points with the same frame and taps (a ray's
+// samples: one run per ray when the render view is the encoder view).  The scatter is a
+// product, G = S dX: S (rows = run x tap, columns = the 32 points) holds each point's
+// bilinear weight of that tap in its run's rows, and dX (32 points x 32 channels) is the
+// accumulator tile of dX = dH W_in re-used in registers as the B operand -- rounded to the
+// autocast dtype, the dtype of the reference's Linear input gradient.  S enters as hi + lo
+// 16-bit parts (the weights keep >= 16 bits).  Each nonzero G element is one f32 atomic add
+// into the grid gradient: the atomics of the run-summing k_field_gather_bwd, without the
+// dX rows' HBM round trip.  Per-wave LDS tables: w[4][32] f32, run[32], off[32][4] (the
+// element offsets of a run's four tap rows in dgrid).
+// ---------------------------------------------------------------------------
+#define ML_SCR_WORDS (4 * 32 + 32 + 32 * 4)
+
+__device__ __forceinline__ void ml_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// tables of the wave's tile (at the tile start, while the dY loads are in flight);
+// returns the number of runs
+__device__ __forceinline__ int ml_scatter_tables(const sd_mlp_train_args &a, int *scr,
+                                                 int64_t pt, bool valid, int lane) {
+    const int h = lane >> 5, r = lane & 31;
+    float *sw = (float *)scr;
+    int *srun = scr + 128, *soff = scr + 160;
+    // geometry of point pt (both halves; the forward gather's sd_point_geo, same taps)
+    int gi[4] = {0, 0, 0, 0}, gb = -1;
+    float gw[4] = {0.f, 0.f, 0.f, 0.f};
+    if (valid) {
+        const int64_t b = pt / a.P;
+        const PointGeo geo = sd_point_geo(a.cam_f + b * SD_CAM_WORDS, a.xyz[pt * 3],
+                                          a.xyz[pt * 3 + 1], a.xyz[pt * 3 + 2], a.Wf, a.Hf);
+        gi[0] = geo.t.i00; gi[1] = geo.t.i01; gi[2] = geo.t.i10; gi[3] = geo.t.i11;
+        gw[0] = geo.t.w00; gw[1] = geo.t.w01; gw[2] = geo.t.w10; gw[3] = geo.t.w11;
+        gb = (int)b;
+    }
+    // a point opens a run unless it has the previous point's frame and taps
+    const int src = ((lane - 1) & 63) * 4;
+    const int pb = __builtin_amdgcn_ds_bpermute(src, gb);
+    int pi[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) pi[t] = __builtin_amdgcn_ds_bpermute(src, gi[t]);
+    const bool open = valid && (r == 0 || pb != gb || pi[0] != gi[0] || pi[1] != gi[1] ||
+                                pi[2] != gi[2] || pi[3] != gi[3]);
+    const uint64_t om = __ballot(open) & 0xffffffffull;
+    const int run = valid ? __builtin_popcountll(om & ((2ull << r) - 1)) - 1 : -1;
+    ml_wave_sync();  // the previous tile's table reads are done
+    if (h == 0) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) sw[32 * t + r] = gw[t];
+        srun[r] = run;
+        if (open)
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                soff[4 * run + t] = (int)(((int64_t)gb * a.Hf * a.Wf + gi[t]) * a.C);
+    }
+    ml_wave_sync();
+    return __builtin_popcountll(om);
+}
+
+// S fragments of row tile mt (A operand in the k order kappa of ml_frag: k-step s, lane
+// half h, element j = point 16 s + 8 (j >> 2) + 4 h + (j & 3)); row r = run 8 mt + r / 4,
+// tap r % 4
 template <int P>
+__device__ __forceinline__ void ml_s_frags(const int *scr, int mt, int lane,
+                                           typename T16<P>::Frag (&sh)[2],
+                                           typename T16<P>::Frag (&sl)[2]) {
+    typedef typename T16<P>::E E;
+    const int h = lane >> 5, r = lane & 31;
+    const float *sw = (const float *)scr;
+    const int *srun = scr + 128;
+    const int k = 8 * mt + (r >> 2), t = r & 3;
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int q = 16 * s + 8 * (j >> 2) + 4 * h + (j & 3);
+            const float w = srun[q] == k ? sw[32 * t + q] : 0.f;
+            const E hi = (E)w;
+            sh[s][j] = hi;
+            sl[s][j] = (E)(w - (float)hi);
+        }
+}
+
+// G = S dX for one 32-channel column tile and row tile mt, and its atomics.  The G rows of
+// this lane: run 8 mt + 2 (i >> 2) + h, tap i % 4.
+template <int P>
+__device__ __forceinline__ void ml_s_emit(const int *scr, int mt, int nr, int lane,
+                                          const typename T16<P>::Frag (&sh)[2],
+                                          const typename T16<P>::Frag (&sl)[2],
+                                          const typename T16<P>::Frag &b0,
+                                          const typename T16<P>::Frag &b1, float *dg) {
+    typedef T16<P> Tr;
+    const int h = lane >> 5;
+    const int *soff = scr + 160;
+    f32x16 g;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) g[i] = 0.f;
+    g = Tr::mma32(sh[0], b0, g);
+    g = Tr::mma32(sh[1], b1, g);
+    g = Tr::mma32(sl[0], b0, g);
+    g = Tr::mma32(sl[1], b1, g);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int kk = 8 * mt + 2 * (i >> 2) + h;
+        if (kk < nr && g[i] != 0.f) unsafeAtomicAdd(dg + soff[4 * kk + (i & 3)], g[i]);
+    }
+}
+
+// dX = dH W_in, 32 channels at a time, each tile straight into ml_s_emit
+template <int P>
+__device__ __forceinline__ void ml_scatter(const sd_mlp_train_args &a,
+                                           const typename T16<P>::Frag (&af)[8],
+                                           const typename T16<P>::Frag *wx, const int *scr,
+                                           int nr, int lane) {
+    typedef T16<P> Tr;
+    typedef typename Tr::Frag Frag;
+    const int r = lane & 31;
+    Frag s0h[2], s0l[2];
+    ml_s_frags<P>(scr, 0, lane, s0h, s0l);
+    const int nmt = (nr + 7) >> 3;
+    const int UC = a.C >> 5;
+    for (int u = 0; u < UC; ++u) {
+        f32x16 o;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[i] = 0.f;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) o = Tr::mma32(af[s], wx[(u * 8 + s) * 64 + lane], o);
+        const Frag b0 = ml_frag<P>(o, 0), b1 = ml_frag<P>(o, 1);
+        float *dg = a.dgrid + 32 * u + r;
+        ml_s_emit<P>(scr, 0, nr, lane, s0h, s0l, b0, b1, dg);
+        for (int mt = 1; mt < nmt; ++mt) {  // more than 8 runs: points off the encoder view
+            Frag sh[2], sl[2];
+            ml_s_frags<P>(scr, mt, lane, sh, sl);
+            ml_s_emit<P>(scr, mt, nr, lane, sh, sl, b0, b1, dg);
+        }
+    }
+}
+
+template <int P, bool SCAT>
 __global__ void __launch_bounds__(ML_WAVES * 64) k_mlp_bwd(const sd_mlp_train_args a) {
     typedef T16<P> Tr;
     typedef typename Tr::Frag Frag;
@@ -154,6 +297,7 @@ __global__ void __launch_bounds__(ML_WAVES * 64) k_mlp_bwd(const sd_mlp_train_ar
     }
     const Frag *wt = (const Frag *)lds;
     const Frag *wx = wt + n1;
+    int *scr = (int *)(lds + (n1 + n2) * 16);  // per-wave scatter tables (ml_scatter)
     const int lane = threadIdx.x & 63, h = lane >> 5, r = lane & 31;
     const int wave = threadIdx.x >> 6;
     const int64_t ntile = (a.N + 31) >> 5;
@@ -164,6 +308,8 @@ __global__ void __launch_bounds__(ML_WAVES * 64) k_mlp_bwd(const sd_mlp_train_ar
         const bool valid = pt < a.N;
         const int64_t pc = valid ? pt : a.N - 1;
         // dY^T as B operand: lane (point r, half h), k-step s: dY[point][16 s + 8 h + j]
+        int *wscr = scr + wave * ML_SCR_WORDS;
+        const int nr = SCAT ? ml_scatter_tables(a, wscr, pt, valid, lane) : 0;
         const float sg = a.sigma[pc];
         const float dsg = valid ? a.d_sigma[pc] * (1.f - expf(-sg)) : 0.f;  // softplus'
         E *dyr = (E *)a.dy + pt * ML_DYLD;
@@ -234,6 +380,10 @@ __global__ void __launch_bounds__(ML_WAVES * 64) k_mlp_bwd(const sd_mlp_train_ar
         Frag af[8];
 #pragma unroll
         for (int s = 0; s < 8; ++s) af[s] = ml_frag<P>(dh[s >> 1], s & 1);
+        if constexpr (SCAT) {  // fused grid_sample backward: no dX rows
+            ml_scatter<P>(a, af, wx, wscr, nr, lane);
+            continue;
+        }
         for (int u = 0; u < UC; ++u) {
             f32x16 o;
 #pragma unroll
@@ -273,8 +423,13 @@ static int ml_check(const sd_mlp_train_args *a, bool bwd) {
         a->C > a->kx || a->N * a->ldx * 2 >= (1LL << 32))
         return 0;
     if (!bwd) return a->x && a->w1f && a->w2f && a->b_out && a->h && a->sigma && a->dino;
-    return a->lddx >= a->C && a->lddx <= a->ldx && (a->dx_dtype == SD_F32 || a->dx_dtype == a->dtype) && a->wtf && a->wxf && a->h && a->sigma && a->d_sigma && a->d_dino && a->dy && a->dh &&
-           a->dx;
+    if (!(a->wtf && a->wxf && a->h && a->sigma && a->d_sigma && a->d_dino && a->dy && a->dh))
+        return 0;
+    if (a->dgrid)  // fused scatter: the frame / grid geometry of the forward gather
+        return a->xyz && a->cam_f && a->P > 0 && a->N % a->P == 0 && a->Hf > 0 && a->Wf > 0 &&
+               (a->N / a->P) * a->Hf * a->Wf * (int64_t)a->C < (1LL << 31);
+    return a->lddx >= a->C && a->lddx <= a->ldx &&
+           (a->dx_dtype == SD_F32 || a->dx_dtype == a->dtype) && a->dx;
 }
 
 template <typename K>
@@ -320,9 +475,13 @@ extern "C" int sd_mlp_train_bwd(const sd_mlp_train_args *a, void *stream) {
     }
     if (a->N == 0) return 0;
     const int KO = (a->D + 1 + 15) / 16;
-    const int lds = (4 * KO + (a->C / 32) * 8) * 64 * 16;
-    if (a->dtype == SD_F16) return ml_launch(k_mlp_bwd<SD_F16>, a, lds, (hipStream_t)stream);
-    return ml_launch(k_mlp_bwd<SD_BF16>, a, lds, (hipStream_t)stream);
+    const int lds = (4 * KO + (a->C / 32) * 8) * 64 * 16 + ML_WAVES * ML_SCR_WORDS * 4;
+    hipStream_t s = (hipStream_t)stream;
+    if (a->dgrid)
+        return a->dtype == SD_F16 ? ml_launch(k_mlp_bwd<SD_F16, true>, a, lds, s)
+                                  : ml_launch(k_mlp_bwd<SD_BF16, true>, a, lds, s);
+    return a->dtype == SD_F16 ? ml_launch(k_mlp_bwd<SD_F16, false>, a, lds, s)
+                              : ml_launch(k_mlp_bwd<SD_BF16, false>, a, lds, s);
 }
 
 // ---------------------------------------------------------------------------
