@@ -144,7 +144,10 @@ typedef struct sd_render_args {
     const void *grid; int32_t Hf, Wf;     /* (B, Hf, Wf, C) NHWC                   */
     const float *cam_f;                   /* (B, 36)                               */
     const float *img; int32_t nv, Hc, Wc; /* (B, nv, Hc, Wc, 4) or NULL if nv==0   */
-    const float *cam_c;                   /* (B, nv, 36)                           */
+    const float *cam_c;                   /* (B, nv, 36); may alias cam_f (nv == 1, */
+                                          /* colour view = encoder view): the render */
+                                          /* kernels then re-use the encoder taps    */
+                                          /* for the colours at equal resolution     */
     int32_t hard_alpha_cap;
     /* required outputs */
     float *depth;      /* (R)        */

@@ -117,6 +117,18 @@ extern "C" int sd_tile_prof(unsigned long long *out, int reset) {
 #ifndef ST_CODE_FIRST
 #define ST_CODE_FIRST 0     // 1: positional-code MFMAs before the tap blend (spills)
 #endif
+#ifndef ST_HEAD_PF
+#define ST_HEAD_PF 0        // 0: the DINO head loads its W_dino fragments itself (no prefetch across the ray pass)
+#endif
+#ifndef ST_COL_EARLY
+#define ST_COL_EARLY 0      // 1: the next ray's colour texels blended right after its ray pass (not after item 0)
+#endif
+#ifndef ST_HEAD_FIRST
+#define ST_HEAD_FIRST 0     // 1: the previous group's DINO head at the top of the step (before the ray pass)
+#endif
+#ifndef ST_SAME_CAM
+#define ST_SAME_CAM 1       // colour taps re-use the encoder-view projection when cam_c == cam_f
+#endif
 #ifndef ST_FASTPROJ
 #define ST_FASTPROJ 1       // fused-record projection (0: the two-step reference one)
 #endif
@@ -355,6 +367,10 @@ k_render_tile(const st_args sa) {
             // address would turn the camera-record reads into vector loads)
             const int sbi = __builtin_amdgcn_readfirstlane((int)((unsigned)ray / (unsigned)rps));
             rl = (const float *)(lds + ST_L_RAY + (wave * 2 + slot) * 32);
+            // colour view = encoder view (the single-frame render, ids_render = ids_encoder):
+            // the host passes the same camera records for both (cam_c == cam_f), so the
+            // colour taps are the encoder-view taps at equal resolution (kernel-uniform test)
+            const bool same_cam = ST_SAME_CAM && a.cam_c == a.cam_f && a.Wc == Wf && a.Hc == Hf;
             float zq[2 * ST_MAXP];
             load_ray_z(ray, zq);
             ST_T(10);
@@ -372,8 +388,13 @@ k_render_tile(const st_args sa) {
                                                             Wf, Hf);
                     const uint32_t x0 = (uint32_t)geo.t.x0, y0 = (uint32_t)geo.t.y0;
                     bool ic;
-                    const Taps tc = ST_CTAPS((sd_cfloat *)(a.cam_c + sbi * SD_CAM_WORDS), a.Wc, a.Hc, px, py,
-                                                  pz, ic);
+                    Taps tc;
+                    if (same_cam) {  // colour view = encoder view: the same projection and taps
+                        tc = geo.t;
+                        ic = geo.inv_f;
+                    } else {
+                        tc = ST_CTAPS((sd_cfloat *)(a.cam_c + sbi * SD_CAM_WORDS), a.Wc, a.Hc, px, py, pz, ic);
+                    }
                     const uint32_t xy = x0 | (y0 << 15) | (geo.inv_f ? 1u << 30 : 0u) |
                                         (ic ? 1u << 31 : 0u);
                     const uint4 wp = sd_pack_w<P>(geo.t.w00, geo.t.w01, geo.t.w10, geo.t.w11);
@@ -535,7 +556,7 @@ k_render_tile(const st_args sa) {
     // W_dino fragments of the wave's first head tile (dt = wave), loaded one phase ahead
     Frag Wh[4];
     auto head_prefetch = [&]() {
-        if (wave < ndt) {
+        if (ST_HEAD_PF && wave < ndt) {
             const Frag *wo = (const Frag *)m.w_out + (int64_t)wave * 4 * SD_WAVE + lane;
 #pragma unroll
             for (int s = 0; s < 4; ++s) Wh[s] = wo[s * SD_WAVE];
@@ -559,7 +580,7 @@ k_render_tile(const st_args sa) {
             const Frag *wo = (const Frag *)m.w_out + (int64_t)dt * 4 * SD_WAVE + lane;
             f32x4 o = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int s = 0; s < 4; ++s) o = Tr::mma(dt == wave ? Wh[s] : wo[s * SD_WAVE], Bh[s], o);
+            for (int s = 0; s < 4; ++s) o = Tr::mma(ST_HEAD_PF && dt == wave ? Wh[s] : wo[s * SD_WAVE], Bh[s], o);
             // rows 4 g + r of tile dt = dims 16 dt + 4 g + r, column j = ray slot
             const int dim = 16 * dt + 4 * g;
             const f32x4 bd = *(const f32x4 *)(m.b_dino + dim);
@@ -880,15 +901,17 @@ k_render_tile(const st_args sa) {
         };
 
         // item 0 with the next ray's pass and the previous group's head
-        if (prev_ok && !ST_ABL_NOHEAD) head_prefetch();
+        if (ST_HEAD_FIRST && prev_ok && !ST_ABL_NOHEAD) head(prev_grp);
+        if (!ST_HEAD_FIRST && prev_ok && !ST_ABL_NOHEAD) head_prefetch();
         if (has_next && (!ST_ABL_NORAY || n == 0)) ray_pass(nray, buf ^ 1, buf ^ 1);
+        if (ST_COL_EARLY && has_next && (!ST_ABL_NORAY || n == 0)) ray_col(nray, buf ^ 1);
         ST_T(0);
-        if (prev_ok && !ST_ABL_NOHEAD) head(prev_grp);
+        if (!ST_HEAD_FIRST && prev_ok && !ST_ABL_NOHEAD) head(prev_grp);
         ST_T(1);
         IState s0, s1;
         if (active && !ST_ABL_NOITEM) itemA(0, s0);
         ST_T(2);
-        if (has_next && (!ST_ABL_NORAY || n == 0)) ray_col(nray, buf ^ 1);
+        if (!ST_COL_EARLY && has_next && (!ST_ABL_NORAY || n == 0)) ray_col(nray, buf ^ 1);
         ST_T(3);
         st_barrier_lds();  // X: next boxes visible; the head has read the hsum area
         ST_T(4);

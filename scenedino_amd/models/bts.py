@@ -199,6 +199,9 @@ class BTSNet(nn.Module):
         self.grid_c_Ks = Ks_render
         self.grid_c_poses_w2c = poses_w2c_render
         self.grid_c_combine = None
+        # colour view = encoder view (the single-frame render): one set of camera records
+        # for both, which lets the render kernel re-use the encoder projection for colours
+        self._same_views = list(ids_encoder or []) == list(ids_render or [])
         # the ground-truth (loss) features: a second ViT pass (bts.py:207) that only the
         # training loss reads -- run on first access of grid_l_loss_features (SURVEY
         # §8(f) rank 3), so a pure render / voxel query never pays for it
@@ -308,8 +311,11 @@ class BTSNet(nn.Module):
             "C": C, "Hf": Hf, "Wf": Wf, "B": B,
             "cam_f": _cam_records(self.grid_f_poses_w2c[:, 0], self.grid_f_Ks[:, 0]),
             "img": img, "nv": nv, "Hc": H, "Wc": W,
-            "cam_c": _cam_records(self.grid_c_poses_w2c, self.grid_c_Ks),
         }
+        if nv == 1 and getattr(self, "_same_views", False):
+            cache["cam_c"] = cache["cam_f"].view(B, 1, -1)
+        else:
+            cache["cam_c"] = _cam_records(self.grid_c_poses_w2c, self.grid_c_Ks)
         self._grid_cache, self._grid_key = cache, key
         return cache
 
