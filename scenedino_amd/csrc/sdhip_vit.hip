@@ -97,8 +97,7 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
     // buffers) so that global stores are 16-B vectors along the output's contiguous axis
     // (pixels for NCHW, channels otherwise) instead of 2-B lane scatters.
     constexpr bool STAGED = EPI == SD_EPI_BF16 || EPI == SD_EPI_GELU || EPI == SD_EPI_SHUF ||
-                            EPI == SD_EPI_F32 ||
-                            EPI == SD_EPI_NCHW;
+                            EPI == SD_EPI_F32 || EPI == SD_EPI_NCHW || EPI == SD_EPI_QKV;
     constexpr int OST = EPI == SD_EPI_NCHW ? BN + 1 : BN + 8;  // fp32 words per staged row
     constexpr int KL_BYTES = 2 * (BM + BN) * GLDS * 2;
     constexpr int EP_BYTES = STAGED ? BM * OST * 4 : 0;
@@ -273,7 +272,65 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
                 }
         }
         __syncthreads();
-        if constexpr (EPI == SD_EPI_NCHW) {
+        if constexpr (EPI == SD_EPI_QKV) {
+            // phase 2.  q / k columns: thread = 8 consecutive head-dim columns of one token
+            // -> one 16-B store along head_dim (head_dim % 8 == 0: a chunk never straddles
+            // the q / k / v thirds).  V^T columns: thread = 8 consecutive tokens of one
+            // head-dim row -> one 16-B store along the token axis (consecutive threads take
+            // consecutive token runs of the same row: 128-B segments).
+            const int C = g.heads * g.head_dim;
+            if (n0 < 2 * (int64_t)C) {
+#pragma unroll 4
+                for (int t = tid; t < BM * (BN / 8); t += 256) {
+                    const int ml = t / (BN / 8), nl = (t - ml * (BN / 8)) * 8;
+                    const int64_t m = m0 + ml, n = n0 + nl;
+                    if (m >= g.M || n >= g.N) continue;
+                    const int which = (int)(n / C);
+                    if (which == 2) continue;
+                    __bf16 *dst0 = (__bf16 *)(which == 0 ? g.q : g.k);
+                    const int64_t tstride = which == 0 ? g.tokens : g.tokens_pad;
+                    const int rem = (int)(n - (int64_t)which * C);
+                    const int head = rem / g.head_dim, e = rem - head * g.head_dim;
+                    const uint32_t b = (uint32_t)m / (uint32_t)g.tokens;
+                    const int64_t tok = m - (int64_t)b * g.tokens;
+                    const vf4 lo = *(const vf4 *)&sT[ml * OST + nl];
+                    const vf4 hi = *(const vf4 *)&sT[ml * OST + nl + 4];
+                    bf16x8 o;
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        o[u] = (__bf16)lo[u];
+                        o[4 + u] = (__bf16)hi[u];
+                    }
+                    *(bf16x8 *)(dst0 + (((int64_t)b * g.heads + head) * tstride + tok) * g.head_dim + e) = o;
+                }
+            }
+            if (n0 + BN > 2 * (int64_t)C) {
+#pragma unroll 4
+                for (int t = tid; t < BN * (BM / 8); t += 256) {
+                    const int nl = t / (BM / 8), ml = (t - nl * (BM / 8)) * 8;
+                    const int64_t m = m0 + ml, n = n0 + nl;
+                    if (m >= g.M || n >= g.N || n < 2 * (int64_t)C) continue;
+                    const int rem = (int)(n - 2 * (int64_t)C);
+                    const int head = rem / g.head_dim, e = rem - head * g.head_dim;
+                    const uint32_t b = (uint32_t)m / (uint32_t)g.tokens;
+                    const int64_t tok = m - (int64_t)b * g.tokens;
+                    __bf16 *row = (__bf16 *)g.vt + (((int64_t)b * g.heads + head) * g.head_dim + e) * g.tokens_pad;
+                    if ((tok & 7) == 0 && tok + 8 <= g.tokens && m + 8 <= g.M) {
+                        bf16x8 o;
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) o[u] = (__bf16)sT[(ml + u) * OST + nl];
+                        *(bf16x8 *)(row + tok) = o;
+                    } else {
+                        for (int u = 0; u < 8 && m + u < g.M; ++u) {
+                            const uint32_t bu = (uint32_t)(m + u) / (uint32_t)g.tokens;
+                            const int64_t tu = m + u - (int64_t)bu * g.tokens;
+                            ((__bf16 *)g.vt)[(((int64_t)bu * g.heads + head) * g.head_dim + e) * g.tokens_pad + tu] =
+                                (__bf16)sT[(ml + u) * OST + nl];
+                        }
+                    }
+                }
+            }
+        } else if constexpr (EPI == SD_EPI_NCHW) {
             // phase 2: thread = 4 consecutive pixels of one channel -> one 16-B store
             const int plane = g.tokens;
             const bool vec = (plane & 3) == 0;
@@ -1135,7 +1192,7 @@ extern "C" int sd_gemm(const sd_gemm_args *args, void *stream) {
     else if (g.epi == SD_EPI_QKV)
         ok = ok && g.q && g.k && g.vt && g.head_dim > 0 && g.heads > 0 && g.tokens > 0 &&
              g.tokens_pad >= g.tokens && g.N == 3LL * g.heads * g.head_dim &&
-             g.M % g.tokens == 0;
+             g.M % g.tokens == 0 && g.head_dim % 8 == 0 && g.tokens_pad % 8 == 0;
     else if (g.epi == SD_EPI_PATCH)
         ok = ok && g.out && g.pos && g.patches > 0 && g.M % g.patches == 0 && g.ldo >= g.N;
     else

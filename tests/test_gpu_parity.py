@@ -48,6 +48,16 @@ FP32_ATOL = {"depth": 1e-6, "weights": 1e-6, "alphas": 1e-6, "rgb": 1e-5, "rgb_s
 # the full 256x192x640-grid render from the offset pose (64 samples through the scan)
 FP32_ATOL_FULL = {"depth": 1e-6, "weights": 1e-5, "alphas": 1e-4, "rgb": 1e-5, "dino": 5e-5}
 LOWP_DEPTH_MAX = {"bf16": 5e-2, "fp16": 1e-2}
+# SURVEY §8(c) states 1e-2 m for depth.  bf16 (the default, BASELINE configs[1]) meets it for
+# all but a small fraction of rays; the measured maxima per fixture (MI355X,
+# profiles/r2_parity_report.txt, "proj" = tile kernel / "grid" = sd_render_fused) are
+#   render_k32_cap0     bf16 proj 2.53e-2 m, grid 1.71e-2 m;  fp16 proj 3.32e-3 m
+#   render_k64_cap1     bf16 proj 4.50e-2 m, grid 2.05e-2 m;  fp16 proj 4.14e-3 m
+#   render_full_offset  bf16 proj 4.5e-2 m (offset pose, 122 880 rays)
+# so the bf16 bound is 5e-2 m for the maximum, and at most LOWP_DEPTH_FRAC_OVER of the rays
+# may exceed the contract's 1e-2 m (fp16 meets 1e-2 m everywhere).
+LOWP_DEPTH_CONTRACT = 1e-2
+LOWP_DEPTH_FRAC_OVER = {"bf16": 5e-2, "fp16": 0.0}
 
 
 def check_lowp(c, ref, precision, rgb=True):
@@ -57,6 +67,9 @@ def check_lowp(c, ref, precision, rgb=True):
     assert float(dw.max()) <= 2e-3, f"{precision} weights max |d| {float(dw.max()):.3g}"
     dd = (torch.as_tensor(c["depth"]).double().cpu() - torch.as_tensor(np.asarray(ref["depth"])).double().reshape(c["depth"].shape)).abs()
     assert float(dd.max()) <= LOWP_DEPTH_MAX[precision], f"{precision} depth max |d| {float(dd.max()):.3g}"
+    over = float((dd > LOWP_DEPTH_CONTRACT).double().mean())
+    assert over <= LOWP_DEPTH_FRAC_OVER[precision], \
+        f"{precision}: {over:.3%} of the rays exceed the contract's {LOWP_DEPTH_CONTRACT} m depth"
     assert rel_l2(c["depth"], ref["depth"]) <= 2e-3
     assert rel_l2(c["dino_features"], ref["dino_features"]) <= 1e-2
     if rgb:
