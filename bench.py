@@ -415,11 +415,14 @@ def main_c5(args, world, rank, local_rank, dist, device, host_stage=False):
         # HBM bytes per k_seg_head launch (1-GPU launch shape) from the committed PMC
         # summary (tools/c5_traffic.sh: FETCH_SIZE x 2 + WRITE_SIZE, separate passes)
         seg_traffic, seg_tsrc = None, None
-        tf = os.path.join(ROOT, "profiles", "r2_c5_traffic.json")
-        if not dist and os.path.exists(tf):
+        for tn in ("r3_c5_traffic.json", "r2_c5_traffic.json"):
+            tf = os.path.join(ROOT, "profiles", tn)
+            if dist or not os.path.exists(tf):
+                continue
             try:
                 seg_traffic = json.load(open(tf))["kernels"]["k_seg_head"]["hbm_bytes"]
-                seg_tsrc = "profiles/r2_c5_traffic.json (rocprofv3 PMC, per launch)"
+                seg_tsrc = f"profiles/{tn} (rocprofv3 PMC, per launch)"
+                break
             except (KeyError, TypeError, ValueError):
                 seg_traffic = None
         # the roofline is priced on the folded algorithm the kernel runs: its
