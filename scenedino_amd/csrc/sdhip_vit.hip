@@ -43,6 +43,9 @@ __device__ __forceinline__ f32x16 vt_zero16() {
 // ---------------------------------------------------------------------------
 // GEMM
 // ---------------------------------------------------------------------------
+#ifndef VT_NS_SMALL
+#define VT_NS_SMALL 2  // staging-ring depth of the 64 x 64 and 32 x 32 split-K tiles (4, 6: slower)
+#endif
 #define GK 32       // K granularity of sd_gemm (the K loop runs in steps of BK = 64 or 32)
 
 __device__ __forceinline__ float vt_gelu(float x) {
@@ -113,10 +116,13 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
     const __bf16 *Wt = (const __bf16 *)g.w;
     const int nk = (int)(g.K / BK);
 
-    // Two register staging sets: the tile of step k + 2 is loaded while step k computes
-    // and step k + 1's tile (loaded one step earlier) goes to LDS after it -- global
-    // latency gets two steps of MFMA work to hide under, at one LDS double buffer.
-    bf16x8 ra0[CA], rb0[CB], ra1[CA], rb1[CB];
+    // NS register staging sets (a ring): step k's compute runs while the tiles of steps
+    // k + 1 .. k + NS - 1 are in flight; step k + 1's tile goes to LDS after step k's
+    // MFMAs and its set is re-filled with step k + 1 + NS -- global latency gets NS - 1
+    // steps of MFMA work to hide under, at one LDS double buffer.  The small tiles (32 x 32
+    // split-K, 64 x 64) have little MFMA work per step and the VGPRs for a deep ring.
+    constexpr int NS = BM >= 128 ? 2 : VT_NS_SMALL;
+    bf16x8 ra[NS][CA], rb[NS][CB];
     // Rows past M (N) are clamped to the last row instead of predicated: they only feed
     // output rows (columns) that are never stored, and unpredicated loads keep the
     // compiler's vmcnt accounting exact (a masked load forces vmcnt(0) waits).
@@ -198,12 +204,8 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = vt_zero16();
 
-    auto step = [&](int kt, bf16x8 (&ca)[CA], bf16x8 (&cb)[CB], bf16x8 (&na)[CA],
-                    bf16x8 (&nb)[CB]) {
+    auto compute = [&](int kt) {
         const int buf = kt & 1;
-        // unconditional (the last steps re-load stage nk - 1): a load issued on one path
-        // only makes the compiler's vmcnt model wait for the newest loads as well
-        gload(min(kt + 2, nk - 1), na, nb);
 #pragma unroll
         for (int s0 = 0; s0 < (SK ? BK / 64 : BK / 16); ++s0) {
             const int s = SK ? 4 * s0 + wave : s0;
@@ -219,17 +221,28 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
 #pragma unroll
                 for (int j = 0; j < TN; ++j) acc[i][j] = VT_MFMA(af[i], bfr[j], acc[i][j]);
         }
-        if (kt + 1 < nk) lstore(buf ^ 1, ca, cb);
-        __syncthreads();
     };
 
-    gload(0, ra0, rb0);
-    lstore(0, ra0, rb0);
-    gload(min(1, nk - 1), ra0, rb0);
+    // prologue: set i <- step i (i < NS), step 0 to LDS, set 0 <- step NS.  Loads past the
+    // last step re-load step nk - 1 (unconditional: a load issued on one path only makes the
+    // compiler's vmcnt model wait for the newest loads as well)
+#pragma unroll
+    for (int i = 0; i < NS; ++i) gload(min(i, nk - 1), ra[i], rb[i]);
+    lstore(0, ra[0], rb[0]);
+    gload(min(NS, nk - 1), ra[0], rb[0]);
     __syncthreads();
-    for (int kt = 0; kt < nk; kt += 2) {
-        step(kt, ra0, rb0, ra1, rb1);          // set 0 holds step kt + 1, set 1 gets kt + 2
-        if (kt + 1 < nk) step(kt + 1, ra1, rb1, ra0, rb0);
+    for (int kt = 0; kt < nk; kt += NS) {
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            const int k = kt + i;
+            if (k < nk) {  // workgroup-uniform
+                compute(k);
+                const int nx = (i + 1) % NS;  // the set holding step k + 1 (constant once unrolled)
+                if (k + 1 < nk) lstore((k + 1) & 1, ra[nx], rb[nx]);
+                gload(min(k + 1 + NS, nk - 1), ra[nx], rb[nx]);
+                __syncthreads();
+            }
+        }
     }
 
     if constexpr (SK) {
@@ -1144,8 +1157,31 @@ static void vt_launch_gemm(const sd_gemm_args &g, hipStream_t s) {
 #define SD_CONV_SK_MID 256  // conv: split-K tiles below this many 64x64 tiles (1024: no gain)
 #endif
 
+// SD_GEMM_TILE (diagnostic A/B runs, read once): "128", "64" or "sk" forces that tiling
+static int vt_forced_tile() {
+    static int f = -2;
+    if (f == -2) {
+        const char *e = getenv("SD_GEMM_TILE");
+        f = !e ? -1 : !strcmp(e, "128") ? 128 : !strcmp(e, "64") ? 64 : !strcmp(e, "sk") ? 32 : -1;
+    }
+    return f;
+}
+
 template <bool CONV>
 static void vt_pick_gemm(const sd_gemm_args &g, hipStream_t s) {
+    const int ft = vt_forced_tile();
+    if (ft == 32 && g.K % 128 == 0 && g.K >= 256 && (!CONV || g.Cin % 128 == 0)) {
+        vt_launch_gemm<32, 32, 128, CONV>(g, s);
+        return;
+    }
+    if (ft == 128 || ft == 64) {
+        if (g.K % 64 == 0) {
+            if (ft == 128) vt_launch_gemm<128, 128, 64, CONV>(g, s); else vt_launch_gemm<64, 64, 64, CONV>(g, s);
+        } else {
+            if (ft == 128) vt_launch_gemm<128, 128, 32, CONV>(g, s); else vt_launch_gemm<64, 64, 32, CONV>(g, s);
+        }
+        return;
+    }
     // K steps of 64 whenever K allows (half the barriers, twice the work under each
     // prefetch); 128x128 tiles once they fill the chip, else 64x64
     const int64_t big = ((g.M + 127) / 128) * ((g.N + 127) / 128);
@@ -1158,13 +1194,18 @@ static void vt_pick_gemm(const sd_gemm_args &g, hipStream_t s) {
         vt_launch_gemm<32, 32, 128, CONV>(g, s);  // split-K over the 4 waves
         return;
     }
+    // 128x128 tiles need about two per CU, or one per CU with a long K loop to amortise
+    // their prologue / epilogue; below that the 64x64 tiling wins (sd_gemm on the ViT-B/8
+    // block shapes at 1921 tokens, tools/gemm_bench.py: qkv 24.6 -> 18.6 us, fc1 22.4 ->
+    // 20.3 us; the DPT's 3x3 convolutions at K = 2304 keep 128x128)
+    const bool use128 = big >= 512 || (big >= 256 && g.K >= 2048);
     if (g.K % 64 == 0) {
-        if (big >= 256)
+        if (use128)
             vt_launch_gemm<128, 128, 64, CONV>(g, s);
         else
             vt_launch_gemm<64, 64, 64, CONV>(g, s);
     } else {
-        if (big >= 256)
+        if (use128)
             vt_launch_gemm<128, 128, 32, CONV>(g, s);
         else
             vt_launch_gemm<64, 64, 32, CONV>(g, s);
