@@ -72,6 +72,9 @@
 #ifndef ST_ABL_NOHC
 #define ST_ABL_NOHC 0
 #endif
+#ifndef ST_SIG_VALU
+#define ST_SIG_VALU 0       // sigma by v_dot2 on the relu tiles + permlane swaps (1: weights in VGPRs, 2: from LDS) instead of 4 MFMAs
+#endif
 #ifndef ST_ABL_NOSIG
 #define ST_ABL_NOSIG 0
 #endif
@@ -600,6 +603,13 @@ k_render_tile(const st_args sa) {
     const bool bc0 = bsel && (j >> 3) == 0, bc1 = bsel && (j >> 3) == 1;
     const bool br1 = (j & 1) != 0;
     const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+#if ST_SIG_VALU == 1
+    // sigma weights of this lane's relu elements (every row of the sigma A fragment holds
+    // W_out[0] at hid(s, g, e), mlp_pack.py), kept in registers
+    uint4 wsig_r[4];
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) wsig_r[s2] = *(const uint4 *)(lds + ST_L_SIG + (s2 * SD_WAVE + lane) * 16);
+#endif
     // identity B operand of the 16x16x16 transposition (lane (n, g): rows 4 g + e)
     const Frag4 Iden = __builtin_bit_cast(
         Frag4, uint2{sd_pack2<E>(4 * g == j ? 1.f : 0.f, 4 * g + 1 == j ? 1.f : 0.f),
@@ -814,10 +824,35 @@ k_render_tile(const st_args sa) {
             const float sigma = __builtin_bit_cast(float, __builtin_bit_cast(uint4, st.X[0]).x & 0x3fffffffu) + m.b_sigma;
 #else
             ST_T2(15);
+#if ST_SIG_VALU
+            // sigma = sum_h W_out[0][h] relu(h): this lane's 32 hidden by v_dot2 (4 chains),
+            // then the sum over the 4 lane groups g (rows) by two permlane swaps -- every
+            // lane of column j ends with sample j's sigma, as from the MFMA
+            float sp[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s2 = 0; s2 < 4; ++s2) {
+                const uint4 x4 = __builtin_bit_cast(uint4, st.X[s2]);
+#if ST_SIG_VALU == 1
+                const uint4 w4 = wsig_r[s2];
+#else
+                const uint4 w4 = *(const uint4 *)(lds + ST_L_SIG + ((s2 + lo) * SD_WAVE + lane) * 16);
+#endif
+                sp[0] = Tr::dot2(x4.x, w4.x, sp[0]);
+                sp[1] = Tr::dot2(x4.y, w4.y, sp[1]);
+                sp[2] = Tr::dot2(x4.z, w4.z, sp[2]);
+                sp[3] = Tr::dot2(x4.w, w4.w, sp[3]);
+            }
+            float sa = (sp[0] + sp[1]) + (sp[2] + sp[3]), sb = sa;
+            asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(sa), "+v"(sb));
+            float sc = sa + sb, sd = sc;
+            asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(sc), "+v"(sd));
+            const float sv = (sc + sd) + m.b_sigma;
+#else
             f32x4 sg = zero4;
 #pragma unroll
             for (int s2 = 0; s2 < 4; ++s2) sg = Tr::mma(lw[ST_L_SIG / 16 + s2 * SD_WAVE + lane], st.X[s2], sg);
             const float sv = sg[0] + m.b_sigma;
+#endif
             const float sigma = sd_softplus_fast(sv);
 #endif
             // alpha compositing (nerf.py:376-389)
