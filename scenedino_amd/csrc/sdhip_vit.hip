@@ -837,7 +837,23 @@ __global__ void __launch_bounds__(256) k_attn_dir(const __bf16 *__restrict__ Q,
 // ---------------------------------------------------------------------------
 // LayerNorm (one wave per row), patchify, tokens -> grid
 // ---------------------------------------------------------------------------
-template <int PER, bool F32OUT>
+// sum over the 64 lanes, result in every lane: DPP row reductions (row_ror 8, 4, 2, 1) then
+// the four row sums by readlane (no LDS round trip, unlike a __shfl_xor butterfly)
+__device__ __forceinline__ float vt_wave_sum(float x) {
+    x += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x128, 0xf, 0xf, true));
+    x += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x124, 0xf, 0xf, true));
+    x += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x122, 0xf, 0xf, true));
+    x += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x121, 0xf, 0xf, true));
+    const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 0));
+    const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 16));
+    const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 32));
+    const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 48));
+    return (r0 + r1) + (r2 + r3);
+}
+
+// One wave per row; lane = 4 consecutive channels per 256-channel chunk (16-B loads, 8-B
+// bf16 / 16-B f32 stores); PER4 chunks of 256 channels (C <= 256 PER4, C % 4 == 0).
+template <int PER4, bool F32OUT>
 __global__ void __launch_bounds__(256) k_layernorm(const float *__restrict__ x, int64_t rows,
                                                    int C, const float *__restrict__ w,
                                                    const float *__restrict__ b, float eps,
@@ -846,36 +862,44 @@ __global__ void __launch_bounds__(256) k_layernorm(const float *__restrict__ x, 
     const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= rows) return;
     const float *xr = x + row * C;
-    float v[PER];
+    vf4 v[PER4];
     float s = 0.f;
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-        const int c = lane + 64 * i;
-        v[i] = c < C ? xr[c] : 0.f;
-        s += v[i];
+    for (int i = 0; i < PER4; ++i) {
+        const int c = 4 * lane + 256 * i;
+        v[i] = c < C ? *(const vf4 *)(xr + c) : vf4{0.f, 0.f, 0.f, 0.f};
+        s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
     }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off);
-    const float mean = s / (float)C;
+    const float mean = vt_wave_sum(s) / (float)C;
     float q = 0.f;
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-        const int c = lane + 64 * i;
-        const float d = c < C ? v[i] - mean : 0.f;
-        q = fmaf(d, d, q);
-    }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) q += __shfl_xor(q, off);
-    const float rstd = 1.f / sqrtf(q / (float)C + eps);
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-        const int c = lane + 64 * i;
+    for (int i = 0; i < PER4; ++i) {
+        const int c = 4 * lane + 256 * i;
         if (c < C) {
-            const float y = (v[i] - mean) * rstd * w[c] + b[c];
-            if (F32OUT)
-                ((float *)out)[row * C + c] = y;
-            else
-                ((__bf16 *)out)[row * C + c] = (__bf16)y;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const float d = v[i][u] - mean;
+                q = fmaf(d, d, q);
+            }
+        }
+    }
+    const float rstd = 1.f / sqrtf(vt_wave_sum(q) / (float)C + eps);
+#pragma unroll
+    for (int i = 0; i < PER4; ++i) {
+        const int c = 4 * lane + 256 * i;
+        if (c < C) {
+            const vf4 wv = *(const vf4 *)(w + c), bv = *(const vf4 *)(b + c);
+            vf4 y;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) y[u] = (v[i][u] - mean) * rstd * wv[u] + bv[u];
+            if (F32OUT) {
+                *(vf4 *)((float *)out + row * C + c) = y;
+            } else {
+                bf16x4 o;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) o[u] = (__bf16)y[u];
+                *(bf16x4 *)((__bf16 *)out + row * C + c) = o;
+            }
         }
     }
 }
@@ -1334,8 +1358,9 @@ extern "C" int sd_attention(const void *q, const void *k, const void *vt, int32_
 extern "C" int sd_layernorm(const float *x, int64_t rows, int32_t C, const float *w,
                             const float *b, float eps, void *out, int32_t out_f32,
                             void *stream) {
-    if (!x || !w || !b || !out || rows < 0 || C <= 0 || C > 1024) {
-        sd_set_error("sd_layernorm: invalid argument (C <= 1024)");
+    if (!x || !w || !b || !out || rows < 0 || C <= 0 || C > 1024 || C % 4 != 0 ||
+        ((uintptr_t)x | (uintptr_t)w | (uintptr_t)b | (uintptr_t)out) & 15) {
+        sd_set_error("sd_layernorm: invalid argument (C <= 1024, C % 4 == 0, 16-B aligned)");
         return -1;
     }
     if (rows == 0) return 0;
@@ -1350,12 +1375,12 @@ extern "C" int sd_layernorm(const float *x, int64_t rows, int32_t C, const float
             hipLaunchKernelGGL((k_layernorm<PER, false>), grid, dim3(256), 0, s, x, rows, C,   \
                                w, b, eps, out);                                             \
     } while (0)
-    if (C <= 384)
-        SD_LN(6);
+    if (C <= 512)
+        SD_LN(2);
     else if (C <= 768)
-        SD_LN(12);
+        SD_LN(3);
     else
-        SD_LN(16);
+        SD_LN(4);
 #undef SD_LN
     if (hipGetLastError() != hipSuccess) {
         sd_set_error("sd_layernorm: launch failed");

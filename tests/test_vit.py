@@ -143,7 +143,7 @@ def test_qkv_scatter_and_attention(gpu, B, H, T, mode, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("C", [384, 768])
+@pytest.mark.parametrize("C", [384, 768, 1024, 68])
 def test_layernorm(gpu, C):
     from scenedino_amd import _lib
     g = torch.Generator().manual_seed(C)
