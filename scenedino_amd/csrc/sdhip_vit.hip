@@ -935,29 +935,52 @@ __global__ void __launch_bounds__(256) k_patchify(const float *__restrict__ img,
     }
 }
 
+// A workgroup transposes a block of 64 consecutive output tokens x 64 channels (blockIdx.y):
+// rows read coalesced into a padded LDS tile, written along the pixel axis (a wave stores 64
+// consecutive pixels of one channel plane: 256 B).  With L2 normalisation each block first
+// computes its 64 tokens' norms (a wave per token, full-row reads from L2).
 __global__ void __launch_bounds__(256) k_tokens_to_grid(const float *__restrict__ x, int B, int T,
                                                         int C, int n_prefix, int gh, int gw,
                                                         int l2, float *__restrict__ out) {
-    // one wave per output token: read C channels (coalesced), optional L2 norm, write planes
-    const int lane = threadIdx.x & 63;
-    const int64_t tok = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int64_t n_tok = (int64_t)B * gh * gw;
-    if (tok >= n_tok) return;
-    const int b = (int)(tok / (gh * gw)), pi = (int)(tok - (int64_t)b * gh * gw);
-    const float *xr = x + ((int64_t)b * T + n_prefix + pi) * C;
-    float scale = 1.f;
+    __shared__ float tile[64][65];
+    __shared__ float sc[64];
+    __shared__ const float *rows[64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int ghw = gh * gw;
+    const int n_tok = B * ghw, tok0 = blockIdx.x * 64;  // < 2^31 (checked at the ABI)
+    const int c0 = blockIdx.y * 64;
+    // the block's 64 input rows, one 32-bit division per token
+    const int tok = tok0 + lane;
+    const int bb = (unsigned)min(tok, n_tok - 1) / (unsigned)ghw;
+    const int pi = min(tok, n_tok - 1) - bb * ghw;
+    if (wave == 0) rows[lane] = x + ((int64_t)bb * T + n_prefix + pi) * C;
+    __syncthreads();
     if (l2) {
-        float s = 0.f;
-        for (int c = lane; c < C; c += 64) s = fmaf(xr[c], xr[c], s);
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off);
-        // F.normalize(p=2, eps=1e-12) applied twice (vit.py:188, dinov2_module.py:282):
-        // the second pass divides a unit vector by its own norm
-        const float n1 = fmaxf(sqrtf(s), 1e-12f);
-        scale = 1.f / n1;
+        for (int i = wave; i < 64; i += 4) {
+            float scale = 1.f;
+            if (tok0 + i < n_tok) {
+                const float *xr = rows[i];
+                float s2 = 0.f;
+                for (int c = lane; c < C; c += 64) s2 = fmaf(xr[c], xr[c], s2);
+                // F.normalize(p=2, eps=1e-12) applied twice (vit.py:188,
+                // dinov2_module.py:282): the second pass divides a unit vector by its norm
+                scale = 1.f / fmaxf(sqrtf(vt_wave_sum(s2)), 1e-12f);
+            }
+            if (lane == 0) sc[i] = scale;
+        }
+        __syncthreads();
     }
-    for (int c = lane; c < C; c += 64)
-        out[(((int64_t)b * C + c) * gh) * gw + pi] = xr[c] * scale;
+    for (int e = tid; e < 64 * 64; e += 256) {
+        const int i = e >> 6, c = c0 + (e & 63);
+        float v = (tok0 + i < n_tok && c < C) ? rows[i][c] : 0.f;
+        if (l2) v *= sc[i];
+        tile[i][e & 63] = v;
+    }
+    __syncthreads();
+    if (tok < n_tok) {
+        float *o = out + ((int64_t)bb * C + c0) * ghw + pi;
+        for (int cc = wave; cc < 64 && c0 + cc < C; cc += 4) o[(int64_t)cc * ghw] = tile[lane][cc];
+    }
 }
 
 // tokens (B, T, C) f32 -> NHWC bf16 (B, gh*gw, C) (prefix tokens dropped, optional L2
@@ -1420,12 +1443,12 @@ extern "C" int sd_tokens_to_grid(const float *x, int32_t B, int32_t T, int32_t C
                                  int32_t n_prefix, int32_t gh, int32_t gw, int32_t l2norm,
                                  float *out, void *stream) {
     if (!x || !out || B <= 0 || C <= 0 || n_prefix < 0 || gh <= 0 || gw <= 0 ||
-        (int64_t)n_prefix + (int64_t)gh * gw > T) {
+        (int64_t)n_prefix + (int64_t)gh * gw > T || (int64_t)B * gh * gw >= ((int64_t)1 << 31)) {
         sd_set_error("sd_tokens_to_grid: invalid argument");
         return -1;
     }
     const int64_t n = (int64_t)B * gh * gw;
-    hipLaunchKernelGGL(k_tokens_to_grid, dim3((unsigned)((n + 3) / 4)), dim3(256), 0,
+    hipLaunchKernelGGL(k_tokens_to_grid, dim3((unsigned)((n + 63) / 64), (unsigned)((C + 63) / 64)), dim3(256), 0,
                        (hipStream_t)stream, x, B, T, C, n_prefix, gh, gw, l2norm, out);
     if (hipGetLastError() != hipSuccess) {
         sd_set_error("sd_tokens_to_grid: launch failed");

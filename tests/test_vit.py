@@ -265,3 +265,21 @@ def test_graph_replay_matches_eager(gpu):
     for e, gr in zip(eager, graph):
         for a, b in zip(e, gr):
             assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,gh,gw,C,l2", [(1, 24, 80, 768, False), (2, 13, 45, 96, True),
+                                          (1, 3, 5, 70, True)])
+def test_tokens_to_grid(gpu, B, gh, gw, C, l2):
+    """sd_tokens_to_grid (class token dropped, (B, T, C) -> (B, C, gh, gw), optional double
+    F.normalize as vit.py:188 + dinov2_module.py:282) against the torch view."""
+    from scenedino_amd import _lib
+    g = torch.Generator().manual_seed(gh * gw + C)
+    T = 1 + gh * gw
+    x = (3 * torch.randn(B * T, C, generator=g)).to(gpu)
+    out = _lib.tokens_to_grid(x, B, T, C, 1, gh, gw, l2)
+    ref = x.view(B, T, C)[:, 1:].reshape(B, gh, gw, C).permute(0, 3, 1, 2)
+    if l2:
+        ref = F.normalize(F.normalize(ref, dim=1), dim=1)
+    assert tuple(out.shape) == (B, C, gh, gw)
+    assert (out - ref).abs().max().item() <= 1e-6 * (1 if l2 else ref.abs().max().item())
