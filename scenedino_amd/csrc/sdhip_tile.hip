@@ -72,6 +72,9 @@
 #ifndef ST_ABL_NOHC
 #define ST_ABL_NOHC 0
 #endif
+#ifndef ST_HOIST_W
+#define ST_HOIST_W 1        // the code-column weight fragments held in VGPRs (48 of them; 230 in all)
+#endif
 #ifndef ST_SIG_VALU
 #define ST_SIG_VALU 0       // sigma by v_dot2 on the relu tiles + permlane swaps (1: weights in VGPRs, 2: from LDS) instead of 4 MFMAs
 #endif
@@ -603,6 +606,16 @@ k_render_tile(const st_args sa) {
     const bool bc0 = bsel && (j >> 3) == 0, bc1 = bsel && (j >> 3) == 1;
     const bool br1 = (j & 1) != 0;
     const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+    // ST_HOIST_W: this lane's code-column weight fragments held in VGPRs for the whole kernel
+    Frag wpe[8];
+    Frag4 wpe1[8];
+    if (ST_HOIST_W) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            wpe[t] = lf[ST_L_PE / 16 + t * SD_WAVE + lane];
+            wpe1[t] = ((const Frag4 *)(lds + ST_L_PE1))[t * SD_WAVE + lane];
+        }
+    }
 #if ST_SIG_VALU == 1
     // sigma weights of this lane's relu elements (every row of the sigma A fragment holds
     // W_out[0] at hid(s, g, e), mlp_pack.py), kept in registers
@@ -706,7 +719,7 @@ k_render_tile(const st_args sa) {
             // overlaps the code evaluation and its MFMAs
             ST_T2(14);
             // positional-code columns
-            const int lo = sd_opaque0();
+            const int lo = ST_HOIST_W ? 0 : sd_opaque0();
             const Frag *lw = lf + lo;
             {
                 Frag f0;
@@ -787,7 +800,7 @@ k_render_tile(const st_args sa) {
 #endif
             ST_T2(14);
             // positional-code columns
-            const int lo = sd_opaque0();
+            const int lo = ST_HOIST_W ? 0 : sd_opaque0();
             const Frag *lw = lf + lo;
             {
                 Frag f0;
@@ -805,11 +818,11 @@ k_render_tile(const st_args sa) {
 #pragma unroll
                 for (int t = 0; t < 8; ++t)
                     if (!ST_ABL_NOCODE || t == 0)
-                        acc[t] = Tr::mma(lw[ST_L_PE / 16 + t * SD_WAVE + lane], f0, acc[t]);
+                        acc[t] = Tr::mma(ST_HOIST_W ? wpe[t] : lw[ST_L_PE / 16 + t * SD_WAVE + lane], f0, acc[t]);
 #pragma unroll
                 for (int t = 0; t < 8; ++t)
                     if (!ST_ABL_NOCODE || t == 0)
-                        acc[t] = Tr::mma16(lw1[t * SD_WAVE + lane], f1, acc[t]);
+                        acc[t] = Tr::mma16(ST_HOIST_W ? wpe1[t] : lw1[t * SD_WAVE + lane], f1, acc[t]);
             }
 #endif
 #pragma unroll

@@ -1205,6 +1205,7 @@ static void vt_launch_gemm(const sd_gemm_args &g, hipStream_t s) {
 #endif
 
 // SD_GEMM_TILE (diagnostic A/B runs, read once): "128", "64" or "sk" forces that tiling
+// (64x128 tiles and 64x64 tiles with BK = 128 were measured slower on every encoder shape)
 static int vt_forced_tile() {
     static int f = -2;
     if (f == -2) {
