@@ -75,6 +75,9 @@
 #ifndef ST_HOIST_W
 #define ST_HOIST_W 1        // the code-column weight fragments held in VGPRs (48 of them; 230 in all)
 #endif
+#ifndef ST_HOIST_SIG
+#define ST_HOIST_SIG 1      // the sigma A fragments held in VGPRs as well (16 more: 244 in all)
+#endif
 #ifndef ST_SIG_VALU
 #define ST_SIG_VALU 0       // sigma by v_dot2 on the relu tiles + permlane swaps (1: weights in VGPRs, 2: from LDS) instead of 4 MFMAs
 #endif
@@ -616,7 +619,7 @@ k_render_tile(const st_args sa) {
             wpe1[t] = ((const Frag4 *)(lds + ST_L_PE1))[t * SD_WAVE + lane];
         }
     }
-#if ST_SIG_VALU == 1
+#if ST_SIG_VALU == 1 || ST_HOIST_SIG
     // sigma weights of this lane's relu elements (every row of the sigma A fragment holds
     // W_out[0] at hid(s, g, e), mlp_pack.py), kept in registers
     uint4 wsig_r[4];
@@ -863,7 +866,9 @@ k_render_tile(const st_args sa) {
 #else
             f32x4 sg = zero4;
 #pragma unroll
-            for (int s2 = 0; s2 < 4; ++s2) sg = Tr::mma(lw[ST_L_SIG / 16 + s2 * SD_WAVE + lane], st.X[s2], sg);
+            for (int s2 = 0; s2 < 4; ++s2)
+                sg = Tr::mma(ST_HOIST_SIG ? __builtin_bit_cast(Frag, wsig_r[s2]) : lw[ST_L_SIG / 16 + s2 * SD_WAVE + lane],
+                             st.X[s2], sg);
             const float sv = sg[0] + m.b_sigma;
 #endif
             const float sigma = sd_softplus_fast(sv);
