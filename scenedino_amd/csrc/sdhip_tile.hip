@@ -158,10 +158,17 @@ struct st_args {
 };
 
 // LDS image (byte offsets)
+// the code / sigma A fragments go through LDS only in the diagnostic builds that read them
+// there per item; the shipped kernel holds them in VGPRs, loaded from global memory once,
+// and gives their 16 KiB to the tile buffers
+#ifndef ST_FRAG_LDS_FORCE
+#define ST_FRAG_LDS_FORCE 0  // 1: keep the fragment copy in LDS (A/B of the larger tile buffers)
+#endif
+#define ST_FRAG_LDS (ST_FRAG_LDS_FORCE || !(ST_HOIST_W && ST_HOIST_SIG) || ST_CODE_FIRST || ST_SIG_VALU == 2)
 #define ST_L_PE 0                              // [8][64] x 16 B code A fragments (16x16x32)
 #define ST_L_PE1 (ST_L_PE + 8 * 64 * 16)      // [8][64] x 8 B code A fragments (16x16x16)
 #define ST_L_SIG (ST_L_PE1 + 8 * 64 * 8)      // [4][64] x 16 B sigma A fragments
-#define ST_L_BOX (ST_L_SIG + 4 * 64 * 16)      // [2][NW waves][2 halves] u32 (min, max) packed
+#define ST_L_BOX (ST_FRAG_LDS ? ST_L_SIG + 4 * 64 * 16 : 0)  // [2][NW waves][2 halves] u32 (min, max) packed
 // then, sized by NW (waves = rays per group):
 __host__ __device__ constexpr int st_l_hs(int nw) { return ST_L_BOX + 2 * nw * 16; }  // [NW rays][128] 16-bit hidden sums
 __host__ __device__ constexpr int st_l_ws(int nw) { return st_l_hs(nw) + nw * 128 * 2; }  // [NW] f32 weight sums
@@ -285,8 +292,10 @@ k_render_tile(const st_args sa) {
     {
         const uint4 *pe = (const uint4 *)m.w_pe, *sg = (const uint4 *)m.w_sig;
         uint4 *d = (uint4 *)lds;
-        for (int i = threadIdx.x; i < 12 * SD_WAVE; i += blockDim.x) d[ST_L_PE / 16 + i] = pe[i];
-        for (int i = threadIdx.x; i < 4 * SD_WAVE; i += blockDim.x) d[ST_L_SIG / 16 + i] = sg[i];
+        if (ST_FRAG_LDS) {
+            for (int i = threadIdx.x; i < 12 * SD_WAVE; i += blockDim.x) d[ST_L_PE / 16 + i] = pe[i];
+            for (int i = threadIdx.x; i < 4 * SD_WAVE; i += blockDim.x) d[ST_L_SIG / 16 + i] = sg[i];
+        }
     }
     const Frag *lf = (const Frag *)lds;
     const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_void *)lds;  // LDS byte address of lds[0]
@@ -615,8 +624,8 @@ k_render_tile(const st_args sa) {
     if (ST_HOIST_W) {
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
-            wpe[t] = lf[ST_L_PE / 16 + t * SD_WAVE + lane];
-            wpe1[t] = ((const Frag4 *)(lds + ST_L_PE1))[t * SD_WAVE + lane];
+            wpe[t] = ((const Frag *)m.w_pe)[t * SD_WAVE + lane];
+            wpe1[t] = ((const Frag4 *)((const uint8_t *)m.w_pe + 8 * SD_WAVE * 16))[t * SD_WAVE + lane];
         }
     }
 #if ST_SIG_VALU == 1 || ST_HOIST_SIG
@@ -624,7 +633,7 @@ k_render_tile(const st_args sa) {
     // W_out[0] at hid(s, g, e), mlp_pack.py), kept in registers
     uint4 wsig_r[4];
 #pragma unroll
-    for (int s2 = 0; s2 < 4; ++s2) wsig_r[s2] = *(const uint4 *)(lds + ST_L_SIG + (s2 * SD_WAVE + lane) * 16);
+    for (int s2 = 0; s2 < 4; ++s2) wsig_r[s2] = ((const uint4 *)m.w_sig)[s2 * SD_WAVE + lane];
 #endif
     // identity B operand of the 16x16x16 transposition (lane (n, g): rows 4 g + e)
     const Frag4 Iden = __builtin_bit_cast(
