@@ -54,8 +54,14 @@
 // lane's pixel read from NCHW (32 consecutive floats per channel across a half) or, NHWC
 // (the native encoder's channels-last grid), as two 16-B loads of the pixel's row.
 // ---------------------------------------------------------------------------
+// waves per SIMD the channels-last k_project's register budget is cut for (1: the compiler's
+// choice, 176 VGPRs = 2 waves per SIMD).  3 (167 VGPRs, no spill) measured the same time
+// (C2 50-53 us either way, tools/proj_ab.sh): more resident waves do not move this kernel
+#ifndef SD_PROJ_WPE
+#define SD_PROJ_WPE 1
+#endif
 template <int P, bool NHWC>
-__global__ void __launch_bounds__(SD_PWG)
+__global__ void __launch_bounds__(SD_PWG) __attribute__((amdgpu_waves_per_eu(NHWC ? SD_PROJ_WPE : 1)))
 k_project(const float *__restrict__ grid, int64_t B, int C, int64_t HW, int W, const sd_mlp m,
           uint32_t *__restrict__ out) {
     typedef T16<P> Tr;
