@@ -663,15 +663,24 @@ __device__ __forceinline__ void at_store(const f32x16 o[2], float inv, __bf16 *d
         }
 }
 
+// KS = key splits per workgroup.  KS = 1: 4 waves = 128 queries over all keys.  KS = 2 (small
+// grids, e.g. ViT-B/8 at batch 1: 12 heads x 15 query tiles = 180 workgroups for 256 CUs):
+// 2 waves = 64 queries per key half, each half staging its own K / V^T blocks, twice the
+// workgroups; the halves' (m, l, O) states merge through LDS at the end.
+template <int KS>
 __global__ void __launch_bounds__(256) k_attn_lds(const __bf16 *__restrict__ Q,
                                                   const __bf16 *__restrict__ K,
                                                   const __bf16 *__restrict__ Vt, int T, int Tp,
                                                   int H, float sl2e, __bf16 *__restrict__ out) {
-    __shared__ __attribute__((aligned(16))) __bf16 s_kv[2][2][64 * AT_ROW];  // [buf][K | V^T]
+    constexpr int QW = 4 / KS;          // query waves per key split
+    constexpr int ST = 64 * QW;         // staging threads per key split
+    constexpr int CH = 512 / ST;        // 16-B chunks per thread per K (or V^T) block
+    __shared__ __attribute__((aligned(16))) __bf16 s_kv[KS][2][2][64 * AT_ROW];  // [split][buf][K | V^T]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, h = lane >> 5;
+    const int ks = wave / QW, qw = wave - ks * QW, stid = tid - ks * ST;
     const int bh = blockIdx.y;
-    const int q = blockIdx.x * 128 + 32 * wave + r;
+    const int q = blockIdx.x * (32 * QW) + 32 * qw + r;
     const __bf16 *Kh = K + (int64_t)bh * Tp * AT_HD;
     const __bf16 *Vh = Vt + (int64_t)bh * AT_HD * Tp;
     bf16x8 qb[4];
@@ -681,49 +690,83 @@ __global__ void __launch_bounds__(256) k_attn_lds(const __bf16 *__restrict__ Q,
     S.o[1] = vt_zero16();
     S.m = -INFINITY;
     S.l = 0.f;
-    // staging: chunk c = tid + 256 i of a 64-row x 128-B tile, row c / 8, 16-B column c % 8
-    bf16x8 gk[2], gv[2];
+    // this split's 64-key blocks [b0, b1)
+    const int nb = Tp >> 6;
+    const int b0 = nb * ks / KS, b1 = nb * (ks + 1) / KS, nmax = (nb + KS - 1) / KS;
+    // staging: chunk c = stid + ST i of a 64-row x 128-B tile, row c / 8, 16-B column c % 8
+    bf16x8 gk[CH], gv[CH];
     auto gload = [&](int kb) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int c = tid + 256 * i, row = c >> 3, col = (c & 7) * 8;
+        for (int i = 0; i < CH; ++i) {
+            const int c = stid + ST * i, row = c >> 3, col = (c & 7) * 8;
             gk[i] = *(const bf16x8 *)(Kh + (int64_t)(kb + row) * AT_HD + col);
             gv[i] = *(const bf16x8 *)(Vh + (int64_t)row * Tp + kb + col);
         }
     };
     auto swrite = [&](int buf) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int c = tid + 256 * i, row = c >> 3, col = (c & 7) * 8;
-            *(bf16x8 *)(s_kv[buf][0] + row * AT_ROW + col) = gk[i];
-            *(bf16x8 *)(s_kv[buf][1] + row * AT_ROW + col) = gv[i];
+        for (int i = 0; i < CH; ++i) {
+            const int c = stid + ST * i, row = c >> 3, col = (c & 7) * 8;
+            *(bf16x8 *)(s_kv[ks][buf][0] + row * AT_ROW + col) = gk[i];
+            *(bf16x8 *)(s_kv[ks][buf][1] + row * AT_ROW + col) = gv[i];
         }
     };
-    gload(0);
-    swrite(0);
+    if (b0 < b1) {
+        gload(64 * b0);
+        swrite(0);
+    }
     __syncthreads();
-    const int nb = Tp >> 6;
     const int pr = at_perm(r);
-    for (int b = 0; b < nb; ++b) {
-        if (b + 1 < nb) gload(64 * (b + 1));
-        const __bf16 *sK = s_kv[b & 1][0], *sV = s_kv[b & 1][1];
-        bf16x8 kf[2][4], vf[2][2][2];
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int s = 0; s < 4; ++s)
-                kf[t][s] = *(const bf16x8 *)(sK + (32 * t + pr) * AT_ROW + 16 * s + 8 * h);
-#pragma unroll
-        for (int ht = 0; ht < 2; ++ht)
+    // both splits run nmax steps (a split with fewer blocks idles through its last one):
+    // the barrier is workgroup-wide
+    for (int i = 0; i < nmax; ++i) {
+        const int b = b0 + i;
+        const bool live = b < b1;
+        if (b + 1 < b1) gload(64 * (b + 1));
+        if (live) {
+            const __bf16 *sK = s_kv[ks][i & 1][0], *sV = s_kv[ks][i & 1][1];
+            bf16x8 kf[2][4], vf[2][2][2];
 #pragma unroll
             for (int t = 0; t < 2; ++t)
 #pragma unroll
-                for (int s = 0; s < 2; ++s)
-                    vf[ht][t][s] =
-                        *(const bf16x8 *)(sV + (32 * ht + r) * AT_ROW + 32 * t + 16 * s + 8 * h);
-        at_block(S, qb, kf, vf, 64 * b, T, h, sl2e);
-        if (b + 1 < nb) swrite((b + 1) & 1);
+                for (int s = 0; s < 4; ++s)
+                    kf[t][s] = *(const bf16x8 *)(sK + (32 * t + pr) * AT_ROW + 16 * s + 8 * h);
+#pragma unroll
+            for (int ht = 0; ht < 2; ++ht)
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+#pragma unroll
+                    for (int s = 0; s < 2; ++s)
+                        vf[ht][t][s] =
+                            *(const bf16x8 *)(sV + (32 * ht + r) * AT_ROW + 32 * t + 16 * s + 8 * h);
+            at_block(S, qb, kf, vf, 64 * b, T, h, sl2e);
+        }
+        if (b + 1 < b1) swrite((i + 1) & 1);
         __syncthreads();
+    }
+    if (KS == 2) {
+        // merge: the second half's waves park (m, l, O) in the (now idle) staging area, the
+        // first half's combine them (exp2 domain: m is scaled by scale * log2 e)
+        float *park = (float *)&s_kv[0][0][0][0] + (size_t)qw * 34 * 64;
+        if (ks == 1) {
+            park[lane] = S.m;
+            park[64 + lane] = S.l;
+#pragma unroll
+            for (int ht = 0; ht < 2; ++ht)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) park[(2 + 16 * ht + i) * 64 + lane] = S.o[ht][i];
+        }
+        __syncthreads();
+        if (ks == 1) return;
+        const float m1 = park[lane], l1 = park[64 + lane];
+        const float m = fmaxf(S.m, m1);
+        const float a0 = S.m == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(S.m - m);
+        const float a1 = m1 == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m1 - m);
+        S.l = S.l * a0 + l1 * a1;
+#pragma unroll
+        for (int ht = 0; ht < 2; ++ht)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) S.o[ht][i] = S.o[ht][i] * a0 + park[(2 + 16 * ht + i) * 64 + lane] * a1;
     }
     const float l = S.l + __shfl_xor(S.l, 32);
     if (q < T) {
@@ -1360,10 +1403,17 @@ extern "C" int sd_attention(const void *q, const void *k, const void *vt, int32_
     const float sl2e = scale * 1.4426950408889634f;
     const int64_t wg128 = (int64_t)((tokens + 127) / 128) * B * heads;
     const char *force = getenv("SD_ATTN");
-    const bool lds = (force && force[0]) ? force[0] == 'l' : 2 * wg128 >= (int64_t)sd_num_cus();
-    if (lds) {
+    const bool lds = (force && force[0]) ? force[0] == 'l' || force[0] == '2' : 2 * wg128 >= (int64_t)sd_num_cus();
+    // under one 128-query workgroup per CU: 64-query workgroups over two key halves
+    const bool split = (force && force[0]) ? force[0] == '2' : wg128 < (int64_t)sd_num_cus();
+    if (lds && split) {
+        dim3 grid((unsigned)((tokens + 63) / 64), (unsigned)(B * heads));
+        hipLaunchKernelGGL(k_attn_lds<2>, grid, dim3(256), 0, (hipStream_t)stream, (const __bf16 *)q,
+                           (const __bf16 *)k, (const __bf16 *)vt, tokens, tokens_pad, heads, sl2e,
+                           (__bf16 *)out);
+    } else if (lds) {
         dim3 grid((unsigned)((tokens + 127) / 128), (unsigned)(B * heads));
-        hipLaunchKernelGGL(k_attn_lds, grid, dim3(256), 0, (hipStream_t)stream, (const __bf16 *)q,
+        hipLaunchKernelGGL(k_attn_lds<1>, grid, dim3(256), 0, (hipStream_t)stream, (const __bf16 *)q,
                            (const __bf16 *)k, (const __bf16 *)vt, tokens, tokens_pad, heads, sl2e,
                            (__bf16 *)out);
     } else {

@@ -111,10 +111,11 @@ def test_gemm_epilogues(gpu, M, N, K):
 @pytest.mark.gpu
 @pytest.mark.parametrize("B,H,T", [(1, 6, 481), (2, 12, 77), (1, 12, 1921), (1, 1, 1),
                                    (4, 12, 1921)])
-@pytest.mark.parametrize("mode", ["auto", "lds", "dir"])
+@pytest.mark.parametrize("mode", ["auto", "lds", "dir", "2split"])
 def test_qkv_scatter_and_attention(gpu, B, H, T, mode, monkeypatch):
-    """k_attn_lds (128 queries sharing LDS K / V^T) and k_attn_dir (32 queries x 4 key
-    quarters, fragments from L2): the launcher picks by occupancy, SD_ATTN forces one."""
+    """k_attn_lds<1> (128 queries sharing LDS K / V^T), k_attn_lds<2> (64 queries per key
+    half, halves merged through LDS) and k_attn_dir (32 queries x 4 key quarters, fragments
+    from L2): the launcher picks by occupancy, SD_ATTN forces one."""
     if mode != "auto":
         monkeypatch.setenv("SD_ATTN", mode)
     from scenedino_amd import _lib
