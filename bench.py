@@ -286,6 +286,19 @@ def cpu_baseline(budget_s: float = 20.0, offset_pose: bool = True):
             done_rays += rows_per_chunk * W
             row += rows_per_chunk
         dt = time.perf_counter() - t0
+        # the same oracle on os.cpu_count() threads (SURVEY §8(d)'s count), one image row:
+        # reported beside the main number, which uses the CPUs the job may actually use
+        at_count = None
+        ncpu = os.cpu_count() or 1
+        if ncpu != threads and os.environ.get("SD_CPU_COUNT_RUN", "1") != "0":
+            torch.set_num_threads(ncpu)
+            sl = slice(0, W)
+            t1 = time.perf_counter()
+            O.render(rays[sl], u[:W], *args, sb=1)
+            d1 = time.perf_counter() - t1
+            at_count = {"value": W / d1, "unit": "rays/s", "cores": ncpu,
+                        "sample": f"{W} rays (1 row), {d1:.1f} s on {ncpu} threads"}
+            torch.set_num_threads(threads)
     cpu = platform.processor() or platform.machine()
     try:
         with open("/proc/cpuinfo") as f:
@@ -302,7 +315,8 @@ def cpu_baseline(budget_s: float = 20.0, offset_pose: bool = True):
             "sample": f"{done_rays} rays ({row} of {H} rows) of the same 192x640x64 frame"
                       f"{' (offset render pose)' if offset_pose else ''}, "
                       f"fp32 torch-CPU oracle restatement, {dt:.1f} s on {threads} threads "
-                      f"({cpu}); encoder excluded"}
+                      f"({cpu}); encoder excluded",
+            "at_os_cpu_count": at_count}
 
 
 def _traffic_from_profile(pose):
