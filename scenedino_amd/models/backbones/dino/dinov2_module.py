@@ -186,7 +186,8 @@ class DINOv2Module(nn.Module):
         if not self.use_graph or not x.is_cuda:
             return self._decode(x)
         dpt = isinstance(self.decoder, DPTHead)
-        key = (tuple(x.shape), str(x.device), _param_key(self.encoder), _param_key(self.decoder))
+        dkey = _param_key(self.decoder)  # also validates the decoder's packed weights below
+        key = (tuple(x.shape), str(x.device), _param_key(self.encoder), dkey)
         if self._graph is None or self._graph[0] != key:
             self._graph = None
             static_in = x.detach().float().contiguous().clone()
@@ -203,7 +204,7 @@ class DINOv2Module(nn.Module):
         static_in.copy_(x)
         graph.replay()
         if dpt:  # the final convolution writes a fresh output (no copy of a graph buffer)
-            return self.decoder.forward_last(outs)
+            return self.decoder.forward_last(outs, key=dkey)
         return [o.clone() for o in outs]
 
     def forward(self, x, ground_truth: bool = False):

@@ -124,8 +124,10 @@ class DPTHead(nn.Module):
         self.output_head = OutputHead(d_out)
         self._packed = None
 
-    def _pack(self):
-        key = _param_key(self)
+    def _pack(self, key=None):
+        """Packed weights, re-packed when the parameters changed (``key``: this module's
+        _param_key if the caller has it already)."""
+        key = _param_key(self) if key is None else key
         if self._packed is not None and self._packed[0] == key:
             return self._packed[1]
         rb = self.reassemble_blocks
@@ -197,13 +199,13 @@ class DPTHead(nn.Module):
         out = L.linear_nhwc(out, wt, bt, shuf=k)
         return self.forward_last(out) if last else out
 
-    def forward_last(self, x):
+    def forward_last(self, x, key=None):
         """output_head.head_modules[2] (3x3 conv) on NHWC bf16 -> [(B, C, H, W) f32 grid].
         The grid is written channels-last (the GEMM's natural, coalesced output rows) and
         returned as its (B, C, H, W) permuted view: the reference's shape and values, and
         the layout every grid consumer here reads without a transposition
         (sd_project_grid_nhwc, sd_cast_grid, the training gather)."""
-        w2, b2 = self._pack()["head2"]
+        w2, b2 = self._pack(key)["head2"]
         return [_lib.conv3x3(x, w2, b2, epi=_lib.SD_EPI_F32).permute(0, 3, 1, 2)]
 
     def forward(self, inputs):
