@@ -57,6 +57,9 @@
 // waves per SIMD the channels-last k_project's register budget is cut for (1: the compiler's
 // choice, 176 VGPRs = 2 waves per SIMD).  3 (167 VGPRs, no spill) measured the same time
 // (C2 50-53 us either way, tools/proj_ab.sh): more resident waves do not move this kernel
+#ifndef SD_PROJ_STAGE
+#define SD_PROJ_STAGE 1  // output tile staged through LDS for whole-row 16-B stores (0: 8-B scatter)
+#endif
 #ifndef SD_PROJ_WPE
 #define SD_PROJ_WPE 1
 #endif
@@ -125,7 +128,30 @@ k_project(const float *__restrict__ grid, int64_t B, int C, int64_t HW, int W, c
             kstep(q + 1, x1);
         }
         if (q < nq) kstep(q, x0);
-        if (valid) {
+        if (SD_PROJ_STAGE) {
+            // the wave's 32 x 128 tile through LDS (68-dword pixel rows: 2-way conflicts at
+            // most), then 16-B stores: 4 whole 256-B pixel rows per wave instruction
+            uint32_t *so = (uint32_t *)(lds + nq * 4 * SD_WAVE * 16) + wave * (32 * 68);
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int r4 = 0; r4 < 4; ++r4)
+                    // accumulator rows 4 r4 .. 4 r4 + 3 = hidden 32 t + 8 r4 + 4 h + 0..3
+                    *(uint2 *)(so + li * 68 + (32 * t + 8 * r4 + 4 * h) / 2) =
+                        uint2{sd_pack2<typename Tr::E>(acc[t][4 * r4], acc[t][4 * r4 + 1]),
+                              sd_pack2<typename Tr::E>(acc[t][4 * r4 + 2], acc[t][4 * r4 + 3])};
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own LDS writes
+            const int64_t pix0 = (task - b * ntile) * 32;
+            const int c = lane & 15;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int pp = 4 * k + (lane >> 4);
+                if (pix0 + pp < HW) {
+                    const uint4 v = *(const uint4 *)(so + pp * 68 + 4 * c);
+                    *(uint4 *)(out + (b * HW + pix0 + pp) * (SD_DH / 2) + 4 * c) = v;
+                }
+            }
+        } else if (valid) {
             uint2 *op = (uint2 *)(out + (b * HW + pix) * (SD_DH / 2));
 #pragma unroll
             for (int t = 0; t < 4; ++t)
@@ -728,7 +754,7 @@ static int sd_project_any(const float *grid, int64_t B, int64_t Hf, int64_t Wf, 
         return -1;
     }
     const int64_t HW = Hf * Wf;
-    const int lds_bytes = m->C / 16 * 4 * SD_WAVE * 16;
+    const int lds_bytes = m->C / 16 * 4 * SD_WAVE * 16 + (SD_PROJ_STAGE ? SD_PWG / 64 * 32 * 68 * 4 : 0);
     if (lds_bytes > 160 * 1024) {
         sd_set_error("sd_project_grid: C too large for the LDS-staged weights");
         return -1;

@@ -46,6 +46,21 @@ __device__ __forceinline__ f32x16 vt_zero16() {
 #ifndef VT_NS_SMALL
 #define VT_NS_SMALL 2  // staging-ring depth of the 64 x 64 and 32 x 32 split-K tiles (4, 6: slower)
 #endif
+// VT_MF16 = 1: the GEMM's 32 x 32 accumulator blocks computed as 2 x 2
+// v_mfma_f32_16x16x32_bf16 tiles instead of one v_mfma_f32_32x32x16_bf16 (register q of block
+// (i, j) is element q & 3 of sub-tile q >> 2 = 2 a + b: row 16 a + 4 (lane >> 4) + (q & 3),
+// column 16 b + (lane & 15)).  Measured 4-13 % slower on every encoder shape
+// (tools/gemm_bench.py: 16 more VGPRs on the 128 x 128 tile, twice the fragment reads per
+// MFMA cycle), so off.
+#ifndef VT_MF16
+#define VT_MF16 0
+#endif
+__device__ __forceinline__ int vt_row(int q, int lane) {
+    return VT_MF16 ? 16 * (q >> 3) + 4 * ((lane >> 4) & 3) + (q & 3) : (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5);
+}
+__device__ __forceinline__ int vt_col(int q, int lane) {
+    return VT_MF16 ? 16 * ((q >> 2) & 1) + (lane & 15) : (lane & 31);
+}
 #define GK 32       // K granularity of sd_gemm (the K loop runs in steps of BK = 64 or 32)
 
 __device__ __forceinline__ float vt_gelu(float x) {
@@ -206,6 +221,42 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
 
     auto compute = [&](int kt) {
         const int buf = kt & 1;
+        if (VT_MF16) {
+            // 32-deep k-steps: lane (row l & 15, group l >> 4) holds k = 8 (l >> 4) .. + 7
+            const int rr = lane & 15, kg = lane >> 4;
+#pragma unroll
+            for (int s0 = 0; s0 < (SK ? BK / 128 : BK / 32); ++s0) {
+                const int s = SK ? 4 * s0 + wave : s0;
+                bf16x8 af[TM][2], bfr[TN][2];
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int a = 0; a < 2; ++a)
+                        af[i][a] = *(const bf16x8 *)&SA(buf)[(wm * WM + i * 32 + 16 * a + rr) * GLDS + 32 * s + 8 * kg];
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int b = 0; b < 2; ++b)
+                        bfr[j][b] = *(const bf16x8 *)&SB(buf)[(wn * WN + j * 32 + 16 * b + rr) * GLDS + 32 * s + 8 * kg];
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+#pragma unroll
+                        for (int a = 0; a < 2; ++a)
+#pragma unroll
+                            for (int b = 0; b < 2; ++b) {
+                                const int o = 4 * (2 * a + b);
+                                f32x4 c = {acc[i][j][o], acc[i][j][o + 1], acc[i][j][o + 2], acc[i][j][o + 3]};
+                                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][a], bfr[j][b], c, 0, 0, 0);
+                                acc[i][j][o] = c[0];
+                                acc[i][j][o + 1] = c[1];
+                                acc[i][j][o + 2] = c[2];
+                                acc[i][j][o + 3] = c[3];
+                            }
+            }
+            return;
+        }
 #pragma unroll
         for (int s0 = 0; s0 < (SK ? BK / 64 : BK / 16); ++s0) {
             const int s = SK ? 4 * s0 + wave : s0;
@@ -272,14 +323,19 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
             if (SK && wave != 0) break;
-            const int nl = wn * WN + j * 32 + r;
-            const float bias = (g.bias && n0 + nl < g.N) ? g.bias[n0 + nl] : 0.f;
+            float bias2[2];  // the lane's (at most two) columns of block column j
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                const int nl = wn * WN + j * 32 + vt_col(4 * b, lane);
+                bias2[b] = (g.bias && n0 + nl < g.N) ? g.bias[n0 + nl] : 0.f;
+            }
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int q = 0; q < 16; ++q) {
-                    const int ml = wm * WM + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
-                    float v = acc[i][j][q] + bias;
+                    const int ml = wm * WM + i * 32 + vt_row(q, lane);
+                    const int nl = wn * WN + j * 32 + vt_col(q, lane);
+                    float v = acc[i][j][q] + bias2[VT_MF16 ? (q >> 2) & 1 : 0];
                     if (EPI == SD_EPI_GELU) v = vt_gelu(v);
                     sT[ml * OST + nl] = v;
                 }
@@ -446,100 +502,22 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
         }
         return;
     }
+    // unstaged epilogues (residual update, patch embedding): lane-scattered 4-B stores
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-        const int64_t n = n0 + wn * WN + j * 32 + r;
-        if (n >= g.N) continue;
-        const float bias = g.bias ? g.bias[n] : 0.f;
-        float gam = 1.f;
-        if (EPI == SD_EPI_RESID && g.gamma) gam = g.gamma[n];
-        // qkv scatter coordinates of column n
-        int which = 0, head = 0, e = 0;
-        if (EPI == SD_EPI_QKV) {
-            const int C = g.heads * g.head_dim;
-            which = (int)(n / C);
-            const int rem = (int)(n - (int64_t)which * C);
-            head = rem / g.head_dim;
-            e = rem - head * g.head_dim;
-            if (which == 2) {
-                // V^T: a lane's registers 4g..4g+3 are 4 consecutive tokens of its head-dim
-                // row -> one 8-B store instead of four 2-B stores into four cache lines
-                // (the 32-column tile lies inside the V third: `which` is wave-uniform)
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-#pragma unroll
-                    for (int gq = 0; gq < 4; ++gq) {
-                        const int64_t m = m0 + wm * WM + i * 32 + 8 * gq + 4 * h;
-                        if (m >= g.M) continue;
-                        const uint32_t b = (uint32_t)m / (uint32_t)g.tokens;
-                        const int64_t t = m - (int64_t)b * g.tokens;
-                        __bf16 *dst = (__bf16 *)g.vt +
-                                      (((int64_t)b * g.heads + head) * g.head_dim + e) * g.tokens_pad + t;
-                        if (m + 3 < g.M && t + 3 < g.tokens && (t & 3) == 0) {
-                            bf16x4 v4;
-#pragma unroll
-                            for (int u = 0; u < 4; ++u) v4[u] = (__bf16)(acc[i][j][4 * gq + u] + bias);
-                            *(bf16x4 *)dst = v4;
-                        } else {
-                            for (int u = 0; u < 4 && m + u < g.M; ++u) {
-                                const uint32_t bu = (uint32_t)(m + u) / (uint32_t)g.tokens;
-                                const int64_t tu = m + u - (int64_t)bu * g.tokens;
-                                ((__bf16 *)g.vt)[(((int64_t)bu * g.heads + head) * g.head_dim + e) *
-                                                     g.tokens_pad + tu] =
-                                    (__bf16)(acc[i][j][4 * gq + u] + bias);
-                            }
-                        }
-                    }
-                continue;
-            }
-        }
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
-                const int64_t m = m0 + wm * WM + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
-                if (m >= g.M) continue;
-                float v = acc[i][j][q] + bias;
-                if (EPI == SD_EPI_BF16 || EPI == SD_EPI_F32) {
-                    if (g.res) v += (float)((const __bf16 *)g.res)[m * g.ldo + n];
-                    if (g.res2) v += (float)((const __bf16 *)g.res2)[m * g.ldo + n];
-                }
-                if (EPI == SD_EPI_BF16) {
-                    ((__bf16 *)g.out)[m * g.ldo + n] = (__bf16)v;
-                } else if (EPI == SD_EPI_SHUF) {
-                    const int kk = g.shuf_k, cout = (int)(g.N / (kk * kk));
-                    const int sub = (int)(n / cout), co = (int)(n - (int64_t)sub * cout);
-                    const int dy = sub / kk, dx = sub - dy * kk;
-                    const int hw = g.in_h * g.in_w;
-                    const int b = (int)((uint32_t)m / (uint32_t)hw);
-                    const int pix = (int)(m - (int64_t)b * hw);
-                    const int y = pix / g.in_w, x = pix - y * g.in_w;
-                    const int64_t orow = ((int64_t)b * g.in_h * kk + y * kk + dy) * (g.in_w * kk) +
-                                         x * kk + dx;
-                    ((__bf16 *)g.out)[orow * cout + co] = (__bf16)v;
-                } else if (EPI == SD_EPI_NCHW) {
-                    const int plane = g.tokens;
-                    const int b = (int)((uint32_t)m / (uint32_t)plane);
-                    const int64_t pix = m - (int64_t)b * plane;
-                    ((float *)g.out)[((int64_t)b * g.N + n) * plane + pix] = v;
-                } else if (EPI == SD_EPI_GELU) {
-                    ((__bf16 *)g.out)[m * g.ldo + n] = (__bf16)vt_gelu(v);
-                } else if (EPI == SD_EPI_F32) {
-                    ((float *)g.out)[m * g.ldo + n] = v;
-                } else if (EPI == SD_EPI_RESID) {
+                const int64_t n = n0 + wn * WN + j * 32 + vt_col(q, lane);
+                const int64_t m = m0 + wm * WM + i * 32 + vt_row(q, lane);
+                if (m >= g.M || n >= g.N) continue;
+                const float bias = g.bias ? g.bias[n] : 0.f;
+                const float v = acc[i][j][q] + bias;
+                if constexpr (EPI == SD_EPI_RESID) {
+                    const float gam = g.gamma ? g.gamma[n] : 1.f;
                     float *o = (float *)g.out + m * g.ldo + n;
                     *o = *o + gam * v;
-                } else if (EPI == SD_EPI_QKV) {
-                    // 32-bit division (M < 2^31 is checked at the ABI)
-                    const uint32_t b = (uint32_t)m / (uint32_t)g.tokens;
-                    const int64_t t = m - (int64_t)b * g.tokens;
-                    const int64_t bh = (int64_t)b * g.heads + head;
-                    if (which == 0)
-                        ((__bf16 *)g.q)[(bh * g.tokens + t) * g.head_dim + e] = (__bf16)v;
-                    else if (which == 1)
-                        ((__bf16 *)g.k)[(bh * g.tokens_pad + t) * g.head_dim + e] = (__bf16)v;
-                    else
-                        ((__bf16 *)g.vt)[(bh * g.head_dim + e) * g.tokens_pad + t] = (__bf16)v;
                 } else {  // SD_EPI_PATCH: patch row m = b * patches + p -> token 1 + p
                     const uint32_t bq = (uint32_t)m / (uint32_t)g.patches;
                     const int64_t b = bq, p = m - b * g.patches;
