@@ -43,6 +43,9 @@ __device__ __forceinline__ f32x16 vt_zero16() {
 // ---------------------------------------------------------------------------
 // GEMM
 // ---------------------------------------------------------------------------
+#ifndef VT_NS_BIG
+#define VT_NS_BIG 2    // staging-ring depth of the 128 x 128 tiles
+#endif
 #ifndef VT_NS_SMALL
 #define VT_NS_SMALL 2  // staging-ring depth of the 64 x 64 and 32 x 32 split-K tiles (4, 6: slower)
 #endif
@@ -136,7 +139,7 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
     // MFMAs and its set is re-filled with step k + 1 + NS -- global latency gets NS - 1
     // steps of MFMA work to hide under, at one LDS double buffer.  The small tiles (32 x 32
     // split-K, 64 x 64) have little MFMA work per step and the VGPRs for a deep ring.
-    constexpr int NS = BM >= 128 ? 2 : VT_NS_SMALL;
+    constexpr int NS = BM >= 128 ? VT_NS_BIG : VT_NS_SMALL;
     bf16x8 ra[NS][CA], rb[NS][CB];
     // Rows past M (N) are clamped to the last row instead of predicated: they only feed
     // output rows (columns) that are never stored, and unpredicated loads keep the
