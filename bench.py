@@ -921,6 +921,10 @@ def main_c2(args, world, rank, device, dist, host_stage):
             "workload": ("C2: KITTI-360 192x640 frustum, 64 samples/ray, ViT-S/16-shaped "
                          "256x192x640 DPT feature grid, ResnetFC 295-128-65, lindisp"
                          if args.config == "c2" else
+                         "C1 shape: 192x640 frustum, 32 samples/ray (configs/renderer/"
+                         "pixelnerf.yaml), 256x192x640 DPT feature grid, ResnetFC 295-128-65, "
+                         "lindisp"
+                         if args.config == "c1" else
                          "C4: KITTI-360 192x640 frustum, 128 samples/ray, DINOv2-B/14-shaped "
                          "256x192x640 DPT feature grid, ResnetFC 295-128-385 (384-d field), "
                          "lindisp") +
@@ -985,8 +989,9 @@ def main():
     ap.add_argument("--grid-layout", default="nhwc", choices=["nhwc", "nchw"],
                     help="synthetic feature-grid layout: nhwc = channels-last, what the native "
                          "encoder writes (default); nchw = the reference's contiguous layout")
-    ap.add_argument("--config", default="c2", choices=["c2", "c4", "c5", "vit", "encode", "train"],
-                    help="c2: BASELINE configs[1] (K=64, D=64, the metric's config); c4: "
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c4", "c5", "vit", "encode", "train"],
+                    help="c1: BASELINE configs[0] render shape (K=32, the demo's sampler); "
+                         "c2: BASELINE configs[1] (K=64, D=64, the metric's config); c4: "
                          "configs[3] render shape (K=128, 384-d feature field); c5: "
                          "configs[4] SSCBench voxel query (voxels/s); vit: the DINO ViT "
                          "encoder forward (a19); encode: ViT + DPT decoder (DINOv2Module); "
@@ -1007,6 +1012,8 @@ def main():
     GRID_LAYOUT = args.grid_layout
     if args.config == "c4":
         K_SAMPLES, D_DINO = 128, 384
+    elif args.config == "c1":
+        K_SAMPLES = 32
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(_launch_ranks(args))
