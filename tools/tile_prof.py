@@ -16,6 +16,9 @@ NAMES = ["ray_pass", "head", "itemA0", "ray_col", "barrier_X", "stage", "items",
 
 def main():
     offset = "--identity" not in sys.argv
+    for a in sys.argv[1:]:
+        if a.startswith("--k="):  # samples per ray (C1: 32)
+            bench.K_SAMPLES = int(a[4:])
     dev = torch.device("cuda:0")
     net, renderer, wrapper, sampler, pose, Ks = bench.make_scene(0, dev, "bf16", offset)
     f = _lib.load().sd_tile_prof
@@ -33,7 +36,7 @@ def main():
         f(buf, 1)
     waves = buf[31]
     tot = sum(buf[i] for i in range(10))  # 10..12 subdivide ray_pass
-    print(f"{'offset' if offset else 'identity'}: waves {waves}, cycles per wave {tot / max(waves, 1):.0f}")
+    print(f"{'offset' if offset else 'identity'} K={bench.K_SAMPLES}: waves {waves}, cycles per wave {tot / max(waves, 1):.0f}")
     for i, nm in enumerate(NAMES):
         print(f"  {nm:10s} {buf[i] / max(waves, 1):10.0f} cyc/wave  {100 * buf[i] / max(tot, 1):5.1f}%")
 
