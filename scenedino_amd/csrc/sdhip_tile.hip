@@ -69,6 +69,12 @@
 #ifndef ST_ABL_NOCODE
 #define ST_ABL_NOCODE 0
 #endif
+#ifndef ST_EPI_BFLY
+#define ST_EPI_BFLY 1    // hidden sums of the ray epilogue by a bank-masked DPP butterfly
+#endif
+#ifndef ST_ABL_NOHSUM
+#define ST_ABL_NOHSUM 0  // cost probe: the epilogue's 32 hidden-sum reductions skipped (wrong dino)
+#endif
 #ifndef ST_ABL_NOHC
 #define ST_ABL_NOHC 0
 #endif
@@ -179,6 +185,18 @@ static_assert(st_l_rec(8) % 16 == 0 && st_l_rec(12) % 16 == 0, "record area alig
 __host__ __device__ constexpr int st_rec_bytes(int nw, int K) { return nw * 2 * K * 40; }
 
 // packed u16x2 (x | y << 16) component-wise min / max
+// one butterfly level of a 16-lane row sum over two values: lanes of banks MA (groups of 4
+// lanes) get a + a(lane - RA), lanes of banks MB get b + b(lane - RB), both into a.  The
+// bank-masked DPP add is inline asm (the compiler does not fold a partially masked DPP move
+// into its user); s_nop 1 covers the VALU-write -> DPP-read hazard of the sources.
+#define ST_BFLY(a, b, RA, RB, MA, MB)                                                         \
+    do {                                                                                      \
+        asm("s_nop 1\n\tv_add_f32_dpp %0, %0, %0 row_ror:" #RA " row_mask:0xf bank_mask:" #MA \
+            : "+v"(a));                                                                       \
+        asm("s_nop 1\n\tv_add_f32_dpp %0, %1, %1 row_ror:" #RB " row_mask:0xf bank_mask:" #MB \
+            : "+v"(a) : "v"(b));                                                              \
+    } while (0)
+
 __device__ __forceinline__ uint32_t st_min2(uint32_t a, uint32_t b) {
     typedef __attribute__((ext_vector_type(2))) unsigned short u16x2;
     return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a),
@@ -1039,16 +1057,45 @@ k_render_tile(const st_args sa) {
             }
 #else
             uint8_t *hs = lds + ST_L_HS + wave * 256;
+#if ST_EPI_BFLY
+            if (!ST_ABL_NOHSUM) {
+                // the 32 hidden sums q = 4 t + r reduced over the 16 sample lanes of the row
+                // as a butterfly (64 VALU ops instead of 32 x 4): bank-masked DPP halves the
+                // live values at the first two levels, quad permutes finish -- lane bank b
+                // then holds q = i + 8 b, i = 0..7 (hidden 16 (2 b + (i >> 2)) + 4 g + (i & 3))
+                float v[16];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    v[i] = hacc[i >> 2][i & 3];
+                    ST_BFLY(v[i], hacc[(i + 16) >> 2][i & 3], 8, 8, 0x3, 0xc);
+                }
+#pragma unroll
+                for (int i = 0; i < 8; ++i) ST_BFLY(v[i], v[i + 8], 12, 4, 0x5, 0xa);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    v[i] += SD_DPP0(v[i], 0xb1);  // quad_perm [1, 0, 3, 2]
+                    v[i] += SD_DPP0(v[i], 0x4e);  // quad_perm [2, 3, 0, 1]
+                }
+                if ((j & 3) == 0) {
+                    const int b = j >> 2;
+                    *(uint2 *)(hs + (32 * b + 4 * g) * 2) =
+                        uint2{sd_pack2<E>(v[0], v[1]), sd_pack2<E>(v[2], v[3])};
+                    *(uint2 *)(hs + (32 * b + 16 + 4 * g) * 2) =
+                        uint2{sd_pack2<E>(v[4], v[5]), sd_pack2<E>(v[6], v[7])};
+                }
+            }
+#else
 #pragma unroll
             for (int t = 0; t < 8; ++t) {
                 f32x4 vsum;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) vsum[r] = sd_rowsum16(hacc[t][r]);
+                for (int r = 0; r < 4; ++r) vsum[r] = ST_ABL_NOHSUM ? hacc[t][r] : sd_rowsum16(hacc[t][r]);
                 // hidden 16 t + 4 g + r
                 if (j == 0)
                     *(uint2 *)(hs + (16 * t + 4 * g) * 2) =
                         uint2{sd_pack2<E>(vsum[0], vsum[1]), sd_pack2<E>(vsum[2], vsum[3])};
             }
+#endif
 #endif
 #if ST_EPI_STORES
             {
