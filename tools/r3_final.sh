@@ -21,7 +21,7 @@ t 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $O/prof_c2/pmc1 -o run --outp
 t 120 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $O/prof_c2/pmc2 -o run --output-format csv -- python3 $B > $O/pmc2.log 2>&1 || { tail -20 $O/pmc2.log; exit 7; }
 echo part1-done
 else
-for c in c5 c4 encode vit train; do
+for c in c1 c5 c4 encode vit train; do
   t 300 python bench.py --config $c > $O/bench_$c.log 2>&1 || { tail -20 $O/bench_$c.log; exit 8; }
   grep '^{' $O/bench_$c.log | cut -c1-300
 done
