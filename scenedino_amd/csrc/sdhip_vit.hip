@@ -1161,12 +1161,13 @@ __global__ void __launch_bounds__(256) k_lngemm(sd_gemm_args g, const float *__r
         for (int t = 0; t < 2; ++t) {
             const f32x4 a = t ? acc1 : acc0;
             const int64_t mb = m0 + 16 * t + 4 * kq;
+            // (image, token) of row mb by one divide; rows mb + 1 .. mb + 3 step from it
+            const uint32_t b0 = (uint32_t)mb / (uint32_t)g.tokens;
+            const int64_t tk0 = mb - (int64_t)b0 * g.tokens;
             if (which == 2) {
                 // V^T: the lane's 4 rows are 4 consecutive tokens of its head-dim row
-                const uint32_t b = (uint32_t)mb / (uint32_t)g.tokens;
-                const int64_t tk = mb - (int64_t)b * g.tokens;
-                __bf16 *dst = (__bf16 *)g.vt + (((int64_t)b * g.heads + head) * g.head_dim + e) * g.tokens_pad + tk;
-                if (mb + 3 < g.M && tk + 3 < g.tokens && (tk & 3) == 0) {
+                __bf16 *dst = (__bf16 *)g.vt + (((int64_t)b0 * g.heads + head) * g.head_dim + e) * g.tokens_pad + tk0;
+                if (mb + 3 < g.M && tk0 + 3 < g.tokens && (tk0 & 3) == 0) {
                     bf16x4 v4;
 #pragma unroll
                     for (int u = 0; u < 4; ++u) v4[u] = (__bf16)(a[u] + bias);
@@ -1178,8 +1179,16 @@ __global__ void __launch_bounds__(256) k_lngemm(sd_gemm_args g, const float *__r
             for (int u = 0; u < 4; ++u) {
                 const int64_t m = mb + u;
                 if (m >= g.M) break;
-                const uint32_t b = (uint32_t)m / (uint32_t)g.tokens;
-                const int64_t tk = m - (int64_t)b * g.tokens;
+                uint32_t b;
+                int64_t tk;
+                if (g.tokens >= 4) {  // at most one image boundary in 4 rows
+                    const bool wrap = tk0 + u >= g.tokens;
+                    b = b0 + (wrap ? 1u : 0u);
+                    tk = tk0 + u - (wrap ? g.tokens : 0);
+                } else {
+                    b = (uint32_t)m / (uint32_t)g.tokens;
+                    tk = m - (int64_t)b * g.tokens;
+                }
                 const int64_t bh = (int64_t)b * g.heads + head;
                 const __bf16 v = (__bf16)(a[u] + bias);
                 if (which == 0)
