@@ -35,6 +35,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 H, W, K_SAMPLES = 192, 640, 64
+# diagnostic A/B only (default on: demo_script asks for per-sample weights and alphas)
+WANT_SAMPLES = os.environ.get("SCENEDINO_AMD_BENCH_NO_SAMPLES") != "1"
 C_GRID, HF, WF = 256, 192, 640
 KITTI_K = [[0.7849, 0.0, -0.0312], [0.0, 2.9391, 0.2701], [0.0, 0.0, 1.0]]
 PEAK_TFLOPS = {"bf16": 2500.0, "fp16": 2500.0, "fp32": 157.3,   # MI355X dense MFMA
@@ -824,7 +826,8 @@ def c2_pose_run(args, world, rank, device, dist, offset_pose, host_stage):
     def step(i):
         if gather is not None:  # frame f on rank f; maps rendered into the gather send slot
             net.render_into = gather.send(i)
-        out = render_step(net, wrapper, sampler, pose, Ks, band)
+        out = render_step(net, wrapper, sampler, pose, Ks, band, want_weights=WANT_SAMPLES,
+                          want_alphas=WANT_SAMPLES)
         if gather is not None:
             gather.start(i)
         return out
