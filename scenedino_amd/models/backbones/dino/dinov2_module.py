@@ -15,8 +15,9 @@ The loss-side downsampler (``downsampler_arch``: ``featup`` = PatchSalienceDowns
 the sd_salience kernels, ``bilinear``) is built as in the reference (same
 ``encoder.downsampler.*`` checkpoint keys).  Out of scope (training-loss machinery, SURVEY
 §8 "out"): the feature-upsampling GT wrappers of ``mode="upsample-gt"`` (upsampler.py,
-kornia).  ``VisualizationModule``
-(PCA / k-means colouring of feature maps for TensorBoard) is not built.
+kornia).  ``VisualizationModule`` (PCA / cosine k-means colouring of feature maps, the
+demo's and the validation panels' ``fit_visualization`` / ``transform_visualization``) is
+built as in the reference, as plain device tensor ops (visualization.py).
 """
 from __future__ import annotations
 
@@ -29,6 +30,7 @@ from torch import nn
 from .dim_reduction import MlpDimReduction, NoDimReduction
 from .downsampler import BilinearDownsampler, PatchSalienceDownsampler
 from .dpt_head import DPTHead
+from .visualization import VisualizationModule
 from .vit import DINOv2Encoder, _param_key, vit_forward
 
 
@@ -164,6 +166,7 @@ class DINOv2Module(nn.Module):
         self.dino_pca_dim = dino_pca_dim
         self.dim_reduction = build_dim_reduction(dim_reduction_arch, self.encoder.latent_size,
                                                  dino_pca_dim)
+        self.visualization = VisualizationModule(self.encoder.latent_size)
         self.use_graph = True
         self._graph = None
 
@@ -242,6 +245,18 @@ class DINOv2Module(nn.Module):
     def expand_dim(self, features):
         """dinov2_module.py:191-192."""
         return self.dim_reduction.transform_expand(features)
+
+    def fit_visualization(self, features, refit=True):
+        """dinov2_module.py:194-195."""
+        return self.visualization.fit_pca(features, refit)
+
+    def transform_visualization(self, features, norm=False, from_dim=0):
+        """dinov2_module.py:197-198."""
+        return self.visualization.transform_pca(features, norm, from_dim)
+
+    def fit_transform_kmeans_visualization(self, features):
+        """dinov2_module.py:200-201."""
+        return self.visualization.fit_transform_kmeans_batch(features)
 
     @classmethod
     def from_conf(cls, conf):

@@ -639,6 +639,54 @@ def fx_salience_downsampler():
     np.savez_compressed(os.path.join(HERE, "salience_downsampler.npz"), **out)
 
 
+def fx_visualization():
+    """VisualizationModule (models/backbones/dino/visualization.py:9-153), the encoder's
+    PCA / k-means colouring API (dinov2_module.py:156,194-201): fit_pca under a seeded global
+    RNG (torch.pca_lowrank draws its sketch from it), transform_pca in every mode the callers
+    use, and fit_transform_kmeans_batch.  pykeops is absent: its ``LazyTensor`` is stubbed by
+    the dense equivalent of the two operations the k-means loop uses (``x_i | c_j`` = the
+    (N, K) dot products, ``.argmax(dim=1)``), so the loop itself is the reference's."""
+    import importlib.util
+    pk = types.ModuleType("pykeops")
+    pkt = types.ModuleType("pykeops.torch")
+
+    class LazyTensor:  # dense stand-in for the two LazyTensor ops of visualization.py:142-143
+        def __init__(self, t):
+            self.t = t
+
+        def __or__(self, other):
+            return LazyTensor((self.t * other.t).sum(-1))
+
+        def argmax(self, dim):
+            return self.t.argmax(dim=dim)
+
+    pkt.LazyTensor = LazyTensor
+    pk.torch = pkt
+    sys.modules["pykeops"], sys.modules["pykeops.torch"] = pk, pkt
+    spec = importlib.util.spec_from_file_location(
+        "ref_visualization", os.path.join(REF, "scenedino/models/backbones/dino/visualization.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    g = torch.Generator().manual_seed(91)
+    feats = torch.randn(600, 64, generator=g) @ torch.randn(64, 64, generator=g) * 0.3 + 0.1
+    feats[[5, 77, 301]] = float("nan")
+    img = torch.randn(6, 10, 64, generator=g) + 0.2
+    vis = mod.VisualizationModule(768)
+    torch.manual_seed(92)
+    vis.fit_pca(feats, refit=True)
+    out = {"feats": np32(feats), "img": np32(img), "mean": np32(vis.batch_rgb_mean),
+           "comp": np32(vis.batch_rgb_comp)}
+    for fd in (0, 3, 6):
+        for norm in (False, True):
+            out[f"t_{fd}_{int(norm)}"] = np32(vis.transform_pca(img, norm, fd))
+    km_in = torch.randn(3, 40, 1, 64, generator=g)
+    km_in[:, :, :, :4] += 2.0 * torch.randn(3, 40, 1, 4, generator=g).sign()
+    out["km_in"] = np32(km_in)
+    out["km_map"] = np32(vis.fit_transform_kmeans_batch(km_in))
+    out["km_centers"] = np32(vis.kmeans_cluster_centers)
+    np.savez_compressed(os.path.join(HERE, "visualization.npz"), **out)
+
+
 def det_fill(module, seed):
     """Deterministic parameter fill by sorted state_dict name (shared with tests/test_dpt.py):
     weights N(0, 1/fan) with fan = numel of one output slice, vectors N(0, 0.05^2)."""
@@ -759,6 +807,10 @@ def main():
         fx_ssc_scoring()
         print("ssc scoring fixture written to", HERE)
         return
+    if os.environ.get("GOLDEN_ONLY") == "visualization":
+        fx_visualization()
+        print("visualization fixture written to", HERE)
+        return
     if os.environ.get("GOLDEN_ONLY") == "seg":
         _install_stubs()
         fx_seg_head()
@@ -805,6 +857,7 @@ def main():
     fx_ssc_scoring()
     fx_patch_sampler(ref)
     fx_salience_downsampler()
+    fx_visualization()
     print("golden fixtures written to", HERE)
 
 
