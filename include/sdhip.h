@@ -412,7 +412,8 @@ int sd_gemm(const sd_gemm_args *args, void *stream);
 
 /* nn.LayerNorm(K, eps) fused into the prologue of a GEMM (timm Block: norm1 -> attn.qkv,
  * norm2 -> mlp.fc1, vit.py:112-189 over timm's VisionTransformer): out = EPI(LN(x) W^T + b)
- * for x (M, K) f32 rows (K = C in {384, 768}), W = args->w (N, K) bf16; args->a is unused.
+ * for x (M, K) f32 rows, dense with row stride K (K = C in {384, 768}), W = args->w (N, K)
+ * bf16; args->a is unused.  SD_EPI_QKV needs head_dim % 8 == 0 and tokens_pad % 8 == 0.
  * epi SD_EPI_QKV / SD_EPI_GELU / SD_EPI_BF16 with the sd_gemm fields they read.  The
  * normalised rows are the bf16 ones sd_layernorm would write (same arithmetic). */
 int sd_ln_gemm(const sd_gemm_args *args, const float *x, const float *ln_w, const float *ln_b,

@@ -226,13 +226,14 @@ class FieldMLPFused(torch.autograd.Function):
         return (dx if ctx.needs_input_grad[0] else None, *rest, None)
 
     @staticmethod
-    def grads(ctx, g_sigma, g_dino, full_rows=False, dx16=False, scatter=None):
+    def grads(ctx, g_sigma, g_dino, full_rows=False, dx16=False, scatter=None, no_dx=False):
         """(dX, dW_in, db_in, dW_out, db_out) of the saved forward; dX rows are the C
         feature columns, or (full_rows) as wide as x with zero code / ones columns; f32, or
         (dx16) in x's 16-bit dtype -- the dtype the reference's autocast Linear backward
         hands to grid_sample's backward.  ``scatter = (xyz (B, P, 3), cam_f, Hf, Wf, dgrid)``:
         the grid_sample backward fused into the kernel -- dX (in x's dtype) goes straight
-        into the NHWC f32 grid gradient dgrid, and dX is returned as None."""
+        into the NHWC f32 grid gradient dgrid, and dX is returned as None.  ``no_dx``: no
+        input gradient wanted -- the kernel skips the dX product and dX is None."""
         x_aug, h, sigma = ctx.saved_tensors
         p = ctx.p
         N, ldx, d_in, D, C, dt, pdt = ctx.meta
@@ -254,6 +255,8 @@ class FieldMLPFused(torch.autograd.Function):
             a.dx_dtype, a.lddx = dt, C
             a.xyz, a.cam_f, a.dgrid = xyz.data_ptr(), cam_f.data_ptr(), dgrid.data_ptr()
             a.P, a.Hf, a.Wf = xyz.shape[1], Hf, Wf
+        elif no_dx:
+            dx = None
         else:
             dx = torch.empty(N, ldx if full_rows else C, device=dev,
                              dtype=x_aug.dtype if dx16 else torch.float32)
@@ -320,8 +323,8 @@ class FieldGatherMLP(torch.autograd.Function):
                 sc = (ctx.xyz, ctx.cam_f, Hf, Wf, buf)
                 _, dw_in, db_in, dw_out, db_out = FieldMLPFused.grads(ctx, gs, gd, scatter=sc)
                 d_grid = buf if first else None
-            else:
-                _, dw_in, db_in, dw_out, db_out = FieldMLPFused.grads(ctx, gs, gd, dx16=True)
+            else:  # the grid needs no gradient: weight gradients only (no dX product)
+                _, dw_in, db_in, dw_out, db_out = FieldMLPFused.grads(ctx, gs, gd, no_dx=True)
             return (d_grid, None, None, None, None, None, None, None, dw_in, db_in, dw_out,
                     db_out)
         dx, dw_in, db_in, dw_out, db_out = FieldMLPFused.grads(ctx, gs, gd, dx16=DX16)

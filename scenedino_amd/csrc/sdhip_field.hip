@@ -1018,7 +1018,9 @@ extern "C" int sd_field_query(const sd_field_args *args, const sd_mlp *mlp, void
     if (a.B <= 0 || a.P < 0 || !a.xyz || !a.grid || !a.cam_f || !a.sigma || !a.dino ||
         a.Hf <= 0 || a.Wf <= 0 || a.nv < 0 || a.nv > SD_MAX_NV ||
         (a.dino_dtype != SD_F32 && a.dino_dtype != SD_BF16) ||
-        a.B * a.P * (int64_t)mlp->D * (a.dino_dtype == SD_BF16 ? 2 : 4) >= (1LL << 32) ||
+        // the dino rows of the last 32-point tile's padding lanes are dropped by the buffer
+        // descriptor's range check: their offsets must not wrap, so the bound is on the padded count
+        (a.B * a.P + 31) / 32 * 32 * (int64_t)mlp->D * (a.dino_dtype == SD_BF16 ? 2 : 4) >= (1LL << 32) ||
         a.B * (int64_t)a.Hf * a.Wf * mlp->C * (mlp->dtype == SD_F32 ? 4 : 2) >= (1LL << 32) ||
         (a.nv > 0 && (a.rgb || a.invalid) && (!a.img || !a.cam_c || a.Hc <= 0 || a.Wc <= 0))) {
         sd_set_error("sd_field_query: invalid argument (all grid planes < 4 GiB)");

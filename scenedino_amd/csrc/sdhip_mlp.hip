@@ -376,6 +376,9 @@ __global__ void __launch_bounds__(ML_WAVES * 64) k_mlp_bwd(const sd_mlp_train_ar
                         uint2{sd_pack2<E>(dh[t][4 * g], dh[t][4 * g + 1]),
                               sd_pack2<E>(dh[t][4 * g + 2], dh[t][4 * g + 3])};
             }
+        if constexpr (!SCAT) {
+            if (!a.dx) continue;  // the caller needs no input gradient: dH / dY only
+        }
         // dX = dH W_in[:, :C]: A = dH (rows = points) from the accumulators
         Frag af[8];
 #pragma unroll
@@ -428,8 +431,9 @@ static int ml_check(const sd_mlp_train_args *a, bool bwd) {
     if (a->dgrid)  // fused scatter: the frame / grid geometry of the forward gather
         return a->xyz && a->cam_f && a->P > 0 && a->N % a->P == 0 && a->Hf > 0 && a->Wf > 0 &&
                (a->N / a->P) * a->Hf * a->Wf * (int64_t)a->C < (1LL << 31);
+    if (!a->dx) return 1;  // no dX wanted (weight gradients only)
     return a->lddx >= a->C && a->lddx <= a->ldx &&
-           (a->dx_dtype == SD_F32 || a->dx_dtype == a->dtype) && a->dx;
+           (a->dx_dtype == SD_F32 || a->dx_dtype == a->dtype);
 }
 
 template <typename K>

@@ -26,6 +26,7 @@
 // while item i computes.
 #include "sdhip_render.h"
 #include <stdlib.h>
+#include <type_traits>
 
 // diagnostic ablation switches (timing experiments only; outputs are wrong when set)
 #ifndef SD_ABL_NORAYPASS
@@ -163,6 +164,121 @@ k_project(const float *__restrict__ grid, int64_t B, int C, int64_t HW, int W, c
                               sd_pack2<typename Tr::E>(acc[t][4 * r4 + 2], acc[t][4 * r4 + 3])};
         }
     }
+}
+
+// ---------------------------------------------------------------------------
+// k_project_lds: the channels-last projection (C = 256) as a streaming kernel.  k_project
+// reads each lane's own pixel row 32 B at a time (32 pixel rows, 1 KiB apart, per wave
+// instruction) and reached ~3.3 TB/s; here the grid is swept in order by LDS-DMA of whole
+// half pixel rows (512 contiguous bytes, 128 channels) into a ring of PJ_NS slots of 32
+// rows, up to PJ_NS - 1 slots (~115 KiB) in flight per CU.  Workgroup = 4 waves, one per
+// CU; wave w owns hidden tile w (32 hidden): its 16 layer-1 A fragments (one per K step of
+// 16 channels) stay in 64 VGPRs for the whole kernel, so the LDS holds only the grid rows.
+// Per 32-pixel chunk: slot 2k = channels 0..127, slot 2k + 1 = channels 128..255; every wave
+// reads a slot's rows as the MFMA B operand (lane (pixel n, half h): 8 channels, 32 B),
+// converts them to the 16-bit type and issues 8 32x32x16 MFMAs -- the same products in
+// the same order as k_project, so P is bit-identical.  The 32 x 128 output tile goes
+// through an LDS staging area and leaves as 16-B stores of whole 256-B pixel rows.
+// ---------------------------------------------------------------------------
+#define PJ_NS 8                    // ring slots (half-chunks)
+#define PJ_ROWB 528                // LDS bytes per staged half row: 512 + 16 pad (conflict-free reads)
+#define PJ_SLOT (32 * PJ_ROWB)
+#define PJ_OUTROW 272              // staging row stride (256 B of P + 16 pad)
+#define PJ_LDS (PJ_NS * PJ_SLOT + 32 * PJ_OUTROW)
+
+template <int P>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1)))
+k_project_lds(const float *__restrict__ grid, int64_t npix, const sd_mlp m, uint32_t *__restrict__ out) {
+    typedef T16<P> Tr;
+    typedef typename Tr::Frag Frag;
+    typedef typename Tr::E E;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void *)lds;
+    const int lane = threadIdx.x & 63, h = lane >> 5, li = lane & 31;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t nch = (npix + 31) / 32;
+    if ((int64_t)blockIdx.x >= nch) return;  // workgroup-uniform
+    const int my = (int)((nch - 1 - blockIdx.x) / gridDim.x + 1);  // chunks of this workgroup
+
+    // layer-1 A fragments of hidden tile `wave` (k_project's w_in: [q][ht][lane]) + bias rows
+    Frag W[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) W[q] = ((const Frag *)m.w_in)[(q * 4 + wave) * SD_WAVE + lane];
+    f32x16 bias;
+    {
+        const f32x4 *bb = (const f32x4 *)(m.b_in_h + (wave * 2 + h) * 16);
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) {
+            const f32x4 v = bb[q4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) bias[4 * q4 + i] = v[i];
+        }
+    }
+    // slot i = (chunk i >> 1, half i & 1): this wave DMAs rows 8 wave .. 8 wave + 7, 512 B each
+    // (lanes 0..31).  Slots past the workgroup's last chunk re-read the last pixel (kept so
+    // that every iteration issues the same number of vector-memory operations).
+    auto issue = [&](int i) {
+        const int64_t c = (int64_t)blockIdx.x + (int64_t)(i >> 1) * gridDim.x;
+        const uint32_t sb = lds0 + (uint32_t)(i % PJ_NS) * PJ_SLOT;
+        if (lane < 32) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                const int row = 8 * wave + r;
+                int64_t pix = c * 32 + row;
+                pix = pix < npix ? pix : npix - 1;
+                const float *src = grid + pix * 256 + (i & 1) * 128 + 4 * lane;
+                sd_dma16(src, sb + (uint32_t)row * PJ_ROWB);
+            }
+        }
+    };
+#pragma unroll
+    for (int i = 0; i < PJ_NS - 1; ++i) issue(i);
+
+    f32x16 acc = bias;
+    uint8_t *stg = lds + PJ_NS * PJ_SLOT;
+    // one half-chunk: wait for slot i, refill the ring, 8 K steps (A fragments W[8 HALF + q]:
+    // compile-time indices, so the 16 fragments stay in VGPRs)
+    auto half_step = [&](int i, auto half_c) {
+        constexpr int HALF = decltype(half_c)::value;
+        // this wave's rows of slot i landed: 8 (PJ_NS - 2) of its DMAs (+ any stores) are younger
+        asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
+        static_assert(8 * (PJ_NS - 2) == 48, "vmcnt immediate");
+        __syncthreads();  // every wave's rows landed; slot i - 1 is free (all waves past it)
+        issue(i + PJ_NS - 1);
+        const uint8_t *sl = lds + (i % PJ_NS) * PJ_SLOT + li * PJ_ROWB + 32 * h;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const f32x4 a = *(const f32x4 *)(sl + 64 * q), b = *(const f32x4 *)(sl + 64 * q + 16);
+            Frag f;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                f[e] = (E)a[e];
+                f[4 + e] = (E)b[e];
+            }
+            acc = Tr::mma32(W[8 * HALF + q], f, acc);
+        }
+    };
+    for (int k = 0; k < my; ++k) {
+        half_step(2 * k, std::integral_constant<int, 0>());
+        half_step(2 * k + 1, std::integral_constant<int, 1>());
+        // accumulator rows 4 r4 .. 4 r4 + 3 = hidden 32 wave + 8 r4 + 4 h + 0..3 of pixel li
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4)
+            *(uint2 *)(stg + li * PJ_OUTROW + 2 * (32 * wave + 8 * r4 + 4 * h)) =
+                uint2{sd_pack2<E>(acc[4 * r4], acc[4 * r4 + 1]),
+                      sd_pack2<E>(acc[4 * r4 + 2], acc[4 * r4 + 3])};
+        acc = bias;
+        __syncthreads();  // the 32 x 128 tile is complete in the staging rows
+        const int64_t pix0 = ((int64_t)blockIdx.x + (int64_t)k * gridDim.x) * 32;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int pp = 8 * wave + 4 * kk + (lane >> 4);
+            const uint4 v = *(const uint4 *)(stg + pp * PJ_OUTROW + 16 * (lane & 15));
+            if (pix0 + pp < npix)
+                *(uint4 *)(out + (pix0 + pp) * (SD_DH / 2) + 4 * (lane & 15)) = v;
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the workgroup
 }
 
 // ---------------------------------------------------------------------------
@@ -762,6 +878,19 @@ static int sd_project_any(const float *grid, int64_t B, int64_t Hf, int64_t Wf, 
     hipStream_t s = (hipStream_t)stream;
     int64_t nblk;
     const int64_t work = B * ((HW + 31) / 32);
+    static const bool old_proj = getenv("SDHIP_PROJ_OLD") != nullptr;  // diagnostic A/B switch
+    if (nhwc && m->C == 256 && !old_proj) {  // the streaming LDS-DMA kernel
+        const int64_t nch = work;
+        nblk = sd_num_cus();
+        if (nblk > nch) nblk = nch;
+        auto go = [&](auto kern) {
+            (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, PJ_LDS);
+            hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(256), PJ_LDS, s, grid, B * HW, *m,
+                               (uint32_t *)out);
+        };
+        if (m->dtype == SD_F16) go(k_project_lds<SD_F16>); else go(k_project_lds<SD_BF16>);
+        return sd_check_err();
+    }
 #define SD_PROJ_LAUNCH(PP, NH)                                                                  \
     do {                                                                                        \
         sd_launch_proj(k_project<PP, NH>, work, lds_bytes, s, nblk);                            \

@@ -3,11 +3,22 @@
 #pragma once
 #ifndef SD_PE_DIRECT
 #define SD_PE_DIRECT 0
+#endif
 // overflow list of the tile kernel: entries are blocks of SD_LIST_BLK consecutive rays
 // (a group of 8 or 12 rays lists 2 or 3 blocks); the fallback kernels render the blocks
 #define SD_LIST_BLK 4
-#endif
 #include "sdhip_point.h"
+
+// LDS-DMA of 16 B per active lane (global_load_lds_dwordx4) into lds_addr + 16 * lane, as
+// inline asm: issued through the builtin, the compiler treats every later LDS read as a
+// possible alias of the in-flight DMA and waits for it (s_waitcnt vmcnt(0)) at the first
+// one; the kernels order these DMAs themselves (s_waitcnt vmcnt + barrier before the staged
+// data is read).  m0 = LDS destination of lane 0, one wait state after the SALU write.
+__device__ __forceinline__ void sd_dma16(const void *src, uint32_t lds_addr) {
+    lds_addr = __builtin_amdgcn_readfirstlane(lds_addr);  // wave-uniform by construction
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+                 :: "v"(src), "s"(lds_addr) : "memory");
+}
 
 // 16-bit element traits.  Blend of the pair-interleaved projected grid (k_project):
 // every dword of a row holds (P[x0][c], P[x1][c]) of one channel c, so a bilinear

@@ -1350,7 +1350,8 @@ extern "C" int sd_ln_gemm(const sd_gemm_args *args, const float *x, const float 
               g.M * C < ((int64_t)1 << 31) && g.N * C < ((int64_t)1 << 31);
     if (g.epi == SD_EPI_QKV)
         ok = ok && g.q && g.k && g.vt && g.head_dim > 0 && g.heads > 0 && g.tokens > 0 &&
-             g.tokens_pad >= g.tokens && g.N == 3LL * g.heads * g.head_dim && g.M % g.tokens == 0;
+             g.tokens_pad >= g.tokens && g.N == 3LL * g.heads * g.head_dim && g.M % g.tokens == 0 &&
+             g.head_dim % 8 == 0 && g.tokens_pad % 8 == 0;  // 8-B V^T stores, as sd_gemm
     else
         ok = ok && g.out && g.ldo >= g.N;
     if (!ok) {

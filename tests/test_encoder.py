@@ -187,3 +187,12 @@ def test_make_model_encode_render_end_to_end(gpu):
     for k in ("depth", "dino_features", "weights"):
         assert torch.isfinite(outs[0][k]).all()
         assert torch.equal(outs[0][k], outs[1][k]), k
+
+
+def test_default_precision_is_the_contract_meeting_one():
+    """The reference's configs carry no precision key; the build then renders in fp16, the
+    16-bit mode within SURVEY §8(c)'s 1e-2 m depth contract (bf16 is selectable)."""
+    from scenedino_amd.models import make_model
+    conf = {k: v for k, v in MODEL_CONF.items() if k != "precision"}
+    assert make_model(conf).precision == "fp16"
+    assert make_model(MODEL_CONF).precision == "bf16"

@@ -12,9 +12,10 @@ tools/parity_report.py):
     295-term layer; the full-grid offset render: the same through 64 composited samples).
   * 16-bit paths (bf16 / fp16 operands, fp32 accumulate; "proj": sd_project_grid +
     sd_render_proj = tile kernel + overflow fallback, "grid": sd_render_fused): weights
-    max |d| <= 2e-3, DINO and colour rel-L2 <= 1e-2, depth max |d| <= 1e-2 m (fp16) /
-    5e-2 m (bf16: an 8-bit mantissa on sigma moves alpha by ~1e-3 at samples up to 30 m
-    apart) and depth rel-L2 <= 2e-3.
+    max |d| <= 2e-3, DINO and colour rel-L2 <= 1e-2, depth max |d| <= 1e-2 m (fp16, the
+    default precision) / 5e-2 m (bf16: an 8-bit mantissa on the projected grid and the
+    bilinear weights moves alpha by ~1e-3 at samples up to 30 m apart) and
+    depth rel-L2 <= 2e-3.
 """
 import hashlib
 import json
@@ -48,14 +49,19 @@ FP32_ATOL = {"depth": 1e-6, "weights": 1e-6, "alphas": 1e-6, "rgb": 1e-5, "rgb_s
 # the full 256x192x640-grid render from the offset pose (64 samples through the scan)
 FP32_ATOL_FULL = {"depth": 1e-6, "weights": 1e-5, "alphas": 1e-4, "rgb": 1e-5, "dino": 5e-5}
 LOWP_DEPTH_MAX = {"bf16": 5e-2, "fp16": 1e-2}
-# SURVEY §8(c) states 1e-2 m for depth.  bf16 (the default, BASELINE configs[1]) meets it for
-# all but a small fraction of rays; the measured maxima per fixture (MI355X,
-# profiles/r2_parity_report.txt, "proj" = tile kernel / "grid" = sd_render_fused) are
+# SURVEY §8(c) states 1e-2 m for depth.  fp16 -- BTSNet's default precision since round 4 --
+# meets it on every fixture (measured 3.3e-3 / 4.1e-3 m below, 6.2e-3 m on the full
+# offset frame).  bf16 (BASELINE configs[1]'s dtype) cannot: the CPU emulation of the same
+# projected-grid arithmetic (tools/lowp_depth_emul.py, profiles/r4_lowp_depth_emul.txt)
+# puts the 8-bit mantissa's depth error at 1.3-3.4e-2 m, and at 1.2-3.3e-2 m even with an
+# exact sigma column -- the projected grid and the bilinear tap weights in bf16 dominate.
+# Measured maxima per fixture (MI355X, profiles/r2_parity_report.txt, "proj" = tile
+# kernel / "grid" = sd_render_fused):
 #   render_k32_cap0     bf16 proj 2.53e-2 m, grid 1.71e-2 m;  fp16 proj 3.32e-3 m
 #   render_k64_cap1     bf16 proj 4.50e-2 m, grid 2.05e-2 m;  fp16 proj 4.14e-3 m
 #   render_full_offset  bf16 proj 4.5e-2 m (offset pose, 122 880 rays)
 # so the bf16 bound is 5e-2 m for the maximum, and at most LOWP_DEPTH_FRAC_OVER of the rays
-# may exceed the contract's 1e-2 m (fp16 meets 1e-2 m everywhere).
+# may exceed the contract's 1e-2 m (fp16: none).
 LOWP_DEPTH_CONTRACT = 1e-2
 LOWP_DEPTH_FRAC_OVER = {"bf16": 5e-2, "fp16": 0.0}
 
@@ -261,6 +267,29 @@ def test_channels_last_grid_bit_equal(precision, mode):
     b = _render(d, precision, mode=mode, channels_last=True)["coarse"]
     for k in ("weights", "alphas", "depth", "rgb", "dino_features", "invalid", "invalid_features"):
         assert torch.equal(a[k], b[k]), k
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp16"])
+@pytest.mark.parametrize("B,Hf,Wf", [(2, 37, 53), (1, 192, 640), (3, 5, 7), (1, 1, 1)])
+def test_projected_grid_channels_last_streaming_bit_equal(precision, B, Hf, Wf):
+    """k_project_lds (the channels-last C = 256 projection: LDS-DMA ring of half pixel rows,
+    weights in VGPRs) writes the same P bits as k_project over the NCHW grid: the same
+    MFMAs in the same K order.  Ragged pixel counts (a partial last 32-pixel chunk, fewer
+    chunks than workgroups) and the full C2 grid."""
+    from scenedino_amd import _lib
+    from scenedino_amd.mlp_pack import PackedMLP
+    g = torch.Generator().manual_seed(13)
+    C = 256
+    grid = torch.randn(B, C, Hf, Wf, generator=g).to(DEV)
+    W_in = torch.randn(128, C + 39, generator=g) * 0.06
+    b_in = torch.randn(128, generator=g) * 0.1
+    W_out = torch.randn(65, 128, generator=g) * 0.1
+    b_out = torch.randn(65, generator=g) * 0.1
+    dt = _lib.SD_BF16 if precision == "bf16" else _lib.SD_F16
+    pk = PackedMLP(W_in.to(DEV), b_in.to(DEV), W_out.to(DEV), b_out.to(DEV), dt)
+    P_nchw = _lib.project_grid(grid.contiguous(), pk.rec, dt)
+    P_nhwc = _lib.project_grid(grid.contiguous(memory_format=torch.channels_last), pk.rec, dt)
+    assert torch.equal(P_nchw.view(torch.int16), P_nhwc.view(torch.int16))
 
 
 @pytest.mark.parametrize("precision", ["bf16", "fp16"])
