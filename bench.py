@@ -665,7 +665,12 @@ def main_train(args, world, rank, device):
     # optimizer steps the head (a frozen-encoder config; encoder backward is not ours)
     # Adam as one fused kernel over the head's parameters (torch's fused implementation, the
     # same update as the reference's Adam: base_trainer.py optimizer)
-    opt = torch.optim.Adam(head.parameters(), lr=1e-4, fused=True)
+    # graph mode (--graph, one GPU): everything after the host's patch draws -- the device
+    # sampler, forward, loss, backward, Adam -- replayed as one captured HIP graph per step,
+    # so the host only draws patches and launches the graph (round 3 measured the eager step
+    # host-paced: ~1.3 ms of issue against ~1.0 ms of GPU work)
+    graph_mode = world == 1 and args.graph
+    opt = torch.optim.Adam(head.parameters(), lr=1e-4, fused=True, capturable=graph_mode)
     amp = not args.no_amp  # train_scenedino_kitti_360.yaml: with_amp: true (fp16 autocast)
     npatch = RB // (PS * PS)
 
@@ -700,15 +705,84 @@ def main_train(args, world, rank, device):
         mark("optimizer", t0)
         return loss
 
+    eager_step = step
+
     timer = KernelTimer()
     sda.kernel_timer = timer
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    if graph_mode:
+        # the step from the device sampler on, captured twice (two pinned host slots for the
+        # drawn patches: the host fills one while the other graph's copy may still be queued).
+        # The depth jitter is drawn on the device inside the graph (torch.rand_like, as
+        # nerf.py:134 does), so every replay samples new depths; the kernel timer is off
+        # during capture (its events would be frozen into the graph).
+        sda.kernel_timer = None
+        dino_hw = tuple(dino_gt_map.shape[-2:])
+        shape = sampler.draw(images, dino_gt_map).shape
+        host_slots = [torch.empty(shape, dtype=torch.int32, pin_memory=True) for _ in range(2)]
+        dev_slots = [torch.empty(shape, dtype=torch.int32, device=device) for _ in range(2)]
+        zj = torch.empty(NB * RB, KT, device=device)
+        renderer.z_jitter = zj
+
+        def body(k):
+            dev_slots[k].copy_(host_slots[k], non_blocking=True)
+            rays, rgb_gt, dino_gt = sampler.sample_patches(dev_slots[k], images, ray_poses, Ks,
+                                                           dino_features=dino_gt_map)
+            zj.uniform_()
+            with torch.autocast("cuda", dtype=torch.float16, enabled=amp, cache_enabled=False):
+                out = wrapper(rays, want_weights=True)["coarse"]
+                pd = out["dino_features"].float().view(NB, npatch, PS * PS, D_DINO).mean(2)
+                loss = ((pd - dino_gt) ** 2).mean() + \
+                    (out["rgb"].float() - (rgb_gt * 0.5 + 0.5)).abs().mean()
+            opt.zero_grad(set_to_none=True)
+            leaf.grad = None
+            loss.backward()
+            opt.step()
+            return loss
+
+        side = torch.cuda.Stream(device=device)
+        side.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(side):  # warm-up of the captured code path (allocations, packing)
+            for i in range(3):
+                host_slots[i & 1].copy_(sampler.draw(images, dino_gt_map))
+                body(i & 1)
+        torch.cuda.current_stream(device).wait_stream(side)
+        torch.cuda.synchronize()
+        graphs, pool = [], None
+        for k in range(2):
+            host_slots[k].copy_(sampler.draw(images, dino_gt_map))
+            gph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gph, pool=pool):
+                body(k)
+            pool = gph.pool()
+            graphs.append(gph)
+        torch.cuda.synchronize()
+        done = [None, None]
+        nstep = [0]
+
+        def step():  # noqa: F811 -- the graphed steady-state step
+            t0 = time.perf_counter()
+            k = nstep[0] & 1
+            nstep[0] += 1
+            if done[k] is not None:
+                done[k].synchronize()  # graph k's copy of its host slot has run
+            host_slots[k].copy_(sampler.draw(images, dino_gt_map))
+            t0 = mark("sample", t0)
+            graphs[k].replay()
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(device))
+            done[k] = ev
+            mark("replay", t0)
+
+        for _ in range(2):
+            step()
+        torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
-    timer.on = True
+    timer.on = not graph_mode
     if host is not None:
         host.clear()  # steady state only
     t0 = time.perf_counter()
@@ -721,6 +795,16 @@ def main_train(args, world, rank, device):
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     timer.on = False
+    if graph_mode:
+        # the kernels' own durations (roofline fields) from eager steps after the timed region
+        renderer.z_jitter = None
+        sda.kernel_timer = timer
+        timer.on = True
+        for _ in range(4):
+            eager_step()
+            timer.tick()
+        torch.cuda.synchronize()
+        timer.on = False
     sda.kernel_timer = None
     if host is not None and rank == 0:
         n = args.steps
@@ -763,6 +847,8 @@ def main_train(args, world, rank, device):
         "value": world * NB * RB * args.steps / elapsed, "unit": "rays/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "step_issue": ("one captured HIP graph per step (host: patch draws + replay)"
+                       if graph_mode else "eager"),
         "dtype": "fp16 autocast MLP, fp32 gather / compositing" if amp else "fp32",
         "data": "synthetic (N(0,1) 4x256x192x640 grid, U[-1,1) images, random targets)",
         "config": {"workload": "train: 4 frames x 2048 rays (PatchRaySampler: 32 snapped 8x8 "
@@ -1015,6 +1101,9 @@ def main():
                          "encoder forward (a19); encode: ViT + DPT decoder (DINOv2Module); "
                          "train: render forward + backward (training step)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--graph", action="store_true",
+                    help="--config train: replay the step as a captured HIP graph (host: patch "
+                         "draws + one graph launch) instead of issuing it eagerly")
     ap.add_argument("--no-amp", action="store_true",
                     help="--config train: fp32 MLP instead of the reference's fp16 autocast")
     ap.add_argument("--no-fp16-line", action="store_true",

@@ -109,15 +109,29 @@ class PatchRaySampler(RaySampler):
 
     def sample(self, images, poses, projs, image_ids=None, dino_features=None,
                loss_feature_grid_shift=None):
+        patches = self.draw(images, dino_features, loss_feature_grid_shift)
+        if images.device.type != "cuda":
+            raise RuntimeError("PatchRaySampler: the device sampler needs CUDA (HIP) tensors")
+        patches = self._upload(patches, images.device)
+        return self.sample_patches(patches, images, poses, projs, image_ids, dino_features)
+
+    def draw(self, images, dino_features=None, loss_feature_grid_shift=None):
+        """The host half of ``sample``: the reference's randint draws as a (n, patches, 4)
+        int32 CPU tensor (``sample_patches`` takes them once they are on the device)."""
+        n, v, c, h, w = images.shape
+        dino_hw = tuple(dino_features.shape[-2:]) if dino_features is not None else None
+        return self._draw(n, v, h, w, dino_hw, loss_feature_grid_shift)
+
+    def sample_patches(self, patches, images, poses, projs, image_ids=None, dino_features=None):
+        """The device half of ``sample``: rays / colour (and DINO) targets of the drawn
+        patches (a device int32 tensor from ``draw``).  No host synchronisation and no
+        host-to-device copy: a training step can be captured into a HIP graph from here on
+        (the patch draws stay on the host, copied into the graph's input buffer each step)."""
         n, v, c, h, w = images.shape
         self.channels = c
         device = images.device
         psy, psx, pc = self.patch_size_y, self.patch_size_x, self._patch_count
         dino_hw = tuple(dino_features.shape[-2:]) if dino_features is not None else None
-        patches = self._draw(n, v, h, w, dino_hw, loss_feature_grid_shift)
-        if device.type != "cuda":
-            raise RuntimeError("PatchRaySampler: the device sampler needs CUDA (HIP) tensors")
-        patches = self._upload(patches, device)
         if image_ids is None:
             key = (v, str(device))
             ids = self._ids_cache.get(key)

@@ -20,7 +20,10 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 
 // torch.linspace(start, end, n)[i] in fp32 (identical on CPU and CUDA builds of
 // torch; verified against the reference's rays bit for bit, tests/golden).
-__device__ __forceinline__ float sd_linspace_at(float start, float end, int64_t n, int64_t i) {
+// I: int64_t, or int where n fits (the render kernels' K: 32-bit compare / convert); the
+// float results are the same for every n, i < 2^24
+template <typename I>
+__device__ __forceinline__ float sd_linspace_at(float start, float end, I n, I i) {
     if (n == 1) return start;
     float step = (end - start) / (float)(n - 1);
     int64_t half = n / 2;
@@ -87,7 +90,8 @@ __device__ __forceinline__ Taps sd_taps(float x, float y, int w, int h) {
 // NeRFRenderer.sample_coarse for sample k of a ray (nerf.py:121-141) given its jitter
 // uu: t = linspace(0, 1 - 1/K, K)[k] + uu / K, then lindisp / linear depth.  Every
 // operation separately rounded (bit-exact with the reference, tests/golden).
-__device__ __forceinline__ float sd_z_sample(float near, float far, int64_t K, int64_t k, float uu,
+template <typename I>
+__device__ __forceinline__ float sd_z_sample(float near, float far, I K, I k, float uu,
                                              float step, float t_end, int lindisp) {
     const float t = sd_linspace_at(0.0f, t_end, K, k) + uu * step;
     if (lindisp) {

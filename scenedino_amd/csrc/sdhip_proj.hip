@@ -170,19 +170,23 @@ k_project(const float *__restrict__ grid, int64_t B, int C, int64_t HW, int W, c
 // k_project_lds: the channels-last projection (C = 256) as a streaming kernel.  k_project
 // reads each lane's own pixel row 32 B at a time (32 pixel rows, 1 KiB apart, per wave
 // instruction) and reached ~3.3 TB/s; here the grid is swept in order by LDS-DMA of whole
-// half pixel rows (512 contiguous bytes, 128 channels) into a ring of PJ_NS slots of 32
-// rows, up to PJ_NS - 1 slots (~115 KiB) in flight per CU.  Workgroup = 4 waves, one per
-// CU; wave w owns hidden tile w (32 hidden): its 16 layer-1 A fragments (one per K step of
-// 16 channels) stay in 64 VGPRs for the whole kernel, so the LDS holds only the grid rows.
-// Per 32-pixel chunk: slot 2k = channels 0..127, slot 2k + 1 = channels 128..255; every wave
-// reads a slot's rows as the MFMA B operand (lane (pixel n, half h): 8 channels, 32 B),
-// converts them to the 16-bit type and issues 8 32x32x16 MFMAs -- the same products in
-// the same order as k_project, so P is bit-identical.  The 32 x 128 output tile goes
+// pixel rows (1 KiB = one 64-lane DMA instruction) into a ring of PJ_NS slots of 16 rows,
+// up to 6 slots (~96 KiB) in flight per CU.  Workgroup = 4 waves, one per CU; wave w owns
+// hidden tile w (32 hidden): its 16 layer-1 A fragments (one per K step of 16 channels)
+// stay in 64 VGPRs for the whole kernel, so the LDS holds only the grid rows.  Per
+// 32-pixel chunk (slots 2k, 2k + 1) every wave reads the rows as the MFMA B operand
+// (lane (pixel n, half h): 8 channels, 32 B), converts them to the 16-bit type and issues
+// 16 32x32x16 MFMAs -- the same products in the same order as k_project, so P is
+// bit-identical.  (PJ_FULLROW=0: the round-4 first version, half rows per slot.)  The 32 x 128 output tile goes
 // through an LDS staging area and leaves as 16-B stores of whole 256-B pixel rows.
 // ---------------------------------------------------------------------------
-#define PJ_NS 8                    // ring slots (half-chunks)
-#define PJ_ROWB 528                // LDS bytes per staged half row: 512 + 16 pad (conflict-free reads)
-#define PJ_SLOT (32 * PJ_ROWB)
+#ifndef PJ_FULLROW
+#define PJ_FULLROW 1               // 1: slots of 16 whole pixel rows (1-KiB DMAs); 0: half rows
+#endif
+#define PJ_NS 8                    // ring slots
+#define PJ_ROWB (PJ_FULLROW ? 1040 : 528)  // LDS bytes per staged row: data + 16 B pad (conflict-free reads)
+#define PJ_SROWS (PJ_FULLROW ? 16 : 32)    // pixel rows per slot
+#define PJ_SLOT (PJ_SROWS * PJ_ROWB)
 #define PJ_OUTROW 272              // staging row stride (256 B of P + 16 pad)
 #define PJ_LDS (PJ_NS * PJ_SLOT + 32 * PJ_OUTROW)
 
@@ -214,9 +218,70 @@ k_project_lds(const float *__restrict__ grid, int64_t npix, const sd_mlp m, uint
             for (int i = 0; i < 4; ++i) bias[4 * q4 + i] = v[i];
         }
     }
+    uint8_t *stg = lds + PJ_NS * PJ_SLOT;
+    f32x16 acc = bias;
+    // 32 x 128 accumulator tile of chunk k -> staging rows -> 16-B stores of whole pixel rows
+    auto store_chunk = [&](int k) {
+        // accumulator rows 4 r4 .. 4 r4 + 3 = hidden 32 wave + 8 r4 + 4 h + 0..3 of pixel li
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4)
+            *(uint2 *)(stg + li * PJ_OUTROW + 2 * (32 * wave + 8 * r4 + 4 * h)) =
+                uint2{sd_pack2<E>(acc[4 * r4], acc[4 * r4 + 1]),
+                      sd_pack2<E>(acc[4 * r4 + 2], acc[4 * r4 + 3])};
+        acc = bias;
+        __syncthreads();  // the 32 x 128 tile is complete in the staging rows
+        const int64_t pix0 = ((int64_t)blockIdx.x + (int64_t)k * gridDim.x) * 32;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int pp = 8 * wave + 4 * kk + (lane >> 4);
+            const uint4 v = *(const uint4 *)(stg + pp * PJ_OUTROW + 16 * (lane & 15));
+            if (pix0 + pp < npix)
+                *(uint4 *)(out + (pix0 + pp) * (SD_DH / 2) + 4 * (lane & 15)) = v;
+        }
+    };
+#if PJ_FULLROW
+    // slot i = rows 16 (i & 1) .. + 15 of chunk i >> 1, whole 1-KiB pixel rows: this wave
+    // DMAs rows 4 wave .. 4 wave + 3.  Slots past the workgroup's last chunk re-read the last
+    // pixel (every chunk issues the same number of vector-memory operations).
+    auto issue = [&](int i) {
+        const int64_t c = (int64_t)blockIdx.x + (int64_t)(i >> 1) * gridDim.x;
+        const uint32_t sb = lds0 + (uint32_t)(i % PJ_NS) * PJ_SLOT;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int row = 4 * wave + r;
+            int64_t pix = c * 32 + 16 * (i & 1) + row;
+            pix = pix < npix ? pix : npix - 1;
+            sd_dma16(grid + pix * 256 + 4 * lane, sb + (uint32_t)row * PJ_ROWB);
+        }
+    };
+#pragma unroll
+    for (int i = 0; i < PJ_NS - 2; ++i) issue(i);
+    for (int k = 0; k < my; ++k) {
+        // slots 2k, 2k + 1 landed: this wave's DMAs of slots 2k + 2 .. 2k + PJ_NS - 3 (4 each,
+        // + any stores) are younger
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        static_assert(4 * (PJ_NS - 4) == 16, "vmcnt immediate");
+        __syncthreads();  // every wave's rows landed; chunk k - 1's slots are free
+        issue(2 * k + PJ_NS - 2);
+        issue(2 * k + PJ_NS - 1);
+        // lane (pixel li, half h): slot 2k + (li >> 4), row li & 15, channels 16 q + 8 h ..
+        const uint8_t *sl = lds + ((2 * k + (li >> 4)) % PJ_NS) * PJ_SLOT + (li & 15) * PJ_ROWB + 32 * h;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const f32x4 a = *(const f32x4 *)(sl + 64 * q), b = *(const f32x4 *)(sl + 64 * q + 16);
+            Frag f;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                f[e] = (E)a[e];
+                f[4 + e] = (E)b[e];
+            }
+            acc = Tr::mma32(W[q], f, acc);
+        }
+        store_chunk(k);
+    }
+#else
     // slot i = (chunk i >> 1, half i & 1): this wave DMAs rows 8 wave .. 8 wave + 7, 512 B each
-    // (lanes 0..31).  Slots past the workgroup's last chunk re-read the last pixel (kept so
-    // that every iteration issues the same number of vector-memory operations).
+    // (lanes 0..31)
     auto issue = [&](int i) {
         const int64_t c = (int64_t)blockIdx.x + (int64_t)(i >> 1) * gridDim.x;
         const uint32_t sb = lds0 + (uint32_t)(i % PJ_NS) * PJ_SLOT;
@@ -226,24 +291,17 @@ k_project_lds(const float *__restrict__ grid, int64_t npix, const sd_mlp m, uint
                 const int row = 8 * wave + r;
                 int64_t pix = c * 32 + row;
                 pix = pix < npix ? pix : npix - 1;
-                const float *src = grid + pix * 256 + (i & 1) * 128 + 4 * lane;
-                sd_dma16(src, sb + (uint32_t)row * PJ_ROWB);
+                sd_dma16(grid + pix * 256 + (i & 1) * 128 + 4 * lane, sb + (uint32_t)row * PJ_ROWB);
             }
         }
     };
 #pragma unroll
     for (int i = 0; i < PJ_NS - 1; ++i) issue(i);
-
-    f32x16 acc = bias;
-    uint8_t *stg = lds + PJ_NS * PJ_SLOT;
-    // one half-chunk: wait for slot i, refill the ring, 8 K steps (A fragments W[8 HALF + q]:
-    // compile-time indices, so the 16 fragments stay in VGPRs)
     auto half_step = [&](int i, auto half_c) {
         constexpr int HALF = decltype(half_c)::value;
-        // this wave's rows of slot i landed: 8 (PJ_NS - 2) of its DMAs (+ any stores) are younger
         asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
         static_assert(8 * (PJ_NS - 2) == 48, "vmcnt immediate");
-        __syncthreads();  // every wave's rows landed; slot i - 1 is free (all waves past it)
+        __syncthreads();
         issue(i + PJ_NS - 1);
         const uint8_t *sl = lds + (i % PJ_NS) * PJ_SLOT + li * PJ_ROWB + 32 * h;
 #pragma unroll
@@ -261,23 +319,9 @@ k_project_lds(const float *__restrict__ grid, int64_t npix, const sd_mlp m, uint
     for (int k = 0; k < my; ++k) {
         half_step(2 * k, std::integral_constant<int, 0>());
         half_step(2 * k + 1, std::integral_constant<int, 1>());
-        // accumulator rows 4 r4 .. 4 r4 + 3 = hidden 32 wave + 8 r4 + 4 h + 0..3 of pixel li
-#pragma unroll
-        for (int r4 = 0; r4 < 4; ++r4)
-            *(uint2 *)(stg + li * PJ_OUTROW + 2 * (32 * wave + 8 * r4 + 4 * h)) =
-                uint2{sd_pack2<E>(acc[4 * r4], acc[4 * r4 + 1]),
-                      sd_pack2<E>(acc[4 * r4 + 2], acc[4 * r4 + 3])};
-        acc = bias;
-        __syncthreads();  // the 32 x 128 tile is complete in the staging rows
-        const int64_t pix0 = ((int64_t)blockIdx.x + (int64_t)k * gridDim.x) * 32;
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-            const int pp = 8 * wave + 4 * kk + (lane >> 4);
-            const uint4 v = *(const uint4 *)(stg + pp * PJ_OUTROW + 16 * (lane & 15));
-            if (pix0 + pp < npix)
-                *(uint4 *)(out + (pix0 + pp) * (SD_DH / 2) + 4 * (lane & 15)) = v;
-        }
+        store_chunk(k);
     }
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the workgroup
 }
 

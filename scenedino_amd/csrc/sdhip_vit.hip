@@ -58,6 +58,30 @@ __device__ __forceinline__ f32x16 vt_zero16() {
 #ifndef VT_MF16
 #define VT_MF16 0
 #endif
+// VT_RING = 1: the K loop's A / W tiles go global -> LDS by LDS-DMA (buffer_load ... lds,
+// per-lane source offsets) into a ring of vt_ring_stages() stages, so several K steps are in
+// flight at once and a step waits for its own tile only (the register-staging loop of
+// round 3 hid at most one step of load latency: the small ViT / DPT GEMMs of a 481-token
+// or 12x40..48x160 frame are latency-bound).  The tiles sit unpadded in LDS with their
+// 16-B chunks XOR-swizzled per row (vt_swz), which keeps the fragment reads conflict-free.
+#ifndef VT_RING
+#define VT_RING 0  // (off until A/B-measured on the GPU: tools/build_variant.py ring -DVT_RING=1)
+#endif
+__host__ __device__ constexpr int vt_ring_stages(int BM, int BN) { return BM >= 128 || BN >= 128 ? 3 : 4; }
+template <int BM, int BN, int BK>
+__host__ __device__ constexpr int vt_ring_bytes() { return vt_ring_stages(BM, BN) * (BM + BN) * BK * 2; }
+// chunk slot of 16-B chunk kc of tile row `row` (CPR chunks per row): rows sharing 256 B of
+// LDS use disjoint chunk sets, 16 consecutive rows cover the 64 banks once
+template <int CPR>
+__device__ __forceinline__ int vt_swz(int row, int kc) {
+    return kc ^ ((row / (16 / CPR)) & (CPR - 1));
+}
+__device__ __forceinline__ void vt_dma16(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff,
+                                         uint32_t lds_addr) {
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %3 offen lds"
+                 :: "v"(voff), "s"(rs), "s"(lds_addr), "s"(soff) : "memory");
+}
+
 __device__ __forceinline__ int vt_row(int q, int lane) {
     return VT_MF16 ? 16 * (q >> 3) + 4 * ((lane >> 4) & 3) + (q & 3) : (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5);
 }
@@ -122,7 +146,12 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
     constexpr int OST = EPI == SD_EPI_NCHW ? BN + 1 : BN + 8;  // fp32 words per staged row
     constexpr int KL_BYTES = 2 * (BM + BN) * GLDS * 2;
     constexpr int EP_BYTES = STAGED ? BM * OST * 4 : 0;
+    constexpr bool RING = VT_RING && !VT_MF16;
+#if VT_RING && !VT_MF16
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];  // vt_ring_bytes + epilogue
+#else
     __shared__ __attribute__((aligned(16))) uint8_t smem[KL_BYTES > EP_BYTES ? KL_BYTES : EP_BYTES];
+#endif
 #define SA(buf) ((__bf16 *)smem + (buf) * (BM * GLDS))
 #define SB(buf) ((__bf16 *)smem + 2 * BM * GLDS + (buf) * (BN * GLDS))
 
@@ -277,6 +306,101 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
         }
     };
 
+    if constexpr (RING) {
+        // ---- LDS-DMA ring: stage kt of the K loop in slot kt % RS ----------------------
+        constexpr int RS = vt_ring_stages(BM, BN);
+        constexpr int STB = (BM + BN) * BK * 2;  // bytes per stage: A tile, then W tile
+        const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void *)smem;
+        // this thread's chunks: DMA instruction i of the wave (64 consecutive 16-B slots);
+        // slot -> (row, swizzled chunk) -> source chunk
+        uint32_t dA[CA], dB[CB];
+#pragma unroll
+        for (int c = 0; c < CA; ++c) {
+            const int slot = (c * 4 + wave) * 64 + lane, row = slot / CPR;
+            const int kc = vt_swz<CPR>(row, slot % CPR);  // the source chunk this slot holds
+            if (CONV) voA[c] = (uint32_t)(kc * 8);
+            else voA[c] = (uint32_t)(((int64_t)min(m0 + row, g.M - 1) * g.lda + kc * 8) * 2);
+            if (CONV) {
+                const int64_t m = min(m0 + row, g.M - 1);
+                const int ohw = g.OH * g.OW;
+                const int b = (int)((uint32_t)m / (uint32_t)ohw);
+                const int p = (int)(m - (int64_t)b * ohw);
+                const int oy = p / g.OW, ox = p - oy * g.OW;
+                cpix[c] = b * g.H * g.W;
+                ciy[c] = oy * g.stride - 1;
+                cix[c] = ox * g.stride - 1;
+            }
+            dA[c] = (uint32_t)(c * 4 + wave) * 1024u;
+        }
+#pragma unroll
+        for (int c = 0; c < CB; ++c) {
+            const int slot = (c * 4 + wave) * 64 + lane, row = slot / CPR;
+            const int kc = vt_swz<CPR>(row, slot % CPR);
+            voB[c] = (uint32_t)((min(n0 + row, g.N - 1) * g.K + kc * 8) * 2);
+            dB[c] = (uint32_t)(BM * BK * 2) + (uint32_t)(c * 4 + wave) * 1024u;
+        }
+        // issue stage kt (steps past the last re-load step nk - 1 into their free slot, so
+        // that every step issues CA + CB DMAs and the vmcnt count below is exact)
+        auto issue = [&](int kt) {
+            const int k = min(kt, nk - 1);
+            const uint32_t st = lds0 + (uint32_t)(kt % RS) * STB;
+            if (CONV) {
+                const int k0 = k * BK;
+                const int tap = k0 / g.Cin, ci0 = k0 - tap * g.Cin;
+                const int ky = tap / 3, kx = tap - 3 * (tap / 3);
+#pragma unroll
+                for (int c = 0; c < CA; ++c) {
+                    const int iy = ciy[c] + ky, ix = cix[c] + kx;
+                    const bool ok = (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
+                    const uint32_t off =
+                        ok ? (uint32_t)(((cpix[c] + iy * g.W + ix) * g.Cin + ci0) * 2) + voA[c] * 2
+                           : 0x80000000u;  // past the buffer: the DMA writes zeros (padding)
+                    vt_dma16(rsA, off, 0u, __builtin_amdgcn_readfirstlane(st + dA[c]));
+                }
+            } else {
+#pragma unroll
+                for (int c = 0; c < CA; ++c)
+                    vt_dma16(rsA, voA[c], (uint32_t)k * BK * 2, __builtin_amdgcn_readfirstlane(st + dA[c]));
+            }
+#pragma unroll
+            for (int c = 0; c < CB; ++c)
+                vt_dma16(rsB, voB[c], (uint32_t)k * BK * 2, __builtin_amdgcn_readfirstlane(st + dB[c]));
+        };
+#pragma unroll
+        for (int i = 0; i < RS - 1; ++i) issue(i);
+        for (int kt = 0; kt < nk; ++kt) {
+            // stage kt landed: this thread's DMAs of stages kt + 1 .. kt + RS - 2 are younger
+            static_assert((RS - 2) * (CA + CB) <= 63, "vmcnt range");
+            asm volatile("s_waitcnt vmcnt(%0)" :: "i"((RS - 2) * (CA + CB)) : "memory");
+            __syncthreads();  // every thread's chunks of stage kt landed; slot (kt - 1) % RS free
+            issue(kt + RS - 1);
+            const __bf16 *sa = (const __bf16 *)(smem + (kt % RS) * STB);
+            const __bf16 *sb = sa + BM * BK;
+#pragma unroll
+            for (int s0 = 0; s0 < (SK ? BK / 64 : BK / 16); ++s0) {
+                const int s = SK ? 4 * s0 + wave : s0;
+                const int kc = 2 * s + h;  // 16-B chunk of the lane's k-range
+                bf16x8 af[TM], bfr[TN];
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    const int row = wm * WM + i * 32 + r;
+                    af[i] = *(const bf16x8 *)&sa[row * BK + 8 * vt_swz<CPR>(row, kc)];
+                    if (CONV && g.relu_in) af[i] = vt_relu8(af[i]);
+                }
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const int row = wn * WN + j * 32 + r;
+                    bfr[j] = *(const bf16x8 *)&sb[row * BK + 8 * vt_swz<CPR>(row, kc)];
+                }
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) acc[i][j] = VT_MFMA(af[i], bfr[j], acc[i][j]);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dummy stages' DMAs
+        __syncthreads();  // every wave is done with the ring: the epilogue reuses the LDS
+    } else {
     // prologue: set i <- step i (i < NS), step 0 to LDS, set 0 <- step NS.  Loads past the
     // last step re-load step nk - 1 (unconditional: a load issued on one path only makes the
     // compiler's vmcnt model wait for the newest loads as well)
@@ -297,6 +421,7 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
                 __syncthreads();
             }
         }
+    }
     }
 
     if constexpr (SK) {
@@ -1221,15 +1346,23 @@ __global__ void __launch_bounds__(256) k_lngemm(sd_gemm_args g, const float *__r
 template <int BM, int BN, int BK, bool CONV>
 static void vt_launch_gemm(const sd_gemm_args &g, hipStream_t s) {
     dim3 grid((unsigned)((g.N + BN - 1) / BN), (unsigned)((g.M + BM - 1) / BM));
+    // the ring kernels take their LDS dynamically (the ring, reused by the epilogue: > 64 KiB
+    // for the 128 x 128 tiles)
+    constexpr int ep = BM * (BN + 8) * 4;  // the widest staged epilogue tile (k_gemm's OST)
+    const int lds = (VT_RING && !VT_MF16) ? (vt_ring_bytes<BM, BN, BK>() > ep ? vt_ring_bytes<BM, BN, BK>() : ep) : 0;
+    auto go = [&](auto kern) {
+        if (lds) (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, g);
+    };
     switch (g.epi) {
-    case SD_EPI_BF16: hipLaunchKernelGGL((k_gemm<BM, BN, BK, SD_EPI_BF16, CONV>), grid, dim3(256), 0, s, g); break;
-    case SD_EPI_GELU: hipLaunchKernelGGL((k_gemm<BM, BN, BK, SD_EPI_GELU, CONV>), grid, dim3(256), 0, s, g); break;
-    case SD_EPI_F32: hipLaunchKernelGGL((k_gemm<BM, BN, BK, SD_EPI_F32, CONV>), grid, dim3(256), 0, s, g); break;
-    case SD_EPI_RESID: hipLaunchKernelGGL((k_gemm<BM, BN, BK, SD_EPI_RESID, CONV>), grid, dim3(256), 0, s, g); break;
-    case SD_EPI_QKV: hipLaunchKernelGGL((k_gemm<BM, BN, BK, SD_EPI_QKV, CONV>), grid, dim3(256), 0, s, g); break;
-    case SD_EPI_SHUF: hipLaunchKernelGGL((k_gemm<BM, BN, BK, SD_EPI_SHUF, CONV>), grid, dim3(256), 0, s, g); break;
-    case SD_EPI_NCHW: hipLaunchKernelGGL((k_gemm<BM, BN, BK, SD_EPI_NCHW, CONV>), grid, dim3(256), 0, s, g); break;
-    default: hipLaunchKernelGGL((k_gemm<BM, BN, BK, SD_EPI_PATCH, CONV>), grid, dim3(256), 0, s, g); break;
+    case SD_EPI_BF16: go(k_gemm<BM, BN, BK, SD_EPI_BF16, CONV>); break;
+    case SD_EPI_GELU: go(k_gemm<BM, BN, BK, SD_EPI_GELU, CONV>); break;
+    case SD_EPI_F32: go(k_gemm<BM, BN, BK, SD_EPI_F32, CONV>); break;
+    case SD_EPI_RESID: go(k_gemm<BM, BN, BK, SD_EPI_RESID, CONV>); break;
+    case SD_EPI_QKV: go(k_gemm<BM, BN, BK, SD_EPI_QKV, CONV>); break;
+    case SD_EPI_SHUF: go(k_gemm<BM, BN, BK, SD_EPI_SHUF, CONV>); break;
+    case SD_EPI_NCHW: go(k_gemm<BM, BN, BK, SD_EPI_NCHW, CONV>); break;
+    default: go(k_gemm<BM, BN, BK, SD_EPI_PATCH, CONV>); break;
     }
 }
 

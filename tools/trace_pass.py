@@ -27,3 +27,7 @@ for i, (n, s, e, gx, wx) in enumerate(seg):
 print(f"pass: {len(seg)} kernels, wall {(seg[-1][2] - t0) / 1e3:.1f} us, kernel sum {tot_k:.1f} us")
 for k, (cnt, d, g) in sorted(agg.items(), key=lambda x: -x[1][1]):
     print(f"{k:60s} x{cnt:3d}  {d:8.1f} us  avg {d / cnt:6.2f}  gaps before {g:7.1f} us")
+if "--list" in sys.argv:  # every launch of the pass in order: duration, gap before, grid
+    for i, (n, s, e, gx, wx) in enumerate(seg):
+        gap = (s - seg[i - 1][2]) / 1e3 if i else 0.0
+        print(f"{i:3d} {n.split('(')[0][:58]:58s} {(e - s) / 1e3:7.2f} us  gap {gap:6.2f}  grid {gx // max(wx, 1)} x {wx}")
