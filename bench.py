@@ -709,8 +709,9 @@ def main_train(args, world, rank, device):
 
     timer = KernelTimer()
     sda.kernel_timer = timer
-    for _ in range(args.warmup):
-        step()
+    if not graph_mode:  # (graph mode warms up on the capture's side stream below)
+        for _ in range(args.warmup):
+            step()
     torch.cuda.synchronize()
     if graph_mode:
         # the step from the device sampler on, captured twice (two pinned host slots for the
@@ -727,7 +728,6 @@ def main_train(args, world, rank, device):
         renderer.z_jitter = zj
 
         def body(k):
-            dev_slots[k].copy_(host_slots[k], non_blocking=True)
             rays, rgb_gt, dino_gt = sampler.sample_patches(dev_slots[k], images, ray_poses, Ks,
                                                            dino_features=dino_gt_map)
             zj.uniform_()
@@ -745,14 +745,15 @@ def main_train(args, world, rank, device):
         side = torch.cuda.Stream(device=device)
         side.wait_stream(torch.cuda.current_stream(device))
         with torch.cuda.stream(side):  # warm-up of the captured code path (allocations, packing)
-            for i in range(3):
+            for i in range(max(3, args.warmup)):
                 host_slots[i & 1].copy_(sampler.draw(images, dino_gt_map))
+                dev_slots[i & 1].copy_(host_slots[i & 1], non_blocking=True)
                 body(i & 1)
+                torch.cuda.current_stream(device).synchronize()
         torch.cuda.current_stream(device).wait_stream(side)
         torch.cuda.synchronize()
         graphs, pool = [], None
         for k in range(2):
-            host_slots[k].copy_(sampler.draw(images, dino_gt_map))
             gph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(gph, pool=pool):
                 body(k)
@@ -767,9 +768,10 @@ def main_train(args, world, rank, device):
             k = nstep[0] & 1
             nstep[0] += 1
             if done[k] is not None:
-                done[k].synchronize()  # graph k's copy of its host slot has run
+                done[k].synchronize()  # the copy out of host slot k two steps ago has run
             host_slots[k].copy_(sampler.draw(images, dino_gt_map))
             t0 = mark("sample", t0)
+            dev_slots[k].copy_(host_slots[k], non_blocking=True)  # into the graph's input slot
             graphs[k].replay()
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(device))
@@ -796,13 +798,16 @@ def main_train(args, world, rank, device):
     elapsed = time.perf_counter() - t0
     timer.on = False
     if graph_mode:
-        # the kernels' own durations (roofline fields) from eager steps after the timed region
+        # the kernels' own durations (roofline fields) from eager steps after the timed region,
+        # on the side stream the captured step's autograd state lives on
         renderer.z_jitter = None
         sda.kernel_timer = timer
         timer.on = True
-        for _ in range(4):
-            eager_step()
-            timer.tick()
+        side.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(side):
+            for _ in range(4):
+                eager_step()
+                timer.tick()
         torch.cuda.synchronize()
         timer.on = False
     sda.kernel_timer = None

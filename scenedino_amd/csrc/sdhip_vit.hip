@@ -68,6 +68,14 @@ __device__ __forceinline__ f32x16 vt_zero16() {
 #define VT_RING 0  // (off until A/B-measured on the GPU: tools/build_variant.py ring -DVT_RING=1)
 #endif
 __host__ __device__ constexpr int vt_ring_stages(int BM, int BN) { return BM >= 128 || BN >= 128 ? 3 : 4; }
+// which tiles take the ring: the 32 x 32 split-K tiles of the small-M GEMMs (ViT-S/16 and
+// DINOv2-B/14 at 481 tokens, the DPT's 12x40 / 24x80 convolutions).  VT_RING_ALL = 1 puts
+// every tile on it (the 64 x 64 and 128 x 128 tiles measured slower: one 96-KiB ring per CU
+// halves their occupancy -- ViT-B/8 + DPT 3.46 -> 4.13 ms)
+#ifndef VT_RING_ALL
+#define VT_RING_ALL 0
+#endif
+__host__ __device__ constexpr bool vt_ring_tile(int BM) { return VT_RING && !VT_MF16 && (BM == 32 || VT_RING_ALL); }
 template <int BM, int BN, int BK>
 __host__ __device__ constexpr int vt_ring_bytes() { return vt_ring_stages(BM, BN) * (BM + BN) * BK * 2; }
 // chunk slot of 16-B chunk kc of tile row `row` (CPR chunks per row): rows sharing 256 B of
@@ -146,12 +154,12 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
     constexpr int OST = EPI == SD_EPI_NCHW ? BN + 1 : BN + 8;  // fp32 words per staged row
     constexpr int KL_BYTES = 2 * (BM + BN) * GLDS * 2;
     constexpr int EP_BYTES = STAGED ? BM * OST * 4 : 0;
-    constexpr bool RING = VT_RING && !VT_MF16;
-#if VT_RING && !VT_MF16
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];  // vt_ring_bytes + epilogue
-#else
-    __shared__ __attribute__((aligned(16))) uint8_t smem[KL_BYTES > EP_BYTES ? KL_BYTES : EP_BYTES];
-#endif
+    constexpr bool RING = vt_ring_tile(BM);
+    // the ring kernels take their LDS dynamically (vt_launch_gemm sizes it), the others a
+    // static operand double buffer
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem_dyn[];
+    __shared__ __attribute__((aligned(16))) uint8_t smem_st[RING ? 16 : (KL_BYTES > EP_BYTES ? KL_BYTES : EP_BYTES)];
+    uint8_t *const smem = RING ? smem_dyn : smem_st;
 #define SA(buf) ((__bf16 *)smem + (buf) * (BM * GLDS))
 #define SB(buf) ((__bf16 *)smem + 2 * BM * GLDS + (buf) * (BN * GLDS))
 
@@ -1349,7 +1357,7 @@ static void vt_launch_gemm(const sd_gemm_args &g, hipStream_t s) {
     // the ring kernels take their LDS dynamically (the ring, reused by the epilogue: > 64 KiB
     // for the 128 x 128 tiles)
     constexpr int ep = BM * (BN + 8) * 4;  // the widest staged epilogue tile (k_gemm's OST)
-    const int lds = (VT_RING && !VT_MF16) ? (vt_ring_bytes<BM, BN, BK>() > ep ? vt_ring_bytes<BM, BN, BK>() : ep) : 0;
+    const int lds = vt_ring_tile(BM) ? (vt_ring_bytes<BM, BN, BK>() > ep ? vt_ring_bytes<BM, BN, BK>() : ep) : 0;
     auto go = [&](auto kern) {
         if (lds) (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, g);

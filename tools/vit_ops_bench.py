@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Diagnostic: the ViT block's kernels at 481 tokens one by one (ViT-S/16: C 384, 6 heads;
-DINOv2-B/14: C 768, 12 heads), microseconds per call (HIP events over 50 back-to-back
-calls, random operands).  SDHIP_LIB selects a variant build."""
+DINOv2-B/14: C 768, 12 heads), microseconds per call (HIP events around graph replays of 20
+back-to-back calls, random operands).  SDHIP_LIB selects a variant build."""
 import json
 import os
 import sys
@@ -19,16 +19,28 @@ def rnd(*s):
     return (torch.rand(*s, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
 
 
-def timeit(fn, n=50):
-    fn()
+def timeit(fn, n=20):
+    """Device time per call: n calls captured in one HIP graph, replayed 5 times (eager
+    ctypes calls from Python are host-bound at ~8 us each)."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fn()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    gph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gph):
+        for _ in range(n):
+            fn()
+    gph.replay()
     torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
-    for _ in range(n):
-        fn()
+    for _ in range(5):
+        gph.replay()
     b.record()
     torch.cuda.synchronize()
-    return round(a.elapsed_time(b) * 1e3 / n, 2)
+    return round(a.elapsed_time(b) * 1e3 / (5 * n), 2)
 
 
 _lib.load()
