@@ -13,7 +13,7 @@ from concurrent.futures import ThreadPoolExecutor
 HERE = os.path.dirname(os.path.abspath(__file__))
 SOURCES = ["csrc/sdhip_rays.hip", "csrc/sdhip_field.hip", "csrc/sdhip_proj.hip", "csrc/sdhip_tile.hip",
            "csrc/sdhip_seg.hip", "csrc/sdhip_ssc.hip", "csrc/sdhip_vit.hip", "csrc/sdhip_train.hip",
-           "csrc/sdhip_down.hip", "csrc/sdhip_mlp.hip"]
+           "csrc/sdhip_down.hip", "csrc/sdhip_mlp.hip", "csrc/sdhip_conv.hip"]
 HEADERS = ["csrc/sdhip_common.h", "csrc/sdhip_point.h", "csrc/sdhip_render.h", "../include/sdhip.h"]
 OUT = os.path.join(HERE, "libsdhip.so")
 OBJ_DIR = os.path.join(HERE, "_obj")

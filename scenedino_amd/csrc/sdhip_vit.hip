@@ -27,9 +27,12 @@
 #include "sdhip_point.h"
 
 extern "C" void sd_set_error(const char *msg);
+int sd_conv_big_try(const sd_gemm_args *args, void *stream);  // sdhip_conv.hip
 
 typedef __attribute__((ext_vector_type(4))) float vf4;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+typedef __attribute__((ext_vector_type(2))) float f32x2;
 
 #define VT_MFMA(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_bf16((a), (b), (c), 0, 0, 0)
 
@@ -65,7 +68,7 @@ __device__ __forceinline__ f32x16 vt_zero16() {
 // or 12x40..48x160 frame are latency-bound).  The tiles sit unpadded in LDS with their
 // 16-B chunks XOR-swizzled per row (vt_swz), which keeps the fragment reads conflict-free.
 #ifndef VT_RING
-#define VT_RING 0  // (off until A/B-measured on the GPU: tools/build_variant.py ring -DVT_RING=1)
+#define VT_RING 1  // round 4 A/B (graph-replayed passes, 2 reps): ViT-S/16 0.615 -> 0.599 ms, encode 1.30 -> 1.276
 #endif
 __host__ __device__ constexpr int vt_ring_stages(int BM, int BN) { return BM >= 128 || BN >= 128 ? 3 : 4; }
 // which tiles take the ring: the 32 x 32 split-K tiles of the small-M GEMMs (ViT-S/16 and
@@ -1027,7 +1030,8 @@ __global__ void __launch_bounds__(256) k_layernorm(const float *__restrict__ x, 
         v[i] = c < C ? *(const vf4 *)(xr + c) : vf4{0.f, 0.f, 0.f, 0.f};
         s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
     }
-    const float mean = vt_wave_sum(s) / (float)C;
+    const float inv_c = 1.f / (float)C;
+    const float mean = vt_wave_sum(s) * inv_c;
     float q = 0.f;
 #pragma unroll
     for (int i = 0; i < PER4; ++i) {
@@ -1040,7 +1044,7 @@ __global__ void __launch_bounds__(256) k_layernorm(const float *__restrict__ x, 
             }
         }
     }
-    const float rstd = 1.f / sqrtf(vt_wave_sum(q) / (float)C + eps);
+    const float rstd = __builtin_amdgcn_rsqf(vt_wave_sum(q) * inv_c + eps);
 #pragma unroll
     for (int i = 0; i < PER4; ++i) {
         const int c = 4 * lane + 256 * i;
@@ -1227,50 +1231,57 @@ __global__ void __launch_bounds__(256) k_lngemm(sd_gemm_args g, const float *__r
     // all their loads issued first (one memory latency per batch, the reductions of the
     // batch's rows interleaved)
     constexpr int RB = PER <= 6 ? 8 : 4;
+    // lane = column pairs 2 lane + 128 i: 8-B loads, packed f32 math (v_pk_*), one packed
+    // bf16 pair per LDS write
+    constexpr int P2 = PER / 2;
+    f32x2 lwv[P2], lbv[P2];
+#pragma unroll
+    for (int i = 0; i < P2; ++i) {
+        lwv[i] = *(const f32x2 *)(lw + 2 * lane + 128 * i);
+        lbv[i] = *(const f32x2 *)(lb + 2 * lane + 128 * i);
+    }
 #pragma unroll
     for (int r0 = 0; r0 < 8; r0 += RB) {
-        float v[RB][PER];
+        f32x2 v[RB][P2];
 #pragma unroll
         for (int rr = 0; rr < RB; ++rr) {
             const float *xr = x + min(m0 + 8 * wave + r0 + rr, g.M - 1) * C;
 #pragma unroll
-            for (int i = 0; i < PER; ++i) v[rr][i] = xr[lane + 64 * i];
+            for (int i = 0; i < P2; ++i) v[rr][i] = *(const f32x2 *)(xr + 2 * lane + 128 * i);
         }
+        // the row statistics by vt_wave_sum (DPP + readlane: no LDS round trip per level,
+        // unlike a __shfl_xor butterfly), the divisions by C as multiplications by 1 / C
+        constexpr float INV_C = 1.f / (float)C;
         float mean[RB], rstd[RB];
 #pragma unroll
         for (int rr = 0; rr < RB; ++rr) {
-            float sum = 0.f;
+            f32x2 s2 = v[rr][0];
 #pragma unroll
-            for (int i = 0; i < PER; ++i) sum += v[rr][i];
-            mean[rr] = sum;
+            for (int i = 1; i < P2; ++i) s2 += v[rr][i];
+            mean[rr] = vt_wave_sum(s2.x + s2.y) * INV_C;
         }
 #pragma unroll
-        for (int off = 32; off >= 1; off >>= 1)
-#pragma unroll
-            for (int rr = 0; rr < RB; ++rr) mean[rr] += __shfl_xor(mean[rr], off);
-#pragma unroll
         for (int rr = 0; rr < RB; ++rr) {
-            mean[rr] = mean[rr] / (float)C;
-            float q = 0.f;
+            const f32x2 mu = {mean[rr], mean[rr]};
+            f32x2 q2 = {0.f, 0.f};
 #pragma unroll
-            for (int i = 0; i < PER; ++i) {
-                const float d = v[rr][i] - mean[rr];
-                q = fmaf(d, d, q);
+            for (int i = 0; i < P2; ++i) {
+                v[rr][i] -= mu;  // centred in place (the output reuses it)
+                q2 = __builtin_elementwise_fma(v[rr][i], v[rr][i], q2);
             }
-            rstd[rr] = q;
+            rstd[rr] = __builtin_amdgcn_rsqf(vt_wave_sum(q2.x + q2.y) * INV_C + eps);
         }
 #pragma unroll
-        for (int off = 32; off >= 1; off >>= 1)
-#pragma unroll
-            for (int rr = 0; rr < RB; ++rr) rstd[rr] += __shfl_xor(rstd[rr], off);
-#pragma unroll
         for (int rr = 0; rr < RB; ++rr) {
-            const float rs = 1.f / sqrtf(rstd[rr] / (float)C + eps);
             const int rl = 8 * wave + r0 + rr;
+            const f32x2 rs = {rstd[rr], rstd[rr]};
 #pragma unroll
-            for (int i = 0; i < PER; ++i) {
-                const int c = lane + 64 * i;
-                sA[rl * LDA + c] = (__bf16)((v[rr][i] - mean[rr]) * rs * lw[c] + lb[c]);
+            for (int i = 0; i < P2; ++i) {
+                const f32x2 y = __builtin_elementwise_fma(v[rr][i] * rs, lwv[i], lbv[i]);
+                bf16x2 o;
+                o[0] = (__bf16)y.x;
+                o[1] = (__bf16)y.y;
+                *(bf16x2 *)&sA[rl * LDA + 2 * lane + 128 * i] = o;
             }
         }
     }
@@ -1287,49 +1298,43 @@ __global__ void __launch_bounds__(256) k_lngemm(sd_gemm_args g, const float *__r
     // D layout: lane (j, kq) holds rows 4 kq + r of each 16-row tile, column n
     const float bias = g.bias ? g.bias[n] : 0.f;
     if (EPI == SD_EPI_QKV) {
-        const int Cq = g.heads * g.head_dim;
-        const int which = (int)(n / Cq), rem = (int)(n - (int64_t)which * Cq);
-        const int head = rem / g.head_dim, e = rem - head * g.head_dim;
+        // 32-bit index math (sd_ln_gemm checks every destination < 2^31 elements)
+        const uint32_t Cq = (uint32_t)(g.heads * g.head_dim), nn = (uint32_t)n;
+        const uint32_t which = nn / Cq, rem = nn - which * Cq;
+        const uint32_t head = rem / (uint32_t)g.head_dim, e = rem - head * (uint32_t)g.head_dim;
+        const uint32_t T = (uint32_t)g.tokens, Tp = (uint32_t)g.tokens_pad, HD = (uint32_t)g.head_dim;
+        __bf16 *const dq = (__bf16 *)(which == 0 ? g.q : which == 1 ? g.k : g.vt);
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
             const f32x4 a = t ? acc1 : acc0;
-            const int64_t mb = m0 + 16 * t + 4 * kq;
+            const uint32_t mb = (uint32_t)m0 + 16 * t + 4 * kq;
             // (image, token) of row mb by one divide; rows mb + 1 .. mb + 3 step from it
-            const uint32_t b0 = (uint32_t)mb / (uint32_t)g.tokens;
-            const int64_t tk0 = mb - (int64_t)b0 * g.tokens;
-            if (which == 2) {
+            const uint32_t b0 = mb / T, tk0 = mb - b0 * T;
+            if (which == 2 && mb + 3 < (uint32_t)g.M && tk0 + 3 < T && (tk0 & 3) == 0) {
                 // V^T: the lane's 4 rows are 4 consecutive tokens of its head-dim row
-                __bf16 *dst = (__bf16 *)g.vt + (((int64_t)b0 * g.heads + head) * g.head_dim + e) * g.tokens_pad + tk0;
-                if (mb + 3 < g.M && tk0 + 3 < g.tokens && (tk0 & 3) == 0) {
-                    bf16x4 v4;
+                bf16x4 v4;
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) v4[u] = (__bf16)(a[u] + bias);
-                    *(bf16x4 *)dst = v4;
-                    continue;
-                }
+                for (int u = 0; u < 4; ++u) v4[u] = (__bf16)(a[u] + bias);
+                *(bf16x4 *)(dq + ((b0 * g.heads + head) * HD + e) * Tp + tk0) = v4;
+                continue;
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const int64_t m = mb + u;
-                if (m >= g.M) break;
-                uint32_t b;
-                int64_t tk;
-                if (g.tokens >= 4) {  // at most one image boundary in 4 rows
-                    const bool wrap = tk0 + u >= g.tokens;
+                const uint32_t m = mb + u;
+                if (m >= (uint32_t)g.M) break;
+                uint32_t b, tk;
+                if (T >= 4) {  // at most one image boundary in 4 rows
+                    const bool wrap = tk0 + u >= T;
                     b = b0 + (wrap ? 1u : 0u);
-                    tk = tk0 + u - (wrap ? g.tokens : 0);
+                    tk = tk0 + u - (wrap ? T : 0u);
                 } else {
-                    b = (uint32_t)m / (uint32_t)g.tokens;
-                    tk = m - (int64_t)b * g.tokens;
+                    b = m / T;
+                    tk = m - b * T;
                 }
-                const int64_t bh = (int64_t)b * g.heads + head;
-                const __bf16 v = (__bf16)(a[u] + bias);
-                if (which == 0)
-                    ((__bf16 *)g.q)[(bh * g.tokens + tk) * g.head_dim + e] = v;
-                else if (which == 1)
-                    ((__bf16 *)g.k)[(bh * g.tokens_pad + tk) * g.head_dim + e] = v;
-                else
-                    ((__bf16 *)g.vt)[(bh * g.head_dim + e) * g.tokens_pad + tk] = v;
+                const uint32_t bh = b * g.heads + head;
+                const uint32_t off = which == 0 ? (bh * T + tk) * HD + e
+                                   : which == 1 ? (bh * Tp + tk) * HD + e : (bh * HD + e) * Tp + tk;
+                dq[off] = (__bf16)(a[u] + bias);
             }
         }
     } else {
@@ -1467,10 +1472,17 @@ extern "C" int sd_gemm(const sd_gemm_args *args, void *stream) {
     }
     if (g.M == 0) return 0;
     hipStream_t s = (hipStream_t)stream;
-    if (g.conv)
-        vt_pick_gemm<true>(g, s);
-    else
-        vt_pick_gemm<false>(g, s);
+    const int big = sd_conv_big_try(&g, stream);  // the DPT's 192x640 / 96x320 layers
+    if (big < 0) {
+        sd_set_error("sd_gemm: launch failed");
+        return -2;
+    }
+    if (!big) {
+        if (g.conv)
+            vt_pick_gemm<true>(g, s);
+        else
+            vt_pick_gemm<false>(g, s);
+    }
     if (hipGetLastError() != hipSuccess) {
         sd_set_error("sd_gemm: launch failed");
         return -2;
@@ -1492,7 +1504,8 @@ extern "C" int sd_ln_gemm(const sd_gemm_args *args, const float *x, const float 
     if (g.epi == SD_EPI_QKV)
         ok = ok && g.q && g.k && g.vt && g.head_dim > 0 && g.heads > 0 && g.tokens > 0 &&
              g.tokens_pad >= g.tokens && g.N == 3LL * g.heads * g.head_dim && g.M % g.tokens == 0 &&
-             g.head_dim % 8 == 0 && g.tokens_pad % 8 == 0;  // 8-B V^T stores, as sd_gemm
+             g.head_dim % 8 == 0 && g.tokens_pad % 8 == 0 &&  // 8-B V^T stores, as sd_gemm
+             (g.M / g.tokens) * g.heads * g.tokens_pad * g.head_dim < ((int64_t)1 << 31);
     else
         ok = ok && g.out && g.ldo >= g.N;
     if (!ok) {

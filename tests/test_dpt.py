@@ -141,3 +141,63 @@ def test_dpt_head_vs_reference(gpu):
     assert out.shape == ref.shape
     rel = ((out.cpu() - ref).norm() / ref.norm()).item()
     assert rel <= 3e-2, f"DPT rel-L2 {rel:.3g}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,H,W,Cin,Cout,f32", [(1, 96, 320, 256, 256, False), (1, 192, 640, 256, 256, True),
+                                                (1, 192, 640, 256, 256, False), (2, 61, 250, 128, 384, True)])
+def test_conv3x3_big_tiles(gpu, B, H, W, Cin, Cout, f32, monkeypatch):
+    """The 256-row LDS-DMA tiles of sdhip_conv.hip (the DPT head's 96x320 / 192x640
+    convolutions; 2 x 61 x 250 with Cout 384: ragged last tile, 128-column tiles, two
+    images' padding) against torch fp32 on the same bf16 operands, and against sd_gemm's
+    k_gemm path on the same inputs (SD_CONV_BIG=0)."""
+    from scenedino_amd import _lib
+    g = torch.Generator().manual_seed(H + W + Cout)
+    x = torch.randn(B, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) / math.sqrt(9 * Cin)
+    b = 0.1 * torch.randn(Cout, generator=g)
+    xq, wq = _q(x).to(gpu), _q(w).to(gpu)
+    xn = x.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous().to(gpu)
+    wp = w.permute(0, 2, 3, 1).reshape(Cout, -1).to(torch.bfloat16).contiguous().to(gpu)
+    epi = _lib.SD_EPI_F32 if f32 else _lib.SD_EPI_BF16
+    ref = F.conv2d(xq, wq, b.to(gpu), padding=1).permute(0, 2, 3, 1)
+    got = _lib.conv3x3(xn, wp, b.to(gpu), epi=epi).float()
+    monkeypatch.setenv("SD_CONV_BIG", "0")
+    old = _lib.conv3x3(xn, wp, b.to(gpu), epi=epi).float()
+    torch.cuda.synchronize()
+    scale = ref.abs().max().item()
+    tol = (1e-3 if f32 else 2e-2) * scale  # f32 out: fp32 accumulation order only
+    assert (got - ref).abs().max().item() <= tol
+    assert (got - old).abs().max().item() <= tol
+    assert torch.isfinite(got).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,H,W,Cin,Cout,k", [(1, 96, 320, 256, 256, 2), (1, 96, 320, 256, 256, None),
+                                              (2, 37, 211, 128, 128, 2)])
+def test_linear_big_tiles(gpu, B, H, W, Cin, Cout, k, monkeypatch):
+    """Dense-A forms of sdhip_conv.hip's 256-row tiles: the output head's ConvTranspose2d(2, 2)
+    at 96x320 (sub-pixel scatter epilogue), a 1x1 convolution, and a ragged two-image
+    transposed convolution, against torch fp32 and sd_gemm's k_gemm path (SD_CONV_BIG=0)."""
+    from scenedino_amd import _lib
+    from scenedino_amd.models.backbones.dino.dpt_head import _pack_conv1, _pack_convT
+    g = torch.Generator().manual_seed(H * W + Cout)
+    x = torch.randn(B, Cin, H, W, generator=g)
+    if k:
+        conv = torch.nn.ConvTranspose2d(Cin, Cout, kernel_size=k, stride=k)
+        wp, bp, kk = _pack_convT(conv)
+        ref = F.conv_transpose2d(_q(x).to(gpu), _q(conv.weight.detach()).to(gpu),
+                                 conv.bias.detach().to(gpu), stride=k)
+    else:
+        conv = torch.nn.Conv2d(Cin, Cout, kernel_size=1)
+        (wp, bp), kk = _pack_conv1(conv), None
+        ref = F.conv2d(_q(x).to(gpu), _q(conv.weight.detach()).to(gpu), conv.bias.detach().to(gpu))
+    xn = x.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous().to(gpu)
+    got = _lib.linear_nhwc(xn, wp.to(gpu), bp.to(gpu), shuf=kk).float().permute(0, 3, 1, 2)
+    monkeypatch.setenv("SD_CONV_BIG", "0")
+    old = _lib.linear_nhwc(xn, wp.to(gpu), bp.to(gpu), shuf=kk).float().permute(0, 3, 1, 2)
+    torch.cuda.synchronize()
+    assert got.shape == ref.shape
+    tol = 2e-2 * ref.abs().max().item()
+    assert (got - ref).abs().max().item() <= tol
+    assert (got - old).abs().max().item() <= tol
