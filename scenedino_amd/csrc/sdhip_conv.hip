@@ -1,64 +1,109 @@
-// sdhip_conv.hip -- the DPT head's large 3x3 convolutions on gfx950 (CDNA4) MFMA.
+// sdhip_conv.hip -- the DPT head's full-chip convolutions on gfx950 (CDNA4) MFMA.
 //
-// The reference runs them as torch Conv2d (scenedino/models/backbones/dino/dpt_head.py:
-// 160-176, 226-236: DPTHead.project and the output head's two 3x3 convolutions, 256 -> 256
-// channels at 96x320 and 192x640 for a 192x640 frame).  Same implicit GEMM as k_gemm's CONV
-// form (rows m = output pixels, k = (ky, kx, ci), out-of-image taps read as zeros through
-// the buffer bounds), re-tiled for a chip-filling launch with long K (K = 2304):
-//   * one 512-thread workgroup per CU, 8 waves as 2 (M) x 4 (N), a 256 x BN output tile
-//     (BN = 256: wave tile 128 x 64; BN = 128: 128 x 32) on v_mfma_f32_16x16x32_bf16;
+// The reference runs them as torch Conv2d / ConvTranspose2d (scenedino/models/backbones/dino/
+// dpt_head.py:160-176, 226-236: the residual conv units at 48x160, DPTHead.project and the
+// output head at 96x320 and 192x640, 256 channels, for a 192x640 frame).  Same implicit GEMM
+// as k_gemm's CONV form (rows m = output pixels, k = (ky, kx, ci), out-of-image taps read as
+// zeros through the buffer bounds), re-tiled for launches whose tiles cover the CUs:
+//   * one 512-thread workgroup per CU, 8 waves as 2 (M) x 4 (N), a BM x BN output tile
+//     (256 x 256: wave tile 128 x 64; 256 x 128; 128 x 128; 128 x 64: 64 x 16) on
+//     v_mfma_f32_16x16x32_bf16;
 //   * 64-deep K steps, A (im2col rows) and W tiles moved global -> LDS by LDS-DMA
 //     (buffer_load ... lds, 8 rows of 128 B per wave instruction) into a ring of RS stages,
 //     16-B chunks XOR-swizzled per row on the SOURCE side (conflict-free ds_read_b128 of
 //     the fragments, MI355X guide rule 21); the loads of RS - 1 steps stay in flight across
 //     the per-step barrier (counted vmcnt, raw s_barrier: never a vmcnt(0) in the loop);
-//   * epilogue: bias, bf16 or f32 NHWC rows staged through LDS for 16-B stores.
-// 2 x 128 x 64 (or 32) MFMA work per wave per barrier instead of k_gemm<128,128>'s 64 x 64
-// with two barriers: the 128-row tiles' structure tops out near 0.75 PFLOP/s on these shapes.
+//   * the residual units' pre-activation ReLU on the A fragments (v_pk_max_i16 on the bf16
+//     bit patterns: sign set -> +0);
+//   * epilogue: bias (+ the bf16 residuals), bf16 or f32 NHWC rows or the sub-pixel scatter
+//     of a ConvTranspose2d(k, stride k), staged per wave through LDS for 16-B stores.
+// 2 x 128 x 64 MFMA work per wave per barrier at 256 x 256 instead of k_gemm<128,128>'s
+// 64 x 64 with two barriers: the 128-row tiles' structure tops out near 0.75 PFLOP/s here.
 #include <cstdlib>
 
 #include "sdhip_common.h"
 #include "sdhip_point.h"
 
-#define CV_BM 256
 #define CV_BK 64
+#define CV_LDS_MAX (144 * 1024)
 
 typedef __attribute__((ext_vector_type(4))) float cvf4;
+typedef __attribute__((ext_vector_type(2))) short cvs2;
 
-__device__ __forceinline__ void cv_dma16(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t lds_addr) {
-    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
-                 :: "v"(voff), "s"(rs), "s"(lds_addr) : "memory");
+// LDS-DMA of 16 B per lane: source = buffer + voff (per lane) + soff (wave-uniform), LDS
+// destination = lds_addr + 16 lane (M0 set in the same asm, the DMA right behind it)
+__device__ __forceinline__ void cv_dma16s(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff, uint32_t lds_addr) {
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %3 offen lds"
+                 :: "v"(voff), "s"(rs), "s"(lds_addr), "s"(soff) : "memory");
 }
 // 16-B chunk slot of logical chunk kc in a 128-B tile row (an involution): the 16 rows a
 // ds_read_b128 lane group reads land on 16 distinct 16-B bank slots
 __device__ __forceinline__ int cv_swz(int row, int kc) { return kc ^ ((row >> 1) & 7); }
 
-template <int BN>
-__host__ __device__ constexpr int cv_stages() { return BN >= 256 ? 2 : 3; }
-template <int BN>
-__host__ __device__ constexpr int cv_ring_bytes() { return cv_stages<BN>() * (CV_BM + BN) * CV_BK * 2; }
-// epilogue staging: per wave ER rows x WN values (+16 B pad per row)
-template <int BN, bool F32>
-__host__ __device__ constexpr int cv_epi_rows() { return F32 && BN >= 256 ? 64 : 128; }
-template <int BN, bool F32>
-__host__ __device__ constexpr int cv_epi_pitch() { return (BN / 4) * (F32 ? 4 : 2) + 16; }
-template <int BN, bool F32>
-__host__ __device__ constexpr int cv_lds_bytes() {
-    return cv_ring_bytes<BN>() > 8 * cv_epi_rows<BN, F32>() * cv_epi_pitch<BN, F32>()
-               ? cv_ring_bytes<BN>() : 8 * cv_epi_rows<BN, F32>() * cv_epi_pitch<BN, F32>();
+// ReLU of 8 bf16 values: as int16 a bf16 with the sign bit set is negative (-0 included)
+__device__ __forceinline__ bf16x8 cv_relu8(bf16x8 v) {
+    uint4 u = __builtin_bit_cast(uint4, v);
+    const cvs2 z = {0, 0};
+    u.x = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(cvs2, u.x), z));
+    u.y = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(cvs2, u.y), z));
+    u.z = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(cvs2, u.z), z));
+    u.w = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(cvs2, u.w), z));
+    return __builtin_bit_cast(bf16x8, u);
 }
 
-// EPI: SD_EPI_BF16 / SD_EPI_F32 (out (M, ldo) = acc + bias) or SD_EPI_SHUF (the
-// ConvTranspose2d(k, stride k) sub-pixel scatter, bf16); CONV: implicit 3x3 im2col A rows
-// (else dense A rows of stride lda: the 1x1 convolutions / transposed convolutions)
-template <int BN, int EPI, bool CONV>
+template <int BM, int BN>
+__host__ __device__ constexpr int cv_stage_bytes() { return (BM + BN) * CV_BK * 2; }
+#ifndef CV_RELU_LDS
+#define CV_RELU_LDS 1
+#endif
+#ifndef CV_CHUNK_MAJOR
+#define CV_CHUNK_MAJOR 1
+#endif
+#ifndef CV_MAX_STAGES
+#define CV_MAX_STAGES 6
+#endif
+// as many ring stages as fit (at most CV_MAX_STAGES): the loop is bound by the bytes each CU
+// keeps in flight (L2 / Infinity Cache latency), not by the MFMA
+template <int BM, int BN>
+__host__ __device__ constexpr int cv_stages() {
+    return CV_LDS_MAX / cv_stage_bytes<BM, BN>() >= CV_MAX_STAGES ? CV_MAX_STAGES : CV_LDS_MAX / cv_stage_bytes<BM, BN>();
+}
+// s_waitcnt vmcnt(A * PER) for a runtime A in [0, RS - 2] (the immediate must be a constant)
+template <int PER, int RS>
+__device__ __forceinline__ void cv_wait_ahead(int ahead) {
+    if (RS >= 6 && ahead >= 4) asm volatile("s_waitcnt vmcnt(%0)" :: "i"(4 * PER) : "memory");
+    else if (RS >= 5 && ahead >= 3) asm volatile("s_waitcnt vmcnt(%0)" :: "i"(3 * PER) : "memory");
+    else if (RS >= 4 && ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" :: "i"(2 * PER) : "memory");
+    else if (RS >= 3 && ahead >= 1) asm volatile("s_waitcnt vmcnt(%0)" :: "i"(PER) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+// epilogue staging: f32 when the output is f32 or residuals are added before the bf16
+// rounding, else bf16; per wave ER rows of WN values + 16 B
+template <int BN, bool STF32>
+__host__ __device__ constexpr int cv_epi_pitch() { return (BN / 4) * (STF32 ? 4 : 2) + 16; }
+template <int BM, int BN, bool STF32>
+__host__ __device__ constexpr int cv_epi_rows() {
+    return 8 * (BM / 2) * cv_epi_pitch<BN, STF32>() <= CV_LDS_MAX ? BM / 2 : BM / 4;
+}
+template <int BM, int BN, bool STF32>
+__host__ __device__ constexpr int cv_lds_bytes() {
+    return cv_stages<BM, BN>() * cv_stage_bytes<BM, BN>() > 8 * cv_epi_rows<BM, BN, STF32>() * cv_epi_pitch<BN, STF32>()
+               ? cv_stages<BM, BN>() * cv_stage_bytes<BM, BN>()
+               : 8 * cv_epi_rows<BM, BN, STF32>() * cv_epi_pitch<BN, STF32>();
+}
+
+// EPI: SD_EPI_BF16 / SD_EPI_F32 (out (M, ldo) = acc + bias [+ res + res2 when RES]) or
+// SD_EPI_SHUF (the ConvTranspose2d(k, stride k) sub-pixel scatter, bf16); CONV: implicit
+// 3x3 im2col A rows (else dense A rows of stride lda: 1x1 / transposed convolutions);
+// RELU: ReLU on the A operand (the pre-activation of the residual conv units)
+template <int BM, int BN, int EPI, bool CONV, bool RELU, bool RES>
 __global__ void __launch_bounds__(512) k_conv_big(sd_gemm_args g) {
-    constexpr bool F32 = EPI == SD_EPI_F32;
-    constexpr int BM = CV_BM, BK = CV_BK, RS = cv_stages<BN>();
-    constexpr int WN = BN / 4, TJ = WN / 16;       // wave columns, 16-col MFMA tiles per wave
-    constexpr int STB = (BM + BN) * BK * 2;        // bytes per ring stage: A rows, then W rows
-    constexpr int CA = BM * 8 / 512, CB = BN * 8 / 512;  // 16-B chunks per thread per stage
-    constexpr int PER = CA + CB;                   // LDS-DMAs per thread per stage
+    constexpr bool OUTF32 = EPI == SD_EPI_F32, STF32 = OUTF32 || RES;
+    constexpr int BK = CV_BK, RS = cv_stages<BM, BN>(), STB = cv_stage_bytes<BM, BN>();
+    constexpr int WM = BM / 2, WN = BN / 4, TI = WM / 16, TJ = WN / 16;  // wave tile, 16x16 MFMA tiles
+    constexpr int CA = BM * 8 / 512, CB = BN * 8 / 512;  // 16-B DMA chunks per thread per stage
+    constexpr int PER = CA + CB;
+    static_assert(CB >= 1 && TJ >= 1 && RS >= 2 && RS <= 6 && (RS - 2) * PER <= 63, "tile shape");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -100,31 +145,58 @@ __global__ void __launch_bounds__(512) k_conv_big(sd_gemm_args g) {
         const int row = 8 * (8 * c + wave) + (lane >> 3);
         voB[c] = (uint32_t)((min(n0 + row, g.N - 1) * g.K) * 2) + (uint32_t)cv_swz(row, lane & 7) * 16u;
     }
+    // conv K order: channel-chunk major, tap minor -- step kt = (chunk kt / 9, tap kt % 9),
+    // the matching W columns tap Cin + 64 chunk .. + 63 (any order of the K steps gives the
+    // same sum up to fp32 rounding).  The 9 taps of a chunk read the same input pixels
+    // (shifted by one pixel or row) in 9 consecutive steps, so the tile's input rows are
+    // re-read from L2 instead of from beyond it (tap-major order re-read each row 3 rows'
+    // worth of steps later, after the XCD's tiles had streamed ~3x its L2 through).
+    // The chunk's channel offset goes in the DMA's scalar offset.
     auto issue = [&](int kt) {
         const uint32_t st = lds0 + (uint32_t)(kt % RS) * STB;
-        const int k0 = kt * BK;
-        const int tap = CONV ? k0 / g.Cin : 0, ci0 = k0 - tap * g.Cin;
+        int tap = 0, ci0 = kt * BK;
+        if (CONV && CV_CHUNK_MAJOR) {
+            const int chunk = kt / 9;
+            tap = kt - 9 * chunk;
+            ci0 = chunk * BK;
+        } else if (CONV) {  // tap-major (the weight layout's own order; A/B runs)
+            tap = ci0 / g.Cin;
+            ci0 -= tap * g.Cin;
+        }
         const int ky = tap / 3, kx = tap - 3 * ky;
 #pragma unroll
         for (int c = 0; c < CA; ++c) {
-            if (!CONV) {
-                cv_dma16(rsA, kcA[c] + (uint32_t)k0 * 2u, st + (uint32_t)(8 * c + wave) * 1024u);
-                continue;
+            uint32_t vo = kcA[c];
+            if (CONV) {
+                const int iy = ciy[c] + ky, ix = cix[c] + kx;
+                const bool ok = (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
+                // past the buffer (also with the channel offset added): the DMA writes zeros
+                vo = ok ? (uint32_t)((cpix[c] + iy * g.W + ix) * g.Cin * 2) + kcA[c] : 0x80000000u;
             }
-            const int iy = ciy[c] + ky, ix = cix[c] + kx;
-            const bool ok = (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
-            const uint32_t off = ok ? (uint32_t)(((cpix[c] + iy * g.W + ix) * g.Cin + ci0) * 2) + kcA[c]
-                                    : 0x80000000u;  // past the buffer: the DMA writes zeros (padding)
-            cv_dma16(rsA, off, st + (uint32_t)(8 * c + wave) * 1024u);
+            cv_dma16s(rsA, vo, (uint32_t)ci0 * 2u, st + (uint32_t)(8 * c + wave) * 1024u);
         }
+        const uint32_t kb = (uint32_t)(CONV ? tap * g.Cin + ci0 : ci0) * 2u;  // W column offset
 #pragma unroll
         for (int c = 0; c < CB; ++c)
-            cv_dma16(rsB, voB[c] + (uint32_t)k0 * 2u, st + (uint32_t)(BM * BK * 2) + (uint32_t)(8 * c + wave) * 1024u);
+            cv_dma16s(rsB, voB[c], kb, st + (uint32_t)(BM * BK * 2) + (uint32_t)(8 * c + wave) * 1024u);
+    };
+    // ReLU of the A chunks this thread DMA'd into stage kt, in place (after its own vmcnt
+    // covers them; the next barrier publishes them): once per element, not once per
+    // fragment read by each of the 4 column waves.  Needs RS >= 3 (stage kt + 1 is waited
+    // for one step early); RS = 2 tiles apply it to the fragments instead.
+    constexpr bool RELU_LDS = RELU && RS >= 3 && CV_RELU_LDS, RELU_FRAG = RELU && !RELU_LDS;
+    auto relu_own = [&](int kt) {
+        uint8_t *st = smem + (kt % RS) * STB;
+#pragma unroll
+        for (int c = 0; c < CA; ++c) {
+            bf16x8 *p = (bf16x8 *)(st + (8 * c + wave) * 1024 + lane * 16);
+            *p = cv_relu8(*p);
+        }
     };
 
-    cvf4 acc[8][TJ];
+    cvf4 acc[TI][TJ];
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int j = 0; j < TJ; ++j) acc[i][j] = cvf4{0.f, 0.f, 0.f, 0.f};
 
@@ -132,13 +204,22 @@ __global__ void __launch_bounds__(512) k_conv_big(sd_gemm_args g) {
 #pragma unroll
     for (int i = 0; i < RS - 1; ++i)
         if (i < nk) issue(i);
+    if (RELU_LDS) {  // stage 0
+        cv_wait_ahead<PER, RS>(min(RS - 2, nk - 1));
+        relu_own(0);
+    }
     for (int kt = 0; kt < nk; ++kt) {
-        // stage kt landed: of this thread's DMAs only those of stages kt + 1 .. kt + RS - 2
-        // (the ones issued) may be younger
-        if (RS >= 3 && kt + RS - 2 < nk)
-            asm volatile("s_waitcnt vmcnt(%0)" :: "i"((RS >= 3 ? RS - 2 : 0) * PER) : "memory");
-        else
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // stage kt landed: this thread's DMAs of the issued stages kt + 1 .. kt + RS - 2 may
+        // be younger (fewer near the end: no stage is issued past nk - 1).  RELU_LDS: stage
+        // kt + 1 landed (stage kt was waited for and rectified one step earlier)
+        if (RELU_LDS) {
+            if (kt + 1 < nk) {
+                cv_wait_ahead<PER, RS>(min(RS - 3, nk - 2 - kt));
+                relu_own(kt + 1);
+            }
+        } else {
+            cv_wait_ahead<PER, RS>(min(RS - 2, nk - 1 - kt));
+        }
         // every wave's DMAs of stage kt landed, every wave's fragment reads of step kt - 1
         // retired: slot (kt - 1) % RS is free
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -148,11 +229,12 @@ __global__ void __launch_bounds__(512) k_conv_big(sd_gemm_args g) {
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
             const int kc = 4 * s + fk;
-            bf16x8 af[8], bfr[TJ];
+            bf16x8 af[TI], bfr[TJ];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const int row = wm * 128 + 16 * i + fr;
+            for (int i = 0; i < TI; ++i) {
+                const int row = wm * WM + 16 * i + fr;
                 af[i] = *(const bf16x8 *)(sa + row * 128 + 16 * cv_swz(row, kc));
+                if (RELU_FRAG) af[i] = cv_relu8(af[i]);
             }
 #pragma unroll
             for (int j = 0; j < TJ; ++j) {
@@ -160,7 +242,7 @@ __global__ void __launch_bounds__(512) k_conv_big(sd_gemm_args g) {
                 bfr[j] = *(const bf16x8 *)(sb + row * 128 + 16 * cv_swz(row, kc));
             }
 #pragma unroll
-            for (int i = 0; i < 8; ++i)
+            for (int i = 0; i < TI; ++i)
 #pragma unroll
                 for (int j = 0; j < TJ; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
@@ -177,101 +259,135 @@ __global__ void __launch_bounds__(512) k_conv_big(sd_gemm_args g) {
         const int64_t n = min(n0 + wn * WN + 16 * j + fr, g.N - 1);
         bias[j] = g.bias ? g.bias[n] : 0.f;
     }
-    constexpr int ER = cv_epi_rows<BN, F32>(), PITCH = cv_epi_pitch<BN, F32>();
-    constexpr int ES = F32 ? 4 : 2;
-    constexpr int CPRW = WN * ES / 16;  // 16-B chunks per wave row
+    constexpr int ER = cv_epi_rows<BM, BN, STF32>(), PITCH = cv_epi_pitch<BN, STF32>();
+    constexpr int CC = OUTF32 ? 4 : 8;  // columns per 16-B output store
+    constexpr int CPRW = WN / CC;       // store chunks per wave row
+    static_assert((ER * CPRW) % 64 == 0, "epilogue chunking");
     uint8_t *reg = smem + wave * ER * PITCH;
 #pragma unroll
-    for (int half = 0; half < 128 / ER; ++half) {
-        if (half) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    for (int part = 0; part < WM / ER; ++part) {
+        if (part) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #pragma unroll
-        for (int i = half * (ER / 16); i < (half + 1) * (ER / 16); ++i)
+        for (int i = part * (ER / 16); i < (part + 1) * (ER / 16); ++i)
 #pragma unroll
             for (int j = 0; j < TJ; ++j)
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    const int r = 16 * i + 4 * fk + e - half * ER;
+                    const int r = 16 * i + 4 * fk + e - part * ER;
                     const float v = acc[i][j][e] + bias[j];
-                    if (F32)
+                    if (STF32)
                         *(float *)(reg + r * PITCH + (16 * j + fr) * 4) = v;
                     else
                         *(__bf16 *)(reg + r * PITCH + (16 * j + fr) * 2) = (__bf16)v;
                 }
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        // the wave stores its own ER x WN block: lane -> (row, 16-B chunk)
+        // the wave stores its own ER x WN block: lane -> (row, chunk of CC columns)
 #pragma unroll
         for (int it = 0; it < ER * CPRW / 64; ++it) {
             const int idx = it * 64 + lane, r = idx / CPRW, ch = idx - r * CPRW;
-            const int64_t m = m0 + wm * 128 + half * ER + r;
-            const int64_t n = n0 + wn * WN + ch * (16 / ES);
-            if (m < g.M && n < g.N) {
-                const uint4 v = *(const uint4 *)(reg + r * PITCH + ch * 16);
-                int64_t base = m * g.ldo + n;  // element index of (m, n)
-                if (EPI == SD_EPI_SHUF) {  // 8 columns inside one sub-pixel (cout % 8 == 0)
-                    const int kk = g.shuf_k, hw = g.in_h * g.in_w, cout = (int)(g.N / (kk * kk));
-                    const int b = (int)((uint32_t)m / (uint32_t)hw);
-                    const int pix = (int)(m - (int64_t)b * hw);
-                    const int y = pix / g.in_w, x = pix - y * g.in_w;
-                    const int sub = (int)(n / cout), co = (int)(n - (int64_t)sub * cout);
-                    const int dy = sub / kk, dx = sub - dy * kk;
-                    base = (((int64_t)b * g.in_h * kk + y * kk + dy) * (g.in_w * kk) + x * kk + dx) * cout + co;
+            const int64_t m = m0 + wm * WM + part * ER + r;
+            const int64_t n = n0 + wn * WN + ch * CC;
+            if (m >= g.M || n >= g.N) continue;
+            uint4 v;
+            if (STF32 && !OUTF32) {  // f32 staging, residuals added before the bf16 rounding
+                const cvf4 lo = *(const cvf4 *)(reg + r * PITCH + ch * 32);
+                const cvf4 hi = *(const cvf4 *)(reg + r * PITCH + ch * 32 + 16);
+                float f[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                if (RES) {
+                    if (g.res) {
+                        const bf16x8 a = *(const bf16x8 *)((const __bf16 *)g.res + m * g.ldo + n);
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) f[u] += (float)a[u];
+                    }
+                    if (g.res2) {
+                        const bf16x8 a = *(const bf16x8 *)((const __bf16 *)g.res2 + m * g.ldo + n);
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) f[u] += (float)a[u];
+                    }
                 }
-                *(uint4 *)((uint8_t *)g.out + base * ES) = v;
+                bf16x8 o;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) o[u] = (__bf16)f[u];
+                v = __builtin_bit_cast(uint4, o);
+            } else {
+                v = *(const uint4 *)(reg + r * PITCH + ch * 16);
             }
+            int64_t base = m * g.ldo + n;  // element index of (m, n)
+            if (EPI == SD_EPI_SHUF) {  // 8 columns inside one sub-pixel (cout % 8 == 0)
+                const int kk = g.shuf_k, hw = g.in_h * g.in_w, cout = (int)(g.N / (kk * kk));
+                const int b = (int)((uint32_t)m / (uint32_t)hw);
+                const int pix = (int)(m - (int64_t)b * hw);
+                const int y = pix / g.in_w, x = pix - y * g.in_w;
+                const int sub = (int)(n / cout), co = (int)(n - (int64_t)sub * cout);
+                const int dy = sub / kk, dx = sub - dy * kk;
+                base = (((int64_t)b * g.in_h * kk + y * kk + dy) * (g.in_w * kk) + x * kk + dx) * cout + co;
+            }
+            *(uint4 *)((uint8_t *)g.out + base * (OUTF32 ? 4 : 2)) = v;
         }
     }
 }
 
 // The shapes this kernel takes (else sd_gemm's k_gemm path), with enough output tiles to
-// give every CU a 256-row tile: a 3x3 stride-1 convolution with Cin % 64 == 0 and a plain
-// bf16 / f32 epilogue (bias only), or a dense GEMM with K % 64 == 0 and a plain bf16 or the
-// transposed-convolution (SHUF) epilogue; N % 128 == 0.  BN = 256 when the 256 x 256 tiles
-// cover the CUs about twice (192x640: 480 tiles), else 256 x 128 tiles (96x320: 240).
-// Returns 1 when launched, 0 when the shape is not one of these (the caller runs k_gemm),
-// -2 on a launch error.  SD_CONV_BIG=0 in the environment (read per call) disables it
-// (tests, A/B runs).
+// give every CU one: a 3x3 stride-1 convolution with Cin % 64 == 0 (pre-activation ReLU and
+// bf16 residuals allowed) and a bf16 / f32 epilogue, or a dense GEMM with K % 64 == 0 and a
+// plain bf16 or the transposed-convolution (SHUF) epilogue; N % 64 == 0.  Tile: 256 x 256
+// when those cover the CUs about twice (192x640: 480 tiles), else the first of 256 x 128,
+// 128 x 128, 128 x 64 with at least 7/8 of a tile per CU (96x320: 240 of 256 x 128; 48x160:
+// 240 of 128 x 64).  Returns 1 when launched, 0 when the shape is not one of these (the
+// caller runs k_gemm), -2 on a launch error.  SD_CONV_BIG=0 in the environment (read per
+// call) disables it (tests, A/B runs).
 int sd_conv_big_try(const sd_gemm_args *args, void *stream) {
     const char *e = getenv("SD_CONV_BIG");
     if (e && e[0] == '0') return 0;
     const sd_gemm_args &g = *args;
-    if (g.res || g.res2 || g.N % 128 || g.K % CV_BK) return 0;
+    if (g.N % 64 || g.K % CV_BK) return 0;
+    const bool res = g.res || g.res2;
     if (g.conv) {
-        if (g.stride != 1 || g.relu_in || g.Cin % 64 || g.K != 9LL * g.Cin ||
-            (g.epi != SD_EPI_BF16 && g.epi != SD_EPI_F32) || g.ldo % 8 || g.ldo < g.N)
+        if (g.stride != 1 || g.Cin % 64 || g.K != 9LL * g.Cin || g.ldo % 8 || g.ldo < g.N ||
+            (g.epi != SD_EPI_BF16 && g.epi != SD_EPI_F32) || (res && g.epi != SD_EPI_BF16))
             return 0;
     } else {
-        if (g.lda % 8 || g.lda < g.K) return 0;
+        if (g.lda % 8 || g.lda < g.K || res || g.relu_in) return 0;
         if (g.epi == SD_EPI_SHUF) {
             if (g.shuf_k <= 0 || (g.N / (g.shuf_k * g.shuf_k)) % 8) return 0;
         } else if (g.epi != SD_EPI_BF16 || g.ldo % 8 || g.ldo < g.N) {
             return 0;
         }
     }
-    const int ncu = sd_num_cus();
-    const int64_t t256 = (g.M + CV_BM - 1) / CV_BM;
-    if (t256 * (g.N / 128) < (int64_t)ncu * 7 / 8) return 0;  // too few tiles: k_gemm's split forms
     const int64_t a_bytes = g.conv ? (g.M / ((int64_t)g.OH * g.OW)) * g.H * g.W * g.Cin * 2 : g.M * g.lda * 2;
     if (a_bytes >= ((int64_t)1 << 31) || g.N * g.K * 2 >= ((int64_t)1 << 31)) return 0;
-    const bool wide = g.N % 256 == 0 && t256 * (g.N / 256) >= (int64_t)ncu * 15 / 8;
+    const int64_t ncu = sd_num_cus();
+    auto tiles = [&](int bm, int bn) { return g.N % bn ? 0 : ((g.M + bm - 1) / bm) * (g.N / bn); };
+    int bm, bn;
+    if (tiles(256, 256) >= ncu * 15 / 8) bm = 256, bn = 256;
+    else if (tiles(256, 128) >= ncu * 7 / 8) bm = 256, bn = 128;
+    else if (tiles(128, 128) >= ncu * 7 / 8) bm = 128, bn = 128;
+    else if (tiles(128, 64) >= ncu * 7 / 8) bm = 128, bn = 64;
+    else return 0;
     hipStream_t s = (hipStream_t)stream;
-    auto go = [&](auto kern, int bn, int lds) {
+    auto go = [&](auto kern, int lds) {
         (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        hipLaunchKernelGGL(kern, dim3((unsigned)t256, (unsigned)(g.N / bn)), dim3(512), lds, s, g);
+        hipLaunchKernelGGL(kern, dim3((unsigned)((g.M + bm - 1) / bm), (unsigned)(g.N / bn)), dim3(512), lds, s, g);
     };
-#define CV_GO(BNV, E, C) go(k_conv_big<BNV, E, C>, BNV, cv_lds_bytes<BNV, E == SD_EPI_F32>())
-    if (g.conv) {
-        if (wide) {
-            if (g.epi == SD_EPI_F32) CV_GO(256, SD_EPI_F32, true); else CV_GO(256, SD_EPI_BF16, true);
-        } else {
-            if (g.epi == SD_EPI_F32) CV_GO(128, SD_EPI_F32, true); else CV_GO(128, SD_EPI_BF16, true);
-        }
-    } else {
-        if (wide) {
-            if (g.epi == SD_EPI_SHUF) CV_GO(256, SD_EPI_SHUF, false); else CV_GO(256, SD_EPI_BF16, false);
-        } else {
-            if (g.epi == SD_EPI_SHUF) CV_GO(128, SD_EPI_SHUF, false); else CV_GO(128, SD_EPI_BF16, false);
-        }
+#define CV_K(BM_, BN_, E, C, R, RS_) go(k_conv_big<BM_, BN_, E, C, R, RS_>, cv_lds_bytes<BM_, BN_, E == SD_EPI_F32 || RS_>())
+#define CV_TILE(BM_, BN_)                                                                            \
+    if (bm == BM_ && bn == BN_) {                                                                    \
+        if (!g.conv) {                                                                               \
+            if (g.epi == SD_EPI_SHUF) CV_K(BM_, BN_, SD_EPI_SHUF, false, false, false);              \
+            else CV_K(BM_, BN_, SD_EPI_BF16, false, false, false);                                   \
+        } else if (g.epi == SD_EPI_F32) {                                                            \
+            if (g.relu_in) CV_K(BM_, BN_, SD_EPI_F32, true, true, false);                            \
+            else CV_K(BM_, BN_, SD_EPI_F32, true, false, false);                                     \
+        } else if (res) {                                                                            \
+            if (g.relu_in) CV_K(BM_, BN_, SD_EPI_BF16, true, true, true);                            \
+            else CV_K(BM_, BN_, SD_EPI_BF16, true, false, true);                                     \
+        } else {                                                                                     \
+            if (g.relu_in) CV_K(BM_, BN_, SD_EPI_BF16, true, true, false);                           \
+            else CV_K(BM_, BN_, SD_EPI_BF16, true, false, false);                                    \
+        }                                                                                            \
     }
-#undef CV_GO
+    CV_TILE(256, 256) else CV_TILE(256, 128) else CV_TILE(128, 128) else CV_TILE(128, 64)
+#undef CV_TILE
+#undef CV_K
     return hipGetLastError() == hipSuccess ? 1 : -2;
 }

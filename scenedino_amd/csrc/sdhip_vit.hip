@@ -70,7 +70,10 @@ __device__ __forceinline__ f32x16 vt_zero16() {
 #ifndef VT_RING
 #define VT_RING 1  // round 4 A/B (graph-replayed passes, 2 reps): ViT-S/16 0.615 -> 0.599 ms, encode 1.30 -> 1.276
 #endif
-__host__ __device__ constexpr int vt_ring_stages(int BM, int BN) { return BM >= 128 || BN >= 128 ? 3 : 4; }
+#ifndef VT_RS_SK
+#define VT_RS_SK 4  // ring stages of the 32 x 32 split-K tiles (16 KiB each at BK = 128)
+#endif
+__host__ __device__ constexpr int vt_ring_stages(int BM, int BN) { return BM >= 128 || BN >= 128 ? 3 : BM == 32 ? VT_RS_SK : 4; }
 // which tiles take the ring: the 32 x 32 split-K tiles of the small-M GEMMs (ViT-S/16 and
 // DINOv2-B/14 at 481 tokens, the DPT's 12x40 / 24x80 convolutions).  VT_RING_ALL = 1 puts
 // every tile on it (the 64 x 64 and 128 x 128 tiles measured slower: one 96-KiB ring per CU
@@ -85,7 +88,8 @@ __host__ __device__ constexpr int vt_ring_bytes() { return vt_ring_stages(BM, BN
 // LDS use disjoint chunk sets, 16 consecutive rows cover the 64 banks once
 template <int CPR>
 __device__ __forceinline__ int vt_swz(int row, int kc) {
-    return kc ^ ((row / (16 / CPR)) & (CPR - 1));
+    if constexpr (CPR >= 16) return kc ^ (row & 15);  // rows of >= 256 B: one row per bank sweep
+    else return kc ^ ((row / (16 / CPR)) & (CPR - 1));
 }
 __device__ __forceinline__ void vt_dma16(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff,
                                          uint32_t lds_addr) {
@@ -1379,6 +1383,9 @@ static void vt_launch_gemm(const sd_gemm_args &g, hipStream_t s) {
     }
 }
 
+#ifndef VT_SK256
+#define VT_SK256 1
+#endif
 #ifndef SD_CONV_SK_MID
 #define SD_CONV_SK_MID 256  // conv: split-K tiles below this many 64x64 tiles (1024: no gain)
 #endif
@@ -1416,6 +1423,15 @@ static void vt_pick_gemm(const sd_gemm_args &g, hipStream_t s) {
     // conv: a 128-deep K step must stay inside one 3x3 tap (Cin % 128 == 0); the DPT's
     // low-resolution 256-channel convolutions (12x40, 24x80) are exactly these small-M,
     // large-K GEMMs
+    // split-K tiles that leave CUs idle (ViT-S/16 fc2 at 481 tokens: 192; the DPT's 12x40
+    // convolutions: 120) take 256-deep K steps: half the dependent ring steps per tile, a
+    // 128-KiB ring (one tile per CU is all there is anyway)
+    const int64_t t32 = ((g.M + 31) / 32) * ((g.N + 31) / 32);
+    if (VT_SK256 && VT_RING && t32 <= (int64_t)sd_num_cus() && g.K % 256 == 0 &&
+        (CONV ? g.Cin % 256 == 0 && mid < SD_CONV_SK_MID : mid < 256)) {
+        vt_launch_gemm<32, 32, 256, CONV>(g, s);
+        return;
+    }
     if ((CONV ? g.Cin % 128 == 0 && mid < SD_CONV_SK_MID : mid < 256) && g.K % 128 == 0 &&
         g.K >= 256) {
         vt_launch_gemm<32, 32, 128, CONV>(g, s);  // split-K over the 4 waves

@@ -201,3 +201,36 @@ def test_linear_big_tiles(gpu, B, H, W, Cin, Cout, k, monkeypatch):
     tol = 2e-2 * ref.abs().max().item()
     assert (got - ref).abs().max().item() <= tol
     assert (got - old).abs().max().item() <= tol
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,H,W,C", [(1, 48, 160, 256), (2, 61, 130, 128)])
+def test_conv3x3_big_tiles_residual_unit(gpu, B, H, W, C, monkeypatch):
+    """The residual conv units' convolutions on sdhip_conv.hip's 128-row tiles (48x160: 240
+    tiles of 128 x 64): pre-activation ReLU on the input, the two bf16 residuals added
+    before the output rounding (dpt_head.py PreActResidualConvUnit / FeatureFusionBlock),
+    against torch fp32 and the k_gemm path (SD_CONV_BIG=0)."""
+    from scenedino_amd import _lib
+    g = torch.Generator().manual_seed(H * W + C)
+    x = torch.randn(B, C, H, W, generator=g)
+    w = torch.randn(C, C, 3, 3, generator=g) / math.sqrt(9 * C)
+    b = 0.1 * torch.randn(C, generator=g)
+    r1 = torch.randn(B, H, W, C, generator=g).to(torch.bfloat16)
+    r2 = torch.randn(B, H, W, C, generator=g).to(torch.bfloat16)
+    xq, wq = _q(x).to(gpu), _q(w).to(gpu)
+    xn = x.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous().to(gpu)
+    wp = w.permute(0, 2, 3, 1).reshape(C, -1).to(torch.bfloat16).contiguous().to(gpu)
+    r1g, r2g = r1.to(gpu), r2.to(gpu)
+    for relu, res in ((True, False), (True, True), (False, True)):
+        ref = F.conv2d(F.relu(xq) if relu else xq, wq, b.to(gpu), padding=1).permute(0, 2, 3, 1)
+        if res:
+            ref = ref + r1g.float() + r2g.float()
+        kw = dict(relu_in=relu, res=r1g if res else None, res2=r2g if res else None)
+        monkeypatch.delenv("SD_CONV_BIG", raising=False)
+        got = _lib.conv3x3(xn, wp, b.to(gpu), **kw).float()
+        monkeypatch.setenv("SD_CONV_BIG", "0")
+        old = _lib.conv3x3(xn, wp, b.to(gpu), **kw).float()
+        torch.cuda.synchronize()
+        tol = 2e-2 * ref.abs().max().item()
+        assert (got - ref).abs().max().item() <= tol, (relu, res)
+        assert (got - old).abs().max().item() <= tol, (relu, res)
