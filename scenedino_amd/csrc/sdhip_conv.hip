@@ -53,8 +53,11 @@ __device__ __forceinline__ bf16x8 cv_relu8(bf16x8 v) {
 
 template <int BM, int BN>
 __host__ __device__ constexpr int cv_stage_bytes() { return (BM + BN) * CV_BK * 2; }
+// CV_RELU_LDS = 1: rectify the A chunks once in LDS (one step ahead) instead of on every
+// fragment read; measured slower on the 48x160 residual units (30.5 vs 25.1 us, one step
+// less in flight and the extra LDS pass on the critical path), so off
 #ifndef CV_RELU_LDS
-#define CV_RELU_LDS 1
+#define CV_RELU_LDS 0
 #endif
 #ifndef CV_CHUNK_MAJOR
 #define CV_CHUNK_MAJOR 1
@@ -281,12 +284,41 @@ __global__ void __launch_bounds__(512) k_conv_big(sd_gemm_args g) {
                         *(__bf16 *)(reg + r * PITCH + (16 * j + fr) * 2) = (__bf16)v;
                 }
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        // the wave stores its own ER x WN block: lane -> (row, chunk of CC columns)
+        // the wave stores its own ER x WN block: lane -> (row, chunk of CC columns); the
+        // lane's chunk (so its columns) is the same in every iteration, its row advances by
+        // 64 / CPRW
+        // SHUF: the lane's (image, y, x) of its first row by two divides, then stepped; its
+        // sub-pixel and channel once (per-chunk 64-bit divides made the epilogue VALU-bound)
+        uint32_t sb = 0, sy = 0, sx = 0, soff = 0;
+        if (EPI == SD_EPI_SHUF) {
+            const uint32_t kk = (uint32_t)g.shuf_k, iw = (uint32_t)g.in_w, ih = (uint32_t)g.in_h;
+            const uint32_t cout = (uint32_t)(g.N / (kk * kk));
+            const uint32_t m_first = (uint32_t)(m0 + wm * WM + part * ER + lane / CPRW);
+            sb = m_first / (ih * iw);
+            const uint32_t pix = m_first - sb * ih * iw;
+            sy = pix / iw;
+            sx = pix - sy * iw;
+            const uint32_t n = (uint32_t)(n0 + wn * WN + (lane % CPRW) * CC);
+            const uint32_t sub = n / cout, co = n - sub * cout, dy = sub / kk, dx = sub - dy * kk;
+            soff = dy * iw * kk * cout + dx * cout + co;  // offset of (dy, dx, co) from pixel (y kk, x kk)
+        }
 #pragma unroll
         for (int it = 0; it < ER * CPRW / 64; ++it) {
             const int idx = it * 64 + lane, r = idx / CPRW, ch = idx - r * CPRW;
             const int64_t m = m0 + wm * WM + part * ER + r;
             const int64_t n = n0 + wn * WN + ch * CC;
+            int64_t sbase = 0;
+            if (EPI == SD_EPI_SHUF) {
+                if (it) {  // advance the row by 64 / CPRW pixels
+                    sx += 64 / CPRW;
+                    while (sx >= (uint32_t)g.in_w) {
+                        sx -= (uint32_t)g.in_w;
+                        if (++sy == (uint32_t)g.in_h) sy = 0, ++sb;
+                    }
+                }
+                const int64_t kk = g.shuf_k;
+                sbase = (((int64_t)sb * g.in_h + sy) * kk * g.in_w + sx) * kk * (g.N / (kk * kk)) + soff;
+            }
             if (m >= g.M || n >= g.N) continue;
             uint4 v;
             if (STF32 && !OUTF32) {  // f32 staging, residuals added before the bf16 rounding
@@ -312,17 +344,237 @@ __global__ void __launch_bounds__(512) k_conv_big(sd_gemm_args g) {
             } else {
                 v = *(const uint4 *)(reg + r * PITCH + ch * 16);
             }
-            int64_t base = m * g.ldo + n;  // element index of (m, n)
-            if (EPI == SD_EPI_SHUF) {  // 8 columns inside one sub-pixel (cout % 8 == 0)
-                const int kk = g.shuf_k, hw = g.in_h * g.in_w, cout = (int)(g.N / (kk * kk));
-                const int b = (int)((uint32_t)m / (uint32_t)hw);
-                const int pix = (int)(m - (int64_t)b * hw);
-                const int y = pix / g.in_w, x = pix - y * g.in_w;
-                const int sub = (int)(n / cout), co = (int)(n - (int64_t)sub * cout);
-                const int dy = sub / kk, dx = sub - dy * kk;
-                base = (((int64_t)b * g.in_h * kk + y * kk + dy) * (g.in_w * kk) + x * kk + dx) * cout + co;
-            }
+            // element index of (m, n); SHUF: 8 columns inside one sub-pixel (cout % 8 == 0)
+            const int64_t base = EPI == SD_EPI_SHUF ? sbase : m * g.ldo + n;
             *(uint4 *)((uint8_t *)g.out + base * (OUTF32 ? 4 : 2)) = v;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Halo tiles: 2-D output tiles of 8 rows x TW pixels for the 3x3 convolutions.  k_conv_big
+// streams the im2col rows, so every input pixel crosses L2 -> LDS 9 times per column tile
+// (once per tap; PMC: the DPT's 3x3 layers run at ~35 GB/s per CU, bound by the bytes each
+// CU keeps in flight, not by the MFMA).  Here each 64-channel chunk of the tile's input
+// halo ((8 + 2) x (TW + 2) pixels) is DMA'd into LDS once and the 9 taps read it shifted;
+// only the weight tile is streamed per tap (a ring of RSB stages).  K order: chunk major,
+// tap minor.  Per-thread halo offsets are fixed for the tile (the chunk's channel offset
+// goes in the DMA's scalar offset).  Same 8-wave 2 x 4 MFMA layout, ReLU (on the halo, in
+// LDS, once per chunk) and epilogues as k_conv_big.
+#define CVH_TH 8
+#ifndef CV_HALO
+#define CV_HALO 1
+#endif
+template <int TW>
+__host__ __device__ constexpr int cvh_hpix() { return (CVH_TH + 2) * (TW + 2); }
+template <int TW>
+__host__ __device__ constexpr int cvh_ha() { return (cvh_hpix<TW>() * 8 + 511) / 512; }  // halo DMAs / thread
+template <int TW>
+__host__ __device__ constexpr int cvh_halo_bytes() { return cvh_ha<TW>() * 512 * 16; }
+template <int TW, int BN>
+__host__ __device__ constexpr int cvh_rsb() {
+    return (CV_LDS_MAX - 2 * cvh_halo_bytes<TW>()) / (BN * 128) >= 6 ? 6 : (CV_LDS_MAX - 2 * cvh_halo_bytes<TW>()) / (BN * 128);
+}
+template <int TW, int BN, bool STF32>
+__host__ __device__ constexpr int cvh_lds_bytes() {
+    return 2 * cvh_halo_bytes<TW>() + cvh_rsb<TW, BN>() * BN * 128 > 8 * cv_epi_rows<CVH_TH * TW, BN, STF32>() * cv_epi_pitch<BN, STF32>()
+               ? 2 * cvh_halo_bytes<TW>() + cvh_rsb<TW, BN>() * BN * 128
+               : 8 * cv_epi_rows<CVH_TH * TW, BN, STF32>() * cv_epi_pitch<BN, STF32>();
+}
+// s_waitcnt vmcnt(n) for a runtime n (the count of this thread's younger DMAs)
+__device__ __forceinline__ void cv_vmcnt(int n) {
+#define CVW(i) case i: asm volatile("s_waitcnt vmcnt(" #i ")" ::: "memory"); break;
+    switch (n) {
+        CVW(1) CVW(2) CVW(3) CVW(4) CVW(5) CVW(6) CVW(7) CVW(8) CVW(9) CVW(10) CVW(11) CVW(12)
+        CVW(13) CVW(14) CVW(15) CVW(16)
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+#undef CVW
+}
+
+template <int TW, int BN, int EPI, bool RELU, bool RES>
+__global__ void __launch_bounds__(512) k_conv_halo(sd_gemm_args g) {
+    constexpr bool OUTF32 = EPI == SD_EPI_F32, STF32 = OUTF32 || RES;
+    constexpr int TH = CVH_TH, BM = TH * TW, HW2 = TW + 2;
+    constexpr int HP = cvh_hpix<TW>(), HA = cvh_ha<TW>(), HB = cvh_halo_bytes<TW>();
+    constexpr int RSB = cvh_rsb<TW, BN>(), SBB = BN * 128;
+    constexpr int WM = BM / 2, WN = BN / 4, TI = WM / 16, TJ = WN / 16;
+    constexpr int CB = BN * 8 / 512;
+    static_assert(CB >= 1 && TJ >= 1 && RSB >= 2 && TW % 16 == 0 && (RSB - 2) * CB + HA <= 16, "halo tile shape");
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2, wn = wave & 3;
+    const int txn = (g.OW + TW - 1) / TW, tyn = (g.OH + TH - 1) / TH;
+    const int tile = blockIdx.x, b = tile / (txn * tyn), trem = tile - b * txn * tyn;
+    const int ty = trem / txn, tx = trem - ty * txn;
+    const int y0 = ty * TH, x0 = tx * TW;
+    const int64_t n0 = (int64_t)blockIdx.y * BN;
+    const int nch = g.Cin / CV_BK, nk = 9 * nch;
+    const int64_t a_bytes = (g.M / ((int64_t)g.OH * g.OW)) * g.H * g.W * g.Cin * 2;
+    const __amdgpu_buffer_rsrc_t rsA =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(g.a), 0, (uint32_t)a_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<void *>(g.w), 0, (uint32_t)(g.N * g.K * 2), 0x00020000);
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void *)smem;
+    const uint32_t ldsB = lds0 + 2 * HB;
+
+    // halo DMA chunks: wave instruction q = 8 h + wave fills LDS bytes [1024 q, + 1024) of
+    // the halo buffer = halo pixels 8 q .. 8 q + 7; lane -> pixel 8 q + lane / 8, slot
+    // lane % 8 (holding source chunk cv_swz(pixel, slot)); pixels past the halo and outside
+    // the image read as zeros
+    uint32_t voH[HA];
+#pragma unroll
+    for (int q = 0; q < HA; ++q) {
+        const int hp = 8 * (8 * q + wave) + (lane >> 3);
+        const int hr = hp / HW2, hc = hp - hr * HW2;
+        const int y = y0 - 1 + hr, x = x0 - 1 + hc;
+        const bool ok = hp < HP && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W;
+        voH[q] = ok ? (uint32_t)((((int64_t)b * g.H + y) * g.W + x) * g.Cin * 2) + (uint32_t)cv_swz(hp, lane & 7) * 16u
+                    : 0x80000000u;
+    }
+    uint32_t voB[CB];
+#pragma unroll
+    for (int c = 0; c < CB; ++c) {
+        const int row = 8 * (8 * c + wave) + (lane >> 3);
+        voB[c] = (uint32_t)((min(n0 + row, g.N - 1) * g.K) * 2) + (uint32_t)cv_swz(row, lane & 7) * 16u;
+    }
+    // group s: the weight tile of step s (+ the halo of chunk s / 9 when s starts a chunk)
+    auto issue = [&](int s) {
+        const int chunk = s / 9, tap = s - 9 * chunk, ci0 = chunk * CV_BK;
+        const uint32_t kb = (uint32_t)(tap * g.Cin + ci0) * 2u;
+#pragma unroll
+        for (int c = 0; c < CB; ++c)
+            cv_dma16s(rsB, voB[c], kb, ldsB + (uint32_t)(s % RSB) * SBB + (uint32_t)(8 * c + wave) * 1024u);
+        if (tap == 0) {
+#pragma unroll
+            for (int q = 0; q < HA; ++q)
+                cv_dma16s(rsA, voH[q], (uint32_t)ci0 * 2u, lds0 + (uint32_t)(chunk & 1) * HB + (uint32_t)(8 * q + wave) * 1024u);
+        }
+    };
+    auto group_size = [&](int s) { return CB + (s % 9 == 0 ? HA : 0); };
+
+    cvf4 acc[TI][TJ];
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) acc[i][j] = cvf4{0.f, 0.f, 0.f, 0.f};
+    const int fr = lane & 15, fk = lane >> 4;
+    // the lane's fragment pixels: tile row / column of pixel wm WM + 16 i + fr
+    int prow[TI], pcol[TI];
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+        const int q = wm * WM + 16 * i + fr;
+        prow[i] = q / TW;
+        pcol[i] = q - prow[i] * TW;
+    }
+
+#pragma unroll
+    for (int i = 0; i < RSB - 1; ++i)
+        if (i < nk) issue(i);
+    for (int s = 0; s < nk; ++s) {
+        int younger = 0;  // this thread's DMAs issued after group s
+        for (int u = s + 1; u <= min(s + RSB - 2, nk - 1); ++u) younger += group_size(u);
+        cv_vmcnt(younger);
+        const int chunk = s / 9, tap = s - 9 * chunk;
+        const uint8_t *hb = smem + (chunk & 1) * HB;
+        if (RELU && tap == 0) {  // rectify this thread's halo chunks once (the barrier publishes)
+#pragma unroll
+            for (int q = 0; q < HA; ++q) {
+                bf16x8 *p = (bf16x8 *)(smem + (chunk & 1) * HB + (8 * q + wave) * 1024 + lane * 16);
+                *p = cv_relu8(*p);
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (s + RSB - 1 < nk) issue(s + RSB - 1);
+        const int ky = tap / 3, kx = tap - 3 * ky;
+        const uint8_t *sb = smem + 2 * HB + (s % RSB) * SBB;
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+            const int kc = 4 * h2 + fk;
+            bf16x8 af[TI], bfr[TJ];
+#pragma unroll
+            for (int i = 0; i < TI; ++i) {
+                const int hp = (prow[i] + ky) * HW2 + pcol[i] + kx;
+                af[i] = *(const bf16x8 *)(hb + hp * 128 + 16 * cv_swz(hp, kc));
+            }
+#pragma unroll
+            for (int j = 0; j < TJ; ++j) {
+                const int row = wn * WN + 16 * j + fr;
+                bfr[j] = *(const bf16x8 *)(sb + row * 128 + 16 * cv_swz(row, kc));
+            }
+#pragma unroll
+            for (int i = 0; i < TI; ++i)
+#pragma unroll
+                for (int j = 0; j < TJ; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+
+    // ---- epilogue (k_conv_big's, with the 2-D tile's pixel -> row map) ----
+    float bias[TJ];
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+        const int64_t n = min(n0 + wn * WN + 16 * j + fr, g.N - 1);
+        bias[j] = g.bias ? g.bias[n] : 0.f;
+    }
+    constexpr int ER = cv_epi_rows<BM, BN, STF32>(), PITCH = cv_epi_pitch<BN, STF32>();
+    constexpr int CC = OUTF32 ? 4 : 8;
+    constexpr int CPRW = WN / CC;
+    static_assert((ER * CPRW) % 64 == 0, "epilogue chunking");
+    uint8_t *reg = smem + wave * ER * PITCH;
+#pragma unroll
+    for (int part = 0; part < WM / ER; ++part) {
+        if (part) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll
+        for (int i = part * (ER / 16); i < (part + 1) * (ER / 16); ++i)
+#pragma unroll
+            for (int j = 0; j < TJ; ++j)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int r = 16 * i + 4 * fk + e - part * ER;
+                    const float v = acc[i][j][e] + bias[j];
+                    if (STF32)
+                        *(float *)(reg + r * PITCH + (16 * j + fr) * 4) = v;
+                    else
+                        *(__bf16 *)(reg + r * PITCH + (16 * j + fr) * 2) = (__bf16)v;
+                }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll
+        for (int it = 0; it < ER * CPRW / 64; ++it) {
+            const int idx = it * 64 + lane, r = idx / CPRW, ch = idx - r * CPRW;
+            const int q = wm * WM + part * ER + r;  // tile pixel
+            const int y = y0 + q / TW, x = x0 + q % TW;
+            const int64_t n = n0 + wn * WN + ch * CC;
+            if (y >= g.OH || x >= g.OW || n >= g.N) continue;
+            const int64_t m = ((int64_t)b * g.OH + y) * g.OW + x;
+            uint4 v;
+            if (STF32 && !OUTF32) {
+                const cvf4 lo = *(const cvf4 *)(reg + r * PITCH + ch * 32);
+                const cvf4 hi = *(const cvf4 *)(reg + r * PITCH + ch * 32 + 16);
+                float f[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                if (RES) {
+                    if (g.res) {
+                        const bf16x8 a = *(const bf16x8 *)((const __bf16 *)g.res + m * g.ldo + n);
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) f[u] += (float)a[u];
+                    }
+                    if (g.res2) {
+                        const bf16x8 a = *(const bf16x8 *)((const __bf16 *)g.res2 + m * g.ldo + n);
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) f[u] += (float)a[u];
+                    }
+                }
+                bf16x8 o;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) o[u] = (__bf16)f[u];
+                v = __builtin_bit_cast(uint4, o);
+            } else {
+                v = *(const uint4 *)(reg + r * PITCH + ch * 16);
+            }
+            *(uint4 *)((uint8_t *)g.out + (m * g.ldo + n) * (OUTF32 ? 4 : 2)) = v;
         }
     }
 }
@@ -357,6 +609,45 @@ int sd_conv_big_try(const sd_gemm_args *args, void *stream) {
     const int64_t a_bytes = g.conv ? (g.M / ((int64_t)g.OH * g.OW)) * g.H * g.W * g.Cin * 2 : g.M * g.lda * 2;
     if (a_bytes >= ((int64_t)1 << 31) || g.N * g.K * 2 >= ((int64_t)1 << 31)) return 0;
     const int64_t ncu = sd_num_cus();
+    hipStream_t s = (hipStream_t)stream;
+    if (g.conv && CV_HALO && !(e && e[0] == 'b')) {  // SD_CONV_BIG=b: the im2col tiles only
+        const int64_t nb = g.M / ((int64_t)g.OH * g.OW);
+        auto htiles = [&](int tw, int bn) {
+            return g.N % bn ? 0 : nb * ((g.OH + CVH_TH - 1) / CVH_TH) * ((g.OW + tw - 1) / tw) * (g.N / bn);
+        };
+        // 8 x 32 halo tiles where the im2col tiles would be 256 x 128 (96x320: 43.5 vs 47.8
+        // us); the 192x640 layer keeps the 256 x 256 im2col tiles (143 vs 161 us with 128-
+        // column halo tiles) and the 48x160 residual units the 128 x 64 ones (25 vs 34 us with
+        // 8 x 16 halo tiles; tools/dpt_ops_bench.py, profiles/r4_dpt_ops.txt)
+        int tw = 0, hbn = 0;
+        const int64_t t256 = ((g.M + 255) / 256) * (g.N % 256 ? 0 : g.N / 256);
+        if (t256 < ncu * 15 / 8 && g.OW >= 32 && htiles(32, 128) >= ncu * 7 / 8) tw = 32, hbn = 128;
+        if (tw) {
+            auto hgo = [&](auto kern, int lds) {
+                (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+                hipLaunchKernelGGL(kern, dim3((unsigned)(htiles(tw, hbn) / (g.N / hbn)), (unsigned)(g.N / hbn)),
+                                   dim3(512), lds, s, g);
+            };
+#define CVH_K(TW_, BN_, E, R, RS_) hgo(k_conv_halo<TW_, BN_, E, R, RS_>, cvh_lds_bytes<TW_, BN_, E == SD_EPI_F32 || RS_>())
+#define CVH_TILE(TW_, BN_)                                                                           \
+            if (tw == TW_) {                                                                         \
+                if (g.epi == SD_EPI_F32) {                                                           \
+                    if (g.relu_in) CVH_K(TW_, BN_, SD_EPI_F32, true, false);                         \
+                    else CVH_K(TW_, BN_, SD_EPI_F32, false, false);                                  \
+                } else if (res) {                                                                    \
+                    if (g.relu_in) CVH_K(TW_, BN_, SD_EPI_BF16, true, true);                         \
+                    else CVH_K(TW_, BN_, SD_EPI_BF16, false, true);                                  \
+                } else {                                                                             \
+                    if (g.relu_in) CVH_K(TW_, BN_, SD_EPI_BF16, true, false);                        \
+                    else CVH_K(TW_, BN_, SD_EPI_BF16, false, false);                                 \
+                }                                                                                    \
+            }
+            CVH_TILE(32, 128)
+#undef CVH_TILE
+#undef CVH_K
+            return hipGetLastError() == hipSuccess ? 1 : -2;
+        }
+    }
     auto tiles = [&](int bm, int bn) { return g.N % bn ? 0 : ((g.M + bm - 1) / bm) * (g.N / bn); };
     int bm, bn;
     if (tiles(256, 256) >= ncu * 15 / 8) bm = 256, bn = 256;
@@ -364,7 +655,6 @@ int sd_conv_big_try(const sd_gemm_args *args, void *stream) {
     else if (tiles(128, 128) >= ncu * 7 / 8) bm = 128, bn = 128;
     else if (tiles(128, 64) >= ncu * 7 / 8) bm = 128, bn = 64;
     else return 0;
-    hipStream_t s = (hipStream_t)stream;
     auto go = [&](auto kern, int lds) {
         (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         hipLaunchKernelGGL(kern, dim3((unsigned)((g.M + bm - 1) / bm), (unsigned)(g.N / bn)), dim3(512), lds, s, g);

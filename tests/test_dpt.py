@@ -147,10 +147,10 @@ def test_dpt_head_vs_reference(gpu):
 @pytest.mark.parametrize("B,H,W,Cin,Cout,f32", [(1, 96, 320, 256, 256, False), (1, 192, 640, 256, 256, True),
                                                 (1, 192, 640, 256, 256, False), (2, 61, 250, 128, 384, True)])
 def test_conv3x3_big_tiles(gpu, B, H, W, Cin, Cout, f32, monkeypatch):
-    """The 256-row LDS-DMA tiles of sdhip_conv.hip (the DPT head's 96x320 / 192x640
-    convolutions; 2 x 61 x 250 with Cout 384: ragged last tile, 128-column tiles, two
-    images' padding) against torch fp32 on the same bf16 operands, and against sd_gemm's
-    k_gemm path on the same inputs (SD_CONV_BIG=0)."""
+    """sdhip_conv.hip's tiles for the DPT head's 96x320 / 192x640 convolutions -- the 8 x 32
+    halo tiles (default) and the 256-row im2col tiles (SD_CONV_BIG=b); 2 x 61 x 250 with
+    Cout 384: ragged edge tiles, 128-column tiles, two images' padding -- against torch fp32
+    on the same bf16 operands and against sd_gemm's k_gemm path (SD_CONV_BIG=0)."""
     from scenedino_amd import _lib
     g = torch.Generator().manual_seed(H + W + Cout)
     x = torch.randn(B, Cin, H, W, generator=g)
@@ -161,15 +161,18 @@ def test_conv3x3_big_tiles(gpu, B, H, W, Cin, Cout, f32, monkeypatch):
     wp = w.permute(0, 2, 3, 1).reshape(Cout, -1).to(torch.bfloat16).contiguous().to(gpu)
     epi = _lib.SD_EPI_F32 if f32 else _lib.SD_EPI_BF16
     ref = F.conv2d(xq, wq, b.to(gpu), padding=1).permute(0, 2, 3, 1)
-    got = _lib.conv3x3(xn, wp, b.to(gpu), epi=epi).float()
+    got = _lib.conv3x3(xn, wp, b.to(gpu), epi=epi).float()  # halo tiles where they fit
+    monkeypatch.setenv("SD_CONV_BIG", "b")
+    im2col = _lib.conv3x3(xn, wp, b.to(gpu), epi=epi).float()  # 256-row im2col tiles
     monkeypatch.setenv("SD_CONV_BIG", "0")
     old = _lib.conv3x3(xn, wp, b.to(gpu), epi=epi).float()
     torch.cuda.synchronize()
     scale = ref.abs().max().item()
     tol = (1e-3 if f32 else 2e-2) * scale  # f32 out: fp32 accumulation order only
-    assert (got - ref).abs().max().item() <= tol
-    assert (got - old).abs().max().item() <= tol
-    assert torch.isfinite(got).all()
+    for t in (got, im2col):
+        assert (t - ref).abs().max().item() <= tol
+        assert (t - old).abs().max().item() <= tol
+        assert torch.isfinite(t).all()
 
 
 @pytest.mark.gpu
@@ -206,8 +209,9 @@ def test_linear_big_tiles(gpu, B, H, W, Cin, Cout, k, monkeypatch):
 @pytest.mark.gpu
 @pytest.mark.parametrize("B,H,W,C", [(1, 48, 160, 256), (2, 61, 130, 128)])
 def test_conv3x3_big_tiles_residual_unit(gpu, B, H, W, C, monkeypatch):
-    """The residual conv units' convolutions on sdhip_conv.hip's 128-row tiles (48x160: 240
-    tiles of 128 x 64): pre-activation ReLU on the input, the two bf16 residuals added
+    """The residual conv units' convolutions on sdhip_conv.hip's 128-row im2col tiles
+    (48x160: 240 tiles of 128 x 64; the default and SD_CONV_BIG=b agree here): pre-activation
+    ReLU, the two bf16 residuals added
     before the output rounding (dpt_head.py PreActResidualConvUnit / FeatureFusionBlock),
     against torch fp32 and the k_gemm path (SD_CONV_BIG=0)."""
     from scenedino_amd import _lib
@@ -227,10 +231,13 @@ def test_conv3x3_big_tiles_residual_unit(gpu, B, H, W, C, monkeypatch):
             ref = ref + r1g.float() + r2g.float()
         kw = dict(relu_in=relu, res=r1g if res else None, res2=r2g if res else None)
         monkeypatch.delenv("SD_CONV_BIG", raising=False)
-        got = _lib.conv3x3(xn, wp, b.to(gpu), **kw).float()
+        got = _lib.conv3x3(xn, wp, b.to(gpu), **kw).float()  # halo tiles
+        monkeypatch.setenv("SD_CONV_BIG", "b")
+        im2col = _lib.conv3x3(xn, wp, b.to(gpu), **kw).float()  # 128-row im2col tiles
         monkeypatch.setenv("SD_CONV_BIG", "0")
         old = _lib.conv3x3(xn, wp, b.to(gpu), **kw).float()
         torch.cuda.synchronize()
         tol = 2e-2 * ref.abs().max().item()
-        assert (got - ref).abs().max().item() <= tol, (relu, res)
-        assert (got - old).abs().max().item() <= tol, (relu, res)
+        for t in (got, im2col):
+            assert (t - ref).abs().max().item() <= tol, (relu, res)
+            assert (t - old).abs().max().item() <= tol, (relu, res)
