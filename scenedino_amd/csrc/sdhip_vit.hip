@@ -142,7 +142,7 @@ __device__ __forceinline__ bf16x8 vt_relu8(bf16x8 v) {
 // epilogue.  Four times the workgroups of the 64x64 tiling, a quarter of the MFMA chain per
 // wave.
 template <int BM, int BN, int BK, int EPI, bool CONV>
-__global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
+__global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g, float *__restrict__ sk_slab, uint32_t *__restrict__ sk_cnt) {
     constexpr bool SK = BM == 32;
     static_assert(!SK || (BN == 32 && BK % 64 == 0), "split-K tile: 32x32, BK multiple of 64");
     constexpr int WM = SK ? 32 : BM / 2, WN = SK ? 32 : BN / 2;  // per-wave tile (2 x 2 waves)
@@ -176,7 +176,11 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
     const int64_t m0 = (int64_t)blockIdx.y * BM, n0 = (int64_t)blockIdx.x * BN;
     const __bf16 *A = (const __bf16 *)g.a;
     const __bf16 *Wt = (const __bf16 *)g.w;
-    const int nk = (int)(g.K / BK);
+    // cross-workgroup split-K (32 x 32 ring tiles, gridDim.z > 1): this workgroup's K steps
+    // [kbeg, kbeg + nk) of the K / BK
+    const int nk_all = (int)(g.K / BK), nzs = (int)gridDim.z, zs = (int)blockIdx.z;
+    const int kbeg = (int)((int64_t)nk_all * zs / nzs);
+    const int nk = (int)((int64_t)nk_all * (zs + 1) / nzs) - kbeg;
 
     // NS register staging sets (a ring): step k's compute runs while the tiles of steps
     // k + 1 .. k + NS - 1 are in flight; step k + 1's tile goes to LDS after step k's
@@ -357,7 +361,7 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
         // issue stage kt (steps past the last re-load step nk - 1 into their free slot, so
         // that every step issues CA + CB DMAs and the vmcnt count below is exact)
         auto issue = [&](int kt) {
-            const int k = min(kt, nk - 1);
+            const int k = kbeg + min(kt, nk - 1);
             const uint32_t st = lds0 + (uint32_t)(kt % RS) * STB;
             if (CONV) {
                 const int k0 = k * BK;
@@ -453,6 +457,39 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g) {
             for (int w = 0; w < 3; ++w)
 #pragma unroll
                 for (int q = 0; q < 16; ++q) acc[0][0][q] += part[(w * 16 + q) * 64 + lane];
+        }
+        if (RING && nzs > 1) {
+            // cross-workgroup combine, deterministic: every K slice writes its 32 x 32 partial
+            // (write-through sc1 stores: no release fence), takes a ticket; the last arriver
+            // sums the slices in slice order (sc1 loads), resets the ticket for the next
+            // launch and runs the epilogue (MI355X guide §5, split-K reduction recipe)
+            const int tile = blockIdx.y * gridDim.x + blockIdx.x;
+            float *slab = sk_slab + (int64_t)tile * nzs * 1024;
+            if (wave == 0) {
+#pragma unroll
+                for (int q = 0; q < 16; ++q)
+                    __hip_atomic_store(slab + zs * 1024 + q * 64 + lane, acc[0][0][q], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            __syncthreads();
+            uint32_t *flag = (uint32_t *)smem;
+            if (tid == 0)
+                *flag = __hip_atomic_fetch_add(sk_cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                        (uint32_t)(nzs - 1);
+            __syncthreads();
+            if (!*flag) return;  // workgroup-uniform
+            if (wave == 0) {
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    float v = 0.f;
+                    for (int z = 0; z < nzs; ++z)
+                        v += __hip_atomic_load(slab + z * 1024 + q * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    acc[0][0][q] = v;
+                }
+            }
+            if (tid == 0) __hip_atomic_store(sk_cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __syncthreads();  // the flag word is part of the epilogue's LDS
         }
         if constexpr (!STAGED) {
             if (wave != 0) return;
@@ -1360,16 +1397,50 @@ __global__ void __launch_bounds__(256) k_lngemm(sd_gemm_args g, const float *__r
 // ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
+// cross-workgroup split-K workspace (per device, allocated once outside graph capture):
+// 32 x 32 f32 partials and self-resetting tickets (zeroed at allocation)
+#define VT_SK_SLABS 2048
+#define VT_SK_TILES 4096
+struct VtSplitWs {
+    float *slab = nullptr;
+    uint32_t *cnt = nullptr;
+};
+static bool vt_split_ws(hipStream_t s, VtSplitWs &w) {
+    static VtSplitWs ws[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
+    if (!ws[dev].slab) {
+        hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return false;
+        float *p = nullptr;
+        uint32_t *c = nullptr;
+        if (hipMalloc((void **)&p, (size_t)VT_SK_SLABS * 4096) != hipSuccess) return false;
+        if (hipMalloc((void **)&c, (size_t)VT_SK_TILES * 4) != hipSuccess ||
+            hipMemset(c, 0, (size_t)VT_SK_TILES * 4) != hipSuccess) {
+            (void)hipFree(p);
+            return false;
+        }
+        ws[dev].slab = p;
+        ws[dev].cnt = c;
+    }
+    w = ws[dev];
+    return true;
+}
+
 template <int BM, int BN, int BK, bool CONV>
-static void vt_launch_gemm(const sd_gemm_args &g, hipStream_t s) {
+static void vt_launch_gemm(const sd_gemm_args &g, hipStream_t s, int ksplit = 1) {
     dim3 grid((unsigned)((g.N + BN - 1) / BN), (unsigned)((g.M + BM - 1) / BM));
+    VtSplitWs w;
+    if (ksplit > 1 && vt_ring_tile(BM) && (int64_t)grid.x * grid.y <= VT_SK_TILES &&
+        (int64_t)grid.x * grid.y * ksplit <= VT_SK_SLABS && vt_split_ws(s, w))
+        grid.z = (unsigned)ksplit;
     // the ring kernels take their LDS dynamically (the ring, reused by the epilogue: > 64 KiB
     // for the 128 x 128 tiles)
     constexpr int ep = BM * (BN + 8) * 4;  // the widest staged epilogue tile (k_gemm's OST)
     const int lds = vt_ring_tile(BM) ? (vt_ring_bytes<BM, BN, BK>() > ep ? vt_ring_bytes<BM, BN, BK>() : ep) : 0;
     auto go = [&](auto kern) {
         if (lds) (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, g);
+        hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, g, w.slab, w.cnt);
     };
     switch (g.epi) {
     case SD_EPI_BF16: go(k_gemm<BM, BN, BK, SD_EPI_BF16, CONV>); break;
@@ -1427,14 +1498,24 @@ static void vt_pick_gemm(const sd_gemm_args &g, hipStream_t s) {
     // convolutions: 120) take 256-deep K steps: half the dependent ring steps per tile, a
     // 128-KiB ring (one tile per CU is all there is anyway)
     const int64_t t32 = ((g.M + 31) / 32) * ((g.N + 31) / 32);
+    // and, where the tiles leave most CUs idle, their K range split over workgroups
+    // (deterministic last-arriver combine): the largest of 2, 4, 8 slices keeping
+    // tiles x slices <= SD_SPLITK_WG (default 2 per CU) and >= 2 K steps per slice
+    auto ksplit = [&](int bk) {
+        const char *e = getenv("SD_SPLITK_WG");
+        const int64_t cap = (e && e[0]) ? atoll(e) : 2 * (int64_t)sd_num_cus();
+        int ks = 1;
+        while (ks < 8 && t32 * ks * 2 <= cap && g.K / bk >= 4 * ks) ks *= 2;
+        return ks;
+    };
     if (VT_SK256 && VT_RING && t32 <= (int64_t)sd_num_cus() && g.K % 256 == 0 &&
         (CONV ? g.Cin % 256 == 0 && mid < SD_CONV_SK_MID : mid < 256)) {
-        vt_launch_gemm<32, 32, 256, CONV>(g, s);
+        vt_launch_gemm<32, 32, 256, CONV>(g, s, ksplit(256));
         return;
     }
     if ((CONV ? g.Cin % 128 == 0 && mid < SD_CONV_SK_MID : mid < 256) && g.K % 128 == 0 &&
         g.K >= 256) {
-        vt_launch_gemm<32, 32, 128, CONV>(g, s);  // split-K over the 4 waves
+        vt_launch_gemm<32, 32, 128, CONV>(g, s, ksplit(128));  // split-K over the 4 waves
         return;
     }
     // 128x128 tiles need about two per CU, or one per CU with a long K loop to amortise

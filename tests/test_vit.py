@@ -109,6 +109,48 @@ def test_gemm_epilogues(gpu, M, N, K):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(481, 384, 1536), (481, 384, 1024), (97, 64, 2048)])
+def test_gemm_cross_workgroup_split_k(gpu, M, N, K, monkeypatch):
+    """32 x 32 tiles whose K range is split over workgroups (ViT-S/16 fc2 at 481 tokens: two
+    slices; the last arriver sums the slices' f32 partials in slice order): every epilogue
+    equals the f32 product within the single-workgroup tolerance, the result is
+    bit-identical across launches (deterministic combine, self-resetting tickets), and
+    SD_SPLITK_WG=0 (no split) agrees."""
+    from scenedino_amd import _lib
+    g = torch.Generator().manual_seed(M + K)
+    a = _bf(torch.randn(M, K, generator=g)).to(gpu)
+    w = _bf(torch.randn(N, K, generator=g) / math.sqrt(K)).to(gpu)
+    bias = (0.1 * torch.randn(N, generator=g)).to(gpu)
+    ref = a.float() @ w.float().t() + bias
+    scale = ref.abs().max().item()
+    res = torch.randn(M, N, generator=g).to(gpu)
+    gam = torch.rand(N, generator=g).to(gpu)
+
+    def run():
+        out = torch.empty(M, N, device=gpu)
+        _lib.gemm(a, w, bias, _lib.SD_EPI_F32, out=out)
+        x = res.clone()
+        _lib.gemm(a, w, bias, _lib.SD_EPI_RESID, out=x, gamma=gam)
+        ob = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+        _lib.gemm(a, w, bias, _lib.SD_EPI_GELU, out=ob)
+        torch.cuda.synchronize()
+        return out, x, ob
+
+    runs = [run() for _ in range(3)]
+    out, x, ob = runs[0]
+    assert (out - ref).abs().max().item() <= 1e-4 * scale + 1e-5
+    assert (x - (res + gam * ref)).abs().max().item() <= 1e-4 * scale + 1e-5
+    assert (ob.float() - F.gelu(ref)).abs().max().item() <= 8e-3 * scale
+    for r in runs[1:]:
+        for t0, t1 in zip(runs[0], r):
+            assert torch.equal(t0, t1)
+    monkeypatch.setenv("SD_SPLITK_WG", "0")
+    o1, x1, _ = run()
+    assert (o1 - out).abs().max().item() <= 1e-4 * scale + 1e-5
+    assert (x1 - x).abs().max().item() <= 1e-4 * scale + 1e-5
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("B,H,T", [(1, 6, 481), (2, 12, 77), (1, 12, 1921), (1, 1, 1),
                                    (4, 12, 1921)])
 @pytest.mark.parametrize("mode", ["auto", "lds", "dir", "2split"])
