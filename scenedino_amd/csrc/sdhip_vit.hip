@@ -1498,12 +1498,16 @@ static void vt_pick_gemm(const sd_gemm_args &g, hipStream_t s) {
     // convolutions: 120) take 256-deep K steps: half the dependent ring steps per tile, a
     // 128-KiB ring (one tile per CU is all there is anyway)
     const int64_t t32 = ((g.M + 31) / 32) * ((g.N + 31) / 32);
-    // and, where the tiles leave most CUs idle, their K range split over workgroups
-    // (deterministic last-arriver combine): the largest of 2, 4, 8 slices keeping
-    // tiles x slices <= SD_SPLITK_WG (default 2 per CU) and >= 2 K steps per slice
+    // and, where the tiles leave most CUs idle, optionally their K range split over
+    // workgroups (deterministic last-arriver combine): the largest of 2, 4, 8 slices keeping
+    // tiles x slices <= SD_SPLITK_WG and >= 2 K steps per slice.  Off by default: at 2 tiles
+    // per CU it ran 2.5x slower on the ViT-S/16 fc2 and the DPT's 12x40 convolutions (8.5 ->
+    // 21.5 us, 10.3 -> 25 us: one 128-KiB-ring tile per CU serialises the slices, and the
+    // write-through partials and tickets cost more than the shortened K loop saves;
+    // profiles/r4_splitk_ab.txt)
     auto ksplit = [&](int bk) {
         const char *e = getenv("SD_SPLITK_WG");
-        const int64_t cap = (e && e[0]) ? atoll(e) : 2 * (int64_t)sd_num_cus();
+        const int64_t cap = (e && e[0]) ? atoll(e) : 0;
         int ks = 1;
         while (ks < 8 && t32 * ks * 2 <= cap && g.K / bk >= 4 * ks) ks *= 2;
         return ks;

@@ -101,7 +101,7 @@ def test_conv3x3(gpu, B, H, W, Cin, Cout, stride):
     ref = F.conv2d(xq, wq, b, stride=stride, padding=1)
     out = _lib.conv3x3(xn, wp, b.to(gpu), stride=stride, epi=_lib.SD_EPI_NCHW)
     assert (out.cpu() - ref).abs().max().item() <= 1e-3 * ref.abs().max().item()
-    # 12x40 x 256: the K range split over 4 workgroups per tile; deterministic across launches
+    # deterministic across launches
     out2 = _lib.conv3x3(xn, wp, b.to(gpu), stride=stride, epi=_lib.SD_EPI_NCHW)
     assert torch.equal(out, out2)
 
