@@ -480,12 +480,16 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g, float *__restrict_
             __syncthreads();
             if (!*flag) return;  // workgroup-uniform
             if (wave == 0) {
+                // one slice per round trip: its 16 loads issued together, summed in slice order
 #pragma unroll
-                for (int q = 0; q < 16; ++q) {
-                    float v = 0.f;
-                    for (int z = 0; z < nzs; ++z)
-                        v += __hip_atomic_load(slab + z * 1024 + q * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    acc[0][0][q] = v;
+                for (int q = 0; q < 16; ++q) acc[0][0][q] = 0.f;
+                for (int z = 0; z < nzs; ++z) {
+                    float v[16];
+#pragma unroll
+                    for (int q = 0; q < 16; ++q)
+                        v[q] = __hip_atomic_load(slab + z * 1024 + q * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) acc[0][0][q] += v[q];
                 }
             }
             if (tid == 0) __hip_atomic_store(sk_cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1498,16 +1502,16 @@ static void vt_pick_gemm(const sd_gemm_args &g, hipStream_t s) {
     // convolutions: 120) take 256-deep K steps: half the dependent ring steps per tile, a
     // 128-KiB ring (one tile per CU is all there is anyway)
     const int64_t t32 = ((g.M + 31) / 32) * ((g.N + 31) / 32);
-    // and, where the tiles leave most CUs idle, optionally their K range split over
-    // workgroups (deterministic last-arriver combine): the largest of 2, 4, 8 slices keeping
-    // tiles x slices <= SD_SPLITK_WG and >= 2 K steps per slice.  Off by default: at 2 tiles
-    // per CU it ran 2.5x slower on the ViT-S/16 fc2 and the DPT's 12x40 convolutions (8.5 ->
-    // 21.5 us, 10.3 -> 25 us: one 128-KiB-ring tile per CU serialises the slices, and the
-    // write-through partials and tickets cost more than the shortened K loop saves;
-    // profiles/r4_splitk_ab.txt)
+    // and, where the tiles leave most CUs idle, their K range split over workgroups
+    // (deterministic last-arriver combine): the largest of 2, 4, 8 slices keeping
+    // tiles x slices <= SD_SPLITK_WG (default: one per CU) and >= 2 K steps per slice.
+    // Measured (profiles/r4_splitk_ab.txt, interleaved): at one tile per CU only the DPT's
+    // 12x40 convolutions split (2 slices; encode 1.16 -> 1.15 ms); at two per CU the
+    // ViT-S/16 fc2 splits too and runs slower (the 128-KiB-ring tiles no longer co-reside:
+    // ViT-S/16 0.576 -> 0.624 ms); SD_SPLITK_WG=0 turns it off
     auto ksplit = [&](int bk) {
         const char *e = getenv("SD_SPLITK_WG");
-        const int64_t cap = (e && e[0]) ? atoll(e) : 0;
+        const int64_t cap = (e && e[0]) ? atoll(e) : (int64_t)sd_num_cus();
         int ks = 1;
         while (ks < 8 && t32 * ks * 2 <= cap && g.K / bk >= 4 * ks) ks *= 2;
         return ks;

@@ -111,11 +111,11 @@ def test_gemm_epilogues(gpu, M, N, K):
 @pytest.mark.gpu
 @pytest.mark.parametrize("M,N,K", [(481, 384, 1536), (481, 384, 1024), (97, 64, 2048)])
 def test_gemm_cross_workgroup_split_k(gpu, M, N, K, monkeypatch):
-    """32 x 32 tiles whose K range is split over workgroups (SD_SPLITK_WG=512: ViT-S/16 fc2 at 481 tokens: two
+    """32 x 32 tiles whose K range is split over workgroups (SD_SPLITK_WG=512 forces it on the ViT-S/16 fc2 at 481 tokens: two
     slices; the last arriver sums the slices' f32 partials in slice order): every epilogue
     equals the f32 product within the single-workgroup tolerance, the result is
     bit-identical across launches (deterministic combine, self-resetting tickets), and
-    SD_SPLITK_WG=0 (no split, the default) agrees."""
+    SD_SPLITK_WG=0 (no split) agrees."""
     from scenedino_amd import _lib
     g = torch.Generator().manual_seed(M + K)
     a = _bf(torch.randn(M, K, generator=g)).to(gpu)
@@ -136,7 +136,7 @@ def test_gemm_cross_workgroup_split_k(gpu, M, N, K, monkeypatch):
         torch.cuda.synchronize()
         return out, x, ob
 
-    monkeypatch.setenv("SD_SPLITK_WG", "512")  # split (off by default)
+    monkeypatch.setenv("SD_SPLITK_WG", "512")  # split these shapes (the default cap is 1 tile per CU)
     runs = [run() for _ in range(3)]
     out, x, ob = runs[0]
     assert (out - ref).abs().max().item() <= 1e-4 * scale + 1e-5
