@@ -95,6 +95,26 @@ __host__ __device__ constexpr int cv_lds_bytes() {
                : 8 * cv_epi_rows<BM, BN, STF32>() * cv_epi_pitch<BN, STF32>();
 }
 
+// XCD-aware tile order (MI355X guide §5 T1, the bijective form): the hardware deals
+// workgroups round-robin over the 8 XCDs (linear id % 8); this maps XCD x's workgroups to
+// one contiguous range of (row tile, column tile) pairs, column tiles of a row tile
+// adjacent, so the row tiles an XCD runs at once share their input rows (3x3 halos) and
+// weights in that XCD's L2 instead of every XCD streaming every row.  CV_XCD_REMAP=0: off.
+#ifndef CV_XCD_REMAP
+#define CV_XCD_REMAP 1
+#endif
+__device__ __forceinline__ void cv_tile_of(int &mt, int &nt) {
+    const int gx = gridDim.x, gy = gridDim.y, nwg = gx * gy;
+    const int lin = blockIdx.x + gx * blockIdx.y;
+    int w = lin;
+    if (CV_XCD_REMAP && nwg > 8) {
+        const int xcd = lin & 7, q = nwg >> 3, r = nwg & 7;
+        w = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (lin >> 3);
+    }
+    mt = w / gy;
+    nt = w - mt * gy;
+}
+
 // EPI: SD_EPI_BF16 / SD_EPI_F32 (out (M, ldo) = acc + bias [+ res + res2 when RES]) or
 // SD_EPI_SHUF (the ConvTranspose2d(k, stride k) sub-pixel scatter, bf16); CONV: implicit
 // 3x3 im2col A rows (else dense A rows of stride lda: 1x1 / transposed convolutions);
@@ -112,7 +132,9 @@ __global__ void __launch_bounds__(512) k_conv_big(sd_gemm_args g) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 2, wn = wave & 3;
-    const int64_t m0 = (int64_t)blockIdx.x * BM, n0 = (int64_t)blockIdx.y * BN;
+    int mt, nt;
+    cv_tile_of(mt, nt);
+    const int64_t m0 = (int64_t)mt * BM, n0 = (int64_t)nt * BN;
     const int nk = (int)(g.K / BK);
     const int64_t a_bytes = CONV ? (g.M / ((int64_t)g.OH * g.OW)) * g.H * g.W * g.Cin * 2 : g.M * g.lda * 2;
     const __amdgpu_buffer_rsrc_t rsA =
@@ -407,10 +429,12 @@ __global__ void __launch_bounds__(512) k_conv_halo(sd_gemm_args g) {
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 2, wn = wave & 3;
     const int txn = (g.OW + TW - 1) / TW, tyn = (g.OH + TH - 1) / TH;
-    const int tile = blockIdx.x, b = tile / (txn * tyn), trem = tile - b * txn * tyn;
+    int tile, ntile;
+    cv_tile_of(tile, ntile);
+    const int b = tile / (txn * tyn), trem = tile - b * txn * tyn;
     const int ty = trem / txn, tx = trem - ty * txn;
     const int y0 = ty * TH, x0 = tx * TW;
-    const int64_t n0 = (int64_t)blockIdx.y * BN;
+    const int64_t n0 = (int64_t)ntile * BN;
     const int nch = g.Cin / CV_BK, nk = 9 * nch;
     const int64_t a_bytes = (g.M / ((int64_t)g.OH * g.OW)) * g.H * g.W * g.Cin * 2;
     const __amdgpu_buffer_rsrc_t rsA =
