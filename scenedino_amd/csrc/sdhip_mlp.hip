@@ -151,6 +151,9 @@ __global__ void __launch_bounds__(ML_WAVES * 64) k_mlp_fwd(const sd_mlp_train_ar
 // element offsets of a run's four tap rows in dgrid).
 // ---------------------------------------------------------------------------
 #define ML_SCR_WORDS (4 * 32 + 32 + 32 * 4)
+#ifndef ML_DIAG_NO_ATOMICS
+#define ML_DIAG_NO_ATOMICS 0  // diagnostic builds only (tools/build_variant.py): drop the grid-gradient atomics
+#endif
 
 __device__ __forceinline__ void ml_wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -245,7 +248,7 @@ __device__ __forceinline__ void ml_s_emit(const int *scr, int mt, int nr, int la
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         const int kk = 8 * mt + 2 * (i >> 2) + h;
-        if (kk < nr && g[i] != 0.f) unsafeAtomicAdd(dg + soff[4 * kk + (i & 3)], g[i]);
+        if (kk < nr && g[i] != 0.f && !ML_DIAG_NO_ATOMICS) unsafeAtomicAdd(dg + soff[4 * kk + (i & 3)], g[i]);
     }
 }
 
