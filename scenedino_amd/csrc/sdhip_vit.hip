@@ -1502,16 +1502,17 @@ static void vt_pick_gemm(const sd_gemm_args &g, hipStream_t s) {
     // convolutions: 120) take 256-deep K steps: half the dependent ring steps per tile, a
     // 128-KiB ring (one tile per CU is all there is anyway)
     const int64_t t32 = ((g.M + 31) / 32) * ((g.N + 31) / 32);
-    // and, where the tiles leave most CUs idle, their K range split over workgroups
-    // (deterministic last-arriver combine): the largest of 2, 4, 8 slices keeping
-    // tiles x slices <= SD_SPLITK_WG (default: one per CU) and >= 2 K steps per slice.
-    // Measured (profiles/r4_splitk_ab.txt, interleaved): at one tile per CU only the DPT's
-    // 12x40 convolutions split (2 slices; encode 1.16 -> 1.15 ms); at two per CU the
-    // ViT-S/16 fc2 splits too and runs slower (the 128-KiB-ring tiles no longer co-reside:
-    // ViT-S/16 0.576 -> 0.624 ms); SD_SPLITK_WG=0 turns it off
+    // and, where the tiles leave most CUs idle, optionally their K range split over
+    // workgroups (deterministic last-arriver combine): the largest of 2, 4, 8 slices keeping
+    // tiles x slices <= SD_SPLITK_WG and >= 2 K steps per slice.  Off by default: the
+    // tickets and partial slabs are one workspace per device, so two split launches must
+    // not run concurrently -- and the encoder now runs the DPT's level fronts on side
+    // streams beside the ViT.  Measured (profiles/r4_splitk_ab.txt, interleaved, one
+    // stream): at one tile per CU only the 12x40 convolutions split (encode 1.16 -> 1.15 ms);
+    // at two per CU the ViT-S/16 fc2 splits too and runs slower (0.576 -> 0.624 ms)
     auto ksplit = [&](int bk) {
         const char *e = getenv("SD_SPLITK_WG");
-        const int64_t cap = (e && e[0]) ? atoll(e) : (int64_t)sd_num_cus();
+        const int64_t cap = (e && e[0]) ? atoll(e) : 0;
         int ks = 1;
         while (ks < 8 && t32 * ks * 2 <= cap && g.K / bk >= 4 * ks) ks *= 2;
         return ks;

@@ -21,6 +21,7 @@ built as in the reference, as plain device tensor ops (visualization.py).
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Tuple
 
 import torch
@@ -169,6 +170,13 @@ class DINOv2Module(nn.Module):
         self.visualization = VisualizationModule(self.encoder.latent_size)
         self.use_graph = True
         self._graph = None
+        # DPT level fronts on side streams beside the ViT (SCENEDINO_AMD_DPT_OVERLAP=1 at
+        # construction; same kernels and results as the one-stream order).  Off by default:
+        # measured slower (ViT-S/16 + DPT 1.14 -> 1.23 ms, profiles/r4_dpt_overlap_ab.txt) --
+        # the side streams' full-chip convolutions hold every CU's LDS and delay the
+        # latency-bound ViT launches on the critical path
+        self.overlap_levels = os.environ.get("SCENEDINO_AMD_DPT_OVERLAP", "0") == "1"
+        self._side = None
 
     # -- prediction pass --------------------------------------------------------
     def _decode(self, x, last: bool = True):
@@ -180,8 +188,35 @@ class DINOv2Module(nn.Module):
                               antialias=True)
         vit = enc.model
         if isinstance(self.decoder, DPTHead):
-            grids, final = vit_forward(vit.vit, x, vit.packed(), vit.intermediate, nhwc=True)
-            return self.decoder.forward_nhwc(grids + [final], last=last)
+            if not (x.is_cuda and self.overlap_levels):
+                grids, final = vit_forward(vit.vit, x, vit.packed(), vit.intermediate, nhwc=True)
+                return self.decoder.forward_nhwc(grids + [final], last=last)
+            # the DPT's per-level fronts (projection, resize, 3x3 conv) on side streams as
+            # soon as their token grids exist, overlapping the later ViT blocks (latency-bound
+            # 481-token launches that leave most CUs idle); joined before the fusion chain
+            main = torch.cuda.current_stream(x.device)
+            if self._side is None or self._side[0] != x.device:
+                self._side = (x.device, [torch.cuda.Stream(device=x.device) for _ in range(3)])
+            side = self._side[1]
+            levels = [None] * (len(vit.intermediate) + 1)
+
+            def on_grid(i, g):
+                if i >= len(side):
+                    return
+                s = side[i]
+                s.wait_stream(main)
+                with torch.cuda.stream(s):
+                    levels[i] = self.decoder.forward_level(i, g)
+                if not torch.cuda.is_current_stream_capturing():  # eager: cross-stream lifetimes
+                    g.record_stream(s)
+                    levels[i].record_stream(main)
+
+            grids, final = vit_forward(vit.vit, x, vit.packed(), vit.intermediate, nhwc=True,
+                                       on_grid=on_grid)
+            for i, s in enumerate(side):
+                if levels[i] is not None:
+                    main.wait_stream(s)
+            return self.decoder.forward_nhwc(grids + [final], last=last, levels=levels)
         grids, final = vit_forward(vit.vit, x, vit.packed(), vit.intermediate)
         return self.decoder(grids + [final])
 

@@ -150,27 +150,36 @@ class DPTHead(nn.Module):
         self._packed = (key, P)
         return P
 
-    def forward_nhwc(self, xs, last: bool = True):
+    def forward_level(self, i, x):
+        """The per-level front of the head for NHWC bf16 tokens x of level i: the
+        reassemble projection (+ its resize layer) and ``convs[i]`` (dpt_head.py:56-92,
+        226-229).  The four levels are independent, so a caller may run them on side
+        streams as their token grids appear (DINOv2Module._decode)."""
+        L = _lib
+        P = self._pack()
+        w, b = P["proj"][i]
+        y = L.linear_nhwc(x, w, b)
+        if i == 0 or i == 1:
+            wt, bt, k = P["up0" if i == 0 else "up1"]
+            y = L.linear_nhwc(y, wt, bt, shuf=k)
+        elif i == 3:
+            w3, b3 = P["down3"]
+            y = L.conv3x3(y, w3, b3, stride=2)
+        return L.conv3x3(y, *P["convs"][i])
+
+    def forward_nhwc(self, xs, last: bool = True, levels=None):
         """xs: 4 NHWC bf16 tensors (B, h, w, embed) -> [f32 (B, d_out, H, W), channels-last].
         ``last=False`` stops before the final convolution and returns its NHWC bf16 input
         (``forward_last`` applies it: the graph-captured pass leaves that one launch out,
-        so its output is a fresh tensor instead of a copy of a graph-owned buffer)."""
+        so its output is a fresh tensor instead of a copy of a graph-owned buffer).
+        ``levels``: forward_level outputs already computed (None entries are computed
+        here)."""
         if torch.is_grad_enabled() and self.training:
             raise NotImplementedError("scenedino_amd DPT: no backward kernels; use no_grad / eval")
         L = _lib
         P = self._pack()
-        r = []
-        for i, x in enumerate(xs):
-            w, b = P["proj"][i]
-            y = L.linear_nhwc(x, w, b)
-            if i == 0 or i == 1:
-                wt, bt, k = P["up0" if i == 0 else "up1"]
-                y = L.linear_nhwc(y, wt, bt, shuf=k)
-            elif i == 3:
-                w3, b3 = P["down3"]
-                y = L.conv3x3(y, w3, b3, stride=2)
-            r.append(y)
-        f = [L.conv3x3(y, *P["convs"][i]) for i, y in enumerate(r)]
+        levels = list(levels) if levels is not None else [None] * len(xs)
+        f = [levels[i] if levels[i] is not None else self.forward_level(i, x) for i, x in enumerate(xs)]
 
         def rcu(x, pk, extra=None):
             (w1, b1), (w2, b2) = pk

@@ -144,12 +144,14 @@ LN_GEMM = os.environ.get("SCENEDINO_AMD_LN_GEMM", "1") != "0"
 
 
 def vit_forward(vit: VisionTransformer, images: torch.Tensor, packed: _Packed,
-                intermediate: List[int], nhwc: bool = False):
+                intermediate: List[int], nhwc: bool = False, on_grid=None):
     """images (B, 3, H, W) in [-1, 1] (DINOv2Encoder input, before _normalize_input) ->
     (intermediate block outputs as (B, C, gh, gw) f32 grids, final-norm tokens
     L2-normalised as a grid).  ``nhwc=True`` returns (B, gh, gw, C) bf16 grids instead: the
-    DPT decoder's operand layout, written straight from the token rows.  Every arithmetic
-    step is a libsdhip.so kernel."""
+    DPT decoder's operand layout, written straight from the token rows.  ``on_grid(i, g)``
+    is called as each intermediate grid is written (the caller may start consuming it on
+    another stream while the later blocks run).  Every arithmetic step is a libsdhip.so
+    kernel."""
     if torch.is_grad_enabled() and vit.training:
         raise NotImplementedError("scenedino_amd ViT: no backward kernels; use no_grad / eval")
     B, _, H, W = images.shape
@@ -205,6 +207,8 @@ def vit_forward(vit: VisionTransformer, images: torch.Tensor, packed: _Packed,
         _lib.gemm(hid, blk["fc2_w"], blk["fc2_b"], _lib.SD_EPI_RESID, out=x, gamma=blk["ls2"])
         if i in intermediate:
             grids.append(to_grid(x, B, T, C, 1, gh, gw, False))
+            if on_grid is not None:
+                on_grid(len(grids) - 1, grids[-1])
     xf = torch.empty(B * T, C, device=dev)
     _lib.layernorm(x, packed.nw, packed.nb, 1e-6, xf)
     final = to_grid(xf, B, T, C, 1, gh, gw, True)

@@ -143,6 +143,29 @@ def test_encoder_graph_replay_matches_eager(gpu):
         assert torch.equal(a, b)
 
 
+@pytest.mark.gpu
+def test_dpt_level_fronts_on_side_streams_match_one_stream(gpu):
+    """DINOv2Module can run the DPT's per-level fronts on side streams beside the later ViT
+    blocks (overlap_levels; off by default, slower): the same kernels on the same operands,
+    so the grid equals the one-stream order bit for bit, eager and graph-replayed."""
+    m = make(seed=23).to(gpu)
+    g = torch.Generator().manual_seed(24)
+    xs = [(torch.rand(1, 3, 64, 160, generator=g) * 2 - 1).to(gpu) for _ in range(3)]
+    outs = {}
+    with torch.no_grad():
+        for ov in (False, True):
+            m.overlap_levels = ov
+            for ug in (False, True):
+                m.use_graph = ug
+                m._graph = None
+                outs[(ov, ug)] = [m(x)[0].clone() for x in xs]
+    torch.cuda.synchronize()
+    ref = outs[(False, False)]
+    for key, o in outs.items():
+        for a, b in zip(ref, o):
+            assert torch.equal(a, b), key
+
+
 MODEL_CONF = {"arch": "BTSNet", "predict_dino": True, "dino_dims": 64, "learn_empty": False,
               "code_mode": "z", "inv_z": True, "z_near": 3, "z_far": 80, "sample_color": True,
               "encoder": CONF, "code": {"num_freqs": 6, "freq_factor": 1.5, "include_input": True},
