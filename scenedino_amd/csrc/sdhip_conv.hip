@@ -85,17 +85,25 @@ __device__ __forceinline__ void cv_wait_ahead(int ahead) {
 }
 // epilogue staging: f32 when the output is f32 or residuals are added before the bf16
 // rounding, else bf16; per wave ER rows of WN values + 16 B
-template <int BN, bool STF32>
-__host__ __device__ constexpr int cv_epi_pitch() { return (BN / 4) * (STF32 ? 4 : 2) + 16; }
+// waves along M of the 8-wave grid (the rest along N): 4 x 2 for the 128 x 64 tiles (wave
+// tile 32 x 32: 64 KiB of fragment reads per K step instead of 80 with 64 x 16), else 2 x 4
+#ifndef CV_WGM4
+#define CV_WGM4 1
+#endif
+template <int BM, int BN>
+__host__ __device__ constexpr int cv_wgm() { return CV_WGM4 && BM == 128 && BN == 64 ? 4 : 2; }
+template <int BM, int BN, bool STF32>
+__host__ __device__ constexpr int cv_epi_pitch() { return (BN / (8 / cv_wgm<BM, BN>())) * (STF32 ? 4 : 2) + 16; }
 template <int BM, int BN, bool STF32>
 __host__ __device__ constexpr int cv_epi_rows() {
-    return 8 * (BM / 2) * cv_epi_pitch<BN, STF32>() <= CV_LDS_MAX ? BM / 2 : BM / 4;
+    return 8 * (BM / cv_wgm<BM, BN>()) * cv_epi_pitch<BM, BN, STF32>() <= CV_LDS_MAX ? BM / cv_wgm<BM, BN>()
+                                                                                   : BM / cv_wgm<BM, BN>() / 2;
 }
 template <int BM, int BN, bool STF32>
 __host__ __device__ constexpr int cv_lds_bytes() {
-    return cv_stages<BM, BN>() * cv_stage_bytes<BM, BN>() > 8 * cv_epi_rows<BM, BN, STF32>() * cv_epi_pitch<BN, STF32>()
+    return cv_stages<BM, BN>() * cv_stage_bytes<BM, BN>() > 8 * cv_epi_rows<BM, BN, STF32>() * cv_epi_pitch<BM, BN, STF32>()
                ? cv_stages<BM, BN>() * cv_stage_bytes<BM, BN>()
-               : 8 * cv_epi_rows<BM, BN, STF32>() * cv_epi_pitch<BN, STF32>();
+               : 8 * cv_epi_rows<BM, BN, STF32>() * cv_epi_pitch<BM, BN, STF32>();
 }
 
 // XCD-aware tile order (MI355X guide §5 T1, the bijective form): the hardware deals
@@ -126,7 +134,8 @@ template <int BM, int BN, int EPI, bool CONV, bool RELU, bool RES>
 __global__ void __launch_bounds__(512) k_conv_big(sd_gemm_args g) {
     constexpr bool OUTF32 = EPI == SD_EPI_F32, STF32 = OUTF32 || RES;
     constexpr int BK = CV_BK, RS = cv_stages<BM, BN>(), STB = cv_stage_bytes<BM, BN>();
-    constexpr int WM = BM / 2, WN = BN / 4, TI = WM / 16, TJ = WN / 16;  // wave tile, 16x16 MFMA tiles
+    constexpr int WGM = cv_wgm<BM, BN>(), WGN = 8 / WGM;
+    constexpr int WM = BM / WGM, WN = BN / WGN, TI = WM / 16, TJ = WN / 16;  // wave tile, 16x16 MFMA tiles
     constexpr int CA = BM * 8 / 512, CB = BN * 8 / 512;  // 16-B DMA chunks per thread per stage
     constexpr int PER = CA + CB;
     static_assert(CB >= 1 && TJ >= 1 && RS >= 2 && RS <= 6 && (RS - 2) * PER <= 63, "tile shape");
@@ -134,7 +143,7 @@ __global__ void __launch_bounds__(512) k_conv_big(sd_gemm_args g) {
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave >> 2, wn = wave & 3;
+    const int wm = wave / WGN, wn = wave % WGN;
     int mt, nt;
     cv_tile_of(mt, nt);
     const int64_t m0 = (int64_t)mt * BM, n0 = (int64_t)nt * BN;
@@ -298,7 +307,7 @@ __global__ void __launch_bounds__(512) k_conv_big(sd_gemm_args g) {
         const int64_t n = min(n0 + wn * WN + 16 * j + fr, g.N - 1);
         bias[j] = g.bias ? g.bias[n] : 0.f;
     }
-    constexpr int ER = cv_epi_rows<BM, BN, STF32>(), PITCH = cv_epi_pitch<BN, STF32>();
+    constexpr int ER = cv_epi_rows<BM, BN, STF32>(), PITCH = cv_epi_pitch<BM, BN, STF32>();
     constexpr int CC = OUTF32 ? 4 : 8;  // columns per 16-B output store
     constexpr int CPRW = WN / CC;       // store chunks per wave row
     static_assert((ER * CPRW) % 64 == 0, "epilogue chunking");
@@ -413,9 +422,9 @@ __host__ __device__ constexpr int cvh_rsb() {
 }
 template <int TW, int BN, bool STF32>
 __host__ __device__ constexpr int cvh_lds_bytes() {
-    return 2 * cvh_halo_bytes<TW>() + cvh_rsb<TW, BN>() * BN * 128 > 8 * cv_epi_rows<CVH_TH * TW, BN, STF32>() * cv_epi_pitch<BN, STF32>()
+    return 2 * cvh_halo_bytes<TW>() + cvh_rsb<TW, BN>() * BN * 128 > 8 * cv_epi_rows<CVH_TH * TW, BN, STF32>() * cv_epi_pitch<CVH_TH * TW, BN, STF32>()
                ? 2 * cvh_halo_bytes<TW>() + cvh_rsb<TW, BN>() * BN * 128
-               : 8 * cv_epi_rows<CVH_TH * TW, BN, STF32>() * cv_epi_pitch<BN, STF32>();
+               : 8 * cv_epi_rows<CVH_TH * TW, BN, STF32>() * cv_epi_pitch<CVH_TH * TW, BN, STF32>();
 }
 // s_waitcnt vmcnt(n) for a runtime n (the count of this thread's younger DMAs)
 __device__ __forceinline__ void cv_vmcnt(int n) {
@@ -558,7 +567,7 @@ __global__ void __launch_bounds__(512) k_conv_halo(sd_gemm_args g) {
         const int64_t n = min(n0 + wn * WN + 16 * j + fr, g.N - 1);
         bias[j] = g.bias ? g.bias[n] : 0.f;
     }
-    constexpr int ER = cv_epi_rows<BM, BN, STF32>(), PITCH = cv_epi_pitch<BN, STF32>();
+    constexpr int ER = cv_epi_rows<BM, BN, STF32>(), PITCH = cv_epi_pitch<BM, BN, STF32>();
     constexpr int CC = OUTF32 ? 4 : 8;
     constexpr int CPRW = WN / CC;
     static_assert((ER * CPRW) % 64 == 0, "epilogue chunking");

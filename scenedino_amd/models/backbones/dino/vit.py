@@ -141,6 +141,7 @@ def _param_key(m: nn.Module):
 # fuse the block norms into the qkv / fc1 GEMMs (sd_ln_gemm); SCENEDINO_AMD_LN_GEMM=0 keeps
 # the separate sd_layernorm launches (A/B runs)
 LN_GEMM = os.environ.get("SCENEDINO_AMD_LN_GEMM", "1") != "0"
+LN_GEMM_ALL = os.environ.get("SCENEDINO_AMD_LN_GEMM", "1") == "all"  # also C = 768 (A/B runs)
 
 
 def vit_forward(vit: VisionTransformer, images: torch.Tensor, packed: _Packed,
@@ -187,7 +188,7 @@ def vit_forward(vit: VisionTransformer, images: torch.Tensor, packed: _Packed,
     # ViT-S at small token counts (481 tokens: 0.61 -> 0.57 ms per pass); measured slower
     # for C = 768 (DINOv2-B/14: 0.90 -> 0.99 ms against sd_layernorm + the 64 x 64-tile
     # sd_gemm) and at 1921 tokens (the narrow tile re-reads the weights per row tile)
-    fuse_ln = C == 384 and LN_GEMM and B * T <= 1024
+    fuse_ln = (C == 384 or LN_GEMM_ALL) and LN_GEMM and B * T <= 1024
     for i, blk in enumerate(packed.blocks):
         if fuse_ln:
             _lib.ln_gemm(x, blk["n1w"], blk["n1b"], 1e-6, blk["qkv_w"], blk["qkv_b"],
