@@ -394,7 +394,10 @@ typedef struct sd_gemm_args {
     int32_t epi;
     void *out; int64_t ldo;     /* output / residual, element stride between rows        */
     const float *gamma;         /* SD_EPI_RESID layer scale (N) or NULL (= 1)            */
-    void *q, *k, *vt;           /* SD_EPI_QKV destinations                               */
+    void *q, *k, *vt;           /* SD_EPI_QKV destinations; SD_EPI_RESID: q (or NULL) =
+                                 * a bf16 (B, tokens - 1, N) copy of the updated rows
+                                 * without each image's first (class) token -- the
+                                 * timm intermediate-layer grid, tokens_to_nhwc's output  */
     int32_t tokens, heads, head_dim, tokens_pad;
     const float *pos;           /* SD_EPI_PATCH position embedding (patches+1, N)        */
     int32_t patches;

@@ -591,8 +591,10 @@ def composite_bwd(z, sigma, feat, rgb, hard_alpha_cap, g_depth, g_feat, g_rgb, g
 # ViT encoder kernels (sdhip_vit.hip)
 # ---------------------------------------------------------------------------
 def gemm(a, w, bias, epi, out=None, gamma=None, qkv=None, tokens=0, heads=0, pos=None,
-         patches=0):
-    """sd_gemm: a (M, K) bf16 (row stride a.stride(0)), w (N, K) bf16 contiguous."""
+         patches=0, grid_out=None):
+    """sd_gemm: a (M, K) bf16 (row stride a.stride(0)), w (N, K) bf16 contiguous.
+    SD_EPI_RESID with grid_out (B, tokens - 1, N)-shaped bf16: also writes the updated rows
+    without each image's class token there (tokens_to_nhwc's output, no extra launch)."""
     lib = load()
     M, K = a.shape
     N = w.shape[0]
@@ -610,6 +612,11 @@ def gemm(a, w, bias, epi, out=None, gamma=None, qkv=None, tokens=0, heads=0, pos
         g.tokens, g.heads, g.head_dim, g.tokens_pad = tokens, heads, q.shape[-1], k.shape[-2]
     if pos is not None:
         g.pos, g.patches = pos.data_ptr(), patches
+    if grid_out is not None:
+        _req(grid_out, "grid_out", torch.bfloat16)
+        if grid_out.numel() != (M // tokens) * (tokens - 1) * N:
+            raise ValueError("sd_gemm: grid_out must hold (M / tokens) x (tokens - 1) x N values")
+        g.q, g.tokens = grid_out.data_ptr(), tokens
     _check(lib.sd_gemm(ctypes.byref(g), stream_of(a)), "sd_gemm")
 
 

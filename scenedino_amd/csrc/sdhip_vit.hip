@@ -701,7 +701,12 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g, float *__restrict_
                 if constexpr (EPI == SD_EPI_RESID) {
                     const float gam = g.gamma ? g.gamma[n] : 1.f;
                     float *o = (float *)g.out + m * g.ldo + n;
-                    *o = *o + gam * v;
+                    const float nv = *o + gam * v;
+                    *o = nv;
+                    if (g.q) {  // the intermediate-layer grid (k_tokens_to_nhwc's rounding)
+                        const uint32_t T = (uint32_t)g.tokens, b = (uint32_t)m / T, tok = (uint32_t)m - b * T;
+                        if (tok > 0) ((__bf16 *)g.q)[((int64_t)b * (T - 1) + tok - 1) * g.N + n] = (__bf16)nv;
+                    }
                 } else {  // SD_EPI_PATCH: patch row m = b * patches + p -> token 1 + p
                     const uint32_t bq = (uint32_t)m / (uint32_t)g.patches;
                     const int64_t b = bq, p = m - b * g.patches;
@@ -1569,6 +1574,8 @@ extern "C" int sd_gemm(const sd_gemm_args *args, void *stream) {
              g.M % g.tokens == 0 && g.head_dim % 8 == 0 && g.tokens_pad % 8 == 0;
     else if (g.epi == SD_EPI_PATCH)
         ok = ok && g.out && g.pos && g.patches > 0 && g.M % g.patches == 0 && g.ldo >= g.N;
+    else if (g.epi == SD_EPI_RESID && g.q)
+        ok = ok && g.out && g.ldo >= g.N && g.tokens > 1 && g.M % g.tokens == 0;
     else
         ok = ok && g.out && g.ldo >= g.N;
     if (!ok) {

@@ -142,6 +142,9 @@ def _param_key(m: nn.Module):
 # the separate sd_layernorm launches (A/B runs)
 LN_GEMM = os.environ.get("SCENEDINO_AMD_LN_GEMM", "1") != "0"
 LN_GEMM_ALL = os.environ.get("SCENEDINO_AMD_LN_GEMM", "1") == "all"  # also C = 768 (A/B runs)
+# the DPT's intermediate token grids written by fc2's residual epilogue (no tokens_to_nhwc
+# launches); SCENEDINO_AMD_FC2_GRID=0 restores the separate launches (A/B runs)
+FC2_GRID = os.environ.get("SCENEDINO_AMD_FC2_GRID", "1") != "0"
 
 
 def vit_forward(vit: VisionTransformer, images: torch.Tensor, packed: _Packed,
@@ -205,9 +208,16 @@ def vit_forward(vit: VisionTransformer, images: torch.Tensor, packed: _Packed,
         else:
             _lib.layernorm(x, blk["n2w"], blk["n2b"], 1e-6, xn)
             _lib.gemm(xn, blk["fc1_w"], blk["fc1_b"], _lib.SD_EPI_GELU, out=hid)
-        _lib.gemm(hid, blk["fc2_w"], blk["fc2_b"], _lib.SD_EPI_RESID, out=x, gamma=blk["ls2"])
+        if i in intermediate and nhwc and FC2_GRID:  # the DPT's bf16 token grid from fc2's epilogue
+            grid = torch.empty(B, gh, gw, C, device=dev, dtype=bf)
+            _lib.gemm(hid, blk["fc2_w"], blk["fc2_b"], _lib.SD_EPI_RESID, out=x, gamma=blk["ls2"],
+                      tokens=T, grid_out=grid)
+            grids.append(grid)
+        else:
+            _lib.gemm(hid, blk["fc2_w"], blk["fc2_b"], _lib.SD_EPI_RESID, out=x, gamma=blk["ls2"])
+            if i in intermediate:
+                grids.append(to_grid(x, B, T, C, 1, gh, gw, False))
         if i in intermediate:
-            grids.append(to_grid(x, B, T, C, 1, gh, gw, False))
             if on_grid is not None:
                 on_grid(len(grids) - 1, grids[-1])
     xf = torch.empty(B * T, C, device=dev)

@@ -109,6 +109,31 @@ def test_gemm_epilogues(gpu, M, N, K):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("B,gh,gw,C,Kh", [(1, 12, 40, 384, 1536), (2, 3, 5, 768, 3072)])
+def test_resid_epilogue_writes_the_token_grid(gpu, B, gh, gw, C, Kh):
+    """fc2's residual epilogue with grid_out also writes the intermediate-layer NHWC bf16
+    grid (the class token dropped): bit-equal to sd_tokens_to_nhwc of the updated rows,
+    which the ViT no longer launches for the DPT's intermediate layers."""
+    from scenedino_amd import _lib
+    g = torch.Generator().manual_seed(B * gh + C)
+    T = gh * gw + 1
+    M = B * T
+    hid = _bf(torch.randn(M, Kh, generator=g)).to(gpu)
+    w = _bf(torch.randn(C, Kh, generator=g) / math.sqrt(Kh)).to(gpu)
+    b = (0.1 * torch.randn(C, generator=g)).to(gpu)
+    gam = torch.rand(C, generator=g).to(gpu)
+    x0 = torch.randn(M, C, generator=g).to(gpu)
+    x1, x2 = x0.clone(), x0.clone()
+    grid = torch.empty(B, gh, gw, C, device=gpu, dtype=torch.bfloat16)
+    _lib.gemm(hid, w, b, _lib.SD_EPI_RESID, out=x1, gamma=gam, tokens=T, grid_out=grid)
+    _lib.gemm(hid, w, b, _lib.SD_EPI_RESID, out=x2, gamma=gam)
+    assert torch.equal(x1, x2)
+    ref = _lib.tokens_to_nhwc(x2, B, T, C, 1, gh, gw, False)
+    torch.cuda.synchronize()
+    assert torch.equal(grid, ref)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("M,N,K", [(481, 384, 1536), (481, 384, 1024), (97, 64, 2048)])
 def test_gemm_cross_workgroup_split_k(gpu, M, N, K, monkeypatch):
     """32 x 32 tiles whose K range is split over workgroups (SD_SPLITK_WG=512 forces it on the ViT-S/16 fc2 at 481 tokens: two
