@@ -433,6 +433,15 @@ int sd_attention(const void *q, const void *k, const void *vt, int32_t B, int32_
 int sd_layernorm(const float *x, int64_t rows, int32_t C, const float *w, const float *b,
                  float eps, void *out, int32_t out_f32, void *stream);
 
+/* The encoder's final norm into the DPT's last token grid (vit.py:188 over timm's
+ * VisionTransformer.norm, then the prefix tokens dropped and the optional L2 normalisation
+ * of dinov2_module.py:270-287): x (B, T, C) f32 rows -> out (B, npix, C) bf16 for tokens
+ * n_prefix .. n_prefix + npix - 1 = sd_layernorm (out_f32 = 1) followed by
+ * sd_tokens_to_nhwc, bit for bit, in one launch. */
+int sd_layernorm_nhwc(const float *x, int32_t B, int32_t T, int32_t C, const float *w,
+                      const float *b, float eps, int32_t n_prefix, int32_t npix, int32_t l2norm,
+                      void *out, void *stream);
+
 /* img (B,3,H,W) in [-1,1] -> normalised ((x/2+0.5 - mean)/std) im2col patches
  * (B*Np, Kp) bf16 (zero-padded columns >= 3 p p), and class-token rows of x (B, Np+1, C):
  * x[b,0,:] = cls + pos[0,:].  mean3/std3: HOST pointers (3). */

@@ -202,6 +202,7 @@ SIGNATURES = {
                     ctypes.POINTER(ctypes.c_float), _vp, _vp, _vp, _vp, _i32, _vp],
     "sd_tokens_to_grid": [_vp, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp],
     "sd_tokens_to_nhwc": [_vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp],
+    "sd_layernorm_nhwc": [_vp, _i32, _i32, _i32, _vp, _vp, ctypes.c_float, _i32, _i32, _i32, _vp, _vp],
     "sd_upsample2x": [_vp, _i32, _i32, _i32, _i32, _vp, _vp],
 }
 
@@ -719,6 +720,17 @@ def linear_nhwc(x, w, bias, epi=None, out=None, shuf=None, res=None):
                    out=out.data_ptr(), ldo=N, res=res.data_ptr() if res is not None else None,
                    shuf_k=shuf or 0, in_h=H, in_w=W)
     _check(lib.sd_gemm(ctypes.byref(g), stream_of(x)), "sd_gemm(1x1)")
+    return out
+
+
+def layernorm_nhwc(x, w, b, eps, B, T, C, n_prefix, gh, gw, l2norm):
+    """sd_layernorm_nhwc: LayerNorm of the non-prefix token rows of x (B T, C) f32 straight
+    into a (B, gh, gw, C) bf16 grid (= layernorm(out_f32) + tokens_to_nhwc, one launch)."""
+    lib = load()
+    out = torch.empty(B, gh, gw, C, device=x.device, dtype=torch.bfloat16)
+    _check(lib.sd_layernorm_nhwc(ptr(_req(x, "x")), B, T, C, ptr(_req(w, "w")), ptr(_req(b, "b")),
+                                 float(eps), n_prefix, gh * gw, int(bool(l2norm)), ptr(out),
+                                 stream_of(x)), "sd_layernorm_nhwc")
     return out
 
 

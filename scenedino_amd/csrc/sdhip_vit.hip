@@ -1115,6 +1115,71 @@ __global__ void __launch_bounds__(256) k_layernorm(const float *__restrict__ x, 
     }
 }
 
+// The encoder's final norm straight into the DPT's last token grid: k_layernorm's f32 rows
+// (same arithmetic) of the non-prefix tokens, then k_tokens_to_nhwc's optional L2
+// normalisation (its lane order, through a wave-private LDS row) and bf16 NHWC store --
+// one launch instead of two, bit-equal to them (test_layernorm_nhwc_equals_two_launches).
+template <int PER4>
+__global__ void __launch_bounds__(256) k_layernorm_nhwc(const float *__restrict__ x, int B, int T, int C,
+                                                        int n_prefix, int npix,
+                                                        const float *__restrict__ w,
+                                                        const float *__restrict__ b, float eps,
+                                                        int l2, __bf16 *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) float srow[4][256 * PER4];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t tok = (int64_t)blockIdx.x * 4 + wv;
+    if (tok >= (int64_t)B * npix) return;  // wave-uniform
+    const int bi = (int)(tok / npix), pi = (int)(tok - (int64_t)bi * npix);
+    const float *xr = x + ((int64_t)bi * T + n_prefix + pi) * C;
+    vf4 v[PER4];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER4; ++i) {
+        const int c = 4 * lane + 256 * i;
+        v[i] = c < C ? *(const vf4 *)(xr + c) : vf4{0.f, 0.f, 0.f, 0.f};
+        s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
+    }
+    const float inv_c = 1.f / (float)C;
+    const float mean = vt_wave_sum(s) * inv_c;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER4; ++i) {
+        const int c = 4 * lane + 256 * i;
+        if (c < C) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const float d = v[i][u] - mean;
+                q = fmaf(d, d, q);
+            }
+        }
+    }
+    const float rstd = __builtin_amdgcn_rsqf(vt_wave_sum(q) * inv_c + eps);
+    float *row = srow[wv];
+#pragma unroll
+    for (int i = 0; i < PER4; ++i) {
+        const int c = 4 * lane + 256 * i;
+        if (c < C) {
+            const vf4 wv4 = *(const vf4 *)(w + c), bv = *(const vf4 *)(b + c);
+            vf4 y;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) y[u] = (v[i][u] - mean) * rstd * wv4[u] + bv[u];
+            *(vf4 *)(row + c) = y;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    float scale = 1.f;
+    if (l2) {
+        float s2 = 0.f;
+        for (int c = lane; c < C; c += 64) s2 = fmaf(row[c], row[c], s2);
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) s2 += __shfl_xor(s2, off);
+        scale = 1.f / fmaxf(sqrtf(s2), 1e-12f);
+    }
+    for (int c = lane; c < C; c += 64) out[tok * C + c] = (__bf16)(row[c] * scale);
+}
+
 // patches (B * Np, Kp) bf16, Kp >= 3 p p (zero-padded), column c * p * p + ky * p + kx;
 // class-token rows x[b, 0, :] = cls + pos[0].
 __global__ void __launch_bounds__(256) k_patchify(const float *__restrict__ img, int B, int Hh,
@@ -1779,6 +1844,34 @@ extern "C" int sd_tokens_to_nhwc(const float *x, int32_t B, int32_t T, int32_t C
                        (hipStream_t)stream, x, B, T, C, n_prefix, npix, l2norm, (__bf16 *)out);
     if (hipGetLastError() != hipSuccess) {
         sd_set_error("sd_tokens_to_nhwc: launch failed");
+        return -2;
+    }
+    return 0;
+}
+
+extern "C" int sd_layernorm_nhwc(const float *x, int32_t B, int32_t T, int32_t C,
+                                 const float *w, const float *b, float eps, int32_t n_prefix,
+                                 int32_t npix, int32_t l2norm, void *out, void *stream) {
+    if (!x || !w || !b || !out || B <= 0 || C <= 0 || C > 1024 || C % 4 != 0 || n_prefix < 0 ||
+        npix <= 0 || (int64_t)n_prefix + npix > T ||
+        ((uintptr_t)x | (uintptr_t)w | (uintptr_t)b) & 15) {
+        sd_set_error("sd_layernorm_nhwc: invalid argument (C <= 1024, C % 4 == 0, 16-B aligned)");
+        return -1;
+    }
+    const int64_t n = (int64_t)B * npix;
+    dim3 grid((unsigned)((n + 3) / 4));
+    hipStream_t s = (hipStream_t)stream;
+#define SD_LNG(PER) hipLaunchKernelGGL((k_layernorm_nhwc<PER>), grid, dim3(256), 0, s, x, B, T, C, \
+                                       n_prefix, npix, w, b, eps, l2norm, (__bf16 *)out)
+    if (C <= 512)
+        SD_LNG(2);
+    else if (C <= 768)
+        SD_LNG(3);
+    else
+        SD_LNG(4);
+#undef SD_LNG
+    if (hipGetLastError() != hipSuccess) {
+        sd_set_error("sd_layernorm_nhwc: launch failed");
         return -2;
     }
     return 0;

@@ -220,6 +220,8 @@ def vit_forward(vit: VisionTransformer, images: torch.Tensor, packed: _Packed,
         if i in intermediate:
             if on_grid is not None:
                 on_grid(len(grids) - 1, grids[-1])
+    if nhwc and FC2_GRID:  # final norm + L2-normalised bf16 grid in one launch
+        return grids, _lib.layernorm_nhwc(x, packed.nw, packed.nb, 1e-6, B, T, C, 1, gh, gw, True)
     xf = torch.empty(B * T, C, device=dev)
     _lib.layernorm(x, packed.nw, packed.nb, 1e-6, xf)
     final = to_grid(xf, B, T, C, 1, gh, gw, True)

@@ -109,6 +109,26 @@ def test_gemm_epilogues(gpu, M, N, K):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("B,gh,gw,C", [(1, 12, 40, 384), (2, 3, 5, 768), (1, 1, 3, 1024)])
+@pytest.mark.parametrize("l2", [True, False])
+def test_layernorm_nhwc_equals_two_launches(gpu, B, gh, gw, C, l2):
+    """sd_layernorm_nhwc (the encoder's final norm straight into the DPT's last token grid)
+    is bit-equal to sd_layernorm (f32 rows) followed by sd_tokens_to_nhwc."""
+    from scenedino_amd import _lib
+    g = torch.Generator().manual_seed(C + gw)
+    T = gh * gw + 1
+    x = (2 * torch.randn(B * T, C, generator=g) + 0.3).to(gpu)
+    w = (1 + 0.1 * torch.randn(C, generator=g)).to(gpu)
+    b = (0.1 * torch.randn(C, generator=g)).to(gpu)
+    xf = torch.empty(B * T, C, device=gpu)
+    _lib.layernorm(x, w, b, 1e-6, xf)
+    ref = _lib.tokens_to_nhwc(xf, B, T, C, 1, gh, gw, l2)
+    got = _lib.layernorm_nhwc(x, w, b, 1e-6, B, T, C, 1, gh, gw, l2)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("B,gh,gw,C,Kh", [(1, 12, 40, 384, 1536), (2, 3, 5, 768, 3072)])
 def test_resid_epilogue_writes_the_token_grid(gpu, B, gh, gw, C, Kh):
     """fc2's residual epilogue with grid_out also writes the intermediate-layer NHWC bf16
