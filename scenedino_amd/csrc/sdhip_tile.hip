@@ -93,8 +93,11 @@ struct st_args {
 // records [NW waves][2][K] x 40 B and two tile buffers.  The code-column and sigma A
 // fragments live in VGPRs for the whole kernel (loaded from global memory once).
 #define ST_L_BOX 0                                                                           // [2][NW waves] (min, max) per half ray, u16x2 packed
+// hidden-sum rows padded to 272 B: the DINO head reads the same 8-B slot of the NW rows in
+// one instruction (256-B rows put them on one bank pair: 8-way conflicts)
+#define ST_HS_ROW 272
 __host__ __device__ constexpr int st_l_hs(int nw) { return ST_L_BOX + 2 * nw * 16; }         // [NW rays][128] 16-bit hidden sums
-__host__ __device__ constexpr int st_l_ws(int nw) { return st_l_hs(nw) + nw * 128 * 2; }     // [NW] f32 weight sums
+__host__ __device__ constexpr int st_l_ws(int nw) { return st_l_hs(nw) + nw * ST_HS_ROW; }   // [NW] f32 weight sums
 __host__ __device__ constexpr int st_l_ray(int nw) { return st_l_ws(nw) + 16 * 4; }          // [NW waves][2] x 32 B ray words 0..7 (LDS-DMA)
 __host__ __device__ constexpr int st_l_rec(int nw) { return st_l_ray(nw) + nw * 2 * 32; }    // records: [NW waves][2][K] x 40 B
 static_assert(st_l_rec(8) % 16 == 0 && st_l_rec(12) % 16 == 0, "record area alignment");
@@ -500,7 +503,7 @@ k_render_tile(const st_args sa) {
         if (wave >= ndt) return;
         const int slot = j < NW ? j : 0;  // B columns j >= NW: not stored
         Frag Bh[4];
-        const uint8_t *hs = lds + ST_L_HS + slot * 256;
+        const uint8_t *hs = lds + ST_L_HS + slot * ST_HS_ROW;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             const uint2 lo = *(const uint2 *)(hs + (32 * s + 4 * g) * 2);
@@ -731,7 +734,7 @@ k_render_tile(const st_args sa) {
             const float dsum = sd_rowsum16(dpart), wsum = sd_rowsum16(wpart);
             const float c0s = sd_rowsum16(cpart[0]), c1s = sd_rowsum16(cpart[1]),
                         c2s = sd_rowsum16(cpart[2]);
-            uint8_t *hs = lds + ST_L_HS + wave * 256;
+            uint8_t *hs = lds + ST_L_HS + wave * ST_HS_ROW;
             // the 32 hidden sums q = 4 t + r reduced over the 16 sample lanes of the row as a
             // butterfly (64 VALU ops instead of 32 x 4): bank-masked DPP halves the live
             // values at the first two levels, quad permutes finish -- lane bank b then holds
