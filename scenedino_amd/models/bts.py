@@ -30,6 +30,14 @@ EPS = 1e-3  # scenedino/common/cameras/pinhole.py:3
 PRECISIONS = {"fp32": _lib.SD_F32, "bf16": _lib.SD_BF16, "fp16": _lib.SD_F16}
 
 
+def voxel_chunks(n_points: int) -> int:
+    """Chunks of a large predict_voxels query (SCENEDINO_AMD_VOXEL_CHUNKS, default 1: one
+    field launch, then one seg-head launch); chunks below 2^18 points are not split."""
+    import os
+    k = max(1, int(os.environ.get("SCENEDINO_AMD_VOXEL_CHUNKS", "1")))
+    return max(1, min(k, n_points >> 18))
+
+
 def _id_list(ids):
     """View ids as a list of ints (None stays None): lists, tuples, tensors and arrays alike,
     without calling bool() on a multi-element tensor."""
@@ -473,9 +481,9 @@ class BTSNet(nn.Module):
         w2c, Ks = self.grid_f_poses_w2c, self.grid_f_Ks
         key = (xyz.data_ptr(), xyz._version, NP, w2c.data_ptr(), w2c._version, Ks.data_ptr(),
                Ks._version, gc["Hf"], gc["Wf"])
-        c = getattr(self, "_order_cache", None)
-        if c is not None and c[0] == key:
-            return c[1]
+        c = self.__dict__.setdefault("_order_cache", {})  # (chunked queries: one per chunk)
+        if key in c:
+            return c[key]
         dev = xyz.device
         idx = (torch.arange(nt, device=dev) * 32 + 16).clamp_max(NP - 1)
         pts = xyz.reshape(NP, 3).float().index_select(0, idx)
@@ -492,7 +500,9 @@ class BTSNet(nn.Module):
         vb = ((v + 2) * (gc["Hf"] / 32)).floor()
         cell = torch.where(front, ub * 4096 + vb, torch.full_like(ub, 2.0 ** 24))
         order = torch.argsort(b.double() * 2.0 ** 26 + cell.double(), stable=True).to(torch.int32)
-        self._order_cache = (key, order)
+        if len(c) >= 16:
+            c.clear()
+        c[key] = order
         return order
 
     def query(self, xyz, colors: bool = True, dino_dtype=torch.float32, locality=None):
@@ -640,13 +650,48 @@ class BTSNet(nn.Module):
                                       "(the SSCBench 'scenedino' mode)")
         if self.downstream_head is None:
             raise ValueError("predict_voxels needs a downstream (segmentation) head")
-        sigma, dino, _, _, _ = self.query(xyz, colors=False, dino_dtype=torch.bfloat16)
         rec = self._seg_rec(True)
+        n_, P_all, _ = xyz.shape
+        nch = voxel_chunks(n_ * P_all)
+        if n_ == 1 and nch > 1 and not torch.cuda.is_current_stream_capturing():
+            return self._predict_voxels_chunked(xyz, rec, voxel_size, nch)
+        sigma, dino, _, _, _ = self.query(xyz, colors=False, dino_dtype=torch.bfloat16)
         P = sigma.numel()
         _, seg, _ = self._timed("seg", lambda: _lib.seg_query(
             dino.reshape(P, -1), rec.rec, sigma=sigma.reshape(P), voxel_size=voxel_size,
             want_labels=False, want_seg=True))
         return sigma.reshape(P), seg
+
+    def _predict_voxels_chunked(self, xyz, rec, voxel_size, nch):
+        """predict_voxels over ``nch`` point chunks, the field query of chunk i + 1 on the
+        current stream while the seg head of chunk i runs on a side stream (the two kernels'
+        workgroups share the CUs: k_field waits on its grid gathers, k_seg_head on its MFMA
+        chains).  Same outputs as one launch of each (point-wise kernels)."""
+        P = xyz.shape[1]
+        main = torch.cuda.current_stream(xyz.device)
+        side = getattr(self, "_seg_side", None)
+        if side is None or side.device != xyz.device:
+            side = self._seg_side = torch.cuda.Stream(device=xyz.device)
+        # chunk bounds on 256-point boundaries (whole k_seg_head workgroups)
+        cut = [min(P, ((P * i // nch) + 255) // 256 * 256) for i in range(nch)] + [P]
+        sigmas, segs = [], []
+        for a, b in zip(cut[:-1], cut[1:]):
+            if b <= a:
+                continue
+            sigma, dino, _, _, _ = self.query(xyz[:, a:b], colors=False,
+                                              dino_dtype=torch.bfloat16)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                _, seg, _ = self._timed("seg", lambda: _lib.seg_query(
+                    dino.reshape(b - a, -1), rec.rec, sigma=sigma.reshape(-1),
+                    voxel_size=voxel_size, want_labels=False, want_seg=True))
+            dino.record_stream(side)
+            sigma.record_stream(side)
+            seg.record_stream(main)
+            sigmas.append(sigma.reshape(-1))
+            segs.append(seg)
+        main.wait_stream(side)
+        return torch.cat(sigmas), torch.cat(segs)
 
     def forward(self, xyz: torch.Tensor, **kwargs):
         """Same return contract as bts.py:476-595."""

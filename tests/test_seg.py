@@ -590,9 +590,32 @@ def test_voxel_query_tile_order_is_speed_only(gpu):
     with torch.no_grad():
         a = net.query(pts.reshape(1, -1, 3), colors=False, dino_dtype=torch.bfloat16, locality=True)
         b = net.query(pts.reshape(1, -1, 3), colors=False, dino_dtype=torch.bfloat16, locality=False)
-    order = net._order_cache[1]
+    (order,) = net._order_cache.values()
     nt = (pts.shape[0] + 31) // 32
     assert torch.equal(order.sort().values.cpu(), torch.arange(nt, dtype=torch.int32))
     assert not torch.equal(order.cpu(), torch.arange(nt, dtype=torch.int32))
     for x, y in ((a[0], b[0]), (a[1], b[1]), (a[4], b[4])):
         assert torch.equal(x, y)
+
+
+@pytest.mark.gpu
+def test_voxel_query_chunked_on_two_streams_is_bit_equal(gpu, monkeypatch):
+    """predict_voxels in chunks (SCENEDINO_AMD_VOXEL_CHUNKS: the field query of chunk i + 1
+    beside the seg head of chunk i on a side stream) gives the single-launch sigma and
+    classes bit for bit on the full C5 voxel grid, ragged last chunk included."""
+    import sys
+    from conftest import ROOT
+    sys.path.insert(0, ROOT)
+    import bench
+    from scenedino_amd import sscbench
+    net, pts, dims = bench.c5_scene(torch.device(gpu), "bf16", 0)
+    xyz = pts.reshape(1, -1, 3)
+    with torch.no_grad():
+        monkeypatch.setenv("SCENEDINO_AMD_VOXEL_CHUNKS", "1")
+        s1, g1 = net.predict_voxels(xyz, voxel_size=sscbench.VOXEL_SIZE)
+        for k in ("3", "4"):
+            monkeypatch.setenv("SCENEDINO_AMD_VOXEL_CHUNKS", k)
+            sk, gk = net.predict_voxels(xyz, voxel_size=sscbench.VOXEL_SIZE)
+            torch.cuda.synchronize()
+            assert torch.equal(sk, s1) and torch.equal(gk, g1), k
+            assert len(net._order_cache) >= int(k)  # one tile order per chunk
