@@ -413,6 +413,15 @@ typedef struct sd_gemm_args {
 
 int sd_gemm(const sd_gemm_args *args, void *stream);
 
+/* sd_gemm with SD_EPI_RESID, plus the LayerNorm of the updated residual rows (the next
+ * block norm, timm Block norm1 / norm2, vit.py:112-189) in the same launch: ln_out (M, N)
+ * bf16 = LayerNorm(N, eps) of the updated out rows, bit-equal to sd_layernorm on them.
+ * The last workgroup to finish a row band normalises it (write-through residual stores,
+ * a ticket per band).  ln_ws: ceil(M / 32) zeroed uint32 tickets, left zeroed (one
+ * workspace per concurrently running call).  N <= 1024, N % 4 == 0; no conv. */
+int sd_gemm_resid_ln(const sd_gemm_args *args, const float *ln_w, const float *ln_b, float eps,
+                     void *ln_out, uint32_t *ln_ws, void *stream);
+
 /* nn.LayerNorm(K, eps) fused into the prologue of a GEMM (timm Block: norm1 -> attn.qkv,
  * norm2 -> mlp.fc1, vit.py:112-189 over timm's VisionTransformer): out = EPI(LN(x) W^T + b)
  * for x (M, K) f32 rows, dense with row stride K (K = C in {384, 768}), W = args->w (N, K)

@@ -196,6 +196,7 @@ SIGNATURES = {
     "sd_salience_fwd": [ctypes.POINTER(SdSalienceArgs), _vp],
     "sd_salience_bwd": [ctypes.POINTER(SdSalienceArgs), _vp],
     "sd_gemm": [ctypes.POINTER(SdGemmArgs), _vp],
+    "sd_gemm_resid_ln": [ctypes.POINTER(SdGemmArgs), _vp, _vp, ctypes.c_float, _vp, _vp, _vp],
     "sd_attention": [_vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, ctypes.c_float, _vp, _vp],
     "sd_layernorm": [_vp, _i64, _i32, _vp, _vp, ctypes.c_float, _vp, _i32, _vp],
     "sd_patchify": [_vp, _i32, _i32, _i32, _i32, _i32, ctypes.POINTER(ctypes.c_float),
@@ -592,10 +593,13 @@ def composite_bwd(z, sigma, feat, rgb, hard_alpha_cap, g_depth, g_feat, g_rgb, g
 # ViT encoder kernels (sdhip_vit.hip)
 # ---------------------------------------------------------------------------
 def gemm(a, w, bias, epi, out=None, gamma=None, qkv=None, tokens=0, heads=0, pos=None,
-         patches=0, grid_out=None):
+         patches=0, grid_out=None, ln=None):
     """sd_gemm: a (M, K) bf16 (row stride a.stride(0)), w (N, K) bf16 contiguous.
     SD_EPI_RESID with grid_out (B, tokens - 1, N)-shaped bf16: also writes the updated rows
-    without each image's class token there (tokens_to_nhwc's output, no extra launch)."""
+    without each image's class token there (tokens_to_nhwc's output, no extra launch).
+    SD_EPI_RESID with ln = (ln_w, ln_b, eps, ln_out, ws): sd_gemm_resid_ln -- ln_out (M, N)
+    bf16 = LayerNorm of the updated rows (bit-equal to layernorm()), ws a zeroed int32
+    workspace of >= ceil(M / 32) words (left zeroed)."""
     lib = load()
     M, K = a.shape
     N = w.shape[0]
@@ -618,6 +622,15 @@ def gemm(a, w, bias, epi, out=None, gamma=None, qkv=None, tokens=0, heads=0, pos
         if grid_out.numel() != (M // tokens) * (tokens - 1) * N:
             raise ValueError("sd_gemm: grid_out must hold (M / tokens) x (tokens - 1) x N values")
         g.q, g.tokens = grid_out.data_ptr(), tokens
+    if ln is not None:
+        ln_w, ln_b, eps, ln_out, ws = ln
+        _req(ln_out, "ln_out", torch.bfloat16)
+        _req(ws, "ln_ws", torch.int32)
+        if ln_out.numel() != M * N or ws.numel() < (M + 31) // 32:
+            raise ValueError("sd_gemm_resid_ln: ln_out must hold M x N values, ws ceil(M / 32)")
+        _check(lib.sd_gemm_resid_ln(ctypes.byref(g), ptr(_req(ln_w, "ln_w")), ptr(_req(ln_b, "ln_b")),
+                                    float(eps), ptr(ln_out), ptr(ws), stream_of(a)), "sd_gemm_resid_ln")
+        return
     _check(lib.sd_gemm(ctypes.byref(g), stream_of(a)), "sd_gemm")
 
 

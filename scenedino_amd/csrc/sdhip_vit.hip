@@ -141,8 +141,96 @@ __device__ __forceinline__ bf16x8 vt_relu8(bf16x8 v) {
 // accumulators are summed through LDS in a fixed order (deterministic) and wave 0 runs the
 // epilogue.  Four times the workgroups of the 64x64 tiling, a quarter of the MFMA chain per
 // wave.
+// LayerNorm of the residual stream in the tail of the residual GEMM (sd_gemm_resid_ln): the
+// residual update's f32 rows go out as write-through (sc1) stores, every workgroup of a
+// BM-row band takes a ticket, and the band's last arriver reads the band's rows back (sc1
+// loads) and writes LN(x) as the next GEMM's bf16 A operand -- k_layernorm's per-row
+// arithmetic in its order (bit-equal), without its launch.  The ticket self-resets.
+#define VT_EPI_RESID_LN 100  // internal epilogue: SD_EPI_RESID + the LayerNorm tail (its own kernel)
+struct VtLnTail {
+    const float *w, *b;
+    float eps;
+    __bf16 *out;    // (M, N) bf16, or nullptr: no tail
+    uint32_t *cnt;  // one zeroed ticket per row band
+};
+
+__device__ __forceinline__ float vt_wave_sum(float x);
+
+template <int BM>
+__device__ __forceinline__ void vt_ln_tail(const sd_gemm_args &g, const VtLnTail &lt, int64_t m0,
+                                           uint8_t *smem, int tid) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's write-through stores
+    __syncthreads();
+    uint32_t *flag = (uint32_t *)smem;
+    if (tid == 0)
+        *flag = __hip_atomic_fetch_add(lt.cnt + blockIdx.y, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                gridDim.x - 1;
+    __syncthreads();
+    if (!*flag) return;  // workgroup-uniform
+    if (tid == 0) __hip_atomic_store(lt.cnt + blockIdx.y, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int lane = tid & 63, wave = tid >> 6;
+    const int C = (int)g.N;
+    const int nch = C <= 512 ? 2 : C <= 768 ? 3 : 4;  // sd_layernorm's PER
+    const float inv_c = 1.f / (float)C;
+    const int64_t mend = min(m0 + BM, g.M);
+    constexpr int RB = BM / 4 < 8 ? BM / 4 : 8;  // rows per wave whose loads go out together
+    for (int64_t r0 = m0 + wave; r0 < mend; r0 += 4 * RB) {
+        vf4 v[RB][4];
+#pragma unroll
+        for (int k = 0; k < RB; ++k) {
+            const int64_t row = r0 + 4 * k;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int c = 4 * lane + 256 * i;
+                v[k][i] = vf4{0.f, 0.f, 0.f, 0.f};
+                if (i < nch && row < mend && c < C) {
+                    const float *p = (const float *)g.out + row * g.ldo + c;
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        v[k][i][u] = __hip_atomic_load(p + u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < RB; ++k) {
+            const int64_t row = r0 + 4 * k;
+            float s = 0.f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (i < nch) s += (v[k][i][0] + v[k][i][1]) + (v[k][i][2] + v[k][i][3]);
+            const float mean = vt_wave_sum(s) * inv_c;
+            float q = 0.f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int c = 4 * lane + 256 * i;
+                if (i < nch && c < C) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const float d = v[k][i][u] - mean;
+                        q = fmaf(d, d, q);
+                    }
+                }
+            }
+            const float rstd = __builtin_amdgcn_rsqf(vt_wave_sum(q) * inv_c + lt.eps);
+            if (row >= mend) continue;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int c = 4 * lane + 256 * i;
+                if (i < nch && c < C) {
+                    const vf4 wv = *(const vf4 *)(lt.w + c), bv = *(const vf4 *)(lt.b + c);
+                    bf16x4 o;
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) o[u] = (__bf16)((v[k][i][u] - mean) * rstd * wv[u] + bv[u]);
+                    *(bf16x4 *)(lt.out + row * C + c) = o;
+                }
+            }
+        }
+    }
+}
+
 template <int BM, int BN, int BK, int EPI, bool CONV>
-__global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g, float *__restrict__ sk_slab, uint32_t *__restrict__ sk_cnt) {
+__global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g, float *__restrict__ sk_slab, uint32_t *__restrict__ sk_cnt,
+                                              VtLnTail lt) {
     constexpr bool SK = BM == 32;
     static_assert(!SK || (BN == 32 && BK % 64 == 0), "split-K tile: 32x32, BK multiple of 64");
     constexpr int WM = SK ? 32 : BM / 2, WN = SK ? 32 : BN / 2;  // per-wave tile (2 x 2 waves)
@@ -496,7 +584,7 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g, float *__restrict_
             __syncthreads();  // the flag word is part of the epilogue's LDS
         }
         if constexpr (!STAGED) {
-            if (wave != 0) return;
+            if (wave != 0 && EPI != VT_EPI_RESID_LN) return;  // (the LN tail needs all waves)
         }
     }
     // epilogue: accumulator register q of tile (i, j): row (q&3)+8(q>>2)+4h, column r
@@ -689,6 +777,7 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g, float *__restrict_
     // unstaged epilogues (residual update, patch embedding): lane-scattered 4-B stores
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
+        if (SK && wave != 0) break;
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -698,11 +787,12 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g, float *__restrict_
                 if (m >= g.M || n >= g.N) continue;
                 const float bias = g.bias ? g.bias[n] : 0.f;
                 const float v = acc[i][j][q] + bias;
-                if constexpr (EPI == SD_EPI_RESID) {
+                if constexpr (EPI == SD_EPI_RESID || EPI == VT_EPI_RESID_LN) {
                     const float gam = g.gamma ? g.gamma[n] : 1.f;
                     float *o = (float *)g.out + m * g.ldo + n;
                     const float nv = *o + gam * v;
-                    *o = nv;
+                    if (EPI == VT_EPI_RESID_LN) __hip_atomic_store(o, nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    else *o = nv;
                     if (g.q) {  // the intermediate-layer grid (k_tokens_to_nhwc's rounding)
                         const uint32_t T = (uint32_t)g.tokens, b = (uint32_t)m / T, tok = (uint32_t)m - b * T;
                         if (tok > 0) ((__bf16 *)g.q)[((int64_t)b * (T - 1) + tok - 1) * g.N + n] = (__bf16)nv;
@@ -716,6 +806,7 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g, float *__restrict_
                 }
             }
     }
+    if constexpr (EPI == VT_EPI_RESID_LN) vt_ln_tail<BM>(g, lt, m0, smem, tid);
 }
 
 #undef SA
@@ -1502,7 +1593,7 @@ static bool vt_split_ws(hipStream_t s, VtSplitWs &w) {
 }
 
 template <int BM, int BN, int BK, bool CONV>
-static void vt_launch_gemm(const sd_gemm_args &g, hipStream_t s, int ksplit = 1) {
+static void vt_launch_gemm(const sd_gemm_args &g, hipStream_t s, int ksplit = 1, const VtLnTail &lt = VtLnTail{}) {
     dim3 grid((unsigned)((g.N + BN - 1) / BN), (unsigned)((g.M + BM - 1) / BM));
     VtSplitWs w;
     if (ksplit > 1 && vt_ring_tile(BM) && (int64_t)grid.x * grid.y <= VT_SK_TILES &&
@@ -1514,13 +1605,16 @@ static void vt_launch_gemm(const sd_gemm_args &g, hipStream_t s, int ksplit = 1)
     const int lds = vt_ring_tile(BM) ? (vt_ring_bytes<BM, BN, BK>() > ep ? vt_ring_bytes<BM, BN, BK>() : ep) : 0;
     auto go = [&](auto kern) {
         if (lds) (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, g, w.slab, w.cnt);
+        hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, g, w.slab, w.cnt, lt);
     };
     switch (g.epi) {
     case SD_EPI_BF16: go(k_gemm<BM, BN, BK, SD_EPI_BF16, CONV>); break;
     case SD_EPI_GELU: go(k_gemm<BM, BN, BK, SD_EPI_GELU, CONV>); break;
     case SD_EPI_F32: go(k_gemm<BM, BN, BK, SD_EPI_F32, CONV>); break;
-    case SD_EPI_RESID: go(k_gemm<BM, BN, BK, SD_EPI_RESID, CONV>); break;
+    case SD_EPI_RESID:
+        if (lt.out && !CONV) go(k_gemm<BM, BN, BK, VT_EPI_RESID_LN, false>);
+        else go(k_gemm<BM, BN, BK, SD_EPI_RESID, CONV>);
+        break;
     case SD_EPI_QKV: go(k_gemm<BM, BN, BK, SD_EPI_QKV, CONV>); break;
     case SD_EPI_SHUF: go(k_gemm<BM, BN, BK, SD_EPI_SHUF, CONV>); break;
     case SD_EPI_NCHW: go(k_gemm<BM, BN, BK, SD_EPI_NCHW, CONV>); break;
@@ -1547,17 +1641,17 @@ static int vt_forced_tile() {
 }
 
 template <bool CONV>
-static void vt_pick_gemm(const sd_gemm_args &g, hipStream_t s) {
+static void vt_pick_gemm(const sd_gemm_args &g, hipStream_t s, const VtLnTail &lt = VtLnTail{}) {
     const int ft = vt_forced_tile();
     if (ft == 32 && g.K % 128 == 0 && g.K >= 256 && (!CONV || g.Cin % 128 == 0)) {
-        vt_launch_gemm<32, 32, 128, CONV>(g, s);
+        vt_launch_gemm<32, 32, 128, CONV>(g, s, 1, lt);
         return;
     }
     if (ft == 128 || ft == 64) {
         if (g.K % 64 == 0) {
-            if (ft == 128) vt_launch_gemm<128, 128, 64, CONV>(g, s); else vt_launch_gemm<64, 64, 64, CONV>(g, s);
+            if (ft == 128) vt_launch_gemm<128, 128, 64, CONV>(g, s, 1, lt); else vt_launch_gemm<64, 64, 64, CONV>(g, s, 1, lt);
         } else {
-            if (ft == 128) vt_launch_gemm<128, 128, 32, CONV>(g, s); else vt_launch_gemm<64, 64, 32, CONV>(g, s);
+            if (ft == 128) vt_launch_gemm<128, 128, 32, CONV>(g, s, 1, lt); else vt_launch_gemm<64, 64, 32, CONV>(g, s, 1, lt);
         }
         return;
     }
@@ -1589,12 +1683,12 @@ static void vt_pick_gemm(const sd_gemm_args &g, hipStream_t s) {
     };
     if (VT_SK256 && VT_RING && t32 <= (int64_t)sd_num_cus() && g.K % 256 == 0 &&
         (CONV ? g.Cin % 256 == 0 && mid < SD_CONV_SK_MID : mid < 256)) {
-        vt_launch_gemm<32, 32, 256, CONV>(g, s, ksplit(256));
+        vt_launch_gemm<32, 32, 256, CONV>(g, s, ksplit(256), lt);
         return;
     }
     if ((CONV ? g.Cin % 128 == 0 && mid < SD_CONV_SK_MID : mid < 256) && g.K % 128 == 0 &&
         g.K >= 256) {
-        vt_launch_gemm<32, 32, 128, CONV>(g, s, ksplit(128));  // split-K over the 4 waves
+        vt_launch_gemm<32, 32, 128, CONV>(g, s, ksplit(128), lt);  // split-K over the 4 waves
         return;
     }
     // 128x128 tiles need about two per CU, or one per CU with a long K loop to amortise
@@ -1604,14 +1698,14 @@ static void vt_pick_gemm(const sd_gemm_args &g, hipStream_t s) {
     const bool use128 = big >= 512 || (big >= 256 && g.K >= 2048);
     if (g.K % 64 == 0) {
         if (use128)
-            vt_launch_gemm<128, 128, 64, CONV>(g, s);
+            vt_launch_gemm<128, 128, 64, CONV>(g, s, 1, lt);
         else
-            vt_launch_gemm<64, 64, 64, CONV>(g, s);
+            vt_launch_gemm<64, 64, 64, CONV>(g, s, 1, lt);
     } else {
         if (use128)
-            vt_launch_gemm<128, 128, 32, CONV>(g, s);
+            vt_launch_gemm<128, 128, 32, CONV>(g, s, 1, lt);
         else
-            vt_launch_gemm<64, 64, 32, CONV>(g, s);
+            vt_launch_gemm<64, 64, 32, CONV>(g, s, 1, lt);
     }
 }
 
@@ -1663,6 +1757,35 @@ extern "C" int sd_gemm(const sd_gemm_args *args, void *stream) {
     }
     if (hipGetLastError() != hipSuccess) {
         sd_set_error("sd_gemm: launch failed");
+        return -2;
+    }
+    return 0;
+}
+
+extern "C" int sd_gemm_resid_ln(const sd_gemm_args *args, const float *ln_w, const float *ln_b,
+                                float eps, void *ln_out, uint32_t *ln_ws, void *stream) {
+    if (!args) {
+        sd_set_error("sd_gemm_resid_ln: null args");
+        return -1;
+    }
+    const sd_gemm_args &g = *args;
+    const bool ok = g.epi == SD_EPI_RESID && !g.conv && g.a && g.w && g.out && g.M >= 0 &&
+                    g.N > 0 && g.N <= 1024 && g.N % 4 == 0 && g.K > 0 && g.K % GK == 0 &&
+                    g.lda >= g.K && g.lda % 8 == 0 && g.ldo >= g.N &&
+                    g.M * (int64_t)g.lda < ((int64_t)1 << 31) && g.M * (int64_t)g.ldo < ((int64_t)1 << 31) &&
+                    g.N * g.K < ((int64_t)1 << 31) && (!g.q || (g.tokens > 1 && g.M % g.tokens == 0)) &&
+                    ln_w && ln_b && ln_out && ln_ws && g.ldo % 4 == 0 &&
+                    !(((uintptr_t)ln_w | (uintptr_t)ln_b | (uintptr_t)g.out) & 15) && !((uintptr_t)ln_out & 7);
+    if (!ok) {
+        sd_set_error("sd_gemm_resid_ln: invalid argument (SD_EPI_RESID, N <= 1024 and N % 4 == 0, "
+                     "16-B aligned rows, LayerNorm weights / output / ticket workspace)");
+        return -1;
+    }
+    if (g.M == 0) return 0;
+    const VtLnTail lt{ln_w, ln_b, eps, (__bf16 *)ln_out, ln_ws};
+    vt_pick_gemm<false>(g, (hipStream_t)stream, lt);
+    if (hipGetLastError() != hipSuccess) {
+        sd_set_error("sd_gemm_resid_ln: launch failed");
         return -2;
     }
     return 0;

@@ -142,6 +142,12 @@ def _param_key(m: nn.Module):
 # the separate sd_layernorm launches (A/B runs)
 LN_GEMM = os.environ.get("SCENEDINO_AMD_LN_GEMM", "1") != "0"
 LN_GEMM_ALL = os.environ.get("SCENEDINO_AMD_LN_GEMM", "1") == "all"  # also C = 768 (A/B runs)
+# SCENEDINO_AMD_LN_TAIL=1: the block norms written by the preceding residual GEMM's last
+# workgroup per row band (sd_gemm_resid_ln): no LayerNorm launch, a plain GEMM for qkv /
+# fc1.  Bit-equal, but measured slower (ViT-S/16 0.588 -> 0.88 ms, DINOv2-B/14 0.876 ->
+# 1.23: the band's write-through stores, ticket and read-back cost 11-16 us per residual
+# GEMM against the 5 us LayerNorm launch they replace, profiles/r4_ln_tail_ab.txt): off
+LN_TAIL = os.environ.get("SCENEDINO_AMD_LN_TAIL", "0") == "1"
 # the DPT's intermediate token grids written by fc2's residual epilogue (no tokens_to_nhwc
 # launches); SCENEDINO_AMD_FC2_GRID=0 restores the separate launches (A/B runs)
 FC2_GRID = os.environ.get("SCENEDINO_AMD_FC2_GRID", "1") != "0"
@@ -192,8 +198,21 @@ def vit_forward(vit: VisionTransformer, images: torch.Tensor, packed: _Packed,
     # for C = 768 (DINOv2-B/14: 0.90 -> 0.99 ms against sd_layernorm + the 64 x 64-tile
     # sd_gemm) and at 1921 tokens (the narrow tile re-reads the weights per row tile)
     fuse_ln = (C == 384 or LN_GEMM_ALL) and LN_GEMM and B * T <= 1024
+    # the LayerNorm tails: the token-global residual stream is normalised by the residual
+    # GEMM that produced it (one ticket word per 32-row band, self-resetting, per model)
+    tail = LN_TAIL and C <= 1024 and C % 4 == 0
+    ws = None
+    if tail:
+        ws = getattr(packed, "_ln_ws", None)
+        if ws is None or ws.device != dev or ws.numel() < (B * T + 31) // 32:
+            ws = packed._ln_ws = torch.zeros((B * T + 31) // 32, device=dev, dtype=torch.int32)
+    nblk = len(packed.blocks)
+    xn_ready = False  # xn holds this block's norm1 (the previous fc2's tail)
     for i, blk in enumerate(packed.blocks):
-        if fuse_ln:
+        if xn_ready:
+            _lib.gemm(xn, blk["qkv_w"], blk["qkv_b"], _lib.SD_EPI_QKV, qkv=(q, k, vt), tokens=T,
+                      heads=nh)
+        elif fuse_ln:
             _lib.ln_gemm(x, blk["n1w"], blk["n1b"], 1e-6, blk["qkv_w"], blk["qkv_b"],
                          _lib.SD_EPI_QKV, qkv=(q, k, vt), tokens=T, heads=nh)
         else:
@@ -201,22 +220,31 @@ def vit_forward(vit: VisionTransformer, images: torch.Tensor, packed: _Packed,
             _lib.gemm(xn, blk["qkv_w"], blk["qkv_b"], _lib.SD_EPI_QKV, qkv=(q, k, vt), tokens=T,
                       heads=nh)
         _lib.attention(q, k, vt, scale, ao)
-        _lib.gemm(ao, blk["proj_w"], blk["proj_b"], _lib.SD_EPI_RESID, out=x, gamma=blk["ls1"])
-        if fuse_ln:
-            _lib.ln_gemm(x, blk["n2w"], blk["n2b"], 1e-6, blk["fc1_w"], blk["fc1_b"],
-                         _lib.SD_EPI_GELU, out=hid)
-        else:
-            _lib.layernorm(x, blk["n2w"], blk["n2b"], 1e-6, xn)
+        if tail:  # proj + norm2 -> xn, then fc1 as a plain GEMM
+            _lib.gemm(ao, blk["proj_w"], blk["proj_b"], _lib.SD_EPI_RESID, out=x, gamma=blk["ls1"],
+                      ln=(blk["n2w"], blk["n2b"], 1e-6, xn, ws))
             _lib.gemm(xn, blk["fc1_w"], blk["fc1_b"], _lib.SD_EPI_GELU, out=hid)
+        else:
+            _lib.gemm(ao, blk["proj_w"], blk["proj_b"], _lib.SD_EPI_RESID, out=x, gamma=blk["ls1"])
+            if fuse_ln:
+                _lib.ln_gemm(x, blk["n2w"], blk["n2b"], 1e-6, blk["fc1_w"], blk["fc1_b"],
+                             _lib.SD_EPI_GELU, out=hid)
+            else:
+                _lib.layernorm(x, blk["n2w"], blk["n2b"], 1e-6, xn)
+                _lib.gemm(xn, blk["fc1_w"], blk["fc1_b"], _lib.SD_EPI_GELU, out=hid)
+        nxt = packed.blocks[i + 1] if tail and i + 1 < nblk else None
+        ln = (nxt["n1w"], nxt["n1b"], 1e-6, xn, ws) if nxt is not None else None
         if i in intermediate and nhwc and FC2_GRID:  # the DPT's bf16 token grid from fc2's epilogue
             grid = torch.empty(B, gh, gw, C, device=dev, dtype=bf)
             _lib.gemm(hid, blk["fc2_w"], blk["fc2_b"], _lib.SD_EPI_RESID, out=x, gamma=blk["ls2"],
-                      tokens=T, grid_out=grid)
+                      tokens=T, grid_out=grid, ln=ln)
             grids.append(grid)
         else:
-            _lib.gemm(hid, blk["fc2_w"], blk["fc2_b"], _lib.SD_EPI_RESID, out=x, gamma=blk["ls2"])
+            _lib.gemm(hid, blk["fc2_w"], blk["fc2_b"], _lib.SD_EPI_RESID, out=x, gamma=blk["ls2"],
+                      ln=ln)
             if i in intermediate:
                 grids.append(to_grid(x, B, T, C, 1, gh, gw, False))
+        xn_ready = nxt is not None
         if i in intermediate:
             if on_grid is not None:
                 on_grid(len(grids) - 1, grids[-1])

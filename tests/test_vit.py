@@ -154,6 +154,42 @@ def test_resid_epilogue_writes_the_token_grid(gpu, B, gh, gw, C, Kh):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(481, 384, 384), (481, 384, 1536), (481, 768, 768),
+                                   (481, 768, 3072), (1921, 768, 3072), (97, 384, 1536),
+                                   (8192, 1024, 256), (50, 256, 512)])
+def test_resid_gemm_layernorm_tail_equals_two_launches(gpu, M, N, K):
+    """sd_gemm_resid_ln: the residual GEMM whose row bands' last workgroups also write the
+    next block norm's bf16 rows -- the residual stream bit-equal to sd_gemm and the
+    normalised rows bit-equal to sd_layernorm on it, on each tiling the shapes pick (32 x 32
+    split-K tiles with 128- / 256-deep steps, 64 x 64, 128 x 128; ragged last bands), over
+    repeated launches (self-resetting tickets)."""
+    from scenedino_amd import _lib
+    g = torch.Generator().manual_seed(M + N + K)
+    a = _bf(torch.randn(M, K, generator=g)).to(gpu)
+    w = _bf(torch.randn(N, K, generator=g) / math.sqrt(K)).to(gpu)
+    b = (0.1 * torch.randn(N, generator=g)).to(gpu)
+    gam = torch.rand(N, generator=g).to(gpu)
+    lw = (1 + 0.1 * torch.randn(N, generator=g)).to(gpu)
+    lb = (0.1 * torch.randn(N, generator=g)).to(gpu)
+    x0 = (torch.randn(M, N, generator=g) + 0.5).to(gpu)
+    ws = torch.zeros((M + 31) // 32, device=gpu, dtype=torch.int32)
+    x2 = x0.clone()
+    _lib.gemm(a, w, b, _lib.SD_EPI_RESID, out=x2, gamma=gam)
+    ref = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    _lib.layernorm(x2, lw, lb, 1e-6, ref)
+    for _ in range(3):
+        x1 = x0.clone()
+        xn = torch.full((M, N), float("nan"), device=gpu, dtype=torch.bfloat16)
+        _lib.gemm(a, w, b, _lib.SD_EPI_RESID, out=x1, gamma=gam, ln=(lw, lb, 1e-6, xn, ws))
+        torch.cuda.synchronize()
+        assert torch.equal(x1, x2)
+        assert torch.equal(xn, ref)
+        assert int(ws.abs().sum()) == 0  # tickets reset
+    ln_ref = torch.nn.functional.layer_norm(x2, (N,), lw, lb, 1e-6)
+    assert (xn.float() - ln_ref).abs().max().item() < 0.05
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("M,N,K", [(481, 384, 1536), (481, 384, 1024), (97, 64, 2048)])
 def test_gemm_cross_workgroup_split_k(gpu, M, N, K, monkeypatch):
     """32 x 32 tiles whose K range is split over workgroups (SD_SPLITK_WG=512 forces it on the ViT-S/16 fc2 at 481 tokens: two
@@ -336,6 +372,26 @@ def test_encoder_vit_b8_1921_tokens_two_blocks(gpu):
     for a, r in zip(grids + [final], ref):
         rel = ((a.double().cpu() - r.double()).norm() / r.double().norm()).item()
         assert rel <= 3e-2, rel
+
+
+@pytest.mark.gpu
+def test_encoder_layernorm_tails_bit_equal(gpu, monkeypatch):
+    """DINOv2-B/14 (C = 768: separate LayerNorm launches) with the block norms written by the
+    residual GEMMs' tails (SCENEDINO_AMD_LN_TAIL=1, off by default: slower) gives the same
+    grids bit for bit."""
+    from scenedino_amd.models.backbones.dino import vit as vm
+    enc = vm.DINOv2Encoder("vit-b", (64, 224), [3, 6, 9], False, "v2")
+    init_vit(enc.model.vit, 9)
+    enc = enc.to(gpu).eval()
+    enc.model.use_graph = False
+    img = (torch.rand(2, 3, 64, 224, generator=torch.Generator().manual_seed(10)) * 2 - 1).to(gpu)
+    with torch.no_grad():
+        monkeypatch.setattr(vm, "LN_TAIL", False)
+        ref = enc(img)
+        monkeypatch.setattr(vm, "LN_TAIL", True)
+        out = enc(img)
+    for a, b in zip(ref, out):
+        assert torch.equal(a, b)
 
 
 @pytest.mark.gpu
