@@ -22,7 +22,7 @@ dev = "cuda"
 dr = MlpDimReduction(768, 64, 128).to(dev).eval()
 sh = SemanticHead(19, 19, 768, 64).to(dev).eval()
 pk = PackedSegHead(dr, sh.stego_head, sh.stego_cluster_head)
-x = torch.randn(256 * 256 * 32, 64, device=dev)
+x = torch.randn(256 * 256 * 32, 64, device=dev).to(torch.bfloat16)  # C5 passes bf16 codes
 buf = (ctypes.c_ulonglong * 16)()
 _lib.seg_query(x, pk.rec, want_labels=True)
 torch.cuda.synchronize()
