@@ -1061,6 +1061,10 @@ def main_c2(args, world, rank, device, dist, host_stage):
             "algorithmic_flops_per_launch": flops,
             "executed_mfma_flops_per_launch": exec_flops,
             "executed_tflops": exec_flops / (kern_ms * 1e-3) / 1e12,
+            # frac is priced on SURVEY §8(d)'s algorithmic FLOPs; the MFMA utilisation of the
+            # instructions the kernels actually issue is executed_frac
+            "frac_basis": "algorithmic",
+            "executed_frac": exec_flops / (kern_ms * 1e-3) / 1e12 / peak,
         },
     }
     if "gathered_maps" in r:
