@@ -347,6 +347,23 @@ __global__ void __launch_bounds__(512) k_conv_big(sd_gemm_args g) {
             const uint32_t sub = n / cout, co = n - sub * cout, dy = sub / kk, dx = sub - dy * kk;
             soff = dy * iw * kk * cout + dx * cout + co;  // offset of (dy, dx, co) from pixel (y kk, x kk)
         }
+        // the residual rows of every iteration loaded before the first store (loads after
+        // a store to possibly-aliasing memory wait for it: one round trip per iteration)
+        constexpr int NIT = ER * CPRW / 64;
+        bf16x8 rpre[RES ? NIT : 1][2];
+        if constexpr (RES && STF32 && !OUTF32) {
+#pragma unroll
+            for (int it = 0; it < NIT; ++it) {
+                const int idx = it * 64 + lane, r = idx / CPRW, ch = idx - r * CPRW;
+                const int64_t m = m0 + wm * WM + part * ER + r;
+                const int64_t n = n0 + wn * WN + ch * CC;
+                const bool ok = m < g.M && n < g.N;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) rpre[it][0][u] = rpre[it][1][u] = (__bf16)0.f;
+                if (ok && g.res) rpre[it][0] = *(const bf16x8 *)((const __bf16 *)g.res + m * g.ldo + n);
+                if (ok && g.res2) rpre[it][1] = *(const bf16x8 *)((const __bf16 *)g.res2 + m * g.ldo + n);
+            }
+        }
 #pragma unroll
         for (int it = 0; it < ER * CPRW / 64; ++it) {
             const int idx = it * 64 + lane, r = idx / CPRW, ch = idx - r * CPRW;
@@ -370,16 +387,14 @@ __global__ void __launch_bounds__(512) k_conv_big(sd_gemm_args g) {
                 const cvf4 lo = *(const cvf4 *)(reg + r * PITCH + ch * 32);
                 const cvf4 hi = *(const cvf4 *)(reg + r * PITCH + ch * 32 + 16);
                 float f[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                if (RES) {
+                if constexpr (RES) {
                     if (g.res) {
-                        const bf16x8 a = *(const bf16x8 *)((const __bf16 *)g.res + m * g.ldo + n);
 #pragma unroll
-                        for (int u = 0; u < 8; ++u) f[u] += (float)a[u];
+                        for (int u = 0; u < 8; ++u) f[u] += (float)rpre[it][0][u];
                     }
                     if (g.res2) {
-                        const bf16x8 a = *(const bf16x8 *)((const __bf16 *)g.res2 + m * g.ldo + n);
 #pragma unroll
-                        for (int u = 0; u < 8; ++u) f[u] += (float)a[u];
+                        for (int u = 0; u < 8; ++u) f[u] += (float)rpre[it][1][u];
                     }
                 }
                 bf16x8 o;

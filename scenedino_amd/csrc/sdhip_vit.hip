@@ -774,37 +774,134 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g, float *__restrict_
         }
         return;
     }
-    // unstaged epilogues (residual update, patch embedding): lane-scattered 4-B stores
+    // unstaged epilogues (residual update, patch embedding): lane-scattered 4-B stores.
+    // The residual update issues every load (bias, layer scale, the residual rows) before
+    // its first store: interleaved, each store-then-load pair drained the vector memory
+    // counter (it counts stores too), one memory round trip per accumulator register
+    static_assert(!VT_MF16, "the unstaged epilogues take one output column per lane and tile");
+    // SD_EPI_RESID, outputs < 2 GiB: buffer loads / stores whose offsets (out-of-range
+    // rows and columns -> past the buffer: loads read 0, stores are dropped) and data sit
+    // in registers of their own, computed before the first store, so the 16 stores of a
+    // tile issue back to back (a store whose address or data register is rewritten while
+    // the store is pending, or one under its own exec branch, costs a vmcnt(0) drain)
+    bool resid_done = false;
+    if constexpr (EPI == SD_EPI_RESID) {
+        if (g.M * g.ldo < ((int64_t)1 << 29) && (!g.q || g.M * g.N < ((int64_t)1 << 30))) {
+            resid_done = true;
+            if (!(SK && wave != 0)) {
+                const __amdgpu_buffer_rsrc_t rsO =
+                    __builtin_amdgcn_make_buffer_rsrc(g.out, 0, (uint32_t)(g.M * g.ldo * 4), 0x00020000);
+                const uint32_t T = g.tokens > 1 ? (uint32_t)g.tokens : 1u;
+                const __amdgpu_buffer_rsrc_t rsQ = __builtin_amdgcn_make_buffer_rsrc(
+                    g.q ? g.q : g.out, 0, g.q ? (uint32_t)((g.M / T) * (T - 1) * g.N * 2) : 0u, 0x00020000);
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-        if (SK && wave != 0) break;
+                for (int j = 0; j < TN; ++j) {
+                    const int64_t n = n0 + wn * WN + j * 32 + vt_col(0, lane);
+                    const bool nok = n < g.N;
+                    const float bias = (g.bias && nok) ? g.bias[n] : 0.f;
+                    const float gam = (g.gamma && nok) ? g.gamma[n] : 1.f;
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+                    for (int i = 0; i < TM; ++i) {
+                        uint32_t va[16];
+                        float nv[16];
 #pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const int64_t n = n0 + wn * WN + j * 32 + vt_col(q, lane);
-                const int64_t m = m0 + wm * WM + i * 32 + vt_row(q, lane);
-                if (m >= g.M || n >= g.N) continue;
-                const float bias = g.bias ? g.bias[n] : 0.f;
-                const float v = acc[i][j][q] + bias;
-                if constexpr (EPI == SD_EPI_RESID || EPI == VT_EPI_RESID_LN) {
-                    const float gam = g.gamma ? g.gamma[n] : 1.f;
-                    float *o = (float *)g.out + m * g.ldo + n;
-                    const float nv = *o + gam * v;
-                    if (EPI == VT_EPI_RESID_LN) __hip_atomic_store(o, nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    else *o = nv;
-                    if (g.q) {  // the intermediate-layer grid (k_tokens_to_nhwc's rounding)
-                        const uint32_t T = (uint32_t)g.tokens, b = (uint32_t)m / T, tok = (uint32_t)m - b * T;
-                        if (tok > 0) ((__bf16 *)g.q)[((int64_t)b * (T - 1) + tok - 1) * g.N + n] = (__bf16)nv;
+                        for (int q = 0; q < 16; ++q) {
+                            const int64_t m = m0 + wm * WM + i * 32 + vt_row(q, lane);
+                            va[q] = (nok && m < g.M) ? (uint32_t)((m * g.ldo + n) * 4) : 0x80000000u;
+                            nv[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsO, va[q], 0, 0));
+                        }
+#pragma unroll
+                        for (int q = 0; q < 16; ++q) nv[q] = nv[q] + gam * (acc[i][j][q] + bias);
+#pragma unroll
+                        for (int q = 0; q < 16; ++q)
+                            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, nv[q]), rsO, va[q], 0, 0);
+                        if (g.q) {  // the intermediate-layer grid (k_tokens_to_nhwc's rounding)
+                            uint32_t qa[16];
+                            uint16_t qv[16];
+#pragma unroll
+                            for (int q = 0; q < 16; ++q) {
+                                const int64_t m = m0 + wm * WM + i * 32 + vt_row(q, lane);
+                                const uint32_t b = (uint32_t)m / T, tok = (uint32_t)m - b * T;
+                                qa[q] = (nok && m < g.M && tok > 0)
+                                            ? (uint32_t)((((int64_t)b * (T - 1) + tok - 1) * g.N + n) * 2)
+                                            : 0x80000000u;
+                                qv[q] = __builtin_bit_cast(uint16_t, (__bf16)nv[q]);
+                            }
+#pragma unroll
+                            for (int q = 0; q < 16; ++q) __builtin_amdgcn_raw_buffer_store_b16(qv[q], rsQ, qa[q], 0, 0);
+                        }
                     }
-                } else {  // SD_EPI_PATCH: patch row m = b * patches + p -> token 1 + p
-                    const uint32_t bq = (uint32_t)m / (uint32_t)g.patches;
-                    const int64_t b = bq, p = m - b * g.patches;
-                    const int64_t tok = 1 + p;
-                    const int64_t T = g.patches + 1;
-                    ((float *)g.out)[(b * T + tok) * g.ldo + n] = v + g.pos[tok * g.N + n];
                 }
             }
+        }
+    }
+    if constexpr (EPI == SD_EPI_RESID || EPI == VT_EPI_RESID_LN) {
+        if (!(SK && wave != 0) && !resid_done) {
+            float bj[TN], gj[TN], ov[TM][TN][16];
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int64_t n = n0 + wn * WN + j * 32 + vt_col(0, lane);
+                bj[j] = (g.bias && n < g.N) ? g.bias[n] : 0.f;
+                gj[j] = (g.gamma && n < g.N) ? g.gamma[n] : 1.f;
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) {
+                        const int64_t m = m0 + wm * WM + i * 32 + vt_row(q, lane);
+                        ov[i][j][q] = (m < g.M && n < g.N) ? ((const float *)g.out)[m * g.ldo + n] : 0.f;
+                    }
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) {
+                        const int64_t n = n0 + wn * WN + j * 32 + vt_col(q, lane);
+                        const int64_t m = m0 + wm * WM + i * 32 + vt_row(q, lane);
+                        if (m >= g.M || n >= g.N) continue;
+                        const float v = acc[i][j][q] + bj[j];
+                        const float nv = ov[i][j][q] + gj[j] * v;
+                        float *o = (float *)g.out + m * g.ldo + n;
+                        if (EPI == VT_EPI_RESID_LN) __hip_atomic_store(o, nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        else *o = nv;
+                        if (g.q) {  // the intermediate-layer grid (k_tokens_to_nhwc's rounding)
+                            const uint32_t T = (uint32_t)g.tokens, b = (uint32_t)m / T, tok = (uint32_t)m - b * T;
+                            if (tok > 0) ((__bf16 *)g.q)[((int64_t)b * (T - 1) + tok - 1) * g.N + n] = (__bf16)nv;
+                        }
+                    }
+        }
+    }
+    if constexpr (EPI == SD_EPI_PATCH) {  // patch row m = b * patches + p -> token 1 + p
+        if (!(SK && wave != 0)) {
+            float bj[TN], pv[TM][TN][16];  // (loads first, as above)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int64_t n = n0 + wn * WN + j * 32 + vt_col(0, lane);
+                bj[j] = (g.bias && n < g.N) ? g.bias[n] : 0.f;
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) {
+                        const int64_t m = m0 + wm * WM + i * 32 + vt_row(q, lane);
+                        const int64_t tok = 1 + (m - (int64_t)((uint32_t)m / (uint32_t)g.patches) * g.patches);
+                        pv[i][j][q] = (m < g.M && n < g.N) ? g.pos[tok * g.N + n] : 0.f;
+                    }
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) {
+                        const int64_t n = n0 + wn * WN + j * 32 + vt_col(q, lane);
+                        const int64_t m = m0 + wm * WM + i * 32 + vt_row(q, lane);
+                        if (m >= g.M || n >= g.N) continue;
+                        const int64_t b = (uint32_t)m / (uint32_t)g.patches, p = m - b * g.patches;
+                        const int64_t T = g.patches + 1;
+                        ((float *)g.out)[(b * T + 1 + p) * g.ldo + n] = (acc[i][j][q] + bj[j]) + pv[i][j][q];
+                    }
+        }
     }
     if constexpr (EPI == VT_EPI_RESID_LN) vt_ln_tail<BM>(g, lt, m0, smem, tid);
 }
