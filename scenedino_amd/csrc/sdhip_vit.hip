@@ -1419,15 +1419,40 @@ __global__ void __launch_bounds__(256) k_tokens_to_grid(const float *__restrict_
     const int pi = min(tok, n_tok - 1) - bb * ghw;
     if (wave == 0) rows[lane] = x + ((int64_t)bb * T + n_prefix + pi) * C;
     __syncthreads();
-    if (l2) {
+    if (l2 && C <= 1024) {
+        // 4 tokens' rows loaded together per round trip (one token at a time: 16 dependent
+        // L2 round trips per wave); the same per-lane sums in the same order
+        for (int i0 = wave; i0 < 64; i0 += 16) {
+            float v[4][16];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int i = i0 + 4 * u;
+                const bool ok = tok0 + i < n_tok;
+#pragma unroll
+                for (int k = 0; k < 16; ++k) {
+                    const int c = lane + 64 * k;
+                    v[u][k] = (ok && c < C) ? rows[i][c] : 0.f;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                float s2 = 0.f;
+#pragma unroll
+                for (int k = 0; k < 16; ++k) s2 = fmaf(v[u][k], v[u][k], s2);
+                // F.normalize(p=2, eps=1e-12) applied twice (vit.py:188,
+                // dinov2_module.py:282): the second pass divides a unit vector by its norm
+                const float scale = 1.f / fmaxf(sqrtf(vt_wave_sum(s2)), 1e-12f);
+                if (lane == 0) sc[i0 + 4 * u] = tok0 + i0 + 4 * u < n_tok ? scale : 1.f;
+            }
+        }
+        __syncthreads();
+    } else if (l2) {
         for (int i = wave; i < 64; i += 4) {
             float scale = 1.f;
             if (tok0 + i < n_tok) {
                 const float *xr = rows[i];
                 float s2 = 0.f;
                 for (int c = lane; c < C; c += 64) s2 = fmaf(xr[c], xr[c], s2);
-                // F.normalize(p=2, eps=1e-12) applied twice (vit.py:188,
-                // dinov2_module.py:282): the second pass divides a unit vector by its norm
                 scale = 1.f / fmaxf(sqrtf(vt_wave_sum(s2)), 1e-12f);
             }
             if (lane == 0) sc[i] = scale;
