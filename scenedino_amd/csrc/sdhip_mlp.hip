@@ -27,6 +27,9 @@ extern "C" void sd_set_error(const char *msg);
 #define ML_DYLD 72  // dY row: D dino (<= 64) ... d out_0, zeros
 #define ML_MAXKS 20  // k-steps of x held in registers (kx <= 320)
 #define ML_MAXKO ((ML_DYLD + 15) / 16)  // k-steps over the outputs (D + 1 <= 72)
+#ifndef ML_FWD_BUF
+#define ML_FWD_BUF 1
+#endif
 
 template <int P>
 __device__ __forceinline__ typename T16<P>::Frag ml_frag(const f32x16 &acc, int c) {
@@ -63,6 +66,19 @@ __global__ void __launch_bounds__(ML_WAVES * 64) k_mlp_fwd(const sd_mlp_train_ar
     const int64_t ntile = (a.N + 31) >> 5;
     const __amdgpu_buffer_rsrc_t rx =
         sd_rsrc(a.x, (uint32_t)((a.N * a.ldx) * (int64_t)sizeof(E)));
+    // the output stores go through buffers with out-of-range points past the end (dropped)
+    // and every value in a register of its own, the output biases loaded once up front: no
+    // store drains the memory counter for the next (ML_FWD_BUF 0: the per-element stores)
+    const bool obuf = ML_FWD_BUF && a.N * a.D < ((int64_t)1 << 29);
+    const __amdgpu_buffer_rsrc_t rdn = sd_rsrc(a.dino, obuf ? (uint32_t)(a.N * a.D * 4) : 0u);
+    const __amdgpu_buffer_rsrc_t rsg = sd_rsrc(a.sigma, obuf ? (uint32_t)(a.N * 4) : 0u);
+    float bdv[(ML_DYLD + 31) / 32];
+#pragma unroll
+    for (int u = 0; u < (ML_DYLD + 31) / 32; ++u) {
+        const int col = 32 * u + r;
+        bdv[u] = (u < U && col < a.D) ? a.b_out[1 + col] : 0.f;
+    }
+    const float bsg = a.b_out[0];
     for (int64_t tile = (int64_t)blockIdx.x * ML_WAVES + wave; tile < ntile;
          tile += (int64_t)gridDim.x * ML_WAVES) {
         const int64_t p0 = tile * 32;
@@ -109,7 +125,9 @@ __global__ void __launch_bounds__(ML_WAVES * 64) k_mlp_fwd(const sd_mlp_train_ar
         Frag af[8];
 #pragma unroll
         for (int s = 0; s < 8; ++s) af[s] = ml_frag<P>(acc[s >> 1], s & 1);
-        for (int u = 0; u < U; ++u) {
+#pragma unroll
+        for (int u = 0; u < (ML_DYLD + 31) / 32; ++u) {  // (U <= 3: D + 1 <= 72)
+            if (u >= U) break;
             f32x16 o;
 #pragma unroll
             for (int i = 0; i < 16; ++i) o[i] = 0.f;
@@ -118,6 +136,29 @@ __global__ void __launch_bounds__(ML_WAVES * 64) k_mlp_fwd(const sd_mlp_train_ar
             // o: row = point p0 + 8 (i >> 2) + 4 h + (i & 3), column = output 32 u + r
             // (outputs 0 .. D-1 = dino, D = sigma)
             const int col = 32 * u + r;
+            if (obuf) {
+                float vd[16], vs[16];
+                uint32_t od[16], os[16];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int64_t p = p0 + 8 * (i >> 2) + 4 * h + (i & 3);
+                    const bool pin = p < a.N;
+                    vd[i] = o[i] + bdv[u];
+                    od[i] = (pin && col < a.D) ? (uint32_t)((p * a.D + col) * 4) : 0x80000000u;
+                    os[i] = (pin && col == a.D) ? (uint32_t)(p * 4) : 0x80000000u;
+                }
+#pragma unroll
+                for (int i = 0; i < 16; ++i)
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, vd[i]), rdn, od[i], 0, 0);
+                if (32 * u + 32 > a.D) {  // the tile holding sigma (wave-uniform)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) vs[i] = ml_softplus(o[i] + bsg);
+#pragma unroll
+                    for (int i = 0; i < 16; ++i)
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, vs[i]), rsg, os[i], 0, 0);
+                }
+                continue;
+            }
             if (col < a.D) {
                 const float bd = a.b_out[1 + col];
 #pragma unroll
