@@ -80,22 +80,55 @@ k_field_gather(const float *__restrict__ xyz, int64_t B, int64_t P,
     const int64_t plane = (int64_t)Hf * Wf * C;
     const int64_t cplane = (int64_t)Hc * Wc * 4;
     const int64_t nruns = (NP + TR_FRUN - 1) / TR_FRUN;
-    for (int64_t run = (int64_t)blockIdx.x * TR_WAVES + (threadIdx.x >> 6); run < nruns;
-         run += (int64_t)gridDim.x * TR_WAVES) {
+    // Order within a run: every load (the next run's coordinates, the colour taps, the grid
+    // taps) before the run's first store -- a load issued after a store waits for it in
+    // the memory counter, so interleaving cost a round trip per phase
+    const int64_t rstep = (int64_t)gridDim.x * TR_WAVES;
+    int64_t run = (int64_t)blockIdx.x * TR_WAVES + (threadIdx.x >> 6);
+    float qx = 0.f, qy = 0.f, qz = 0.f;  // lane < TR_FRUN: its point of the run
+    auto fetch = [&](int64_t rn) {
+        const int64_t p = rn * TR_FRUN + lane;
+        if (lane < TR_FRUN && rn < nruns && p < NP) {
+            qx = xyz[p * 3];
+            qy = xyz[p * 3 + 1];
+            qz = xyz[p * 3 + 2];
+        }
+    };
+    fetch(run);
+    for (; run < nruns; run += rstep) {
         const int64_t p0 = run * TR_FRUN;
         const int n = (int)(p0 + TR_FRUN < NP ? TR_FRUN : NP - p0);
+        const float px0 = qx, py0 = qy, pz0 = qz;
+        fetch(run + rstep);
         int gi[4] = {0, 0, 0, 0}, gb = 0;
         float gw[4] = {0.f, 0.f, 0.f, 0.f}, gv[3] = {0.f, 0.f, 0.f};
+        bool invf = false;
         if (lane < n) {
             const int64_t p = p0 + lane;
             const int64_t b = p / P;
-            const PointGeo geo = sd_point_geo(cam_f + b * SD_CAM_WORDS, xyz[p * 3], xyz[p * 3 + 1],
-                                              xyz[p * 3 + 2], Wf, Hf);
+            const PointGeo geo = sd_point_geo(cam_f + b * SD_CAM_WORDS, px0, py0, pz0, Wf, Hf);
             gi[0] = geo.t.i00; gi[1] = geo.t.i01; gi[2] = geo.t.i10; gi[3] = geo.t.i11;
             gw[0] = geo.t.w00; gw[1] = geo.t.w01; gw[2] = geo.t.w10; gw[3] = geo.t.w11;
             gv[0] = geo.v[0]; gv[1] = geo.v[1]; gv[2] = geo.v[2];
             gb = (int)b;
-            if (invalid_f) invalid_f[p] = geo.inv_f ? 1 : 0;
+            invf = geo.inv_f;
+        }
+        // colour samples / masks: lane = (point, view); the point's coordinates from its lane
+        const bool cdo = nv > 0 && (rgb || invalid) && lane < n * nv;
+        const int cj = cdo ? lane / nv : 0;
+        const float cx = __shfl(px0, cj), cy = __shfl(py0, cj), cz = __shfl(pz0, cj);
+        float col[3] = {0.f, 0.f, 0.f};
+        float cinv = 0.f;
+        if (cdo) {
+            const int v = lane - cj * nv;
+            const int64_t b = (p0 + cj) / P;
+            const bool ic = sd_color_view(cam_c + (b * nv + v) * SD_CAM_WORDS, img + (b * nv + v) * cplane,
+                                          Wc, Hc, cx, cy, cz, col);
+            if (invalid) {
+                float x, y, zc;  // the encoder-frustum test of sd_point_geo, same arithmetic
+                sd_project(cam_f + b * SD_CAM_WORDS, cx, cy, cz, x, y, zc);
+                cinv = (ic | sd_outside(x, y, zc)) ? 1.f : 0.f;
+            }
         }
         for (int c = lane * 4; c < C; c += 256) {
             f32x4 t[TR_FRUN][4];
@@ -150,26 +183,17 @@ k_field_gather(const float *__restrict__ xyz, int64_t B, int64_t P,
                 }
             }
         }
-        // colour samples / masks: lane = (point, view)
-        if (nv > 0 && (rgb || invalid) && lane < n * nv) {
-            const int j = lane / nv, v = lane - j * nv;
-            const int64_t p = p0 + j;
-            const int64_t b = p / P;
-            const float px = xyz[p * 3], py = xyz[p * 3 + 1], pz = xyz[p * 3 + 2];
-            float col[3];
-            const bool ic = sd_color_view(cam_c + (b * nv + v) * SD_CAM_WORDS, img + (b * nv + v) * cplane,
-                                          Wc, Hc, px, py, pz, col);
+        if (cdo) {
+            const int64_t p = p0 + cj;
+            const int v = lane - cj * nv;
             if (rgb) {
                 rgb[(p * nv + v) * 3] = col[0];
                 rgb[(p * nv + v) * 3 + 1] = col[1];
                 rgb[(p * nv + v) * 3 + 2] = col[2];
             }
-            if (invalid) {
-                float x, y, zc;  // the encoder-frustum test of sd_point_geo, same arithmetic
-                sd_project(cam_f + b * SD_CAM_WORDS, px, py, pz, x, y, zc);
-                invalid[p * nv + v] = (ic | sd_outside(x, y, zc)) ? 1.f : 0.f;
-            }
+            if (invalid) invalid[p * nv + v] = cinv;
         }
+        if (lane < n && invalid_f) invalid_f[p0 + lane] = invf ? 1 : 0;
     }
 }
 
