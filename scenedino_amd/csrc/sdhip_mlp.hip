@@ -592,47 +592,48 @@ __global__ void __launch_bounds__(256) k_wgrad(const sd_wgrad_args g) {
     for (int j = 0; j < NT; ++j)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
-    uint4 st[WG_MAXLD];  // staged chunk pieces (nld <= WG_MAXLD)
-    auto gload = [&](int64_t p0) {
+    // staged chunk pieces (nld <= WG_MAXLD), two sets: chunk k + 2 loads while chunk k is
+    // multiplied (one set in flight left each chunk's MFMAs waiting on a memory round trip)
+    uint4 st0[WG_MAXLD], st1[WG_MAXLD];
+    uint32_t ok0 = 0, ok1 = 0;  // which pieces are real (the zeros are applied at the LDS store)
+    // every load issued unconditionally (invalid lanes read the first row, dropped at the
+    // LDS store), so the count in flight is static and the wait for one set leaves the
+    // other in flight
+    auto gload = [&](uint4 (&st)[WG_MAXLD], uint32_t &okm, int64_t p0) {
+        okm = 0;
+#pragma unroll
+        for (int i = 0; i < WG_MAXLD; ++i) {
+            const int c = tid + 256 * i;
+            const bool isa = c < nca;
+            const int cc = isa ? c : c - nca;
+            const int row = isa ? c / ca : cc / cb;
+            const int col = isa ? (c - row * ca) * 8 : nb0 + (cc - row * cb) * 8;
+            const int64_t p = p0 + row;
+            const bool ok = i < nld && c < nca + ncb && p < p_hi;
+            const uint16_t *src = !ok ? (const uint16_t *)g.a
+                                      : isa ? (const uint16_t *)g.a + p * g.lda + col
+                                            : (const uint16_t *)g.b + p * g.ldb + col;
+            st[i] = *(const uint4 *)src;
+            okm |= ok ? 1u << i : 0u;
+        }
+    };
+    auto lstore = [&](const uint4 (&st)[WG_MAXLD], uint32_t okm) {
 #pragma unroll
         for (int i = 0; i < WG_MAXLD; ++i) {
             const int c = tid + 256 * i;
             if (i < nld && c < nca + ncb) {
+                const uint4 v = (okm >> i) & 1u ? st[i] : uint4{0u, 0u, 0u, 0u};
                 if (c < nca) {
                     const int row = c / ca, col = (c - row * ca) * 8;
-                    const int64_t p = p0 + row;
-                    st[i] = p < p_hi ? *(const uint4 *)((const uint16_t *)g.a + p * g.lda + col)
-                                     : uint4{0u, 0u, 0u, 0u};
+                    *(uint4 *)(sA + row * rsa + col) = v;
                 } else {
                     const int cc = c - nca, row = cc / cb, col = (cc - row * cb) * 8;
-                    const int64_t p = p0 + row;
-                    st[i] = p < p_hi ? *(const uint4 *)((const uint16_t *)g.b + p * g.ldb + nb0 + col)
-                                     : uint4{0u, 0u, 0u, 0u};
+                    *(uint4 *)(sB + row * rsb + col) = v;
                 }
             }
         }
     };
-    auto lstore = [&]() {
-#pragma unroll
-        for (int i = 0; i < WG_MAXLD; ++i) {
-            const int c = tid + 256 * i;
-            if (i < nld && c < nca + ncb) {
-                if (c < nca) {
-                    const int row = c / ca, col = (c - row * ca) * 8;
-                    *(uint4 *)(sA + row * rsa + col) = st[i];
-                } else {
-                    const int cc = c - nca, row = cc / cb, col = (cc - row * cb) * 8;
-                    *(uint4 *)(sB + row * rsb + col) = st[i];
-                }
-            }
-        }
-    };
-    if (p_lo < p_hi) gload(p_lo);
-    for (int64_t p0 = p_lo; p0 < p_hi; p0 += 32) {
-        __syncthreads();  // the previous chunk's reads are done
-        lstore();
-        __syncthreads();
-        if (p0 + 32 < p_hi) gload(p0 + 32);  // next chunk in flight under this one
+    auto compute = [&]() {
         if (own) {
 #pragma unroll
             for (int s = 0; s < 2; ++s) {  // two k-steps of 16 points
@@ -648,6 +649,21 @@ __global__ void __launch_bounds__(256) k_wgrad(const sd_wgrad_args g) {
                 }
             }
         }
+    };
+    if (p_lo < p_hi) gload(st0, ok0, p_lo);
+    if (p_lo + 32 < p_hi) gload(st1, ok1, p_lo + 32);
+    for (int64_t p0 = p_lo; p0 < p_hi; p0 += 64) {
+        __syncthreads();  // the previous chunk's reads are done
+        lstore(st0, ok0);
+        __syncthreads();
+        if (p0 + 64 < p_hi) gload(st0, ok0, p0 + 64);
+        compute();
+        if (p0 + 32 >= p_hi) break;  // workgroup-uniform
+        __syncthreads();
+        lstore(st1, ok1);
+        __syncthreads();
+        if (p0 + 96 < p_hi) gload(st1, ok1, p0 + 96);
+        compute();
     }
     // partial tile: acc[i][j] register e = C[32 ti + 8 (e >> 2) + 4 h + (e & 3)][32 j + r]
     float *out = g.part + (int64_t)blockIdx.x * MaP * NbP;
