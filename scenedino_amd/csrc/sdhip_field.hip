@@ -885,6 +885,46 @@ k_composite(const float *__restrict__ z, const float *__restrict__ sigma,
     const int nf = (int)((F + 63) / 64);
     float facc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     float cacc = 0.f;
+    if (K <= 32 && nf <= 1) {
+        // every load first (lane k: z, sigma of sample k; the K feature / colour values of
+        // the lane's column), the recurrence over k in registers (readlane broadcasts, the
+        // same products in the same order), every store at the end: the loop used to store
+        // the weights / alphas of sample k before loading sample k + 1, one memory round
+        // trip per sample
+        const float zl = lane < K ? zr[lane] : 0.f;
+        const float zn = lane + 1 < K ? zr[lane + 1] : 0.f;
+        const float sl = lane < K ? sr[lane] : 0.f;
+        float fv[32], cv[32];
+#pragma unroll
+        for (int k = 0; k < 32; ++k) {
+            fv[k] = (feat && k < K && lane < F) ? feat[(ray * K + k) * F + lane] : 0.f;
+            cv[k] = (rgb && k < K && lane < Cc) ? rgb[(ray * K + k) * Cc + lane] : 0.f;
+        }
+        const float delta = (lane + 1 < K) ? zn - zl : 1e10f;
+        float alpha = 1.f - expf(-fabsf(delta) * fmaxf(sl, 0.f));
+        if (hard_cap && lane == K - 1) alpha = 1.f;
+        float wl = 0.f;
+#pragma unroll
+        for (int k = 0; k < 32; ++k) {
+            if (k >= K) break;
+            const float ak = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, alpha), k));
+            const float zk = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, zl), k));
+            const float w = ak * T;
+            T = T * ((1.f - ak) + 1e-10f);
+            dep += w * zk;
+            if (lane == k) wl = w;
+            if (feat) facc[0] += fv[k] * w;
+            if (rgb) cacc += w * cv[k];
+        }
+        if (lane < K) {
+            if (weights) weights[ray * K + lane] = wl;
+            if (alphas) alphas[ray * K + lane] = alpha;
+        }
+        if (lane == 0 && depth) depth[ray] = dep;
+        if (feat && feat_out && lane < F) feat_out[ray * F + lane] = facc[0];
+        if (rgb && rgb_out && lane < Cc) rgb_out[ray * Cc + lane] = cacc;
+        return;
+    }
     for (int k = 0; k < K; ++k) {
         float zk = zr[k];
         float delta = (k + 1 < K) ? zr[k + 1] - zk : 1e10f;
