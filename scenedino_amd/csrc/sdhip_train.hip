@@ -358,8 +358,35 @@ k_composite_bwd(const float *__restrict__ z, const float *__restrict__ sigma,
             sg[k] = g;
         }
         sd_wave_lds_sync();
-        // phase 2 (one lane): T_k forward, U_k backward; sa <- w_k, sg <- dL/da_k
-        if (lane == 0) {
+        // phase 2: T_k forward, U_k backward; sa <- w_k, sg <- dL/da_k.  K <= 64: the
+        // recurrences over readlane broadcasts of the lanes' (alpha, g) (the same products
+        // in the same order as the one-lane LDS loop below, without its LDS round trips)
+        if (K <= 64) {
+            const float al = lane < K ? sa[lane] : 0.f, gl = lane < K ? sg[lane] : 0.f;
+            float T = 1.f, tl = 0.f;
+            for (int k = 0; k < K; ++k) {
+                if (lane == k) tl = T;
+                const float a = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, al), k));
+                T = T * ((1.f - a) + 1e-10f);
+            }
+            float U = 0.f, dal = 0.f, wl = 0.f;
+            for (int k = K - 1; k >= 0; --k) {
+                const float a = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, al), k));
+                const float g = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, gl), k));
+                const float tk = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, tl), k));
+                const float da = tk * (g - U);
+                U = g * a + ((1.f - a) + 1e-10f) * U;
+                if (lane == k) {
+                    dal = da;
+                    wl = a * tk;
+                }
+            }
+            sd_wave_lds_sync();  // every lane has read its (alpha, g)
+            if (lane < K) {
+                sg[lane] = dal;
+                sa[lane] = wl;
+            }
+        } else if (lane == 0) {
             float T = 1.f;
             for (int k = 0; k < K; ++k) {
                 st[k] = T;
@@ -391,7 +418,13 @@ k_composite_bwd(const float *__restrict__ z, const float *__restrict__ sigma,
             d_sigma[ray * K + k] = ds;
         }
         // phase 4 (lane = channel): d feat_k = w_k dL/dfeat, d rgb_k = w_k dL/drgb
-        if (d_feat && g_feat) {
+        if (d_feat && g_feat && F <= 64) {  // the lane's dL/dfeat loaded once, not after every store
+            const float gfl = lane < F ? g_feat[ray * F + lane] : 0.f;
+            for (int k = 0; k < K; ++k) {
+                const float w = sa[k];
+                if (lane < F) d_feat[(ray * K + k) * (int64_t)F + lane] = w * gfl;
+            }
+        } else if (d_feat && g_feat) {
             for (int k = 0; k < K; ++k) {
                 const float w = sa[k];
                 for (int c = lane; c < F; c += 64)
