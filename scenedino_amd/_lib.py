@@ -22,6 +22,11 @@ SD_BF16 = 1
 SD_F16 = 2
 TORCH_DTYPE = {SD_F32: torch.float32, SD_BF16: torch.bfloat16, SD_F16: torch.float16}
 SD_OF_TORCH = {v: k for k, v in TORCH_DTYPE.items()}
+# element type of the render / field kernels' grid operands (the NHWC grid, the projected
+# grid P) and of every MLP operand upstream of sigma, per precision mode: f16 in both 16-bit
+# modes -- the bf16 mode keeps bf16 for the DINO output layer only (include/sdhip.h sd_mlp,
+# csrc/sdhip_render.h RMode; SURVEY §8(c)'s 1e-2 m depth contract)
+FIELD_DTYPE = {SD_F32: SD_F32, SD_BF16: SD_F16, SD_F16: SD_F16}
 
 _vp = ctypes.c_void_p
 _i64 = ctypes.c_int64
@@ -389,11 +394,12 @@ def render_fused(args: SdRenderArgs, mlp: SdMlp, ref_tensor):
 
 
 def project_grid(grid, mlp: SdMlp, dtype):
-    """P = W_in[:, :C] . grid + b_in per pixel: (B, Hf, Wf, 128) in dtype (plain NHWC,
-    256 B per pixel).  grid (B, C, Hf, Wf) f32, NCHW or channels-last."""
+    """P = W_in[:, :C] . grid + b_in per pixel: (B, Hf, Wf, 128) in FIELD_DTYPE[dtype] (f16
+    for both 16-bit modes; plain NHWC, 256 B per pixel).  grid (B, C, Hf, Wf) f32, NCHW or
+    channels-last."""
     lib = load()
     B, C, H, W = grid.shape
-    out = torch.empty(B, H, W, 128, device=grid.device, dtype=TORCH_DTYPE[dtype])
+    out = torch.empty(B, H, W, 128, device=grid.device, dtype=TORCH_DTYPE[FIELD_DTYPE[dtype]])
     if channels_last(grid):
         _check(lib.sd_project_grid_nhwc(ptr(_req(grid.permute(0, 2, 3, 1), "grid")), B, H, W,
                                         ctypes.byref(mlp), ptr(out), stream_of(out)),

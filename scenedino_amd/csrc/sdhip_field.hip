@@ -22,8 +22,8 @@
 // dims on lanes).  Colours: bilinear NHWC4 fp32 in each render view.
 //
 // Precision modes (template P): SD_F32 (f32 grid, exact-f32 MFMA 32x32x2, accurate
-// sinf), SD_BF16 (bf16 grid, fp32 blend, bf16 MFMA), SD_F16 (f16 grid, packed-f16
-// blend, f16 MFMA).  All modes accumulate in fp32 and keep geometry, alpha and
+// sinf), SD_F16 (f16 grid, packed-f16 blend, f16 MFMA), SD_BF16 (as SD_F16 up to sigma,
+// the DINO output layer on bf16 MFMA: RMode in sdhip_render.h).  All modes accumulate in fp32 and keep geometry, alpha and
 // transmittance in fp32.
 //
 // Reference: NeRFRenderer.composite (scenedino/renderer/nerf.py:230-449),
@@ -101,72 +101,7 @@ __device__ __forceinline__ Raw16 sd_load16(__amdgpu_buffer_rsrc_t rs, const TapO
     return r;
 }
 
-// 16-bit field blends: 1 = v_perm + v_dot2 with (w00, w01), (w10, w11) packed in the grid's
-// 16-bit type (the projected render kernels' form: ~half the VALU of the unpack + FMA chain,
-// the weights rounded to the operand type like the MFMA blend of k_render_tile)
-#ifndef SD_FQ_DOT2
-#define SD_FQ_DOT2 1
-#endif
-
-template <> struct Prec<SD_BF16> {
-    typedef uint16_t G;
-    typedef Raw16 Raw;
-    typedef bf16x8 Frag;
-    static constexpr bool FAST_PE = true;
-    static constexpr int ESZ = 2, DEPTH = 4;
-    static __device__ __forceinline__ Raw load(__amdgpu_buffer_rsrc_t rs, const TapOff &o, int q) {
-        return sd_load16(rs, o, q);
-    }
-    static __device__ __forceinline__ float b1(uint32_t a, uint32_t b, uint32_t c, uint32_t d,
-                                               bool hi, const Taps &t) {
-        float va = hi ? bf16hi(a) : bf16lo(a), vb = hi ? bf16hi(b) : bf16lo(b);
-        float vc = hi ? bf16hi(c) : bf16lo(c), vd = hi ? bf16hi(d) : bf16lo(d);
-        return fmaf(vd, t.w11, fmaf(vc, t.w10, fmaf(vb, t.w01, va * t.w00)));
-    }
-    static __device__ __forceinline__ Frag blend(const Raw &r, const Taps &t) {
-        if (SD_FQ_DOT2)  // horizontal tap pairs by v_perm, two v_dot2 per channel
-            return sd_blend_plain<SD_BF16>(r.a, r.b, r.c, r.d, sd_pack_w<SD_BF16>(t.w00, t.w01, t.w10, t.w11));
-        uint32_t A[4] = {r.a.x, r.a.y, r.a.z, r.a.w}, B[4] = {r.b.x, r.b.y, r.b.z, r.b.w};
-        uint32_t Cc[4] = {r.c.x, r.c.y, r.c.z, r.c.w}, D[4] = {r.d.x, r.d.y, r.d.z, r.d.w};
-        Frag o;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            o[2 * i] = (__bf16)b1(A[i], B[i], Cc[i], D[i], false, t);
-            o[2 * i + 1] = (__bf16)b1(A[i], B[i], Cc[i], D[i], true, t);
-        }
-        return o;
-    }
-    static __device__ __forceinline__ Frag from_f(const float f[8]) {
-        Frag o;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) o[i] = (__bf16)f[i];
-        return o;
-    }
-    // acc[ht] += W_in(q, ht) . X^T  (A fragments from LDS: [q][ht][lane] x 16 B)
-    static __device__ __forceinline__ void mma1(const uint8_t *lw, int q, int lane, const Frag &b,
-                                                f32x16 acc[4]) {
-        const Frag *w = (const Frag *)lw + (q * 4) * SD_WAVE + lane;
-#pragma unroll
-        for (int ht = 0; ht < 4; ++ht)
-            acc[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[ht * SD_WAVE], b, acc[ht], 0, 0, 0);
-    }
-    // out (32 points x 32 dims, O layout) += X^T . W_out^T[dt]; X in accumulator layout.
-    // w_out: [dt][t][s][lane] x 16 B
-    static __device__ __forceinline__ void mma2(const uint8_t *w_out, int dt, const f32x16 X[4],
-                                                int lane, f32x16 &out) {
-        const Frag *w = (const Frag *)w_out + (dt * 8) * SD_WAVE + lane;
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                Frag a;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) a[j] = (__bf16)X[t][8 * s + j];
-                out = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, w[(t * 2 + s) * SD_WAVE], out, 0, 0, 0);
-            }
-    }
-};
-
+// 16-bit field blend: packed-f16 FMAs over the four taps (4 v_pk_fma per channel pair)
 template <> struct Prec<SD_F16> {
     typedef uint16_t G;
     typedef Raw16 Raw;
@@ -217,6 +152,26 @@ template <> struct Prec<SD_F16> {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) a[j] = (_Float16)X[t][8 * s + j];
                 out = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, w[(t * 2 + s) * SD_WAVE], out, 0, 0, 0);
+            }
+    }
+};
+
+// bf16 mode (RMode, sdhip_render.h): the grid, its blend, layer 1 and sigma as the fp16
+// mode (an f16 grid); only the DINO output layer on bf16 operands
+template <> struct Prec<SD_BF16> : Prec<SD_F16> {
+    // out (32 points x 32 dims, O layout) += X^T . W_out^T[dt]; X in accumulator layout.
+    // w_out: [dt][t][s][lane] x 16 B
+    static __device__ __forceinline__ void mma2(const uint8_t *w_out, int dt, const f32x16 X[4],
+                                                int lane, f32x16 &out) {
+        const bf16x8 *w = (const bf16x8 *)w_out + (dt * 8) * SD_WAVE + lane;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                bf16x8 a;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) a[j] = (__bf16)X[t][8 * s + j];
+                out = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, w[(t * 2 + s) * SD_WAVE], out, 0, 0, 0);
             }
     }
 };

@@ -402,7 +402,9 @@ struct RCursor {
 template <int P, int NV, int NDT>
 __global__ void __launch_bounds__(SD_RWG) __attribute__((amdgpu_waves_per_eu(SD_RWAVES)))
 k_render_proj(const sd_render_args a, const sd_head m, const int32_t *__restrict__ list) {
-    typedef T16<P> Tr;
+    typedef typename RMode<P>::F Tr;  // operands upstream of sigma (f16 in both modes)
+    typedef typename RMode<P>::H Th;  // DINO head (bf16 in the bf16 mode)
+    constexpr bool HEAD_CVT = !std::is_same<Tr, Th>::value;  // X re-rounded for the head
     typedef typename Tr::Frag Frag;
     typedef typename Tr::Frag4 Frag4;
     typedef typename Tr::E E;
@@ -550,7 +552,7 @@ k_render_proj(const sd_render_args a, const sd_head m, const int32_t *__restrict
                 }
                 rb[0 * K + k] = uint4{(uint32_t)geo.t.i00 * 256u | (geo.inv_f ? 1u : 0u),
                                       (uint32_t)geo.t.i10 * 256u | invc, 0u, 0u};
-                rb[1 * K + k] = sd_pack_w<P>(geo.t.w00, geo.t.w01, geo.t.w10, geo.t.w11);
+                rb[1 * K + k] = sd_pack_w<SD_F16>(geo.t.w00, geo.t.w01, geo.t.w10, geo.t.w11);
                 rb[2 * K + k] = __builtin_bit_cast(uint4, f32x4{geo.v[0], geo.v[1], geo.v[2], z0});
                 if (!(DEFER && p == 0))
                     rb[3 * K + k] = __builtin_bit_cast(uint4, f32x4{delta, col[0], col[1], col[2]});
@@ -673,7 +675,7 @@ k_render_proj(const sd_render_args a, const sd_head m, const int32_t *__restrict
 #define SD_PCHUNK(r, q)                                                        \
         {                                                                      \
             Frag f_ = SD_ABL_NOBLEND ? __builtin_bit_cast(Frag, r.a ^ r.b ^ r.c ^ r.d) \
-                                     : sd_blend_plain<P>(r.a, r.b, r.c, r.d, cur.wp); \
+                                     : sd_blend_plain<SD_F16>(r.a, r.b, r.c, r.d, cur.wp); \
             r = sd_pload(nxt, q);                                              \
             acc[2 * q] = Tr::mma(id0, f_, zero4);                              \
             acc[2 * q + 1] = Tr::mma(id1, f_, zero4);                          \
@@ -739,18 +741,37 @@ k_render_proj(const sd_render_args a, const sd_head m, const int32_t *__restrict
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const int t = 2 * s2 + (q >> 1), r = 2 * (q & 1);
-                    hacc[t][r] = fmaf(w, sd_unpack_lo<P>(d4[q]), hacc[t][r]);
-                    hacc[t][r + 1] = fmaf(w, sd_unpack_hi<P>(d4[q]), hacc[t][r + 1]);
+                    hacc[t][r] = fmaf(w, sd_unpack_lo<SD_F16>(d4[q]), hacc[t][r]);
+                    hacc[t][r + 1] = fmaf(w, sd_unpack_hi<SD_F16>(d4[q]), hacc[t][r + 1]);
                 }
             }
         }
-        // DINO head folded into the compositing sum: dacc += w_j (W_dino h_j)
+        // DINO head folded into the compositing sum: dacc += w_j (W_dino h_j); in the bf16
+        // mode relu(h) re-rounded to the head's bf16 operands
+        typename Th::Frag XH[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            if constexpr (HEAD_CVT) {
+                if (NDT > 0) {
+                    const uint4 u = __builtin_bit_cast(uint4, X[s]);
+                    const uint32_t d4[4] = {u.x, u.y, u.z, u.w};
+                    uint32_t o4[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        o4[q] = sd_pack2<typename Th::E>(sd_unpack_lo<SD_F16>(d4[q]), sd_unpack_hi<SD_F16>(d4[q]));
+                    XH[s] = __builtin_bit_cast(typename Th::Frag, uint4{o4[0], o4[1], o4[2], o4[3]});
+                }
+            } else {
+                XH[s] = __builtin_bit_cast(typename Th::Frag, X[s]);
+            }
+        }
+        const typename Th::Frag *lwh = (const typename Th::Frag *)lds + lo;
 #pragma unroll
         for (int dt = 0; dt < NDT; ++dt) {
             f32x4 o = zero4;
 #pragma unroll
             for (int s = 0; s < 4; ++s)
-                if (!SD_ABL_NODINO || s == 0) o = Tr::mma(lw[SD_LDS_OUT + (dt * 4 + s) * SD_WAVE + lane], X[s], o);
+                if (!SD_ABL_NODINO || s == 0) o = Th::mma(lwh[SD_LDS_OUT + (dt * 4 + s) * SD_WAVE + lane], XH[s], o);
 #pragma unroll
             for (int r = 0; r < 4; ++r) dacc[dt][r] = fmaf(w, o[r], dacc[dt][r]);
         }
@@ -830,7 +851,7 @@ template <int P>
 __global__ void __launch_bounds__(SD_PWG)
 k_head_hc(const float *__restrict__ work, int64_t R, const sd_head m, float *__restrict__ dino,
           int64_t ld_dino, const int32_t *__restrict__ list) {
-    typedef T16<P> Tr;
+    typedef typename RMode<P>::H Tr;  // the DINO head's operand type
     typedef typename Tr::Frag Frag;
     typedef typename Tr::E E;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -932,7 +953,7 @@ static int sd_project_any(const float *grid, int64_t B, int64_t Hf, int64_t Wf, 
             hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(256), PJ_LDS, s, grid, B * HW, *m,
                                (uint32_t *)out);
         };
-        if (m->dtype == SD_F16) go(k_project_lds<SD_F16>); else go(k_project_lds<SD_BF16>);
+        go(k_project_lds<SD_F16>);  // both 16-bit modes: P in f16 (RMode, sdhip_render.h)
         return sd_check_err();
     }
 #define SD_PROJ_LAUNCH(PP, NH)                                                                  \
@@ -941,11 +962,7 @@ static int sd_project_any(const float *grid, int64_t B, int64_t Hf, int64_t Wf, 
         hipLaunchKernelGGL((k_project<PP, NH>), dim3((unsigned)nblk), dim3(SD_PWG), lds_bytes, s, \
                            grid, B, m->C, HW, (int)Wf, *m, (uint32_t *)out);                    \
     } while (0)
-    if (m->dtype == SD_F16) {
-        if (nhwc) SD_PROJ_LAUNCH(SD_F16, true); else SD_PROJ_LAUNCH(SD_F16, false);
-    } else {
-        if (nhwc) SD_PROJ_LAUNCH(SD_BF16, true); else SD_PROJ_LAUNCH(SD_BF16, false);
-    }
+    if (nhwc) SD_PROJ_LAUNCH(SD_F16, true); else SD_PROJ_LAUNCH(SD_F16, false);
 #undef SD_PROJ_LAUNCH
     return sd_check_err();
 }

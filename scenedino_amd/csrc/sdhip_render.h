@@ -81,6 +81,21 @@ template <> struct T16<SD_BF16> {
     }
 };
 
+// Operand types of the two 16-bit render modes.  F: every operand upstream
+// of sigma -- the projected grid P (or the NHWC grid G), the bilinear tap weights, the
+// positional-code fragments and their W_in columns, relu(h) and W_sigma.  H: the DINO output
+// layer (W_dino x hidden vectors / hidden sums).
+//   fp16 mode: F = H = f16.
+//   bf16 mode (BASELINE configs[1]): F = f16, H = bf16.  An 8-bit mantissa on any operand
+//   upstream of sigma moves the composited depth past the 1e-2 m contract (1.3-3.4 cm with
+//   every operand bf16; 0.98 cm with only the code columns bf16 -- the replay of the kernels'
+//   arithmetic in tools/lowp_depth_emul.py, profiles/r5_lowp_depth_emul.txt), so bf16 is
+//   kept where it costs no depth: the DINO head.  Same MFMA rate either way.
+template <int P> struct RMode {
+    typedef T16<SD_F16> F;
+    typedef T16<P> H;
+};
+
 // two floats -> one packed 16-bit pair (v_cvt_pk_f16_f32 / v_cvt_pk_bf16_f32, RNE)
 template <typename E>
 __device__ __forceinline__ uint32_t sd_pack2(float a, float b) {
@@ -100,6 +115,7 @@ template <int P> __device__ __forceinline__ float sd_unpack_hi(uint32_t d) {
 }
 
 // blend weights as the ray pass stores them: (w00, w01), (w10, w11) packed in E
+// (P = SD_F16 for both render modes, RMode)
 template <int P>
 __device__ __forceinline__ uint4 sd_pack_w(float w00, float w01, float w10, float w11) {
     typedef typename T16<P>::E E;

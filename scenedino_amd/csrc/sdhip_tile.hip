@@ -202,7 +202,8 @@ k_render_tile(const st_args sa) {
     constexpr int ST_WAVES = NW;
     constexpr int ST_L_HS = st_l_hs(NW), ST_L_WS = st_l_ws(NW), ST_L_RAY = st_l_ray(NW),
                   ST_L_REC = st_l_rec(NW);
-    typedef T16<P> Tr;
+    typedef typename RMode<P>::F Tr;  // operands upstream of sigma (f16 in both modes)
+    typedef typename RMode<P>::H Th;  // DINO head (bf16 in the bf16 mode)
     typedef typename Tr::Frag Frag;
     typedef typename Tr::Frag4 Frag4;
     typedef typename Tr::E E;
@@ -327,7 +328,7 @@ k_render_tile(const st_args sa) {
                     }
                     const uint32_t xy = x0 | (y0 << 15) | (geo.inv_f ? 1u << 30 : 0u) |
                                         (ic ? 1u << 31 : 0u);
-                    const uint4 wp = sd_pack_w<P>(geo.t.w00, geo.t.w01, geo.t.w10, geo.t.w11);
+                    const uint4 wp = sd_pack_w<SD_F16>(geo.t.w00, geo.t.w01, geo.t.w10, geo.t.w11);
                     r1[k] = f32x4{geo.v[0], geo.v[1], geo.v[2], z0};
                     if (p == 0) {
                         sd_color_issue(a.img + (int64_t)sbi * cplane, tc, cpend);
@@ -502,22 +503,22 @@ k_render_tile(const st_args sa) {
     auto head = [&](int grp) {
         if (wave >= ndt) return;
         const int slot = j < NW ? j : 0;  // B columns j >= NW: not stored
-        Frag Bh[4];
+        typename Th::Frag Bh[4];
         const uint8_t *hs = lds + ST_L_HS + slot * ST_HS_ROW;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             const uint2 lo = *(const uint2 *)(hs + (32 * s + 4 * g) * 2);
             const uint2 hi = *(const uint2 *)(hs + (32 * s + 16 + 4 * g) * 2);
-            Bh[s] = __builtin_bit_cast(Frag, uint4{lo.x, lo.y, hi.x, hi.y});
+            Bh[s] = __builtin_bit_cast(typename Th::Frag, uint4{lo.x, lo.y, hi.x, hi.y});
         }
         const float ws = *(const float *)(lds + ST_L_WS + slot * 4);
         const int ray = NW * grp + j;
         const bool store = j < NW && ray < R;
         for (int dt = wave; dt < ndt; dt += ST_WAVES) {
-            const Frag *wo = (const Frag *)m.w_out + (int64_t)dt * 4 * SD_WAVE + lane;
+            const typename Th::Frag *wo = (const typename Th::Frag *)m.w_out + (int64_t)dt * 4 * SD_WAVE + lane;
             f32x4 o = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int s = 0; s < 4; ++s) o = Tr::mma(wo[s * SD_WAVE], Bh[s], o);
+            for (int s = 0; s < 4; ++s) o = Th::mma(wo[s * SD_WAVE], Bh[s], o);
             // rows 4 g + r of tile dt = dims 16 dt + 4 g + r, column j = ray slot
             const int dim = 16 * dt + 4 * g;
             const f32x4 bd = *(const f32x4 *)(m.b_dino + dim);
@@ -757,10 +758,11 @@ k_render_tile(const st_args sa) {
                 }
                 if ((j & 3) == 0) {
                     const int b = j >> 2;
+                    typedef typename Th::E EH;  // the head's operand type
                     *(uint2 *)(hs + (32 * b + 4 * g) * 2) =
-                        uint2{sd_pack2<E>(v[0], v[1]), sd_pack2<E>(v[2], v[3])};
+                        uint2{sd_pack2<EH>(v[0], v[1]), sd_pack2<EH>(v[2], v[3])};
                     *(uint2 *)(hs + (32 * b + 16 + 4 * g) * 2) =
-                        uint2{sd_pack2<E>(v[4], v[5]), sd_pack2<E>(v[6], v[7])};
+                        uint2{sd_pack2<EH>(v[4], v[5]), sd_pack2<EH>(v[6], v[7])};
                 }
             }
             {

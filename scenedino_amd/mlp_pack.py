@@ -162,8 +162,11 @@ class PackedMLP:
         Wz = torch.cat((W_in, torch.zeros(dh, 1, device=dev)), 1)  # column din = zero pad
         cols1 = torch.where(ix["cols1"] < 0, torch.full_like(ix["cols1"], din), ix["cols1"])
         w1 = Wz[ix["rows1"], cols1]
+        # operands upstream of sigma in the field dtype (f16 for both 16-bit modes), the DINO
+        # output layer in the mode's dtype (RMode, csrc/sdhip_render.h)
         tdt = _lib.TORCH_DTYPE[dtype]
-        self.w_in = w1.to(tdt).contiguous()
+        fdt = _lib.TORCH_DTYPE[_lib.FIELD_DTYPE[dtype]]
+        self.w_in = w1.to(fdt).contiguous()
         self.b_in_h = b_in[ix["accrow"]].contiguous()
         self.w_sig_h = W_out[0][ix["accrow"]].contiguous()
         self.b_empty_h = None
@@ -184,8 +187,8 @@ class PackedMLP:
         if dtype != _lib.SD_F32 and D % 16 == 0 and D <= 512:
             px = {k: v.to(dev) for k, v in _proj_tables(C, D).items()}
             pe_cols = torch.where(px["pe_cols"] < 0, torch.full_like(px["pe_cols"], din), px["pe_cols"])
-            self.w_pe16 = Wz[px["pe_rows"], pe_cols].to(tdt).contiguous()
-            self.w_sig16 = W_out[0][px["sig_cols"]].to(tdt).contiguous()
+            self.w_pe16 = Wz[px["pe_rows"], pe_cols].to(fdt).contiguous()
+            self.w_sig16 = W_out[0][px["sig_cols"]].to(fdt).contiguous()
             self.w_out16 = W_out[px["out_rows"], px["out_cols"]].to(tdt).contiguous()
             self.head_rec = _lib.SdHead(
                 w_pe=self.w_pe16.data_ptr(), w_sig=self.w_sig16.data_ptr(),

@@ -10,12 +10,11 @@ hand-written gfx950 kernels of libsdhip.so (``sd_field_query``; and, through
 
 Precision: ``precision="fp16"`` (default; f16 projected grid, f16 bilinear blend and
 f16 MFMA, fp32 accumulate and fp32 geometry / compositing -- the reference's own AMP
-dtype, and the 16-bit mode that meets SURVEY §8(c)'s 1e-2 m depth contract), ``"bf16"``
-(the same kernels on bf16 operands, BASELINE configs[1]'s dtype: an 8-bit mantissa on the
-projected grid and the bilinear weights alone moves the composited depth by 1-3 cm,
-tools/lowp_depth_emul.py) or ``"fp32"`` (f32 grid + exact-f32 MFMA) for
-fp32-tolerance parity with the reference.  Set via ``conf["precision"]`` or
-``net.set_precision``.
+dtype), ``"bf16"`` (BASELINE configs[1]'s dtype: the DINO output layer on bf16 MFMA, every
+operand upstream of sigma in f16 -- an 8-bit mantissa there moves the composited depth past
+SURVEY §8(c)'s 1e-2 m contract, tools/lowp_depth_emul.py) or ``"fp32"`` (f32 grid +
+exact-f32 MFMA) for fp32-tolerance parity with the reference.  Both 16-bit modes meet the
+1e-2 m depth contract.  Set via ``conf["precision"]`` or ``net.set_precision``.
 """
 from __future__ import annotations
 
@@ -343,9 +342,10 @@ class BTSNet(nn.Module):
         return cache
 
     def _grid_nhwc(self, gc):
-        """Encoder grid packed NHWC in the MLP dtype (sd_render_fused / sd_field_query)."""
+        """Encoder grid packed NHWC in the field dtype (sd_render_fused / sd_field_query;
+        f16 for both 16-bit modes, _lib.FIELD_DTYPE)."""
         if gc["grid"] is None:
-            gc["grid"] = _lib.pack_grid(gc["grid_nchw"].float(), self._dtype())
+            gc["grid"] = _lib.pack_grid(gc["grid_nchw"].float(), _lib.FIELD_DTYPE[self._dtype()])
         return gc["grid"]
 
     def _grid_proj(self, gc, m):

@@ -120,8 +120,10 @@ def test_layer1_and_layer2_fragments(mlp_params, dtype):
             feats[q, l] = X[p, 16 * q + 8 * h: 16 * q + 8 * h + 8].numpy()
         for pc in range(3):
             feats[C // 16 + pc, l] = pe_chunk(V[p].numpy(), pc, h)
+    # bf16 mode: layer 1 on f16 operands, the DINO output layer on bf16 (FIELD_DTYPE)
     if dtype == _lib.SD_BF16:
-        feats = torch.tensor(feats).to(torch.bfloat16).double().numpy()
+        assert pk.w_in.dtype == torch.float16 and pk.w_out.dtype == torch.bfloat16
+        feats = torch.tensor(feats).to(torch.float16).double().numpy()
     acc = [np.zeros((64, 16)) for _ in range(4)]
     for q in range(nq):
         for ht in range(4):
@@ -144,10 +146,10 @@ def test_layer1_and_layer2_fragments(mlp_params, dtype):
     xin = np.concatenate([X.numpy(), np.array(code)], 1)
     Wd = W_in.double().numpy()
     if dtype == _lib.SD_BF16:
-        Wd = W_in.to(torch.bfloat16).double().numpy()
-        xin = torch.tensor(xin).to(torch.bfloat16).double().numpy()
+        Wd = W_in.to(torch.float16).double().numpy()
+        xin = torch.tensor(xin).to(torch.float16).double().numpy()
     hdense = Wd @ xin.T  # (128, 32)
-    tol = 2e-2 if dtype == _lib.SD_BF16 else 1e-5
+    tol = 2e-3 if dtype == _lib.SD_BF16 else 1e-5
     for ht in range(4):
         for l in range(64):
             for r in range(16):

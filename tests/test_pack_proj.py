@@ -124,8 +124,11 @@ def test_projected_head_reproduces_dense_mlp(D):
     for t in range(8):
         acc[t] = mfma_16x16x32(wpe0[t], b0, acc[t])
         acc[t] = mfma_16x16x16(wpe1[t], b1, acc[t])
-    # dense reference with the same (bf16-rounded) code weights
-    Wpe_bf = W_in[:, C:].to(torch.bfloat16).double().numpy()
+    # dense reference with the same rounded code weights (bf16 mode: f16 up to sigma, the
+    # DINO head bf16 -- _lib.FIELD_DTYPE)
+    assert pk.w_pe16.dtype == torch.float16 and pk.w_sig16.dtype == torch.float16
+    assert pk.w_out16.dtype == torch.bfloat16
+    Wpe_bf = W_in[:, C:].to(torch.float16).double().numpy()
     codes = np.array([ref_code(V[i]) for i in range(16)])
     hdense = Pm + codes @ Wpe_bf.T                         # (16, 128)
     for t in range(8):
@@ -144,7 +147,7 @@ def test_projected_head_reproduces_dense_mlp(D):
     wsig = f(pk.w_sig16)
     for s in range(4):
         sg = mfma_16x16x32(wsig[s], Xf[s], sg)
-    sig_ref = Hh @ W_out[0].to(torch.bfloat16).double().numpy()
+    sig_ref = Hh @ W_out[0].to(torch.float16).double().numpy()
     for l in range(64):
         for r in range(4):
             assert abs(sg[l, r] - sig_ref[LI[l]]) < 1e-6

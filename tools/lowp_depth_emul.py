@@ -88,14 +88,24 @@ class Emu:
         # only the texels the samples touch are projected
         flat = torch.stack([y0 * Wf + x0, y0 * Wf + x1, y1 * Wf + x0, y1 * Wf + x1])
         uniq, inv = torch.unique(flat, return_inverse=True)
-        G = grid[0].reshape(C, -1)[:, uniq]
-        self.P = (s["W_in"][:, :C] @ G + s["b_in"].view(-1, 1)).t()  # (texels, 128)
+        self.G = grid[0].reshape(C, -1)[:, uniq]
+        self.P = (s["W_in"][:, :C] @ self.G + s["b_in"].view(-1, 1)).t()  # (texels, 128)
+        self._Pq = {}
         self.inv = inv
         self.K, self.C = K, C
 
-    def depth(self, rP=I, rw=I, rcode=I, rWc=I, rX=I, rWs=I):
+    def depth(self, rP=I, rw=I, rcode=I, rWc=I, rX=I, rWs=I, rG=I):
+        """rG: rounding of the projection's operands (grid G and W_in[:, :C], k_project's
+        MFMA inputs) before P itself is rounded by rP."""
         s = self.s
-        Pq = rP(self.P)
+        if rG is I:
+            Pq = rP(self.P)
+        else:
+            if rG not in self._Pq:
+                C = self.C
+                self._Pq[rG] = (rG(s["W_in"][:, :C]).double() @ rG(self.G).double()
+                                + s["b_in"].double().view(-1, 1)).float().t()
+            Pq = rP(self._Pq[rG])
         h = sum(rw(w).unsqueeze(-1) * Pq[self.inv[q]] for q, w in enumerate(self.ws))
         h = h + rcode(self.code) @ rWc(s["W_in"][:, self.C:]).t()
         X = rX(torch.relu(h))
@@ -114,6 +124,10 @@ SCHEMES = [
     ("bf16 but P, w fp16", dict(rP=HF, rw=HF, rcode=BF, rWc=BF, rX=BF, rWs=BF)),
     ("P, w, X, Ws fp16; code, Wc bf16", dict(rP=HF, rw=HF, rcode=BF, rWc=BF, rX=HF, rWs=HF)),
     ("all fp16 (the fp16 kernels)", dict(rP=HF, rw=HF, rcode=HF, rWc=HF, rX=HF, rWs=HF)),
+    ("r5 bf16 mode A: G,Wg,P,w,X,Ws f16; code,Wc bf16",
+     dict(rG=HF, rP=HF, rw=HF, rcode=BF, rWc=BF, rX=HF, rWs=HF)),
+    ("r5 bf16 mode B: all f16 but the DINO head",
+     dict(rG=HF, rP=HF, rw=HF, rcode=HF, rWc=HF, rX=HF, rWs=HF)),
     ("only P bf16", dict(rP=BF)),
     ("only w bf16", dict(rw=BF)),
     ("only code + Wc bf16", dict(rcode=BF, rWc=BF)),
