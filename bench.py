@@ -616,22 +616,21 @@ def main_encode(args, world, rank, device):
         }), flush=True)
 
 
-def main_train(args, world, rank, device):
-    """Training step through the render path (SURVEY §8(f) rank 1; train_scenedino_kitti_360
-    .yaml: batch_size 4, n_coarse 32, hard_alpha_cap, training/scenedino.yaml ray_batch_size
-    2048 in 8x8 patches): per step 4 frames x 2048 rays x 32 samples through BTSNet.forward
-    (sd_field_gather -> ResnetFC -> softplus) + sd_composite, an L2 loss on the rendered
-    DINO / colour maps, and loss.backward() (sd_composite_bwd, ResnetFC GEMM backward,
-    sd_field_gather_bwd into the 4 x 256 x 192 x 640 grid gradient).  The encoder backward is
-    not part of the step (the grid is the leaf)."""
-    from scenedino_amd import autograd as sda
+def train_setup(device, rank=0, NB=4, RB=2048, KT=32, PS=8, amp=True, offset_pose=False,
+                capturable=False, world=1):
+    """The training scene of ``main_train`` (also built by tests/test_train_graph.py): a
+    BTSNet over a fixed N(0, 1) grid leaf, NeRFRenderer(n_coarse KT, hard_alpha_cap),
+    PatchRaySampler (RB rays per frame in PS x PS snapped patches), random targets and a fused
+    Adam on the head.  ``body(patches)`` is one step from the device sampler on: rays and
+    targets from the drawn patches (sd_patch_rays), depth jitter into ``zj`` (drawn when
+    draw_jitter, else the values already in zj), forward, loss, backward, Adam."""
+    from types import SimpleNamespace
     from scenedino_amd import distributed as sdd
     from scenedino_amd.models import BTSNet
     from scenedino_amd.models.prediction_heads import ResnetFC
     from scenedino_amd.common.positional_encoding import PositionalEncoding
     from scenedino_amd.renderer import NeRFRenderer
     from scenedino_amd.common.ray_sampler import PatchRaySampler
-    NB, RB, KT, PS = 4, 2048, 32, 8
     g = torch.Generator(device=device).manual_seed(rank)
     grid = _layout(torch.randn(NB, C_GRID, HF, WF, device=device, generator=g))
     torch.manual_seed(2)
@@ -651,8 +650,8 @@ def main_train(args, world, rank, device):
     renderer = NeRFRenderer(n_coarse=KT, lindisp=True, hard_alpha_cap=True, eval_batch_size=65536)
     wrapper = renderer.bind_parallel(net, gpus=None).train()
     ray_poses = poses
-    if args.offset_pose:  # rays from a 0.5 m lateral / 2 deg yaw view: samples of a ray
-        import math        # project onto different texels of the encoder grid
+    if offset_pose:  # rays from a 0.5 m lateral / 2 deg yaw view: samples of a ray
+        import math   # project onto different texels of the encoder grid
         a = math.radians(2.0)
         ray_poses = poses.clone()
         ray_poses[:, 0, 0, 0] = math.cos(a); ray_poses[:, 0, 0, 2] = math.sin(a)
@@ -662,17 +661,62 @@ def main_train(args, world, rank, device):
     sampler = PatchRaySampler(3, 80, RB, PS, snap_to_grid=True, dino_upscaled=False)
     dino_gt_map = torch.randn(NB, 1, D_DINO, H // PS, W // PS, device=device, generator=g)
     # the grid is an activation (the encoder's output): its gradient is computed, the
-    # optimizer steps the head (a frozen-encoder config; encoder backward is not ours)
+    # optimizer steps the head (a frozen-encoder config; encoder backward is not ours).
     # Adam as one fused kernel over the head's parameters (torch's fused implementation, the
     # same update as the reference's Adam: base_trainer.py optimizer)
+    opt = torch.optim.Adam(head.parameters(), lr=1e-4, fused=True, capturable=capturable)
+    npatch = RB // (PS * PS)
+    zj = torch.empty(NB * RB, KT, device=device)
+
+    def loss_of(out, rgb_gt, dino_gt):
+        pd = out["dino_features"].float().view(NB, npatch, PS * PS, D_DINO).mean(2)
+        return ((pd - dino_gt) ** 2).mean() + (out["rgb"].float() - (rgb_gt * 0.5 + 0.5)).abs().mean()
+
+    def body(patches, draw_jitter=True):
+        rays, rgb_gt, dino_gt = sampler.sample_patches(patches, images, ray_poses, Ks,
+                                                       dino_features=dino_gt_map)
+        if draw_jitter:
+            zj.uniform_()
+        renderer.z_jitter = zj
+        with torch.autocast("cuda", dtype=torch.float16, enabled=amp, cache_enabled=False):
+            out = wrapper(rays, want_weights=True)["coarse"]
+            loss = loss_of(out, rgb_gt, dino_gt)
+        opt.zero_grad(set_to_none=True)
+        leaf.grad = None
+        loss.backward()
+        if world > 1:  # data-parallel head: one RCCL all-reduce of the gradient bucket
+            sdd.allreduce_grads(head.parameters())
+        opt.step()
+        renderer.z_jitter = None
+        return loss
+
+    return SimpleNamespace(net=net, head=head, leaf=leaf, renderer=renderer, wrapper=wrapper,
+                           sampler=sampler, images=images, ray_poses=ray_poses, Ks=Ks,
+                           dino_gt_map=dino_gt_map, opt=opt, zj=zj, body=body, loss_of=loss_of,
+                           NB=NB, RB=RB, KT=KT, PS=PS, npatch=npatch)
+
+
+def main_train(args, world, rank, device):
+    """Training step through the render path (SURVEY §8(f) rank 1; train_scenedino_kitti_360
+    .yaml: batch_size 4, n_coarse 32, hard_alpha_cap, training/scenedino.yaml ray_batch_size
+    2048 in 8x8 patches): per step 4 frames x 2048 rays x 32 samples through BTSNet.forward
+    (sd_field_gather -> ResnetFC -> softplus) + sd_composite, an L2 loss on the rendered
+    DINO / colour maps, and loss.backward() (sd_composite_bwd, ResnetFC GEMM backward,
+    sd_field_gather_bwd into the 4 x 256 x 192 x 640 grid gradient).  The encoder backward is
+    not part of the step (the grid is the leaf)."""
+    from scenedino_amd import autograd as sda
+    from scenedino_amd import distributed as sdd
+    NB, RB, KT, PS = 4, 2048, 32, 8
     # graph mode (the default on one GPU; --no-graph: eager): everything after the host's patch draws -- the device
     # sampler, forward, loss, backward, Adam -- replayed as one captured HIP graph per step,
     # so the host only draws patches and launches the graph (round 3 measured the eager step
     # host-paced: ~1.3 ms of issue against ~1.0 ms of GPU work)
     graph_mode = world == 1 and args.graph
-    opt = torch.optim.Adam(head.parameters(), lr=1e-4, fused=True, capturable=graph_mode)
     amp = not args.no_amp  # train_scenedino_kitti_360.yaml: with_amp: true (fp16 autocast)
-    npatch = RB // (PS * PS)
+    ts = train_setup(device, rank, NB, RB, KT, PS, amp=amp, offset_pose=args.offset_pose,
+                     capturable=graph_mode, world=world)
+    head, leaf, renderer, wrapper, sampler = ts.head, ts.leaf, ts.renderer, ts.wrapper, ts.sampler
+    images, ray_poses, Ks, dino_gt_map, opt = ts.images, ts.ray_poses, ts.Ks, ts.dino_gt_map, ts.opt
 
     host = {} if os.environ.get("SCENEDINO_AMD_HOST_PROFILE") == "1" else None
 
@@ -691,9 +735,7 @@ def main_train(args, world, rank, device):
         with torch.autocast("cuda", dtype=torch.float16, enabled=amp):
             out = wrapper(rays, want_weights=True)["coarse"]
             t0 = mark("forward", t0)
-            pd = out["dino_features"].float().view(NB, npatch, PS * PS, D_DINO).mean(2)
-            loss = ((pd - dino_gt) ** 2).mean() + \
-                (out["rgb"].float() - (rgb_gt * 0.5 + 0.5)).abs().mean()
+            loss = ts.loss_of(out, rgb_gt, dino_gt)
         t0 = mark("loss", t0)
         opt.zero_grad(set_to_none=True)
         leaf.grad = None
@@ -720,27 +762,12 @@ def main_train(args, world, rank, device):
         # nerf.py:134 does), so every replay samples new depths; the kernel timer is off
         # during capture (its events would be frozen into the graph).
         sda.kernel_timer = None
-        dino_hw = tuple(dino_gt_map.shape[-2:])
         shape = sampler.draw(images, dino_gt_map).shape
         host_slots = [torch.empty(shape, dtype=torch.int32, pin_memory=True) for _ in range(2)]
         dev_slots = [torch.empty(shape, dtype=torch.int32, device=device) for _ in range(2)]
-        zj = torch.empty(NB * RB, KT, device=device)
-        renderer.z_jitter = zj
 
         def body(k):
-            rays, rgb_gt, dino_gt = sampler.sample_patches(dev_slots[k], images, ray_poses, Ks,
-                                                           dino_features=dino_gt_map)
-            zj.uniform_()
-            with torch.autocast("cuda", dtype=torch.float16, enabled=amp, cache_enabled=False):
-                out = wrapper(rays, want_weights=True)["coarse"]
-                pd = out["dino_features"].float().view(NB, npatch, PS * PS, D_DINO).mean(2)
-                loss = ((pd - dino_gt) ** 2).mean() + \
-                    (out["rgb"].float() - (rgb_gt * 0.5 + 0.5)).abs().mean()
-            opt.zero_grad(set_to_none=True)
-            leaf.grad = None
-            loss.backward()
-            opt.step()
-            return loss
+            return ts.body(dev_slots[k])
 
         side = torch.cuda.Stream(device=device)
         side.wait_stream(torch.cuda.current_stream(device))
@@ -798,16 +825,12 @@ def main_train(args, world, rank, device):
     elapsed = time.perf_counter() - t0
     timer.on = False
     if graph_mode:
-        # the kernels' own durations (roofline fields) from eager steps after the timed region,
-        # on the side stream the captured step's autograd state lives on
-        renderer.z_jitter = None
+        # the kernels' own durations (roofline fields) from eager steps after the timed region
         sda.kernel_timer = timer
         timer.on = True
-        side.wait_stream(torch.cuda.current_stream(device))
-        with torch.cuda.stream(side):
-            for _ in range(4):
-                eager_step()
-                timer.tick()
+        for _ in range(4):  # (on the default stream: no autograd state outlives a step)
+            eager_step()
+            timer.tick()
         torch.cuda.synchronize()
         timer.on = False
     sda.kernel_timer = None
@@ -840,7 +863,7 @@ def main_train(args, world, rank, device):
             "k_field_gather_bwd"
         bwd_bytes = chunk * 4 * C_GRID
     traffic, tsrc = None, None
-    for tf in ("r3_train_traffic.json", "r2_train_traffic.json"):
+    for tf in ("r5_train_traffic.json", "r4_train_traffic.json", "r3_train_traffic.json"):
         try:
             traffic = json.load(open(os.path.join(ROOT, "profiles", tf)))["kernels"][tkey]["hbm_bytes"]
             tsrc = f"profiles/{tf} (rocprofv3 PMC, per launch)"

@@ -174,17 +174,14 @@ class FieldMLP(torch.autograd.Function):
                 dWo[:, :dh_].contiguous(), dWo[:, dh_].contiguous())
 
 
-_train_pack = {}
-
-
 def _packed_train(w_in, b_in, w_out, b_out, dtype, C):
-    from .mlp_pack import PackedTrainMLP, param_key
-    key = param_key(w_in, b_in, w_out, b_out) + (dtype, C)
-    p = _train_pack.get("p")
-    if p is None or _train_pack.get("key") != key:
-        p = PackedTrainMLP(w_in, b_in, w_out, b_out, dtype, C)
-        _train_pack["p"], _train_pack["key"] = p, key
-    return p
+    """Fragments of the current weights, packed on every call (one gather through a cached
+    index, csrc/sdhip_mlp.hip's operand order).  Not cached by tensor version: torch's fused
+    Adam (the bench's optimizer, capturable inside a HIP graph) updates parameters in place
+    without bumping their version counter, so a version-keyed cache served the previous
+    step's weights (found by tests/test_train_graph.py)."""
+    from .mlp_pack import PackedTrainMLP
+    return PackedTrainMLP(w_in, b_in, w_out, b_out, dtype, C)
 
 
 class FieldMLPFused(torch.autograd.Function):

@@ -328,8 +328,14 @@ class BTSNet(nn.Module):
         imgs = self.grid_c_imgs
         n, nv, c3, H, W = imgs.shape
         img = _lib.pack_image(imgs.reshape(n * nv, c3, H, W).float().contiguous())
+        # grid_nchw feeds the inference kernels only (packing / projection): held DETACHED.
+        # A view with a grad_fn would keep the grid leaf's AccumulateGrad node alive across
+        # steps, bound to the stream of the step that created it -- the round-4 graph-mode
+        # training crash: the node was made on the legacy default stream by an eager
+        # warm-up step, and the captured backward then had the engine make that stream wait on
+        # the capture stream, which the default stream cannot join (host segfault in HIP).
         cache = {
-            "grid_nchw": g.reshape(B, C, Hf, Wf), "grid": None, "proj": None, "proj_key": None,
+            "grid_nchw": g.detach().reshape(B, C, Hf, Wf), "grid": None, "proj": None, "proj_key": None,
             "C": C, "Hf": Hf, "Wf": Wf, "B": B,
             "cam_f": _cam_records(self.grid_f_poses_w2c[:, 0], self.grid_f_Ks[:, 0]),
             "img": img, "nv": nv, "Hc": H, "Wc": W,
@@ -572,6 +578,11 @@ class BTSNet(nn.Module):
         parameters as in bts.py:476-595."""
         from ..autograd import FieldGather, FieldGatherMLP, FieldMLP, GatherAcc, GridNHWC
         self._check_supported()
+        # a training step follows: the inference kernels' packed weights are stale from here
+        # on (an optimizer may update the parameters in place without bumping their version
+        # counters -- torch's fused Adam does -- so the version key alone cannot tell)
+        self._packed = None
+        self._packed_q = None
         head = self.heads[self.final_pred_head]
         if len(self.heads) != 1:
             raise NotImplementedError("the field path supports a single prediction head")
