@@ -67,6 +67,18 @@ extern "C" int sd_tile_prof(unsigned long long *out, int reset) {
 #define ST_T(i)
 #endif
 
+#ifndef ST_WAIT_FIX
+#define ST_WAIT_FIX 1       // compiler-visible vmcnt(0) after the register-resident weight loads
+#endif
+#ifndef ST_HEAD_PRE
+#define ST_HEAD_PRE 2       // 2: the previous group's DINO head before the ray pass (its W_dino
+                            // loads' wait then does not cover the pass's colour loads); 1: its
+                            // first W_dino tile preloaded across the pass (spills); 0: after
+#endif
+#ifndef ST_HC16
+#define ST_HC16 1           // hidden-space compositing by v_pk_fma_f16 into packed f16 per-lane
+                            // partial sums (0: v_dot2 into f32, twice the instructions)
+#endif
 #ifndef ST_SAME_CAM
 #define ST_SAME_CAM 1       // colour taps re-use the encoder-view projection when cam_c == cam_f
 #endif
@@ -500,7 +512,16 @@ k_render_tile(const st_args sa) {
     };
 
     // ---- DINO head of one group (hsum of its NW rays in LDS) --------------------------
-    auto head = [&](int grp) {
+    // W_dino fragments of tile dt (4 x 16 B per lane).  ST_HEAD_PRE: the wave's first tile is
+    // loaded before the step's ray pass, so the head's wait for it does not also wait for the
+    // ray pass's colour loads (issued later, consumed after item 0)
+    typedef typename Th::Frag HFrag;
+    auto head_w = [&](int dt, HFrag w[4]) {
+        const HFrag *wo = (const HFrag *)m.w_out + (int64_t)dt * 4 * SD_WAVE + lane;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) w[s] = wo[s * SD_WAVE];
+    };
+    auto head = [&](int grp, const HFrag w0[4]) {
         if (wave >= ndt) return;
         const int slot = j < NW ? j : 0;  // B columns j >= NW: not stored
         typename Th::Frag Bh[4];
@@ -515,10 +536,16 @@ k_render_tile(const st_args sa) {
         const int ray = NW * grp + j;
         const bool store = j < NW && ray < R;
         for (int dt = wave; dt < ndt; dt += ST_WAVES) {
-            const typename Th::Frag *wo = (const typename Th::Frag *)m.w_out + (int64_t)dt * 4 * SD_WAVE + lane;
+            HFrag wl[4];
+            if (ST_HEAD_PRE == 1 && dt == wave) {
+#pragma unroll
+                for (int s = 0; s < 4; ++s) wl[s] = w0[s];
+            } else {
+                head_w(dt, wl);
+            }
             f32x4 o = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int s = 0; s < 4; ++s) o = Th::mma(wo[s * SD_WAVE], Bh[s], o);
+            for (int s = 0; s < 4; ++s) o = Th::mma(wl[s], Bh[s], o);
             // rows 4 g + r of tile dt = dims 16 dt + 4 g + r, column j = ray slot
             const int dim = 16 * dt + 4 * g;
             const f32x4 bd = *(const f32x4 *)(m.b_dino + dim);
@@ -551,6 +578,14 @@ k_render_tile(const st_args sa) {
     uint4 wsig_r[4];
 #pragma unroll
     for (int s2 = 0; s2 < 4; ++s2) wsig_r[s2] = ((const uint4 *)m.w_sig)[s2 * SD_WAVE + lane];
+    // a wait the compiler SEES (the builtin, not inline asm: vmcnt(0), expcnt / lgkmcnt
+    // unconstrained): without it its wait-count tracking keeps these 20 loads pending into
+    // the item loop and guards their first uses there with vmcnt(19) .. vmcnt(0) -- which the
+    // hardware also counts the in-flight tile LDS-DMA against, so every item waited for the
+    // next group's staging to land
+#if ST_WAIT_FIX
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+#endif
 
     // ---- prologue: records + tile of step 0 -------------------------------------------
     int grp = gfirst;
@@ -583,9 +618,18 @@ k_render_tile(const st_args sa) {
         uint32_t lane_off = (uint32_t)((tq & 1) + (tq >> 1) * cur.pitch) * ST_TEX + 8u * (uint32_t)tp;
 
         float Tc = 1.f, dpart = 0.f, wpart = 0.f, cpart[3] = {0.f, 0.f, 0.f};
+#if ST_HC16
+        // per-lane partial sums sum_k w_k relu(h_k) over this lane's samples (one per item:
+        // K / 16 = 2..8 terms), packed f16 pairs in X's element order; the 16-lane sums of
+        // the epilogue are f32
+        f16x2 hacc16[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) hacc16[i] = f16x2{(_Float16)0.f, (_Float16)0.f};
+#else
         f32x4 hacc[8];
 #pragma unroll
         for (int t = 0; t < 8; ++t) hacc[t] = zero4;
+#endif
 
         // An item is split in two: A = records, taps, MFMA MLP, sigma, alpha, local
         // transmittance scan; B = weights with the carried transmittance, compositing sums,
@@ -672,6 +716,20 @@ k_render_tile(const st_args sa) {
             cpart[0] += w * st.col[0];
             cpart[1] += w * st.col[1];
             cpart[2] += w * st.col[2];
+#if ST_HC16
+            // hidden-space compositing: one v_pk_fma_f16 per packed pair of relu(h) (X is f16
+            // in both modes, RMode)
+            const f16x2 ww = __builtin_bit_cast(f16x2, sd_pack2<_Float16>(w, w));
+#pragma unroll
+            for (int s2 = 0; s2 < 4; ++s2) {
+                const uint4 u = __builtin_bit_cast(uint4, st.X[s2]);
+                const uint32_t d4[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    hacc16[4 * s2 + q] = __builtin_elementwise_fma(__builtin_bit_cast(f16x2, d4[q]), ww,
+                                                                   hacc16[4 * s2 + q]);
+            }
+#else
             // hidden-space compositing: v_dot2 of the packed hidden pairs with (w, 0) / (0, w)
             const uint32_t wl = sd_pack2<E>(w, 0.f), wh = sd_pack2<E>(0.f, w);
 #pragma unroll
@@ -685,15 +743,19 @@ k_render_tile(const st_args sa) {
                     hacc[t][r + 1] = Tr::dot2(d4[q], wh, hacc[t][r + 1]);
                 }
             }
+#endif
             // weight and alpha into the sample's record (q1.x / .y are dead once itemA has
             // read the point); the ray epilogue stores every per-sample output coalesced
             if (g == 0) *(float2 *)&rq1(buf)[k] = float2{w, st.alpha};
         };
 
         // item 0 with the next ray's pass and the previous group's head
+        HFrag hw[4];
+        if (ST_HEAD_PRE == 1 && prev_ok && wave < ndt) head_w(wave, hw);
+        if (ST_HEAD_PRE == 2 && prev_ok) head(prev_grp, hw);
         if (has_next) ray_pass(nray, buf ^ 1, buf ^ 1);
         ST_T(0);
-        if (prev_ok) head(prev_grp);
+        if (ST_HEAD_PRE != 2 && prev_ok) head(prev_grp, hw);
         ST_T(1);
         IState s0;
         if (active) itemA(0, s0);
@@ -741,6 +803,18 @@ k_render_tile(const st_args sa) {
             // values at the first two levels, quad permutes finish -- lane bank b then holds
             // q = i + 8 b, i = 0..7 (hidden 16 (2 b + (i >> 2)) + 4 g + (i & 3))
             {
+#if ST_HC16
+                // the packed partial sums in the f32 [t][r] order of the butterfly
+                float hacc[8][4];
+#pragma unroll
+                for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int t = 2 * s2 + (q >> 1), r = 2 * (q & 1);
+                        hacc[t][r] = (float)hacc16[4 * s2 + q][0];
+                        hacc[t][r + 1] = (float)hacc16[4 * s2 + q][1];
+                    }
+#endif
                 float u[16], v[8];
                 // level 1 reads the hacc values of the item loop (one s_nop 1 in front of the
                 // first statement covers any of them written just before); level 2 reads
@@ -807,7 +881,11 @@ k_render_tile(const st_args sa) {
         st_barrier_lds();  // Y: next tile complete; hsum of this group written
         ST_T(9);
     }
-    if (prev_ok) head(prev_grp);
+    if (prev_ok) {
+        HFrag hw[4];
+        if (ST_HEAD_PRE == 1 && wave < ndt) head_w(wave, hw);
+        head(prev_grp, hw);
+    }
 #if ST_PROF
     if (lane < 19) {
         uint32_t v = 0;
