@@ -31,6 +31,7 @@
 // and is applied per GROUP: hsum of the 8 rays as the B operand (8 of 16 columns),
 // D / 16 MFMA tiles spread over the waves.
 #include "sdhip_render.h"
+#include <stdlib.h>
 
 // waves per workgroup = rays per group (NW): 8 (2 waves per SIMD), or for K <= 64 the
 // ST_NW_SMALLK-wave variant (12: 3 waves per SIMD, the kernel compiled for <= 168 VGPRs)
@@ -108,13 +109,16 @@ struct st_args {
 // hidden-sum rows padded to 272 B: the DINO head reads the same 8-B slot of the NW rows in
 // one instruction (256-B rows put them on one bank pair: 8-way conflicts)
 #define ST_HS_ROW 272
-__host__ __device__ constexpr int st_l_hs(int nw) { return ST_L_BOX + 2 * nw * 16; }         // [NW rays][128] 16-bit hidden sums
-__host__ __device__ constexpr int st_l_ws(int nw) { return st_l_hs(nw) + nw * ST_HS_ROW; }   // [NW] f32 weight sums
-__host__ __device__ constexpr int st_l_ray(int nw) { return st_l_ws(nw) + 16 * 4; }          // [NW waves][2] x 32 B ray words 0..7 (LDS-DMA)
-__host__ __device__ constexpr int st_l_rec(int nw) { return st_l_ray(nw) + nw * 2 * 32; }    // records: [NW waves][2][K] x 40 B
-static_assert(st_l_rec(8) % 16 == 0 && st_l_rec(12) % 16 == 0, "record area alignment");
+// rpw = rays per wave and step (2 for K <= 32: a group is NW rpw rays)
+__host__ __device__ constexpr int st_l_hs(int nw) { return ST_L_BOX + 2 * nw * 16; }         // [NW rpw rays][128] 16-bit hidden sums
+__host__ __device__ constexpr int st_l_ws(int nw, int rpw) { return st_l_hs(nw) + nw * rpw * ST_HS_ROW; }  // [NW rpw] f32 weight sums
+__host__ __device__ constexpr int st_l_ray(int nw, int rpw) { return st_l_ws(nw, rpw) + 16 * 4; }          // [NW waves][2] x rpw x 32 B ray words 0..7 (LDS-DMA)
+__host__ __device__ constexpr int st_l_rec(int nw, int rpw) { return st_l_ray(nw, rpw) + nw * 2 * 32 * rpw; }  // records: [NW waves][2][rpw K] x 40 B
+static_assert(st_l_rec(8, 1) % 16 == 0 && st_l_rec(12, 1) % 16 == 0 && st_l_rec(8, 2) % 16 == 0,
+              "record area alignment");
 
-__host__ __device__ constexpr int st_rec_bytes(int nw, int K) { return nw * 2 * K * 40; }
+// record bytes for samples-per-wave-step kw = rpw K
+__host__ __device__ constexpr int st_rec_bytes(int nw, int kw) { return nw * 2 * kw * 40; }
 
 // one butterfly level of a 16-lane row sum over two values: out = a + a(lane - RA) on the
 // lanes of banks MA (groups of 4 lanes), b + b(lane - RB) on the lanes of banks MB (MA | MB =
@@ -208,12 +212,18 @@ __device__ __forceinline__ uint2 st_tr(uint32_t addr) {
 // ZIN: depths given (args.z, parity tests) instead of drawn in the kernel.  A template
 // parameter, not a branch: with both paths in one body the compiler's wait for the z loads
 // also drains other loads on the drawing path.
-template <int P, bool ZIN, int NW>
+// RPW = 2 (K <= 32): every wave takes TWO neighbouring rays per step -- the ray pass runs
+// their 2 K samples on the 64 lanes, a group is 2 NW rays (one tile box, barrier pair, DINO
+// head and set of DMA issues per 16 rays), the items of ray A then of ray B, one sum
+// epilogue per ray.  The per-step phases that cost the same at any K are paid once per two
+// rays (round-4 phase split at K = 32: items only 23 % of the wave time).
+template <int P, bool ZIN, int NW, int RPW>
 __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4)))
 k_render_tile(const st_args sa) {
     constexpr int ST_WAVES = NW;
-    constexpr int ST_L_HS = st_l_hs(NW), ST_L_WS = st_l_ws(NW), ST_L_RAY = st_l_ray(NW),
-                  ST_L_REC = st_l_rec(NW);
+    constexpr int GR = NW * RPW;  // rays per group
+    constexpr int ST_L_HS = st_l_hs(NW), ST_L_WS = st_l_ws(NW, RPW), ST_L_RAY = st_l_ray(NW, RPW),
+                  ST_L_REC = st_l_rec(NW, RPW);
     typedef typename RMode<P>::F Tr;  // operands upstream of sigma (f16 in both modes)
     typedef typename RMode<P>::H Th;  // DINO head (bf16 in the bf16 mode)
     typedef typename Tr::Frag Frag;
@@ -230,7 +240,8 @@ k_render_tile(const st_args sa) {
 
     const int lane = threadIdx.x & 63, j = lane & 15, g = lane >> 4;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int K = a.K, nsub = K >> 4;
+    const int K = a.K, nsub = K >> 4;   // samples / items per ray
+    const int KW = K * RPW, nsubw = KW >> 4;  // per wave and step
     const int R = (int)a.R, rps = (int)a.rays_per_sb;
     const int D = m.D, ndt = D >> 4;
     const int Wf = a.Wf, Hf = a.Hf;
@@ -239,11 +250,12 @@ k_render_tile(const st_args sa) {
     // records: SoA per (wave, buffer): q0 [K] x 16 B | q1 [K] x 16 B | c [K] x 8 B
     //   q0 = {x0 | y0 << 15 | inv_f << 30 | invc << 31, (w00, w01), (w10, w11), r}
     //   q1 = {x, y, z~, z}   c = {g, b}
-    const uint32_t rec_base = ST_L_REC + (uint32_t)wave * 2 * K * 40;
-    auto rq0 = [&](int buf) { return (uint4 *)(lds + rec_base + buf * K * 40); };
-    auto rq1 = [&](int buf) { return (f32x4 *)(lds + rec_base + buf * K * 40 + K * 16); };
-    auto rqc = [&](int buf) { return (float2 *)(lds + rec_base + buf * K * 40 + K * 32); };
-    const uint32_t tile0 = ST_L_REC + st_rec_bytes(NW, K);
+    // (RPW = 2: record k' = r K + k is sample k of the wave's ray r)
+    const uint32_t rec_base = ST_L_REC + (uint32_t)wave * 2 * KW * 40;
+    auto rq0 = [&](int buf) { return (uint4 *)(lds + rec_base + buf * KW * 40); };
+    auto rq1 = [&](int buf) { return (f32x4 *)(lds + rec_base + buf * KW * 40 + KW * 16); };
+    auto rqc = [&](int buf) { return (float2 *)(lds + rec_base + buf * KW * 40 + KW * 32); };
+    const uint32_t tile0 = ST_L_REC + st_rec_bytes(NW, KW);
 
     // XCD-aware group ranges (workgroups b, b + 8, ... share an XCD, speed only)
     const int NG = sa.ngroups;
@@ -262,25 +274,37 @@ k_render_tile(const st_args sa) {
     // LDS-DMA one step ahead (completed by the step's closing vmcnt(0)), so the ray pass
     // reads them from LDS instead of waiting on scalar loads
     const int nrw = min(a.ray_dim, 8);
+    // the wave's RPW rays ray .. ray + RPW - 1: lane 8 r + w fetches word w of ray r
     auto ray_fetch = [&](int ray, int slot) {
-        if (ray < R && lane < nrw)
-            st_dma4(a.rays + (int64_t)ray * a.ray_dim + lane, lds0 + ST_L_RAY + (wave * 2 + slot) * 32);
+        const int r = lane >> 3, w = lane & 7;
+        if (r < RPW && w < nrw && ray + r < R)
+            st_dma4(a.rays + (int64_t)(ray + r) * a.ray_dim + w,
+                    lds0 + ST_L_RAY + (wave * 2 + slot) * 32 * RPW);
     };
-    const float *rl = nullptr;  // this ray pass's words (set by ray_pass)
+    // this lane's ray of the wave's RPW (ray pass: lane = record k' = rsl K + k)
+    const int rsl = RPW == 1 ? 0 : min(lane / K, RPW - 1);
+    const int kl = lane - rsl * K;  // its sample (RPW = 2)
+    const float *rl = nullptr;  // this ray pass's words (set by ray_pass; RPW = 2: per lane)
     auto load_ray_z = [&](int ray, float zq[2 * ST_MAXP]) {
         float zo[ST_MAXP];
         if (ZIN) {
-            const float *zr = a.z + (int64_t)ray * K;
+            if (RPW == 1) {
+                const float *zr = a.z + (int64_t)ray * K;
 #pragma unroll
-            for (int p = 0; p < ST_MAXP; ++p) zo[p] = zr[min(64 * p + lane, K - 1)];
+                for (int p = 0; p < ST_MAXP; ++p) zo[p] = zr[min(64 * p + lane, K - 1)];
+            } else {
+                const float *zr = a.z + (int64_t)min(ray + rsl, R - 1) * K;
+                zo[0] = zr[min(kl, K - 1)];  // (lanes past 2 K: K = 16)
+                zo[1] = 0.f;
+            }
         } else {
             const float near = rl[6], far = rl[7];
-            const uint64_t base = a.z_offset + (uint64_t)ray * (uint64_t)K;
+            const uint64_t base = a.z_offset + (uint64_t)(ray + rsl) * (uint64_t)K;
             zo[1] = 0.f;
 #pragma unroll
             for (int p = 0; p < ST_MAXP; ++p) {
-                if (64 * p >= K) break;  // wave-uniform: K <= 64 draws one sample per lane
-                const int k = min(64 * p + lane, K - 1);
+                if (64 * p >= KW) break;  // wave-uniform: KW <= 64 draws one sample per lane
+                const int k = RPW == 1 ? min(64 * p + lane, K - 1) : kl;
                 zo[p] = sd_z_sample(near, far, K, k, sd_uniform(a.z_seed, base + k), zstep, zend,
                                     a.z_lindisp);
             }
@@ -292,7 +316,7 @@ k_render_tile(const st_args sa) {
                 ? __builtin_bit_cast(float, __builtin_amdgcn_readlane(
                       __builtin_bit_cast(int, zo[p + 1 < ST_MAXP ? p + 1 : p]), 0))
                 : zo[p];
-            if (lane == 63) nx2 = (p + 1 < ST_MAXP && 64 * (p + 1) < K) ? first_next : zo[p];
+            if (lane == 63) nx2 = (p + 1 < ST_MAXP && 64 * (p + 1) < KW) ? first_next : zo[p];
             zq[2 * p] = zo[p];
             zq[2 * p + 1] = nx2;
         }
@@ -302,14 +326,16 @@ k_render_tile(const st_args sa) {
     ColPend cpend;
     // tap boxes per half ray: samples [0, kh) and [kh, K), kh = 16 (nsub / 2) -- a group
     // whose whole box does not fit a tile buffer is staged and rendered half by half
-    const int kh = 16 * (nsub >> 1);
+    // (RPW = 2: the halves are the two rays)
+    const int kh = RPW == 1 ? 16 * (nsub >> 1) : K;
     auto ray_pass = [&](int ray, int buf, int slot) {
         uint32_t bmin0 = 0xffffffffu, bmax0 = 0u, bmin1 = 0xffffffffu, bmax1 = 0u;
         if (ray < R) {
             // wave-uniform (readfirstlane: the u32 divide runs on the VALU, and a VGPR
-            // address would turn the camera-record reads into vector loads)
+            // address would turn the camera-record reads into vector loads); a group's rays
+            // share their super-batch (rays_per_sb % GR == 0)
             const int sbi = __builtin_amdgcn_readfirstlane((int)((unsigned)ray / (unsigned)rps));
-            rl = (const float *)(lds + ST_L_RAY + (wave * 2 + slot) * 32);
+            rl = (const float *)(lds + ST_L_RAY + (wave * 2 + slot) * 32 * RPW) + 8 * rsl;
             // colour view = encoder view (the single-frame render, ids_render = ids_encoder):
             // the host passes the same camera records for both (cam_c == cam_f), so the
             // colour taps are the encoder-view taps at equal resolution (kernel-uniform test)
@@ -323,8 +349,8 @@ k_render_tile(const st_args sa) {
             float2 *rc = rqc(buf);
 #pragma unroll
             for (int p = 0; p < ST_MAXP; ++p) {
-                const int k = 64 * p + lane;
-                if (64 * p < K && k < K) {
+                const int k = 64 * p + lane;  // record k' (RPW = 2: ray rsl's sample kl)
+                if (64 * p < KW && k < KW && (RPW == 1 || ray + rsl < R)) {
                     const float z0 = zq[2 * p];
                     const float px = ox + z0 * dx, py = oy + z0 * dy, pz = oz + z0 * dz;  // nerf.py:252
                     const PointGeo geo = ST_GEO((sd_cfloat *)(a.cam_f + sbi * SD_CAM_WORDS), px, py, pz,
@@ -363,7 +389,7 @@ k_render_tile(const st_args sa) {
             }
         }
         ST_T(11);
-        if (K == 64) {
+        if (KW == 64) {
             // one sample per lane, halves = lanes [0, 32) and [32, 64): rows 0-1 / 2-3
             const uint32_t mnv = st_row_red2<false>(lane < 32 ? bmin0 : bmin1);
             const uint32_t mxv = st_row_red2<true>(lane < 32 ? bmax0 : bmax1);
@@ -382,7 +408,7 @@ k_render_tile(const st_args sa) {
             *(uint4 *)(lds + ST_L_BOX + (slot * ST_WAVES + wave) * 16) = uint4{bmin0, bmax0, bmin1, bmax1};
     };
     auto ray_col = [&](int ray, int buf) {
-        if (ray < R && lane < K) {
+        if (ray + rsl < R && lane < KW) {
             float col[3];
             sd_color_finish(cpend, col);
             rq0(buf)[lane].w = __builtin_bit_cast(uint32_t, col[0]);
@@ -472,9 +498,9 @@ k_render_tile(const st_args sa) {
         }
         if (!t.ok) {
             if (wave == 0 && lane == 0) {  // the group's rays as NW / SD_LIST_BLK list blocks
-                const int i = atomicAdd(sa.ovf, NW / SD_LIST_BLK);
-                for (int b = 0; b < NW / SD_LIST_BLK; ++b)
-                    sa.ovf[1 + i + b] = grp * (NW / SD_LIST_BLK) + b;
+                const int i = atomicAdd(sa.ovf, GR / SD_LIST_BLK);
+                for (int b = 0; b < GR / SD_LIST_BLK; ++b)
+                    sa.ovf[1 + i + b] = grp * (GR / SD_LIST_BLK) + b;
             }
             return t;
         }
@@ -501,7 +527,7 @@ k_render_tile(const st_args sa) {
 #pragma unroll
         for (int p = 0; p < ST_MAXP; ++p) {
             const int k = 64 * p + lane;
-            if (64 * p < K && k < K) {
+            if (64 * p < KW && k < KW) {
                 const uint32_t xy = w[4 * k];
                 const Tile &tt = (t.split && k >= kh) ? t2 : t;
                 const int x0 = (int)(xy & 0x7fffu), y0 = (int)((xy >> 15) & 0x7fffu);
@@ -523,7 +549,7 @@ k_render_tile(const st_args sa) {
     };
     auto head = [&](int grp, const HFrag w0[4]) {
         if (wave >= ndt) return;
-        const int slot = j < NW ? j : 0;  // B columns j >= NW: not stored
+        const int slot = j < GR ? j : 0;  // B columns j >= GR: not stored
         typename Th::Frag Bh[4];
         const uint8_t *hs = lds + ST_L_HS + slot * ST_HS_ROW;
 #pragma unroll
@@ -533,8 +559,8 @@ k_render_tile(const st_args sa) {
             Bh[s] = __builtin_bit_cast(typename Th::Frag, uint4{lo.x, lo.y, hi.x, hi.y});
         }
         const float ws = *(const float *)(lds + ST_L_WS + slot * 4);
-        const int ray = NW * grp + j;
-        const bool store = j < NW && ray < R;
+        const int ray = GR * grp + j;
+        const bool store = j < GR && ray < R;
         for (int dt = wave; dt < ndt; dt += ST_WAVES) {
             HFrag wl[4];
             if (ST_HEAD_PRE == 1 && dt == wave) {
@@ -589,10 +615,10 @@ k_render_tile(const st_args sa) {
 
     // ---- prologue: records + tile of step 0 -------------------------------------------
     int grp = gfirst;
-    int ray = NW * grp + wave;
-    int sbi = __builtin_amdgcn_readfirstlane((int)((unsigned)min(NW * grp, R - 1) / (unsigned)rps));
+    int ray = GR * grp + RPW * wave;  // the wave's first ray of the step
+    int sbi = __builtin_amdgcn_readfirstlane((int)((unsigned)min(GR * grp, R - 1) / (unsigned)rps));
     ray_fetch(ray, 0);
-    ray_fetch(NW * (grp + nwg) + wave, 1);
+    ray_fetch(GR * (grp + nwg) + RPW * wave, 1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     ray_pass(ray, 0, 0);
     ray_col(ray, 0);
@@ -612,24 +638,32 @@ k_render_tile(const st_args sa) {
         const int buf = n & 1;
         const bool has_next = n + 1 < nsteps;
         const int ngrp = grp + nwg;
-        const int nray = NW * ngrp + wave;
-        const int nsbi = has_next ? __builtin_amdgcn_readfirstlane((int)((unsigned)min(NW * ngrp, R - 1) / (unsigned)rps)) : 0;
-        const bool active = cur.ok && ray < R;
+        const int nray = GR * ngrp + RPW * wave;
+        const int nsbi = has_next ? __builtin_amdgcn_readfirstlane((int)((unsigned)min(GR * ngrp, R - 1) / (unsigned)rps)) : 0;
         uint32_t lane_off = (uint32_t)((tq & 1) + (tq >> 1) * cur.pitch) * ST_TEX + 8u * (uint32_t)tp;
 
-        float Tc = 1.f, dpart = 0.f, wpart = 0.f, cpart[3] = {0.f, 0.f, 0.f};
+        // per-ray compositing state (RPW = 2: reset between the wave's two rays)
+        float Tc, dpart, wpart, cpart[3];
 #if ST_HC16
         // per-lane partial sums sum_k w_k relu(h_k) over this lane's samples (one per item:
-        // K / 16 = 2..8 terms), packed f16 pairs in X's element order; the 16-lane sums of
+        // K / 16 = 1..8 terms), packed f16 pairs in X's element order; the 16-lane sums of
         // the epilogue are f32
         f16x2 hacc16[16];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) hacc16[i] = f16x2{(_Float16)0.f, (_Float16)0.f};
 #else
         f32x4 hacc[8];
-#pragma unroll
-        for (int t = 0; t < 8; ++t) hacc[t] = zero4;
 #endif
+        auto reset = [&]() {
+            Tc = 1.f;
+            dpart = wpart = cpart[0] = cpart[1] = cpart[2] = 0.f;
+#if ST_HC16
+#pragma unroll
+            for (int i = 0; i < 16; ++i) hacc16[i] = f16x2{(_Float16)0.f, (_Float16)0.f};
+#else
+#pragma unroll
+            for (int t = 0; t < 8; ++t) hacc[t] = zero4;
+#endif
+        };
+        reset();
 
         // An item is split in two: A = records, taps, MFMA MLP, sigma, alpha, local
         // transmittance scan; B = weights with the carried transmittance, compositing sums,
@@ -639,11 +673,12 @@ k_render_tile(const st_args sa) {
             float alpha, excl, tmul, zk, col[3];
         };
         auto itemA = [&](int sub, IState &st) {
-            const int k = sub * 16 + j;
-            const uint4 q0 = rq0(buf)[k];
-            const f32x4 q1 = rq1(buf)[k];
-            const float2 cgb = rqc(buf)[k];
-            const float znext = k + 1 < K ? rq1(buf)[k + 1][3] : 0.f;
+            const int kr = sub * 16 + j;                                 // record k'
+            const int k = RPW == 1 ? kr : kr - (sub / nsub) * K;         // sample of its ray
+            const uint4 q0 = rq0(buf)[kr];
+            const f32x4 q1 = rq1(buf)[kr];
+            const float2 cgb = rqc(buf)[kr];
+            const float znext = k + 1 < K ? rq1(buf)[kr + 1][3] : 0.f;
             const float v[3] = {q1[0], q1[1], q1[2]};
             st.zk = q1[3];
             const float delta = k + 1 < K ? znext - st.zk : 1e10f;
@@ -708,7 +743,7 @@ k_render_tile(const st_args sa) {
             st.tmul = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, incl), 15));
         };
         auto itemB = [&](int sub, const IState &st) {
-            const int k = sub * 16 + j;
+            const int k = sub * 16 + j;  // record k'
             const float w = st.alpha * (Tc * st.excl);
             Tc *= st.tmul;
             dpart += w * st.zk;
@@ -753,12 +788,13 @@ k_render_tile(const st_args sa) {
         HFrag hw[4];
         if (ST_HEAD_PRE == 1 && prev_ok && wave < ndt) head_w(wave, hw);
         if (ST_HEAD_PRE == 2 && prev_ok) head(prev_grp, hw);
+        if (ST_HEAD_PRE == 2) ST_T(1);
         if (has_next) ray_pass(nray, buf ^ 1, buf ^ 1);
         ST_T(0);
         if (ST_HEAD_PRE != 2 && prev_ok) head(prev_grp, hw);
-        ST_T(1);
+        if (ST_HEAD_PRE != 2) ST_T(1);
         IState s0;
-        if (active) itemA(0, s0);
+        if (cur.ok && ray < R) itemA(0, s0);
         ST_T(2);
         if (has_next) ray_col(nray, buf ^ 1);
         ST_T(3);
@@ -774,30 +810,14 @@ k_render_tile(const st_args sa) {
         // half's box is staged into the same buffer (workgroup-uniform branch, taken by
         // every wave: it holds barriers).  One item loop for both cases keeps the kernel
         // small (a second inlined copy of the items measured slower).
-        const int nfirst = cur.split ? (nsub >> 1) : nsub;
-        for (int sub = 0; sub < nsub; ++sub) {
-            if (sub == nfirst) {
-                st_barrier_lds();  // every wave is done with the first half's taps
-                uint32_t mn1, mx1;
-                box_union(buf, 1, mn1, mx1);
-                cur = geom(mn1, mx1);  // fits: checked when the split was chosen
-                dma(cur, buf, sbi);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                st_barrier_lds();
-                lane_off = (uint32_t)((tq & 1) + (tq >> 1) * cur.pitch) * ST_TEX + 8u * (uint32_t)tp;
-            }
-            if (active) {
-                if (sub) itemA(sub, s0);
-                itemB(sub, s0);
-            }
-        }
-        ST_T(6);
-        if (active) {
-            // ray epilogue: sums over the 16 sample lanes of every row
+        // (RPW = 2: the first half is ray A -- a split group restages at the ray boundary)
+        const int nfirst = cur.split ? (nsubw >> 1) : nsubw;
+        // ray epilogue of the wave's ray r: sums over the 16 sample lanes of every row
+        auto ray_sums = [&](int r) {
             const float dsum = sd_rowsum16(dpart), wsum = sd_rowsum16(wpart);
             const float c0s = sd_rowsum16(cpart[0]), c1s = sd_rowsum16(cpart[1]),
                         c2s = sd_rowsum16(cpart[2]);
-            uint8_t *hs = lds + ST_L_HS + wave * ST_HS_ROW;
+            uint8_t *hs = lds + ST_L_HS + (wave * RPW + r) * ST_HS_ROW;
             // the 32 hidden sums q = 4 t + r reduced over the 16 sample lanes of the row as a
             // butterfly (64 VALU ops instead of 32 x 4): bank-masked DPP halves the live
             // values at the first two levels, quad permutes finish -- lane bank b then holds
@@ -811,14 +831,29 @@ k_render_tile(const st_args sa) {
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
                         const int t = 2 * s2 + (q >> 1), r = 2 * (q & 1);
-                        hacc[t][r] = (float)hacc16[4 * s2 + q][0];
-                        hacc[t][r + 1] = (float)hacc16[4 * s2 + q][1];
+                        // (from the bits: element extraction of the f16x2 array lost one
+                        // conversion in an inlined copy of this epilogue, hipcc 7.2)
+                        const uint32_t hb = __builtin_bit_cast(uint32_t, hacc16[4 * s2 + q]);
+                        hacc[t][r] = (float)__builtin_bit_cast(_Float16, (uint16_t)(hb & 0xffffu));
+                        hacc[t][r + 1] = (float)__builtin_bit_cast(_Float16, (uint16_t)(hb >> 16));
                     }
 #endif
                 float u[16], v[8];
-                // level 1 reads the hacc values of the item loop (one s_nop 1 in front of the
-                // first statement covers any of them written just before); level 2 reads
-                // u[i], u[i + 8], written by level-1 statements at least 14 ops earlier
+                // Every level-1 input is pinned in its register by two fence statements ("+v",
+                // each with s_nop 1) before the first DPP: the compiler cannot schedule an
+                // input's last VALU write (e.g. an f16 -> f32 conversion) right in front of the
+                // DPP statement that reads it -- a VALU-write -> DPP-read hazard without the
+                // two wait states, which it does not see inside inline asm (round 5: one
+                // inlined copy of this epilogue read a packed f16 pair as f32).  Level 2 reads
+                // u[i], u[i + 8], written by level-1 statements at least 14 ops earlier.
+                asm volatile("s_nop 1" : "+v"(hacc[0][0]), "+v"(hacc[0][1]), "+v"(hacc[0][2]), "+v"(hacc[0][3]),
+                             "+v"(hacc[1][0]), "+v"(hacc[1][1]), "+v"(hacc[1][2]), "+v"(hacc[1][3]),
+                             "+v"(hacc[2][0]), "+v"(hacc[2][1]), "+v"(hacc[2][2]), "+v"(hacc[2][3]),
+                             "+v"(hacc[3][0]), "+v"(hacc[3][1]), "+v"(hacc[3][2]), "+v"(hacc[3][3]));
+                asm volatile("s_nop 1" : "+v"(hacc[4][0]), "+v"(hacc[4][1]), "+v"(hacc[4][2]), "+v"(hacc[4][3]),
+                             "+v"(hacc[5][0]), "+v"(hacc[5][1]), "+v"(hacc[5][2]), "+v"(hacc[5][3]),
+                             "+v"(hacc[6][0]), "+v"(hacc[6][1]), "+v"(hacc[6][2]), "+v"(hacc[6][3]),
+                             "+v"(hacc[7][0]), "+v"(hacc[7][1]), "+v"(hacc[7][2]), "+v"(hacc[7][3]));
                 ST_BFLY("s_nop 1\n\t", u[0], hacc[0][0], hacc[4][0], 8, 8, 0x3, 0xc);
 #pragma unroll
                 for (int i = 1; i < 16; ++i)
@@ -839,33 +874,60 @@ k_render_tile(const st_args sa) {
                         uint2{sd_pack2<EH>(v[4], v[5]), sd_pack2<EH>(v[6], v[7])};
                 }
             }
-            {
-                // per-sample outputs, lane = sample (one coalesced store per array)
-                const int64_t rk = (int64_t)ray * K;
+            if (lane == 0) {
+                *(float *)(lds + ST_L_WS + (wave * RPW + r) * 4) = wsum;
+                a.depth[(int64_t)(ray + r) * a.ld_depth] = dsum;
+                float *rp = a.rgb + (int64_t)(ray + r) * a.ld_rgb;
+                rp[0] = c0s; rp[1] = c1s; rp[2] = c2s;
+            }
+        };
+        for (int sub = 0; sub < nsubw; ++sub) {
+            if (sub == nfirst) {
+                st_barrier_lds();  // every wave is done with the first half's taps
+                uint32_t mn1, mx1;
+                box_union(buf, 1, mn1, mx1);
+                cur = geom(mn1, mx1);  // fits: checked when the split was chosen
+                dma(cur, buf, sbi);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                st_barrier_lds();
+                lane_off = (uint32_t)((tq & 1) + (tq >> 1) * cur.pitch) * ST_TEX + 8u * (uint32_t)tp;
+            }
+            const int r = RPW == 1 ? 0 : sub / nsub;
+            const bool act = cur.ok && ray + r < R;
+            if (act) {
+                if (sub) itemA(sub, s0);
+                itemB(sub, s0);
+            }
+            if (RPW > 1 && (sub + 1) % nsub == 0 && sub + 1 < nsubw) {  // ray r done
+                if (act) ray_sums(r);
+                reset();
+            }
+        }
+        ST_T(6);
+        if (cur.ok && ray + RPW - 1 < R) ray_sums(RPW - 1);
+        if (cur.ok) {
+            // per-sample outputs of the wave's RPW rays, lane = record k' (one coalesced store
+            // per array)
 #pragma unroll
-                for (int p = 0; p < ST_MAXP; ++p) {
-                    const int k = 64 * p + lane;
-                    if (64 * p < K && k < K) {
-                        const f32x4 q1v = rq1(buf)[k];
-                        const uint4 q0v = rq0(buf)[k];
-                        const uint32_t fl = q0v.x >> 30;
-                        if (a.weights) a.weights[rk + k] = q1v[0];
-                        if (a.alphas) a.alphas[rk + k] = q1v[1];
-                        if (a.invalid_f) a.invalid_f[rk + k] = (uint8_t)(fl & 1u);
-                        if (a.invalid) a.invalid[rk + k] = fl ? 1.f : 0.f;
-                        if (a.rgb_samps) {
-                            const float2 cgb = rqc(buf)[k];
-                            float *rsp = a.rgb_samps + (rk + k) * 3;
-                            rsp[0] = __builtin_bit_cast(float, q0v.w); rsp[1] = cgb.x; rsp[2] = cgb.y;
-                        }
+            for (int p = 0; p < ST_MAXP; ++p) {
+                const int kr = 64 * p + lane;
+                const int rr = RPW == 1 ? 0 : min(kr / K, RPW - 1);
+                const int k = kr - rr * K;
+                if (64 * p < KW && kr < KW && ray + rr < R) {
+                    const int64_t rk = (int64_t)(ray + rr) * K;
+                    const f32x4 q1v = rq1(buf)[kr];
+                    const uint4 q0v = rq0(buf)[kr];
+                    const uint32_t fl = q0v.x >> 30;
+                    if (a.weights) a.weights[rk + k] = q1v[0];
+                    if (a.alphas) a.alphas[rk + k] = q1v[1];
+                    if (a.invalid_f) a.invalid_f[rk + k] = (uint8_t)(fl & 1u);
+                    if (a.invalid) a.invalid[rk + k] = fl ? 1.f : 0.f;
+                    if (a.rgb_samps) {
+                        const float2 cgb = rqc(buf)[kr];
+                        float *rsp = a.rgb_samps + (rk + k) * 3;
+                        rsp[0] = __builtin_bit_cast(float, q0v.w); rsp[1] = cgb.x; rsp[2] = cgb.y;
                     }
                 }
-            }
-            if (lane == 0) {
-                *(float *)(lds + ST_L_WS + wave * 4) = wsum;
-                a.depth[(int64_t)ray * a.ld_depth] = dsum;
-                float *rp = a.rgb + (int64_t)ray * a.ld_rgb;
-                rp[0] = c0s; rp[1] = c1s; rp[2] = c2s;
             }
         }
         ST_T(7);
@@ -875,7 +937,7 @@ k_render_tile(const st_args sa) {
         ray = nray;
         sbi = nsbi;
         cur = nxt;
-        if (n + 2 < nsteps) ray_fetch(NW * (ngrp + nwg) + wave, buf);  // ray of step n + 2
+        if (n + 2 < nsteps) ray_fetch(GR * (ngrp + nwg) + RPW * wave, buf);  // rays of step n + 2
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed
         ST_T(8);
         st_barrier_lds();  // Y: next tile complete; hsum of this group written
@@ -912,17 +974,27 @@ static int sd_check_last(const char *what) {
 
 static int st_nw(int K) { return K <= 64 ? ST_NW_SMALLK : 8; }
 
+// rays per wave and step: 2 for K <= 32 (SDHIP_TILE_RPW=1 forces one, diagnostic A/B)
+static int st_rpw(int K) {
+    static const int force1 = getenv("SDHIP_TILE_RPW") && atoi(getenv("SDHIP_TILE_RPW")) == 1;
+    return (K <= 32 && !force1 && st_nw(K) == 8) ? 2 : 1;
+}
+
+static int st_lds_fixed(int K) {
+    const int nw = st_nw(K), rpw = st_rpw(K);
+    return st_l_rec(nw, rpw) + st_rec_bytes(nw, K * rpw);
+}
+
 static int st_tile_bytes(int K) {
-    const int nw = st_nw(K);
-    const int fixed = st_l_rec(nw) + st_rec_bytes(nw, K);
-    const int avail = 160 * 1024 - fixed;
+    const int avail = 160 * 1024 - st_lds_fixed(K);
     return ((avail / 2) / 1024) * 1024;
 }
 
 // Can the tile kernel take this render?  (colour in exactly one render view, batches of
 // whole groups, K <= 128, room for one tile buffer pair.)
 extern "C" int sd_render_tile_ok(const sd_render_args *a, const sd_head *m) {
-    return a->nv == 1 && a->K % 16 == 0 && a->K <= 128 && a->rays_per_sb % st_nw(a->K) == 0 &&
+    return a->nv == 1 && a->K % 16 == 0 && a->K <= 128 &&
+           a->rays_per_sb % (st_nw(a->K) * st_rpw(a->K)) == 0 &&
            m->D % 16 == 0 && m->D <= 512 && a->Wf < 32768 && a->Hf < 32768 &&
            st_tile_bytes(a->K) >= 16 * 1024;
 }
@@ -936,10 +1008,10 @@ extern "C" int sd_render_tile_launch(const sd_render_args *a, const sd_head *m, 
     sa.a = *a;
     sa.m = *m;
     sa.ovf = ovf;
-    const int nw = st_nw(a->K);
-    sa.ngroups = (int)((a->R + nw - 1) / nw);
+    const int nw = st_nw(a->K), rpw = st_rpw(a->K);
+    sa.ngroups = (int)((a->R + nw * rpw - 1) / (nw * rpw));
     sa.tile_bytes = st_tile_bytes(a->K);
-    const int lds_bytes = st_l_rec(nw) + st_rec_bytes(nw, a->K) + 2 * sa.tile_bytes;
+    const int lds_bytes = st_lds_fixed(a->K) + 2 * sa.tile_bytes;
     if (hipMemsetAsync(ovf, 0, sizeof(int32_t), s) != hipSuccess) {
         sd_set_error("sd_render_proj: overflow counter reset failed");
         return -2;
@@ -953,16 +1025,18 @@ extern "C" int sd_render_tile_launch(const sd_render_args *a, const sd_head *m, 
         hipLaunchKernelGGL(kern, dim3((unsigned)ncu), dim3(64 * nw), lds_bytes, s, sa);
     };
     const bool zin = a->z != nullptr;
-#define ST_GO(NWV)                                                                              \
-    if (m->dtype == SD_F16) {                                                                   \
-        if (zin) go(k_render_tile<SD_F16, true, NWV>); else go(k_render_tile<SD_F16, false, NWV>); \
-    } else {                                                                                    \
-        if (zin) go(k_render_tile<SD_BF16, true, NWV>); else go(k_render_tile<SD_BF16, false, NWV>); \
+#define ST_GO(NWV, RPWV)                                                                              \
+    if (m->dtype == SD_F16) {                                                                         \
+        if (zin) go(k_render_tile<SD_F16, true, NWV, RPWV>); else go(k_render_tile<SD_F16, false, NWV, RPWV>); \
+    } else {                                                                                          \
+        if (zin) go(k_render_tile<SD_BF16, true, NWV, RPWV>); else go(k_render_tile<SD_BF16, false, NWV, RPWV>); \
     }
-    if (nw == 8) {
-        ST_GO(8)
+    if (nw == 8 && rpw == 2) {
+        ST_GO(8, 2)
+    } else if (nw == 8) {
+        ST_GO(8, 1)
     } else {
-        ST_GO(ST_NW_SMALLK)
+        ST_GO(ST_NW_SMALLK, 1)
     }
 #undef ST_GO
     return sd_check_last("sd_render_proj (tile kernel)");

@@ -559,3 +559,46 @@ def test_wide_dino_head_vs_oracle(precision, D, K):
     assert c["dino_features"].shape[-1] == D
     for k in ("depth", "dino_features", "rgb", "weights"):
         assert rel_l2(c[k], ref[k]) < 1e-2, k
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp16"])
+@pytest.mark.parametrize("K", [16, 32])
+def test_tile_two_rays_per_wave_vs_oracle(precision, K):
+    """K <= 32 renders through the tile kernel's two-rays-per-wave form (RPW = 2: 16-ray
+    groups, both rays' samples in one ray pass, per-ray epilogues, a split group restaging
+    at the ray boundary) -- configs[0]'s K = 32 (pixelnerf.yaml) and K = 16 -- from an
+    offset render pose, against the CPU oracle (the reference's op sequence) with the 16-bit
+    tolerances of the module docstring; masks exact."""
+    from scenedino_amd.renderer import NeRFRenderer
+    from scenedino_amd.common.ray_sampler import ImageRaySampler
+    from oracle import render_oracle as O
+    import math
+    g = torch.Generator().manual_seed(200 + K)
+    H, W, C, D = 24, 80, 256, 64
+    images = torch.rand(1, 1, 3, H, W, generator=g) * 2 - 1
+    grid = torch.randn(1, C, 12, 40, generator=g)
+    W_in = torch.randn(128, C + 39, generator=g) * 0.06
+    b_in = torch.randn(128, generator=g) * 0.1
+    W_out = torch.randn(1 + D, 128, generator=g) * 0.1
+    b_out = torch.randn(1 + D, generator=g) * 0.1
+    Kn = torch.tensor([[0.7849, 0.0, -0.0312], [0.0, 2.9391, 0.2701], [0.0, 0.0, 1.0]]).view(1, 1, 3, 3)
+    pose = torch.eye(4).view(1, 1, 4, 4)
+    a = math.radians(2.0)
+    rpose = pose.clone()
+    rpose[0, 0, 0, 0] = math.cos(a); rpose[0, 0, 0, 2] = math.sin(a)
+    rpose[0, 0, 2, 0] = -math.sin(a); rpose[0, 0, 2, 2] = math.cos(a)
+    rpose[0, 0, 0, 3] = 0.5
+    u = torch.rand(H * W, K, generator=g)
+    net = build_net(grid, W_in, b_in, W_out, b_out, precision, DEV)
+    net.encode(images.to(DEV), Kn.to(DEV), pose.to(DEV), ids_encoder=[0], ids_render=[0])
+    rays, _ = ImageRaySampler(3, 80, H, W).sample(None, rpose.to(DEV), Kn.to(DEV))
+    r = NeRFRenderer(n_coarse=K, lindisp=True, hard_alpha_cap=True)
+    r.z_jitter = u.to(DEV)
+    with torch.no_grad():
+        c = r.bind_parallel(net).eval()(rays, want_weights=True, want_alphas=True)["coarse"]
+    w2c = torch.inverse(pose)
+    ref = O.render(rays[0].cpu(), u, grid, w2c[:, 0], Kn[:, 0], images * 0.5 + 0.5, w2c, Kn,
+                   W_in, b_in, W_out, b_out, sb=1, hard_alpha_cap=True)
+    check_lowp(c, ref, precision)
+    assert torch.equal(c["invalid"].cpu(), ref["invalid"])
+    assert float((c["alphas"].cpu() - ref["alphas"]).abs().max()) <= 2e-3

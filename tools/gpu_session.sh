@@ -10,7 +10,9 @@
 #   smoke                __graft_entry__.smoke()
 #   bench:CFG[:ARGS]     python bench.py --config CFG ARGS (',' for spaces)
 #   prof:CFG[:ARGS]      rocprofv3 --kernel-trace --stats of a short bench run
-#   pmc:CFG:COUNTERS     one rocprofv3 --pmc pass (COUNTERS ',' separated, within one block's limit)
+#   pmc:CFG:COUNTERS[:ARGS] one rocprofv3 --pmc pass (COUNTERS ',' separated, within one
+#                        block's limit; ARGS: extra bench.py arguments, ',' for spaces)
+#   env:VAR=VALUE        export VAR for the following steps (env:VAR= unsets it)
 #   ab:CFG:VARIANT:REPS  interleaved bench runs of the shipped library and
 #                        scenedino_amd/variants/VARIANT.so (tools/build_variant.py)
 #   py:SCRIPT[:ARGS]     python SCRIPT ARGS (a GPU tool under tools/)
@@ -56,7 +58,7 @@ for step in "$@"; do
     pmc)
       d=$O/pmc_${a1}$n
       t 180 rocprofv3 --kernel-trace --pmc ${a2//,/ } -d $d -o run --output-format csv -- \
-        python3 bench.py --config $a1 --steps 3 --warmup 1 --no-cpu-baseline --no-end-to-end > $d.log 2>&1 \
+        python3 bench.py --config $a1 --steps 3 --warmup 1 --no-cpu-baseline --no-end-to-end ${a3//,/ } > $d.log 2>&1 \
         || { tail -20 $d.log; exit 6; }
       echo "pmc $a1 $a2 -> $d" ;;
     ab)
@@ -68,6 +70,9 @@ for step in "$@"; do
           python3 -c "import json,sys; d=json.loads([l for l in open('$f') if l.startswith('{')][-1]); print('ab $a1 $v', round(d['ms_per_step'],4))"
         done
       done ;;
+    env)
+      v=${step#env:}; if [ -z "${v#*=}" ]; then unset "${v%%=*}"; else export "$v"; fi
+      echo "env $v" ;;
     py)
       f=$O/py$n.log
       t 400 python -u $a1 ${a2//,/ } > $f 2>&1 || { tail -30 $f; exit 8; }
