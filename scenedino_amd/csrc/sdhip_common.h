@@ -8,6 +8,21 @@
 
 #include "../../include/sdhip.h"
 
+#include <mutex>
+#include <unordered_map>
+
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per kernel (and on growth), not per
+// launch: a host call on every launch of the latency-bound eager paths otherwise
+static inline void sd_lds_attr(const void *kern, int bytes) {
+    static std::mutex mu;
+    static std::unordered_map<const void *, int> set;
+    std::lock_guard<std::mutex> g(mu);
+    auto it = set.find(kern);
+    if (it != set.end() && it->second >= bytes) return;
+    (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    set[kern] = bytes;
+}
+
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 typedef __attribute__((ext_vector_type(4))) float f32x4;

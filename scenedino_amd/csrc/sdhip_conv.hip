@@ -686,7 +686,7 @@ int sd_conv_big_try(const sd_gemm_args *args, void *stream) {
         if (t256 < ncu * 15 / 8 && g.OW >= 32 && htiles(32, 128) >= ncu * 7 / 8) tw = 32, hbn = 128;
         if (tw) {
             auto hgo = [&](auto kern, int lds) {
-                (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+                sd_lds_attr((const void *)kern, lds);
                 hipLaunchKernelGGL(kern, dim3((unsigned)(htiles(tw, hbn) / (g.N / hbn)), (unsigned)(g.N / hbn)),
                                    dim3(512), lds, s, g);
             };
@@ -718,7 +718,7 @@ int sd_conv_big_try(const sd_gemm_args *args, void *stream) {
     else if (tiles(128, 64) >= ncu * 7 / 8) bm = 128, bn = 64;
     else return 0;
     auto go = [&](auto kern, int lds) {
-        (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        sd_lds_attr((const void *)kern, lds);
         hipLaunchKernelGGL(kern, dim3((unsigned)((g.M + bm - 1) / bm), (unsigned)(g.N / bn)), dim3(512), lds, s, g);
     };
 #define CV_K(BM_, BN_, E, C, R, RS_) go(k_conv_big<BM_, BN_, E, C, R, RS_>, cv_lds_bytes<BM_, BN_, E == SD_EPI_F32 || RS_>())

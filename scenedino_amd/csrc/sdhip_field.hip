@@ -943,8 +943,7 @@ static int sd_launch(KernT kern, int64_t work_waves, const LdsPlan &pl, hipStrea
                      const ArgT &a, const sd_mlp &m) {
     int64_t nblk = (work_waves + WG<P>::W - 1) / WG<P>::W;
     if (nblk > sd_num_cus()) nblk = sd_num_cus();
-    (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
+    sd_lds_attr((const void *)kern, 160 * 1024);
     hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(WG<P>::T), pl.total, s, a, m, pl);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {

@@ -486,8 +486,7 @@ static int ml_launch(K kern, const sd_mlp_train_args *a, int lds_bytes, hipStrea
         sd_set_error("sd_mlp_train: packed weights exceed the 160 KiB LDS");
         return -1;
     }
-    (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
+    sd_lds_attr((const void *)kern, 160 * 1024);
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess)
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);

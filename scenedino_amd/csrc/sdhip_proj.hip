@@ -905,8 +905,7 @@ k_head_hc(const float *__restrict__ work, int64_t R, const sd_head m, float *__r
 template <typename KernT>
 static int sd_launch_proj(KernT kern, int64_t work_waves, int lds_bytes, hipStream_t s,
                           int64_t &nblk, int wg = SD_PWG) {
-    (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              lds_bytes);
+    sd_lds_attr((const void *)kern, lds_bytes);
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, wg, lds_bytes) !=
             hipSuccess || per_cu <= 0)
@@ -949,7 +948,7 @@ static int sd_project_any(const float *grid, int64_t B, int64_t Hf, int64_t Wf, 
         nblk = sd_num_cus();
         if (nblk > nch) nblk = nch;
         auto go = [&](auto kern) {
-            (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, PJ_LDS);
+            sd_lds_attr((const void *)kern, PJ_LDS);
             hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(256), PJ_LDS, s, grid, B * HW, *m,
                                (uint32_t *)out);
         };

@@ -1021,7 +1021,7 @@ extern "C" int sd_render_tile_launch(const sd_render_args *a, const sd_head *m, 
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
         ncu = 256;
     auto go = [&](auto kern) {
-        (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+        sd_lds_attr((const void *)kern, lds_bytes);
         hipLaunchKernelGGL(kern, dim3((unsigned)ncu), dim3(64 * nw), lds_bytes, s, sa);
     };
     const bool zin = a->z != nullptr;

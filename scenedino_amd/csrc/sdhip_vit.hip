@@ -163,7 +163,7 @@ __device__ __forceinline__ void vt_ln_tail(const sd_gemm_args &g, const VtLnTail
     __syncthreads();
     uint32_t *flag = (uint32_t *)smem;
     if (tid == 0)
-        *flag = __hip_atomic_fetch_add(lt.cnt + blockIdx.y, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+        *flag = __hip_atomic_fetch_add(lt.cnt + blockIdx.y, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
                 gridDim.x - 1;
     __syncthreads();
     if (!*flag) return;  // workgroup-uniform
@@ -563,7 +563,7 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g, float *__restrict_
             __syncthreads();
             uint32_t *flag = (uint32_t *)smem;
             if (tid == 0)
-                *flag = __hip_atomic_fetch_add(sk_cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                *flag = __hip_atomic_fetch_add(sk_cnt + tile, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
                         (uint32_t)(nzs - 1);
             __syncthreads();
             if (!*flag) return;  // workgroup-uniform
@@ -1726,7 +1726,7 @@ static void vt_launch_gemm(const sd_gemm_args &g, hipStream_t s, int ksplit = 1,
     constexpr int ep = BM * (BN + 8) * 4;  // the widest staged epilogue tile (k_gemm's OST)
     const int lds = vt_ring_tile(BM) ? (vt_ring_bytes<BM, BN, BK>() > ep ? vt_ring_bytes<BM, BN, BK>() : ep) : 0;
     auto go = [&](auto kern) {
-        if (lds) (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        if (lds) sd_lds_attr((const void *)kern, lds);
         hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, g, w.slab, w.cnt, lt);
     };
     switch (g.epi) {

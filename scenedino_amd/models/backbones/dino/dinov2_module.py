@@ -176,6 +176,10 @@ class DINOv2Module(nn.Module):
         # the side streams' full-chip convolutions hold every CU's LDS and delay the
         # latency-bound ViT launches on the critical path
         self.overlap_levels = os.environ.get("SCENEDINO_AMD_DPT_OVERLAP", "0") == "1"
+        if self.overlap_levels and int(os.environ.get("SD_SPLITK_WG", "0") or 0) > 0:
+            # the cross-workgroup split-K tiles share one ticket / partial workspace per device:
+            # split launches on the side streams and on the main stream would corrupt it
+            raise ValueError("SCENEDINO_AMD_DPT_OVERLAP=1 and SD_SPLITK_WG>0 cannot be combined")
         self._side = None
 
     # -- prediction pass --------------------------------------------------------
@@ -195,6 +199,10 @@ class DINOv2Module(nn.Module):
             # soon as their token grids exist, overlapping the later ViT blocks (latency-bound
             # 481-token launches that leave most CUs idle); joined before the fusion chain
             main = torch.cuda.current_stream(x.device)
+            # (re)pack the decoder weights on the main stream first: the side streams only
+            # wait on main, so a pack made inside the first level front (side stream 0) would
+            # race the other fronts' reads
+            self.decoder._pack()
             if self._side is None or self._side[0] != x.device:
                 self._side = (x.device, [torch.cuda.Stream(device=x.device) for _ in range(3)])
             side = self._side[1]

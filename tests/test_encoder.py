@@ -166,6 +166,25 @@ def test_dpt_level_fronts_on_side_streams_match_one_stream(gpu):
             assert torch.equal(a, b), key
 
 
+@pytest.mark.gpu
+def test_dpt_level_fronts_cold_pack_with_overlap(gpu):
+    """The overlapped level fronts starting from a cold weight pack (the first forward of a
+    fresh module with overlap on) equal the one-stream order: the pack is made on the main
+    stream before any side stream starts."""
+    xs = [(torch.rand(1, 3, 64, 160, generator=torch.Generator().manual_seed(25 + i)) * 2 - 1).to(gpu)
+          for i in range(2)]
+    with torch.no_grad():
+        m1 = make(seed=26).to(gpu)
+        m1.overlap_levels, m1.use_graph = True, False
+        a = [m1(x)[0].clone() for x in xs]
+        m2 = make(seed=26).to(gpu)
+        m2.overlap_levels, m2.use_graph = False, False
+        b = [m2(x)[0].clone() for x in xs]
+    torch.cuda.synchronize()
+    for u, v in zip(a, b):
+        assert torch.equal(u, v)
+
+
 MODEL_CONF = {"arch": "BTSNet", "predict_dino": True, "dino_dims": 64, "learn_empty": False,
               "code_mode": "z", "inv_z": True, "z_near": 3, "z_far": 80, "sample_color": True,
               "encoder": CONF, "code": {"num_freqs": 6, "freq_factor": 1.5, "include_input": True},
