@@ -117,6 +117,21 @@ __device__ __forceinline__ float sd_z_sample(float near, float far, I K, I k, fl
     return near * (1.0f - t) + far * t;
 }
 
+// The same stratified sample for the counter-RNG jitter (perf mode: sd_sample_z with
+// u == NULL and the render kernels' in-kernel depths, which no reference value pins --
+// any uniform stream is a valid draw): hardware reciprocals instead of the three IEEE
+// divisions of the reference recipe (within 1-2 ulp of it).
+template <typename I>
+__device__ __forceinline__ float sd_z_sample_rng(float near, float far, I K, I k, float uu,
+                                                 float step, float t_end, int lindisp) {
+    const float t = sd_linspace_at(0.0f, t_end, K, k) + uu * step;
+    if (lindisp) {
+        const float a = __builtin_amdgcn_rcpf(near) * (1.0f - t);
+        return __builtin_amdgcn_rcpf(fmaf(__builtin_amdgcn_rcpf(far), t, a));
+    }
+    return near * (1.0f - t) + far * t;
+}
+
 // Counter-based uniform [0,1) (24-bit mantissa) for perf-mode jitter: murmur3's 32-bit
 // finaliser over the counter, keyed by both halves of the 64-bit seed (the reference draws
 // torch.rand_like, nerf.py:134; any uniform stream is a valid stratified sample).

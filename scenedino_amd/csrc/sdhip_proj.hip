@@ -493,7 +493,7 @@ k_render_proj(const sd_render_args a, const sd_head m, const int32_t *__restrict
 #pragma unroll
             for (int p = 0; p < MAXP; ++p) {
                 const int k = min(64 * p + lane, K - 1);
-                zo[p] = sd_z_sample(near, far, K, k, sd_uniform(a.z_seed, base + k), zstep, zend,
+                zo[p] = sd_z_sample_rng(near, far, K, k, sd_uniform(a.z_seed, base + k), zstep, zend,
                                     a.z_lindisp);
             }
         }

@@ -102,8 +102,10 @@ __global__ void __launch_bounds__(256) k_sample_z(const float *__restrict__ rays
     if (gid >= R * K) return;
     int64_t r = gid / K, k = gid - r * K;
     float near = rays[r * ray_dim + 6], far = rays[r * ray_dim + 7];
-    float uu = u ? u[gid] : sd_uniform(seed, offset + (uint64_t)gid);
-    float zz = sd_z_sample(near, far, K, k, uu, step, t_end, lindisp);
+    // (u given: the reference's recipe, bit-exact; counter RNG: the render kernels' fast form)
+    float zz = u ? sd_z_sample(near, far, K, k, u[gid], step, t_end, lindisp)
+                 : sd_z_sample_rng(near, far, K, k, sd_uniform(seed, offset + (uint64_t)gid), step,
+                                   t_end, lindisp);
     z[gid] = zz;
 }
 

@@ -305,7 +305,7 @@ k_render_tile(const st_args sa) {
             for (int p = 0; p < ST_MAXP; ++p) {
                 if (64 * p >= KW) break;  // wave-uniform: KW <= 64 draws one sample per lane
                 const int k = RPW == 1 ? min(64 * p + lane, K - 1) : kl;
-                zo[p] = sd_z_sample(near, far, K, k, sd_uniform(a.z_seed, base + k), zstep, zend,
+                zo[p] = sd_z_sample_rng(near, far, K, k, sd_uniform(a.z_seed, base + k), zstep, zend,
                                     a.z_lindisp);
             }
         }
