@@ -72,9 +72,12 @@ extern "C" int sd_tile_prof(unsigned long long *out, int reset) {
 #define ST_WAIT_FIX 1       // compiler-visible vmcnt(0) after the register-resident weight loads
 #endif
 #ifndef ST_HEAD_PRE
-#define ST_HEAD_PRE 2       // 2: the previous group's DINO head before the ray pass (its W_dino
-                            // loads' wait then does not cover the pass's colour loads); 1: its
-                            // first W_dino tile preloaded across the pass (spills); 0: after
+#define ST_HEAD_PRE 3       // 3: the previous group's DINO head before the ray pass, its first
+                            // W_dino tile loaded at the end of the step before (the loads land
+                            // during the closing vmcnt(0) wait for the tile DMA, and the 16
+                            // VGPRs are live only across the step boundary, not the items);
+                            // 2: the head before the ray pass, W_dino loaded inside it; 1: the
+                            // first tile preloaded across the pass (spills); 0: after the pass
 #endif
 #ifndef ST_HC16
 #define ST_HC16 1           // hidden-space compositing by v_pk_fma_f16 into packed f16 per-lane
@@ -220,6 +223,9 @@ __device__ __forceinline__ uint2 st_tr(uint32_t addr) {
 template <int P, bool ZIN, int NW, int RPW>
 __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4)))
 k_render_tile(const st_args sa) {
+    // the head's W_dino prefetch across the step boundary (mode 3) costs 16-20 VGPRs: the
+    // two-rays-per-wave body (245 VGPRs) would spill, so it loads them inside the head
+    constexpr int HPRE = (RPW == 2 && ST_HEAD_PRE == 3) ? 2 : ST_HEAD_PRE;
     constexpr int ST_WAVES = NW;
     constexpr int GR = NW * RPW;  // rays per group
     constexpr int ST_L_HS = st_l_hs(NW), ST_L_WS = st_l_ws(NW, RPW), ST_L_RAY = st_l_ray(NW, RPW),
@@ -538,7 +544,7 @@ k_render_tile(const st_args sa) {
     };
 
     // ---- DINO head of one group (hsum of its NW rays in LDS) --------------------------
-    // W_dino fragments of tile dt (4 x 16 B per lane).  ST_HEAD_PRE: the wave's first tile is
+    // W_dino fragments of tile dt (4 x 16 B per lane).  HPRE: the wave's first tile is
     // loaded before the step's ray pass, so the head's wait for it does not also wait for the
     // ray pass's colour loads (issued later, consumed after item 0)
     typedef typename Th::Frag HFrag;
@@ -563,7 +569,7 @@ k_render_tile(const st_args sa) {
         const bool store = j < GR && ray < R;
         for (int dt = wave; dt < ndt; dt += ST_WAVES) {
             HFrag wl[4];
-            if (ST_HEAD_PRE == 1 && dt == wave) {
+            if ((HPRE == 1 || HPRE == 3) && dt == wave) {
 #pragma unroll
                 for (int s = 0; s < 4; ++s) wl[s] = w0[s];
             } else {
@@ -629,6 +635,7 @@ k_render_tile(const st_args sa) {
     __syncthreads();
 
     int prev_grp = -1, prev_ok = 0;
+    HFrag hwn[4];  // HPRE 3: W_dino tile `wave` for the next step's head
 #if ST_PROF
 #pragma unroll
     for (int i = 0; i < 19; ++i) pacc[i] = 0;
@@ -786,13 +793,14 @@ k_render_tile(const st_args sa) {
 
         // item 0 with the next ray's pass and the previous group's head
         HFrag hw[4];
-        if (ST_HEAD_PRE == 1 && prev_ok && wave < ndt) head_w(wave, hw);
-        if (ST_HEAD_PRE == 2 && prev_ok) head(prev_grp, hw);
-        if (ST_HEAD_PRE == 2) ST_T(1);
+        if (HPRE == 1 && prev_ok && wave < ndt) head_w(wave, hw);
+        if (HPRE == 2 && prev_ok) head(prev_grp, hw);
+        if (HPRE == 3 && prev_ok) head(prev_grp, hwn);
+        if (HPRE >= 2) ST_T(1);
         if (has_next) ray_pass(nray, buf ^ 1, buf ^ 1);
         ST_T(0);
-        if (ST_HEAD_PRE != 2 && prev_ok) head(prev_grp, hw);
-        if (ST_HEAD_PRE != 2) ST_T(1);
+        if (HPRE < 2 && prev_ok) head(prev_grp, hw);
+        if (HPRE < 2) ST_T(1);
         IState s0;
         if (cur.ok && ray < R) itemA(0, s0);
         ST_T(2);
@@ -938,15 +946,20 @@ k_render_tile(const st_args sa) {
         sbi = nsbi;
         cur = nxt;
         if (n + 2 < nsteps) ray_fetch(GR * (ngrp + nwg) + RPW * wave, buf);  // rays of step n + 2
+        if (HPRE == 3 && prev_ok && wave < ndt) head_w(wave, hwn);  // the next head's W_dino
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed
         ST_T(8);
         st_barrier_lds();  // Y: next tile complete; hsum of this group written
         ST_T(9);
     }
     if (prev_ok) {
-        HFrag hw[4];
-        if (ST_HEAD_PRE == 1 && wave < ndt) head_w(wave, hw);
-        head(prev_grp, hw);
+        if (HPRE == 1) {
+            HFrag hw[4];
+            if (wave < ndt) head_w(wave, hw);
+            head(prev_grp, hw);
+        } else {
+            head(prev_grp, hwn);  // (mode 3: loaded at the end of the last step)
+        }
     }
 #if ST_PROF
     if (lane < 19) {
