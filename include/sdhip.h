@@ -535,6 +535,26 @@ typedef struct sd_wgrad_args {
 
 int sd_wgrad(const sd_wgrad_args *args, void *stream);
 
+/* Both weight gradients of the training MLP in one pass over the rows sd_mlp_train_fwd /
+ * _bwd leave (the Linear backward of resnetfc.py:135-203 under autocast): dW1 = dh^T x
+ * (x: ldx-strided rows, kx = d_in + 1 used columns, the ones column giving db_in) and
+ * dW_o = dy^T [h | 1] (dy: (N, 72) = [d dino | d out_0 | 0..], h: (N, 136)).  The outputs
+ * are the f32 gradients in the parameters' layout: dw_in (128, kx - 1), db_in (128),
+ * dw_out (1 + D, 128) and db_out (1 + D) with row 0 = out_0 (sigma), rows 1..D = dino --
+ * resnetfc.py's lin_out rows.  work: sd_mlp_train_wgrad_work(nparts) f32 of scratch for
+ * the nparts partial sums (deterministic: fixed summation order).  kx <= 320, kx % 8 == 0,
+ * D <= 64, D % 8 == 0. */
+typedef struct sd_mlp_wgrad_args {
+    const void *x, *dh, *dy, *h;
+    int64_t N;
+    int32_t ldx, kx, D, dtype, nparts, pad;
+    float *work;
+    float *dw_in, *db_in, *dw_out, *db_out;
+} sd_mlp_wgrad_args;
+
+int64_t sd_mlp_train_wgrad_work(int32_t nparts);
+int sd_mlp_train_wgrad(const sd_mlp_wgrad_args *args, void *stream);
+
 int sd_mlp_train_fwd(const sd_mlp_train_args *args, void *stream);
 int sd_mlp_train_bwd(const sd_mlp_train_args *args, void *stream);
 

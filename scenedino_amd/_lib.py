@@ -133,6 +133,13 @@ class SdWgradArgs(ctypes.Structure):
                 ("Ma", _i32), ("Nb", _i32), ("dtype", _i32), ("nparts", _i32), ("part", _vp)]
 
 
+class SdMlpWgradArgs(ctypes.Structure):
+    """sd_mlp_wgrad_args (include/sdhip.h): both training-MLP weight gradients."""
+    _fields_ = [("x", _vp), ("dh", _vp), ("dy", _vp), ("h", _vp), ("N", _i64), ("ldx", _i32),
+                ("kx", _i32), ("D", _i32), ("dtype", _i32), ("nparts", _i32), ("pad", _i32),
+                ("work", _vp), ("dw_in", _vp), ("db_in", _vp), ("dw_out", _vp), ("db_out", _vp)]
+
+
 class SdSalienceArgs(ctypes.Structure):
     """sd_salience_args (include/sdhip.h): PatchSalienceDownsampler forward / backward."""
     _fields_ = [
@@ -198,6 +205,8 @@ SIGNATURES = {
     "sd_mlp_train_fwd": [ctypes.POINTER(SdMlpTrainArgs), _vp],
     "sd_mlp_train_bwd": [ctypes.POINTER(SdMlpTrainArgs), _vp],
     "sd_wgrad": [ctypes.POINTER(SdWgradArgs), _vp],
+    "sd_mlp_train_wgrad": [ctypes.POINTER(SdMlpWgradArgs), _vp],
+    "sd_mlp_train_wgrad_work": [_i32],
     "sd_salience_fwd": [ctypes.POINTER(SdSalienceArgs), _vp],
     "sd_salience_bwd": [ctypes.POINTER(SdSalienceArgs), _vp],
     "sd_gemm": [ctypes.POINTER(SdGemmArgs), _vp],
@@ -231,6 +240,7 @@ def load(path: str = LIB_PATH):
         fn.restype = ctypes.c_int
     lib.sd_last_error.restype = ctypes.c_char_p
     lib.sd_render_proj_work_bytes.restype = ctypes.c_int64
+    lib.sd_mlp_train_wgrad_work.restype = ctypes.c_int64
     if lib.sd_abi_version() != ABI_VERSION:
         raise RuntimeError("scenedino_amd: libsdhip.so ABI version mismatch; rebuild it")
     _lib = lib
@@ -300,6 +310,29 @@ def wgrad(a, b, Ma, Nb, nparts=None):
                     part=part.data_ptr())
     _check(lib.sd_wgrad(ctypes.byref(g), stream_of(a)), "sd_wgrad")
     return part.sum(0)[:Ma, :Nb]
+
+
+def mlp_train_wgrad(x, dh, dy, h, kx, D, nparts=None):
+    """Both weight gradients of the training MLP (sd_mlp_train_wgrad) from the 16-bit rows
+    of sd_mlp_train_fwd / _bwd: (dw_in (128, kx - 1), db_in (128), dw_out (1 + D, 128),
+    db_out (1 + D)) f32, lin_out rows in the parameter order (out_0 first)."""
+    lib = load()
+    N, ldx = x.shape
+    dev = x.device
+    if nparts is None:  # one workgroup per CU
+        nparts = max(1, min(torch.cuda.get_device_properties(dev).multi_processor_count,
+                            (N + 31) // 32))
+    work = torch.empty(int(lib.sd_mlp_train_wgrad_work(nparts)), device=dev)
+    dw_in = torch.empty(128, kx - 1, device=dev)
+    db_in = torch.empty(128, device=dev)
+    dw_out = torch.empty(1 + D, 128, device=dev)
+    db_out = torch.empty(1 + D, device=dev)
+    g = SdMlpWgradArgs(x=x.data_ptr(), dh=dh.data_ptr(), dy=dy.data_ptr(), h=h.data_ptr(), N=N,
+                       ldx=ldx, kx=kx, D=D, dtype=SD_OF_TORCH[x.dtype], nparts=nparts,
+                       work=work.data_ptr(), dw_in=dw_in.data_ptr(), db_in=db_in.data_ptr(),
+                       dw_out=dw_out.data_ptr(), db_out=db_out.data_ptr())
+    _check(lib.sd_mlp_train_wgrad(ctypes.byref(g), stream_of(x)), "sd_mlp_train_wgrad")
+    return dw_in, db_in, dw_out, db_out
 
 
 def salience_fwd(args: SdSalienceArgs, ref_tensor):

@@ -260,12 +260,10 @@ class FieldMLPFused(torch.autograd.Function):
             a.lddx, a.dx_dtype = dx.shape[1], dt if dx16 else _lib.SD_F32
             a.dx = dx.data_ptr()
         _timed("mlp_bwd", lambda: _lib.mlp_train_bwd(a, x_aug))
-        dW1 = _lib.wgrad(dh, x_aug, 128, d_in + 1)   # (128, d_in + 1): [dW_in | db_in]
-        dWo = _lib.wgrad(dy, h, 72, 136)             # rows dino 0..D-1, out_0; col 128 bias
-        dw_out = torch.cat((dWo[D:D + 1, :128], dWo[:D, :128]), 0)
-        db_out = torch.cat((dWo[D:D + 1, 128], dWo[:D, 128]), 0)
-        return (dx, dW1[:, :d_in].to(pdt).contiguous(), dW1[:, d_in].to(pdt).contiguous(),
-                dw_out.to(pdt).contiguous(), db_out.to(pdt).contiguous())
+        # dW1 = dH^T X ([dW_in | db_in]) and dW_o = dY^T [H | 1] in one pass over the rows,
+        # written in the parameter layout
+        grads = _lib.mlp_train_wgrad(x_aug, dh, dy, h, d_in + 1, D)
+        return (dx,) + tuple(t if t.dtype == pdt else t.to(pdt) for t in grads)
 
 
 # 16-bit dX rows from the fused MLP backward into the gather's scatter (the autocast

@@ -179,19 +179,22 @@ __global__ void __launch_bounds__(ML_WAVES * 64) k_mlp_fwd(const sd_mlp_train_ar
 }
 
 // ---------------------------------------------------------------------------
-// Fused grid_sample backward of k_mlp_bwd (dgrid != NULL; bts.py:299-309).  The wave's 32
-// points split into runs of consecutive points with the same frame and taps (a ray's
-// samples: one run per ray when the render view is the encoder view).  The scatter is a
-// product, G = S dX: S (rows = run x tap, columns = the 32 points) holds each point's
-// bilinear weight of that tap in its run's rows, and dX (32 points x 32 channels) is the
-// accumulator tile of dX = dH W_in re-used in registers as the B operand -- rounded to the
-// autocast dtype, the dtype of the reference's Linear input gradient.  S enters as hi + lo
-// 16-bit parts (the weights keep >= 16 bits).  Each nonzero G element is one f32 atomic add
-// into the grid gradient: the atomics of the run-summing k_field_gather_bwd, without the
-// dX rows' HBM round trip.  Per-wave LDS tables: w[4][32] f32, run[32], off[32][4] (the
-// element offsets of a run's four tap rows in dgrid).
+// Fused grid_sample backward of k_mlp_bwd (dgrid != NULL; bts.py:299-309).  The scatter is
+// a product, G = S dX: S (rows = the distinct texels the wave's 32 points tap with a nonzero
+// bilinear weight, columns = the points) holds at (texel, point) the sum of the point's
+// weights of its taps on that texel, and dX (32 points x 32 channels) is the accumulator
+// tile of dX = dH W_in re-used in registers as the B operand -- rounded to the autocast
+// dtype, the dtype of the reference's Linear input gradient.  S enters as hi + lo 16-bit
+// parts (the weights keep >= 16 bits).  Each nonzero G element is one f32 atomic add into
+// the grid gradient.  One row per distinct texel, not per (run of equal tap quads, tap):
+// a ray's samples straddle texel borders through rounding (encoder view) or walk along an
+// epipolar line (other views), and consecutive quads share texels -- 3.5 rows per wave
+// instead of 20.6 on the bench's encoder-view rays (the float atomics run at ~1.3 TB/s of
+// added bytes chip-wide, microarch guide: they were most of this kernel's time).
+// Per-wave LDS tables: w[32][4] f32 (each point's four tap weights), row[32] (the S row of
+// each tap, one byte each, 0xff = none), off[128] (each row's element offset in dgrid).
 // ---------------------------------------------------------------------------
-#define ML_SCR_WORDS (4 * 32 + 32 + 32 * 4)
+#define ML_SCR_WORDS (4 * 32 + 32 + 128)
 #ifndef ML_DIAG_NO_ATOMICS
 #define ML_DIAG_NO_ATOMICS 0  // diagnostic builds only (tools/build_variant.py): drop the grid-gradient atomics
 #endif
@@ -203,73 +206,82 @@ __device__ __forceinline__ void ml_wave_sync() {
 }
 
 // tables of the wave's tile (at the tile start, while the dY loads are in flight);
-// returns the number of runs
+// returns the number of S rows (distinct texels, <= 128)
 __device__ __forceinline__ int ml_scatter_tables(const sd_mlp_train_args &a, int *scr,
                                                  int64_t pt, bool valid, int lane) {
     const int h = lane >> 5, r = lane & 31;
     float *sw = (float *)scr;
-    int *srun = scr + 128, *soff = scr + 160;
-    // geometry of point pt (both halves; the forward gather's sd_point_geo, same taps)
-    int gi[4] = {0, 0, 0, 0}, gb = -1;
-    float gw[4] = {0.f, 0.f, 0.f, 0.f};
+    uint16_t *srow = (uint16_t *)(scr + 128);
+    int *soff = scr + 160;
+    // geometry of point pt (both halves; the forward gather's sd_point_geo, same taps);
+    // lane half h owns taps 2 h and 2 h + 1
+    int key[2] = {-1, -1};
+    float gw[2] = {0.f, 0.f};
     if (valid) {
         const int64_t b = pt / a.P;
         const PointGeo geo = sd_point_geo(a.cam_f + b * SD_CAM_WORDS, a.xyz[pt * 3],
                                           a.xyz[pt * 3 + 1], a.xyz[pt * 3 + 2], a.Wf, a.Hf);
-        gi[0] = geo.t.i00; gi[1] = geo.t.i01; gi[2] = geo.t.i10; gi[3] = geo.t.i11;
-        gw[0] = geo.t.w00; gw[1] = geo.t.w01; gw[2] = geo.t.w10; gw[3] = geo.t.w11;
-        gb = (int)b;
+        const int base = (int)b * a.Hf * a.Wf;
+        const int i0 = h ? geo.t.i10 : geo.t.i00, i1 = h ? geo.t.i11 : geo.t.i01;
+        gw[0] = h ? geo.t.w10 : geo.t.w00;
+        gw[1] = h ? geo.t.w11 : geo.t.w01;
+        key[0] = gw[0] != 0.f ? base + i0 : -1;  // a zero weight adds nothing: no row
+        key[1] = gw[1] != 0.f ? base + i1 : -1;
     }
-    // a point opens a run unless it has the previous point's frame and taps
-    const int src = ((lane - 1) & 63) * 4;
-    const int pb = __builtin_amdgcn_ds_bpermute(src, gb);
-    int pi[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) pi[t] = __builtin_amdgcn_ds_bpermute(src, gi[t]);
-    const bool open = valid && (r == 0 || pb != gb || pi[0] != gi[0] || pi[1] != gi[1] ||
-                                pi[2] != gi[2] || pi[3] != gi[3]);
-    const uint64_t om = __ballot(open) & 0xffffffffull;
-    const int run = valid ? __builtin_popcountll(om & ((2ull << r) - 1)) - 1 : -1;
+    // rows in order of first appearance: each pass takes the first unassigned key of the
+    // wave and gives every equal key its row (passes = distinct texels)
+    int row[2] = {-1, -1};
+    int nrow = 0;
     ml_wave_sync();  // the previous tile's table reads are done
-    if (h == 0) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) sw[32 * t + r] = gw[t];
-        srun[r] = run;
-        if (open)
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-                soff[4 * run + t] = (int)(((int64_t)gb * a.Hf * a.Wf + gi[t]) * a.C);
+    for (;;) {
+        const uint64_t m0 = __ballot(key[0] >= 0 && row[0] < 0);
+        const uint64_t m1 = __ballot(key[1] >= 0 && row[1] < 0);
+        if (!(m0 | m1)) break;
+        const int kv = m0 ? __builtin_amdgcn_readlane(key[0], __builtin_ctzll(m0))
+                          : __builtin_amdgcn_readlane(key[1], __builtin_ctzll(m1));
+        if (key[0] == kv) row[0] = nrow;
+        if (key[1] == kv) row[1] = nrow;
+        if (lane == 0) soff[nrow] = kv * a.C;
+        ++nrow;
     }
+    *(float2 *)(sw + 4 * r + 2 * h) = make_float2(gw[0], gw[1]);
+    srow[2 * r + h] = (uint16_t)((row[0] & 0xff) | (row[1] & 0xff) << 8);
     ml_wave_sync();
-    return __builtin_popcountll(om);
+    return nrow;
 }
 
 // S fragments of row tile mt (A operand in the k order kappa of ml_frag: k-step s, lane
-// half h, element j = point 16 s + 8 (j >> 2) + 4 h + (j & 3)); row r = run 8 mt + r / 4,
-// tap r % 4
+// half h, element j = point 16 s + 8 (j >> 2) + 4 h + (j & 3)); row 32 mt + r
 template <int P>
 __device__ __forceinline__ void ml_s_frags(const int *scr, int mt, int lane,
                                            typename T16<P>::Frag (&sh)[2],
                                            typename T16<P>::Frag (&sl)[2]) {
     typedef typename T16<P>::E E;
     const int h = lane >> 5, r = lane & 31;
-    const float *sw = (const float *)scr;
-    const int *srun = scr + 128;
-    const int k = 8 * mt + (r >> 2), t = r & 3;
+    const float4 *sw = (const float4 *)scr;
+    const uint32_t *srow = (const uint32_t *)(scr + 128);
+    const uint32_t k = 32 * mt + r;
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
+            // four elements' table reads at a time (all 16 hoisted: 80 live registers, spills)
+            if ((j & 3) == 0) __builtin_amdgcn_sched_barrier(0);
             const int q = 16 * s + 8 * (j >> 2) + 4 * h + (j & 3);
-            const float w = srun[q] == k ? sw[32 * t + q] : 0.f;
+            const float4 w4 = sw[q];
+            const uint32_t rq = srow[q];
+            float w = (rq & 0xffu) == k ? w4.x : 0.f;
+            w += ((rq >> 8) & 0xffu) == k ? w4.y : 0.f;
+            w += ((rq >> 16) & 0xffu) == k ? w4.z : 0.f;
+            w += (rq >> 24) == k ? w4.w : 0.f;
             const E hi = (E)w;
             sh[s][j] = hi;
             sl[s][j] = (E)(w - (float)hi);
         }
 }
 
-// G = S dX for one 32-channel column tile and row tile mt, and its atomics.  The G rows of
-// this lane: run 8 mt + 2 (i >> 2) + h, tap i % 4.
+// G = S dX for one 32-channel column tile and row tile mt, and its atomics.  The G row of
+// this lane's element i: 32 mt + 8 (i >> 2) + 4 h + (i & 3).
 template <int P>
 __device__ __forceinline__ void ml_s_emit(const int *scr, int mt, int nr, int lane,
                                           const typename T16<P>::Frag (&sh)[2],
@@ -288,8 +300,8 @@ __device__ __forceinline__ void ml_s_emit(const int *scr, int mt, int nr, int la
     g = Tr::mma32(sl[1], b1, g);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-        const int kk = 8 * mt + 2 * (i >> 2) + h;
-        if (kk < nr && g[i] != 0.f && !ML_DIAG_NO_ATOMICS) unsafeAtomicAdd(dg + soff[4 * kk + (i & 3)], g[i]);
+        const int kk = 32 * mt + 8 * (i >> 2) + 4 * h + (i & 3);
+        if (kk < nr && g[i] != 0.f && !ML_DIAG_NO_ATOMICS) unsafeAtomicAdd(dg + soff[kk], g[i]);
     }
 }
 
@@ -304,7 +316,7 @@ __device__ __forceinline__ void ml_scatter(const sd_mlp_train_args &a,
     const int r = lane & 31;
     Frag s0h[2], s0l[2];
     ml_s_frags<P>(scr, 0, lane, s0h, s0l);
-    const int nmt = (nr + 7) >> 3;
+    const int nmt = (nr + 31) >> 5;
     const int UC = a.C >> 5;
     for (int u = 0; u < UC; ++u) {
         f32x16 o;
@@ -315,7 +327,7 @@ __device__ __forceinline__ void ml_scatter(const sd_mlp_train_args &a,
         const Frag b0 = ml_frag<P>(o, 0), b1 = ml_frag<P>(o, 1);
         float *dg = a.dgrid + 32 * u + r;
         ml_s_emit<P>(scr, 0, nr, lane, s0h, s0l, b0, b1, dg);
-        for (int mt = 1; mt < nmt; ++mt) {  // more than 8 runs: points off the encoder view
+        for (int mt = 1; mt < nmt; ++mt) {  // more than 32 texels: points off the encoder view
             Frag sh[2], sl[2];
             ml_s_frags<P>(scr, mt, lane, sh, sl);
             ml_s_emit<P>(scr, mt, nr, lane, sh, sl, b0, b1, dg);
@@ -717,6 +729,284 @@ extern "C" int sd_wgrad(const sd_wgrad_args *g, void *stream) {
 #undef WG_CASE
     if (hipGetLastError() != hipSuccess) {
         sd_set_error("sd_wgrad: launch failed");
+        return -2;
+    }
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Both weight gradients of the training MLP in one pass (sd_mlp_train_wgrad): dW1 = dH^T X
+// (128 x kx) and dW_o = dY^T [H | 1] (72 x 136) read each point's four rows once -- two
+// sd_wgrad launches re-read dH for their column split and left 73 MB of partials to a
+// separate torch reduction.  A workgroup (8 waves, one per CU) sums every gridDim-th
+// 32-point chunk.  A chunk's four row blocks (32 rows each, contiguous in HBM) go to LDS
+// by LDS-DMA (global_load_lds_dwordx4: 1 KiB per wave instruction, no staging registers)
+// into padded rows, in a ring of three stages: the DMAs of chunks c + 1 and c + 2 are
+// in flight while chunk c is multiplied, one barrier per chunk.  Each wave multiplies its
+// output tiles from LDS read transposed (ds_read_b64_tr_b16, as k_wgrad): wave w owns dW1
+// row tile w & 3 and column tiles 5 (w >> 2) .. + 4, and dW_o tiles w and w + 8 of its
+// 3 x 5.  Tiles reach past the used columns (X to 320, H to 160, dY to 96 rows) into the
+// rows' zero pads: those output elements are dropped.  Rows past N: the dH / dY rows are
+// zeroed (the stale X / H rows then add 0).  Partials (nparts x 56320 f32) are summed in
+// MW_S splits (k_mw_split) and then across the splits into the parameter layout
+// (k_mw_final).  Algorithmic bytes: N (2 ldx + 256 + 144 + 272) read.
+// ---------------------------------------------------------------------------
+#define MW_S 16                      // splits of the partial sum
+#define MW_KXP 320                   // X columns of the partial (kx, ldx <= 320)
+#define MW_P1 (128 * MW_KXP)         // dW1 partial
+#define MW_P2 (96 * 160)             // dW_o partial (rows 72.. and columns 136.. dropped)
+#define MW_PT (MW_P1 + MW_P2)
+#define MW_RING 3
+#ifndef MW_DIAG
+#define MW_DIAG 0  // diagnostic builds only (tools/build_variant.py): 1 no MFMA, 2 no DMA, 3 no partial stores
+#endif
+// LDS stage: X [32][ldx], dH [32][128], dY [32][72], H [32][136] 16-bit rows at row strides
+// of 64 or 192 B mod 256 (X: 2 ldx rounded up to one, 704 B for ldx 296..320; dH 320, dY
+// 192, H 320): the 4 rows x 64 B of a half-wave's ds_read_b64_tr_b16 fall in 4 disjoint
+// 16-bank groups (rows of 256 / 272 B put all four in the same banks: 4-way conflicts).
+// The pads are never written (zero from the start) and the tiles' reach past the used
+// columns stays inside them.
+__host__ __device__ constexpr int mw_xstride(int ldx) {
+    int s = (2 * ldx + 63) & ~63;
+    while (s % 256 != 64 && s % 256 != 192) s += 64;
+    return s;
+}
+__host__ __device__ constexpr int mw_stage_bytes(int ldx) { return 32 * (mw_xstride(ldx) + 320 + 192 + 320); }
+
+template <int P>
+__global__ void __launch_bounds__(512) k_mlp_wgrad(const sd_mlp_wgrad_args g) {
+    typedef T16<P> Tr;
+    typedef typename Tr::Frag Frag;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: scalar tile choice
+    const int h = lane >> 5;
+    const int sbx = mw_xstride(g.ldx), SZ = mw_stage_bytes(g.ldx);
+    const int oDH = 32 * sbx, oDY = oDH + 32 * 320, oH = oDY + 32 * 192;
+    // zero the ring once (the pads are never written)
+    for (int i = tid; i < MW_RING * SZ / 16; i += 512) ((uint4 *)lds)[i] = uint4{0u, 0u, 0u, 0u};
+    __syncthreads();
+    // this workgroup's chunks of 32 points: blockIdx.x + gridDim.x i, i < nch -- the
+    // workgroups sweep the rows together (contiguous ranges per workgroup put 256 streams
+    // at a 256 KiB stride in dH: the same HBM channels at once, 2.2 TB/s)
+    const int64_t nchunk = (g.N + 31) >> 5;
+    const int nch = blockIdx.x < nchunk ? (int)((nchunk - 1 - blockIdx.x) / gridDim.x + 1) : 0;
+    auto chunk_p0 = [&](int ci) { return ((int64_t)blockIdx.x + (int64_t)gridDim.x * ci) * 32; };
+    // DMA units of a chunk (1 KiB of an LDS block each: X sbx / 32, dH 10, dY 6, H 10); wave
+    // w issues units w, w + 8, ...  Lane l of unit lu fills the block's 16-B granule
+    // 64 lu + l: row gl / G, granule gl % G of the row (a pad past the row's bytes: no load).
+    const int ux = sbx >> 5, nu = ux + 26;
+    const int cw = (nu - wave + 7) >> 3;  // this wave's units per chunk (<= 6)
+    int upk[6];  // per unit: source byte in the chunk's block << 5 | row, or -1
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        const int u = wave + 8 * i;
+        int lu, G, rb;
+        if (u < ux) { lu = u; G = sbx >> 4; rb = 2 * g.ldx; }
+        else if (u < ux + 10) { lu = u - ux; G = 20; rb = 256; }
+        else if (u < ux + 16) { lu = u - ux - 10; G = 12; rb = 144; }
+        else { lu = u - ux - 16; G = 20; rb = 272; }
+        const int gl = 64 * lu + lane, row = gl / G, cg = gl - row * G;
+        upk[i] = (u < nu && 16 * cg < rb) ? (row * rb + 16 * cg) << 5 | row : -1;
+    }
+    // per unit (wave-uniform, resolved once: selected inside the loop, the compiler made the
+    // four row pointers a scratch table and waited vmcnt(0) on its load before every DMA,
+    // draining the ring): source rows, bytes per row, LDS destination in the stage
+    const uint32_t lds0 = (uint32_t)(uintptr_t)lds;
+    uint64_t ubase[6];
+    int urb[6];
+    uint32_t udst[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        const int u = wave + 8 * i;
+        uint64_t b;
+        int rb, lu, off;
+        if (u < ux) { b = (uint64_t)g.x; rb = 2 * g.ldx; lu = u; off = 0; }
+        else if (u < ux + 10) { b = (uint64_t)g.dh; rb = 256; lu = u - ux; off = oDH; }
+        else if (u < ux + 16) { b = (uint64_t)g.dy; rb = 144; lu = u - ux - 10; off = oDY; }
+        else { b = (uint64_t)g.h; rb = 272; lu = u - ux - 16; off = oH; }
+        // (uint32_t first: a sign-extended low word set the high bits -- a faulting address)
+        ubase[i] = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b) |
+                   (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(b >> 32)) << 32;
+        urb[i] = __builtin_amdgcn_readfirstlane(rb);
+        udst[i] = (uint32_t)__builtin_amdgcn_readfirstlane((int)(lds0 + off + 1024 * lu));
+    }
+    auto dma = [&](int ci) {  // chunk ci (< nch) into stage ci % 3
+        const int64_t p0 = chunk_p0(ci);
+        const int nv = g.N - p0 < 32 ? (int)(g.N - p0) : 32;  // rows present
+        const uint32_t st = (uint32_t)((ci % MW_RING) * SZ);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            if (i >= cw) break;
+            if (upk[i] >= 0 && (upk[i] & 31) < nv && MW_DIAG != 2)
+                sd_dma16((const uint8_t *)ubase[i] + p0 * urb[i] + (upk[i] >> 5), udst[i] + st);
+        }
+    };
+    // transposed-read lane address (k_wgrad): group G = lane >> 4, lane 4 q + pp of it
+    const int G = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+    const int kb = 8 * (G >> 1), cbase = 16 * (G & 1) + 4 * pp;
+    const int rt1 = wave & 3, ct1 = 5 * (wave >> 2);
+    const int t2a = wave, t2b = wave + 8;  // dW_o tiles (row t / 5, column t % 5)
+    const bool has2b = t2b < 15;
+    f32x16 acc1[5], acc2[2];
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc1[j][e] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc2[j][e] = 0.f;
+    auto frag = [&](const uint16_t *p, int stride) {
+        const uint2 a0 = wg_tr(p), a1 = wg_tr(p + 4 * stride);
+        return __builtin_bit_cast(Frag, uint4{a0.x, a0.y, a1.x, a1.y});
+    };
+    auto compute = [&](const uint8_t *sb) {
+        const uint16_t *sx = (const uint16_t *)sb, *sdh = (const uint16_t *)(sb + oDH);
+        const uint16_t *sdy = (const uint16_t *)(sb + oDY), *sh = (const uint16_t *)(sb + oH);
+        const int ex = sbx >> 1;  // X row stride (elements)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {  // two k-steps of 16 points
+            __builtin_amdgcn_sched_barrier(0);  // one k-step's fragments live at a time
+            const int kr = 16 * ks + kb + q;
+            const Frag af = frag(sdh + kr * 160 + 32 * rt1 + cbase, 160);
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+                const Frag bf = frag(sx + kr * ex + 32 * (ct1 + j) + cbase, ex);
+                acc1[j] = Tr::mma32(af, bf, acc1[j]);
+            }
+            {
+                const Frag a2 = frag(sdy + kr * 96 + 32 * (t2a / 5) + cbase, 96);
+                const Frag b2 = frag(sh + kr * 160 + 32 * (t2a % 5) + cbase, 160);
+                acc2[0] = Tr::mma32(a2, b2, acc2[0]);
+            }
+            if (has2b) {
+                const Frag a2 = frag(sdy + kr * 96 + 32 * (t2b / 5) + cbase, 96);
+                const Frag b2 = frag(sh + kr * 160 + 32 * (t2b % 5) + cbase, 160);
+                acc2[1] = Tr::mma32(a2, b2, acc2[1]);
+            }
+        }
+    };
+    if (nch > 0) dma(0);
+    if (nch > 1) dma(1);
+    for (int c = 0; c < nch; ++c) {
+        // chunk c landed: the wave's cw DMAs of chunk c + 1 (a full chunk) may stay in flight
+        const int64_t pn = chunk_p0(c + 1);
+        if (c + 1 < nch && pn + 32 <= g.N) {  // exactly this wave's count of the next chunk
+            if (cw >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+            else if (cw == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+            else if (cw == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        const int64_t p0 = chunk_p0(c);
+        if (p0 + 32 > g.N) {  // the last chunk: zero its dH / dY rows past N
+            uint8_t *sb = lds + (c % MW_RING) * SZ;
+            const int nv = (int)(g.N - p0);
+            for (int i = tid; i < (32 - nv) * 25; i += 512) {
+                const int row = nv + i / 25, k = i % 25;
+                uint4 *d = k < 16 ? (uint4 *)(sb + oDH + row * 320) + k : (uint4 *)(sb + oDY + row * 192) + (k - 16);
+                *d = uint4{0u, 0u, 0u, 0u};
+            }
+        }
+        __syncthreads();  // chunk c visible to all waves; chunk c - 1's stage reads are done
+        if (c + 2 < nch) dma(c + 2);  // into the stage chunk c - 1 used
+        if (MW_DIAG != 1) compute(lds + (c % MW_RING) * SZ);
+    }
+    if (MW_DIAG == 3 && acc1[0][0] != 12345.f) return;
+    // partial tiles: register e of a tile = C[32 rt + 8 (e >> 2) + 4 h + (e & 3)][32 ct + r]
+    float *out = g.work + (int64_t)blockIdx.x * MW_PT;
+    const int r = lane & 31;
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e)
+            out[(32 * rt1 + 8 * (e >> 2) + 4 * h + (e & 3)) * MW_KXP + 32 * (ct1 + j) + r] = acc1[j][e];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int t = j ? t2b : t2a;
+        if (j && !has2b) break;
+#pragma unroll
+        for (int e = 0; e < 16; ++e)
+            out[MW_P1 + (32 * (t / 5) + 8 * (e >> 2) + 4 * h + (e & 3)) * 160 + 32 * (t % 5) + r] =
+                acc2[j][e];
+    }
+}
+
+// partial sums: split s of the nparts partials, one float4 per thread
+__global__ void __launch_bounds__(256) k_mw_split(float *work, int nparts) {
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= MW_PT / 4) return;
+    const int ps = (nparts + MW_S - 1) / MW_S;
+    const int p0 = blockIdx.y * ps, p1 = p0 + ps < nparts ? p0 + ps : nparts;
+    const float4 *src = (const float4 *)work;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int p = p0; p < p1; ++p) {
+        const float4 v = src[(int64_t)p * (MW_PT / 4) + e];
+        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    ((float4 *)(work + (int64_t)nparts * MW_PT))[blockIdx.y * (MW_PT / 4) + e] = s;
+}
+
+// the MW_S split sums into the parameter layout (lin_in: [dw_in | db_in]; lin_out rows:
+// out_0 first, then dino)
+__global__ void __launch_bounds__(256) k_mw_final(const sd_mlp_wgrad_args g) {
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= MW_PT) return;
+    const float *mid = g.work + (int64_t)g.nparts * MW_PT;
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < MW_S; ++k) s += mid[k * MW_PT + e];
+    const int din = g.kx - 1;
+    if (e < MW_P1) {
+        const int row = e / MW_KXP, col = e - row * MW_KXP;
+        if (col < din) g.dw_in[row * din + col] = s;
+        else if (col == din) g.db_in[row] = s;
+        return;
+    }
+    const int e2 = e - MW_P1, row = e2 / 160, col = e2 - row * 160;
+    if (row > g.D) return;
+    const int orow = row == g.D ? 0 : row + 1;
+    if (col < 128) g.dw_out[orow * 128 + col] = s;
+    else if (col == 128) g.db_out[orow] = s;
+}
+
+extern "C" int64_t sd_mlp_train_wgrad_work(int32_t nparts) {
+    return nparts > 0 ? (int64_t)(nparts + MW_S) * MW_PT : -1;
+}
+
+extern "C" int sd_mlp_train_wgrad(const sd_mlp_wgrad_args *g, void *stream) {
+    if (!g || (g->N > 0 && (!g->x || !g->dh || !g->dy || !g->h)) || !g->work || !g->dw_in || !g->db_in ||
+        !g->dw_out || !g->db_out || g->N < 0 || g->kx <= 8 || g->kx > MW_KXP || g->kx % 8 ||
+        g->ldx < g->kx || g->ldx > MW_KXP || g->ldx % 8 || g->D <= 0 || g->D > 64 || g->D % 8 || g->nparts <= 0 ||
+        (g->dtype != SD_F16 && g->dtype != SD_BF16)) {
+        sd_set_error("sd_mlp_train_wgrad: invalid argument (kx <= 320, kx % 8 == 0, D <= 64, "
+                     "D % 8 == 0, 16-bit rows)");
+        return -1;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    if (g->N == 0) {  // empty: zero gradients
+        const bool ok = hipMemsetAsync(g->dw_in, 0, (size_t)128 * (g->kx - 1) * 4, st) == hipSuccess &&
+                        hipMemsetAsync(g->db_in, 0, 128 * 4, st) == hipSuccess &&
+                        hipMemsetAsync(g->dw_out, 0, (size_t)(g->D + 1) * 128 * 4, st) == hipSuccess &&
+                        hipMemsetAsync(g->db_out, 0, (size_t)(g->D + 1) * 4, st) == hipSuccess;
+        if (!ok) sd_set_error("sd_mlp_train_wgrad: memset failed");
+        return ok ? 0 : -2;
+    }
+    const int lds = MW_RING * mw_stage_bytes(g->ldx);
+    if (g->dtype == SD_F16) {
+        sd_lds_attr((const void *)k_mlp_wgrad<SD_F16>, lds);
+        hipLaunchKernelGGL(k_mlp_wgrad<SD_F16>, dim3(g->nparts), dim3(512), lds, st, *g);
+    } else {
+        sd_lds_attr((const void *)k_mlp_wgrad<SD_BF16>, lds);
+        hipLaunchKernelGGL(k_mlp_wgrad<SD_BF16>, dim3(g->nparts), dim3(512), lds, st, *g);
+    }
+    hipLaunchKernelGGL(k_mw_split, dim3((MW_PT / 4 + 255) / 256, MW_S), dim3(256), 0, st,
+                       g->work, g->nparts);
+    hipLaunchKernelGGL(k_mw_final, dim3((MW_PT + 255) / 256), dim3(256), 0, st, *g);
+    if (hipGetLastError() != hipSuccess) {
+        sd_set_error("sd_mlp_train_wgrad: launch failed");
         return -2;
     }
     return 0;

@@ -95,3 +95,39 @@ def test_wgrad_kernel_vs_matmul(N, Ma, Nb, lda, ldb, dt):
     got = _lib.wgrad(a, b, Ma, Nb)
     ref = a[:, :Ma].double().t() @ b[:, :Nb].double()
     assert rel_l2(got, ref) <= 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,ldx,kx,nparts", [(262144, 296, 296, None), (1000, 304, 296, None),
+                                             (37, 296, 296, None), (4133, 320, 320, 7),
+                                             (64, 128, 104, 256), (0, 296, 296, None)])
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+def test_mlp_wgrad_fused_vs_matmul(N, ldx, kx, nparts, dt):
+    """sd_mlp_train_wgrad (dW1 = dH^T X and dW_o = dY^T [H | 1] in one LDS-DMA pass, the
+    parameter layout out) vs f64 matmuls of the same 16-bit rows: rel-L2 <= 1e-5 (f32
+    accumulation order only).  Partial last chunk (N % 32), more workgroups than chunks,
+    padded rows (ldx > kx), N = 0.  NaN rows past the used columns / past N must not leak."""
+    D = 64
+    dev = "cuda"
+    g = torch.Generator(device=dev).manual_seed(N + kx)
+    # one allocation with NaN after the N rows: DMA reads past N would poison the sums
+    buf = lambda n, w: torch.full((n + 64, w), float("nan"), device=dev, dtype=dt)
+    x, dh, dy, h = buf(N, ldx), buf(N, 128), buf(N, 72), buf(N, 136)
+    x[:N] = torch.randn(N, ldx, device=dev, generator=g).to(dt)
+    dh[:N] = torch.randn(N, 128, device=dev, generator=g).to(dt)
+    dy[:N] = 0
+    dy[:N, :D + 1] = torch.randn(N, D + 1, device=dev, generator=g).to(dt)
+    h[:N] = 0
+    h[:N, :128] = torch.randn(N, 128, device=dev, generator=g).to(dt)
+    h[:N, 128] = 1
+    dw_in, db_in, dw_out, db_out = _lib.mlp_train_wgrad(x[:N], dh[:N], dy[:N], h[:N], kx, D,
+                                                        nparts=nparts)
+    if N == 0:
+        assert not dw_in.any() and not db_in.any() and not dw_out.any() and not db_out.any()
+        return
+    X, dH, dY, H = (t[:N].double() for t in (x, dh, dy, h))
+    dW1 = dH.t() @ X[:, :kx]
+    dWo = dY[:, :D + 1].t() @ H[:, :129]
+    order = [D] + list(range(D))  # lin_out rows: out_0, then dino
+    assert rel_l2(dw_in, dW1[:, :kx - 1]) <= 1e-5 and rel_l2(db_in, dW1[:, kx - 1]) <= 1e-5
+    assert rel_l2(dw_out, dWo[order, :128]) <= 1e-5 and rel_l2(db_out, dWo[order, 128]) <= 1e-5

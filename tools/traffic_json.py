@@ -18,7 +18,8 @@ for f in sorted(glob.glob(os.path.join(d, "pmc*", "*counter_collection.csv"))):
         name = r["Kernel_Name"]
         for k in ("k_render_tile", "k_render_proj", "k_project", "k_head_hc", "k_render<", "k_field_gather_bwd",
                   "k_field_gather", "k_composite_bwd", "k_unpack_grid", "k_pack_grid",
-                  "k_mlp_fwd", "k_mlp_bwd", "k_composite", "k_seg_head", "k_ssc_confusion",
+                  "k_mlp_fwd", "k_mlp_bwd", "k_mlp_wgrad", "k_mw_split", "k_mw_final", "k_wgrad",
+                  "k_composite", "k_seg_head", "k_ssc_confusion",
                   "k_attn_lds", "k_attn_dir", "k_grow3", "k_field"):
             if k in name:
                 vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
