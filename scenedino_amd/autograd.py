@@ -76,6 +76,9 @@ class GatherAcc:
         """(buffer, first) for the running backward pass."""
         task = torch._C._current_graph_task_id()
         if self.buf is None or self.task != task:
+            # (zeroed here, serialised before the scatter: a fill of the 503 MB bench
+            # buffer forked to a side stream during the forward slowed the kernels beside
+            # it by more than its 63 us -- 0.75 vs 0.69 ms per step, profiles/r5_train)
             self.task, self.buf = task, torch.zeros(shape, device=device)
             torch.autograd.Variable._execution_engine.queue_callback(self._release)
             return self.buf, True

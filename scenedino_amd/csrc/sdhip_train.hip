@@ -43,11 +43,16 @@ __device__ __forceinline__ void sd_wave_lds_sync() {
 }
 
 // ---------------------------------------------------------------------------
-// forward gather: one wave per run of TR_FRUN consecutive points; lane j < n computes
-// point j's geometry (broadcast with readlane), then every lane gathers 4 channels
-// (f32x4 of the NHWC grid) of all the run's points with their tap loads issued together
+// forward gather: one wave per tile of 32 consecutive points (a ray's samples).  Lane r
+// (and r + 32) computes point r's geometry; the tile splits into runs of consecutive
+// points with the same frame and tap quad -- a ray's samples straddle one texel quad
+// through rounding when the render view is the encoder view (3.5 runs per 32 samples on
+// the bench's rays) and walk along an epipolar line otherwise.  Each run's four texel
+// rows are loaded ONCE (every lane 4 channels, f32x4 of the NHWC grid; the next run's
+// loads issued before this run's blends) and blended for each of its points: a quad per
+// point re-read 1 KiB x 4 from L2 for every sample (1 GB per bench step, 137 us).
 // ---------------------------------------------------------------------------
-#define TR_FRUN 4
+#define TR_TILE 32
 
 // row element types of X / dX: f32, or the autocast dtype (f16 / bf16) of the MLP GEMMs
 template <int DT> struct TrE { typedef float T; };
@@ -65,6 +70,17 @@ __device__ __forceinline__ void tr_store4(typename TrE<DT>::T *dst, const f32x4 
     }
 }
 
+// positional code entry s (< 39) of v = [x, y, z~] (positional_encoding.py:68-80): v, then
+// sin(f_j v + phi) with rows (freq j, phase) and the 3 coordinates innermost; 39: the 1
+__device__ __forceinline__ float tr_code(const float v[3], int s) {
+    if (s < 3) return s == 0 ? v[0] : s == 1 ? v[1] : v[2];
+    if (s >= 39) return 1.f;
+    const int t = s - 3, fi = t / 6, cs = (t % 6) / 3, co = t % 3;
+    const float f = 1.5f * (float)(1 << fi);
+    const float vv = co == 0 ? v[0] : co == 1 ? v[1] : v[2];
+    return sinf(fmaf(vv, f, cs ? 1.5707963705062866f : 0.f));
+}
+
 template <int DT>
 __global__ void __launch_bounds__(TR_WAVES * 64)
 k_field_gather(const float *__restrict__ xyz, int64_t B, int64_t P,
@@ -74,75 +90,59 @@ k_field_gather(const float *__restrict__ xyz, int64_t B, int64_t P,
                uint8_t *__restrict__ invalid_f, float *__restrict__ rgb,
                float *__restrict__ invalid) {
     typedef typename TrE<DT>::T E;
-    const int lane = threadIdx.x & 63;
+    const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
     const int64_t NP = B * P;
     const int ld = C + 40;  // [feat (C) | code (39) | 1]: the 1 carries the bias through the GEMM
     const int64_t plane = (int64_t)Hf * Wf * C;
     const int64_t cplane = (int64_t)Hc * Wc * 4;
-    const int64_t nruns = (NP + TR_FRUN - 1) / TR_FRUN;
-    // Order within a run: every load (the next run's coordinates, the colour taps, the grid
-    // taps) before the run's first store -- a load issued after a store waits for it in
-    // the memory counter, so interleaving cost a round trip per phase
-    const int64_t rstep = (int64_t)gridDim.x * TR_WAVES;
-    int64_t run = (int64_t)blockIdx.x * TR_WAVES + (threadIdx.x >> 6);
-    float qx = 0.f, qy = 0.f, qz = 0.f;  // lane < TR_FRUN: its point of the run
-    auto fetch = [&](int64_t rn) {
-        const int64_t p = rn * TR_FRUN + lane;
-        if (lane < TR_FRUN && rn < nruns && p < NP) {
-            qx = xyz[p * 3];
-            qy = xyz[p * 3 + 1];
-            qz = xyz[p * 3 + 2];
-        }
-    };
-    fetch(run);
-    for (; run < nruns; run += rstep) {
-        const int64_t p0 = run * TR_FRUN;
-        const int n = (int)(p0 + TR_FRUN < NP ? TR_FRUN : NP - p0);
-        const float px0 = qx, py0 = qy, pz0 = qz;
-        fetch(run + rstep);
-        int gi[4] = {0, 0, 0, 0}, gb = 0;
+    const int64_t ntile = (NP + TR_TILE - 1) / TR_TILE;
+    for (int64_t tile = (int64_t)blockIdx.x * TR_WAVES + (threadIdx.x >> 6); tile < ntile;
+         tile += (int64_t)gridDim.x * TR_WAVES) {
+        const int64_t p0 = tile * TR_TILE;
+        const int64_t pt = p0 + r;
+        const bool valid = pt < NP;
+        float px = 0.f, py = 0.f, pz = 0.f;
+        int gi[4] = {0, 0, 0, 0}, gb = -1;
         float gw[4] = {0.f, 0.f, 0.f, 0.f}, gv[3] = {0.f, 0.f, 0.f};
         bool invf = false;
-        if (lane < n) {
-            const int64_t p = p0 + lane;
-            const int64_t b = p / P;
-            const PointGeo geo = sd_point_geo(cam_f + b * SD_CAM_WORDS, px0, py0, pz0, Wf, Hf);
+        if (valid) {
+            px = xyz[pt * 3]; py = xyz[pt * 3 + 1]; pz = xyz[pt * 3 + 2];
+            const int64_t b = pt / P;
+            const PointGeo geo = sd_point_geo(cam_f + b * SD_CAM_WORDS, px, py, pz, Wf, Hf);
             gi[0] = geo.t.i00; gi[1] = geo.t.i01; gi[2] = geo.t.i10; gi[3] = geo.t.i11;
             gw[0] = geo.t.w00; gw[1] = geo.t.w01; gw[2] = geo.t.w10; gw[3] = geo.t.w11;
             gv[0] = geo.v[0]; gv[1] = geo.v[1]; gv[2] = geo.v[2];
             gb = (int)b;
             invf = geo.inv_f;
         }
-        // colour samples / masks: lane = (point, view); the point's coordinates from its lane
-        const bool cdo = nv > 0 && (rgb || invalid) && lane < n * nv;
-        const int cj = cdo ? lane / nv : 0;
-        const float cx = __shfl(px0, cj), cy = __shfl(py0, cj), cz = __shfl(pz0, cj);
-        float col[3] = {0.f, 0.f, 0.f};
-        float cinv = 0.f;
-        if (cdo) {
-            const int v = lane - cj * nv;
-            const int64_t b = (p0 + cj) / P;
-            const bool ic = sd_color_view(cam_c + (b * nv + v) * SD_CAM_WORDS, img + (b * nv + v) * cplane,
-                                          Wc, Hc, cx, cy, cz, col);
-            if (invalid) {
-                float x, y, zc;  // the encoder-frustum test of sd_point_geo, same arithmetic
-                sd_project(cam_f + b * SD_CAM_WORDS, cx, cy, cz, x, y, zc);
-                cinv = (ic | sd_outside(x, y, zc)) ? 1.f : 0.f;
-            }
-        }
-        for (int c = lane * 4; c < C; c += 256) {
-            f32x4 t[TR_FRUN][4];
-#pragma unroll
-            for (int j = 0; j < TR_FRUN; ++j) {
-                const int jj = j < n ? j : 0;
-                const float *g = grid + (int64_t)__builtin_amdgcn_readlane(gb, jj) * plane + c;
+        // runs: a point opens one unless it has the previous point's frame and taps
+        const int src = ((lane - 1) & 63) * 4;
+        const bool same = __builtin_amdgcn_ds_bpermute(src, gb) == gb &&
+                          __builtin_amdgcn_ds_bpermute(src, gi[0]) == gi[0] &&
+                          __builtin_amdgcn_ds_bpermute(src, gi[1]) == gi[1] &&
+                          __builtin_amdgcn_ds_bpermute(src, gi[2]) == gi[2] &&
+                          __builtin_amdgcn_ds_bpermute(src, gi[3]) == gi[3];
+        const uint32_t om = (uint32_t)__ballot(valid && (r == 0 || !same));
+        const int nvp = __builtin_popcountll(__ballot(valid) & 0xffffffffull);
+        // features: per channel pass (64 lanes x 4 channels), the runs in order
+        for (int c = lane * 4; c - lane * 4 < C; c += 256) {
+            const bool cin = c < C;
+            const int cc = cin ? c : 0;
+            auto issue = [&](int j, f32x4 (&t)[4]) {
+                const float *g = grid + (int64_t)__builtin_amdgcn_readlane(gb, j) * plane + cc;
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
-                    t[j][q] = *(const f32x4 *)(g + (int64_t)__builtin_amdgcn_readlane(gi[q], jj) * C);
-            }
-#pragma unroll
-            for (int j = 0; j < TR_FRUN; ++j) {
-                if (j < n) {
+                    t[q] = *(const f32x4 *)(g + (int64_t)__builtin_amdgcn_readlane(gi[q], j) * C);
+            };
+            uint32_t rem = om;
+            f32x4 t[4], tn[4];
+            if (rem) issue(__builtin_ctz(rem), t);
+            while (rem) {
+                const int s0 = __builtin_ctz(rem);
+                rem &= rem - 1;
+                const int e0 = rem ? __builtin_ctz(rem) : nvp;
+                if (rem) issue(__builtin_ctz(rem), tn);  // the next run's texels in flight
+                for (int j = s0; j < e0; ++j) {
                     float w[4];
 #pragma unroll
                     for (int q = 0; q < 4; ++q)
@@ -151,49 +151,56 @@ k_field_gather(const float *__restrict__ xyz, int64_t B, int64_t P,
                     f32x4 o;
 #pragma unroll
                     for (int i = 0; i < 4; ++i)  // grid_sampler_2d's nw, ne, sw, se order
-                        o[i] = ((t[j][0][i] * w[0] + t[j][1][i] * w[1]) + t[j][2][i] * w[2]) +
-                               t[j][3][i] * w[3];
-                    tr_store4<DT>(x_out + (p0 + j) * ld + c, o);
+                        o[i] = ((t[0][i] * w[0] + t[1][i] * w[1]) + t[2][i] * w[2]) + t[3][i] * w[3];
+                    if (cin) tr_store4<DT>(x_out + (p0 + j) * ld + c, o);
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) t[q] = tn[q];
+            }
+        }
+        // positional code and the bias 1: lane half h writes entries 20 h .. 20 h + 19 of
+        // its point's 40
+        if (valid) {
+            E *xr = x_out + pt * ld + C;
+#pragma unroll 1
+            for (int k = 0; k < 20; k += 2) {  // (one sinf body: unrolled, 169 VGPRs)
+                const int s = 20 * h + k;
+                const float a0 = tr_code(gv, s), a1 = tr_code(gv, s + 1);
+                if constexpr (DT == SD_F32) {
+                    *(float2 *)(xr + s) = make_float2(a0, a1);
+                } else {
+                    typedef __attribute__((ext_vector_type(2))) E e2;
+                    *(e2 *)(xr + s) = e2{(E)a0, (E)a1};
                 }
             }
         }
-        // positional code (positional_encoding.py:68-80): [x, y, z~, sin(f_j v + phi)]
-        // with rows (freq j, phase) and the 3 coordinates innermost; then the bias 1
-#pragma unroll
-        for (int j = 0; j < TR_FRUN; ++j) {
-            if (j < n) {
-                float v[3];
-#pragma unroll
-                for (int e = 0; e < 3; ++e)
-                    v[e] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(
-                                                         __builtin_bit_cast(int, gv[e]), j));
-                E *xr = x_out + (p0 + j) * ld;
-                if (lane < 39) {
-                    float r;
-                    if (lane < 3) {
-                        r = v[lane];
-                    } else {
-                        const int s = lane - 3, fi = s / 6, cs = (s % 6) / 3, co = s % 3;
-                        const float f = 1.5f * (float)(1 << fi);
-                        r = sinf(fmaf(v[co], f, cs ? 1.5707963705062866f : 0.f));
+        // colour samples / masks: lane = (point, view) pairs, 64 per pass
+        if (nv > 0 && (rgb || invalid)) {
+            for (int q0 = 0; q0 < nvp * nv; q0 += 64) {
+                const int q = q0 + lane;
+                const bool cdo = q < nvp * nv;
+                const int cj = cdo ? q / nv : 0, v = cdo ? q - cj * nv : 0;
+                const float cx = __shfl(px, cj), cy = __shfl(py, cj), cz = __shfl(pz, cj);
+                if (cdo) {
+                    const int64_t p = p0 + cj;
+                    const int64_t b = p / P;
+                    float col[3] = {0.f, 0.f, 0.f};
+                    const bool ic = sd_color_view(cam_c + (b * nv + v) * SD_CAM_WORDS,
+                                                  img + (b * nv + v) * cplane, Wc, Hc, cx, cy, cz, col);
+                    if (rgb) {
+                        rgb[(p * nv + v) * 3] = col[0];
+                        rgb[(p * nv + v) * 3 + 1] = col[1];
+                        rgb[(p * nv + v) * 3 + 2] = col[2];
                     }
-                    xr[C + lane] = (E)r;
-                } else if (lane == 39) {
-                    xr[C + 39] = (E)1.f;
+                    if (invalid) {
+                        float x, y, zc;  // the encoder-frustum test of sd_point_geo, same arithmetic
+                        sd_project(cam_f + b * SD_CAM_WORDS, cx, cy, cz, x, y, zc);
+                        invalid[p * nv + v] = (ic | sd_outside(x, y, zc)) ? 1.f : 0.f;
+                    }
                 }
             }
         }
-        if (cdo) {
-            const int64_t p = p0 + cj;
-            const int v = lane - cj * nv;
-            if (rgb) {
-                rgb[(p * nv + v) * 3] = col[0];
-                rgb[(p * nv + v) * 3 + 1] = col[1];
-                rgb[(p * nv + v) * 3 + 2] = col[2];
-            }
-            if (invalid) invalid[p * nv + v] = cinv;
-        }
-        if (lane < n && invalid_f) invalid_f[p0 + lane] = invf ? 1 : 0;
+        if (h == 0 && valid && invalid_f) invalid_f[pt] = invf ? 1 : 0;
     }
 }
 
@@ -516,11 +523,7 @@ extern "C" int sd_field_gather(const float *xyz, int64_t B, int64_t P, const flo
         return -1;
     }
     if (P == 0) return 0;
-    if (nv > 64 / TR_FRUN) {
-        sd_set_error("sd_field_gather: at most 16 colour views");
-        return -1;
-    }
-    const dim3 grid(tr_blocks((B * P + TR_FRUN - 1) / TR_FRUN)), blk(TR_WAVES * 64);
+    const dim3 grid(tr_blocks((B * P + TR_TILE - 1) / TR_TILE)), blk(TR_WAVES * 64);
     hipStream_t s = (hipStream_t)stream;
     if (x_dtype == SD_F16)
         hipLaunchKernelGGL(k_field_gather<SD_F16>, grid, blk, 0, s, xyz, B, P, grid_nhwc, C, Hf,
