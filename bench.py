@@ -431,7 +431,7 @@ def main_c5(args, world, rank, local_rank, dist, device, host_stage=False):
         # HBM bytes per k_seg_head launch (1-GPU launch shape) from the committed PMC
         # summary (tools/c5_traffic.sh: FETCH_SIZE x 2 + WRITE_SIZE, separate passes)
         seg_traffic, seg_tsrc = None, None
-        for tn in ("r3_c5_traffic.json", "r2_c5_traffic.json"):
+        for tn in ("r5_c5_traffic.json", "r3_c5_traffic.json", "r2_c5_traffic.json"):
             tf = os.path.join(ROOT, "profiles", tn)
             if dist or not os.path.exists(tf):
                 continue
@@ -476,6 +476,14 @@ def main_c5(args, world, rank, local_rank, dist, device, host_stage=False):
                 "field_query_tflops": n_launch * mlp_flops_per_point() / (field_ms * 1e-3) / 1e12,
             },
         }
+        if not seg_fp8:  # configs[4] names fp8 MFMA; measured, and not the default
+            line["fp8"] = {
+                "used": False,
+                "reason": "slower and below the label bar: --precision fp8 (the norm product "
+                          "on block-scaled fp8 MFMA) runs 1.41 ms vs 1.27-1.29 ms bf16 "
+                          "(profiles/r5_c5/bench_c5_fp8.log), and fp8 for the M / Wn2 chain "
+                          "keeps < 99 % of the labels at any block scale "
+                          "(profiles/r5_seg_fp8_emul.txt)"}
         print(json.dumps(line), flush=True)
 
 
