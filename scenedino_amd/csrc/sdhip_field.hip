@@ -635,6 +635,30 @@ k_render(const sd_render_args a, const sd_mlp m, const LdsPlan pl) {
 #ifndef SD_FQ_ABL_ONETAP
 #define SD_FQ_ABL_ONETAP 0
 #endif
+// diagnostic build only (SD_FQ_PROF=1): per-phase s_memtime cycles of k_field summed over all
+// waves (tools/field_prof.py); the outputs are unchanged
+#ifndef SD_FQ_PROF
+#define SD_FQ_PROF 0
+#endif
+#if SD_FQ_PROF
+__device__ unsigned long long fq_prof[8];
+#define FQ_T(i)                                                  \
+    {                                                            \
+        const uint64_t _t = __builtin_amdgcn_s_memtime();        \
+        pacc[i] += (uint32_t)(_t - tlast);                       \
+        tlast = _t;                                              \
+    }
+extern "C" int sd_field_prof(unsigned long long *out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(fq_prof), sizeof(fq_prof)) != hipSuccess) return -2;
+    if (reset) {
+        unsigned long long z[8] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(fq_prof), z, sizeof(z)) != hipSuccess) return -2;
+    }
+    return 0;
+}
+#else
+#define FQ_T(i)
+#endif
 #ifndef SD_FQ_ABL_NOSTORE
 #define SD_FQ_ABL_NOSTORE 0
 #endif
@@ -701,6 +725,11 @@ k_field(const sd_field_args a, const sd_mlp m, const LdsPlan pl) {
 #endif
     };
 
+    // the output biases of this lane's dims, loaded once: read in the output phase, the
+    // load waited (in-order vmcnt) for the next tile's tap loads issued before it
+    float bdino[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) bdino[dt] = dt < ndt ? m.b_dino[dt * 32 + li] : 0.f;
     // prologue: tile tt opened, its first DEPTH tap loads and the next tile's points in flight
     FTile cur;
     {
@@ -714,11 +743,16 @@ k_field(const sd_field_args a, const sd_mlp m, const LdsPlan pl) {
         r2 = Pr::load(rs, cur.o, 2);
         r3 = Pr::load(rs, cur.o, 3);
     }
+#if SD_FQ_PROF
+    uint32_t pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t tlast = __builtin_amdgcn_s_memtime();
+#endif
     for (; tt < tend; tt += tstep) {
         const int64_t tn = tt + tstep;
         const bool more = tn < tend;
         float nx0 = 0.f, ny0 = 0.f, nz0 = 0.f;
         if (more) load_pts(tn, nx0, ny0, nz0);  // in flight during this tile's grid chunks
+        FQ_T(5);
 
         const int lo = sd_opaque0();
         const uint8_t *lw = lds + lo;
@@ -749,6 +783,7 @@ k_field(const sd_field_args a, const sd_mlp m, const LdsPlan pl) {
                 SD_STEP(r1, q + 1, false);
             }
         }
+        FQ_T(0);
         // open the next tile and put its first tap loads in flight
         FTile nxt;
         if (more) {
@@ -761,6 +796,7 @@ k_field(const sd_field_args a, const sd_mlp m, const LdsPlan pl) {
             }
         }
 
+        FQ_T(1);
         if (m.b_empty_h) sd_empty_sub(acc, lds_ws + 128 + lo, h, cur.geo.inv_f);
 #pragma unroll
         for (int pc = 0; pc < SD_PE_CHUNKS; ++pc) {
@@ -772,14 +808,17 @@ k_field(const sd_field_args a, const sd_mlp m, const LdsPlan pl) {
         s += __shfl_xor(s, 32);
         const float sigma = sd_softplus(s + m.b_sigma);
 
+        FQ_T(2);
         const uint8_t *wo = wout_base + (WL ? lo : 0);
         const int64_t tile = tile_of(tt);
-        for (int dt = 0; dt < ndt; ++dt) {
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+            if (dt >= ndt) break;
             f32x16 ov = {};
             Prec<P>::mma2(wo, dt, acc, lane, ov);
             // O layout: row = point (r&3)+8(r>>2)+4h of this tile, column = dim li
             const int dim = dt * 32 + li;
-            const float bd = m.b_dino[dim];
+            const float bd = bdino[dt];
             if (SD_FQ_ABL_NOSTORE) {
                 if (ov[0] == 12345.f) a.dino[tile] = ov[1];  // keep the product alive
             } else {
@@ -801,6 +840,7 @@ k_field(const sd_field_args a, const sd_mlp m, const LdsPlan pl) {
                 }
             }
         }
+        FQ_T(3);
         if (cur.valid && h == 0) {
             a.sigma[cur.p] = sigma;
             if (a.invalid_f) a.invalid_f[cur.p] = cur.geo.inv_f ? 1 : 0;
@@ -820,7 +860,12 @@ k_field(const sd_field_args a, const sd_mlp m, const LdsPlan pl) {
             }
         }
         if (more) cur = nxt;
+        FQ_T(4);
     }
+#if SD_FQ_PROF
+    if (lane == 0)
+        for (int i = 0; i < 8; ++i) atomicAdd(&fq_prof[i], (unsigned long long)pacc[i]);
+#endif
 }
 
 // ---------------------------------------------------------------------------
