@@ -397,7 +397,9 @@ typedef struct sd_gemm_args {
     void *q, *k, *vt;           /* SD_EPI_QKV destinations; SD_EPI_RESID: q (or NULL) =
                                  * a bf16 (B, tokens - 1, N) copy of the updated rows
                                  * without each image's first (class) token -- the
-                                 * timm intermediate-layer grid, tokens_to_nhwc's output  */
+                                 * timm intermediate-layer grid, tokens_to_nhwc's output;
+                                 * k (or NULL) = an f32 copy of the updated rows (row
+                                 * stride ldo: sd_vit_mlp's LayerNorm input)              */
     int32_t tokens, heads, head_dim, tokens_pad;
     const float *pos;           /* SD_EPI_PATCH position embedding (patches+1, N)        */
     int32_t patches;
@@ -421,6 +423,18 @@ int sd_gemm(const sd_gemm_args *args, void *stream);
  * workspace per concurrently running call).  N <= 1024, N % 4 == 0; no conv. */
 int sd_gemm_resid_ln(const sd_gemm_args *args, const float *ln_w, const float *ln_b, float eps,
                      void *ln_out, uint32_t *ln_ws, void *stream);
+
+/* One ViT block's MLP half in one launch (timm Block: x = x + ls2 * (fc2(gelu(fc1(norm2(x))))),
+ * scenedino/models/backbones/dino/vit.py:112-189) for C = 384: x (M, C) f32 is updated in place
+ * by f32 atomics (the partial fc2 products of the 256-wide hidden chunks meet there, in arrival
+ * order); x_ln (M, C) f32 is a copy of x taken before the call (sd_gemm SD_EPI_RESID writes one
+ * to args->k), from which the LayerNorm (ln_w, ln_b, eps) is computed.  fc1_w (hidden, C) and
+ * fc2_w (C, hidden) bf16, fc1_b (hidden), fc2_b (C) or NULL, gamma (C) layer scale or NULL.
+ * hidden % 256 == 0. */
+int sd_vit_mlp(const float *x_ln, float *x, int64_t M, int32_t C, int32_t hidden,
+               const float *ln_w, const float *ln_b, float eps, const void *fc1_w,
+               const float *fc1_b, const void *fc2_w, const float *fc2_b, const float *gamma,
+               void *stream);
 
 /* nn.LayerNorm(K, eps) fused into the prologue of a GEMM (timm Block: norm1 -> attn.qkv,
  * norm2 -> mlp.fc1, vit.py:112-189 over timm's VisionTransformer): out = EPI(LN(x) W^T + b)

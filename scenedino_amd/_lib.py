@@ -212,6 +212,8 @@ SIGNATURES = {
     "sd_gemm": [ctypes.POINTER(SdGemmArgs), _vp],
     "sd_gemm_resid_ln": [ctypes.POINTER(SdGemmArgs), _vp, _vp, ctypes.c_float, _vp, _vp, _vp],
     "sd_attention": [_vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, ctypes.c_float, _vp, _vp],
+    "sd_vit_mlp": [_vp, _vp, _i64, _i32, _i32, _vp, _vp, ctypes.c_float, _vp, _vp, _vp, _vp, _vp,
+                   _vp],
     "sd_layernorm": [_vp, _i64, _i32, _vp, _vp, ctypes.c_float, _vp, _i32, _vp],
     "sd_patchify": [_vp, _i32, _i32, _i32, _i32, _i32, ctypes.POINTER(ctypes.c_float),
                     ctypes.POINTER(ctypes.c_float), _vp, _vp, _vp, _vp, _i32, _vp],
@@ -632,7 +634,7 @@ def composite_bwd(z, sigma, feat, rgb, hard_alpha_cap, g_depth, g_feat, g_rgb, g
 # ViT encoder kernels (sdhip_vit.hip)
 # ---------------------------------------------------------------------------
 def gemm(a, w, bias, epi, out=None, gamma=None, qkv=None, tokens=0, heads=0, pos=None,
-         patches=0, grid_out=None, ln=None):
+         patches=0, grid_out=None, ln=None, copy_out=None):
     """sd_gemm: a (M, K) bf16 (row stride a.stride(0)), w (N, K) bf16 contiguous.
     SD_EPI_RESID with grid_out (B, tokens - 1, N)-shaped bf16: also writes the updated rows
     without each image's class token there (tokens_to_nhwc's output, no extra launch).
@@ -656,6 +658,11 @@ def gemm(a, w, bias, epi, out=None, gamma=None, qkv=None, tokens=0, heads=0, pos
         g.tokens, g.heads, g.head_dim, g.tokens_pad = tokens, heads, q.shape[-1], k.shape[-2]
     if pos is not None:
         g.pos, g.patches = pos.data_ptr(), patches
+    if copy_out is not None:  # SD_EPI_RESID: an f32 copy of the updated rows (same strides)
+        _req(copy_out, "copy_out")
+        if epi != SD_EPI_RESID or copy_out.shape != out.shape or copy_out.stride() != out.stride():
+            raise ValueError("sd_gemm: copy_out is an SD_EPI_RESID copy shaped / strided as out")
+        g.k = copy_out.data_ptr()
     if grid_out is not None:
         _req(grid_out, "grid_out", torch.bfloat16)
         if grid_out.numel() != (M // tokens) * (tokens - 1) * N:
@@ -671,6 +678,21 @@ def gemm(a, w, bias, epi, out=None, gamma=None, qkv=None, tokens=0, heads=0, pos
                                     float(eps), ptr(ln_out), ptr(ws), stream_of(a)), "sd_gemm_resid_ln")
         return
     _check(lib.sd_gemm(ctypes.byref(g), stream_of(a)), "sd_gemm")
+
+
+def vit_mlp(x_ln, x, ln_w, ln_b, eps, fc1_w, fc1_b, fc2_w, fc2_b, gamma=None):
+    """sd_vit_mlp: x += gamma * (fc2(gelu(fc1(LN(x_ln)))) + fc2_b) in place (f32 atomics);
+    x_ln a separate f32 copy of x, C = 384."""
+    lib = load()
+    M, C = x.shape
+    _req(x_ln, "x_ln")
+    _req(x, "x")
+    _req(fc1_w, "fc1_w", torch.bfloat16)
+    _req(fc2_w, "fc2_w", torch.bfloat16)
+    _check(lib.sd_vit_mlp(ptr(x_ln), ptr(x), M, C, fc1_w.shape[0], ptr(_req(ln_w, "ln_w")),
+                          ptr(_req(ln_b, "ln_b")), float(eps), ptr(fc1_w), ptr(_req(fc1_b, "fc1_b")),
+                          ptr(fc2_w), ptr(fc2_b) if fc2_b is not None else None,
+                          ptr(gamma) if gamma is not None else None, stream_of(x)), "sd_vit_mlp")
 
 
 def ln_gemm(x, ln_w, ln_b, eps, w, bias, epi, out=None, qkv=None, tokens=0, heads=0):

@@ -815,6 +815,13 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g, float *__restrict_
 #pragma unroll
                         for (int q = 0; q < 16; ++q)
                             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, nv[q]), rsO, va[q], 0, 0);
+                        if (g.k) {  // an f32 copy of the updated rows (sd_vit_mlp's LayerNorm input)
+                            const __amdgpu_buffer_rsrc_t rsK =
+                                __builtin_amdgcn_make_buffer_rsrc(g.k, 0, (uint32_t)(g.M * g.ldo * 4), 0x00020000);
+#pragma unroll
+                            for (int q = 0; q < 16; ++q)
+                                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, nv[q]), rsK, va[q], 0, 0);
+                        }
                         if (g.q) {  // the intermediate-layer grid (k_tokens_to_nhwc's rounding)
                             uint32_t qa[16];
                             uint16_t qv[16];
@@ -865,6 +872,7 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g, float *__restrict_
                         float *o = (float *)g.out + m * g.ldo + n;
                         if (EPI == VT_EPI_RESID_LN) __hip_atomic_store(o, nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         else *o = nv;
+                        if (EPI == SD_EPI_RESID && g.k) ((float *)g.k)[m * g.ldo + n] = nv;
                         if (g.q) {  // the intermediate-layer grid (k_tokens_to_nhwc's rounding)
                             const uint32_t T = (uint32_t)g.tokens, b = (uint32_t)m / T, tok = (uint32_t)m - b * T;
                             if (tok > 0) ((__bf16 *)g.q)[((int64_t)b * (T - 1) + tok - 1) * g.N + n] = (__bf16)nv;
@@ -1682,8 +1690,176 @@ __global__ void __launch_bounds__(256) k_lngemm(sd_gemm_args g, const float *__r
 }
 
 // ---------------------------------------------------------------------------
+// One ViT block's MLP half in one launch (timm Block, vit.py:112-189):
+//   x += ls2 * (fc2(gelu(fc1(norm2(x)))) + b2)
+// for C = 384 (ViT-S: five launches per block -> four).  A 512-thread workgroup owns a
+// 32-row band and a 256-wide hidden chunk: LayerNorm of its rows from x_ln (an f32 copy of x
+// the preceding residual GEMM wrote, so the atomics below never meet a row another
+// workgroup is still normalising) into LDS as bf16 (k_lngemm's arithmetic), fc1 + bias +
+// exact GELU on the chunk (bf16 rows in LDS: the rounding of the GEMM path's hidden rows),
+// then the chunk's partial fc2 product, added into x as ls2 * (partial [+ b2 on chunk 0]) by
+// f32 atomics (the sum over chunks is in arrival order).  Each wave's W1 slice (32 hidden x
+// C) is in registers before the LayerNorm starts and its W2 slice (48 columns x the chunk)
+// is loaded while fc1 finishes: one weight round trip each, no K loop.  v_mfma_f32_16x16x32.
+// ---------------------------------------------------------------------------
+#define VM_BM 32
+#define VM_HC 256
+
+template <int PER>
+__global__ void __launch_bounds__(512) k_vit_mlp(const float *__restrict__ xln, float *__restrict__ x,
+                                                 int M, int hidden, const float *__restrict__ lw,
+                                                 const float *__restrict__ lb, float eps,
+                                                 const __bf16 *__restrict__ w1,
+                                                 const float *__restrict__ b1,
+                                                 const __bf16 *__restrict__ w2,
+                                                 const float *__restrict__ b2,
+                                                 const float *__restrict__ gamma) {
+    constexpr int C = 64 * PER, LDA = C + 8, NK1 = C / 32, LDH = VM_HC + 8, NK2 = VM_HC / 32;
+    constexpr int NT2 = C / 128;  // fc2: 16-column subtiles per wave (8 waves)
+    __shared__ __attribute__((aligned(16))) __bf16 sA[VM_BM * LDA];
+    __shared__ __attribute__((aligned(16))) __bf16 sH[VM_BM * LDH];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int j = lane & 15, kq = lane >> 4;
+    const int m0 = blockIdx.y * VM_BM, c0 = blockIdx.x * VM_HC;
+    // this wave's fc1 columns c0 + 32 w + 16 t + j: all of K in flight
+    bf16x8 wb1[2][NK1];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const __bf16 *wr = w1 + (int64_t)(c0 + 32 * wave + 16 * t + j) * C + 8 * kq;
+#pragma unroll
+        for (int s = 0; s < NK1; ++s) wb1[t][s] = *(const bf16x8 *)(wr + 32 * s);
+    }
+    // LayerNorm of rows 4 w .. 4 w + 3 (lane = column pairs 2 lane + 128 i; k_lngemm's order)
+    {
+        constexpr int P2 = PER / 2;
+        f32x2 lwv[P2], lbv[P2], v[4][P2];
+#pragma unroll
+        for (int i = 0; i < P2; ++i) {
+            lwv[i] = *(const f32x2 *)(lw + 2 * lane + 128 * i);
+            lbv[i] = *(const f32x2 *)(lb + 2 * lane + 128 * i);
+        }
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            const float *xr = xln + (int64_t)min(m0 + 4 * wave + rr, M - 1) * C;
+#pragma unroll
+            for (int i = 0; i < P2; ++i) v[rr][i] = *(const f32x2 *)(xr + 2 * lane + 128 * i);
+        }
+        constexpr float INV_C = 1.f / (float)C;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            f32x2 s2 = v[rr][0];
+#pragma unroll
+            for (int i = 1; i < P2; ++i) s2 += v[rr][i];
+            const float mean = vt_wave_sum(s2.x + s2.y) * INV_C;
+            const f32x2 mu = {mean, mean};
+            f32x2 q2 = {0.f, 0.f};
+#pragma unroll
+            for (int i = 0; i < P2; ++i) {
+                v[rr][i] -= mu;
+                q2 = __builtin_elementwise_fma(v[rr][i], v[rr][i], q2);
+            }
+            const float rstd = __builtin_amdgcn_rsqf(vt_wave_sum(q2.x + q2.y) * INV_C + eps);
+            const f32x2 rs = {rstd, rstd};
+            const int rl = 4 * wave + rr;
+#pragma unroll
+            for (int i = 0; i < P2; ++i) {
+                const f32x2 y = __builtin_elementwise_fma(v[rr][i] * rs, lwv[i], lbv[i]);
+                bf16x2 o;
+                o[0] = (__bf16)y.x;
+                o[1] = (__bf16)y.y;
+                *(bf16x2 *)&sA[rl * LDA + 2 * lane + 128 * i] = o;
+            }
+        }
+    }
+    __syncthreads();
+    // fc1 on the chunk: rows j / 16 + j, columns of subtile t
+    f32x4 acc[2][2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < NK1; ++s) {
+        const bf16x8 a0 = *(const bf16x8 *)&sA[j * LDA + 32 * s + 8 * kq];
+        const bf16x8 a1 = *(const bf16x8 *)&sA[(16 + j) * LDA + 32 * s + 8 * kq];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            acc[t][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, wb1[t][s], acc[t][0], 0, 0, 0);
+            acc[t][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, wb1[t][s], acc[t][1], 0, 0, 0);
+        }
+    }
+    // this wave's fc2 columns 48 w + 16 t + j over the chunk's K, in flight under the GELU
+    bf16x8 wb2[NT2][NK2];
+#pragma unroll
+    for (int t = 0; t < NT2; ++t) {
+        const __bf16 *wr = w2 + (int64_t)(16 * NT2 * wave + 16 * t + j) * hidden + c0 + 8 * kq;
+#pragma unroll
+        for (int s = 0; s < NK2; ++s) wb2[t][s] = *(const bf16x8 *)(wr + 32 * s);
+    }
+    // bias + GELU -> bf16 hidden rows (D layout: lane (j, kq) holds rows 4 kq + u, column j)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const int hc = 32 * wave + 16 * t + j;
+        const float bias = b1[c0 + hc];
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                sH[(16 * rt + 4 * kq + u) * LDH + hc] = (__bf16)vt_gelu(acc[t][rt][u] + bias);
+    }
+    __syncthreads();
+    f32x4 acc2[NT2][2];
+#pragma unroll
+    for (int t = 0; t < NT2; ++t) acc2[t][0] = acc2[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < NK2; ++s) {
+        const bf16x8 a0 = *(const bf16x8 *)&sH[j * LDH + 32 * s + 8 * kq];
+        const bf16x8 a1 = *(const bf16x8 *)&sH[(16 + j) * LDH + 32 * s + 8 * kq];
+#pragma unroll
+        for (int t = 0; t < NT2; ++t) {
+            acc2[t][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, wb2[t][s], acc2[t][0], 0, 0, 0);
+            acc2[t][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, wb2[t][s], acc2[t][1], 0, 0, 0);
+        }
+    }
+    // x += ls2 * (partial [+ b2]): one f32 atomic per element (the chunks' partials meet in x)
+#pragma unroll
+    for (int t = 0; t < NT2; ++t) {
+        const int n = 16 * NT2 * wave + 16 * t + j;
+        const float gm = gamma ? gamma[n] : 1.f;
+        const float bb = (c0 == 0 && b2) ? b2[n] : 0.f;
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int m = m0 + 16 * rt + 4 * kq + u;
+                if (m < M) unsafeAtomicAdd(x + (int64_t)m * C + n, gm * (acc2[t][rt][u] + bb));
+            }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
+extern "C" int sd_vit_mlp(const float *x_ln, float *x, int64_t M, int32_t C, int32_t hidden,
+                          const float *ln_w, const float *ln_b, float eps, const void *fc1_w,
+                          const float *fc1_b, const void *fc2_w, const float *fc2_b,
+                          const float *gamma, void *stream) {
+    if (!x_ln || !x || !ln_w || !ln_b || !fc1_w || !fc1_b || !fc2_w || M < 0 || C != 384 ||
+        hidden <= 0 || hidden % VM_HC || M * (int64_t)C >= ((int64_t)1 << 31) || x_ln == x) {
+        sd_set_error("sd_vit_mlp: invalid argument (C = 384, hidden % 256 == 0, x_ln a separate copy)");
+        return -1;
+    }
+    if (M == 0) return 0;
+    const dim3 grid((unsigned)(hidden / VM_HC), (unsigned)((M + VM_BM - 1) / VM_BM));
+    hipLaunchKernelGGL(k_vit_mlp<6>, grid, dim3(512), 0, (hipStream_t)stream, x_ln, x, (int)M,
+                       hidden, ln_w, ln_b, eps, (const __bf16 *)fc1_w, fc1_b,
+                       (const __bf16 *)fc2_w, fc2_b, gamma);
+    if (hipGetLastError() != hipSuccess) {
+        sd_set_error("sd_vit_mlp: launch failed");
+        return -2;
+    }
+    return 0;
+}
+
 // cross-workgroup split-K workspace (per device, allocated once outside graph capture):
 // 32 x 32 f32 partials and self-resetting tickets (zeroed at allocation)
 #define VT_SK_SLABS 2048

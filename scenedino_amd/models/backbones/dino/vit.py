@@ -151,6 +151,13 @@ LN_TAIL = os.environ.get("SCENEDINO_AMD_LN_TAIL", "0") == "1"
 # the DPT's intermediate token grids written by fc2's residual epilogue (no tokens_to_nhwc
 # launches); SCENEDINO_AMD_FC2_GRID=0 restores the separate launches (A/B runs)
 FC2_GRID = os.environ.get("SCENEDINO_AMD_FC2_GRID", "1") != "0"
+# the MLP half of a C = 384 block as one launch (sd_vit_mlp: norm2 + fc1 + GELU + fc2 +
+# residual, f32 atomics into the residual stream): 5 launches per block -> 4, but measured
+# SLOWER (ViT-S/16 0.519 -> 0.611 ms, profiles/r5_vit_mlp_ab.txt: 96 workgroups each stream
+# 393 KB of fc1 / fc2 weights, against the two GEMMs' 384 + 192 small tiles) and not
+# bit-reproducible (atomics: graph vs eager outputs differ by 5e-4 rel-L2); off by default,
+# SCENEDINO_AMD_VIT_MLP=1 selects it (A/B runs)
+VIT_MLP = os.environ.get("SCENEDINO_AMD_VIT_MLP", "0") == "1"
 
 
 def vit_forward(vit: VisionTransformer, images: torch.Tensor, packed: _Packed,
@@ -207,6 +214,9 @@ def vit_forward(vit: VisionTransformer, images: torch.Tensor, packed: _Packed,
         if ws is None or ws.device != dev or ws.numel() < (B * T + 31) // 32:
             ws = packed._ln_ws = torch.zeros((B * T + 31) // 32, device=dev, dtype=torch.int32)
     nblk = len(packed.blocks)
+    hidden = packed.blocks[0]["fc1_w"].shape[0]
+    fused_mlp = VIT_MLP and not tail and C == 384 and hidden % 256 == 0
+    xc = torch.empty_like(x) if fused_mlp else None  # x after the attention half (LN2 input)
     xn_ready = False  # xn holds this block's norm1 (the previous fc2's tail)
     for i, blk in enumerate(packed.blocks):
         if xn_ready:
@@ -220,6 +230,16 @@ def vit_forward(vit: VisionTransformer, images: torch.Tensor, packed: _Packed,
             _lib.gemm(xn, blk["qkv_w"], blk["qkv_b"], _lib.SD_EPI_QKV, qkv=(q, k, vt), tokens=T,
                       heads=nh)
         _lib.attention(q, k, vt, scale, ao)
+        if fused_mlp:  # proj (+ the f32 copy), then norm2 .. fc2 + residual in one launch
+            _lib.gemm(ao, blk["proj_w"], blk["proj_b"], _lib.SD_EPI_RESID, out=x, gamma=blk["ls1"],
+                      copy_out=xc)
+            _lib.vit_mlp(xc, x, blk["n2w"], blk["n2b"], 1e-6, blk["fc1_w"], blk["fc1_b"],
+                         blk["fc2_w"], blk["fc2_b"], gamma=blk["ls2"])
+            if i in intermediate:
+                grids.append(to_grid(x, B, T, C, 1, gh, gw, False))
+                if on_grid is not None:
+                    on_grid(len(grids) - 1, grids[-1])
+            continue
         if tail:  # proj + norm2 -> xn, then fc1 as a plain GEMM
             _lib.gemm(ao, blk["proj_w"], blk["proj_b"], _lib.SD_EPI_RESID, out=x, gamma=blk["ls1"],
                       ln=(blk["n2w"], blk["n2b"], 1e-6, xn, ws))

@@ -323,6 +323,42 @@ def test_ln_gemm_equals_layernorm_then_gemm(gpu, C, H, T, B):
     assert (hid.float() - ref1).abs().max().item() <= 8e-3 * ref1.abs().max().item()
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,hidden,ls", [(481, 1536, True), (481, 1536, False), (77, 512, True),
+                                         (33, 256, False)])
+def test_vit_mlp_equals_ln_gemm_then_gemm(gpu, M, hidden, ls):
+    """sd_vit_mlp (norm2 + fc1 + GELU + fc2 + residual in one launch, the hidden chunks'
+    partials added into x by f32 atomics) vs the two-launch path it replaces (sd_ln_gemm
+    GELU, then sd_gemm SD_EPI_RESID): the same bf16 LayerNorm rows and bf16 hidden rows, so
+    they differ only by f32 summation order (|d| <= 1e-4 of the update's scale); and the
+    SD_EPI_RESID f32 copy (args->k) equals the updated rows."""
+    from scenedino_amd import _lib
+    C = 384
+    g = torch.Generator().manual_seed(M + hidden)
+    x0 = (2 * torch.randn(M, C, generator=g) + 0.5).to(gpu)
+    lw = (1 + 0.1 * torch.randn(C, generator=g)).to(gpu)
+    lb = (0.1 * torch.randn(C, generator=g)).to(gpu)
+    w1 = _bf(torch.randn(hidden, C, generator=g) / math.sqrt(C)).to(gpu)
+    b1 = (0.1 * torch.randn(hidden, generator=g)).to(gpu)
+    w2 = _bf(torch.randn(C, hidden, generator=g) / math.sqrt(hidden)).to(gpu)
+    b2 = (0.1 * torch.randn(C, generator=g)).to(gpu)
+    gam = (0.5 + torch.rand(C, generator=g)).to(gpu) if ls else None
+    hid = torch.empty(M, hidden, device=gpu, dtype=torch.bfloat16)
+    _lib.ln_gemm(x0, lw, lb, 1e-6, w1, b1, _lib.SD_EPI_GELU, out=hid)
+    ref = x0.clone()
+    _lib.gemm(hid, w2, b2, _lib.SD_EPI_RESID, out=ref, gamma=gam)
+    # the residual GEMM's f32 copy
+    a = _bf(torch.randn(M, C, generator=g)).to(gpu)
+    wa = _bf(torch.randn(C, C, generator=g) / math.sqrt(C)).to(gpu)
+    xr, xc = x0.clone(), torch.full_like(x0, float("nan"))
+    _lib.gemm(a, wa, b2, _lib.SD_EPI_RESID, out=xr, gamma=gam, copy_out=xc)
+    assert torch.equal(xr, xc)
+    x = x0.clone()
+    _lib.vit_mlp(x0.clone(), x, lw, lb, 1e-6, w1, b1, w2, b2, gamma=gam)
+    scale = (ref - x0).abs().max().item()
+    assert (x - ref).abs().max().item() <= 1e-4 * scale + 1e-5
+
+
 def _encoder_check(enc, images, tol=3e-2):
     dev = images.device
     with torch.no_grad():

@@ -1,12 +1,18 @@
 #!/usr/bin/env python3
 """Diagnostic: per-kernel durations and inter-kernel gaps of the last encoder pass in a
 rocprofv3 --kernel-trace database (rocpd sqlite), e.g. from tools/vit_prof.sh.
-usage: trace_pass.py run_results.db [first_kernel_substring]"""
+usage: trace_pass.py run_results.db|run_kernel_trace.csv [first_kernel_substring]"""
 import sqlite3
 import sys
 
-c = sqlite3.connect(sys.argv[1])
-rows = list(c.execute("select name, start, end, grid_x, workgroup_x from kernels order by start"))
+if sys.argv[1].endswith(".csv"):  # rocprofv3 --output-format csv kernel trace
+    import csv
+    rows = sorted(((r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
+                    int(r["Grid_Size_X"]), int(r["Workgroup_Size_X"]))
+                   for r in csv.DictReader(open(sys.argv[1]))), key=lambda r: r[1])
+else:
+    c = sqlite3.connect(sys.argv[1])
+    rows = list(c.execute("select name, start, end, grid_x, workgroup_x from kernels order by start"))
 first = sys.argv[2] if len(sys.argv) > 2 else "k_patchify"
 starts = [i for i, r in enumerate(rows) if first in r[0]]
 a = starts[-2] if len(starts) > 1 else starts[-1]
