@@ -280,11 +280,18 @@ k_render_tile(const st_args sa) {
     // LDS-DMA one step ahead (completed by the step's closing vmcnt(0)), so the ray pass
     // reads them from LDS instead of waiting on scalar loads
     const int nrw = min(a.ray_dim, 8);
-    // the wave's RPW rays ray .. ray + RPW - 1: lane 8 r + w fetches word w of ray r
+    // memory index of the wave's ray r, given ray = GR grp + RPW wave (the wave's first
+    // slot): RPW = 2 pairs ray w with ray w + NW of the group, so the two halves a group
+    // splits into when its tap box overflows (kh = K below: the halves are the rays of slot
+    // 0 and of slot 1) are the group's left and right 8 rays -- as adjacent pairs (2 w,
+    // 2 w + 1) both halves spanned the whole strip and 2.5 % of the C1 offset-pose rays went
+    // to the per-ray fallback kernel (52 us of a 0.43 ms frame)
+    auto rmap = [&](int ray_, int r) { return RPW == 1 ? ray_ + r : ray_ - RPW * wave + r * NW + wave; };
+    // the wave's RPW rays: lane 8 r + w fetches word w of ray r
     auto ray_fetch = [&](int ray, int slot) {
         const int r = lane >> 3, w = lane & 7;
-        if (r < RPW && w < nrw && ray + r < R)
-            st_dma4(a.rays + (int64_t)(ray + r) * a.ray_dim + w,
+        if (r < RPW && w < nrw && rmap(ray, r) < R)
+            st_dma4(a.rays + (int64_t)rmap(ray, r) * a.ray_dim + w,
                     lds0 + ST_L_RAY + (wave * 2 + slot) * 32 * RPW);
     };
     // this lane's ray of the wave's RPW (ray pass: lane = record k' = rsl K + k)
@@ -299,13 +306,13 @@ k_render_tile(const st_args sa) {
 #pragma unroll
                 for (int p = 0; p < ST_MAXP; ++p) zo[p] = zr[min(64 * p + lane, K - 1)];
             } else {
-                const float *zr = a.z + (int64_t)min(ray + rsl, R - 1) * K;
+                const float *zr = a.z + (int64_t)min(rmap(ray, rsl), R - 1) * K;
                 zo[0] = zr[min(kl, K - 1)];  // (lanes past 2 K: K = 16)
                 zo[1] = 0.f;
             }
         } else {
             const float near = rl[6], far = rl[7];
-            const uint64_t base = a.z_offset + (uint64_t)(ray + rsl) * (uint64_t)K;
+            const uint64_t base = a.z_offset + (uint64_t)rmap(ray, rsl) * (uint64_t)K;
             zo[1] = 0.f;
 #pragma unroll
             for (int p = 0; p < ST_MAXP; ++p) {
@@ -356,7 +363,7 @@ k_render_tile(const st_args sa) {
 #pragma unroll
             for (int p = 0; p < ST_MAXP; ++p) {
                 const int k = 64 * p + lane;  // record k' (RPW = 2: ray rsl's sample kl)
-                if (64 * p < KW && k < KW && (RPW == 1 || ray + rsl < R)) {
+                if (64 * p < KW && k < KW && (RPW == 1 || rmap(ray, rsl) < R)) {
                     const float z0 = zq[2 * p];
                     const float px = ox + z0 * dx, py = oy + z0 * dy, pz = oz + z0 * dz;  // nerf.py:252
                     const PointGeo geo = ST_GEO((sd_cfloat *)(a.cam_f + sbi * SD_CAM_WORDS), px, py, pz,
@@ -414,7 +421,7 @@ k_render_tile(const st_args sa) {
             *(uint4 *)(lds + ST_L_BOX + (slot * ST_WAVES + wave) * 16) = uint4{bmin0, bmax0, bmin1, bmax1};
     };
     auto ray_col = [&](int ray, int buf) {
-        if (ray + rsl < R && lane < KW) {
+        if (rmap(ray, rsl) < R && lane < KW) {
             float col[3];
             sd_color_finish(cpend, col);
             rq0(buf)[lane].w = __builtin_bit_cast(uint32_t, col[0]);
@@ -565,7 +572,7 @@ k_render_tile(const st_args sa) {
             Bh[s] = __builtin_bit_cast(typename Th::Frag, uint4{lo.x, lo.y, hi.x, hi.y});
         }
         const float ws = *(const float *)(lds + ST_L_WS + slot * 4);
-        const int ray = GR * grp + j;
+        const int ray = GR * grp + (RPW == 1 ? j : (j % RPW) * NW + j / RPW);  // hs row j = wave RPW + r
         const bool store = j < GR && ray < R;
         for (int dt = wave; dt < ndt; dt += ST_WAVES) {
             HFrag wl[4];
@@ -884,8 +891,8 @@ k_render_tile(const st_args sa) {
             }
             if (lane == 0) {
                 *(float *)(lds + ST_L_WS + (wave * RPW + r) * 4) = wsum;
-                a.depth[(int64_t)(ray + r) * a.ld_depth] = dsum;
-                float *rp = a.rgb + (int64_t)(ray + r) * a.ld_rgb;
+                a.depth[(int64_t)rmap(ray, r) * a.ld_depth] = dsum;
+                float *rp = a.rgb + (int64_t)rmap(ray, r) * a.ld_rgb;
                 rp[0] = c0s; rp[1] = c1s; rp[2] = c2s;
             }
         };
@@ -901,7 +908,7 @@ k_render_tile(const st_args sa) {
                 lane_off = (uint32_t)((tq & 1) + (tq >> 1) * cur.pitch) * ST_TEX + 8u * (uint32_t)tp;
             }
             const int r = RPW == 1 ? 0 : sub / nsub;
-            const bool act = cur.ok && ray + r < R;
+            const bool act = cur.ok && rmap(ray, r) < R;
             if (act) {
                 if (sub) itemA(sub, s0);
                 itemB(sub, s0);
@@ -912,7 +919,7 @@ k_render_tile(const st_args sa) {
             }
         }
         ST_T(6);
-        if (cur.ok && ray + RPW - 1 < R) ray_sums(RPW - 1);
+        if (cur.ok && rmap(ray, RPW - 1) < R) ray_sums(RPW - 1);
         if (cur.ok) {
             // per-sample outputs of the wave's RPW rays, lane = record k' (one coalesced store
             // per array)
@@ -921,8 +928,8 @@ k_render_tile(const st_args sa) {
                 const int kr = 64 * p + lane;
                 const int rr = RPW == 1 ? 0 : min(kr / K, RPW - 1);
                 const int k = kr - rr * K;
-                if (64 * p < KW && kr < KW && ray + rr < R) {
-                    const int64_t rk = (int64_t)(ray + rr) * K;
+                if (64 * p < KW && kr < KW && rmap(ray, rr) < R) {
+                    const int64_t rk = (int64_t)rmap(ray, rr) * K;
                     const f32x4 q1v = rq1(buf)[kr];
                     const uint4 q0v = rq0(buf)[kr];
                     const uint32_t fl = q0v.x >> 30;

@@ -469,6 +469,7 @@ class BTSNet(nn.Module):
             wb = _lib.render_proj_work_bytes(R, m.D)
             work = torch.empty(wb // 4, device=dev) if wb > 0 else None
             args.work = work.data_ptr() if work is not None else None
+            self._last_render_work = work  # diagnostics (tools/ovf_count.py: the overflow list)
             self._timed("render", lambda: _lib.render_proj(args, m.head_rec, rays))
         else:
             self._timed("render", lambda: _lib.render_fused(args, m.rec, rays))
