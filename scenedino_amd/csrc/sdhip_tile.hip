@@ -108,12 +108,14 @@ struct st_args {
 // LDS image (byte offsets): boxes, hidden sums, weight sums, ray words, then the sample
 // records [NW waves][2][K] x 40 B and two tile buffers.  The code-column and sigma A
 // fragments live in VGPRs for the whole kernel (loaded from global memory once).
-#define ST_L_BOX 0                                                                           // [2][NW waves] (min, max) per half ray, u16x2 packed
+// boxes [2][NW waves] x 32 B, u16x2 packed (min, max): per half ray (16 B), or, when a wave
+// step holds 64 samples (K R_pw = 64), per quarter = 16-sample row (halves = unions of two)
+#define ST_L_BOX 0
 // hidden-sum rows padded to 272 B: the DINO head reads the same 8-B slot of the NW rows in
 // one instruction (256-B rows put them on one bank pair: 8-way conflicts)
 #define ST_HS_ROW 272
 // rpw = rays per wave and step (2 for K <= 32: a group is NW rpw rays)
-__host__ __device__ constexpr int st_l_hs(int nw) { return ST_L_BOX + 2 * nw * 16; }         // [NW rpw rays][128] 16-bit hidden sums
+__host__ __device__ constexpr int st_l_hs(int nw) { return ST_L_BOX + 2 * nw * 32; }         // [NW rpw rays][128] 16-bit hidden sums
 __host__ __device__ constexpr int st_l_ws(int nw, int rpw) { return st_l_hs(nw) + nw * rpw * ST_HS_ROW; }  // [NW rpw] f32 weight sums
 __host__ __device__ constexpr int st_l_ray(int nw, int rpw) { return st_l_ws(nw, rpw) + 16 * 4; }          // [NW waves][2] x rpw x 32 B ray words 0..7 (LDS-DMA)
 __host__ __device__ constexpr int st_l_rec(int nw, int rpw) { return st_l_ray(nw, rpw) + nw * 2 * 32 * rpw; }  // records: [NW waves][2][rpw K] x 40 B
@@ -402,23 +404,31 @@ k_render_tile(const st_args sa) {
             }
         }
         ST_T(11);
+        uint8_t *bw = lds + ST_L_BOX + (slot * ST_WAVES + wave) * 32;
         if (KW == 64) {
-            // one sample per lane, halves = lanes [0, 32) and [32, 64): rows 0-1 / 2-3
+            // one sample per lane: quarter q = row q (items 4 q'.. of the step), halves =
+            // lanes [0, 32) and [32, 64)
             const uint32_t mnv = st_row_red2<false>(lane < 32 ? bmin0 : bmin1);
             const uint32_t mxv = st_row_red2<true>(lane < 32 ? bmax0 : bmax1);
-            bmin0 = st_rows2<false>(mnv, 0, 1);
-            bmax0 = st_rows2<true>(mxv, 0, 1);
-            bmin1 = st_rows2<false>(mnv, 2, 3);
-            bmax1 = st_rows2<true>(mxv, 2, 3);
+            uint32_t q[8];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                q[2 * r] = st_rows2<false>(mnv, r, r);
+                q[2 * r + 1] = st_rows2<true>(mxv, r, r);
+            }
+            ST_T(12);
+            if (lane == 0) {
+                *(uint4 *)bw = uint4{q[0], q[1], q[2], q[3]};
+                *(uint4 *)(bw + 16) = uint4{q[4], q[5], q[6], q[7]};
+            }
         } else {
             bmin0 = st_wave_min2(bmin0);
             bmax0 = st_wave_max2(bmax0);
             bmin1 = st_wave_min2(bmin1);
             bmax1 = st_wave_max2(bmax1);
+            ST_T(12);
+            if (lane == 0) *(uint4 *)bw = uint4{bmin0, bmax0, bmin1, bmax1};
         }
-        ST_T(12);
-        if (lane == 0)
-            *(uint4 *)(lds + ST_L_BOX + (slot * ST_WAVES + wave) * 16) = uint4{bmin0, bmax0, bmin1, bmax1};
     };
     auto ray_col = [&](int ray, int buf) {
         if (rmap(ray, rsl) < R && lane < KW) {
@@ -433,19 +443,32 @@ k_render_tile(const st_args sa) {
     struct Tile {
         int bx0, by0, tw, th, pitch, ok, split;
     };
-    // union of the NW waves' boxes of slot: which = 0 / 1 (half ray), 2 (whole ray)
-    auto box_union = [&](int slot, int which, uint32_t &mn, uint32_t &mx) {
-        const uint4 *bx = (const uint4 *)(lds + ST_L_BOX + slot * ST_WAVES * 16);
+    // union of the NW waves' boxes of slot over parts [p0, p1): a wave's entry holds NPART
+    // (min, max) pairs -- the 4 quarters when KW = 64, else the 2 halves -- so half h =
+    // parts [h NPART / 2, (h + 1) NPART / 2), the whole group = [0, NPART).  One copy of the
+    // code for every part range (a select chain per range grew the kernel by half: i-cache)
+    const int NPART = KW == 64 ? 4 : 2;
+    auto box_union = [&](int slot, int p0, int p1, uint32_t &mn, uint32_t &mx) {
+        // lane 2 i + h reads wave i's parts 2 h, 2 h + 1 (one LDS read; a loop over the parts
+        // was four dependent LDS round trips: +45 % stage time at C2), then a wave reduction
+        const uint4 *bx = (const uint4 *)(lds + ST_L_BOX + slot * ST_WAVES * 32);
         mn = 0xffffffffu;
         mx = 0u;
-#pragma unroll
-        for (int i = 0; i < ST_WAVES; ++i) {
-            const uint4 v = bx[i];
-            mn = st_min2(mn, which == 0 ? v.x : which == 1 ? v.z : st_min2(v.x, v.z));
-            mx = st_max2(mx, which == 0 ? v.y : which == 1 ? v.w : st_max2(v.y, v.w));
+        if (lane < 2 * ST_WAVES) {
+            const uint4 v = bx[lane];
+            const int pa = 2 * (lane & 1);
+            if (pa >= p0 && pa < p1) {
+                mn = v.x;
+                mx = v.y;
+            }
+            if (pa + 1 >= p0 && pa + 1 < p1) {
+                mn = st_min2(mn, v.z);
+                mx = st_max2(mx, v.w);
+            }
         }
-        mn = __builtin_amdgcn_readfirstlane(mn);
-        mx = __builtin_amdgcn_readfirstlane(mx);
+        static_assert(2 * ST_WAVES <= 16, "box entries in lane row 0");
+        mn = st_rows2<false>(st_row_red2<false>(mn), 0, 0);
+        mx = st_rows2<true>(st_row_red2<true>(mx), 0, 0);
     };
     // a box row of tw texels = tw x 18 16-B chunks = ceil(tw x 18 / 64) 1-KiB DMA pieces;
     // the box fits when its rows at the tile pitch fit the buffer
@@ -469,15 +492,24 @@ k_render_tile(const st_args sa) {
     // lanes past the row end are masked off (they are never read).
     auto dma = [&](const Tile &t, int tb, int sbi) {
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            (void *)((const uint8_t *)a.grid + (int64_t)sbi * plane_bytes), 0, plane_bytes, 0x00020000);
+            (void *)((const uint8_t *)a.grid + (int64_t)__builtin_amdgcn_readfirstlane(sbi) * plane_bytes), 0,
+            plane_bytes, 0x00020000);
         const uint32_t dst0 = lds0 + tile0 + (uint32_t)tb * (uint32_t)sa.tile_bytes;
         const int nk = (t.tw * ST_TEXQ + 63) >> 6;
         const uint32_t rowb = (uint32_t)t.pitch * ST_TEX;
+        // the lane id through a volatile move: the per-piece (tx, part) below are then
+        // computed here, not hoisted out of the step loop as 8 loop-invariant VGPRs (spilled
+        // at 256 VGPRs: a scratch reload -- and its vmcnt(0) -- in front of every DMA piece)
+        uint32_t ln = (uint32_t)lane;
+#ifndef ST_DMA_LNVOL
+#define ST_DMA_LNVOL 1
+#endif
+        if (ST_DMA_LNVOL) asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
 #pragma unroll
         for (int kk = 0; kk < ST_MAXKW; ++kk) {
             const int c = wave + ST_WAVES * kk;
             if (c >= nk) break;  // wave-uniform
-            const uint32_t ci = (uint32_t)c * 64u + (uint32_t)lane;
+            const uint32_t ci = (uint32_t)c * 64u + ln;
             const uint32_t tx = __umulhi(ci, 238609295u);  // ci / 18
             const uint32_t part = ci - 18u * tx;
             const uint32_t sx = (uint32_t)min(t.bx0 + (int)tx, Wf - 1);
@@ -493,20 +525,31 @@ k_render_tile(const st_args sa) {
     };
     // geometry of slot's group for tile buffer tb, DMA issued: the whole box if it fits,
     // else (nsub >= 2) the first half's box when both halves fit (split = 1: the second
-    // half is staged mid-step), else the group goes to the overflow list (ok = 0)
+    // half is staged mid-step), else (KW = 64) the first quarter's when all four fit
+    // (split = 3: restaged before items 1, 2, 3 -- the C1 offset-pose groups whose halves
+    // overflow, 0.25 % of the rays), else the group goes to the overflow list (ok = 0).
+    // An empty part (its rays past R) fits.
     auto stage = [&](int slot, int tb, int grp, int sbi) {
         uint32_t mn, mx;
-        box_union(slot, 2, mn, mx);
+        box_union(slot, 0, NPART, mn, mx);
         Tile t = geom(mn, mx);
         if (mn == 0xffffffffu) return t;  // no valid ray in the group
         if (!t.ok && nsub >= 2) {
-            uint32_t mn0, mx0, mn1, mx1;
-            box_union(slot, 0, mn0, mx0);
-            box_union(slot, 1, mn1, mx1);
-            const Tile h0 = geom(mn0, mx0), h1 = geom(mn1, mx1);
-            if (h0.ok && h1.ok) {
-                t = h0;
-                t.split = 1;
+#pragma unroll 1
+            for (int np = 2; np <= NPART; np *= 2) {  // halves, then quarters
+                bool all = true;
+                for (int q = 0; q < np && all; ++q) {
+                    uint32_t pn, px;
+                    box_union(slot, q * NPART / np, (q + 1) * NPART / np, pn, px);
+                    all = pn == 0xffffffffu || geom(pn, px).ok;
+                }
+                if (all) {
+                    box_union(slot, 0, NPART / np, mn, mx);
+                    t = geom(mn, mx);
+                    t.ok = 1;
+                    t.split = np - 1;
+                    break;
+                }
             }
         }
         if (!t.ok) {
@@ -529,11 +572,30 @@ k_render_tile(const st_args sa) {
     // second half ray's samples get the second half's geometry.
     auto tap_addrs = [&](int rbuf, int tb, const Tile &t, int ray_) {
         if (!t.ok || ray_ >= R) return;
-        Tile t2 = t;
-        if (t.split) {
+        // part q of a split group (split + 1 parts) = items [q nsubw / np, (q + 1) nsubw / np)
+        // of the step (as the box halves / quarters of ray_pass): its records' geometry
+        int gx[ST_MAXP], gy[ST_MAXP], gp[ST_MAXP];
+#pragma unroll
+        for (int p = 0; p < ST_MAXP; ++p) {
+            gx[p] = t.bx0;
+            gy[p] = t.by0;
+            gp[p] = t.pitch;
+        }
+        const int np = t.split + 1;
+#pragma unroll 1
+        for (int q = 1; q < np; ++q) {
             uint32_t mn1, mx1;
-            box_union(rbuf, 1, mn1, mx1);
-            t2 = geom(mn1, mx1);
+            box_union(rbuf, q * NPART / np, (q + 1) * NPART / np, mn1, mx1);
+            const Tile tq = geom(mn1, mx1);
+            const int s0 = q * nsubw / np, s1 = (q + 1) * nsubw / np;
+#pragma unroll
+            for (int p = 0; p < ST_MAXP; ++p) {
+                const int it = (64 * p + lane) >> 4;
+                const bool mine = it >= s0 && it < s1;
+                gx[p] = mine ? tq.bx0 : gx[p];
+                gy[p] = mine ? tq.by0 : gy[p];
+                gp[p] = mine ? tq.pitch : gp[p];
+            }
         }
         const uint32_t tbase = lds0 + tile0 + (uint32_t)tb * (uint32_t)sa.tile_bytes;
         uint32_t *w = (uint32_t *)rq0(rbuf);
@@ -542,9 +604,9 @@ k_render_tile(const st_args sa) {
             const int k = 64 * p + lane;
             if (64 * p < KW && k < KW) {
                 const uint32_t xy = w[4 * k];
-                const Tile &tt = (t.split && k >= kh) ? t2 : t;
+                const int bx0 = gx[p], by0 = gy[p], pch = gp[p];
                 const int x0 = (int)(xy & 0x7fffu), y0 = (int)((xy >> 15) & 0x7fffu);
-                const uint32_t ad = tbase + (uint32_t)(((y0 - tt.by0) * tt.pitch + (x0 - tt.bx0)) * ST_TEX);
+                const uint32_t ad = tbase + (uint32_t)(((y0 - by0) * pch + (x0 - bx0)) * ST_TEX);
                 w[4 * k] = ad | (xy & 0xc0000000u);
             }
         }
@@ -826,7 +888,9 @@ k_render_tile(const st_args sa) {
         // every wave: it holds barriers).  One item loop for both cases keeps the kernel
         // small (a second inlined copy of the items measured slower).
         // (RPW = 2: the first half is ray A -- a split group restages at the ray boundary)
-        const int nfirst = cur.split ? (nsubw >> 1) : nsubw;
+        // (split = 3: every quarter = item of the step is staged on its own)
+        const int npart = cur.split + 1;
+        int qn = 1, bnd = npart > 1 ? nsubw / npart : nsubw;  // the next part, its first item
         // ray epilogue of the wave's ray r: sums over the 16 sample lanes of every row
         auto ray_sums = [&](int r) {
             const float dsum = sd_rowsum16(dpart), wsum = sd_rowsum16(wpart);
@@ -897,11 +961,14 @@ k_render_tile(const st_args sa) {
             }
         };
         for (int sub = 0; sub < nsubw; ++sub) {
-            if (sub == nfirst) {
-                st_barrier_lds();  // every wave is done with the first half's taps
+            if (sub == bnd) {  // workgroup-uniform
+                st_barrier_lds();  // every wave is done with the previous part's taps
                 uint32_t mn1, mx1;
-                box_union(buf, 1, mn1, mx1);
-                cur = geom(mn1, mx1);  // fits: checked when the split was chosen
+                box_union(buf, qn * NPART / npart, (qn + 1) * NPART / npart, mn1, mx1);
+                ++qn;
+                bnd = qn < npart ? qn * nsubw / npart : nsubw;
+                cur = geom(mn1, mx1);  // fits (or is empty): checked when the split was chosen
+                cur.ok = 1;
                 dma(cur, buf, sbi);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 st_barrier_lds();
