@@ -219,6 +219,12 @@ int sd_render_proj(const sd_render_args *args, const sd_head *head, void *stream
 /* Bytes of args->work sd_render_proj needs for R rays and a D-dim DINO head (0: none). */
 int64_t sd_render_proj_work_bytes(int64_t R, int32_t D);
 
+/* Test hook: cap the tile kernel's tile buffers at `bytes` (rounded down to KiB; 0 = no cap;
+ * below 16 KiB the per-ray kernel renders everything), so a test can force tap boxes into
+ * the per-workgroup overflow lists and the per-ray fallback behind the tile kernel.  Returns
+ * the previous cap.  Process-wide, not thread-safe; the shipped path never sets it. */
+int32_t sd_render_tile_cap(int32_t bytes);
+
 /* Per-point field query without compositing (BTSNet.forward on raw points,
  * bts.py:476-595; SSCBench predict_grid / demo inference_3d).  Points are
  * (B, P, 3); outputs sigma (B,P), dino (B,P,D); colour outputs optional. */

@@ -190,6 +190,7 @@ SIGNATURES = {
     "sd_cast_grid": [_vp, _i64, ctypes.c_int, _vp, _vp],
     "sd_render_proj": [ctypes.POINTER(SdRenderArgs), ctypes.POINTER(SdHead), _vp],
     "sd_render_proj_work_bytes": [_i64, _i32],
+    "sd_render_tile_cap": [_i32],
     "sd_composite": [_vp, _vp, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp,
                      _vp],
     "sd_voxel_points": [ctypes.POINTER(ctypes.c_double), ctypes.c_double, _i64, _i64, _i64,
@@ -447,6 +448,11 @@ def project_grid(grid, mlp: SdMlp, dtype):
 
 def render_proj_work_bytes(R: int, D: int) -> int:
     return int(load().sd_render_proj_work_bytes(R, D))
+
+
+def render_tile_cap(nbytes: int) -> int:
+    """Test hook (sd_render_tile_cap): cap the tile buffers, returns the previous cap."""
+    return int(load().sd_render_tile_cap(int(nbytes)))
 
 
 def render_proj(args: SdRenderArgs, head: SdHead, ref_tensor):

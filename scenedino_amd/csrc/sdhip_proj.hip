@@ -409,14 +409,11 @@ k_render_proj(const sd_render_args a, const sd_head m, const int32_t *__restrict
     typedef typename Tr::Frag4 Frag4;
     typedef typename Tr::E E;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    if (list) {
-        // list mode: workgroups without a listed ray leave before staging the weights (the
-        // list is usually short or empty; the grid is sized for the worst case)
-        const int nx0 = (gridDim.x % 8 == 0) ? 8 : 1;
-        const int64_t ra = (int64_t)__builtin_amdgcn_readfirstlane(list[0]) * SD_LIST_BLK;
-        const int64_t x0 = blockIdx.x % nx0;
-        if ((ra * x0 / nx0) + (int64_t)(blockIdx.x / nx0) * (SD_RWG / 64) >= ra * (x0 + 1) / nx0) return;
-    }
+    // list mode (fallback behind the tile kernel, launched with its grid): workgroup b
+    // renders tile workgroup b's overflow list (sdhip_render.h), usually empty -- it leaves
+    // before staging the weights
+    const int nlist = list ? __builtin_amdgcn_readfirstlane(list[blockIdx.x]) : 0;
+    if (list && nlist == 0) return;
     {
         uint4 *d = (uint4 *)lds;
         const uint4 *pe = (const uint4 *)m.w_pe, *sg = (const uint4 *)m.w_sig,
@@ -446,19 +443,21 @@ k_render_proj(const sd_render_args a, const sd_head m, const int32_t *__restrict
     // a speed assumption only), so XCD x gets the contiguous rays [x R/8, (x+1) R/8): the
     // P rows its rays' epipolar lines cross stay in that XCD's 4 MiB L2 instead of every
     // XCD streaming all of P.  R below is this range's end.
-    const int nx = (gridDim.x % 8 == 0) ? 8 : 1;
+    // (list mode: one range -- the workgroup's own list)
+    const int nx = (!list && gridDim.x % 8 == 0) ? 8 : 1;
     const int xcd = blockIdx.x % nx;
-    const int nwaves = (gridDim.x / nx) * (SD_RWG / 64);
+    const int nwaves = list ? SD_RWG / 64 : (gridDim.x / nx) * (SD_RWG / 64);
     const int rps = (int)a.rays_per_sb;
-    // list != NULL (fallback behind the tile kernel): the rays of the blocks listed in
-    // list[1 .. list[0]] (SD_LIST_BLK consecutive rays each) form the virtual ray sequence
+    // list != NULL: the rays of the blocks in list b (SD_LIST_BLK consecutive rays each)
+    // form the virtual ray sequence of workgroup b
     const int Rreal = (int)a.R;
-    const int64_t RA = list ? (int64_t)__builtin_amdgcn_readfirstlane(list[0]) * SD_LIST_BLK : a.R;
+    const int64_t RA = list ? (int64_t)nlist * SD_LIST_BLK : a.R;
+    const int32_t *lblk = list ? list + gridDim.x + (int64_t)blockIdx.x * sd_ovf_cap(a.R, gridDim.x) : nullptr;
     auto rmap = [&](int v) {
-        return list ? min(list[1 + v / SD_LIST_BLK] * SD_LIST_BLK + v % SD_LIST_BLK, Rreal - 1) : v;
+        return list ? min(lblk[v / SD_LIST_BLK] * SD_LIST_BLK + v % SD_LIST_BLK, Rreal - 1) : v;
     };
     const int R = (int)(RA * (xcd + 1) / nx);
-    const int ray0 = (int)(RA * xcd / nx) + (blockIdx.x / nx) * (SD_RWG / 64) + wave;
+    const int ray0 = (int)(RA * xcd / nx) + (list ? 0 : (blockIdx.x / nx) * (SD_RWG / 64)) + wave;
     if (ray0 >= R) return;
     const int nitems = ((R - ray0 + nwaves - 1) / nwaves) * nsub;
     // in-kernel z (a.z == NULL): sd_sample_z's arithmetic, jitter from the counter RNG
@@ -865,13 +864,16 @@ k_head_hc(const float *__restrict__ work, int64_t R, const sd_head m, float *__r
     const Frag *lw = (const Frag *)lds;
     const int lane = threadIdx.x & 63, j = lane & 15, g = lane >> 4;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // list != NULL: the rays of the listed groups (see k_render_proj)
-    const int64_t RA = list ? (int64_t)__builtin_amdgcn_readfirstlane(list[0]) * SD_LIST_BLK : R;
+    // list != NULL: workgroup b takes tile workgroup b's overflow list (see k_render_proj;
+    // launched with the tile grid)
+    const int64_t RA = list ? (int64_t)__builtin_amdgcn_readfirstlane(list[blockIdx.x]) * SD_LIST_BLK : R;
+    const int32_t *lblk = list ? list + gridDim.x + (int64_t)blockIdx.x * sd_ovf_cap(R, gridDim.x) : nullptr;
     const int64_t ntile = (RA + 15) / 16;
-    for (int64_t tile = (int64_t)blockIdx.x * (SD_PWG / 64) + wave; tile < ntile;
-         tile += (int64_t)gridDim.x * (SD_PWG / 64)) {
+    const int64_t t0 = list ? wave : (int64_t)blockIdx.x * (SD_PWG / 64) + wave;
+    const int64_t tstep = list ? SD_PWG / 64 : (int64_t)gridDim.x * (SD_PWG / 64);
+    for (int64_t tile = t0; tile < ntile; tile += tstep) {
         const int64_t v = min(tile * 16 + j, RA - 1);
-        const int64_t ray = list ? min((int64_t)list[1 + v / SD_LIST_BLK] * SD_LIST_BLK + v % SD_LIST_BLK, R - 1)
+        const int64_t ray = list ? min((int64_t)lblk[v / SD_LIST_BLK] * SD_LIST_BLK + v % SD_LIST_BLK, R - 1)
                                  : tile * 16 + j;
         const float *hs = work + (ray < R ? ray : R - 1) * SD_HC_STRIDE;
         Frag B[4];
@@ -991,6 +993,7 @@ static int sd_rp_launch(const sd_render_args &a, const sd_head &m, hipStream_t s
     }
     int64_t nblk;
     sd_launch_proj(k_render_proj<P, NV, NDT>, a.R, lds_bytes, s, nblk, SD_RWG);
+    if (list) nblk = sd_num_cus();  // list mode: the tile grid (workgroup b = list b)
     hipLaunchKernelGGL((k_render_proj<P, NV, NDT>), dim3((unsigned)nblk), dim3(SD_RWG), lds_bytes,
                        s, a, m, list);
     return sd_check_err();
@@ -1013,6 +1016,7 @@ static int sd_rp_ndt(const sd_render_args &a, const sd_head &m, hipStream_t s,
     const int lds_bytes = (m.D >> 4) * 4 * SD_WAVE * 16;
     int64_t nblk;
     sd_launch_proj(k_head_hc<P>, (a.R + 15) / 16, lds_bytes, s, nblk);
+    if (list) nblk = sd_num_cus();
     hipLaunchKernelGGL(k_head_hc<P>, dim3((unsigned)nblk), dim3(SD_PWG), lds_bytes, s, a.work, a.R,
                        m, a.dino, a.ld_dino, list);
     return sd_check_err();
@@ -1028,7 +1032,7 @@ static int64_t sd_hc_bytes(int64_t R, int32_t D) {
     return sd_head_hc(D) ? R * SD_HC_STRIDE * (int64_t)sizeof(float) : 0;
 }
 extern "C" int64_t sd_render_proj_work_bytes(int64_t R, int32_t D) {
-    return sd_hc_bytes(R, D) + ((4 * (1 + (R + SD_LIST_BLK - 1) / SD_LIST_BLK) + 15) / 16) * 16;
+    return sd_hc_bytes(R, D) + ((4 * sd_ovf_words(R, sd_num_cus()) + 15) / 16) * 16;
 }
 
 extern "C" int sd_render_tile_ok(const sd_render_args *a, const sd_head *m);

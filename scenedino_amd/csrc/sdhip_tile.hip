@@ -100,7 +100,8 @@ extern "C" int sd_tile_prof(unsigned long long *out, int reset) {
 struct st_args {
     sd_render_args a;
     sd_head m;
-    int32_t *ovf;           // [0]: overflow count, [1 + i]: overflowed 4-ray block index
+    int32_t *ovf;           // overflow lists (sdhip_render.h): [gridDim.x] counts, [gridDim.x][ovf_cap] blocks
+    int32_t ovf_cap;
     int32_t ngroups;        // ceil(R / NW)
     int32_t tile_bytes;     // bytes per tile buffer (multiple of 1024)
 };
@@ -272,7 +273,12 @@ k_render_tile(const st_args sa) {
     const int glo = (int)((int64_t)NG * xcd / nx), ghi = (int)((int64_t)NG * (xcd + 1) / nx);
     const int gfirst = glo + lb;
     const int nsteps = gfirst < ghi ? (ghi - gfirst + nwg - 1) / nwg : 0;
-    if (nsteps == 0) return;  // workgroup-uniform
+    int novf = 0;  // this workgroup's overflow blocks (workgroup-uniform)
+    int32_t *ovf_list = sa.ovf + gridDim.x + (int64_t)blockIdx.x * sa.ovf_cap;
+    if (nsteps == 0) {  // workgroup-uniform
+        if (threadIdx.x == 0) sa.ovf[blockIdx.x] = 0;
+        return;
+    }
 
     const float zstep = (float)(1.0 / (double)K), zend = (float)(1.0 - 1.0 / (double)K);
     const int64_t cplane = (int64_t)a.Hc * a.Wc * 4;
@@ -553,11 +559,11 @@ k_render_tile(const st_args sa) {
             }
         }
         if (!t.ok) {
-            if (wave == 0 && lane == 0) {  // the group's rays as NW / SD_LIST_BLK list blocks
-                const int i = atomicAdd(sa.ovf, GR / SD_LIST_BLK);
+            if (wave == 0 && lane == 0) {  // the group's rays as GR / SD_LIST_BLK list blocks
                 for (int b = 0; b < GR / SD_LIST_BLK; ++b)
-                    sa.ovf[1 + i + b] = grp * (GR / SD_LIST_BLK) + b;
+                    ovf_list[novf + b] = grp * (GR / SD_LIST_BLK) + b;
             }
+            novf += GR / SD_LIST_BLK;
             return t;
         }
         dma(t, tb, sbi);
@@ -1026,6 +1032,7 @@ k_render_tile(const st_args sa) {
         st_barrier_lds();  // Y: next tile complete; hsum of this group written
         ST_T(9);
     }
+    if (threadIdx.x == 0) sa.ovf[blockIdx.x] = novf;
     if (prev_ok) {
         if (HPRE == 1) {
             HFrag hw[4];
@@ -1072,9 +1079,18 @@ static int st_lds_fixed(int K) {
     return st_l_rec(nw, rpw) + st_rec_bytes(nw, K * rpw);
 }
 
+// test hook (sd_render_tile_cap): tile buffers capped at this many bytes, 0 = no cap
+static int st_cap_bytes = 0;
+extern "C" int32_t sd_render_tile_cap(int32_t bytes) {
+    const int prev = st_cap_bytes;
+    st_cap_bytes = bytes > 0 ? bytes : 0;
+    return prev;
+}
+
 static int st_tile_bytes(int K) {
     const int avail = 160 * 1024 - st_lds_fixed(K);
-    return ((avail / 2) / 1024) * 1024;
+    const int b = ((avail / 2) / 1024) * 1024;
+    return st_cap_bytes ? min(b, (st_cap_bytes / 1024) * 1024) : b;
 }
 
 // Can the tile kernel take this render?  (colour in exactly one render view, batches of
@@ -1086,8 +1102,8 @@ extern "C" int sd_render_tile_ok(const sd_render_args *a, const sd_head *m) {
            st_tile_bytes(a->K) >= 16 * 1024;
 }
 
-// Launch; ovf: device int32 [1 + ceil(R / SD_LIST_BLK)] (list entries are 4-ray blocks),
-// [0] zeroed by this call.
+// Launch; ovf: device int32 [sd_ovf_words(R, sd_num_cus())] (the per-workgroup overflow
+// lists, sdhip_render.h; every count written by the kernel).
 extern "C" int sd_render_tile_launch(const sd_render_args *a, const sd_head *m, int32_t *ovf,
                                      void *stream) {
     hipStream_t s = (hipStream_t)stream;
@@ -1095,18 +1111,12 @@ extern "C" int sd_render_tile_launch(const sd_render_args *a, const sd_head *m, 
     sa.a = *a;
     sa.m = *m;
     sa.ovf = ovf;
+    const int ncu = sd_num_cus();
+    sa.ovf_cap = (int32_t)sd_ovf_cap(a->R, ncu);
     const int nw = st_nw(a->K), rpw = st_rpw(a->K);
     sa.ngroups = (int)((a->R + nw * rpw - 1) / (nw * rpw));
     sa.tile_bytes = st_tile_bytes(a->K);
     const int lds_bytes = st_lds_fixed(a->K) + 2 * sa.tile_bytes;
-    if (hipMemsetAsync(ovf, 0, sizeof(int32_t), s) != hipSuccess) {
-        sd_set_error("sd_render_proj: overflow counter reset failed");
-        return -2;
-    }
-    int ncu = 0, dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
-        ncu = 256;
     auto go = [&](auto kern) {
         sd_lds_attr((const void *)kern, lds_bytes);
         hipLaunchKernelGGL(kern, dim3((unsigned)ncu), dim3(64 * nw), lds_bytes, s, sa);

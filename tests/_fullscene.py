@@ -28,15 +28,19 @@ def full_scene(seed, gh, gw, precision, dev, H=192, W=640, C=256):
     return net, Kn
 
 
-def render_full_offset(d, precision, dev="cuda"):
-    """The golden's 192x640x64 offset-pose render on the build (jitter injected)."""
+def render_full_offset(d, precision, dev="cuda", nets=None, K=64):
+    """The golden's 192x640x64 offset-pose render on the build (jitter injected).  nets: a
+    list the BTSNet is appended to (tests that read its render scratch); K != 64: the same
+    scene at K samples per ray (no golden: self-consistency tests)."""
     from scenedino_amd.renderer import NeRFRenderer
     from scenedino_amd.common.ray_sampler import ImageRaySampler
     net, Kn = full_scene(int(d["scene_seed"]), 192, 640, precision, dev)
+    if nets is not None:
+        nets.append(net)
     pose = torch.as_tensor(d["render_pose"]).to(dev)
     rays, _ = ImageRaySampler(3, 80, 192, 640).sample(None, pose, Kn)
-    u = torch.rand(rays.shape[1], 64, generator=torch.Generator().manual_seed(int(d["u_seed"])))
-    r = NeRFRenderer(n_coarse=64, lindisp=True, hard_alpha_cap=False, eval_batch_size=65536)
+    u = torch.rand(rays.shape[1], K, generator=torch.Generator().manual_seed(int(d["u_seed"])))
+    r = NeRFRenderer(n_coarse=K, lindisp=True, hard_alpha_cap=False, eval_batch_size=65536)
     r.z_jitter = u.to(dev)
     with torch.no_grad():
         return r.bind_parallel(net).eval()(rays, want_weights=True, want_alphas=True)["coarse"]

@@ -494,6 +494,60 @@ def test_render_full_offset_pose_vs_reference(precision):
         assert abs(float(c["depth"].double().mean()) - float(d["depth_mean"])) < 1e-3
 
 
+def _overflow_blocks(net, R):
+    """4-ray blocks in the tile kernel's per-workgroup overflow lists of net's last render
+    (the tail of its sd_render_proj work: [ncu] counts, [ncu][cap] blocks, sdhip_render.h)."""
+    work = net._last_render_work.view(torch.int32)
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    cap = ((R + ncu - 1) // ncu + 64) // 4 + 1
+    words = ((4 * (ncu + ncu * cap) + 15) // 16) * 16 // 4
+    cnt = work[work.numel() - words:][:ncu]
+    assert int(cnt.min()) >= 0 and int(cnt.max()) <= cap
+    return int(cnt.sum())
+
+
+@pytest.mark.parametrize("K", [64, 32])
+def test_tile_overflow_fallback_full_offset(K):
+    """The offset-pose C2 render (and the C1-like K = 32, two rays per wave) with the tile
+    buffers capped at 16 KiB (sd_render_tile_cap) so that groups overflow -- whole boxes,
+    halves and quarters: the per-workgroup overflow lists and the per-ray kernel behind the
+    tile kernel render them.  The uncapped renders never overflow at these shapes, so this
+    is the fallback's test.  K = 64: the golden checks of
+    test_render_full_offset_pose_vs_reference (bf16); both: the lists hold rays and the
+    frame matches the uncapped one within the 16-bit contract."""
+    import hashlib
+    from _fullscene import render_full_offset
+    from scenedino_amd import _lib
+    d = load("render_full_offset.npz")
+    nets = []
+    prev = _lib.render_tile_cap(16 * 1024)
+    try:
+        c = render_full_offset(d, "bf16", DEV, nets, K=K)
+        torch.cuda.synchronize()
+        nblk = _overflow_blocks(nets[0], 192 * 640)
+    finally:
+        _lib.render_tile_cap(prev)
+    assert nblk > 0, "the cap did not force an overflow"
+    if K == 64:
+        sha = lambda t: hashlib.sha256(t.cpu().numpy().tobytes()).hexdigest()
+        assert sha(c["invalid"]) == str(d["invalid_sha256"])
+        assert sha(c["invalid_features"]) == str(d["invalid_features_sha256"])
+        idx = torch.from_numpy(d["idx"])
+        sub = {k: c[k][0].cpu()[idx] for k in ("depth", "dino_features", "rgb", "weights")}
+        check_lowp(sub, {"depth": d["depth"], "dino_features": d["dino"], "rgb": d["rgb"],
+                         "weights": d["weights"]}, "bf16")
+        assert abs(float(c["depth"].double().mean()) - float(d["depth_mean"])) < 1e-3
+    # the whole capped frame is the uncapped one within the same 16-bit contract
+    nets = []
+    u = render_full_offset(d, "bf16", DEV, nets, K=K)
+    torch.cuda.synchronize()
+    assert _overflow_blocks(nets[0], 192 * 640) == 0
+    for k in ("invalid", "invalid_features"):
+        assert torch.equal(c[k], u[k]), k
+    keys = ("depth", "dino_features", "rgb", "weights")
+    check_lowp({k: c[k][0].cpu() for k in keys}, {k: u[k][0].cpu().numpy() for k in keys}, "bf16")
+
+
 @pytest.mark.parametrize("fx", ["render_k64_cap1.npz", "render_sb2_nv2_k16.npz"])
 @pytest.mark.parametrize("precision", ["bf16", "fp16"])
 def test_in_kernel_z_matches_sample_z(fx, precision):
