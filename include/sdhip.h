@@ -110,6 +110,12 @@ int sd_pack_image(const float *img_nchw, int64_t N, int64_t H, int64_t W, float 
 int sd_cam_records(const float *w2c, int64_t s_w, const float *Ks, int64_t s_k, int64_t n,
                    float *out, void *stream);
 
+/* sd_pack_image + sd_cam_records in one launch (the per-frame render inputs of
+ * BTSNet.encode's colour images and encoder cameras; same outputs as the two calls). */
+int sd_frame_inputs(const float *img_nchw, int64_t N, int64_t H, int64_t W, float *out_nhwc4,
+                    const float *w2c, int64_t s_w, const float *Ks, int64_t s_k, int64_t n,
+                    float *out_cam, void *stream);
+
 /* Per-point MLP parameters, pre-packed (by the host) into MFMA fragment order.
  * ResnetFC(n_blocks=0): out = W_out relu(W_in x + b_in) + b_out
  *   (scenedino/models/prediction_heads/resnetfc.py:135-203). */

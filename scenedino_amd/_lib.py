@@ -177,6 +177,7 @@ SIGNATURES = {
     "sd_pack_grid": [_vp, _i64, _i64, _i64, _i64, ctypes.c_int, _vp, _vp],
     "sd_pack_image": [_vp, _i64, _i64, _i64, _vp, _vp],
     "sd_cam_records": [_vp, _i64, _vp, _i64, _i64, _vp, _vp],
+    "sd_frame_inputs": [_vp, _i64, _i64, _i64, _vp, _vp, _i64, _vp, _i64, _i64, _vp, _vp],
     "sd_render_fused": [ctypes.POINTER(SdRenderArgs), ctypes.POINTER(SdMlp), _vp],
     "sd_field_query": [ctypes.POINTER(SdFieldArgs), ctypes.POINTER(SdMlp), _vp],
     "sd_field_gather": [_vp, _i64, _i64, _vp, _i32, _i32, _i32, _vp, _vp, _i32, _i32, _i32, _vp,
@@ -401,6 +402,32 @@ def pack_image(img_nchw):
     _check(lib.sd_pack_image(ptr(_req(img_nchw, "images")), N, H, W, ptr(out), stream_of(out)),
            "sd_pack_image")
     return out
+
+
+def _cam_operands(poses_w2c, Ks):
+    w = poses_w2c.float().reshape(-1, 4, 4)
+    k = Ks.float().reshape(-1, 3, 3)
+    if w.stride()[1:] != (4, 1):
+        w = w.contiguous()
+    if k.stride()[1:] != (3, 1):
+        k = k.contiguous()
+    n = w.shape[0]
+    if k.shape[0] != n:
+        raise ValueError("poses and intrinsics must have the same number of views")
+    return w, k, n, (w.stride(0) if n > 1 else 16), (k.stride(0) if n > 1 else 9)
+
+
+def frame_inputs(img_nchw, poses_w2c, Ks):
+    """pack_image(img_nchw) and cam_records(poses_w2c, Ks) in one launch (sd_frame_inputs)."""
+    lib = load()
+    N, c3, H, W = img_nchw.shape
+    assert c3 == 3, "colour images must have 3 channels"
+    w, k, n, sw, sk = _cam_operands(poses_w2c, Ks)
+    img = torch.empty(N, H, W, 4, device=img_nchw.device, dtype=torch.float32)
+    cam = torch.empty(*poses_w2c.shape[:-2], CAM_WORDS, device=w.device, dtype=torch.float32)
+    _check(lib.sd_frame_inputs(ptr(_req(img_nchw, "images")), N, H, W, ptr(img), ptr(w), sw,
+                               ptr(k), sk, n, ptr(cam), stream_of(img)), "sd_frame_inputs")
+    return img, cam
 
 
 def cam_records(poses_w2c, Ks):

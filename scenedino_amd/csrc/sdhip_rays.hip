@@ -194,10 +194,9 @@ __global__ void __launch_bounds__(256) k_pack_image(const float *__restrict__ in
 
 // Camera records (SD_CAM_WORDS floats, include/sdhip.h) for n views; one thread per word.
 // The fused projection K . w2c[:3] is accumulated in f64 and rounded once.
-__global__ void __launch_bounds__(256) k_cam_records(const float *__restrict__ w2c, int64_t s_w,
-                                                     const float *__restrict__ Ks, int64_t s_k,
-                                                     int64_t n, float *__restrict__ out) {
-    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void sd_cam_word(const float *__restrict__ w2c, int64_t s_w,
+                                            const float *__restrict__ Ks, int64_t s_k, int64_t n,
+                                            float *__restrict__ out, int64_t gid) {
     if (gid >= n * SD_CAM_WORDS) return;
     const int64_t v = gid / SD_CAM_WORDS;
     const int e = (int)(gid - v * SD_CAM_WORDS);
@@ -215,6 +214,31 @@ __global__ void __launch_bounds__(256) k_cam_records(const float *__restrict__ w
                     (double)k[3 * i + 2] * w[8 + c]);
     }
     out[gid] = r;
+}
+__global__ void __launch_bounds__(256) k_cam_records(const float *__restrict__ w2c, int64_t s_w,
+                                                     const float *__restrict__ Ks, int64_t s_k,
+                                                     int64_t n, float *__restrict__ out) {
+    sd_cam_word(w2c, s_w, Ks, s_k, n, out, (int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+}
+
+// k_pack_image and k_cam_records in one launch (a frame's render inputs: every kernel
+// boundary costs ~4-5 us at these sizes, rocprofv3): blocks [0, nbi) pack the image, the
+// rest write the camera records
+__global__ void __launch_bounds__(256) k_frame_inputs(const float *__restrict__ in, int64_t N,
+                                                      int64_t H, int64_t W, float *__restrict__ img,
+                                                      int64_t nbi, const float *__restrict__ w2c,
+                                                      int64_t s_w, const float *__restrict__ Ks,
+                                                      int64_t s_k, int64_t n, float *__restrict__ cam) {
+    if ((int64_t)blockIdx.x >= nbi) {
+        sd_cam_word(w2c, s_w, Ks, s_k, n, cam, ((int64_t)blockIdx.x - nbi) * blockDim.x + threadIdx.x);
+        return;
+    }
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t hw = H * W;
+    if (gid >= N * hw) return;
+    const int64_t b = gid / hw, p = gid - b * hw;
+    const float *s = in + b * 3 * hw + p;
+    *(f32x4 *)(img + gid * 4) = f32x4{s[0], s[hw], s[2 * hw], 0.f};
 }
 
 // ---------------------------------------------------------------------------
@@ -372,6 +396,21 @@ extern "C" int sd_pack_image(const float *img_nchw, int64_t N, int64_t H, int64_
     hipLaunchKernelGGL(k_pack_image, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                        (hipStream_t)stream, img_nchw, N, H, W, out_nhwc4);
     SD_CHECK_LAUNCH("sd_pack_image");
+    return 0;
+}
+
+extern "C" int sd_frame_inputs(const float *img_nchw, int64_t N, int64_t H, int64_t W,
+                               float *out_nhwc4, const float *w2c, int64_t s_w, const float *Ks,
+                               int64_t s_k, int64_t n, float *out_cam, void *stream) {
+    if (!img_nchw || !out_nhwc4 || N <= 0 || H <= 0 || W <= 0 || !w2c || !Ks || !out_cam ||
+        n <= 0 || s_w < 16 || s_k < 9) {
+        sd_set_error("sd_frame_inputs: invalid argument");
+        return -1;
+    }
+    const int64_t nbi = (N * H * W + 255) / 256, nbc = (n * SD_CAM_WORDS + 255) / 256;
+    hipLaunchKernelGGL(k_frame_inputs, dim3((unsigned)(nbi + nbc)), dim3(256), 0, (hipStream_t)stream,
+                       img_nchw, N, H, W, out_nhwc4, nbi, w2c, s_w, Ks, s_k, n, out_cam);
+    SD_CHECK_LAUNCH("sd_frame_inputs");
     return 0;
 }
 

@@ -327,7 +327,9 @@ class BTSNet(nn.Module):
                                       "(ids_encoder=[0], as every shipped config)")
         imgs = self.grid_c_imgs
         n, nv, c3, H, W = imgs.shape
-        img = _lib.pack_image(imgs.reshape(n * nv, c3, H, W).float().contiguous())
+        # the colour images and the encoder cameras in one launch (sd_frame_inputs)
+        img, cam_f = _lib.frame_inputs(imgs.reshape(n * nv, c3, H, W).float().contiguous(),
+                                       self.grid_f_poses_w2c[:, 0], self.grid_f_Ks[:, 0])
         # grid_nchw feeds the inference kernels only (packing / projection): held DETACHED.
         # A view with a grad_fn would keep the grid leaf's AccumulateGrad node alive across
         # steps, bound to the stream of the step that created it -- the round-4 graph-mode
@@ -337,7 +339,7 @@ class BTSNet(nn.Module):
         cache = {
             "grid_nchw": g.detach().reshape(B, C, Hf, Wf), "grid": None, "proj": None, "proj_key": None,
             "C": C, "Hf": Hf, "Wf": Wf, "B": B,
-            "cam_f": _cam_records(self.grid_f_poses_w2c[:, 0], self.grid_f_Ks[:, 0]),
+            "cam_f": cam_f,
             "img": img, "nv": nv, "Hc": H, "Wc": W,
         }
         if nv == 1 and getattr(self, "_same_views", False):

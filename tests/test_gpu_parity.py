@@ -143,6 +143,19 @@ def test_sample_z_rng_mode_stratified():
     assert torch.equal(z, z2)
 
 
+@pytest.mark.parametrize("n", [1, 3])
+def test_frame_inputs_equal_pack_image_and_cam_records(n):
+    """sd_frame_inputs (one launch) writes exactly what sd_pack_image + sd_cam_records do."""
+    from scenedino_amd import _lib
+    g = torch.Generator().manual_seed(7)
+    imgs = (torch.rand(n, 3, 37, 53, generator=g) * 2 - 1).to(DEV)
+    w2c = torch.linalg.inv(torch.eye(4).repeat(n, 1, 1) + 0.1 * torch.randn(n, 4, 4, generator=g)).to(DEV)
+    Ks = (torch.eye(3).repeat(n, 1, 1) + 0.2 * torch.rand(n, 3, 3, generator=g)).to(DEV)
+    img, cam = _lib.frame_inputs(imgs, w2c, Ks)
+    assert torch.equal(img, _lib.pack_image(imgs))
+    assert torch.equal(cam, _lib.cam_records(w2c, Ks))
+
+
 # --------------------------------------------------------------------------- field query
 @pytest.mark.parametrize("precision", ["fp32", "bf16", "fp16"])
 @pytest.mark.parametrize("fx", ["field_query.npz", "field_query_empty.npz"])
