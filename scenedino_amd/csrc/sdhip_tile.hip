@@ -64,8 +64,24 @@ extern "C" int sd_tile_prof(unsigned long long *out, int reset) {
     }
     return 0;
 }
+#elif defined(ST_MARK) && ST_MARK
+#define ST_T(i) asm volatile(";@T " #i)
 #else
 #define ST_T(i)
+#endif
+// diagnostic build only (ST_MARK=1): asm comments at the item-loop phase boundaries, for the
+// static instruction-category count of tools/tile_isa_count.py (no code of their own; the
+// scheduler may still move arithmetic across them, so the split is approximate)
+#ifndef ST_MARK
+#define ST_MARK 0
+#endif
+#if ST_MARK
+#define ST_M(i) asm volatile(";@M " #i)
+// a marker pinned after the value x is computed (and before its later uses)
+#define ST_MV(i, x) asm volatile(";@M " #i : "+v"(x))
+#else
+#define ST_M(i)
+#define ST_MV(i, x)
 #endif
 
 #ifndef ST_WAIT_FIX
@@ -755,6 +771,7 @@ k_render_tile(const st_args sa) {
             float alpha, excl, tmul, zk, col[3];
         };
         auto itemA = [&](int sub, IState &st) {
+            ST_M(20);
             const int kr = sub * 16 + j;                                 // record k'
             const int k = RPW == 1 ? kr : kr - (sub / nsub) * K;         // sample of its ray
             const uint4 q0 = rq0(buf)[kr];
@@ -775,6 +792,7 @@ k_render_tile(const st_args sa) {
 #pragma unroll
                 for (int r = 0; r < 2; ++r) base[c][r] = (aw[4 * (8 * c + r)] & 0x3ffffu) + lane_off;
             // block-diagonal weight fragments of the two K-chunks
+            ST_M(21);
             const uint32_t w01 = q0.y, w23 = q0.z;
             const uint4 b0 = {bc0 && !br1 ? w01 : 0u, bc0 && !br1 ? w23 : 0u,
                               bc0 && br1 ? w01 : 0u, bc0 && br1 ? w23 : 0u};
@@ -791,6 +809,7 @@ k_render_tile(const st_args sa) {
                 acc[t] = Tr::mma(A0, B0, zero4);
                 acc[t] = Tr::mma(A1, B1, acc[t]);
             }
+            ST_MV(22, acc[7]);
             // positional-code columns: all 16x16x32 steps first, then the 16x16x16 ones
             // (a 16x16x16 MFMA whose accumulator input is the result of the directly
             // preceding 16x16x32 MFMA read a stale accumulator: hipcc 7.2, gfx950,
@@ -804,6 +823,7 @@ k_render_tile(const st_args sa) {
 #pragma unroll
                 for (int t = 0; t < 8; ++t) acc[t] = Tr::mma16(wpe1[t], f1, acc[t]);
             }
+            ST_MV(23, acc[7]);
 #pragma unroll
             for (int s2 = 0; s2 < 4; ++s2) {
                 const uint4 u = {sd_relu2(sd_pack2<E>(acc[2 * s2][0], acc[2 * s2][1])),
@@ -812,6 +832,7 @@ k_render_tile(const st_args sa) {
                                  sd_relu2(sd_pack2<E>(acc[2 * s2 + 1][2], acc[2 * s2 + 1][3]))};
                 st.X[s2] = __builtin_bit_cast(Frag, u);
             }
+            ST_MV(24, st.X[3]);
             f32x4 sg = zero4;
 #pragma unroll
             for (int s2 = 0; s2 < 4; ++s2) sg = Tr::mma(__builtin_bit_cast(Frag, wsig_r[s2]), st.X[s2], sg);
@@ -823,8 +844,10 @@ k_render_tile(const st_args sa) {
             st.alpha = alpha;
             st.excl = SD_DPP1(incl, 0x111);
             st.tmul = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, incl), 15));
+            ST_MV(25, st.tmul);
         };
         auto itemB = [&](int sub, const IState &st) {
+            ST_M(26);
             const int k = sub * 16 + j;  // record k'
             const float w = st.alpha * (Tc * st.excl);
             Tc *= st.tmul;
@@ -833,6 +856,7 @@ k_render_tile(const st_args sa) {
             cpart[0] += w * st.col[0];
             cpart[1] += w * st.col[1];
             cpart[2] += w * st.col[2];
+            ST_MV(27, cpart[2]);
 #if ST_HC16
             // hidden-space compositing: one v_pk_fma_f16 per packed pair of relu(h) (X is f16
             // in both modes, RMode)
@@ -864,6 +888,7 @@ k_render_tile(const st_args sa) {
             // weight and alpha into the sample's record (q1.x / .y are dead once itemA has
             // read the point); the ray epilogue stores every per-sample output coalesced
             if (g == 0) *(float2 *)&rq1(buf)[k] = float2{w, st.alpha};
+            ST_M(28);
         };
 
         // item 0 with the next ray's pass and the previous group's head
