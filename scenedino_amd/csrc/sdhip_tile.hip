@@ -210,6 +210,23 @@ __device__ __forceinline__ void st_barrier_lds() {
 
 typedef __attribute__((address_space(3))) void lds_void;
 
+// Diagnostic switch ST_WT=1: output stores write-through (sc1: the line leaves the XCD's L2
+// clean), so that the ~15 MB of outputs still dirty in L2 when the kernel ends are not
+// written back at the next kernel boundary (rocprofv3 WRITE_SIZE of the launch behind).
+// Measured no faster (C1 0.406-0.409 vs 0.401-0.409, C2 0.620-0.628 vs 0.614-0.616 ms,
+// `profiles/r5_wt_ab.txt`): the write-back is overlapped or replaced by the write-through
+// traffic inside the kernel.  Off.
+#ifndef ST_WT
+#define ST_WT 0
+#endif
+typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_out(float *p, float v) {
+    if (ST_WT)
+        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+        *p = v;
+}
+
 // 4-byte LDS-DMA (ray words), inline asm for the reason given at sd_dma16 (sdhip_render.h)
 __device__ __forceinline__ void st_dma4(const void *src, uint32_t lds_addr) {
     lds_addr = __builtin_amdgcn_readfirstlane(lds_addr);
@@ -675,7 +692,17 @@ k_render_tile(const st_args sa) {
             f32x4 res;
 #pragma unroll
             for (int r = 0; r < 4; ++r) res[r] = o[r] + ws * bd[r];
-            if (store) *(f32x4 *)(a.dino + (int64_t)ray * a.ld_dino + dim) = res;
+            if (store) {
+                if (ST_WT) {  // 16-B write-through store (buffer aux 16 = sc1)
+                    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                        (void *)(a.dino + (int64_t)GR * grp * a.ld_dino), 0, 0x7fffffff, 0x00020000);
+                    __builtin_amdgcn_raw_buffer_store_b128(
+                        __builtin_bit_cast(u32x4v, res), rs,
+                        (uint32_t)(((int64_t)(ray - GR * grp) * a.ld_dino + dim) * 4), 0, 16);
+                } else {
+                    *(f32x4 *)(a.dino + (int64_t)ray * a.ld_dino + dim) = res;
+                }
+            }
         }
     };
 
@@ -986,9 +1013,9 @@ k_render_tile(const st_args sa) {
             }
             if (lane == 0) {
                 *(float *)(lds + ST_L_WS + (wave * RPW + r) * 4) = wsum;
-                a.depth[(int64_t)rmap(ray, r) * a.ld_depth] = dsum;
+                st_out(a.depth + (int64_t)rmap(ray, r) * a.ld_depth, dsum);
                 float *rp = a.rgb + (int64_t)rmap(ray, r) * a.ld_rgb;
-                rp[0] = c0s; rp[1] = c1s; rp[2] = c2s;
+                st_out(rp, c0s); st_out(rp + 1, c1s); st_out(rp + 2, c2s);
             }
         };
         for (int sub = 0; sub < nsubw; ++sub) {
@@ -1031,14 +1058,16 @@ k_render_tile(const st_args sa) {
                     const f32x4 q1v = rq1(buf)[kr];
                     const uint4 q0v = rq0(buf)[kr];
                     const uint32_t fl = q0v.x >> 30;
-                    if (a.weights) a.weights[rk + k] = q1v[0];
-                    if (a.alphas) a.alphas[rk + k] = q1v[1];
+                    if (a.weights) st_out(a.weights + rk + k, q1v[0]);
+                    if (a.alphas) st_out(a.alphas + rk + k, q1v[1]);
                     if (a.invalid_f) a.invalid_f[rk + k] = (uint8_t)(fl & 1u);
-                    if (a.invalid) a.invalid[rk + k] = fl ? 1.f : 0.f;
+                    if (a.invalid) st_out(a.invalid + rk + k, fl ? 1.f : 0.f);
                     if (a.rgb_samps) {
                         const float2 cgb = rqc(buf)[kr];
                         float *rsp = a.rgb_samps + (rk + k) * 3;
-                        rsp[0] = __builtin_bit_cast(float, q0v.w); rsp[1] = cgb.x; rsp[2] = cgb.y;
+                        st_out(rsp, __builtin_bit_cast(float, q0v.w));
+                        st_out(rsp + 1, cgb.x);
+                        st_out(rsp + 2, cgb.y);
                     }
                 }
             }
