@@ -219,6 +219,12 @@ typedef __attribute__((address_space(3))) void lds_void;
 #ifndef ST_WT
 #define ST_WT 0
 #endif
+#ifndef ST_EARLY_HW
+#define ST_EARLY_HW 0     // HPRE 3: the next head's W_dino loaded after staging (0: at step end)
+#endif
+#ifndef ST_EARLY_FETCH
+#define ST_EARLY_FETCH 1  // next-next step's ray words fetched after staging (0: at step end)
+#endif
 typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void st_out(float *p, float v) {
     if (ST_WT)
@@ -940,6 +946,12 @@ k_render_tile(const st_args sa) {
             nxt = stage(buf ^ 1, buf ^ 1, ngrp, nsbi);
             tap_addrs(buf ^ 1, buf ^ 1, nxt, nray);
         }
+        // the rays of step n + 2 into ray slot buf (its words, step n's rays, were read by
+        // the ray pass of step n - 1): issued here, they land under this step's items (issued
+        // in front of the closing vmcnt(0), as before, every step waited one memory latency)
+        if (ST_EARLY_FETCH && n + 2 < nsteps) ray_fetch(GR * (ngrp + nwg) + RPW * wave, buf);
+        // HPRE 3: the next step's head weights (this group's; hwn was read by this step's head)
+        if (ST_EARLY_HW && HPRE == 3 && cur.ok && wave < ndt) head_w(wave, hwn);
         ST_T(5);
         // split group: items of the first half ray from the current tile, then the second
         // half's box is staged into the same buffer (workgroup-uniform branch, taken by
@@ -1079,8 +1091,8 @@ k_render_tile(const st_args sa) {
         ray = nray;
         sbi = nsbi;
         cur = nxt;
-        if (n + 2 < nsteps) ray_fetch(GR * (ngrp + nwg) + RPW * wave, buf);  // rays of step n + 2
-        if (HPRE == 3 && prev_ok && wave < ndt) head_w(wave, hwn);  // the next head's W_dino
+        if (!ST_EARLY_FETCH && n + 2 < nsteps) ray_fetch(GR * (ngrp + nwg) + RPW * wave, buf);
+        if (!ST_EARLY_HW && HPRE == 3 && prev_ok && wave < ndt) head_w(wave, hwn);  // the next head's W_dino
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed
         ST_T(8);
         st_barrier_lds();  // Y: next tile complete; hsum of this group written
