@@ -219,8 +219,11 @@ typedef __attribute__((address_space(3))) void lds_void;
 #ifndef ST_WT
 #define ST_WT 0
 #endif
+#ifndef ST_WAIT_EARLY
+#define ST_WAIT_EARLY 1   // the step's DMA wait before the epilogue's stores (0: after them)
+#endif
 #ifndef ST_EARLY_HW
-#define ST_EARLY_HW 0     // HPRE 3: the next head's W_dino loaded after staging (0: at step end)
+#define ST_EARLY_HW ST_WAIT_EARLY  // HPRE 3: the next head's W_dino loaded after staging (0: at step end)
 #endif
 #ifndef ST_EARLY_FETCH
 #define ST_EARLY_FETCH 1  // next-next step's ray words fetched after staging (0: at step end)
@@ -1055,6 +1058,10 @@ k_render_tile(const st_args sa) {
                 reset();
             }
         }
+        // this wave's LDS-DMA (next tile, ray words) landed -- waited here, in front of the
+        // epilogue's output stores: vmcnt counts stores too, and a wait behind them held every
+        // step for their acknowledgement (~1 memory latency)
+        if (ST_WAIT_EARLY) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         ST_T(6);
         if (cur.ok && rmap(ray, RPW - 1) < R) ray_sums(RPW - 1);
         if (cur.ok) {
@@ -1093,7 +1100,7 @@ k_render_tile(const st_args sa) {
         cur = nxt;
         if (!ST_EARLY_FETCH && n + 2 < nsteps) ray_fetch(GR * (ngrp + nwg) + RPW * wave, buf);
         if (!ST_EARLY_HW && HPRE == 3 && prev_ok && wave < ndt) head_w(wave, hwn);  // the next head's W_dino
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed
+        if (!ST_WAIT_EARLY) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed
         ST_T(8);
         st_barrier_lds();  // Y: next tile complete; hsum of this group written
         ST_T(9);
