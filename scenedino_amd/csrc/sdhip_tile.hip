@@ -270,7 +270,12 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW
 k_render_tile(const st_args sa) {
     // the head's W_dino prefetch across the step boundary (mode 3) costs 16-20 VGPRs: the
     // two-rays-per-wave body (245 VGPRs) would spill, so it loads them inside the head
-    constexpr int HPRE = (RPW == 2 && ST_HEAD_PRE == 3) ? 2 : ST_HEAD_PRE;
+// RPW = 2 head mode: 2 (the W_dino loads inside the head); 1 (loaded before the ray pass,
+// head after it) spills 8 VGPRs at 256
+#ifndef ST_HPRE_RPW2
+#define ST_HPRE_RPW2 2
+#endif
+    constexpr int HPRE = (RPW == 2 && ST_HEAD_PRE == 3) ? ST_HPRE_RPW2 : ST_HEAD_PRE;
     constexpr int ST_WAVES = NW;
     constexpr int GR = NW * RPW;  // rays per group
     constexpr int ST_L_HS = st_l_hs(NW), ST_L_WS = st_l_ws(NW, RPW), ST_L_RAY = st_l_ray(NW, RPW),
