@@ -674,8 +674,12 @@ k_render_tile(const st_args sa) {
     // -- as a global load inside the head it put one memory latency in front of every step's
     // ray pass (C1 -1 %); at RPW = 1 the 4 VGPRs (and the rescheduling) cost more than the
     // load (`profiles/r5_bias_hoist_ab.txt`)
+#ifndef ST_BD_HOIST1
+#define ST_BD_HOIST1 0
+#endif
+    constexpr bool BDH = RPW == 2 || ST_BD_HOIST1;
     f32x4 bdw = {0.f, 0.f, 0.f, 0.f};
-    if (RPW == 2 && wave < ndt) bdw = *(const f32x4 *)(m.b_dino + 16 * wave + 4 * g);
+    if (BDH && wave < ndt) bdw = *(const f32x4 *)(m.b_dino + 16 * wave + 4 * g);
     auto head_w = [&](int dt, HFrag w[4]) {
         const HFrag *wo = (const HFrag *)m.w_out + (int64_t)dt * 4 * SD_WAVE + lane;
 #pragma unroll
@@ -708,7 +712,7 @@ k_render_tile(const st_args sa) {
             for (int s = 0; s < 4; ++s) o = Th::mma(wl[s], Bh[s], o);
             // rows 4 g + r of tile dt = dims 16 dt + 4 g + r, column j = ray slot
             const int dim = 16 * dt + 4 * g;
-            const f32x4 bd = (RPW == 2 && dt == wave) ? bdw : *(const f32x4 *)(m.b_dino + dim);
+            const f32x4 bd = (BDH && dt == wave) ? bdw : *(const f32x4 *)(m.b_dino + dim);
             f32x4 res;
 #pragma unroll
             for (int r = 0; r < 4; ++r) res[r] = o[r] + ws * bd[r];
