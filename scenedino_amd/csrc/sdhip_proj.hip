@@ -251,7 +251,13 @@ k_project_lds(const float *__restrict__ grid, int64_t npix, const sd_mlp m, uint
             const int row = 4 * wave + r;
             int64_t pix = c * 32 + 16 * (i & 1) + row;
             pix = pix < npix ? pix : npix - 1;
-            sd_dma16(grid + pix * 256 + 4 * lane, sb + (uint32_t)row * PJ_ROWB);
+#ifndef PJ_NT
+#define PJ_NT 1  // non-temporal grid stream (read once)
+#endif
+            if (PJ_NT)
+                sd_dma16_nt(grid + pix * 256 + 4 * lane, sb + (uint32_t)row * PJ_ROWB);
+            else
+                sd_dma16(grid + pix * 256 + 4 * lane, sb + (uint32_t)row * PJ_ROWB);
         }
     };
 #pragma unroll

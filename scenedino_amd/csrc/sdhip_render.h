@@ -31,6 +31,12 @@ __device__ __forceinline__ void sd_dma16(const void *src, uint32_t lds_addr) {
     asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
                  :: "v"(src), "s"(lds_addr) : "memory");
 }
+// the same with the non-temporal hint (a stream read once: the projection's grid sweep)
+__device__ __forceinline__ void sd_dma16_nt(const void *src, uint32_t lds_addr) {
+    lds_addr = __builtin_amdgcn_readfirstlane(lds_addr);
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off nt"
+                 :: "v"(src), "s"(lds_addr) : "memory");
+}
 
 // 16-bit element traits.  Blend of the pair-interleaved projected grid (k_project):
 // every dword of a row holds (P[x0][c], P[x1][c]) of one channel c, so a bilinear
