@@ -757,6 +757,9 @@ extern "C" int sd_wgrad(const sd_wgrad_args *g, void *stream) {
 #define MW_P2 (96 * 160)             // dW_o partial (rows 72.. and columns 136.. dropped)
 #define MW_PT (MW_P1 + MW_P2)
 #define MW_RING 3
+#ifndef MW_NT
+#define MW_NT 1  // the chunk rows LDS-DMA'd with the non-temporal hint
+#endif
 #ifndef MW_DIAG
 #define MW_DIAG 0  // diagnostic builds only (tools/build_variant.py): 1 no MFMA, 2 no DMA, 3 no partial stores
 #endif
@@ -839,7 +842,10 @@ __global__ void __launch_bounds__(512) k_mlp_wgrad(const sd_mlp_wgrad_args g) {
         for (int i = 0; i < 6; ++i) {
             if (i >= cw) break;
             if (upk[i] >= 0 && (upk[i] & 31) < nv && MW_DIAG != 2)
-                sd_dma16((const uint8_t *)ubase[i] + p0 * urb[i] + (upk[i] >> 5), udst[i] + st);
+                if (MW_NT)  // X / dH / dY rows are read once: non-temporal stream
+                    sd_dma16_nt((const uint8_t *)ubase[i] + p0 * urb[i] + (upk[i] >> 5), udst[i] + st);
+                else
+                    sd_dma16((const uint8_t *)ubase[i] + p0 * urb[i] + (upk[i] >> 5), udst[i] + st);
         }
     };
     // transposed-read lane address (k_wgrad): group G = lane >> 4, lane 4 q + pp of it

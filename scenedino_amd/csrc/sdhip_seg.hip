@@ -194,6 +194,9 @@ __device__ __forceinline__ bf16x8 sg_relu_b(const f32x16 &acc, int s) {
 // that the compiler does not fence every LDS read behind the DMA (m0 = LDS destination).
 #define SG_SLOT (16 * 1024)  // one tile: 16 Gram fragments, 8 M + 4 Wn2 fragments or 4 KiB fp8
 #define SG_NSLOT 3          // LDS slots (the M loop runs three deep)
+#ifndef SG_NT_IN
+#define SG_NT_IN 1          // the input codes (read once) with the non-temporal hint
+#endif
 __device__ __forceinline__ void sg_dma1k(const uint8_t *src, uint32_t lds_dst, int lane) {
     lds_dst = __builtin_amdgcn_readfirstlane(lds_dst);
     asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
@@ -306,7 +309,8 @@ __global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const void *__restri
             if (p < P && x16) {  // bf16 codes (sd_field_query dino_dtype SD_BF16): as loaded
                 const bf16x8 *src = (const bf16x8 *)dino_in + p * (SG_DR / 8);
 #pragma unroll
-                for (int s = 0; s < SG_DR / 16; ++s) xb[ct][s] = src[2 * s + hh];
+                for (int s = 0; s < SG_DR / 16; ++s)
+                    xb[ct][s] = SG_NT_IN ? __builtin_nontemporal_load(&src[2 * s + hh]) : src[2 * s + hh];
             } else if (p < P) {
                 const f32x4_t *src = (const f32x4_t *)((const float *)dino_in + p * SG_DR);
 #pragma unroll
