@@ -944,7 +944,12 @@ def c2_pose_run(args, world, rank, device, dist, offset_pose, host_stage):
             raise ValueError(f"--shard rows needs H ({H}) divisible by the world size ({world})")
         band = (y0 * W, y1 * W)
     Rr = band[1] - band[0] if band else R
-    gather = sdd.MapGather(Rr, 1 + D_DINO + 3, device, host_stage=host_stage) if dist else None
+    # frames are independent units: sharded with no data-path collective by
+    # default, every rank's maps stay on its GPU; --gather allgather adds the RCCL
+    # all-gather of the maps (under the next frame's render).  Row bands of one frame are
+    # gathered into the frame (that IS the frame's assembly).
+    use_gather = dist and (rows or args.gather == "allgather")
+    gather = sdd.MapGather(Rr, 1 + D_DINO + 3, device, host_stage=host_stage) if use_gather else None
     net.fused_mode = args.mode
     timer = KernelTimer()
     net.kernel_timer = timer
@@ -1074,7 +1079,8 @@ def main_c2(args, world, rank, device, dist, host_stage):
             "frames_per_gpu": 1, "rays_per_frame": R, "samples_per_ray": K_SAMPLES,
             "grid": [C_GRID, HF, WF],
             "parallelism": (f"rows{world}" if rows else f"frames{world}") +
-            (f"+{'rccl' if not host_stage else 'gloo-host'}_allgather" if world > 1 else ""),
+            (f"+{'rccl' if not host_stage else 'gloo-host'}_allgather"
+             if world > 1 and (rows or args.gather == "allgather") else ""),
             "dist_world_size": world,
         },
         "poses": {k: {kk: v[kk] for kk in ("value", "ms_per_step", "render_kernel_ms",
@@ -1129,6 +1135,10 @@ def main():
     ap.add_argument("--shard", default="frames", choices=["frames", "rows"],
                     help="c2 with N > 1: frames (frame r on rank r, configs[2]) or rows (one "
                          "frame's row bands across ranks, the north star's ray tiles)")
+    ap.add_argument("--gather", default="none", choices=["none", "allgather"],
+                    help="c2 --shard frames with N > 1: none (default: independent frames, no "
+                         "data-path collective) or allgather (RCCL all-gather of every rank's "
+                         "maps, overlapped with the next frame)")
     ap.add_argument("--identity-pose", action="store_true",
                     help="c2: time only the identity render pose (profiling runs)")
     ap.add_argument("--mode", default="proj", choices=["proj", "grid"],
