@@ -184,6 +184,9 @@ k_project(const float *__restrict__ grid, int64_t B, int C, int64_t HW, int W, c
 #define PJ_FULLROW 1               // 1: slots of 16 whole pixel rows (1-KiB DMAs); 0: half rows
 #endif
 #define PJ_NS 8                    // ring slots
+#ifndef PJ_WT
+#define PJ_WT 1                    // P stored write-through
+#endif
 #define PJ_ROWB (PJ_FULLROW ? 1040 : 528)  // LDS bytes per staged row: data + 16 B pad (conflict-free reads)
 #define PJ_SROWS (PJ_FULLROW ? 16 : 32)    // pixel rows per slot
 #define PJ_SLOT (PJ_SROWS * PJ_ROWB)
@@ -235,8 +238,17 @@ k_project_lds(const float *__restrict__ grid, int64_t npix, const sd_mlp m, uint
         for (int kk = 0; kk < 2; ++kk) {
             const int pp = 8 * wave + 4 * kk + (lane >> 4);
             const uint4 v = *(const uint4 *)(stg + pp * PJ_OUTROW + 16 * (lane & 15));
-            if (pix0 + pp < npix)
-                *(uint4 *)(out + (pix0 + pp) * (SD_DH / 2) + 4 * (lane & 15)) = v;
+            if (pix0 + pp < npix) {
+                if (PJ_WT) {  // write-through (sc1): P leaves L2 clean, no write-back at the boundary
+                    typedef unsigned u4v __attribute__((ext_vector_type(4)));
+                    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                        (void *)(out + pix0 * (SD_DH / 2)), 0, 0x7fffffff, 0x00020000);
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), rs,
+                                                           (uint32_t)(pp * SD_DH * 2 + 16 * (lane & 15)), 0, 16);
+                } else {
+                    *(uint4 *)(out + (pix0 + pp) * (SD_DH / 2) + 4 * (lane & 15)) = v;
+                }
+            }
         }
     };
 #if PJ_FULLROW
