@@ -130,6 +130,25 @@ __device__ __forceinline__ void cv_tile_of(int &mt, int &nt) {
 // SD_EPI_SHUF (the ConvTranspose2d(k, stride k) sub-pixel scatter, bf16); CONV: implicit
 // 3x3 im2col A rows (else dense A rows of stride lda: 1x1 / transposed convolutions);
 // RELU: ReLU on the A operand (the pre-activation of the residual conv units)
+// Output rows stored write-through (sc1, CV_WT): a full-chip layer's tens of MB of output
+// would otherwise sit partly dirty in L2 when the kernel ends, and the next launch writes
+// them back before it starts (MI355X_MICROARCH.md: boundary + dirty bytes / 6 TB/s).  Inline
+// asm with its own s_nop 1 (the data registers must not be rewritten before the store
+// reads them).
+#ifndef CV_WT
+#define CV_WT 1
+#endif
+__device__ __forceinline__ void cv_store16(uint8_t *p, uint4 v) {
+    if (CV_WT)
+    {
+        typedef unsigned u4v __attribute__((ext_vector_type(4)));
+        const u4v w = __builtin_bit_cast(u4v, v);
+        asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" :: "v"(p), "v"(w) : "memory");
+    }
+    else
+        *(uint4 *)p = v;
+}
+
 template <int BM, int BN, int EPI, bool CONV, bool RELU, bool RES>
 __global__ void __launch_bounds__(512) k_conv_big(sd_gemm_args g) {
     constexpr bool OUTF32 = EPI == SD_EPI_F32, STF32 = OUTF32 || RES;
@@ -406,7 +425,7 @@ __global__ void __launch_bounds__(512) k_conv_big(sd_gemm_args g) {
             }
             // element index of (m, n); SHUF: 8 columns inside one sub-pixel (cout % 8 == 0)
             const int64_t base = EPI == SD_EPI_SHUF ? sbase : m * g.ldo + n;
-            *(uint4 *)((uint8_t *)g.out + base * (OUTF32 ? 4 : 2)) = v;
+            cv_store16((uint8_t *)g.out + base * (OUTF32 ? 4 : 2), v);
         }
     }
 }
@@ -636,7 +655,7 @@ __global__ void __launch_bounds__(512) k_conv_halo(sd_gemm_args g) {
             } else {
                 v = *(const uint4 *)(reg + r * PITCH + ch * 16);
             }
-            *(uint4 *)((uint8_t *)g.out + (m * g.ldo + n) * (OUTF32 ? 4 : 2)) = v;
+            cv_store16((uint8_t *)g.out + (m * g.ldo + n) * (OUTF32 ? 4 : 2), v);
         }
     }
 }
