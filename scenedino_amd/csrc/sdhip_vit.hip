@@ -228,6 +228,24 @@ __device__ __forceinline__ void vt_ln_tail(const sd_gemm_args &g, const VtLnTail
     }
 }
 
+// GEMM output rows (the staged epilogue's 16-B stores) write-through (sc1, VT_WT): the next
+// launch then does not first write back this one's dirty L2 lines (MI355X_MICROARCH.md:
+// boundary + dirty bytes / 6 TB/s; the DPT convolutions gained the same way, sdhip_conv.hip)
+#ifndef VT_WT
+#define VT_WT 1
+#endif
+template <typename T, typename V>
+__device__ __forceinline__ void vt_store16(T *p, const V &v) {
+    static_assert(sizeof(V) == 16, "16-B store");
+    if (VT_WT) {
+        typedef unsigned u4v __attribute__((ext_vector_type(4)));
+        const u4v w = __builtin_bit_cast(u4v, v);
+        asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" :: "v"(p), "v"(w) : "memory");
+    } else {
+        *(V *)p = v;
+    }
+}
+
 template <int BM, int BN, int BK, int EPI, bool CONV>
 __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g, float *__restrict__ sk_slab, uint32_t *__restrict__ sk_cnt,
                                               VtLnTail lt) {
@@ -755,8 +773,8 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g, float *__restrict_
                 if (EPI == SD_EPI_F32) {  // f32 rows (the channels-last DPT grid): 2 x 16 B
                     float *o = (float *)g.out + base;
                     if (full) {
-                        *(vf4 *)o = vf4{v[0], v[1], v[2], v[3]};
-                        *(vf4 *)(o + 4) = vf4{v[4], v[5], v[6], v[7]};
+                        vt_store16(o, vf4{v[0], v[1], v[2], v[3]});
+                        vt_store16(o + 4, vf4{v[4], v[5], v[6], v[7]});
                     } else {
                         for (int u = 0; u < 8 && n + u < g.N; ++u) o[u] = v[u];
                     }
@@ -766,7 +784,7 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g, float *__restrict_
                     bf16x8 o;
 #pragma unroll
                     for (int u = 0; u < 8; ++u) o[u] = (__bf16)v[u];
-                    *(bf16x8 *)((__bf16 *)g.out + base) = o;
+                    vt_store16((__bf16 *)g.out + base, o);
                 } else {
                     for (int u = 0; u < 8 && n + u < g.N; ++u) ((__bf16 *)g.out)[base + u] = (__bf16)v[u];
                 }
