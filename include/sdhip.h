@@ -116,6 +116,12 @@ int sd_frame_inputs(const float *img_nchw, int64_t N, int64_t H, int64_t W, floa
                     const float *w2c, int64_t s_w, const float *Ks, int64_t s_k, int64_t n,
                     float *out_cam, void *stream);
 
+/* The operands of sd_frame_inputs, for sd_project_grid_nhwc_inputs below. */
+typedef struct sd_frame_args {
+    const float *img_nchw; int64_t N, H, W; float *out_nhwc4;
+    const float *w2c; int64_t s_w; const float *Ks; int64_t s_k; int64_t n; float *out_cam;
+} sd_frame_args;
+
 /* Per-point MLP parameters, pre-packed (by the host) into MFMA fragment order.
  * ResnetFC(n_blocks=0): out = W_out relu(W_in x + b_in) + b_out
  *   (scenedino/models/prediction_heads/resnetfc.py:135-203). */
@@ -205,6 +211,14 @@ int sd_project_grid(const float *grid_nchw, int64_t B, int64_t Hf, int64_t Wf,
  * DPT writes (its NCHW-shaped grid_f_features is a permuted view of it). */
 int sd_project_grid_nhwc(const float *grid_nhwc, int64_t B, int64_t Hf, int64_t Wf,
                          const sd_mlp *mlp, void *out, void *stream);
+
+/* sd_project_grid_nhwc + sd_frame_inputs(*frame) -- a new frame's render inputs -- in ONE
+ * launch where the streaming projection kernel takes the grid (C = 256): its workgroups
+ * pack the image and write the camera records before their grid sweep (one kernel
+ * boundary fewer per frame).  Same outputs as the two calls (which it makes otherwise). */
+int sd_project_grid_nhwc_inputs(const float *grid_nhwc, int64_t B, int64_t Hf, int64_t Wf,
+                                const sd_mlp *mlp, void *out, const sd_frame_args *frame,
+                                void *stream);
 
 /* Head of the projected render: code columns of W_in and the output layer, packed
  * for 16x16x32 MFMA (scenedino_amd/mlp_pack.py documents the fragment maps). */

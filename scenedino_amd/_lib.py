@@ -42,6 +42,13 @@ class SdMlp(ctypes.Structure):
     ]
 
 
+class SdFrameArgs(ctypes.Structure):
+    """sd_frame_args (include/sdhip.h): sd_frame_inputs' operands."""
+    _fields_ = [("img_nchw", _vp), ("N", _i64), ("H", _i64), ("W", _i64), ("out_nhwc4", _vp),
+                ("w2c", _vp), ("s_w", _i64), ("Ks", _vp), ("s_k", _i64), ("n", _i64),
+                ("out_cam", _vp)]
+
+
 class SdHead(ctypes.Structure):
     _fields_ = [
         ("w_pe", _vp), ("w_sig", _vp), ("w_out", _vp), ("b_dino", _vp),
@@ -188,6 +195,8 @@ SIGNATURES = {
                          _vp, _vp, _vp, _vp, _vp],
     "sd_project_grid": [_vp, _i64, _i64, _i64, ctypes.POINTER(SdMlp), _vp, _vp],
     "sd_project_grid_nhwc": [_vp, _i64, _i64, _i64, ctypes.POINTER(SdMlp), _vp, _vp],
+    "sd_project_grid_nhwc_inputs": [_vp, _i64, _i64, _i64, ctypes.POINTER(SdMlp), _vp,
+                                    ctypes.POINTER(SdFrameArgs), _vp],
     "sd_cast_grid": [_vp, _i64, ctypes.c_int, _vp, _vp],
     "sd_render_proj": [ctypes.POINTER(SdRenderArgs), ctypes.POINTER(SdHead), _vp],
     "sd_render_proj_work_bytes": [_i64, _i32],
@@ -471,6 +480,29 @@ def project_grid(grid, mlp: SdMlp, dtype):
     _check(lib.sd_project_grid(ptr(_req(grid.contiguous(), "grid")), B, H, W, ctypes.byref(mlp),
                                ptr(out), stream_of(out)), "sd_project_grid")
     return out
+
+
+def project_grid_inputs(grid, mlp: SdMlp, dtype, img_nchw, poses_w2c, Ks):
+    """project_grid(grid) and frame_inputs(img_nchw, poses_w2c, Ks) in one launch
+    (sd_project_grid_nhwc_inputs; channels-last grids -- others take the two calls).
+    Returns (P, packed image, camera records)."""
+    if not channels_last(grid):
+        img, cam = frame_inputs(img_nchw, poses_w2c, Ks)
+        return project_grid(grid, mlp, dtype), img, cam
+    lib = load()
+    B, C, H, W = grid.shape
+    N, c3, Hc, Wc = img_nchw.shape
+    assert c3 == 3, "colour images must have 3 channels"
+    w, k, n, sw, sk = _cam_operands(poses_w2c, Ks)
+    out = torch.empty(B, H, W, 128, device=grid.device, dtype=TORCH_DTYPE[FIELD_DTYPE[dtype]])
+    img = torch.empty(N, Hc, Wc, 4, device=img_nchw.device, dtype=torch.float32)
+    cam = torch.empty(*poses_w2c.shape[:-2], CAM_WORDS, device=w.device, dtype=torch.float32)
+    fa = SdFrameArgs(img_nchw=ptr(_req(img_nchw, "images")), N=N, H=Hc, W=Wc, out_nhwc4=ptr(img),
+                     w2c=ptr(w), s_w=sw, Ks=ptr(k), s_k=sk, n=n, out_cam=ptr(cam))
+    _check(lib.sd_project_grid_nhwc_inputs(ptr(_req(grid.permute(0, 2, 3, 1), "grid")), B, H, W,
+                                           ctypes.byref(mlp), ptr(out), ctypes.byref(fa),
+                                           stream_of(out)), "sd_project_grid_nhwc_inputs")
+    return out, img, cam
 
 
 def render_proj_work_bytes(R: int, D: int) -> int:

@@ -27,6 +27,45 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 
+// Per-frame render inputs (sd_frame_inputs): work item gid < N H W packs pixel gid of the
+// NCHW colour images into NHWC4; gid - N H W < n SD_CAM_WORDS writes one camera-record word
+// (the fused projection K . w2c[:3] accumulated in f64, rounded once)
+__device__ __forceinline__ void sd_cam_word(const float *__restrict__ w2c, int64_t s_w,
+                                            const float *__restrict__ Ks, int64_t s_k, int64_t n,
+                                            float *__restrict__ out, int64_t gid) {
+    if (gid >= n * SD_CAM_WORDS) return;
+    const int64_t v = gid / SD_CAM_WORDS;
+    const int e = (int)(gid - v * SD_CAM_WORDS);
+    const float *w = w2c + v * s_w, *k = Ks + v * s_k;
+    float r;
+    if (e < 12) {
+        r = w[e];
+    } else if (e < 21) {
+        r = k[e - 12];
+    } else if (e < 24) {
+        r = 0.f;
+    } else {
+        const int i = (e - 24) >> 2, c = (e - 24) & 3;
+        r = (float)((double)k[3 * i] * w[c] + (double)k[3 * i + 1] * w[4 + c] +
+                    (double)k[3 * i + 2] * w[8 + c]);
+    }
+    out[gid] = r;
+}
+__device__ __forceinline__ void sd_frame_item(const sd_frame_args &fa, int64_t gid) {
+    const int64_t hw = fa.H * fa.W, np = fa.N * hw;
+    if (gid >= np) {
+        sd_cam_word(fa.w2c, fa.s_w, fa.Ks, fa.s_k, fa.n, fa.out_cam, gid - np);
+        return;
+    }
+    const int64_t b = gid / hw, p = gid - b * hw;
+    const float *s = fa.img_nchw + b * 3 * hw + p;
+    typedef __attribute__((ext_vector_type(4))) float f4;
+    *(f4 *)(fa.out_nhwc4 + gid * 4) = f4{s[0], s[hw], s[2 * hw], 0.f};
+}
+__host__ __device__ inline int64_t sd_frame_items(const sd_frame_args &fa) {
+    return fa.N * fa.H * fa.W + fa.n * SD_CAM_WORDS;
+}
+
 #define SD_WAVE 64
 #define SD_DH 128          // ResnetFC d_hidden (configs/model/dino_downsampler.yaml:39)
 #define SD_PE_CHUNKS 3     // 39 positional-code features padded to 48 = 3 x 16

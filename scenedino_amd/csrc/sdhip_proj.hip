@@ -193,9 +193,10 @@ k_project(const float *__restrict__ grid, int64_t B, int C, int64_t HW, int W, c
 #define PJ_OUTROW 272              // staging row stride (256 B of P + 16 pad)
 #define PJ_LDS (PJ_NS * PJ_SLOT + 32 * PJ_OUTROW)
 
-template <int P>
+template <int P, bool FI>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1)))
-k_project_lds(const float *__restrict__ grid, int64_t npix, const sd_mlp m, uint32_t *__restrict__ out) {
+k_project_lds(const float *__restrict__ grid, int64_t npix, const sd_mlp m, uint32_t *__restrict__ out,
+              const sd_frame_args fa) {
     typedef T16<P> Tr;
     typedef typename Tr::Frag Frag;
     typedef typename Tr::E E;
@@ -204,6 +205,11 @@ k_project_lds(const float *__restrict__ grid, int64_t npix, const sd_mlp m, uint
     const int lane = threadIdx.x & 63, h = lane >> 5, li = lane & 31;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t nch = (npix + 31) / 32;
+    if (FI) {  // the frame's render inputs first (sd_project_grid_nhwc_inputs): grid-stride
+        const int64_t nfi = sd_frame_items(fa);
+        for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < nfi; t += (int64_t)gridDim.x * 256)
+            sd_frame_item(fa, t);
+    }
     if ((int64_t)blockIdx.x >= nch) return;  // workgroup-uniform
     const int my = (int)((nch - 1 - blockIdx.x) / gridDim.x + 1);  // chunks of this workgroup
 
@@ -945,8 +951,12 @@ static int sd_check_err() {
     return 0;
 }
 
+extern "C" int sd_frame_inputs(const float *img_nchw, int64_t N, int64_t H, int64_t W, float *out_nhwc4,
+                               const float *w2c, int64_t s_w, const float *Ks, int64_t s_k, int64_t n,
+                               float *out_cam, void *stream);
+
 static int sd_project_any(const float *grid, int64_t B, int64_t Hf, int64_t Wf, const sd_mlp *m,
-                          void *out, void *stream, bool nhwc) {
+                          void *out, void *stream, bool nhwc, const sd_frame_args *fa = nullptr) {
     if (!grid || !m || !out || !m->w_in || !m->b_in_h || B <= 0 || Hf <= 0 || Wf <= 0 ||
         m->d_hidden != SD_DH || m->C <= 0 || (m->C % 64) ||
         (m->dtype != SD_BF16 && m->dtype != SD_F16)) {
@@ -967,13 +977,20 @@ static int sd_project_any(const float *grid, int64_t B, int64_t Hf, int64_t Wf, 
         const int64_t nch = work;
         nblk = sd_num_cus();
         if (nblk > nch) nblk = nch;
+        const sd_frame_args none = {};
         auto go = [&](auto kern) {
             sd_lds_attr((const void *)kern, PJ_LDS);
             hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(256), PJ_LDS, s, grid, B * HW, *m,
-                               (uint32_t *)out);
+                               (uint32_t *)out, fa ? *fa : none);
         };
-        go(k_project_lds<SD_F16>);  // both 16-bit modes: P in f16 (RMode, sdhip_render.h)
+        // both 16-bit modes: P in f16 (RMode, sdhip_render.h)
+        if (fa) go(k_project_lds<SD_F16, true>); else go(k_project_lds<SD_F16, false>);
         return sd_check_err();
+    }
+    if (fa) {  // other grids: the frame inputs by their own launch
+        int rc = sd_frame_inputs(fa->img_nchw, fa->N, fa->H, fa->W, fa->out_nhwc4, fa->w2c, fa->s_w,
+                                 fa->Ks, fa->s_k, fa->n, fa->out_cam, stream);
+        if (rc) return rc;
     }
 #define SD_PROJ_LAUNCH(PP, NH)                                                                  \
     do {                                                                                        \
@@ -989,6 +1006,21 @@ static int sd_project_any(const float *grid, int64_t B, int64_t Hf, int64_t Wf, 
 extern "C" int sd_project_grid(const float *grid, int64_t B, int64_t Hf, int64_t Wf,
                                const sd_mlp *m, void *out, void *stream) {
     return sd_project_any(grid, B, Hf, Wf, m, out, stream, false);
+}
+
+extern "C" int sd_project_grid_nhwc_inputs(const float *grid, int64_t B, int64_t Hf, int64_t Wf,
+                                           const sd_mlp *m, void *out, const sd_frame_args *fa,
+                                           void *stream) {
+    if (!fa || !fa->img_nchw || !fa->out_nhwc4 || fa->N <= 0 || fa->H <= 0 || fa->W <= 0 || !fa->w2c ||
+        !fa->Ks || !fa->out_cam || fa->n <= 0 || fa->s_w < 16 || fa->s_k < 9) {
+        sd_set_error("sd_project_grid_nhwc_inputs: invalid frame arguments");
+        return -1;
+    }
+    if (((uintptr_t)grid & 15) || ((uintptr_t)fa->out_nhwc4 & 15)) {
+        sd_set_error("sd_project_grid_nhwc_inputs: grid and packed image must be 16-byte aligned");
+        return -1;
+    }
+    return sd_project_any(grid, B, Hf, Wf, m, out, stream, true, fa);
 }
 
 extern "C" int sd_project_grid_nhwc(const float *grid, int64_t B, int64_t Hf, int64_t Wf,

@@ -192,29 +192,8 @@ __global__ void __launch_bounds__(256) k_pack_image(const float *__restrict__ in
     *(f32x4 *)(out + gid * 4) = v;
 }
 
-// Camera records (SD_CAM_WORDS floats, include/sdhip.h) for n views; one thread per word.
-// The fused projection K . w2c[:3] is accumulated in f64 and rounded once.
-__device__ __forceinline__ void sd_cam_word(const float *__restrict__ w2c, int64_t s_w,
-                                            const float *__restrict__ Ks, int64_t s_k, int64_t n,
-                                            float *__restrict__ out, int64_t gid) {
-    if (gid >= n * SD_CAM_WORDS) return;
-    const int64_t v = gid / SD_CAM_WORDS;
-    const int e = (int)(gid - v * SD_CAM_WORDS);
-    const float *w = w2c + v * s_w, *k = Ks + v * s_k;
-    float r;
-    if (e < 12) {
-        r = w[e];
-    } else if (e < 21) {
-        r = k[e - 12];
-    } else if (e < 24) {
-        r = 0.f;
-    } else {
-        const int i = (e - 24) >> 2, c = (e - 24) & 3;
-        r = (float)((double)k[3 * i] * w[c] + (double)k[3 * i + 1] * w[4 + c] +
-                    (double)k[3 * i + 2] * w[8 + c]);
-    }
-    out[gid] = r;
-}
+// Camera records (SD_CAM_WORDS floats, include/sdhip.h) for n views; one thread per word
+// (sd_cam_word, sdhip_common.h).
 __global__ void __launch_bounds__(256) k_cam_records(const float *__restrict__ w2c, int64_t s_w,
                                                      const float *__restrict__ Ks, int64_t s_k,
                                                      int64_t n, float *__restrict__ out) {
@@ -222,23 +201,11 @@ __global__ void __launch_bounds__(256) k_cam_records(const float *__restrict__ w
 }
 
 // k_pack_image and k_cam_records in one launch (a frame's render inputs: every kernel
-// boundary costs ~4-5 us at these sizes, rocprofv3): blocks [0, nbi) pack the image, the
-// rest write the camera records
-__global__ void __launch_bounds__(256) k_frame_inputs(const float *__restrict__ in, int64_t N,
-                                                      int64_t H, int64_t W, float *__restrict__ img,
-                                                      int64_t nbi, const float *__restrict__ w2c,
-                                                      int64_t s_w, const float *__restrict__ Ks,
-                                                      int64_t s_k, int64_t n, float *__restrict__ cam) {
-    if ((int64_t)blockIdx.x >= nbi) {
-        sd_cam_word(w2c, s_w, Ks, s_k, n, cam, ((int64_t)blockIdx.x - nbi) * blockDim.x + threadIdx.x);
-        return;
-    }
+// boundary costs ~4-5 us at these sizes, rocprofv3): one work item per thread
+// (sd_frame_item, sdhip_common.h)
+__global__ void __launch_bounds__(256) k_frame_inputs(const sd_frame_args fa) {
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t hw = H * W;
-    if (gid >= N * hw) return;
-    const int64_t b = gid / hw, p = gid - b * hw;
-    const float *s = in + b * 3 * hw + p;
-    *(f32x4 *)(img + gid * 4) = f32x4{s[0], s[hw], s[2 * hw], 0.f};
+    if (gid < sd_frame_items(fa)) sd_frame_item(fa, gid);
 }
 
 // ---------------------------------------------------------------------------
@@ -407,9 +374,9 @@ extern "C" int sd_frame_inputs(const float *img_nchw, int64_t N, int64_t H, int6
         sd_set_error("sd_frame_inputs: invalid argument");
         return -1;
     }
-    const int64_t nbi = (N * H * W + 255) / 256, nbc = (n * SD_CAM_WORDS + 255) / 256;
-    hipLaunchKernelGGL(k_frame_inputs, dim3((unsigned)(nbi + nbc)), dim3(256), 0, (hipStream_t)stream,
-                       img_nchw, N, H, W, out_nhwc4, nbi, w2c, s_w, Ks, s_k, n, out_cam);
+    const sd_frame_args fa = {img_nchw, N, H, W, out_nhwc4, w2c, s_w, Ks, s_k, n, out_cam};
+    hipLaunchKernelGGL(k_frame_inputs, dim3((unsigned)((sd_frame_items(fa) + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, fa);
     SD_CHECK_LAUNCH("sd_frame_inputs");
     return 0;
 }

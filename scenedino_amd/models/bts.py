@@ -327,9 +327,8 @@ class BTSNet(nn.Module):
                                       "(ids_encoder=[0], as every shipped config)")
         imgs = self.grid_c_imgs
         n, nv, c3, H, W = imgs.shape
-        # the colour images and the encoder cameras in one launch (sd_frame_inputs)
-        img, cam_f = _lib.frame_inputs(imgs.reshape(n * nv, c3, H, W).float().contiguous(),
-                                       self.grid_f_poses_w2c[:, 0], self.grid_f_Ks[:, 0])
+        # the colour images and the encoder cameras (sd_frame_inputs) are made on first use
+        # (_frame): inside the projection launch when the projected render runs next
         # grid_nchw feeds the inference kernels only (packing / projection): held DETACHED.
         # A view with a grad_fn would keep the grid leaf's AccumulateGrad node alive across
         # steps, bound to the stream of the step that created it -- the round-4 graph-mode
@@ -339,15 +338,28 @@ class BTSNet(nn.Module):
         cache = {
             "grid_nchw": g.detach().reshape(B, C, Hf, Wf), "grid": None, "proj": None, "proj_key": None,
             "C": C, "Hf": Hf, "Wf": Wf, "B": B,
-            "cam_f": cam_f,
-            "img": img, "nv": nv, "Hc": H, "Wc": W,
+            "cam_f": None, "img": None, "cam_c": None, "nv": nv, "Hc": H, "Wc": W,
+            "frame": (imgs.reshape(n * nv, c3, H, W).float().contiguous(),
+                      self.grid_f_poses_w2c[:, 0], self.grid_f_Ks[:, 0]),
         }
-        if nv == 1 and getattr(self, "_same_views", False):
-            cache["cam_c"] = cache["cam_f"].view(B, 1, -1)
-        else:
-            cache["cam_c"] = _cam_records(self.grid_c_poses_w2c, self.grid_c_Ks)
         self._grid_cache, self._grid_key = cache, key
         return cache
+
+    def _set_frame(self, gc, img, cam_f):
+        B, nv = gc["B"], gc["nv"]
+        gc["img"], gc["cam_f"], gc["frame"] = img, cam_f, None
+        if nv == 1 and getattr(self, "_same_views", False):
+            gc["cam_c"] = cam_f.view(B, 1, -1)
+        else:
+            gc["cam_c"] = _cam_records(self.grid_c_poses_w2c, self.grid_c_Ks)
+
+    def _frame(self, gc):
+        """The cached frame's packed colour images and camera records (one sd_frame_inputs
+        launch, unless the projection launch already made them)."""
+        if gc["frame"] is not None:
+            imgs, w2c, Ks = gc["frame"]
+            self._set_frame(gc, *_lib.frame_inputs(imgs, w2c, Ks))
+        return gc
 
     def _grid_nhwc(self, gc):
         """Encoder grid packed NHWC in the field dtype (sd_render_fused / sd_field_query;
@@ -360,7 +372,13 @@ class BTSNet(nn.Module):
         """Projected grid P = W_in[:, :C] G + b_in, (B, Hf, Wf, 128) (sd_render_proj)."""
         if gc["proj"] is None or gc["proj_key"] != self._packed_key:
             g = gc["grid_nchw"].float()  # NCHW or the native encoder's channels-last grid
-            gc["proj"] = self._timed("project", lambda: _lib.project_grid(g, m.rec, m.dtype))
+            if gc["frame"] is not None:  # a new frame: its render inputs in the same launch
+                imgs, w2c, Ks = gc["frame"]
+                res = self._timed("project", lambda: _lib.project_grid_inputs(g, m.rec, m.dtype, imgs, w2c, Ks))
+                gc["proj"] = res[0]
+                self._set_frame(gc, res[1], res[2])
+            else:
+                gc["proj"] = self._timed("project", lambda: _lib.project_grid(g, m.rec, m.dtype))
             gc["proj_key"] = self._packed_key
         return gc["proj"]
 
@@ -451,6 +469,7 @@ class BTSNet(nn.Module):
         if z is not None:
             z = z.contiguous()
         grid = self._grid_proj(gc, m) if proj else self._grid_nhwc(gc)
+        self._frame(gc)
         args = _lib.SdRenderArgs(
             rays=rays.data_ptr(), ray_dim=rays.shape[1], R=R, rays_per_sb=R // sb, K=K,
             z=z.data_ptr() if z is not None else None, grid=grid.data_ptr(), Hf=gc["Hf"],
@@ -535,6 +554,7 @@ class BTSNet(nn.Module):
             m = self._mlp_projq()
         else:
             grid = self._grid_nhwc(gc)
+        self._frame(gc)
         n, P, _ = xyz.shape
         if n != gc["B"]:
             raise ValueError(f"xyz batch {n} != encoded batch {gc['B']}")
@@ -589,7 +609,7 @@ class BTSNet(nn.Module):
         head = self.heads[self.final_pred_head]
         if len(self.heads) != 1:
             raise NotImplementedError("the field path supports a single prediction head")
-        gc = self._grids()
+        gc = self._frame(self._grids())
         g = self.grid_f_features[self._scale]
         n, P, _ = xyz.shape
         if n != gc["B"]:

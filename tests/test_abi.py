@@ -54,7 +54,8 @@ def test_struct_layouts_match_the_c_header(tmp_path):
                "sd_seg_head": _lib.SdSegHead, "sd_gemm_args": _lib.SdGemmArgs,
                "sd_ssc_args": _lib.SdSscArgs, "sd_patch_args": _lib.SdPatchArgs,
                "sd_salience_args": _lib.SdSalienceArgs,
-               "sd_mlp_train_args": _lib.SdMlpTrainArgs, "sd_wgrad_args": _lib.SdWgradArgs}
+               "sd_mlp_train_args": _lib.SdMlpTrainArgs, "sd_wgrad_args": _lib.SdWgradArgs,
+               "sd_mlp_wgrad_args": _lib.SdMlpWgradArgs, "sd_frame_args": _lib.SdFrameArgs}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "sdhip.h"', "int main(void){"]
     for cname, py in structs.items():
         lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
