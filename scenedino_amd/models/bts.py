@@ -29,6 +29,11 @@ EPS = 1e-3  # scenedino/common/cameras/pinhole.py:3
 PRECISIONS = {"fp32": _lib.SD_F32, "bf16": _lib.SD_BF16, "fp16": _lib.SD_F16}
 
 
+# the frame's render inputs made inside the projection launch (sd_project_grid_nhwc_inputs);
+# SCENEDINO_AMD_FRAME_FUSED=0: their own sd_frame_inputs launch (A/B switch)
+_FRAME_FUSED = __import__("os").environ.get("SCENEDINO_AMD_FRAME_FUSED", "1") != "0"
+
+
 def voxel_chunks(n_points: int) -> int:
     """Chunks of a large predict_voxels query (SCENEDINO_AMD_VOXEL_CHUNKS, default 1: one
     field launch, then one seg-head launch); chunks below 2^18 points are not split."""
@@ -372,7 +377,7 @@ class BTSNet(nn.Module):
         """Projected grid P = W_in[:, :C] G + b_in, (B, Hf, Wf, 128) (sd_render_proj)."""
         if gc["proj"] is None or gc["proj_key"] != self._packed_key:
             g = gc["grid_nchw"].float()  # NCHW or the native encoder's channels-last grid
-            if gc["frame"] is not None:  # a new frame: its render inputs in the same launch
+            if gc["frame"] is not None and _FRAME_FUSED:  # a new frame: its render inputs in the same launch
                 imgs, w2c, Ks = gc["frame"]
                 res = self._timed("project", lambda: _lib.project_grid_inputs(g, m.rec, m.dtype, imgs, w2c, Ks))
                 gc["proj"] = res[0]
