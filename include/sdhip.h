@@ -20,7 +20,12 @@
  *               3x3), 3 zeros, then the fused projection P = K . w2c[:3] (12 floats,
  *               3x4, rounded once from an exact product) that the 16-bit render kernels
  *               use in place of the two-step pts_into_camera / project_to_image
- *   grid        (B, Hf, Wf, C) NHWC, element type f32 / bf16 / f16 (= the MLP dtype)
+ *   grid        (B, Hf, Wf, C) NHWC, element type = the FIELD dtype of the MLP dtype:
+ *               sd_field_dtype(SD_F32) = SD_F32, sd_field_dtype(SD_BF16) =
+ *               sd_field_dtype(SD_F16) = SD_F16 -- the bf16 mode keeps every operand
+ *               upstream of sigma (grid, W_in, projected grid, taps, code) in f16 and
+ *               only the DINO output layer in bf16.  The render / field
+ *               entry points check the caller's grid_dtype against it (ABI 10).
  *   colour img  (B, nv, Hc, Wc, 4) NHWC4 float32 (rgb + pad)
  */
 #ifndef SDHIP_H
@@ -40,8 +45,16 @@ enum sd_dtype { SD_F32 = 0, SD_BF16 = 1, SD_F16 = 2 };
 /* Last error text of the calling thread ("" if none). */
 const char *sd_last_error(void);
 
-/* Library / ABI version (bumped on any signature change). */
+/* Library / ABI version (bumped on any signature change).  10: grid_dtype fields in
+ * sd_render_args / sd_field_args, sd_field_dtype. */
 int sd_abi_version(void);
+
+/* Element type of the grids the field / render kernels read for an MLP of `dtype`
+ * (sd_mlp.dtype / sd_head.dtype): SD_F32 -> SD_F32, SD_BF16 and SD_F16 -> SD_F16.
+ * Returns -1 for an unknown dtype.  Pack a grid for sd_render_fused / sd_field_query with
+ * sd_pack_grid / sd_cast_grid(dtype = sd_field_dtype(mlp dtype)); sd_project_grid* write
+ * the projected grid in sd_field_dtype(mlp->dtype). */
+int sd_field_dtype(int dtype);
 
 /* Frustum ray generation, bit-exact with the reference's fp32 arithmetic.
  * Replaces util.unproj_map + util.gen_rays + ImageRaySampler.sample
@@ -81,9 +94,11 @@ typedef struct sd_patch_args {
 
 int sd_patch_rays(const sd_patch_args *args, void *stream);
 
-/* Channels-last f32 grid (n elements, n % 4 == 0) -> dtype (SD_BF16 / SD_F16), same layout:
- * the NHWC gather operand of sd_render_fused / sd_field_query when the grid already is
- * channels-last (sd_pack_grid transposes an NCHW one). */
+/* Channels-last f32 grid (n elements, n % 4 == 0) -> element type dtype (SD_BF16 / SD_F16),
+ * same layout: the NHWC gather operand of sd_render_fused / sd_field_query when the grid
+ * already is channels-last (sd_pack_grid transposes an NCHW one).  A plain conversion: for
+ * the render / field kernels pass dtype = sd_field_dtype(mlp dtype) (f16 in both 16-bit
+ * modes) and set grid_dtype to the same value. */
 int sd_cast_grid(const float *grid_nhwc, int64_t n, int dtype, void *out, void *stream);
 
 /* Stratified inverse-depth (lindisp) or linear z sampling.
@@ -93,7 +108,8 @@ int sd_cast_grid(const float *grid_nhwc, int64_t n, int dtype, void *out, void *
 int sd_sample_z(const float *rays, int64_t R, int64_t ray_dim, int64_t K, int lindisp,
                 const float *u, uint64_t seed, uint64_t offset, float *z_out, void *stream);
 
-/* NCHW float32 feature grid (B,C,H,W) -> NHWC (B,H,W,C) in dtype.
+/* NCHW float32 feature grid (B,C,H,W) -> NHWC (B,H,W,C) in element type dtype (a plain
+ * conversion; the render / field kernels read sd_field_dtype(mlp dtype), see above).
  * Layout step for F.grid_sample over BTSNet.grid_f_features (bts.py:299-309). */
 int sd_pack_grid(const float *grid_nchw, int64_t B, int64_t C, int64_t H, int64_t W,
                  int dtype, void *out_nhwc, void *stream);
@@ -135,7 +151,8 @@ typedef struct sd_mlp {
     int32_t C;             /* grid channels (multiple of 32)                               */
     int32_t D;             /* dino dims (multiple of 32)                                   */
     int32_t dtype;         /* SD_F32 (exact-f32 MFMA), SD_BF16 or SD_F16 (16-bit MFMA,   */
-                           /* f32 accumulate); the grid must be packed in the same dtype  */
+                           /* f32 accumulate); grids and w_in are in sd_field_dtype(dtype) */
+                           /* (f16 for SD_BF16 too), the dino output layer in dtype        */
     int32_t d_hidden;      /* must be 128                                                  */
     const float *b_empty_h; /* learn_empty (bts.py:311-319), NULL if off: [4][2][16]       */
                            /* b_in + W_in[:, :C] . empty_feature in accumulator-row order:  */
@@ -187,6 +204,11 @@ typedef struct sd_render_args {
      * render straight into one packed [dino | depth | rgb] row per ray, e.g. the send buffer
      * of the multi-GPU all-gather (sd_render_proj only; sd_render_fused requires 0). */
     int64_t ld_depth, ld_dino, ld_rgb;
+    /* Element type of `grid`, checked against what the kernel reads (ABI 10): sd_render_fused
+     * sd_field_dtype(mlp->dtype); sd_render_proj SD_F16 (the projected grid of both 16-bit
+     * modes).  A mismatch returns -1 instead of reading the bits as another type. */
+    int32_t grid_dtype;
+    int32_t pad1;
 } sd_render_args;
 
 int sd_render_fused(const sd_render_args *args, const sd_mlp *mlp, void *stream);
@@ -201,7 +223,8 @@ int sd_render_fused(const sd_render_args *args, const sd_mlp *mlp, void *stream)
  * the positional-code columns by MFMA.  Same outputs as sd_render_fused up to
  * rounding order (16-bit modes only; the f32 parity mode keeps sd_render_fused). */
 
-/* grid_nchw (B, C, Hf, Wf) float32 -> out (B, Hf, Wf, 128) in mlp->dtype (BF16/F16),
+/* grid_nchw (B, C, Hf, Wf) float32 -> out (B, Hf, Wf, 128) in sd_field_dtype(mlp->dtype)
+ * (f16 for both 16-bit modes; mlp->dtype must be SD_BF16 or SD_F16),
  * plain NHWC: out[b][y][x][n] = P[y][x][n], 256 B per grid pixel.
  * Uses mlp->w_in chunks 0..C/16-1 and mlp->b_in_h. */
 int sd_project_grid(const float *grid_nchw, int64_t B, int64_t Hf, int64_t Wf,
@@ -229,10 +252,12 @@ typedef struct sd_head {
     const float *b_dino;   /* b_out[1:1+D]                                            */
     float b_sigma;         /* b_out[0]                                                */
     int32_t D;             /* multiple of 16, <= 512                                  */
-    int32_t dtype;         /* SD_BF16 or SD_F16                                       */
+    int32_t dtype;         /* SD_BF16 or SD_F16: w_out (the DINO head) in dtype; w_pe and */
+                           /* w_sig in sd_field_dtype(dtype) = f16 in both modes          */
 } sd_head;
 
-/* args->grid = the projected grid (B, Hf, Wf, 128) from sd_project_grid; K % 16 == 0.
+/* args->grid = the projected grid (B, Hf, Wf, 128) f16 from sd_project_grid (grid_dtype
+ * SD_F16); K % 16 == 0.
  * Outputs as sd_render_fused; args->z may be NULL (in-kernel z sampling, see above). */
 int sd_render_proj(const sd_render_args *args, const sd_head *head, void *stream);
 
@@ -261,7 +286,7 @@ typedef struct sd_field_args {
     uint8_t *invalid_f;/* (B, P) or NULL       */
     int32_t dino_dtype;/* SD_F32 (0), or SD_BF16: dino written as bf16 (the input a
                         * following sd_seg_query rounds to bf16 anyway: half the bytes) */
-    int32_t pad0;
+    int32_t grid_dtype;/* element type of grid (ABI 10): sd_field_dtype(mlp->dtype); checked */
     /* Visiting order of the ceil(B P / 32) tiles of 32 consecutive points, or NULL (natural
      * order).  Speed only (every output stays at its point's index): an order in which
      * consecutive tiles project onto neighbouring texels keeps the grid taps in the XCD's

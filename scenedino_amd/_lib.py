@@ -14,7 +14,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # SDHIP_LIB: alternative build of the same library (diagnostic builds only)
 LIB_PATH = os.environ.get("SDHIP_LIB") or os.path.join(_HERE, "libsdhip.so")
-ABI_VERSION = 9
+ABI_VERSION = 10
 CAM_WORDS = 36  # floats per camera record (include/sdhip.h SD_CAM_WORDS)
 
 SD_F32 = 0
@@ -71,6 +71,7 @@ class SdRenderArgs(ctypes.Structure):
         ("z_lindisp", _i32), ("z_seed", ctypes.c_uint64), ("z_offset", ctypes.c_uint64),
         ("work", _vp),
         ("ld_depth", _i64), ("ld_dino", _i64), ("ld_rgb", _i64),
+        ("grid_dtype", _i32), ("pad1", _i32),
     ]
 
 
@@ -82,7 +83,7 @@ class SdFieldArgs(ctypes.Structure):
         ("img", _vp), ("nv", _i32), ("Hc", _i32), ("Wc", _i32),
         ("cam_c", _vp),
         ("sigma", _vp), ("dino", _vp), ("rgb", _vp), ("invalid", _vp), ("invalid_f", _vp),
-        ("dino_dtype", _i32), ("pad0", _i32), ("tile_order", _vp),
+        ("dino_dtype", _i32), ("grid_dtype", _i32), ("tile_order", _vp),
     ]
 
 
@@ -176,6 +177,7 @@ class SdSscArgs(ctypes.Structure):
 SIGNATURES = {
     "sd_last_error": [],
     "sd_abi_version": [],
+    "sd_field_dtype": [ctypes.c_int],
     "sd_ln_gemm": [ctypes.POINTER(SdGemmArgs), _vp, _vp, _vp, ctypes.c_float, _vp],
     "sd_gen_rays": [_vp, _vp, _vp, _i64, _i64, _i64, ctypes.c_float, ctypes.c_float, _vp, _vp],
     "sd_sample_z": [_vp, _i64, _i64, _i64, ctypes.c_int, _vp, ctypes.c_uint64, ctypes.c_uint64,

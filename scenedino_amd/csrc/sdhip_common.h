@@ -11,16 +11,20 @@
 #include <mutex>
 #include <unordered_map>
 
-// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per kernel (and on growth), not per
-// launch: a host call on every launch of the latency-bound eager paths otherwise
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (device, kernel) (and on growth),
+// not per launch: a host call on every launch of the latency-bound eager paths otherwise
+// (ADVICE r4).  Keyed by the current device too: the attribute is set while a device is
+// current, so a process driving several GPUs sets it once on each.
 static inline void sd_lds_attr(const void *kern, int bytes) {
     static std::mutex mu;
-    static std::unordered_map<const void *, int> set;
+    static std::unordered_map<const void *, int> set[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
     std::lock_guard<std::mutex> g(mu);
-    auto it = set.find(kern);
-    if (it != set.end() && it->second >= bytes) return;
+    auto it = set[dev].find(kern);
+    if (it != set[dev].end() && it->second >= bytes) return;
     (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-    set[kern] = bytes;
+    set[dev][kern] = bytes;
 }
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;

@@ -42,7 +42,13 @@ extern "C" void sd_set_error(const char *msg) {
     g_err[sizeof(g_err) - 1] = 0;
 }
 extern "C" const char *sd_last_error(void) { return g_err; }
-extern "C" int sd_abi_version(void) { return 9; }
+extern "C" int sd_abi_version(void) { return 10; }
+
+extern "C" int sd_field_dtype(int dtype) {
+    // Prec<SD_BF16> inherits Prec<SD_F16>: the bf16 mode reads its grids, W_in and the
+    // projected grid as f16 (only the DINO output layer is bf16)
+    return dtype == SD_F32 ? SD_F32 : (dtype == SD_BF16 || dtype == SD_F16) ? SD_F16 : -1;
+}
 
 // Threads per workgroup, one workgroup per CU: 16-bit kernels run 8 waves (2 per SIMD,
 // <= 256 VGPRs each); the f32 parity kernels run 4 waves (1 per SIMD, 512 VGPRs).
@@ -1025,6 +1031,11 @@ extern "C" int sd_render_fused(const sd_render_args *args, const sd_mlp *mlp, vo
     }
     if (sd_plan(mlp, &pl)) return -1;
     const sd_render_args &a = *args;
+    if (a.grid_dtype != sd_field_dtype(mlp->dtype)) {
+        sd_set_error("sd_render_fused: grid_dtype must be sd_field_dtype(mlp->dtype) (f16 for "
+                     "both 16-bit modes)");
+        return -1;
+    }
     if (a.ld_depth || a.ld_dino || a.ld_rgb) {
         sd_set_error("sd_render_fused: output row strides are not supported (must be 0)");
         return -1;
@@ -1054,6 +1065,11 @@ extern "C" int sd_field_query(const sd_field_args *args, const sd_mlp *mlp, void
     }
     if (sd_plan(mlp, &pl)) return -1;
     const sd_field_args &a = *args;
+    if (a.grid_dtype != sd_field_dtype(mlp->dtype)) {
+        sd_set_error("sd_field_query: grid_dtype must be sd_field_dtype(mlp->dtype) (f16 for "
+                     "both 16-bit modes)");
+        return -1;
+    }
     if (a.B <= 0 || a.P < 0 || !a.xyz || !a.grid || !a.cam_f || !a.sigma || !a.dino ||
         a.Hf <= 0 || a.Wf <= 0 || a.nv < 0 || a.nv > SD_MAX_NV ||
         (a.dino_dtype != SD_F32 && a.dino_dtype != SD_BF16) ||

@@ -1096,6 +1096,11 @@ extern "C" int sd_render_proj(const sd_render_args *args, const sd_head *m, void
         sd_set_error("sd_render_proj: invalid head (16-bit dtype, D % 16 == 0, D <= 512)");
         return -1;
     }
+    if (args->grid_dtype != SD_F16) {
+        sd_set_error("sd_render_proj: grid_dtype must be SD_F16 (the projected grid of both "
+                     "16-bit modes, sd_field_dtype)");
+        return -1;
+    }
     if (!args->work) {
         sd_set_error("sd_render_proj: args->work is required (sd_render_proj_work_bytes)");
         return -1;

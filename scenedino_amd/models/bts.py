@@ -142,6 +142,10 @@ class BTSNet(nn.Module):
         self.render_into = None   # optional (R, D + 1 + 3 nv) f32 buffer for dino|depth|rgb
         self._packed = None
         self._packed_key = None
+        # bumped by every training-path forward: an optimizer step that follows may update the
+        # head in place without bumping the parameters' version counters (torch's fused Adam),
+        # so the packed weights and the projected grid P made from them are keyed by it too
+        self._param_gen = 0
         self._grid_cache = None
         self._in_pass, self._pass_nhwc = False, None  # training-path NHWC grid per pass
         self._grid_key = None
@@ -298,7 +302,8 @@ class BTSNet(nn.Module):
             raise NotImplementedError("fused field kernel supports a single prediction head")
         ps = (head.lin_in.weight, head.lin_in.bias, head.lin_out.weight, head.lin_out.bias)
         empty = self.empty_feature if self.learn_empty else None
-        key = param_key(*ps, *([empty] if empty is not None else [])) + (self.precision,)
+        key = param_key(*ps, *([empty] if empty is not None else [])) + (
+            self.precision, getattr(self, "_param_gen", 0))
         if self._packed is None or self._packed_key != key:
             self._packed = PackedMLP(*ps, dtype=self._dtype(), empty_feature=empty)
             self._packed_key = key
@@ -490,7 +495,8 @@ class BTSNet(nn.Module):
             z_lindisp=int(bool(lindisp)), z_seed=(z_seed or 0) & (2**64 - 1), z_offset=int(z_offset),
             ld_depth=depth.stride(0) if maps is not None else 0,
             ld_dino=dino.stride(0) if maps is not None else 0,
-            ld_rgb=rgb.stride(0) if maps is not None else 0)
+            ld_rgb=rgb.stride(0) if maps is not None else 0,
+            grid_dtype=_lib.SD_OF_TORCH[grid.dtype])
         if proj:
             wb = _lib.render_proj_work_bytes(R, m.D)
             work = torch.empty(wb // 4, device=dev) if wb > 0 else None
@@ -582,6 +588,7 @@ class BTSNet(nn.Module):
             dino=dino.data_ptr(), rgb=rgb.data_ptr() if colors else None,
             invalid=inv.data_ptr() if colors else None, invalid_f=invf.data_ptr(),
             dino_dtype=_lib.SD_BF16 if dino_dtype == torch.bfloat16 else _lib.SD_F32,
+            grid_dtype=_lib.SD_OF_TORCH[grid.dtype],
             tile_order=order.data_ptr() if order is not None else None)
         self._timed("field", lambda: _lib.field_query(args, m.rec, xyz))
         return sigma, dino, rgb, inv, invf
@@ -611,6 +618,7 @@ class BTSNet(nn.Module):
         # counters -- torch's fused Adam does -- so the version key alone cannot tell)
         self._packed = None
         self._packed_q = None
+        self._param_gen = getattr(self, "_param_gen", 0) + 1  # stales P's proj_key as well
         head = self.heads[self.final_pred_head]
         if len(self.heads) != 1:
             raise NotImplementedError("the field path supports a single prediction head")

@@ -77,3 +77,22 @@ def test_struct_layouts_match_the_c_header(tmp_path):
         assert ctypes.sizeof(py) == got[(cname, "size")], cname
         for fname, _ in py._fields_:
             assert getattr(py, fname).offset == got[(cname, fname)], (cname, fname)
+
+
+def test_field_dtype_and_grid_dtype_rejection_without_gpu():
+    """ABI 10: the bf16 mode's render / field kernels read f16 grids; the library
+    states that through sd_field_dtype and rejects a grid_dtype that differs instead of
+    reading bf16 bits as f16 (validation runs before any HIP call)."""
+    from scenedino_amd import _lib
+    lib = _lib.load()
+    assert lib.sd_field_dtype(_lib.SD_F32) == _lib.SD_F32
+    assert lib.sd_field_dtype(_lib.SD_BF16) == _lib.SD_F16
+    assert lib.sd_field_dtype(_lib.SD_F16) == _lib.SD_F16
+    assert lib.sd_field_dtype(7) == -1
+    for mode in (_lib.SD_BF16, _lib.SD_F16):
+        assert _lib.FIELD_DTYPE[mode] == lib.sd_field_dtype(mode)
+    head = _lib.SdHead(w_pe=16, w_sig=16, w_out=16, b_dino=16, b_sigma=0.0, D=64,
+                       dtype=_lib.SD_BF16)
+    args = _lib.SdRenderArgs(grid_dtype=_lib.SD_BF16, work=16)
+    rc = lib.sd_render_proj(ctypes.byref(args), ctypes.byref(head), None)
+    assert rc == -1 and b"grid_dtype" in lib.sd_last_error()

@@ -464,3 +464,39 @@ def test_fused_mlp_scatter_gpu(dt, view, monkeypatch):
     _, p_nodx = run(True, grid_grad=False)
     for a, b in zip(p_nodx, p_ref):
         assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["fp16", "bf16"])
+def test_inference_after_inplace_optimizer_step_uses_new_weights(precision):
+    """a training-path forward, then a parameter update that does not bump the
+    tensors' version counters (torch's fused Adam; here `.data` writes), then an inference
+    query of the already-encoded frame: the packed weights AND the projected grid P must be
+    rebuilt from the new weights -- bit-equal to a freshly built model's query."""
+    from _helpers import load, net_from_fixture
+    d = load("field_query.npz")
+    net = net_from_fixture(d, precision)
+    xyz = torch.as_tensor(d["xyz"]).cuda()
+    with torch.no_grad():
+        s0 = net.query(xyz)[0].clone()  # packs the weights and projects P
+    net.train()
+    with torch.enable_grad():
+        sig, dino, *_ = net._query_diff(xyz)
+        (sig.sum() + dino.sum()).backward()
+    net.eval()
+    head = net.heads["normal_head"]
+    g = torch.Generator().manual_seed(7)
+    v0 = head.lin_in.weight._version
+    head.lin_in.weight.data.add_(0.05 * torch.randn(head.lin_in.weight.shape, generator=g).cuda())
+    head.lin_out.weight.data.add_(0.05 * torch.randn(head.lin_out.weight.shape, generator=g).cuda())
+    assert head.lin_in.weight._version == v0  # the case the version key cannot see
+    with torch.no_grad():
+        s1, dn1 = net.query(xyz)[:2]
+    d2 = dict(d)
+    d2["W_in"] = head.lin_in.weight.detach().cpu().numpy()
+    d2["W_out"] = head.lin_out.weight.detach().cpu().numpy()
+    fresh = net_from_fixture(d2, precision)
+    with torch.no_grad():
+        s2, dn2 = fresh.query(xyz)[:2]
+    assert not torch.equal(s1, s0)
+    assert torch.equal(s1, s2) and torch.equal(dn1, dn2)
