@@ -399,6 +399,86 @@ def fx_render_full_offset(ref):
     )
 
 
+
+def fx_render_full_offset_k32(ref):
+    """BASELINE configs[0]'s sample count (K = 32, configs/renderer/pixelnerf.yaml:1) on the
+    scene of fx_render_full_offset (256x192x640 grid, seed 61), whole 192x640 frame from the
+    same offset render pose, jitter seed 63: strided subsample of every output (every 61st
+    ray), SHA-256 of the whole-frame masks, summary statistics."""
+    import hashlib
+    H, W, K = 192, 640, 32
+    n, C, gh, gw = 1, 256, 192, 640
+    images, Ks, poses, grid = make_scene(n, 1, C, gh, gw, H, W, seed=61)
+    net = build_net(ref, grid)
+    net.encode(images, Ks, poses, ids_encoder=[0], ids_render=[0])
+    renderer = ref.NeRFRenderer(n_coarse=K, lindisp=True, hard_alpha_cap=False,
+                                eval_batch_size=65536)
+    wrapper = renderer.bind_parallel(net, gpus=None).eval()
+    sampler = ref.ImageRaySampler(z_near=3, z_far=80, height=H, width=W)
+    render_pose = make_pose(2.0, 0.5).view(1, 1, 4, 4)
+    rays, _ = sampler.sample(None, render_pose, Ks[:, :1])
+    u = torch.rand(rays.shape[1], K, generator=torch.Generator().manual_seed(63))
+    with torch.no_grad(), injected_rand(u):
+        out = wrapper(rays, want_weights=True, want_alphas=True)
+    c = out["coarse"]
+    idx = np.arange(0, H * W, 61)
+    sha = lambda t: hashlib.sha256(np.ascontiguousarray(np32(t)).tobytes()).hexdigest()
+    np.savez_compressed(
+        os.path.join(HERE, "render_full_offset_k32.npz"),
+        scene_seed=np.int64(61), u_seed=np.int64(63), K=np.int64(K), idx=idx,
+        render_pose=np32(render_pose),
+        depth=np32(c["depth"])[0, idx], dino=np32(c["dino_features"])[0, idx],
+        rgb=np32(c["rgb"])[0, idx], weights=np32(c["weights"])[0, idx],
+        alphas=np32(c["alphas"])[0, idx],
+        invalid_sha256=np.array(sha(c["invalid"])),
+        invalid_features_sha256=np.array(sha(c["invalid_features"])),
+        invalid_shape=np.array(c["invalid"].shape),
+        invalid_features_shape=np.array(c["invalid_features"].shape),
+        depth_mean=np.float64(c["depth"].double().mean()),
+        dino_abs_mean=np.float64(c["dino_features"].double().abs().mean()),
+        weights_sum_mean=np.float64(c["weights"].double().sum(-1).mean()),
+    )
+
+
+def fx_render_c4_offset(ref):
+    """BASELINE configs[3]'s render shape: 128 samples per ray and a 384-d feature field
+    (ResnetFC 295 -> 128 -> 385, configs/model/*: dino_dims 384) over the 256x192x640 grid of
+    fx_render_full_offset's scene (seed 61), rays from the same offset render pose.  The
+    reference renders a strided subsample of the frame's rays only (every 61st ray, 2 015
+    rays x 128 samples -- the whole frame would hold 24 GB of per-sample 384-d features on
+    the CPU); the rays are independent, so the GPU test renders the WHOLE frame with the
+    same per-ray jitter rows (seed 64 over all 122 880 rays) and compares these rays.  The
+    head's weights are stored (d_out 385 changes the kaiming draw)."""
+    H, W, K, D = 192, 640, 128, 384
+    n, C, gh, gw = 1, 256, 192, 640
+    images, Ks, poses, grid = make_scene(n, 1, C, gh, gw, H, W, seed=61)
+    net = build_net(ref, grid, dino_dims=D)
+    net.encode(images, Ks, poses, ids_encoder=[0], ids_render=[0])
+    renderer = ref.NeRFRenderer(n_coarse=K, lindisp=True, hard_alpha_cap=False,
+                                eval_batch_size=65536)
+    wrapper = renderer.bind_parallel(net, gpus=None).eval()
+    sampler = ref.ImageRaySampler(z_near=3, z_far=80, height=H, width=W)
+    render_pose = make_pose(2.0, 0.5).view(1, 1, 4, 4)
+    rays, _ = sampler.sample(None, render_pose, Ks[:, :1])
+    u = torch.rand(rays.shape[1], K, generator=torch.Generator().manual_seed(64))
+    idx = np.arange(0, H * W, 61)
+    it = torch.from_numpy(idx)
+    with torch.no_grad(), injected_rand(u[it]):
+        out = wrapper(rays[:, it], want_weights=True, want_alphas=True)
+    c = out["coarse"]
+    head = net.heads["normal_head"]
+    np.savez_compressed(
+        os.path.join(HERE, "render_c4_offset.npz"),
+        scene_seed=np.int64(61), u_seed=np.int64(64), K=np.int64(K), D=np.int64(D), idx=idx,
+        render_pose=np32(render_pose),
+        W_in=np32(head.lin_in.weight), b_in=np32(head.lin_in.bias),
+        W_out=np32(head.lin_out.weight), b_out=np32(head.lin_out.bias),
+        depth=np32(c["depth"])[0], dino=np32(c["dino_features"])[0], rgb=np32(c["rgb"])[0],
+        weights=np32(c["weights"])[0], alphas=np32(c["alphas"])[0],
+        invalid=np32(c["invalid"])[0].astype(np.uint8),
+        invalid_features=np32(c["invalid_features"])[0].astype(np.uint8),
+    )
+
 def load_reference_seg():
     """The reference's MlpDimReduction and SemanticHead pieces (CPU).  semantic_head.py
     imports the CRF helper (pydensecrf, torchvision.transforms.functional: absent here,
@@ -832,6 +912,11 @@ def main():
         fx_render_full_offset(ref)
         print("full offset-pose fixture written to", HERE)
         return
+    if os.environ.get("GOLDEN_ONLY") == "configs03":
+        fx_render_full_offset_k32(ref)
+        fx_render_c4_offset(ref)
+        print("configs[0] / configs[3] full-frame fixtures written to", HERE)
+        return
     if os.environ.get("GOLDEN_ONLY") == "reconstruct":
         fx_reconstruct(ref)
         print("reconstruct fixture written to", HERE)
@@ -849,6 +934,8 @@ def main():
     if os.environ.get("GOLDEN_FULL", "1") == "1":
         fx_render_full_digest(ref)
         fx_render_full_offset(ref)
+        fx_render_full_offset_k32(ref)
+        fx_render_c4_offset(ref)
     fx_state_dict_manifest(ref)
     fx_reconstruct(ref)
     fx_field_query(ref, learn_empty=True)

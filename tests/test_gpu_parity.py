@@ -507,6 +507,64 @@ def test_render_full_offset_pose_vs_reference(precision):
         assert abs(float(c["depth"].double().mean()) - float(d["depth_mean"])) < 1e-3
 
 
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16", "fp16"])
+def test_render_full_offset_k32_vs_reference(precision):
+    """BASELINE configs[0]'s K = 32 (configs/renderer/pixelnerf.yaml:1) over the whole
+    192x640 frame from the offset render pose, against the reference's own full-frame render
+    (make_golden.fx_render_full_offset_k32): the 16-bit modes run the tile kernel's
+    two-rays-per-wave form on every ray of the frame.  Masks bit-exact over the frame
+    (SHA-256), outputs on every 61st ray within the module's tolerances."""
+    import hashlib
+    from _fullscene import render_offset_fixture
+    d = load("render_full_offset_k32.npz")
+    c = render_offset_fixture(d, precision, DEV)
+    sha = lambda t: hashlib.sha256(t.cpu().numpy().tobytes()).hexdigest()
+    assert list(c["invalid"].shape) == list(d["invalid_shape"])
+    assert sha(c["invalid"]) == str(d["invalid_sha256"])
+    assert sha(c["invalid_features"]) == str(d["invalid_features_sha256"])
+    idx = torch.from_numpy(d["idx"])
+    sub = {k: c[k][0].cpu()[idx] for k in ("depth", "dino_features", "rgb", "weights", "alphas")}
+    if precision == "fp32":
+        for k, rk in (("depth", "depth"), ("weights", "weights"), ("alphas", "alphas"),
+                      ("rgb", "rgb"), ("dino_features", "dino")):
+            close(sub[k], d[rk], 1e-5, FP32_ATOL_FULL[rk], k)
+        assert abs(float(c["depth"].double().mean()) - float(d["depth_mean"])) < 1e-5
+    else:
+        check_lowp(sub, {"depth": d["depth"], "dino_features": d["dino"], "rgb": d["rgb"],
+                         "weights": d["weights"]}, precision)
+        assert abs(float(c["depth"].double().mean()) - float(d["depth_mean"])) < 1e-3
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16", "fp16"])
+def test_render_c4_offset_vs_reference(precision):
+    """BASELINE configs[3]'s render shape -- 128 samples per ray, a 384-d feature field
+    (ResnetFC 295 -> 128 -> 385) -- over the 256x192x640 grid from the offset render pose,
+    against the reference's render of every 61st ray of the frame
+    (make_golden.fx_render_c4_offset).  16-bit: the WHOLE frame through the tile kernel
+    (hidden-space compositing + the per-ray 384-d head), compared on the fixture's rays;
+    fp32: the fixture's rays through the generic field query + compositing (the fp32 grid
+    kernel takes D <= 128).  Masks exact on those rays."""
+    from _fullscene import render_offset_fixture
+    d = load("render_c4_offset.npz")
+    whole = precision != "fp32"
+    c = render_offset_fixture(d, precision, DEV, whole_frame=whole)
+    idx = torch.from_numpy(d["idx"]) if whole else torch.arange(d["idx"].shape[0])
+    sub = {k: c[k][0].cpu()[idx] for k in ("depth", "dino_features", "rgb", "weights", "alphas",
+                                          "invalid", "invalid_features")}
+    assert sub["dino_features"].shape[-1] == 384
+    assert torch.equal(sub["invalid"].reshape(-1).bool(),
+                       torch.from_numpy(d["invalid"]).reshape(-1).bool())
+    assert torch.equal(sub["invalid_features"].reshape(-1).bool(),
+                       torch.from_numpy(d["invalid_features"]).reshape(-1).bool())
+    if precision == "fp32":
+        for k, rk in (("depth", "depth"), ("weights", "weights"), ("alphas", "alphas"),
+                      ("rgb", "rgb"), ("dino_features", "dino")):
+            close(sub[k], d[rk], 1e-5, FP32_ATOL_FULL[rk], k)
+    else:
+        check_lowp(sub, {"depth": d["depth"], "dino_features": d["dino"], "rgb": d["rgb"],
+                         "weights": d["weights"]}, precision)
+
 def _overflow_blocks(net, R):
     """4-ray blocks in the tile kernel's per-workgroup overflow lists of net's last render
     (the tail of its sd_render_proj work: [ncu] counts, [ncu][cap] blocks, sdhip_render.h)."""

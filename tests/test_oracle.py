@@ -86,3 +86,32 @@ def test_render_full_subsample_fixture_consistent():
     d = load("render_full_subsample.npz")
     assert d["depth"].shape == d["idx"].shape and d["dino"].shape == (d["idx"].shape[0], 64)
     assert np.isfinite(d["dino"]).all()
+
+
+@pytest.mark.parametrize("fx", ["render_full_offset_k32.npz", "render_c4_offset.npz"])
+def test_torch_oracle_full_frame_offset_fixtures(fx):
+    """BASELINE configs[0] (K = 32) and configs[3] (K = 128, 384-d field) full-frame renders
+    of the reference (make_golden.fx_render_full_offset_k32 / fx_render_c4_offset): the
+    oracle on the fixture's rays of the 192x640 offset-pose frame (rays are independent)."""
+    from _fullscene import scene_arrays, KITTI_K
+    d = load(fx)
+    K = int(d["K"])
+    D = int(d["D"]) if "D" in d else 64
+    images, grid, (W_in, b_in, W_out, b_out) = scene_arrays(
+        int(d["scene_seed"]), D=D, weights=d if "W_in" in d else None)
+    Kn = torch.tensor(KITTI_K).view(1, 3, 3)
+    pose = torch.from_numpy(d["render_pose"]).view(1, 4, 4)
+    rays = O.gen_rays(pose, Kn, 192, 640)
+    u = torch.rand(rays.shape[0], K, generator=torch.Generator().manual_seed(int(d["u_seed"])))
+    it = torch.from_numpy(d["idx"])
+    w2c = torch.eye(4).view(1, 4, 4)
+    with torch.no_grad():
+        out = O.render(rays[it], u[it], grid, w2c, Kn, images * 0.5 + 0.5, w2c.view(1, 1, 4, 4),
+                       Kn.view(1, 1, 3, 3), W_in, b_in, W_out, b_out, sb=1)
+    atol = {"depth": 1e-6, "weights": 1e-5, "alphas": 1e-4, "rgb": 1e-5, "dino": 5e-5}
+    for k, rk in (("depth", "depth"), ("weights", "weights"), ("alphas", "alphas"),
+                  ("rgb", "rgb"), ("dino_features", "dino")):
+        ref = torch.from_numpy(d[rk])
+        assert torch.allclose(out[k].reshape(ref.shape), ref, rtol=1e-5, atol=atol[rk]), k
+    if "invalid" in d:
+        assert torch.equal(out["invalid"].reshape(-1).bool(), torch.from_numpy(d["invalid"]).reshape(-1).bool())

@@ -5,7 +5,7 @@ widen them to f16 for the blend (v_cvt_scalef32_pk_f16_fp8 is exact), so the f16
 P rounded to e4m3 (per-tensor power-of-two scale s, values e4m3(P s) / s, exact in f16) gives
 that kernel's outputs.  Reports sigma rel-L2 and the label / seg agreement of the C5 scene
 against the unquantised run (sigma rel-L2 <= 5e-2, labels >= 99 %).
-usage: field_fp8_emul.py [--scale=tensor|none]"""
+usage: field_fp8_emul.py [--scale=tensor|block32|none]"""
 import sys
 
 import torch
@@ -38,13 +38,25 @@ def main():
             P = net._grid_proj(gc, m)  # (B, Hf, Wf, 128) f16, cached in gc
             if name == "fp8":
                 Pf = P.float()
-                s = 1.0
-                if mode == "tensor":
-                    mx = float(Pf.abs().max())
-                    s = 2.0 ** int(torch.floor(torch.log2(torch.tensor(448.0 / mx))))
-                q = (Pf * s).to(torch.float8_e4m3fn).float() / s
+                if mode == "block32":
+                    # MX-style: one power-of-two (E8M0) scale per 32 consecutive hidden
+                    # channels of a grid pixel -- the K-block v_mfma_scale_f32_*_f8f6f4
+                    # consumes (cbsz / blgp scale operands)
+                    blk = Pf.reshape(*Pf.shape[:-1], Pf.shape[-1] // 32, 32)
+                    amax = blk.abs().amax(-1, keepdim=True).clamp_min(1e-30)
+                    s = torch.exp2(torch.floor(torch.log2(448.0 / amax)))
+                    q = ((blk * s).to(torch.float8_e4m3fn).float() / s).reshape(Pf.shape)
+                    sl = torch.log2(s)
+                    desc = f"per-32-channel block scales 2^{int(sl.min())}..2^{int(sl.max())}"
+                else:
+                    s = 1.0
+                    if mode == "tensor":
+                        mx = float(Pf.abs().max())
+                        s = 2.0 ** int(torch.floor(torch.log2(torch.tensor(448.0 / mx))))
+                    q = (Pf * s).to(torch.float8_e4m3fn).float() / s
+                    desc = f"scale 2^{int(torch.log2(torch.tensor(s)))}"
                 P.copy_(q.to(P.dtype))
-                print(f"P: max |P| {float(Pf.abs().max()):.3f}, scale 2^{int(torch.log2(torch.tensor(s)))}, "
+                print(f"P: max |P| {float(Pf.abs().max()):.3f}, {desc}, "
                       f"P rel-L2 after e4m3 {rel_l2(q, Pf):.3e}")
             sig, dino, _, _, _ = net.query(xyz, colors=False, dino_dtype=torch.bfloat16)
             Pn = sig.numel()
