@@ -668,11 +668,13 @@ extern "C" int sd_field_prof(unsigned long long *out, int reset) {
 #ifndef SD_FQ_ABL_NOSTORE
 #define SD_FQ_ABL_NOSTORE 0
 #endif
-template <int P>
+// WL: the W_out fragments staged in LDS (16-bit, when they fit beside W_in: D <= 128 at
+// C = 256, any D <= 512 on the projected grid's 128 columns), else read from L2 (f32, and
+// 16-bit 384-d heads over a 256-channel grid)
+template <int P, bool WL>
 __global__ void __launch_bounds__(WG<P>::T, 1)
 k_field(const sd_field_args a, const sd_mlp m, const LdsPlan pl) {
     typedef Prec<P> Pr;
-    constexpr bool WL = P != SD_F32;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     sd_stage(lds, m, pl);
     const uint8_t *wout_base = WL ? lds + pl.win_bytes : (const uint8_t *)m.w_out;
@@ -817,14 +819,12 @@ k_field(const sd_field_args a, const sd_mlp m, const LdsPlan pl) {
         FQ_T(2);
         const uint8_t *wo = wout_base + (WL ? lo : 0);
         const int64_t tile = tile_of(tt);
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-            if (dt >= ndt) break;
+        // one 32-dim tile of the DINO output: 8 (f32: 32) MFMAs + 16 row stores
+        auto out_tile = [&](int dt, float bd) __attribute__((always_inline)) {
             f32x16 ov = {};
             Prec<P>::mma2(wo, dt, acc, lane, ov);
             // O layout: row = point (r&3)+8(r>>2)+4h of this tile, column = dim li
             const int dim = dt * 32 + li;
-            const float bd = bdino[dt];
             if (SD_FQ_ABL_NOSTORE) {
                 if (ov[0] == 12345.f) a.dino[tile] = ov[1];  // keep the product alive
             } else {
@@ -845,7 +845,14 @@ k_field(const sd_field_args a, const sd_mlp m, const LdsPlan pl) {
                             __builtin_bit_cast(uint32_t, ov[r] + bd), rdino, ro, 0, 0);
                 }
             }
+        };
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+            if (dt >= ndt) break;
+            out_tile(dt, bdino[dt]);
         }
+        // wide heads (configs[3]: D = 384): the tiles past the 4 with register-cached biases
+        for (int dt = 4; dt < ndt; ++dt) out_tile(dt, m.b_dino[dt * 32 + li]);
         FQ_T(3);
         if (cur.valid && h == 0) {
             a.sigma[cur.p] = sigma;
@@ -968,9 +975,9 @@ static int sd_plan(const sd_mlp *m, LdsPlan *pl) {
         sd_set_error("sd_mlp: null parameter pointer");
         return -1;
     }
-    if (m->d_hidden != SD_DH || m->C <= 0 || (m->C % 64) || m->D <= 0 || (m->D % 32) ||
+    if (m->d_hidden != SD_DH || m->C <= 0 || (m->C % 64) || m->D <= 0 || (m->D % 32) || m->D > 512 ||
         (m->dtype != SD_BF16 && m->dtype != SD_F32 && m->dtype != SD_F16)) {
-        sd_set_error("sd_mlp: unsupported shape (need d_hidden=128, C%64==0, D%32==0)");
+        sd_set_error("sd_mlp: unsupported shape (need d_hidden=128, C%64==0, D%32==0, D<=512)");
         return -1;
     }
     int nq = m->C / 16 + SD_PE_CHUNKS;
@@ -978,7 +985,9 @@ static int sd_plan(const sd_mlp *m, LdsPlan *pl) {
     pl->win_bytes = nq * 4 * SD_WAVE * 8 * esz;
     pl->wout_bytes = (m->D / 32) * 4 * SD_WAVE * (m->dtype == SD_F32 ? 64 : 32);
     int rest = 384 * 4;  // b_in, w_sigma, learn_empty rows
-    pl->wout_in_lds = m->dtype != SD_F32;
+    // 16-bit W_out fragments in LDS when they fit beside W_in (always for D <= 128 at
+    // C <= 256, sd_render_fused's range); otherwise k_field reads them from L2 like f32
+    pl->wout_in_lds = m->dtype != SD_F32 && pl->win_bytes + pl->wout_bytes + rest <= 160 * 1024;
     pl->total = pl->win_bytes + (pl->wout_in_lds ? pl->wout_bytes : 0) + rest;
     if (pl->total > 160 * 1024) {
         sd_set_error("sd_mlp: MLP fragments exceed the 160 KiB LDS (C or D too large)");
@@ -1036,6 +1045,10 @@ extern "C" int sd_render_fused(const sd_render_args *args, const sd_mlp *mlp, vo
                      "both 16-bit modes)");
         return -1;
     }
+    if (mlp->dtype != SD_F32 && !pl.wout_in_lds) {  // k_render stages 16-bit W_out in LDS
+        sd_set_error("sd_render_fused: 16-bit MLP fragments exceed the 160 KiB LDS (C too large)");
+        return -1;
+    }
     if (a.ld_depth || a.ld_dino || a.ld_rgb) {
         sd_set_error("sd_render_fused: output row strides are not supported (must be 0)");
         return -1;
@@ -1084,9 +1097,13 @@ extern "C" int sd_field_query(const sd_field_args *args, const sd_mlp *mlp, void
     if (a.P == 0) return 0;
     const int64_t ntiles = (a.B * a.P + 31) / 32;
     hipStream_t s = (hipStream_t)stream;
-    if (mlp->dtype == SD_F16) return sd_launch<SD_F16>(k_field<SD_F16>, ntiles, pl, s, a, *mlp);
-    if (mlp->dtype == SD_BF16) return sd_launch<SD_BF16>(k_field<SD_BF16>, ntiles, pl, s, a, *mlp);
-    return sd_launch<SD_F32>(k_field<SD_F32>, ntiles, pl, s, a, *mlp);
+    if (mlp->dtype == SD_F16)
+        return pl.wout_in_lds ? sd_launch<SD_F16>(k_field<SD_F16, true>, ntiles, pl, s, a, *mlp)
+                              : sd_launch<SD_F16>(k_field<SD_F16, false>, ntiles, pl, s, a, *mlp);
+    if (mlp->dtype == SD_BF16)
+        return pl.wout_in_lds ? sd_launch<SD_BF16>(k_field<SD_BF16, true>, ntiles, pl, s, a, *mlp)
+                              : sd_launch<SD_BF16>(k_field<SD_BF16, false>, ntiles, pl, s, a, *mlp);
+    return sd_launch<SD_F32>(k_field<SD_F32, false>, ntiles, pl, s, a, *mlp);
 }
 
 extern "C" int sd_composite(const float *z, const float *sigma, const float *feat, int64_t F,

@@ -112,16 +112,23 @@ k_project(const float *__restrict__ grid, int64_t B, int C, int64_t HW, int W, c
             for (int e = 0; e < 8; ++e) x1[e] = gp[16 * cs + e * cs];
         }
         auto kstep = [&](int q, float (&x)[8]) {
-            Frag f;
+            // the f32 grid as a hi + lo pair of 16-bit operands (see k_project_lds)
+            Frag f, fl;
 #pragma unroll
-            for (int e = 0; e < 8; ++e) f[e] = (typename Tr::E)x[e];
+            for (int e = 0; e < 8; ++e) {
+                f[e] = (typename Tr::E)x[e];
+                fl[e] = (typename Tr::E)(x[e] - (float)f[e]);
+            }
             if (q + 2 < nq) {
                 const float *gn = gp + (int64_t)(16 * (q + 2)) * cs;
 #pragma unroll
                 for (int e = 0; e < 8; ++e) x[e] = gn[e * cs];
             }
 #pragma unroll
-            for (int t = 0; t < 4; ++t) acc[t] = Tr::mma32(lw[(q * 4 + t) * SD_WAVE + lane], f, acc[t]);
+            for (int t = 0; t < 4; ++t) {
+                acc[t] = Tr::mma32(lw[(q * 4 + t) * SD_WAVE + lane], f, acc[t]);
+                acc[t] = Tr::mma32(lw[(q * 4 + t) * SD_WAVE + lane], fl, acc[t]);
+            }
         };
         int q = 0;
         for (; q + 1 < nq; q += 2) {
@@ -290,16 +297,24 @@ k_project_lds(const float *__restrict__ grid, int64_t npix, const sd_mlp m, uint
         issue(2 * k + PJ_NS - 1);
         // lane (pixel li, half h): slot 2k + (li >> 4), row li & 15, channels 16 q + 8 h ..
         const uint8_t *sl = lds + ((2 * k + (li >> 4)) % PJ_NS) * PJ_SLOT + (li & 15) * PJ_ROWB + 32 * h;
+        // round 6: the f32 grid enters the MFMA as a hi + lo pair of 16-bit operands
+        // (hi = f16(g), lo = f16(g - hi), g - hi exact in f32): the one rounding of G the
+        // projection made cost up to 5.8e-3 m of composited depth at configs[3]'s K = 128
+        // (tools/lowp_depth_emul.py; W_in stays one f16 operand), twice the MFMAs of an
+        // HBM-bound kernel
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
             const f32x4 a = *(const f32x4 *)(sl + 64 * q), b = *(const f32x4 *)(sl + 64 * q + 16);
-            Frag f;
+            Frag f, fl;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 f[e] = (E)a[e];
                 f[4 + e] = (E)b[e];
+                fl[e] = (E)(a[e] - (float)f[e]);
+                fl[4 + e] = (E)(b[e] - (float)f[4 + e]);
             }
             acc = Tr::mma32(W[q], f, acc);
+            acc = Tr::mma32(W[q], fl, acc);
         }
         store_chunk(k);
     }
@@ -331,13 +346,16 @@ k_project_lds(const float *__restrict__ grid, int64_t npix, const sd_mlp m, uint
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             const f32x4 a = *(const f32x4 *)(sl + 64 * q), b = *(const f32x4 *)(sl + 64 * q + 16);
-            Frag f;
+            Frag f, fl;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 f[e] = (E)a[e];
                 f[4 + e] = (E)b[e];
+                fl[e] = (E)(a[e] - (float)f[e]);
+                fl[4 + e] = (E)(b[e] - (float)f[4 + e]);
             }
             acc = Tr::mma32(W[8 * HALF + q], f, acc);
+            acc = Tr::mma32(W[8 * HALF + q], fl, acc);
         }
     };
     for (int k = 0; k < my; ++k) {

@@ -193,6 +193,48 @@ def test_field_query_vs_reference(precision, fx):
         assert rel_l2(sd["dino_features"], d["dino"]) < 1e-2
 
 
+@pytest.mark.parametrize("precision,mode", [("fp32", "grid"), ("bf16", "proj"), ("fp16", "proj"),
+                                            ("bf16", "grid"), ("fp16", "grid")])
+@pytest.mark.parametrize("D", [96, 384])
+def test_field_query_wide_head_vs_oracle(precision, mode, D):
+    """BTSNet.forward on raw points (the SSCBench / inference_3d query, sd_field_query) with
+    a 384-d feature field (BASELINE configs[3]) and D = 96: every 32-dim output tile, past
+    the 4 whose biases the kernel keeps in registers; the 16-bit grid mode's 384-d W_out
+    fragments do not fit the LDS beside the 256-channel W_in and are read from L2.  Against
+    the CPU oracle on the field_query scene (points with z_cam >= 1 m: fp32 rtol 1e-5 /
+    atol 5e-5; 16-bit: sigma rel-L2 < 2e-2, dino < 1e-2); masks exact."""
+    from oracle import render_oracle as O
+    d = dict(load("field_query.npz"))
+    g = torch.Generator().manual_seed(300 + D)
+    d["W_out"] = (torch.randn(1 + D, 128, generator=g) * 0.1).numpy()
+    d["b_out"] = (torch.randn(1 + D, generator=g) * 0.1).numpy()
+    net = net_from_fixture(d, precision, mode=mode)
+    with torch.no_grad():
+        rgb, invalid, sigma, extras, sd = net(T(d["xyz"]))
+    Tc = torch.from_numpy
+    w2c = torch.inverse(Tc(d["poses"]))
+    r = O.field_query(Tc(d["xyz"]), Tc(d["grid"]), w2c[:, 0], Tc(d["Ks"])[:, 0],
+                      Tc(d["images"]) * 0.5 + 0.5, w2c, Tc(d["Ks"]), Tc(d["W_in"]), Tc(d["b_in"]),
+                      Tc(d["W_out"]), Tc(d["b_out"]))
+    dn = sd["dino_features"].reshape(-1, D).cpu()
+    assert dn.shape[-1] == D
+    assert torch.equal(sd["invalid_features"].reshape(-1).cpu().bool(),
+                       r["invalid_features"].reshape(-1))
+    xyz = torch.as_tensor(d["xyz"]).double().reshape(-1, 3)
+    zc = xyz @ w2c[0, 0].double()[2, :3] + w2c[0, 0].double()[2, 3]
+    ok = zc >= 1.0
+    rd = r["dino"].reshape(-1, D)
+    rs = r["sigma"].reshape(-1)
+    if precision == "fp32":
+        close(sigma.reshape(-1).cpu()[ok], rs[ok], 1e-5, FP32_ATOL["sigma"], "sigma")
+        close(dn[ok], rd[ok], 1e-5, FP32_ATOL_FULL["dino"], "dino")
+    else:
+        assert rel_l2(sigma.reshape(-1).cpu()[ok], rs[ok]) < 2e-2
+        assert rel_l2(dn[ok], rd[ok]) < 1e-2
+        # every 32-dim tile on its own (a tile left unwritten would still pass the global norm)
+        for t in range(D // 32):
+            assert rel_l2(dn[ok][:, 32 * t:32 * t + 32], rd[ok][:, 32 * t:32 * t + 32]) < 1e-2, t
+
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
 def test_field_query_bf16_dino_is_the_rounded_f32(precision):
     """dino_dtype bf16 (the voxel path's input to sd_seg_query): the same values as the f32
@@ -318,12 +360,18 @@ def test_projected_grid_vs_dense_projection(precision):
     pk = PackedMLP(W_in.to(DEV), b_in.to(DEV), W_out.to(DEV), b_out.to(DEV), dt)
     P = _lib.project_grid(grid.to(DEV), pk.rec, dt).double().cpu()   # (2, Hf, Wf, 128)
     assert P.shape == (2, Hf, Wf, 128)
-    # both 16-bit modes project in f16 (the bf16 mode keeps bf16 for the DINO head only)
+    # both 16-bit modes project in f16 (the bf16 mode keeps bf16 for the DINO head only);
+    # round 6: the grid enters as a hi + lo pair of f16 operands (exact to ~2^-22), W_in as
+    # one f16 operand, P rounded once to f16 at the store
     tdt = _lib.TORCH_DTYPE[_lib.FIELD_DTYPE[dt]]
     assert tdt == torch.float16
-    ref = torch.einsum("nc,bchw->bhwn", W_in[:, :C].to(tdt).double(), grid.to(tdt).double()) \
+    ref = torch.einsum("nc,bchw->bhwn", W_in[:, :C].to(tdt).double(), grid.double()) \
         + b_in.double()
-    assert rel_l2(P, ref) < 1e-3
+    assert rel_l2(P, ref) < 6e-4
+    # against the single-rounded grid the error would be the grid's f16 rounding as well
+    ref1 = torch.einsum("nc,bchw->bhwn", W_in[:, :C].to(tdt).double(), grid.to(tdt).double()) \
+        + b_in.double()
+    assert rel_l2(P, ref) < rel_l2(P, ref1)
 
 
 def test_render_full_192x640x64_vs_reference_subsample():

@@ -66,6 +66,25 @@ def scene_full_offset():
                 cap=False, ref=torch.as_tensor(d["depth"]))
 
 
+def scene_offset_fixture(name):
+    """make_golden.fx_render_full_offset_k32 / fx_render_c4_offset (configs[0] / configs[3]):
+    the seed-61 scene, restricted to the fixture's rays (the head from the fixture if it
+    holds one)."""
+    from _fullscene import KITTI_K, scene_arrays
+    d = np.load(os.path.join(GOLD, name + ".npz"))
+    K = int(d["K"])
+    D = int(d["D"]) if "D" in d else 64
+    _, grid, (W_in, b_in, W_out, b_out) = scene_arrays(
+        int(d["scene_seed"]), D=D, weights=d if "W_in" in d else None)
+    Kn = torch.tensor(KITTI_K).view(1, 3, 3)
+    rays = O.gen_rays(torch.as_tensor(d["render_pose"]).view(1, 4, 4), Kn, 192, 640)
+    u = torch.rand(rays.shape[0], K, generator=torch.Generator().manual_seed(int(d["u_seed"])))
+    idx = torch.as_tensor(d["idx"])
+    return dict(rays=rays[idx], u=u[idx], grid=grid, W_in=W_in, b_in=b_in, W_out=W_out,
+                b_out=b_out, w2c=torch.eye(4).view(1, 4, 4), Kf=Kn, cap=False,
+                ref=torch.as_tensor(d["depth"]))
+
+
 class Emu:
     def __init__(self, s):
         self.s = s
@@ -132,6 +151,13 @@ SCHEMES = [
     ("only w bf16", dict(rw=BF)),
     ("only code + Wc bf16", dict(rcode=BF, rWc=BF)),
     ("only X + Ws bf16", dict(rX=BF, rWs=BF)),
+    ("only P f16", dict(rP=HF)),
+    ("only w f16", dict(rw=HF)),
+    ("only code + Wc f16", dict(rcode=HF, rWc=HF)),
+    ("only X + Ws f16", dict(rX=HF, rWs=HF)),
+    ("only G, Wg f16 (projection operands)", dict(rG=HF)),
+    ("all f16 but X, Ws (sigma column hi+lo)", dict(rG=HF, rP=HF, rw=HF, rcode=HF, rWc=HF)),
+    ("all f16 but P (P hi+lo)", dict(rG=HF, rw=HF, rcode=HF, rWc=HF, rX=HF, rWs=HF)),
 ]
 
 
@@ -140,6 +166,10 @@ def main():
     scenes = [("render_k32_cap0", scene_small("render_k32_cap0")),
               ("render_k64_cap1", scene_small("render_k64_cap1")),
               ("render_full_offset", scene_full_offset())]
+    if os.environ.get("EMUL_ONLY_C03") == "1":
+        scenes = []
+    scenes += [("full_offset_k32", scene_offset_fixture("render_full_offset_k32")),
+               ("c4_offset_k128", scene_offset_fixture("render_c4_offset"))]
     emus = [(n, Emu(s), s["ref"]) for n, s in scenes]
     print("max |depth - reference| (m) of the emulated render; contract (SURVEY §8(c)): 1e-2 m")
     print(f"{'scheme':44s}" + "".join(f"{n:>22s}" for n, _, _ in emus))
