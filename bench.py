@@ -928,6 +928,16 @@ def _launch_ranks(args) -> int:
     return subprocess.call(cmd)
 
 
+def reserve_cus(args, world, host_stage) -> int:
+    """CUs the persistent kernels leave to RCCL when a collective runs beside them: --reserve-cus,
+    or (-1, auto) NCCL_MAX_NCHANNELS (bench.py sets 16 for its RCCL gathers) with N > 1 RCCL."""
+    if args.reserve_cus >= 0:
+        return args.reserve_cus
+    if world <= 1 or host_stage:
+        return 0
+    return int(os.environ.get("NCCL_MAX_NCHANNELS", "16"))
+
+
 def c2_pose_run(args, world, rank, device, dist, offset_pose, host_stage):
     """Time the C2 step at one render pose (all ranks; max over ranks)."""
     from scenedino_amd import distributed as sdd
@@ -950,6 +960,11 @@ def c2_pose_run(args, world, rank, device, dist, offset_pose, host_stage):
     # (that IS the frame's assembly).
     use_gather = dist and (rows or args.gather == "allgather")
     gather = sdd.MapGather(Rr, 1 + D_DINO + 3, device, host_stage=host_stage) if use_gather else None
+    # RCCL's all-gather of frame i runs beside frame i+1's projection and render: the
+    # persistent grids leave its CUs free (sd_reserve_cus, one CU per RCCL channel), else the
+    # workgroups whose CUs it holds start only after it
+    from scenedino_amd import _lib as sdl
+    sdl.reserve_cus(reserve_cus(args, world, host_stage) if use_gather else 0)
     net.fused_mode = args.mode
     timer = KernelTimer()
     net.kernel_timer = timer
@@ -1123,6 +1138,8 @@ def main_c2(args, world, rank, device, dist, host_stage):
     }
     if "gathered_maps" in r:
         line["config"]["gathered_maps"] = r["gathered_maps"]
+        line["config"]["reserved_cus"] = reserve_cus(args, world, host_stage)
+        line["config"]["nccl_max_nchannels"] = os.environ.get("NCCL_MAX_NCHANNELS")
         line["config"]["gather_bytes_per_rank_per_step"] = 4 * r["gathered_maps"][1] * \
             r["gathered_maps"][2] * (world - 1)
     if nog is not None:
@@ -1158,6 +1175,9 @@ def main():
                          "next frame's render; the same pose is then also timed without the "
                          "collective and reported as no_gather on the same line) or none (value "
                          "timed with no data-path collective)")
+    ap.add_argument("--reserve-cus", type=int, default=-1,
+                    help="c2 with an RCCL gather: CUs the persistent kernels leave free for RCCL's "
+                         "channels (-1: NCCL_MAX_NCHANNELS, set to 16 by bench.py if unset)")
     ap.add_argument("--identity-pose", action="store_true",
                     help="c2: time only the identity render pose (profiling runs)")
     ap.add_argument("--mode", default="proj", choices=["proj", "grid"],
@@ -1217,6 +1237,9 @@ def main():
         if host_stage:
             tdist.init_process_group("gloo")
         else:
+            # the render's persistent grids leave NCCL_MAX_NCHANNELS CUs to the all-gather
+            # beside them (reserve_cus): bound RCCL's channels -- one workgroup each -- to that
+            os.environ.setdefault("NCCL_MAX_NCHANNELS", "16")
             tdist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
         if tdist.get_world_size() != args.gpus:
             raise SystemExit("bench.py: process-group size differs from --gpus")

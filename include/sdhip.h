@@ -56,6 +56,19 @@ int sd_abi_version(void);
  * the projected grid in sd_field_dtype(mlp->dtype). */
 int sd_field_dtype(int dtype);
 
+/* Leave n CUs of the device to other kernels: the persistent one-workgroup-per-CU grids
+ * (projection, tile render and its fallback, field query, ...) launch on the device's CUs
+ * minus n, rounded down to a multiple of 8.  For the multi-GPU step, whose RCCL all-gather of
+ * the previous frame (one workgroup per channel, NCCL_MAX_NCHANNELS) runs beside the render:
+ * a persistent workgroup whose CU that kernel holds would start only after it.  Process-wide;
+ * set it before sizing sd_render_proj's work (sd_render_proj_work_bytes depends on it).
+ * Returns the previous value. */
+int32_t sd_reserve_cus(int32_t n);
+
+/* Diagnostic: nblocks single-wave workgroups spinning for `us` microseconds on the stream
+ * (stands in for another stream's kernel holding CUs, tools/contention_ab.py). */
+int sd_spin(int32_t nblocks, float us, void *stream);
+
 /* Frustum ray generation, bit-exact with the reference's fp32 arithmetic.
  * Replaces util.unproj_map + util.gen_rays + ImageRaySampler.sample
  *   (scenedino/common/util.py:113-158, util.py:253-285,

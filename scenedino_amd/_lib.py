@@ -178,6 +178,8 @@ SIGNATURES = {
     "sd_last_error": [],
     "sd_abi_version": [],
     "sd_field_dtype": [ctypes.c_int],
+    "sd_reserve_cus": [ctypes.c_int32],
+    "sd_spin": [ctypes.c_int32, ctypes.c_float, _vp],
     "sd_ln_gemm": [ctypes.POINTER(SdGemmArgs), _vp, _vp, _vp, ctypes.c_float, _vp],
     "sd_gen_rays": [_vp, _vp, _vp, _i64, _i64, _i64, ctypes.c_float, ctypes.c_float, _vp, _vp],
     "sd_sample_z": [_vp, _i64, _i64, _i64, ctypes.c_int, _vp, ctypes.c_uint64, ctypes.c_uint64,
@@ -890,3 +892,14 @@ def upsample2x(x):
     _check(lib.sd_upsample2x(ptr(_req(x, "x", torch.bfloat16)), B, H, W, C, ptr(out),
                              stream_of(x)), "sd_upsample2x")
     return out
+
+
+def reserve_cus(n: int) -> int:
+    """sd_reserve_cus: leave n CUs to other kernels (RCCL beside the render); previous value."""
+    return int(load().sd_reserve_cus(int(n)))
+
+
+def spin(nblocks: int, us: float, stream=None) -> None:
+    """sd_spin (diagnostic): nblocks single-wave workgroups holding CUs for us microseconds."""
+    s = stream if stream is not None else torch.cuda.current_stream()
+    _check(load().sd_spin(int(nblocks), float(us), ctypes.c_void_p(s.cuda_stream)), "sd_spin")

@@ -44,6 +44,40 @@ extern "C" void sd_set_error(const char *msg) {
 extern "C" const char *sd_last_error(void) { return g_err; }
 extern "C" int sd_abi_version(void) { return 10; }
 
+int sd_g_cu_reserve = 0;
+
+extern "C" int32_t sd_reserve_cus(int32_t n) {
+    const int prev = sd_g_cu_reserve;
+    sd_g_cu_reserve = n > 0 ? n : 0;
+    return prev;
+}
+
+// diagnostic: nblocks single-wave workgroups with 32 KiB of LDS each that hold a CU for `us`
+// microseconds (the constant 100 MHz wall clock), bounded -- the CU occupancy of another
+// stream's kernel (tools/contention_ab.py stands in for RCCL's all-gather with it: its blocks
+// hold shared memory, and the persistent render workgroups need nearly all of a CU's LDS)
+__global__ void __launch_bounds__(64) k_spin(int64_t ticks) {
+    extern __shared__ float spin_lds[];  // holds LDS like RCCL's per-block shared state
+    const uint64_t t0 = wall_clock64();
+    while ((int64_t)(wall_clock64() - t0) < ticks) __builtin_amdgcn_s_sleep(8);
+    if (ticks < 0) spin_lds[threadIdx.x] = 0.f;
+}
+
+extern "C" int sd_spin(int32_t nblocks, float us, void *stream) {
+    if (nblocks <= 0 || nblocks > 4096 || !(us >= 0.f) || us > 1e6f) {
+        sd_set_error("sd_spin: invalid argument (1..4096 blocks, 0..1e6 us)");
+        return -1;
+    }
+    hipLaunchKernelGGL(k_spin, dim3((unsigned)nblocks), dim3(64), 32768, (hipStream_t)stream,
+                       (int64_t)(us * 100.f));
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        sd_set_error(hipGetErrorString(e));
+        return -2;
+    }
+    return 0;
+}
+
 extern "C" int sd_field_dtype(int dtype) {
     // Prec<SD_BF16> inherits Prec<SD_F16>: the bf16 mode reads its grids, W_in and the
     // projected grid as f16 (only the DINO output layer is bf16)

@@ -192,6 +192,13 @@ __device__ __forceinline__ void sd_color_finish(const ColPend &cp, float out[3])
 }
 
 
+// CUs left to other kernels by the persistent grids (sd_reserve_cus; defined in
+// sdhip_field.hip): the multi-GPU step runs RCCL's all-gather of the previous frame beside the
+// render, one workgroup per channel, and a persistent workgroup whose CU is held waits for it
+extern int sd_g_cu_reserve;
+
+// Workgroups of a persistent one-per-CU grid: the device's CUs minus the reservation, rounded
+// down to a multiple of 8 (the kernels' XCD-aware ranges assume gridDim.x % 8 == 0)
 static int sd_num_cus() {
     static int n = 0;
     if (!n) {
@@ -200,7 +207,10 @@ static int sd_num_cus() {
         if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
             n = 256;
     }
-    return n;
+    const int r = sd_g_cu_reserve;
+    if (r <= 0) return n;
+    const int m = ((n - r) / 8) * 8;
+    return m >= 8 ? m : n;
 }
 
 

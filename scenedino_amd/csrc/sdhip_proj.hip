@@ -452,9 +452,9 @@ k_render_proj(const sd_render_args a, const sd_head m, const int32_t *__restrict
     typedef typename Tr::E E;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     // list mode (fallback behind the tile kernel, launched with its grid): workgroup b
-    // renders the tile kernel's overflow list (sdhip_render.h), usually empty -- every
-    // workgroup leaves before staging the weights
-    const int nlist = list ? __builtin_amdgcn_readfirstlane(list[SD_OVF_COUNT]) : 0;
+    // renders tile workgroup b's overflow list (sdhip_render.h), usually empty -- it leaves
+    // before staging the weights
+    const int nlist = list ? __builtin_amdgcn_readfirstlane(list[blockIdx.x]) : 0;
     if (list && nlist == 0) return;
     {
         uint4 *d = (uint4 *)lds;
@@ -485,21 +485,21 @@ k_render_proj(const sd_render_args a, const sd_head m, const int32_t *__restrict
     // a speed assumption only), so XCD x gets the contiguous rays [x R/8, (x+1) R/8): the
     // P rows its rays' epipolar lines cross stay in that XCD's 4 MiB L2 instead of every
     // XCD streaming all of P.  R below is this range's end.
-    // (list mode: one range -- the listed rays over the whole grid)
+    // (list mode: one range -- the workgroup's own list)
     const int nx = (!list && gridDim.x % 8 == 0) ? 8 : 1;
     const int xcd = blockIdx.x % nx;
-    const int nwaves = (gridDim.x / nx) * (SD_RWG / 64);
+    const int nwaves = list ? SD_RWG / 64 : (gridDim.x / nx) * (SD_RWG / 64);
     const int rps = (int)a.rays_per_sb;
-    // list != NULL: the rays of the listed blocks (SD_LIST_BLK consecutive rays each) form
-    // one virtual ray sequence, spread over the workgroups like a frame's rays
+    // list != NULL: the rays of the blocks in list b (SD_LIST_BLK consecutive rays each)
+    // form the virtual ray sequence of workgroup b
     const int Rreal = (int)a.R;
     const int64_t RA = list ? (int64_t)nlist * SD_LIST_BLK : a.R;
-    const int32_t *lblk = list ? list + SD_TICK_WORDS : nullptr;
+    const int32_t *lblk = list ? list + gridDim.x + (int64_t)blockIdx.x * sd_ovf_cap(a.R, gridDim.x) : nullptr;
     auto rmap = [&](int v) {
         return list ? min(lblk[v / SD_LIST_BLK] * SD_LIST_BLK + v % SD_LIST_BLK, Rreal - 1) : v;
     };
     const int R = (int)(RA * (xcd + 1) / nx);
-    const int ray0 = (int)(RA * xcd / nx) + (blockIdx.x / nx) * (SD_RWG / 64) + wave;
+    const int ray0 = (int)(RA * xcd / nx) + (list ? 0 : (blockIdx.x / nx) * (SD_RWG / 64)) + wave;
     if (ray0 >= R) return;
     const int nitems = ((R - ray0 + nwaves - 1) / nwaves) * nsub;
     // in-kernel z (a.z == NULL): sd_sample_z's arithmetic, jitter from the counter RNG
@@ -906,13 +906,13 @@ k_head_hc(const float *__restrict__ work, int64_t R, const sd_head m, float *__r
     const Frag *lw = (const Frag *)lds;
     const int lane = threadIdx.x & 63, j = lane & 15, g = lane >> 4;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // list != NULL: the tile kernel's overflow list (see k_render_proj; launched with the
-    // tile grid), its rays as one virtual sequence over the grid
-    const int64_t RA = list ? (int64_t)__builtin_amdgcn_readfirstlane(list[SD_OVF_COUNT]) * SD_LIST_BLK : R;
-    const int32_t *lblk = list ? list + SD_TICK_WORDS : nullptr;
+    // list != NULL: workgroup b takes tile workgroup b's overflow list (see k_render_proj;
+    // launched with the tile grid)
+    const int64_t RA = list ? (int64_t)__builtin_amdgcn_readfirstlane(list[blockIdx.x]) * SD_LIST_BLK : R;
+    const int32_t *lblk = list ? list + gridDim.x + (int64_t)blockIdx.x * sd_ovf_cap(R, gridDim.x) : nullptr;
     const int64_t ntile = (RA + 15) / 16;
-    const int64_t t0 = (int64_t)blockIdx.x * (SD_PWG / 64) + wave;
-    const int64_t tstep = (int64_t)gridDim.x * (SD_PWG / 64);
+    const int64_t t0 = list ? wave : (int64_t)blockIdx.x * (SD_PWG / 64) + wave;
+    const int64_t tstep = list ? SD_PWG / 64 : (int64_t)gridDim.x * (SD_PWG / 64);
     for (int64_t tile = t0; tile < ntile; tile += tstep) {
         const int64_t v = min(tile * 16 + j, RA - 1);
         const int64_t ray = list ? min((int64_t)lblk[v / SD_LIST_BLK] * SD_LIST_BLK + v % SD_LIST_BLK, R - 1)
@@ -1100,7 +1100,7 @@ static int64_t sd_hc_bytes(int64_t R, int32_t D) {
     return sd_head_hc(D) ? R * SD_HC_STRIDE * (int64_t)sizeof(float) : 0;
 }
 extern "C" int64_t sd_render_proj_work_bytes(int64_t R, int32_t D) {
-    return sd_hc_bytes(R, D) + ((4 * sd_ovf_words(R) + 15) / 16) * 16;
+    return sd_hc_bytes(R, D) + ((4 * sd_ovf_words(R, sd_num_cus()) + 15) / 16) * 16;
 }
 
 extern "C" int sd_render_tile_ok(const sd_render_args *a, const sd_head *m);
@@ -1154,11 +1154,6 @@ extern "C" int sd_render_proj(const sd_render_args *args, const sd_head *m, void
         // LDS-staged tile kernel (sdhip_tile.hip); groups whose tap box does not fit a tile
         // buffer are listed and rendered by the per-ray kernel behind it
         int32_t *ovf = (int32_t *)((uint8_t *)a.work + sd_hc_bytes(a.R, m->D));
-        // the tile kernel's ticket counters and overflow count start at zero
-        if (hipMemsetAsync(ovf, 0, SD_TICK_WORDS * sizeof(int32_t), s) != hipSuccess) {
-            sd_set_error("sd_render_proj: hipMemsetAsync of the work queue failed");
-            return -2;
-        }
         int rc = sd_render_tile_launch(&a, m, ovf, stream);
         if (rc) return rc;
         if (m->dtype == SD_F16) return sd_rp_ndt<SD_F16, 1>(a, *m, s, ovf);

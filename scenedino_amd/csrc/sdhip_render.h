@@ -8,18 +8,17 @@
 // (a group of 8 or 12 rays lists 2 or 3 blocks); the fallback kernels render the blocks
 #define SD_LIST_BLK 4
 #include "sdhip_point.h"
-// Work queue + overflow list of the tile kernel, in sd_render_proj's work (round 6):
-//   words [0, 8)   per-XCD group ticket counters (the tile kernel's dynamic schedule)
-//   word  8        overflow count (blocks listed)
-//   words [16, ..) the overflow list: block indices, appended by atomics
-// The first SD_TICK_WORDS words are zeroed by sd_render_proj before the tile kernel (one
-// 64-B memset); the list holds at most one entry per block of the frame (every group is
-// listed at most once), so it never overflows.  The fallback kernels read the count and
-// render the listed blocks over their whole grid.
-#define SD_TICK_WORDS 16
-#define SD_OVF_COUNT 8
-__host__ __device__ inline int64_t sd_ovf_words(int64_t R) {
-    return SD_TICK_WORDS + (R + SD_LIST_BLK - 1) / SD_LIST_BLK + 16;
+// The lists live in sd_render_proj's work: one per tile workgroup (slot = blockIdx.x; the
+// tile grid is one workgroup per CU), [slots] counts, then [slots][cap] block indices.  Every
+// tile workgroup writes its count, so nothing is reset before the launch (a 4-byte memset
+// was a 5 us fill kernel per frame), and fallback workgroup b renders list b.  cap bounds a
+// tile workgroup's rays: its XCD share of the groups over its nwg = slots / 8 workgroups,
+// < R / slots + 3 GR <= R / slots + 48.
+__host__ __device__ inline int64_t sd_ovf_cap(int64_t R, int64_t slots) {
+    return ((R + slots - 1) / slots + 64) / SD_LIST_BLK + 1;
+}
+__host__ __device__ inline int64_t sd_ovf_words(int64_t R, int64_t slots) {
+    return slots + slots * sd_ovf_cap(R, slots);
 }
 
 // LDS-DMA of 16 B per active lane (global_load_lds_dwordx4) into lds_addr + 16 * lane, as

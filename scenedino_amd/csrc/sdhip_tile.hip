@@ -116,8 +116,8 @@ extern "C" int sd_tile_prof(unsigned long long *out, int reset) {
 struct st_args {
     sd_render_args a;
     sd_head m;
-    int32_t *ovf;           // work queue + overflow list (sdhip_render.h): [8] XCD ticket counters,
-                            // overflow count, list -- the first SD_TICK_WORDS zeroed by the host
+    int32_t *ovf;           // overflow lists (sdhip_render.h): [gridDim.x] counts, [gridDim.x][ovf_cap] blocks
+    int32_t ovf_cap;
     int32_t ngroups;        // ceil(R / NW)
     int32_t tile_bytes;     // bytes per tile buffer (multiple of 1024)
 };
@@ -134,8 +134,7 @@ struct st_args {
 // rpw = rays per wave and step (2 for K <= 32: a group is NW rpw rays)
 __host__ __device__ constexpr int st_l_hs(int nw) { return ST_L_BOX + 2 * nw * 32; }         // [NW rpw rays][128] 16-bit hidden sums
 __host__ __device__ constexpr int st_l_ws(int nw, int rpw) { return st_l_hs(nw) + nw * rpw * ST_HS_ROW; }  // [NW rpw] f32 weight sums
-__host__ __device__ constexpr int st_l_gq(int nw, int rpw) { return st_l_ws(nw, rpw) + 16 * 4; }           // [4] int32 group queue (dynamic schedule)
-__host__ __device__ constexpr int st_l_ray(int nw, int rpw) { return st_l_gq(nw, rpw) + 16; }               // [NW waves][2] x rpw x 32 B ray words 0..7 (LDS-DMA)
+__host__ __device__ constexpr int st_l_ray(int nw, int rpw) { return st_l_ws(nw, rpw) + 16 * 4; }          // [NW waves][2] x rpw x 32 B ray words 0..7 (LDS-DMA)
 __host__ __device__ constexpr int st_l_rec(int nw, int rpw) { return st_l_ray(nw, rpw) + nw * 2 * 32 * rpw; }  // records: [NW waves][2][rpw K] x 40 B
 static_assert(st_l_rec(8, 1) % 16 == 0 && st_l_rec(12, 1) % 16 == 0 && st_l_rec(8, 2) % 16 == 0,
               "record area alignment");
@@ -198,7 +197,11 @@ __device__ __forceinline__ uint32_t st_wave_max2(uint32_t v) { return st_rows2<t
 // tile pitch (texels per staged row): pitch mod 8 in 2..6, so that the four taps
 // n, n + 1, n + pitch, n + pitch + 1 of a sample (288 B = 8 banks apart per texel) land
 // on four disjoint 8-bank groups of a transposed read
+#ifndef ST_PITCH4
+#define ST_PITCH4 0
+#endif
 __device__ __forceinline__ int st_pitch(int tw) {
+    if (ST_PITCH4) return tw + ((4 - tw) & 7);  // pitch = 4 (mod 8), see below
     const int r = tw & 7;
     return tw + (r == 7 ? 3 : r == 0 ? 2 : r == 1 ? 1 : 0);
 }
@@ -280,7 +283,7 @@ k_render_tile(const st_args sa) {
     constexpr int ST_WAVES = NW;
     constexpr int GR = NW * RPW;  // rays per group
     constexpr int ST_L_HS = st_l_hs(NW), ST_L_WS = st_l_ws(NW, RPW), ST_L_RAY = st_l_ray(NW, RPW),
-                  ST_L_REC = st_l_rec(NW, RPW), ST_L_GQ = st_l_gq(NW, RPW);
+                  ST_L_REC = st_l_rec(NW, RPW);
     typedef typename RMode<P>::F Tr;  // operands upstream of sigma (f16 in both modes)
     typedef typename RMode<P>::H Th;  // DINO head (bf16 in the bf16 mode)
     typedef typename Tr::Frag Frag;
@@ -314,47 +317,19 @@ k_render_tile(const st_args sa) {
     auto rqc = [&](int buf) { return (float2 *)(lds + rec_base + buf * KW * 40 + KW * 32); };
     const uint32_t tile0 = ST_L_REC + st_rec_bytes(NW, KW);
 
-    // Dynamic, XCD-aware schedule (round 6): the groups are cut into 8 contiguous ranges, one
-    // per XCD (workgroups b, b + 8, ... share an XCD: speed only -- neighbouring groups share
-    // P texels in that XCD's L2), each with a ticket counter in sa.ovf[0..8) (zeroed by the
-    // host).  Thread 0 takes the workgroup's next group from its own XCD's range and, once
-    // that is drained, from the next XCDs' in turn; the group ids go through a 4-entry LDS
-    // queue three steps ahead of the render (the ray pass runs one group ahead, the ray-word
-    // fetch two).  A workgroup whose CU was held by another kernel (RCCL's all-gather of the
-    // previous frame on its own stream, the multi-GPU step) and starts late finds the ranges
-    // drained and leaves: the static split made every late workgroup's share wait for it
-    // (tools/contention_ab.py: 16 CUs held 0.4 ms -> 0.62 -> 0.89 ms per frame).
+    // XCD-aware group ranges (workgroups b, b + 8, ... share an XCD, speed only)
     const int NG = sa.ngroups;
     const int nx = (gridDim.x % 8 == 0) ? 8 : 1;
-    const int xcd = blockIdx.x % nx;
-    int tcx = 0;  // thread 0: ranges drained so far (it moves on to XCD xcd + tcx)
-    auto tick = [&]() -> int {  // thread 0: a ticket of the current range (-1: none left)
-        return tcx < nx ? __hip_atomic_fetch_add(sa.ovf + (xcd + tcx) % nx, 1, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT)
-                        : -1;
-    };
-    // ticket t of the current range -> its group, or (range drained) the next ranges' tickets
-    auto resolve = [&](int t) -> int {
-        while (tcx < nx) {
-            const int x = (xcd + tcx) % nx;
-            const int glo = (int)((int64_t)NG * x / nx), ghi = (int)((int64_t)NG * (x + 1) / nx);
-            if (t >= 0 && glo + t < ghi) return glo + t;
-            ++tcx;
-            t = tick();
-        }
-        return -1;
-    };
-    auto take = [&]() -> int { return resolve(tick()); };
-    int *gq = (int *)(lds + ST_L_GQ);
-    if (threadIdx.x == 0) {
-        gq[0] = take();
-        gq[1] = gq[0] >= 0 ? take() : -1;
-        gq[2] = gq[1] >= 0 ? take() : -1;
+    const int xcd = blockIdx.x % nx, lb = blockIdx.x / nx, nwg = gridDim.x / nx;
+    const int glo = (int)((int64_t)NG * xcd / nx), ghi = (int)((int64_t)NG * (xcd + 1) / nx);
+    const int gfirst = glo + lb;
+    const int nsteps = gfirst < ghi ? (ghi - gfirst + nwg - 1) / nwg : 0;
+    int novf = 0;  // this workgroup's overflow blocks (workgroup-uniform)
+    int32_t *ovf_list = sa.ovf + gridDim.x + (int64_t)blockIdx.x * sa.ovf_cap;
+    if (nsteps == 0) {  // workgroup-uniform
+        if (threadIdx.x == 0) sa.ovf[blockIdx.x] = 0;
+        return;
     }
-    __syncthreads();
-    const int gfirst = gq[0];
-    if (gfirst < 0) return;  // workgroup-uniform: nothing left
-    int32_t *ovf_cnt = sa.ovf + SD_OVF_COUNT, *ovf_list = sa.ovf + SD_TICK_WORDS;
 
     const float zstep = (float)(1.0 / (double)K), zend = (float)(1.0 - 1.0 / (double)K);
     const int64_t cplane = (int64_t)a.Hc * a.Wc * 4;
@@ -636,11 +611,10 @@ k_render_tile(const st_args sa) {
         }
         if (!t.ok) {
             if (wave == 0 && lane == 0) {  // the group's rays as GR / SD_LIST_BLK list blocks
-                const int at = __hip_atomic_fetch_add(ovf_cnt, GR / SD_LIST_BLK, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT);
                 for (int b = 0; b < GR / SD_LIST_BLK; ++b)
-                    ovf_list[at + b] = grp * (GR / SD_LIST_BLK) + b;
+                    ovf_list[novf + b] = grp * (GR / SD_LIST_BLK) + b;
             }
+            novf += GR / SD_LIST_BLK;
             return t;
         }
         dma(t, tb, sbi);
@@ -796,7 +770,7 @@ k_render_tile(const st_args sa) {
     int ray = GR * grp + RPW * wave;  // the wave's first ray of the step
     int sbi = __builtin_amdgcn_readfirstlane((int)((unsigned)min(GR * grp, R - 1) / (unsigned)rps));
     ray_fetch(ray, 0);
-    if (gq[1] >= 0) ray_fetch(GR * gq[1] + RPW * wave, 1);
+    ray_fetch(GR * (grp + nwg) + RPW * wave, 1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     ray_pass(ray, 0, 0);
     ray_col(ray, 0);
@@ -813,16 +787,10 @@ k_render_tile(const st_args sa) {
     for (int i = 0; i < 19; ++i) pacc[i] = 0;
     tlast = __builtin_amdgcn_s_memtime();
 #endif
-    for (int n = 0; grp >= 0; ++n) {
+    for (int n = 0; n < nsteps; ++n) {
         const int buf = n & 1;
-        // the queue: groups n + 1, n + 2 (written before the previous step's barrier Y or in
-        // the prologue); thread 0 writes n + 3 into the slot of n - 1 during this step
-        const int ngrp = gq[(n + 1) & 3], nngrp = gq[(n + 2) & 3];
-        // thread 0: group n + 3's ticket, issued here and resolved in front of barrier Y (the
-        // atomic's round trip lands under the step; the wave waits for the step's DMAs there)
-        int tpend = -1;
-        if (threadIdx.x == 0 && nngrp >= 0) tpend = tick();
-        const bool has_next = ngrp >= 0;
+        const bool has_next = n + 1 < nsteps;
+        const int ngrp = grp + nwg;
         const int nray = GR * ngrp + RPW * wave;
         const int nsbi = has_next ? __builtin_amdgcn_readfirstlane((int)((unsigned)min(GR * ngrp, R - 1) / (unsigned)rps)) : 0;
         uint32_t lane_off = (uint32_t)((tq & 1) + (tq >> 1) * cur.pitch) * ST_TEX + 8u * (uint32_t)tp;
@@ -1003,7 +971,7 @@ k_render_tile(const st_args sa) {
         // the rays of step n + 2 into ray slot buf (its words, step n's rays, were read by
         // the ray pass of step n - 1): issued here, they land under this step's items (issued
         // in front of the closing vmcnt(0), as before, every step waited one memory latency)
-        if (ST_EARLY_FETCH && nngrp >= 0) ray_fetch(GR * nngrp + RPW * wave, buf);
+        if (ST_EARLY_FETCH && n + 2 < nsteps) ray_fetch(GR * (ngrp + nwg) + RPW * wave, buf);
         // HPRE 3: the next step's head weights (this group's; hwn was read by this step's head)
         if (ST_EARLY_HW && HPRE == 3 && cur.ok && wave < ndt) head_w(wave, hwn);
         ST_T(5);
@@ -1149,14 +1117,14 @@ k_render_tile(const st_args sa) {
         ray = nray;
         sbi = nsbi;
         cur = nxt;
-        if (!ST_EARLY_FETCH && nngrp >= 0) ray_fetch(GR * nngrp + RPW * wave, buf);
+        if (!ST_EARLY_FETCH && n + 2 < nsteps) ray_fetch(GR * (ngrp + nwg) + RPW * wave, buf);
         if (!ST_EARLY_HW && HPRE == 3 && prev_ok && wave < ndt) head_w(wave, hwn);  // the next head's W_dino
         if (!ST_WAIT_EARLY) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed
         ST_T(8);
-        if (threadIdx.x == 0) gq[(n + 3) & 3] = nngrp >= 0 ? resolve(tpend) : -1;
-        st_barrier_lds();  // Y: next tile complete; hsum of this group written; queue entry n + 3
+        st_barrier_lds();  // Y: next tile complete; hsum of this group written
         ST_T(9);
     }
+    if (threadIdx.x == 0) sa.ovf[blockIdx.x] = novf;
     if (prev_ok) {
         if (HPRE == 1) {
             HFrag hw[4];
@@ -1226,8 +1194,8 @@ extern "C" int sd_render_tile_ok(const sd_render_args *a, const sd_head *m) {
            st_tile_bytes(a->K) >= 16 * 1024;
 }
 
-// Launch; ovf: device int32 [sd_ovf_words(R)] (work queue + overflow list, sdhip_render.h;
-// its first SD_TICK_WORDS words zero).
+// Launch; ovf: device int32 [sd_ovf_words(R, sd_num_cus())] (the per-workgroup overflow
+// lists, sdhip_render.h; every count written by the kernel).
 extern "C" int sd_render_tile_launch(const sd_render_args *a, const sd_head *m, int32_t *ovf,
                                      void *stream) {
     hipStream_t s = (hipStream_t)stream;
@@ -1236,6 +1204,7 @@ extern "C" int sd_render_tile_launch(const sd_render_args *a, const sd_head *m, 
     sa.m = *m;
     sa.ovf = ovf;
     const int ncu = sd_num_cus();
+    sa.ovf_cap = (int32_t)sd_ovf_cap(a->R, ncu);
     const int nw = st_nw(a->K), rpw = st_rpw(a->K);
     sa.ngroups = (int)((a->R + nw * rpw - 1) / (nw * rpw));
     sa.tile_bytes = st_tile_bytes(a->K);

@@ -21,9 +21,12 @@ def main():
         torch.cuda.synchronize()
     work = net._last_render_work.view(torch.int32)
     R = bench.H * bench.W
-    # work queue + overflow list behind the hidden-composite scratch (sdhip_render.h): 8
-    # XCD ticket counters, the overflow count at word 8, the list from word 16
-    nblk = int(work[R * 132 + 8].item())
+    # per-workgroup lists at the end of work (sdhip_render.h): [ncu] counts, [ncu][cap] blocks
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    cap = ((R + ncu - 1) // ncu + 64) // 4 + 1
+    list_words = ((4 * (ncu + ncu * cap) + 15) // 16) * 16 // 4
+    ovf = work[work.numel() - list_words:]
+    nblk = int(ovf[:ncu].sum().item())
     print(f"{'offset' if offset else 'identity'} K={bench.K_SAMPLES}: {nblk} overflow 4-ray blocks = "
           f"{4 * nblk} rays of {R} ({100.0 * 4 * nblk / R:.2f} %)")
 
