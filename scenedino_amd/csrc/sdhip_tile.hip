@@ -197,11 +197,10 @@ __device__ __forceinline__ uint32_t st_wave_max2(uint32_t v) { return st_rows2<t
 // tile pitch (texels per staged row): pitch mod 8 in 2..6, so that the four taps
 // n, n + 1, n + pitch, n + pitch + 1 of a sample (288 B = 8 banks apart per texel) land
 // on four disjoint 8-bank groups of a transposed read
-#ifndef ST_PITCH4
-#define ST_PITCH4 0
-#endif
+// (round 6: pitch = 4 mod 8, conflict-free for the two samples of a half-wave read when they
+// sit 1 or 2 texels apart along an epipolar line, measured C2 neutral and C1 +5 % -- the
+// extra pad texels split more boxes; not kept)
 __device__ __forceinline__ int st_pitch(int tw) {
-    if (ST_PITCH4) return tw + ((4 - tw) & 7);  // pitch = 4 (mod 8), see below
     const int r = tw & 7;
     return tw + (r == 7 ? 3 : r == 0 ? 2 : r == 1 ? 1 : 0);
 }
