@@ -96,3 +96,17 @@ def test_field_dtype_and_grid_dtype_rejection_without_gpu():
     args = _lib.SdRenderArgs(grid_dtype=_lib.SD_BF16, work=16)
     rc = lib.sd_render_proj(ctypes.byref(args), ctypes.byref(head), None)
     assert rc == -1 and b"grid_dtype" in lib.sd_last_error()
+
+
+def test_reserve_cus_setter_without_gpu():
+    """sd_reserve_cus is a process-wide setter returning the previous value (no HIP call)."""
+    from scenedino_amd import _lib
+    prev = _lib.reserve_cus(16)
+    try:
+        assert _lib.reserve_cus(24) == 16
+        assert _lib.reserve_cus(-3) == 24  # negative clamps to 0
+        assert _lib.reserve_cus(0) == 0
+    finally:
+        _lib.reserve_cus(prev)
+    lib = _lib.load()
+    assert lib.sd_spin(0, 1.0, None) == -1 and b"sd_spin" in lib.sd_last_error()
