@@ -171,7 +171,15 @@ typedef struct sd_mlp {
                            /* b_in + W_in[:, :C] . empty_feature in accumulator-row order:  */
                            /* the layer-1 pre-code activation of a point outside the       */
                            /* encoder frustum (sd_render_fused / sd_field_query only)       */
+    int32_t proj_flags;    /* sd_project_grid*: bit 0 (SD_PROJ_EXACT_GRID) = the f32 grid   */
+                           /* enters the MFMA as a hi + lo f16 pair (hi = f16(g), lo =      */
+                           /* f16(g - hi)): P within ~2^-12 of W16 . G instead of W16 . G16 */
+                           /* -- twice the MFMAs; configs[3]'s K = 128 renders need it for  */
+                           /* the 1e-2 m depth bound.  0 = one f16 rounding.    */
+    int32_t pad_mlp;
 } sd_mlp;
+
+#define SD_PROJ_EXACT_GRID 1
 
 /* Fused coarse render of R rays x K samples: point generation, projection into the
  * encoder view, positional code, bilinear feature gather, MFMA MLP, softplus,

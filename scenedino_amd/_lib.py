@@ -38,7 +38,7 @@ class SdMlp(ctypes.Structure):
         ("w_in", _vp), ("b_in_h", _vp), ("w_sig_h", _vp), ("b_sigma", ctypes.c_float),
         ("w_out", _vp), ("b_dino", _vp),
         ("C", _i32), ("D", _i32), ("dtype", _i32), ("d_hidden", _i32),
-        ("b_empty_h", _vp),
+        ("b_empty_h", _vp), ("proj_flags", _i32), ("pad_mlp", _i32),
     ]
 
 
@@ -469,11 +469,22 @@ def render_fused(args: SdRenderArgs, mlp: SdMlp, ref_tensor):
            "sd_render_fused")
 
 
-def project_grid(grid, mlp: SdMlp, dtype):
+SD_PROJ_EXACT_GRID = 1
+
+
+def _with_flags(mlp: SdMlp, exact_grid: bool) -> SdMlp:
+    """A copy of the MLP record with sd_mlp.proj_flags for one projection call."""
+    m = SdMlp.from_buffer_copy(mlp)
+    m.proj_flags = SD_PROJ_EXACT_GRID if exact_grid else 0
+    return m
+
+
+def project_grid(grid, mlp: SdMlp, dtype, exact_grid: bool = False):
     """P = W_in[:, :C] . grid + b_in per pixel: (B, Hf, Wf, 128) in FIELD_DTYPE[dtype] (f16
     for both 16-bit modes; plain NHWC, 256 B per pixel).  grid (B, C, Hf, Wf) f32, NCHW or
-    channels-last."""
+    channels-last.  exact_grid: the grid as a hi + lo f16 operand pair (SD_PROJ_EXACT_GRID)."""
     lib = load()
+    mlp = _with_flags(mlp, exact_grid)
     B, C, H, W = grid.shape
     out = torch.empty(B, H, W, 128, device=grid.device, dtype=TORCH_DTYPE[FIELD_DTYPE[dtype]])
     if channels_last(grid):
@@ -486,14 +497,15 @@ def project_grid(grid, mlp: SdMlp, dtype):
     return out
 
 
-def project_grid_inputs(grid, mlp: SdMlp, dtype, img_nchw, poses_w2c, Ks):
+def project_grid_inputs(grid, mlp: SdMlp, dtype, img_nchw, poses_w2c, Ks, exact_grid: bool = False):
     """project_grid(grid) and frame_inputs(img_nchw, poses_w2c, Ks) in one launch
     (sd_project_grid_nhwc_inputs; channels-last grids -- others take the two calls).
     Returns (P, packed image, camera records)."""
     if not channels_last(grid):
         img, cam = frame_inputs(img_nchw, poses_w2c, Ks)
-        return project_grid(grid, mlp, dtype), img, cam
+        return project_grid(grid, mlp, dtype, exact_grid), img, cam
     lib = load()
+    mlp = _with_flags(mlp, exact_grid)
     B, C, H, W = grid.shape
     N, c3, Hc, Wc = img_nchw.shape
     assert c3 == 3, "colour images must have 3 channels"

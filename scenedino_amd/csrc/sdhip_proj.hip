@@ -64,7 +64,7 @@
 #ifndef SD_PROJ_WPE
 #define SD_PROJ_WPE 1
 #endif
-template <int P, bool NHWC>
+template <int P, bool NHWC, bool HILO>
 __global__ void __launch_bounds__(SD_PWG) __attribute__((amdgpu_waves_per_eu(NHWC ? SD_PROJ_WPE : 1)))
 k_project(const float *__restrict__ grid, int64_t B, int C, int64_t HW, int W, const sd_mlp m,
           uint32_t *__restrict__ out) {
@@ -112,12 +112,12 @@ k_project(const float *__restrict__ grid, int64_t B, int C, int64_t HW, int W, c
             for (int e = 0; e < 8; ++e) x1[e] = gp[16 * cs + e * cs];
         }
         auto kstep = [&](int q, float (&x)[8]) {
-            // the f32 grid as a hi + lo pair of 16-bit operands (see k_project_lds)
+            // HILO: the f32 grid as a hi + lo pair of 16-bit operands (see k_project_lds)
             Frag f, fl;
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
                 f[e] = (typename Tr::E)x[e];
-                fl[e] = (typename Tr::E)(x[e] - (float)f[e]);
+                if (HILO) fl[e] = (typename Tr::E)(x[e] - (float)f[e]);
             }
             if (q + 2 < nq) {
                 const float *gn = gp + (int64_t)(16 * (q + 2)) * cs;
@@ -127,7 +127,7 @@ k_project(const float *__restrict__ grid, int64_t B, int C, int64_t HW, int W, c
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
                 acc[t] = Tr::mma32(lw[(q * 4 + t) * SD_WAVE + lane], f, acc[t]);
-                acc[t] = Tr::mma32(lw[(q * 4 + t) * SD_WAVE + lane], fl, acc[t]);
+                if (HILO) acc[t] = Tr::mma32(lw[(q * 4 + t) * SD_WAVE + lane], fl, acc[t]);
             }
         };
         int q = 0;
@@ -200,7 +200,7 @@ k_project(const float *__restrict__ grid, int64_t B, int C, int64_t HW, int W, c
 #define PJ_OUTROW 272              // staging row stride (256 B of P + 16 pad)
 #define PJ_LDS (PJ_NS * PJ_SLOT + 32 * PJ_OUTROW)
 
-template <int P, bool FI>
+template <int P, bool FI, bool HILO>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1)))
 k_project_lds(const float *__restrict__ grid, int64_t npix, const sd_mlp m, uint32_t *__restrict__ out,
               const sd_frame_args fa) {
@@ -297,11 +297,12 @@ k_project_lds(const float *__restrict__ grid, int64_t npix, const sd_mlp m, uint
         issue(2 * k + PJ_NS - 1);
         // lane (pixel li, half h): slot 2k + (li >> 4), row li & 15, channels 16 q + 8 h ..
         const uint8_t *sl = lds + ((2 * k + (li >> 4)) % PJ_NS) * PJ_SLOT + (li & 15) * PJ_ROWB + 32 * h;
-        // round 6: the f32 grid enters the MFMA as a hi + lo pair of 16-bit operands
-        // (hi = f16(g), lo = f16(g - hi), g - hi exact in f32): the one rounding of G the
-        // projection made cost up to 5.8e-3 m of composited depth at configs[3]'s K = 128
-        // (tools/lowp_depth_emul.py; W_in stays one f16 operand), twice the MFMAs of an
-        // HBM-bound kernel
+        // HILO (sd_mlp.proj_flags, round 6): the f32 grid enters the MFMA as a hi + lo pair
+        // of 16-bit operands (hi = f16(g), lo = f16(g - hi), g - hi exact in f32): the one
+        // rounding of G the projection makes otherwise costs up to 5.8e-3 m of composited
+        // depth at configs[3]'s K = 128 (tools/lowp_depth_emul.py; W_in stays one f16
+        // operand).  Twice the MFMAs and the conversions: C2 +8 us, C5 +48 us, so only the
+        // renders that need it ask for it
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
             const f32x4 a = *(const f32x4 *)(sl + 64 * q), b = *(const f32x4 *)(sl + 64 * q + 16);
@@ -310,11 +311,13 @@ k_project_lds(const float *__restrict__ grid, int64_t npix, const sd_mlp m, uint
             for (int e = 0; e < 4; ++e) {
                 f[e] = (E)a[e];
                 f[4 + e] = (E)b[e];
-                fl[e] = (E)(a[e] - (float)f[e]);
-                fl[4 + e] = (E)(b[e] - (float)f[4 + e]);
+                if (HILO) {
+                    fl[e] = (E)(a[e] - (float)f[e]);
+                    fl[4 + e] = (E)(b[e] - (float)f[4 + e]);
+                }
             }
             acc = Tr::mma32(W[q], f, acc);
-            acc = Tr::mma32(W[q], fl, acc);
+            if (HILO) acc = Tr::mma32(W[q], fl, acc);
         }
         store_chunk(k);
     }
@@ -351,11 +354,13 @@ k_project_lds(const float *__restrict__ grid, int64_t npix, const sd_mlp m, uint
             for (int e = 0; e < 4; ++e) {
                 f[e] = (E)a[e];
                 f[4 + e] = (E)b[e];
-                fl[e] = (E)(a[e] - (float)f[e]);
-                fl[4 + e] = (E)(b[e] - (float)f[4 + e]);
+                if (HILO) {
+                    fl[e] = (E)(a[e] - (float)f[e]);
+                    fl[4 + e] = (E)(b[e] - (float)f[4 + e]);
+                }
             }
             acc = Tr::mma32(W[8 * HALF + q], f, acc);
-            acc = Tr::mma32(W[8 * HALF + q], fl, acc);
+            if (HILO) acc = Tr::mma32(W[8 * HALF + q], fl, acc);
         }
     };
     for (int k = 0; k < my; ++k) {
@@ -1002,7 +1007,12 @@ static int sd_project_any(const float *grid, int64_t B, int64_t Hf, int64_t Wf, 
                                (uint32_t *)out, fa ? *fa : none);
         };
         // both 16-bit modes: P in f16 (RMode, sdhip_render.h)
-        if (fa) go(k_project_lds<SD_F16, true>); else go(k_project_lds<SD_F16, false>);
+        const bool hl = (m->proj_flags & SD_PROJ_EXACT_GRID) != 0;
+        if (fa) {
+            if (hl) go(k_project_lds<SD_F16, true, true>); else go(k_project_lds<SD_F16, true, false>);
+        } else {
+            if (hl) go(k_project_lds<SD_F16, false, true>); else go(k_project_lds<SD_F16, false, false>);
+        }
         return sd_check_err();
     }
     if (fa) {  // other grids: the frame inputs by their own launch
@@ -1010,13 +1020,18 @@ static int sd_project_any(const float *grid, int64_t B, int64_t Hf, int64_t Wf, 
                                  fa->Ks, fa->s_k, fa->n, fa->out_cam, stream);
         if (rc) return rc;
     }
-#define SD_PROJ_LAUNCH(PP, NH)                                                                  \
-    do {                                                                                        \
-        sd_launch_proj(k_project<PP, NH>, work, lds_bytes, s, nblk);                            \
-        hipLaunchKernelGGL((k_project<PP, NH>), dim3((unsigned)nblk), dim3(SD_PWG), lds_bytes, s, \
-                           grid, B, m->C, HW, (int)Wf, *m, (uint32_t *)out);                    \
+#define SD_PROJ_LAUNCH(PP, NH, HL)                                                                \
+    do {                                                                                          \
+        sd_launch_proj(k_project<PP, NH, HL>, work, lds_bytes, s, nblk);                          \
+        hipLaunchKernelGGL((k_project<PP, NH, HL>), dim3((unsigned)nblk), dim3(SD_PWG), lds_bytes, s, \
+                           grid, B, m->C, HW, (int)Wf, *m, (uint32_t *)out);                      \
     } while (0)
-    if (nhwc) SD_PROJ_LAUNCH(SD_F16, true); else SD_PROJ_LAUNCH(SD_F16, false);
+    const bool hl = (m->proj_flags & SD_PROJ_EXACT_GRID) != 0;
+    if (nhwc) {
+        if (hl) SD_PROJ_LAUNCH(SD_F16, true, true); else SD_PROJ_LAUNCH(SD_F16, true, false);
+    } else {
+        if (hl) SD_PROJ_LAUNCH(SD_F16, false, true); else SD_PROJ_LAUNCH(SD_F16, false, false);
+    }
 #undef SD_PROJ_LAUNCH
     return sd_check_err();
 }

@@ -339,9 +339,11 @@ def test_projected_grid_channels_last_streaming_bit_equal(precision, B, Hf, Wf):
     b_out = torch.randn(65, generator=g) * 0.1
     dt = _lib.SD_BF16 if precision == "bf16" else _lib.SD_F16
     pk = PackedMLP(W_in.to(DEV), b_in.to(DEV), W_out.to(DEV), b_out.to(DEV), dt)
-    P_nchw = _lib.project_grid(grid.contiguous(), pk.rec, dt)
-    P_nhwc = _lib.project_grid(grid.contiguous(memory_format=torch.channels_last), pk.rec, dt)
-    assert torch.equal(P_nchw.view(torch.int16), P_nhwc.view(torch.int16))
+    for exact in (False, True):  # one f16 rounding of the grid, and its hi + lo pair
+        P_nchw = _lib.project_grid(grid.contiguous(), pk.rec, dt, exact_grid=exact)
+        P_nhwc = _lib.project_grid(grid.contiguous(memory_format=torch.channels_last), pk.rec, dt,
+                                   exact_grid=exact)
+        assert torch.equal(P_nchw.view(torch.int16), P_nhwc.view(torch.int16)), exact
 
 
 @pytest.mark.parametrize("precision", ["bf16", "fp16"])
@@ -360,18 +362,22 @@ def test_projected_grid_vs_dense_projection(precision):
     pk = PackedMLP(W_in.to(DEV), b_in.to(DEV), W_out.to(DEV), b_out.to(DEV), dt)
     P = _lib.project_grid(grid.to(DEV), pk.rec, dt).double().cpu()   # (2, Hf, Wf, 128)
     assert P.shape == (2, Hf, Wf, 128)
-    # both 16-bit modes project in f16 (the bf16 mode keeps bf16 for the DINO head only);
-    # round 6: the grid enters as a hi + lo pair of f16 operands (exact to ~2^-22), W_in as
-    # one f16 operand, P rounded once to f16 at the store
+    # both 16-bit modes project in f16 (the bf16 mode keeps bf16 for the DINO head only)
     tdt = _lib.TORCH_DTYPE[_lib.FIELD_DTYPE[dt]]
     assert tdt == torch.float16
-    ref = torch.einsum("nc,bchw->bhwn", W_in[:, :C].to(tdt).double(), grid.double()) \
-        + b_in.double()
-    assert rel_l2(P, ref) < 6e-4
-    # against the single-rounded grid the error would be the grid's f16 rounding as well
     ref1 = torch.einsum("nc,bchw->bhwn", W_in[:, :C].to(tdt).double(), grid.to(tdt).double()) \
         + b_in.double()
-    assert rel_l2(P, ref) < rel_l2(P, ref1)
+    assert rel_l2(P, ref1) < 1e-3
+    # SD_PROJ_EXACT_GRID (round 6, the K > 64 renders): the grid as a hi + lo pair of f16
+    # operands (exact to ~2^-22), W_in one f16 operand, P rounded once to f16 at the store
+    Px = _lib.project_grid(grid.to(DEV), pk.rec, dt, exact_grid=True).double().cpu()
+    ref = torch.einsum("nc,bchw->bhwn", W_in[:, :C].to(tdt).double(), grid.double()) \
+        + b_in.double()
+    assert rel_l2(Px, ref) < 6e-4
+    # against the single-rounded grid the error would be the grid's f16 rounding as well
+    assert rel_l2(Px, ref) < rel_l2(Px, ref1) and rel_l2(Px, ref) < rel_l2(P, ref)
+    # the packed record itself is not modified by the per-call flag
+    assert pk.rec.proj_flags == 0
 
 
 def test_render_full_192x640x64_vs_reference_subsample():
