@@ -705,7 +705,12 @@ extern "C" int sd_field_prof(unsigned long long *out, int reset) {
 // WL: the W_out fragments staged in LDS (16-bit, when they fit beside W_in: D <= 128 at
 // C = 256, any D <= 512 on the projected grid's 128 columns), else read from L2 (f32, and
 // 16-bit 384-d heads over a 256-channel grid)
-template <int P, bool WL>
+// DEF (bf16 dino, D <= 64: the SSCBench query feeding sd_seg_query): a tile's outputs leave
+// in the NEXT tile's grid phase, once its tap loads are issued.  Stores count in vmcnt
+// like loads and retire in order with them, so a tap load issued behind a tile's 32
+// row stores waits for their acknowledgements too; issued behind the loads, the stores
+// have a whole tile of MLP work to complete before the next wait that includes them.
+template <int P, bool WL, bool DEF = false>
 __global__ void __launch_bounds__(WG<P>::T, 1)
 k_field(const sd_field_args a, const sd_mlp m, const LdsPlan pl) {
     typedef Prec<P> Pr;
@@ -789,6 +794,31 @@ k_field(const sd_field_args a, const sd_mlp m, const LdsPlan pl) {
     uint32_t pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t tlast = __builtin_amdgcn_s_memtime();
 #endif
+    // DEF: the previous tile's outputs wait in this wave's 4-KiB LDS block (the tile's
+    // 32 rows of D bf16, as in HBM: one contiguous 64 D-byte run), its sigma and frustum
+    // flag in registers, until flush() copies the block out with 16-byte stores
+    uint16_t *scr = (uint16_t *)(lds + pl.total - WG<P>::W * 4096 + wave * 4096);
+    float pend_sig = 0.f;
+    int64_t pend_tile = -1, pend_p = 0;
+    bool pend_ok = false, pend_inv = false;
+    auto flush = [&]() __attribute__((always_inline)) {
+        if (pend_tile < 0) return;
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t vo = (uint32_t)(pend_tile * 64 * m.D);
+        for (int k = 0; k < (m.D >> 4); ++k) {  // 64 D bytes = D / 16 rounds of 64 x 16 B
+            const uint32_t off = (uint32_t)(k * 64 + lane) * 16u;
+            typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+            const u32x4v v = *(const u32x4v *)((const uint8_t *)scr + off);
+            __builtin_amdgcn_raw_buffer_store_b128(v, rdino, vo + off, 0, 0);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (pend_ok && h == 0) {
+            a.sigma[pend_p] = pend_sig;
+            if (a.invalid_f) a.invalid_f[pend_p] = pend_inv ? 1 : 0;
+        }
+    };
     for (; tt < tend; tt += tstep) {
         const int64_t tn = tt + tstep;
         const bool more = tn < tend;
@@ -810,6 +840,10 @@ k_field(const sd_field_args a, const sd_mlp m, const LdsPlan pl) {
                     SD_STEP(r1, q + 1, true);
                     SD_STEP(r2, q + 2, true);
                     SD_STEP(r3, q + 3, true);
+                }
+                if (DEF) {  // every tap load of this tile issued: the previous tile's stores
+                    flush();
+                    pend_tile = -1;
                 }
                 SD_STEP(r0, q, false);
                 SD_STEP(r1, q + 1, false);
@@ -859,7 +893,13 @@ k_field(const sd_field_args a, const sd_mlp m, const LdsPlan pl) {
             Prec<P>::mma2(wo, dt, acc, lane, ov);
             // O layout: row = point (r&3)+8(r>>2)+4h of this tile, column = dim li
             const int dim = dt * 32 + li;
-            if (SD_FQ_ABL_NOSTORE) {
+            if (DEF) {
+                // the previous tile's block left in flush(), before this tile's grid chunks
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    scr[((r & 3) + 8 * (r >> 2) + 4 * h) * m.D + dim] =
+                        __builtin_bit_cast(uint16_t, (__bf16)(ov[r] + bd));
+            } else if (SD_FQ_ABL_NOSTORE) {
                 if (ov[0] == 12345.f) a.dino[tile] = ov[1];  // keep the product alive
             } else {
                 // buffer stores at per-lane byte offsets (row, column dim): rows past the
@@ -886,9 +926,16 @@ k_field(const sd_field_args a, const sd_mlp m, const LdsPlan pl) {
             out_tile(dt, bdino[dt]);
         }
         // wide heads (configs[3]: D = 384): the tiles past the 4 with register-cached biases
-        for (int dt = 4; dt < ndt; ++dt) out_tile(dt, m.b_dino[dt * 32 + li]);
+        if (!DEF)
+            for (int dt = 4; dt < ndt; ++dt) out_tile(dt, m.b_dino[dt * 32 + li]);
         FQ_T(3);
-        if (cur.valid && h == 0) {
+        if (DEF) {
+            pend_tile = tile;
+            pend_p = cur.p;
+            pend_ok = cur.valid;
+            pend_sig = sigma;
+            pend_inv = cur.geo.inv_f;
+        } else if (cur.valid && h == 0) {
             a.sigma[cur.p] = sigma;
             if (a.invalid_f) a.invalid_f[cur.p] = cur.geo.inv_f ? 1 : 0;
         }
@@ -909,6 +956,7 @@ k_field(const sd_field_args a, const sd_mlp m, const LdsPlan pl) {
         if (more) cur = nxt;
         FQ_T(4);
     }
+    if (DEF) flush();  // the last tile's outputs
 #if SD_FQ_PROF
     if (lane == 0)
         for (int i = 0; i < 8; ++i) atomicAdd(&fq_prof[i], (unsigned long long)pacc[i]);
@@ -1131,6 +1179,16 @@ extern "C" int sd_field_query(const sd_field_args *args, const sd_mlp *mlp, void
     if (a.P == 0) return 0;
     const int64_t ntiles = (a.B * a.P + 31) / 32;
     hipStream_t s = (hipStream_t)stream;
+#ifndef SD_FQ_DEFER
+#define SD_FQ_DEFER 1
+#endif
+    // (k_field DEF: + one 4-KiB output block per wave after the plan's LDS image)
+    LdsPlan pd = pl;
+    pd.total += WG<SD_F16>::W * 4096;
+    if (SD_FQ_DEFER && mlp->dtype != SD_F32 && pl.wout_in_lds && a.dino_dtype == SD_BF16 &&
+        mlp->D <= 64 && pd.total <= 160 * 1024)
+        return mlp->dtype == SD_F16 ? sd_launch<SD_F16>(k_field<SD_F16, true, true>, ntiles, pd, s, a, *mlp)
+                                    : sd_launch<SD_BF16>(k_field<SD_BF16, true, true>, ntiles, pd, s, a, *mlp);
     if (mlp->dtype == SD_F16)
         return pl.wout_in_lds ? sd_launch<SD_F16>(k_field<SD_F16, true>, ntiles, pl, s, a, *mlp)
                               : sd_launch<SD_F16>(k_field<SD_F16, false>, ntiles, pl, s, a, *mlp);

@@ -232,7 +232,11 @@ extern "C" int sd_seg_prof(unsigned long long *out, int reset) {
 // with a per-point power-of-two scale (its largest value lands in [128, 256)), W2 with the
 // per-tensor one of the packed record; the scales leave in the f32 epilogue (exact).
 template <int MODE, bool F8>
-__global__ void __launch_bounds__(SG_WAVES * 64) k_seg_head(const void *__restrict__ dino_in,
+#ifndef SG_WPE
+#define SG_WPE 1  // waves per SIMD the register budget must allow (2: measured no faster)
+#endif
+__global__ void __launch_bounds__(SG_WAVES * 64) __attribute__((amdgpu_waves_per_eu(SG_WPE)))
+k_seg_head(const void *__restrict__ dino_in,
                                                             int32_t x16, int64_t P, int32_t DF,
                                                             const float *__restrict__ sigma,
                                                             float neg_vox, sd_seg_head h,
