@@ -46,7 +46,7 @@ enum sd_dtype { SD_F32 = 0, SD_BF16 = 1, SD_F16 = 2 };
 const char *sd_last_error(void);
 
 /* Library / ABI version (bumped on any signature change).  10: grid_dtype fields in
- * sd_render_args / sd_field_args, sd_field_dtype. */
+ * sd_render_args / sd_field_args, sd_field_dtype.  11: sd_seg_head.frag_layout. */
 int sd_abi_version(void);
 
 /* Element type of the grids the field / render kernels read for an MLP of `dtype`
@@ -411,8 +411,25 @@ typedef struct sd_seg_head {
     const void *wg;
     const float *g2;       /* [d_latent/32][2][16]  2 W2^T b2                         */
     float b2sq;            /* |b2|^2                                                   */
-    int32_t pad1;
+    /* SD_SEG_FRAG32 (0): the maps above, v_mfma_f32_32x32x16_bf16 fragments (needed by
+     * the fp8 norm, w2_f8).  SD_SEG_FRAG16 (1, ABI 11, the default record): the same
+     * products on v_mfma_f32_16x16x32_bf16 (lane l: row / column l & 15, k = 8 (l >> 4) + j;
+     * accumulator register i of lane group g = l >> 4 holds row 4 g + i), every map with
+     * 16-row tiles and 32-deep k-steps:
+     *   w1 [d_latent/16][d_in/32][64][8]  W1[16 t + (l&15)][32 s + 8 (l>>4) + j]
+     *   w2, wm [d_full/16][d_latent/32][64][8], wl [d_code/16][d_latent/32][64][8],
+     *   wn2 [d_code/16][d_full/32][64][8]  W[16 t + (l&15)][perm16(q, l>>4, j)],
+     *     perm16(q, g, j) = 32 q + 16 (j >> 2) + 4 g + (j & 3)
+     *   wg [d_latent/32][16][64][8]: fragment i of tile t = G hi (i & 4 == 0) or lo of
+     *     row tile 2 t + (i >> 3), k-step i & 3
+     *   centres [ceil(n_clusters/16)][2][d_code/32][64][8]
+     *   row vectors (b1, b2, bl, bo, bm, bn1, g2) [d/16][4][4]: vec[16 t + 4 g + i]
+     * (scenedino_amd/seg_pack.py builds both)                                           */
+    int32_t frag_layout;
 } sd_seg_head;
+
+#define SD_SEG_FRAG32 0
+#define SD_SEG_FRAG16 1
 
 /* Grow: out = 3x3x3 max filter of the (nx, ny, nz) f32 density grid in (z fastest),
  * F.max_pool3d(kernel_size=3, stride=1, padding=1) as evaluate_model_sscbench.py:755-756

@@ -14,7 +14,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # SDHIP_LIB: alternative build of the same library (diagnostic builds only)
 LIB_PATH = os.environ.get("SDHIP_LIB") or os.path.join(_HERE, "libsdhip.so")
-ABI_VERSION = 10
+ABI_VERSION = 11
 CAM_WORDS = 36  # floats per camera record (include/sdhip.h SD_CAM_WORDS)
 
 SD_F32 = 0
@@ -94,7 +94,7 @@ class SdSegHead(ctypes.Structure):
         ("wn2", _vp), ("centres", _vp), ("assign", _vp),
         ("n_clusters", _i32), ("d_in", _i32), ("d_latent", _i32), ("d_full", _i32),
         ("d_code", _i32), ("w2_f8", _vp), ("w2_f8_scale", ctypes.c_float), ("pad0", _i32),
-        ("wg", _vp), ("g2", _vp), ("b2sq", ctypes.c_float), ("pad1", _i32),
+        ("wg", _vp), ("g2", _vp), ("b2sq", ctypes.c_float), ("frag_layout", _i32),
     ]
 
 
@@ -470,6 +470,8 @@ def render_fused(args: SdRenderArgs, mlp: SdMlp, ref_tensor):
 
 
 SD_PROJ_EXACT_GRID = 1
+SD_SEG_FRAG32 = 0  # sd_seg_head.frag_layout (include/sdhip.h)
+SD_SEG_FRAG16 = 1
 
 
 def _with_flags(mlp: SdMlp, exact_grid: bool) -> SdMlp:

@@ -42,7 +42,7 @@ extern "C" void sd_set_error(const char *msg) {
     g_err[sizeof(g_err) - 1] = 0;
 }
 extern "C" const char *sd_last_error(void) { return g_err; }
-extern "C" int sd_abi_version(void) { return 10; }
+extern "C" int sd_abi_version(void) { return 11; }
 
 int sd_g_cu_reserve = 0;
 

@@ -28,6 +28,8 @@ accumulator register i of lane half h holds row (i & 3) + 8 (i >> 2) + 4 h):
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -65,6 +67,34 @@ def _frag_permuted(W: torch.Tensor):
     j = torch.arange(8, device=dev).view(1, 1, 1, -1)
     rows = 32 * t + (l & 31)
     cols = 32 * (q >> 1) + 16 * (q & 1) + 8 * (j >> 2) + 4 * (l >> 5) + (j & 3)
+    rows, cols = torch.broadcast_tensors(rows, cols)
+    return W[rows, cols]
+
+
+def _accrow16(n_tiles: int, device):
+    """Row vectors of the 16x16x32 layout: register i of lane group g holds row 4 g + i."""
+    t = torch.arange(n_tiles, device=device).view(-1, 1, 1)
+    g = torch.arange(4, device=device).view(1, -1, 1)
+    i = torch.arange(4, device=device).view(1, 1, -1)
+    return 16 * t + 4 * g + i  # (n_tiles, 4, 4)
+
+
+def _frag16(W: torch.Tensor, permuted: bool):
+    """(rows, cols) -> [rows/16][cols/32][64][8]: A operands of v_mfma_f32_16x16x32_bf16
+    (lane l holds A[l & 15][8 (l >> 4) + j]).  permuted: k-step q, element j of lane group
+    g = l >> 4 <- column 32 q + 16 (j >> 2) + 4 g + (j & 3), the rows an accumulator pair
+    (row tiles 2 q, 2 q + 1) holds in the registers the kernel turns into the B operand."""
+    R, Ccols = W.shape
+    dev = W.device
+    t = torch.arange(R // 16, device=dev).view(-1, 1, 1, 1)
+    q = torch.arange(Ccols // 32, device=dev).view(1, -1, 1, 1)
+    l = torch.arange(64, device=dev).view(1, 1, -1, 1)
+    j = torch.arange(8, device=dev).view(1, 1, 1, -1)
+    rows = 16 * t + (l & 15)
+    if permuted:
+        cols = 32 * q + 16 * (j >> 2) + 4 * (l >> 4) + (j & 3)
+    else:
+        cols = 32 * q + 8 * (l >> 4) + j
     rows, cols = torch.broadcast_tensors(rows, cols)
     return W[rows, cols]
 
@@ -112,7 +142,7 @@ class PackedSegHead:
     expand-only record (transform_expand)."""
 
     def __init__(self, dim_reduction, stego_head=None, cluster_head=None, device=None,
-                 frag_dtype=torch.bfloat16, fp8: bool = False):
+                 frag_dtype=torch.bfloat16, fp8: bool = False, mfma: int | None = None):
         W1 = _mat(dim_reduction.linear_in.weight)
         b1 = dim_reduction.linear_in.bias.detach().double()
         W2 = _mat(dim_reduction.linear_out.weight)
@@ -127,15 +157,31 @@ class PackedSegHead:
                 f"linear_in {tuple(W1.shape)}, linear_out {tuple(W2.shape)}")
         bf = frag_dtype  # bf16 for the kernel; float64 lets tests emulate the MFMA chain
         fdt = torch.float64 if frag_dtype == torch.float64 else torch.float32
-        self.w1 = _frag_natural(W1).to(bf).contiguous()
-        self.b1 = b1[_accrow(d_latent // 32, dev)].to(fdt).contiguous()
-        self.w2 = _frag_permuted(W2).to(bf).contiguous()
-        self.b2 = b2[_accrow(d_full // 32, dev)].to(fdt).contiguous()
+        # fragment layout: 16x16x32 by default (faster); the fp8 norm's kernel
+        # reads the 32x32x16 maps
+        # (SCENEDINO_AMD_SEG_MFMA=32 selects the 32x32x16 record for A/B runs)
+        if mfma is None:
+            mfma = 32 if fp8 else int(os.environ.get("SCENEDINO_AMD_SEG_MFMA", "16"))
+        self.mfma = mfma
+        if self.mfma not in (16, 32) or (fp8 and self.mfma != 32):
+            raise ValueError("mfma must be 16 or 32 (fp8 needs 32)")
+        m16 = self.mfma == 16
+        perm = (lambda W: _frag16(W, True)) if m16 else _frag_permuted
+        nat = (lambda W: _frag16(W, False)) if m16 else _frag_natural
+        rowv = (lambda v, n: v[_accrow16(n // 16, dev)]) if m16 else (lambda v, n: v[_accrow(n // 32, dev)])
+        self.w1 = nat(W1).to(bf).contiguous()
+        self.b1 = rowv(b1, d_latent).to(fdt).contiguous()
+        self.w2 = perm(W2).to(bf).contiguous()
+        self.b2 = rowv(b2, d_full).to(fdt).contiguous()
         self.d_in, self.d_latent, self.d_full = d_in, d_latent, d_full
         G = W2.t() @ W2
         Ghi = G.to(bf).double()
-        self.wg = torch.cat([_frag_permuted(Ghi), _frag_permuted(G - Ghi)], 1).to(bf).contiguous()
-        self.g2 = (2 * (W2.t() @ b2))[_accrow(d_latent // 32, dev)].to(fdt).contiguous()
+        if m16:  # tile t = row tiles 2 t, 2 t + 1: [t][(row tile) (hi, lo) (k-step)]
+            gh = torch.stack([perm(Ghi), perm(G - Ghi)], 1)  # (8, 2, 4, 64, 8)
+            self.wg = gh.reshape(d_latent // 32, 16, 64, 8).to(bf).contiguous()
+        else:
+            self.wg = torch.cat([_frag_permuted(Ghi), _frag_permuted(G - Ghi)], 1).to(bf).contiguous()
+        self.g2 = rowv(2 * (W2.t() @ b2), d_latent).to(fdt).contiguous()
         self.b2sq = float(b2 @ b2)
         self.seg = stego_head is not None and cluster_head is not None
         null = None
@@ -143,7 +189,8 @@ class PackedSegHead:
                       b2=self.b2.data_ptr(), wl=null, bl=null, bo=null, wm=null, bm=null,
                       bn1=null, wn2=null, centres=null, assign=null, n_clusters=0,
                       d_in=d_in, d_latent=d_latent, d_full=d_full, d_code=0,
-                      wg=self.wg.data_ptr(), g2=self.g2.data_ptr(), b2sq=self.b2sq)
+                      wg=self.wg.data_ptr(), g2=self.g2.data_ptr(), b2sq=self.b2sq,
+                      frag_layout=_lib.SD_SEG_FRAG16 if m16 else _lib.SD_SEG_FRAG32)
         if self.seg:
             lin = stego_head.linear_path[0]
             nl0, nl2 = stego_head.nonlinear_path[0], stego_head.nonlinear_path[2]
@@ -157,13 +204,13 @@ class PackedSegHead:
                     "sd_seg_query needs StegoClusterHead(d_full -> 64, mid = d_full)")
             L = Wl @ W2
             M = Wn1 @ W2
-            self.wl = _frag_permuted(L).to(bf).contiguous()
-            self.bl = (Wl @ b2)[_accrow(d_code // 32, dev)].to(fdt).contiguous()
-            self.bo = (bl + bn2)[_accrow(d_code // 32, dev)].to(fdt).contiguous()
-            self.wm = _frag_permuted(M).to(bf).contiguous()
-            self.bm = (Wn1 @ b2)[_accrow(d_full // 32, dev)].to(fdt).contiguous()
-            self.bn1 = bn1[_accrow(d_full // 32, dev)].to(fdt).contiguous()
-            self.wn2 = _frag_permuted(Wn2).to(bf).contiguous()
+            self.wl = perm(L).to(bf).contiguous()
+            self.bl = rowv(Wl @ b2, d_code).to(fdt).contiguous()
+            self.bo = rowv(bl + bn2, d_code).to(fdt).contiguous()
+            self.wm = perm(M).to(bf).contiguous()
+            self.bm = rowv(Wn1 @ b2, d_full).to(fdt).contiguous()
+            self.bn1 = rowv(bn1, d_full).to(fdt).contiguous()
+            self.wn2 = perm(Wn2).to(bf).contiguous()
             # KMeansParamHead._kmeans_cosine: F.normalize(cluster_centers, dim=1) (fp32)
             cn = F.normalize(cluster_head.cluster_centers.detach().to(fdt), dim=1).to(dev)
             n_cl = cn.shape[0]
@@ -171,12 +218,13 @@ class PackedSegHead:
                 raise NotImplementedError("cluster centres must be (1..256, 64)")
             self.centres = cn[:, _accrow(d_code // 32, dev)].contiguous()  # (k, rt, h, 16)
             # the kernel's copy: hi + lo bf16 A fragments, rows = clusters (zero-padded to
-            # 32 per tile), [tile][hi, lo][k-step][64][8] in the permuted k order
-            nct = (n_cl + 31) // 32
-            cpad = torch.zeros(32 * nct, d_code, dtype=torch.float64, device=dev)
+            # 32 (16) per tile), [tile][hi, lo][k-step][64][8] in the permuted k order
+            ct_rows = 16 if m16 else 32
+            nct = (n_cl + ct_rows - 1) // ct_rows
+            cpad = torch.zeros(ct_rows * nct, d_code, dtype=torch.float64, device=dev)
             cpad[:n_cl] = cn.double()
             chi = cpad.to(bf).double()
-            self.wc = torch.stack([_frag_permuted(chi), _frag_permuted(cpad - chi)], 1).to(bf).contiguous()
+            self.wc = torch.stack([perm(chi), perm(cpad - chi)], 1).to(bf).contiguous()
             self.assign = cluster_head.pseudo_assignment.detach().to(dev, torch.int32).contiguous()
             if self.assign.numel() != n_cl:
                 raise ValueError("pseudo_assignment must have one entry per cluster")
