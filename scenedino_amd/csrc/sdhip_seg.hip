@@ -233,7 +233,7 @@ extern "C" int sd_seg_prof(unsigned long long *out, int reset) {
 // per-tensor one of the packed record; the scales leave in the f32 epilogue (exact).
 template <int MODE, bool F8>
 #ifndef SG_WPE
-#define SG_WPE 1  // waves per SIMD the register budget must allow (2: measured no faster)
+#define SG_WPE 1  // waves per SIMD the register budget must allow
 #endif
 __global__ void __launch_bounds__(SG_WAVES * 64) __attribute__((amdgpu_waves_per_eu(SG_WPE)))
 k_seg_head(const void *__restrict__ dino_in,
@@ -691,7 +691,9 @@ k_seg_head(const void *__restrict__ dino_in,
 // same FLOPs per cycle as 32x32x16, and the chip holds a higher clock on it under load
 // (MI355X_MICROARCH.md, DVFS item 7); a timing probe of this kernel's MFMA mix measured
 // 0.75 -> 0.69 ms (profiles/r6_c5).
+#ifndef SG16_NCT
 #define SG16_NCT 4  // 16-point column tiles per wave
+#endif
 #define SG_MFMA16(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (c), 0, 0, 0)
 
 __device__ __forceinline__ f32x4_t sg_rows4(const float *__restrict__ vec, int t, int g) {
@@ -1110,7 +1112,7 @@ extern "C" int sd_seg_query(const void *dino, int32_t dino_dtype, int64_t P,
         return -1;
     }
     if (P == 0) return 0;
-    const int64_t per_wg = (int64_t)SG_WAVES * 32 * SG_NT;
+    const int64_t per_wg = (int64_t)SG_WAVES * (h->frag_layout == SD_SEG_FRAG16 ? 16 * SG16_NCT : 32 * SG_NT);
     const int64_t nblk = (P + per_wg - 1) / per_wg;
     if (nblk > 0x7fffffffLL) {
         sd_set_error("sd_seg_query: too many points");
@@ -1131,7 +1133,6 @@ extern "C" int sd_seg_query(const void *dino, int32_t dino_dtype, int64_t P,
                        (int32_t)(dino_dtype == SD_BF16), P, h->d_full, sigma, neg_vox, *h, labels, seg, \
                        dino_full)
     if (h->frag_layout == SD_SEG_FRAG16) {
-        static_assert(SG16_NCT * 16 == SG_NT * 32, "points per wave of the two layouts");
         if (mode == 1) SG_LAUNCH16(1);
         else if (mode == 2) SG_LAUNCH16(2);
         else SG_LAUNCH16(3);
