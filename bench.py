@@ -431,7 +431,7 @@ def main_c5(args, world, rank, local_rank, dist, device, host_stage=False):
         # HBM bytes per k_seg_head launch (1-GPU launch shape) from the committed PMC
         # summary (tools/c5_traffic.sh: FETCH_SIZE x 2 + WRITE_SIZE, separate passes)
         seg_traffic, seg_tsrc = None, None
-        for tn in ("r5_c5_traffic.json", "r3_c5_traffic.json", "r2_c5_traffic.json"):
+        for tn in ("r6_c5_traffic.json", "r5_c5_traffic.json", "r3_c5_traffic.json"):
             tf = os.path.join(ROOT, "profiles", tn)
             if dist or not os.path.exists(tf):
                 continue
