@@ -4,6 +4,8 @@ import ctypes
 import os
 import re
 
+import pytest
+
 from conftest import ROOT
 
 
@@ -110,3 +112,25 @@ def test_reserve_cus_setter_without_gpu():
         _lib.reserve_cus(prev)
     lib = _lib.load()
     assert lib.sd_spin(0, 1.0, None) == -1 and b"sd_spin" in lib.sd_last_error()
+
+
+def test_seg_record_layout_rejection_without_gpu():
+    """ABI 11: sd_seg_head.frag_layout names the record's MFMA fragment maps; an unknown
+    layout, or the fp8 norm (32x32 maps only) on a 16x16 record, is rejected before any HIP
+    call.  The CPU packer writes the layout it built."""
+    import torch
+    from scenedino_amd import _lib
+    from scenedino_amd.seg_pack import PackedSegHead
+    lib = _lib.load()
+    dr = torch.nn.Module()
+    dr.linear_in, dr.linear_out = torch.nn.Linear(64, 128), torch.nn.Linear(128, 768)
+    assert PackedSegHead(dr).rec.frag_layout == _lib.SD_SEG_FRAG16
+    assert PackedSegHead(dr, mfma=32).rec.frag_layout == _lib.SD_SEG_FRAG32
+    with pytest.raises(ValueError):
+        PackedSegHead(dr, mfma=8)
+    for layout, w2_f8, what in ((5, None, b"frag_layout"), (_lib.SD_SEG_FRAG16, 16, b"fp8")):
+        rec = _lib.SdSegHead(w1=16, b1=16, w2=16, b2=16, wg=16, g2=16, d_in=64, d_latent=128,
+                             d_full=768, frag_layout=layout, w2_f8=w2_f8)
+        rc = lib.sd_seg_query(16, _lib.SD_BF16, 32, ctypes.byref(rec), None, 0.2, None, None,
+                              16, None)
+        assert rc == -1 and what in lib.sd_last_error()
