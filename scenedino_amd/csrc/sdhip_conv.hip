@@ -450,9 +450,12 @@ template <int TW>
 __host__ __device__ constexpr int cvh_ha() { return (cvh_hpix<TW>() * 8 + 511) / 512; }  // halo DMAs / thread
 template <int TW>
 __host__ __device__ constexpr int cvh_halo_bytes() { return cvh_ha<TW>() * 512 * 16; }
+// (the 256-column tiles take the whole 160 KiB: two weight stages beside the two halos)
+template <int BN>
+__host__ __device__ constexpr int cvh_lds_max() { return BN == 256 ? 160 * 1024 : CV_LDS_MAX; }
 template <int TW, int BN>
 __host__ __device__ constexpr int cvh_rsb() {
-    return (CV_LDS_MAX - 2 * cvh_halo_bytes<TW>()) / (BN * 128) >= 6 ? 6 : (CV_LDS_MAX - 2 * cvh_halo_bytes<TW>()) / (BN * 128);
+    return (cvh_lds_max<BN>() - 2 * cvh_halo_bytes<TW>()) / (BN * 128) >= 6 ? 6 : (cvh_lds_max<BN>() - 2 * cvh_halo_bytes<TW>()) / (BN * 128);
 }
 template <int TW, int BN, bool STF32>
 __host__ __device__ constexpr int cvh_lds_bytes() {
@@ -703,6 +706,13 @@ int sd_conv_big_try(const sd_gemm_args *args, void *stream) {
         int tw = 0, hbn = 0;
         const int64_t t256 = ((g.M + 255) / 256) * (g.N % 256 ? 0 : g.N / 256);
         if (t256 < ncu * 15 / 8 && g.OW >= 32 && htiles(32, 128) >= ncu * 7 / 8) tw = 32, hbn = 128;
+        // 8 x 32 halo tiles of all 256 output channels where the im2col tiles would be
+        // 256 x 256 (the 192x640 output conv): 143 -> 132 us, bit-equal (the same K order;
+        // tools/conv_halo256_ab.py, profiles/r6_dpt/conv_halo256_ab.txt).  SD_CONV_HALO256=0:
+        // the im2col tiles
+        const char *h256 = getenv("SD_CONV_HALO256");
+        if (!tw && !(h256 && h256[0] == '0') && g.N % 256 == 0 && g.OW >= 32 && t256 >= ncu * 15 / 8)
+            tw = 32, hbn = 256;
         if (tw) {
             auto hgo = [&](auto kern, int lds) {
                 sd_lds_attr((const void *)kern, lds);
@@ -723,7 +733,11 @@ int sd_conv_big_try(const sd_gemm_args *args, void *stream) {
                     else CVH_K(TW_, BN_, SD_EPI_BF16, false, false);                                 \
                 }                                                                                    \
             }
-            CVH_TILE(32, 128)
+            if (hbn == 128) {
+                CVH_TILE(32, 128)
+            } else {
+                CVH_TILE(32, 256)
+            }
 #undef CVH_TILE
 #undef CVH_K
             return hipGetLastError() == hipSuccess ? 1 : -2;

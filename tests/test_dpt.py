@@ -148,12 +148,14 @@ def test_dpt_head_vs_reference(gpu):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("B,H,W,Cin,Cout,f32", [(1, 96, 320, 256, 256, False), (1, 192, 640, 256, 256, True),
-                                                (1, 192, 640, 256, 256, False), (2, 61, 250, 128, 384, True)])
+                                                (1, 192, 640, 256, 256, False), (2, 61, 250, 128, 384, True),
+                                                (1, 197, 650, 256, 256, True)])
 def test_conv3x3_big_tiles(gpu, B, H, W, Cin, Cout, f32, monkeypatch):
     """sdhip_conv.hip's tiles for the DPT head's 96x320 / 192x640 convolutions -- the 8 x 32
-    halo tiles (default) and the 256-row im2col tiles (SD_CONV_BIG=b); 2 x 61 x 250 with
-    Cout 384: ragged edge tiles, 128-column tiles, two images' padding -- against torch fp32
-    on the same bf16 operands and against sd_gemm's k_gemm path (SD_CONV_BIG=0)."""
+    halo tiles (default: 128 output channels per tile at 96x320, all 256 at 192x640) and the
+    256-row im2col tiles (SD_CONV_BIG=b); 2 x 61 x 250 with Cout 384: ragged edge tiles,
+    128-column tiles, two images' padding; 197 x 650: ragged 256-column halo tiles -- against
+    torch fp32 on the same bf16 operands and against sd_gemm's k_gemm path (SD_CONV_BIG=0)."""
     from scenedino_amd import _lib
     g = torch.Generator().manual_seed(H + W + Cout)
     x = torch.randn(B, Cin, H, W, generator=g)
