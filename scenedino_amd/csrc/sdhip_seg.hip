@@ -739,8 +739,11 @@ k_seg_head16(const void *__restrict__ dino_in, int32_t x16, int64_t P, int32_t D
         }
     };
     auto landed = [&]() {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+#ifndef SG16_EXP
+#define SG16_EXP 0  // timing probes only (wrong results): 1 no waits, 2 no barrier
+#endif
+        if (SG16_EXP != 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (SG16_EXP == 0) __syncthreads();
     };
     auto gsrc = [&](int t) { return [=](int i) { return (const uint8_t *)h.wg + (int64_t)t * 16384 + i * 1024; }; };
     const int KS = DF / 32;  // Wn2 k-steps
