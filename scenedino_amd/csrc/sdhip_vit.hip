@@ -1156,12 +1156,23 @@ __global__ void __launch_bounds__(256) k_attn_lds(const __bf16 *__restrict__ Q,
     }
 }
 
-__global__ void __launch_bounds__(256) k_attn_dir(const __bf16 *__restrict__ Q,
-                                                  const __bf16 *__restrict__ K,
-                                                  const __bf16 *__restrict__ Vt, int T, int Tp,
-                                                  int H, float sl2e, __bf16 *__restrict__ out) {
-    __shared__ float s_o[4][2][16][64];  // [wave][hd tile][acc register][lane]
-    __shared__ float s_m[4][64], s_l[4][64];
+// AT_DIR_NW (build knob): waves per k_attn_dir workgroup = key blocks of 64 in flight per
+// 32 queries (4: two blocks per wave at 481 tokens; 8: one -- measured no faster, 7.41 vs
+// 7.31 us at ViT-S/16, `profiles/r6_vit/lg_nw_ab.txt`)
+#ifndef AT_DIR_NW
+#define AT_DIR_NW 4
+#endif
+constexpr int at_dir_lds(int nwa) { return nwa * (2 * 16 * 64 + 2 * 64) * 4; }
+template <int NWA>
+__global__ void __launch_bounds__(64 * NWA) k_attn_dir(const __bf16 *__restrict__ Q,
+                                                       const __bf16 *__restrict__ K,
+                                                       const __bf16 *__restrict__ Vt, int T, int Tp,
+                                                       int H, float sl2e, __bf16 *__restrict__ out) {
+    // dynamic LDS: [wave][hd tile][acc register][lane] partial O, then m and l per wave
+    extern __shared__ __attribute__((aligned(16))) float at_dyn[];
+    float (*s_o)[2][16][64] = (float (*)[2][16][64])at_dyn;
+    float (*s_m)[64] = (float (*)[64])(at_dyn + NWA * 2 * 16 * 64);
+    float (*s_l)[64] = s_m + NWA;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, h = lane >> 5;
     const int bh = blockIdx.y;
@@ -1202,9 +1213,9 @@ __global__ void __launch_bounds__(256) k_attn_dir(const __bf16 *__restrict__ Q,
     };
     int kb = 64 * wave;
     if (kb < Tp) fload(kb, kf, vf);
-    for (; kb < Tp; kb += 256) {
-        const bool more = kb + 256 < Tp;
-        if (more) fload(kb + 256, kn, vn);  // next block in flight under this one
+    for (; kb < Tp; kb += 64 * NWA) {
+        const bool more = kb + 64 * NWA < Tp;
+        if (more) fload(kb + 64 * NWA, kn, vn);  // next block in flight under this one
         at_block(S, qb, kf, vf, kb, T, h, sl2e);
         if (more) {
 #pragma unroll
@@ -1219,7 +1230,7 @@ __global__ void __launch_bounds__(256) k_attn_dir(const __bf16 *__restrict__ Q,
                     for (int s = 0; s < 2; ++s) vf[ht][t][s] = vn[ht][t][s];
         }
     }
-    // merge the 4 waves' partial softmax states
+    // merge the NWA waves' partial softmax states
     s_m[wave][lane] = S.m;  // identical in both halves
     s_l[wave][lane] = S.l;  // per-half partial sums
 #pragma unroll
@@ -1229,31 +1240,35 @@ __global__ void __launch_bounds__(256) k_attn_dir(const __bf16 *__restrict__ Q,
     __syncthreads();
     float M = -INFINITY;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) M = fmaxf(M, s_m[w][lane]);
-    float fw[4], L = 0.f;
+    for (int w = 0; w < NWA; ++w) M = fmaxf(M, s_m[w][lane]);
+    float fw[NWA], L = 0.f;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
+    for (int w = 0; w < NWA; ++w) {
         const float mw = s_m[w][lane];
         fw[w] = mw == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(mw - M);  // a wave with no block
         L = fmaf(fw[w], s_l[w][r] + s_l[w][r + 32], L);
     }
     const float inv = 1.f / L;
     if (q < T) {
-        // wave w writes accumulator registers 4w..4w+3 of both head-dim tiles:
-        // rows 32 ht + 8 w + 4 h + e (4 contiguous head-dim values, one 8-B store)
+        // wave w writes accumulator registers i0 .. i0 + RW - 1 (i0 = RW w, RW = 16 / NWA)
+        // of both head-dim tiles: register i holds row 32 ht + 8 (i / 4) + 4 h + i % 4, so
+        // the wave's RW values are contiguous head-dim entries (one 8-B / 4-B store)
+        constexpr int RW = 16 / NWA;
+        const int i0 = RW * wave;
         const int b = bh / H, head = bh - b * H;
         __bf16 *dst = out + ((int64_t)b * T + q) * (int64_t)(H * AT_HD) + head * AT_HD;
 #pragma unroll
         for (int ht = 0; ht < 2; ++ht) {
-            bf16x4 v;
+            typedef __attribute__((ext_vector_type(RW))) __bf16 bfv;
+            bfv v;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
+            for (int e = 0; e < RW; ++e) {
                 float acc = 0.f;
 #pragma unroll
-                for (int w = 0; w < 4; ++w) acc = fmaf(fw[w], s_o[w][ht][4 * wave + e][lane], acc);
+                for (int w = 0; w < NWA; ++w) acc = fmaf(fw[w], s_o[w][ht][i0 + e][lane], acc);
                 v[e] = (__bf16)(acc * inv);
             }
-            *(bf16x4 *)(dst + 32 * ht + 8 * wave + 4 * h) = v;
+            *(bfv *)(dst + 32 * ht + 8 * (i0 >> 2) + 4 * h + (i0 & 3)) = v;
         }
     }
 }
@@ -1560,16 +1575,25 @@ __global__ void __launch_bounds__(256) k_upsample2x(const __bf16 *__restrict__ i
 // rounded to bf16 as its output is) into LDS, so the normalised rows never reach HBM and the
 // separate norm launch (~5 us at 481 tokens, as long as the GEMM itself) disappears.  The
 // whole K = C of the weight tile is loaded into registers before the norm starts: its
-// latency hides under the norm.  A 256-thread workgroup computes a 32 x 64 tile, wave w
+// latency hides under the norm.  A 64 LG_NW-thread workgroup computes a 32 x 16 LG_NW tile, wave w
 // the columns 16 w .. 16 w + 15 by v_mfma_f32_16x16x32_bf16 (A from LDS, B from registers).
+// LG_NW (build knob): waves per workgroup -- the tile is 32 x 16 LG_NW, each wave normalises
+// 32 / LG_NW rows, so every row's LayerNorm is recomputed once per 16 LG_NW output columns.
+// Round 6: 8 (32 x 128 tiles, 4 rows per wave) instead of 4: ViT-S/16 qkv 7.68 -> 6.85 us,
+// fc1 7.51 -> 6.61 us, pass 0.521 -> 0.496 ms; 2 and 16 waves slower
+// (`profiles/r6_vit/lg_nw_ab.txt`)
+#ifndef LG_NW
+#define LG_NW 8
+#endif
 #define LG_BM 32
-#define LG_BN 64
+#define LG_BN (16 * LG_NW)
 
 template <int PER, int EPI>
-__global__ void __launch_bounds__(256) k_lngemm(sd_gemm_args g, const float *__restrict__ x,
-                                                const float *__restrict__ lw,
-                                                const float *__restrict__ lb, float eps) {
+__global__ void __launch_bounds__(64 * LG_NW) k_lngemm(sd_gemm_args g, const float *__restrict__ x,
+                                                       const float *__restrict__ lw,
+                                                       const float *__restrict__ lb, float eps) {
     constexpr int C = 64 * PER, LDA = C + 8, NK = C / 32;
+    constexpr int RW = LG_BM / LG_NW;  // LayerNorm rows per wave
     __shared__ __attribute__((aligned(16))) __bf16 sA[LG_BM * LDA];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1581,10 +1605,10 @@ __global__ void __launch_bounds__(256) k_lngemm(sd_gemm_args g, const float *__r
     bf16x8 wb[NK];
 #pragma unroll
     for (int s = 0; s < NK; ++s) wb[s] = *(const bf16x8 *)(wr + 32 * s);
-    // LayerNorm of rows 8 w .. 8 w + 7 (lane = columns lane + 64 i), RB rows at a time with
-    // all their loads issued first (one memory latency per batch, the reductions of the
-    // batch's rows interleaved)
-    constexpr int RB = PER <= 6 ? 8 : 4;
+    // LayerNorm of rows RW w .. RW w + RW - 1 (lane = columns lane + 64 i), RB rows at a
+    // time with all their loads issued first (one memory latency per batch, the reductions
+    // of the batch's rows interleaved)
+    constexpr int RB = (PER <= 6 ? 8 : 4) < RW ? (PER <= 6 ? 8 : 4) : RW;
     // lane = column pairs 2 lane + 128 i: 8-B loads, packed f32 math (v_pk_*), one packed
     // bf16 pair per LDS write
     constexpr int P2 = PER / 2;
@@ -1595,11 +1619,11 @@ __global__ void __launch_bounds__(256) k_lngemm(sd_gemm_args g, const float *__r
         lbv[i] = *(const f32x2 *)(lb + 2 * lane + 128 * i);
     }
 #pragma unroll
-    for (int r0 = 0; r0 < 8; r0 += RB) {
+    for (int r0 = 0; r0 < RW; r0 += RB) {
         f32x2 v[RB][P2];
 #pragma unroll
         for (int rr = 0; rr < RB; ++rr) {
-            const float *xr = x + min(m0 + 8 * wave + r0 + rr, g.M - 1) * C;
+            const float *xr = x + min(m0 + RW * wave + r0 + rr, g.M - 1) * C;
 #pragma unroll
             for (int i = 0; i < P2; ++i) v[rr][i] = *(const f32x2 *)(xr + 2 * lane + 128 * i);
         }
@@ -1627,7 +1651,7 @@ __global__ void __launch_bounds__(256) k_lngemm(sd_gemm_args g, const float *__r
         }
 #pragma unroll
         for (int rr = 0; rr < RB; ++rr) {
-            const int rl = 8 * wave + r0 + rr;
+            const int rl = RW * wave + r0 + rr;
             const f32x2 rs = {rstd[rr], rstd[rr]};
 #pragma unroll
             for (int i = 0; i < P2; ++i) {
@@ -2132,7 +2156,7 @@ extern "C" int sd_ln_gemm(const sd_gemm_args *args, const float *x, const float 
     if (g.M == 0) return 0;
     dim3 grid((unsigned)((g.N + LG_BN - 1) / LG_BN), (unsigned)((g.M + LG_BM - 1) / LG_BM));
     hipStream_t s = (hipStream_t)stream;
-#define SD_LG(PER, E) hipLaunchKernelGGL((k_lngemm<PER, E>), grid, dim3(256), 0, s, g, x, ln_w, ln_b, eps)
+#define SD_LG(PER, E) hipLaunchKernelGGL((k_lngemm<PER, E>), grid, dim3(64 * LG_NW), 0, s, g, x, ln_w, ln_b, eps)
     if (C == 384) {
         if (g.epi == SD_EPI_QKV) SD_LG(6, SD_EPI_QKV);
         else if (g.epi == SD_EPI_GELU) SD_LG(6, SD_EPI_GELU);
@@ -2180,7 +2204,9 @@ extern "C" int sd_attention(const void *q, const void *k, const void *vt, int32_
                            (__bf16 *)out);
     } else {
         dim3 grid((unsigned)((tokens + 31) / 32), (unsigned)(B * heads));
-        hipLaunchKernelGGL(k_attn_dir, grid, dim3(256), 0, (hipStream_t)stream, (const __bf16 *)q,
+        constexpr int lds_b = at_dir_lds(AT_DIR_NW);
+        if (lds_b > 64 * 1024) sd_lds_attr((const void *)k_attn_dir<AT_DIR_NW>, lds_b);
+        hipLaunchKernelGGL(k_attn_dir<AT_DIR_NW>, grid, dim3(64 * AT_DIR_NW), lds_b, (hipStream_t)stream, (const __bf16 *)q,
                            (const __bf16 *)k, (const __bf16 *)vt, tokens, tokens_pad, heads, sl2e,
                            (__bf16 *)out);
     }

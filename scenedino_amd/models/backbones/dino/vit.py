@@ -200,7 +200,7 @@ def vit_forward(vit: VisionTransformer, images: torch.Tensor, packed: _Packed,
     grids = []
     to_grid = _lib.tokens_to_nhwc if nhwc else _lib.tokens_to_grid
     scale = hd ** -0.5
-    # norm1 / norm2 fused into the qkv / fc1 GEMM prologues (sd_ln_gemm: 32 x 64 tiles) for
+    # norm1 / norm2 fused into the qkv / fc1 GEMM prologues (sd_ln_gemm: 32 x 128 tiles) for
     # ViT-S at small token counts (481 tokens: 0.61 -> 0.57 ms per pass); measured slower
     # for C = 768 (DINOv2-B/14: 0.90 -> 0.99 ms against sd_layernorm + the 64 x 64-tile
     # sd_gemm) and at 1921 tokens (the narrow tile re-reads the weights per row tile)
