@@ -163,11 +163,11 @@ __device__ __forceinline__ void vt_ln_tail(const sd_gemm_args &g, const VtLnTail
     __syncthreads();
     uint32_t *flag = (uint32_t *)smem;
     if (tid == 0)
-        *flag = __hip_atomic_fetch_add(lt.cnt + blockIdx.y, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+        *flag = __hip_atomic_fetch_add(lt.cnt + m0 / BM, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
                 gridDim.x - 1;
     __syncthreads();
     if (!*flag) return;  // workgroup-uniform
-    if (tid == 0) __hip_atomic_store(lt.cnt + blockIdx.y, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) __hip_atomic_store(lt.cnt + m0 / BM, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int lane = tid & 63, wave = tid >> 6;
     const int C = (int)g.N;
     const int nch = C <= 512 ? 2 : C <= 768 ? 3 : 4;  // sd_layernorm's PER
@@ -246,6 +246,12 @@ __device__ __forceinline__ void vt_store16(T *p, const V &v) {
     }
 }
 
+#ifndef VT_XCD_MAP
+#define VT_XCD_MAP 0  // measured no faster on the encoder (profiles/r6_vit/gemm_tile_order_splitk_ab.txt)
+#endif
+#ifndef VT_XCD_GM
+#define VT_XCD_GM 4
+#endif
 template <int BM, int BN, int BK, int EPI, bool CONV>
 __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g, float *__restrict__ sk_slab, uint32_t *__restrict__ sk_cnt,
                                               VtLnTail lt) {
@@ -279,7 +285,25 @@ __global__ void __launch_bounds__(256) k_gemm(sd_gemm_args g, float *__restrict_
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = SK ? 0 : wave >> 1, wn = SK ? 0 : wave & 1;
     const int r = lane & 31, h = lane >> 5;
-    const int64_t m0 = (int64_t)blockIdx.y * BM, n0 = (int64_t)blockIdx.x * BN;
+    // XCD-aware tile order (VT_XCD_MAP): workgroups are dealt to the 8 XCDs round-robin by
+    // linear id, so the tiles of XCD x are taken as the x-th contiguous eighth of a grouped
+    // order (VT_XCD_GM row tiles per group, column-major inside it): each XCD works on a
+    // compact block of row x column tiles and re-reads its A rows / B columns from its own L2
+    // instead of every XCD fetching nearly all of A and B.  Tiles only move between
+    // workgroups: the arithmetic is unchanged.
+    int bx = (int)blockIdx.x, by = (int)blockIdx.y;
+    if (VT_XCD_MAP) {
+        const int nx = (int)gridDim.x, ny = (int)gridDim.y, T = nx * ny;
+        if ((T & 7) == 0 && T >= 16 && ny > 1 && nx > 1) {
+            const int lin = by * nx + bx;
+            const int t = (lin & 7) * (T >> 3) + (lin >> 3);
+            const int gsz = VT_XCD_GM * nx, grp = t / gsz, loc = t - grp * gsz;
+            const int rows = min(VT_XCD_GM, ny - grp * VT_XCD_GM);
+            by = grp * VT_XCD_GM + loc % rows;
+            bx = loc / rows;
+        }
+    }
+    const int64_t m0 = (int64_t)by * BM, n0 = (int64_t)bx * BN;
     const __bf16 *A = (const __bf16 *)g.a;
     const __bf16 *Wt = (const __bf16 *)g.w;
     // cross-workgroup split-K (32 x 32 ring tiles, gridDim.z > 1): this workgroup's K steps
@@ -2017,8 +2041,11 @@ static void vt_pick_gemm(const sd_gemm_args &g, hipStream_t s, const VtLnTail &l
     auto ksplit = [&](int bk) {
         const char *e = getenv("SD_SPLITK_WG");
         const int64_t cap = (e && e[0]) ? atoll(e) : 0;
+        // SD_SPLITK_STEPS: the fewest K steps a slice may keep (default 2)
+        const char *es = getenv("SD_SPLITK_STEPS");
+        const int64_t mst = (es && es[0]) ? atoll(es) : 2;
         int ks = 1;
-        while (ks < 8 && t32 * ks * 2 <= cap && g.K / bk >= 4 * ks) ks *= 2;
+        while (ks < 8 && t32 * ks * 2 <= cap && g.K / bk >= mst * ks * 2) ks *= 2;
         return ks;
     };
     if (VT_SK256 && VT_RING && t32 <= (int64_t)sd_num_cus() && g.K % 256 == 0 &&
