@@ -352,10 +352,12 @@ k_render_tile(const st_args sa) {
             st_dma4(a.rays + (int64_t)rmap(ray, r) * a.ray_dim + w,
                     lds0 + ST_L_RAY + (wave * 2 + slot) * 32 * RPW);
     };
-    // this lane's ray of the wave's RPW (ray pass: lane = record k' = rsl K + k)
+    // this lane's ray of the wave's RPW for ray-pass sample slot p (record k' = 64 p + lane
+    // = r K + k: K <= 32 -- p = 0 only, r = lane / K; K = 64 -- r = p)
     const int rsl = RPW == 1 ? 0 : min(lane / K, RPW - 1);
-    const int kl = lane - rsl * K;  // its sample (RPW = 2)
-    const float *rl = nullptr;  // this ray pass's words (set by ray_pass; RPW = 2: per lane)
+    auto rsl_p = [&](int p) { return RPW == 1 ? 0 : min((64 * p + lane) / K, RPW - 1); };
+    auto kl_p = [&](int p) { return RPW == 1 ? 64 * p + lane : 64 * p + lane - rsl_p(p) * K; };
+    const float *rl = nullptr;  // this ray pass's words of the wave's first ray (set by ray_pass)
     auto load_ray_z = [&](int ray, float zq[2 * ST_MAXP]) {
         float zo[ST_MAXP];
         if (ZIN) {
@@ -364,18 +366,24 @@ k_render_tile(const st_args sa) {
 #pragma unroll
                 for (int p = 0; p < ST_MAXP; ++p) zo[p] = zr[min(64 * p + lane, K - 1)];
             } else {
-                const float *zr = a.z + (int64_t)min(rmap(ray, rsl), R - 1) * K;
-                zo[0] = zr[min(kl, K - 1)];  // (lanes past 2 K: K = 16)
                 zo[1] = 0.f;
+#pragma unroll
+                for (int p = 0; p < ST_MAXP; ++p) {
+                    if (64 * p >= KW) break;  // wave-uniform
+                    const float *zr = a.z + (int64_t)min(rmap(ray, rsl_p(p)), R - 1) * K;
+                    zo[p] = zr[min(kl_p(p), K - 1)];  // (lanes past 2 K: K = 16)
+                }
             }
         } else {
-            const float near = rl[6], far = rl[7];
-            const uint64_t base = a.z_offset + (uint64_t)rmap(ray, rsl) * (uint64_t)K;
             zo[1] = 0.f;
 #pragma unroll
             for (int p = 0; p < ST_MAXP; ++p) {
                 if (64 * p >= KW) break;  // wave-uniform: KW <= 64 draws one sample per lane
-                const int k = RPW == 1 ? min(64 * p + lane, K - 1) : kl;
+                const int r = rsl_p(p);
+                const float *rw = rl + 8 * r;
+                const float near = rw[6], far = rw[7];
+                const uint64_t base = a.z_offset + (uint64_t)rmap(ray, r) * (uint64_t)K;
+                const int k = RPW == 1 ? min(64 * p + lane, K - 1) : kl_p(p);
                 zo[p] = sd_z_sample_rng(near, far, K, k, sd_uniform(a.z_seed, base + k), zstep, zend,
                                     a.z_lindisp);
             }
@@ -406,7 +414,7 @@ k_render_tile(const st_args sa) {
             // address would turn the camera-record reads into vector loads); a group's rays
             // share their super-batch (rays_per_sb % GR == 0)
             const int sbi = __builtin_amdgcn_readfirstlane((int)((unsigned)ray / (unsigned)rps));
-            rl = (const float *)(lds + ST_L_RAY + (wave * 2 + slot) * 32 * RPW) + 8 * rsl;
+            rl = (const float *)(lds + ST_L_RAY + (wave * 2 + slot) * 32 * RPW);
             // colour view = encoder view (the single-frame render, ids_render = ids_encoder):
             // the host passes the same camera records for both (cam_c == cam_f), so the
             // colour taps are the encoder-view taps at equal resolution (kernel-uniform test)
@@ -414,14 +422,15 @@ k_render_tile(const st_args sa) {
             float zq[2 * ST_MAXP];
             load_ray_z(ray, zq);
             ST_T(10);
-            const float ox = rl[0], oy = rl[1], oz = rl[2], dx = rl[3], dy = rl[4], dz = rl[5];
             uint4 *r0 = rq0(buf);
             f32x4 *r1 = rq1(buf);
             float2 *rc = rqc(buf);
 #pragma unroll
             for (int p = 0; p < ST_MAXP; ++p) {
-                const int k = 64 * p + lane;  // record k' (RPW = 2: ray rsl's sample kl)
-                if (64 * p < KW && k < KW && (RPW == 1 || rmap(ray, rsl) < R)) {
+                const int k = 64 * p + lane;  // record k' (RPW = 2: ray rsl_p(p)'s sample kl_p(p))
+                if (64 * p < KW && k < KW && (RPW == 1 || rmap(ray, rsl_p(p)) < R)) {
+                    const float *rw = rl + 8 * rsl_p(p);
+                    const float ox = rw[0], oy = rw[1], oz = rw[2], dx = rw[3], dy = rw[4], dz = rw[5];
                     const float z0 = zq[2 * p];
                     const float px = ox + z0 * dx, py = oy + z0 * dy, pz = oz + z0 * dz;  // nerf.py:252
                     const PointGeo geo = ST_GEO((sd_cfloat *)(a.cam_f + sbi * SD_CAM_WORDS), px, py, pz,
@@ -477,6 +486,25 @@ k_render_tile(const st_args sa) {
                 *(uint4 *)bw = uint4{q[0], q[1], q[2], q[3]};
                 *(uint4 *)(bw + 16) = uint4{q[4], q[5], q[6], q[7]};
             }
+        } else if (RPW == 2 && KW == 128) {
+            // two rays of 64 samples, one sample of each per lane (slot p = ray p): part
+            // 2 p + h = lanes [32 h, 32 h + 32) of slot p = items 4 p + 2 h, + 1 (halves = rays)
+            const uint32_t mn0 = st_row_red2<false>(bmin0), mx0 = st_row_red2<true>(bmax0);
+            const uint32_t mn1 = st_row_red2<false>(bmin1), mx1 = st_row_red2<true>(bmax1);
+            uint32_t q[8];
+            q[0] = st_rows2<false>(mn0, 0, 1);
+            q[1] = st_rows2<true>(mx0, 0, 1);
+            q[2] = st_rows2<false>(mn0, 2, 3);
+            q[3] = st_rows2<true>(mx0, 2, 3);
+            q[4] = st_rows2<false>(mn1, 0, 1);
+            q[5] = st_rows2<true>(mx1, 0, 1);
+            q[6] = st_rows2<false>(mn1, 2, 3);
+            q[7] = st_rows2<true>(mx1, 2, 3);
+            ST_T(12);
+            if (lane == 0) {
+                *(uint4 *)bw = uint4{q[0], q[1], q[2], q[3]};
+                *(uint4 *)(bw + 16) = uint4{q[4], q[5], q[6], q[7]};
+            }
         } else {
             bmin0 = st_wave_min2(bmin0);
             bmax0 = st_wave_max2(bmax0);
@@ -503,7 +531,7 @@ k_render_tile(const st_args sa) {
     // (min, max) pairs -- the 4 quarters when KW = 64, else the 2 halves -- so half h =
     // parts [h NPART / 2, (h + 1) NPART / 2), the whole group = [0, NPART).  One copy of the
     // code for every part range (a select chain per range grew the kernel by half: i-cache)
-    const int NPART = KW == 64 ? 4 : 2;
+    const int NPART = (KW == 64 || (RPW == 2 && KW == 128)) ? 4 : 2;
     auto box_union = [&](int slot, int p0, int p1, uint32_t &mn, uint32_t &mx) {
         // lane 2 i + h reads wave i's parts 2 h, 2 h + 1 (one LDS read; a loop over the parts
         // was four dependent LDS round trips: +45 % stage time at C2), then a wave reduction
@@ -1161,8 +1189,11 @@ static int st_nw(int K) { return K <= 64 ? ST_NW_SMALLK : 8; }
 
 // rays per wave and step: 2 for K <= 32 (SDHIP_TILE_RPW=1 forces one, diagnostic A/B)
 static int st_rpw(int K) {
-    static const int force1 = getenv("SDHIP_TILE_RPW") && atoi(getenv("SDHIP_TILE_RPW")) == 1;
-    return (K <= 32 && !force1 && st_nw(K) == 8) ? 2 : 1;
+    static const int force = getenv("SDHIP_TILE_RPW") ? atoi(getenv("SDHIP_TILE_RPW")) : 0;
+    // SDHIP_TILE_RPW=2 also takes K = 64 two rays per wave (80 KiB of records, 37-KiB tile
+    // buffers; A/B runs)
+    const int kmax = force == 2 ? 64 : 32;
+    return (K <= kmax && force != 1 && st_nw(K) == 8) ? 2 : 1;
 }
 
 static int st_lds_fixed(int K) {
