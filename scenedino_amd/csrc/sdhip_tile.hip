@@ -228,6 +228,9 @@ typedef __attribute__((address_space(3))) void lds_void;
 #ifndef ST_EARLY_HW
 #define ST_EARLY_HW ST_WAIT_EARLY  // HPRE 3: the next head's W_dino loaded after staging (0: at step end)
 #endif
+#ifndef ST_PRIO
+#define ST_PRIO 0
+#endif
 #ifndef ST_EARLY_FETCH
 #define ST_EARLY_FETCH 1  // next-next step's ray words fetched after staging (0: at step end)
 #endif
@@ -807,6 +810,11 @@ k_render_tile(const st_args sa) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
+    // ST_PRIO (build knob): static issue priority for one half of the workgroup for the whole
+    // step loop (MI355X guide, two-waves-per-SIMD item 4: the second-dispatched half, waves
+    // NW / 2 .., loses every arbitration; 1 raises that half, 2 the first half, 0 none)
+    if (ST_PRIO == 1 && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+    if (ST_PRIO == 2 && wave < NW / 2) __builtin_amdgcn_s_setprio(1);
     int prev_grp = -1, prev_ok = 0;
     HFrag hwn[4];  // HPRE 3: W_dino tile `wave` for the next step's head
 #if ST_PROF
