@@ -193,8 +193,17 @@ def vit_forward(vit: VisionTransformer, images: torch.Tensor, packed: _Packed,
               patches=Np)
     xn = torch.empty(B * T, C, device=dev, dtype=bf)
     q = torch.empty(B, nh, T, hd, device=dev, dtype=bf)
-    k = torch.zeros(B, nh, Tp, hd, device=dev, dtype=bf)
-    vt = torch.zeros(B, nh, hd, Tp, device=dev, dtype=bf)
+    # K / V^T with their token padding (rows / columns T .. Tp - 1) zero: allocated and zeroed
+    # once per shape and kept on the packed weights -- the qkv epilogue writes only the
+    # first T tokens, so the padding stays zero, and a captured pass holds no memset launches
+    # (two ~5 us fills per pass).  One pass at a time per model, as the LayerNorm-tail
+    # tickets below.
+    kv = getattr(packed, "_kv", None)
+    kkey = (B, nh, T, Tp, hd, str(dev))
+    if kv is None or kv[0] != kkey:
+        kv = packed._kv = (kkey, torch.zeros(B, nh, Tp, hd, device=dev, dtype=bf),
+                           torch.zeros(B, nh, hd, Tp, device=dev, dtype=bf))
+    k, vt = kv[1], kv[2]
     ao = torch.empty(B * T, C, device=dev, dtype=bf)
     hid = torch.empty(B * T, packed.blocks[0]["fc1_w"].shape[0], device=dev, dtype=bf)
     grids = []
