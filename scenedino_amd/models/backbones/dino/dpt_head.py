@@ -21,12 +21,19 @@ Parity: tests/golden/dpt_head.npz, produced by the reference's own DPTHead on CP
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 from torch import nn
 
 from .... import _lib
 from .vit import _param_key
+
+# FeatureFusionBlock's 1x1 projection applied before its x2 upsampling (the reference order,
+# dpt_head.py:156-157, is upsample then project; exact in real arithmetic, one bf16 rounding
+# moved); SCENEDINO_AMD_DPT_PROJECT_FIRST=0 restores the reference order (A/B runs)
+PROJECT_FIRST = os.environ.get("SCENEDINO_AMD_DPT_PROJECT_FIRST", "1") != "0"
 
 
 class ReassembleBlocks(nn.Module):
@@ -195,8 +202,13 @@ class DPTHead(nn.Module):
                     res = res.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()
                 x = rcu(res, fp["rcu1"], extra=x)                   # x + rcu1(res)
             x = rcu(x, fp["rcu2"])
-            x = L.upsample2x(x)
             w, b = fp["project"]
+            if PROJECT_FIRST:
+                # project (1x1 conv) before the x2 upsampling: both are linear and the
+                # align_corners bilinear weights sum to one (the bias passes through), so
+                # upsample(project(x)) = project(upsample(x)) -- on a quarter of the pixels
+                return L.upsample2x(L.linear_nhwc(x, w, b))
+            x = L.upsample2x(x)
             return L.linear_nhwc(x, w, b)
 
         out = fusion(0, f[-1])
