@@ -34,6 +34,11 @@ from .vit import _param_key
 # dpt_head.py:156-157, is upsample then project; exact in real arithmetic, one bf16 rounding
 # moved); SCENEDINO_AMD_DPT_PROJECT_FIRST=0 restores the reference order (A/B runs)
 PROJECT_FIRST = os.environ.get("SCENEDINO_AMD_DPT_PROJECT_FIRST", "1") != "0"
+# levels 0 / 1: the reassemble projection (1x1 conv) folded into the ConvTranspose(k, stride k)
+# behind it -- both linear, no padding, so W_t W_p x + (W_t b_p + b_t) is the same map in one
+# GEMM (weights multiplied in fp32 on the host, one bf16 rounding of the product instead of
+# one of the intermediate activations); SCENEDINO_AMD_DPT_FOLD_UP=0: two GEMMs (A/B runs)
+FOLD_UP = os.environ.get("SCENEDINO_AMD_DPT_FOLD_UP", "1") != "0"
 
 
 class ReassembleBlocks(nn.Module):
@@ -99,6 +104,18 @@ def _pack_conv1(conv):
             conv.bias.detach().float().contiguous() if conv.bias is not None else None)
 
 
+def _pack_proj_convT(proj, conv):
+    """Conv2d(C, c, 1) followed by ConvTranspose2d(c, c', k, stride k) as one GEMM operand:
+    (k k c', C) with column n = (dy k + dx) c' + co (_pack_convT's order), bias per column."""
+    wp = proj.weight.detach().double().reshape(proj.weight.shape[0], -1)  # (c, C)
+    bp = proj.bias.detach().double()
+    w = conv.weight.detach().double()  # (c, c', k, k)
+    cin, cout, k, _ = w.shape
+    wt = w.permute(2, 3, 1, 0).reshape(k * k * cout, cin)  # (k k c', c)
+    bt = conv.bias.detach().double().repeat(k * k)
+    return ((wt @ wp).to(torch.bfloat16).contiguous(), (wt @ bp + bt).float().contiguous(), k)
+
+
 def _pack_convT(conv):
     """ConvTranspose2d(k, stride k): weight (Cin, Cout, k, k) -> (k k Cout, Cin) with column
     n = (dy k + dx) Cout + co; bias repeated per sub-pixel."""
@@ -141,6 +158,7 @@ class DPTHead(nn.Module):
         P = {
             "proj": [_pack_conv1(c) for c in rb.projects],
             "up0": _pack_convT(rb.resize_layers[0]), "up1": _pack_convT(rb.resize_layers[1]),
+            "projup": [_pack_proj_convT(rb.projects[i], rb.resize_layers[i]) for i in (0, 1)],
             "down3": _pack_conv3(rb.resize_layers[3]),
             "convs": [_pack_conv3(c) for c in self.convs],
             "fusion": [{
@@ -164,6 +182,9 @@ class DPTHead(nn.Module):
         streams as their token grids appear (DINOv2Module._decode)."""
         L = _lib
         P = self._pack()
+        if FOLD_UP and (i == 0 or i == 1):
+            wf, bf, k = P["projup"][i]
+            return L.conv3x3(L.linear_nhwc(x, wf, bf, shuf=k), *P["convs"][i])
         w, b = P["proj"][i]
         y = L.linear_nhwc(x, w, b)
         if i == 0 or i == 1:
