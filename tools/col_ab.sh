@@ -1,4 +1,5 @@
 #!/bin/bash
+# (ST_COL16 was measured and reverted -- profiles/r6_tile/rec36_ab.txt; the script records how)
 # Diagnostic A/B: 36-B sample records (ST_COL16=1: red / green as an f16 pair) vs the 40-B
 # records (variant col32), one and two rays per wave at K = 64; the render parity file first
 # under both ray counts.

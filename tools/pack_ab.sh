@@ -1,4 +1,5 @@
 #!/bin/bash
+# (ST_PACK was measured and reverted -- profiles/r6_tile/rpw2_k64_ab.txt; the script records how)
 # Diagnostic A/B: packed per-part staging of split groups (ST_PACK=1, shipped candidate) vs
 # one part per restage (variant nopack), C2 and C1 interleaved, and two rays per wave at K = 64
 # with packing; the render parity file first.
